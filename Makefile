@@ -1,0 +1,56 @@
+# Build of the MI355X (gfx950) ray tracer and its CPU checker.
+#   make            -> product library + demo app + oracle library
+#   make ref        -> oracle/_ref harness compiled against the reference's vendored glm
+#                      (only where /root/reference exists; never on the GPU box)
+ROCM      ?= /opt/rocm
+HIPCC     ?= $(ROCM)/bin/hipcc
+ARCH      ?= gfx950
+PKG       := realtimeraytracing_gradproject_amd
+SRC       := $(PKG)/csrc
+LIBDIR    := $(PKG)/lib
+BUILD     := build
+
+# -ffp-contract=off everywhere on the path: the image is bit-compared with the oracle.
+HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
+             -munsafe-fp-atomics
+CXXFLAGS  := -O2 -std=c++17 -fPIC -ffp-contract=off -Wall
+# Oracle: scalar C, explicit fmaf in the slab test (matches __builtin_fmaf on the GPU).
+OCFLAGS   := -O2 -std=c11 -fPIC -ffp-contract=off -mfma -Wall -Wno-unused-function
+
+LIB       := $(LIBDIR)/librtamd.so
+APP       := $(LIBDIR)/rt_app
+ORACLE    := oracle/liboracle.so
+
+HDRS      := include/rt_api.h $(SRC)/rt_device.hpp $(SRC)/rt_internal.hpp
+
+all: $(LIB) $(ORACLE)
+
+$(BUILD)/%.o: $(SRC)/%.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/rt_api.o: $(SRC)/rt_api.cpp $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/rt_host.o: $(SRC)/rt_host.cpp include/rt_api.h | $(BUILD)
+	g++ $(CXXFLAGS) -c $< -o $@
+
+$(LIB): $(BUILD)/rt_api.o $(BUILD)/rt_host.o $(BUILD)/rt_lbvh.o $(BUILD)/rt_trace.o | $(LIBDIR)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-rpath,$(ROCM)/lib
+
+$(APP): $(SRC)/host/rt_app.cpp $(wildcard $(SRC)/host/*.hpp) $(LIB) | $(LIBDIR)
+	g++ $(CXXFLAGS) -I$(ROCM)/include -D__HIP_PLATFORM_AMD__ -o $@ $(SRC)/host/rt_app.cpp \
+	    -L$(LIBDIR) -lrtamd -L$(ROCM)/lib -lamdhip64 -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(ROCM)/lib
+
+$(ORACLE): oracle/rt_oracle.c oracle/rt_oracle.h
+	gcc $(OCFLAGS) -shared -o $@ oracle/rt_oracle.c -lm -lpthread
+
+ref:
+	$(MAKE) -C oracle -f Makefile.ref
+
+$(BUILD) $(LIBDIR):
+	mkdir -p $@
+
+clean:
+	rm -rf $(BUILD) $(LIB) $(APP) $(ORACLE)
+
+.PHONY: all clean ref

@@ -1,0 +1,216 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mrays/s (primary + shadow) at 1080p on MI355X — BASELINE.json config C2
+(teapot.obj, 1 light, 1920x1080, primary + shadow rays) by default.
+
+A step is one frame: RayGen -> TLAS/BLAS traversal -> shading + shadow rays -> RGBA8 (the
+reference's DispatchRays, D3D12HelloTriangle.cpp:558-592). The scene is static: the LBVH build
+runs once before the timed region and is reported separately (build_ms).
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): the frame is
+split into interleaved 8-row strips (strip s -> rank s mod N), every rank renders its strips into
+a compact buffer, one gather over RCCL brings them to rank 0, which un-interleaves them
+(rt_assemble_strips). Total work per step is fixed (one frame): scaling "strong".
+
+value = rays traced in one frame (all ranks, counted by the device counters in an untimed pass)
+x steps / max-over-ranks wall time of the timed region.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import realtimeraytracing_gradproject_amd as rt  # noqa: E402
+from realtimeraytracing_gradproject_amd import scenes  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+BYTES_PER_AABB_TEST = 24  # one child box (6 floats) per slab test
+BYTES_PER_TRI_TEST = 36   # v0, e1, e2 (9 floats) per Moller-Trumbore test
+BYTES_PER_PIXEL = 4       # RGBA8 write
+STRIP_ROWS = 8
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--config", default="C2", choices=[c for c in scenes.CONFIGS])
+    p.add_argument("--schedule", default="megakernel", choices=["megakernel", "wavefront"])
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=2.0, help="minimum wall time of the CPU baseline sample")
+    p.add_argument("--save-image", default="", help="write the rank-0 frame as .npy")
+    return p.parse_args()
+
+
+def load_traffic(config: str):
+    """HBM bytes per trace launch from the committed rocprofv3 PMC pass (profiles/), if present."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        e = d.get(config)
+        return float(e["bytes_per_launch"]) if e else None
+    except Exception:
+        return None
+
+
+def cpu_baseline(spec, seconds: float):
+    """The oracle (scalar C, pthreads over interleaved rows) on the same frame, on this host."""
+    import oracle
+
+    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    threads = max(1, min(16, ncpu or 1))
+    o = oracle.Scene(spec)
+    rays = 0
+    frames = 0
+    t0 = time.perf_counter()
+    while True:
+        _, _, st = o.render_spec(spec, nthreads=threads, want_float=False)
+        rays += int(st[0] + st[1])
+        frames += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            break
+    return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{frames} full {spec.name} frame(s) {spec.width}x{spec.height} by oracle/rt_oracle.c "
+                      f"({threads} threads, {dt:.1f} s wall)"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        a.gpus = world if world > 1 else a.gpus
+    distributed = world > 1
+    torch.cuda.set_device(local)
+    if distributed:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    spec = scenes.config(a.config)
+    W, H = spec.width, spec.height
+    ctx = rt.Context(local)
+    scenes.upload(ctx, spec)
+    ctx.set_schedule(rt.RT_SCHED_WAVEFRONT if a.schedule == "wavefront" else rt.RT_SCHED_MEGAKERNEL)
+    binfo = [ctx.blas_info(b) for b in range(len(spec.meshes))]
+    tinfo = ctx.tlas_info()
+
+    rows = rt.strip_rows(H, world, rank, STRIP_ROWS) if distributed else None
+    nrows = H if rows is None else len(rows)
+    rows_per_rank = rt.strip_rows_per_rank(H, world, STRIP_ROWS) if distributed else H
+    stream = torch.cuda.Stream()
+    sp = stream.cuda_stream
+    local8 = torch.zeros((rows_per_rank, W, 4), dtype=torch.uint8, device="cuda")
+    gathered = torch.zeros((world, rows_per_rank, W, 4), dtype=torch.uint8, device="cuda") if distributed and rank == 0 else None
+    frame = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") if distributed and rank == 0 else None
+
+    def step():
+        ctx.dispatch(W, H, local8, None, rows=rows, stream=sp)
+        if distributed:
+            with torch.cuda.stream(stream):
+                dist.gather(local8, [gathered[r] for r in range(world)] if rank == 0 else None, dst=0)
+                if rank == 0:
+                    ctx.assemble_strips(W, H, world, STRIP_ROWS, gathered, frame, stream=sp)
+
+    # untimed counter pass: rays, box and triangle tests of this rank's share of the frame
+    ctx.set_stats(True)
+    ctx.stats_reset()
+    ctx.dispatch(W, H, local8, None, rows=rows, stream=sp)
+    torch.cuda.synchronize()
+    st = ctx.stats()
+    ctx.set_stats(False)
+    rays_local = st["primary_rays"] + st["shadow_rays"]
+    counts = torch.tensor([rays_local, st["primary_rays"], st["shadow_rays"]], dtype=torch.float64, device="cuda")
+    if distributed:
+        dist.all_reduce(counts)
+    rays_frame = int(counts[0].item())
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        ev[k][0].record(stream)
+        ctx.dispatch(W, H, local8, None, rows=rows, stream=sp)
+        ev[k][1].record(stream)
+        if distributed:
+            with torch.cuda.stream(stream):
+                dist.gather(local8, [gathered[r] for r in range(world)] if rank == 0 else None, dst=0)
+                if rank == 0:
+                    ctx.assemble_strips(W, H, world, STRIP_ROWS, gathered, frame, stream=sp)
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if distributed:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    tmax = float(tmax.item())
+
+    if a.save_image and rank == 0:
+        img = (frame if distributed else local8[:H]).cpu().numpy()
+        np.save(a.save_image, img)
+
+    if rank == 0:
+        value = rays_frame * a.steps / tmax / 1e6
+        bytes_launch = (BYTES_PER_AABB_TEST * st["aabb_tests"] + BYTES_PER_TRI_TEST * st["tri_tests"]
+                        + BYTES_PER_PIXEL * W * nrows)
+        achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
+        traffic = load_traffic(a.config) if not distributed else None
+        cpu = None
+        if not distributed and not a.no_cpu_baseline:
+            cpu = cpu_baseline(spec, a.cpu_seconds)
+        out = {
+            "metric": "Mrays/sec (primary+shadow) at 1080p",
+            "value": round(value, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(tmax / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic camera/lights of BASELINE config; meshes teapot.obj/rabbit.obj from the reference",
+            "config": {"workload": f"{spec.name}: {spec.model}.obj x{len(spec.instances) - 1} + plane, "
+                                   f"{len(spec.lights)} light(s), {W}x{H}, {spec.spp} spp, shade "
+                                   f"{['ref', 'lambert_shadow', 'primary'][spec.mode]}",
+                       "rays_per_frame": rays_frame, "primary_rays": int(counts[1].item()),
+                       "shadow_rays": int(counts[2].item()), "parallelism": f"strips{world}",
+                       "schedule": a.schedule},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "k_trace_frame", "kernel_ms": round(kernel_ms, 4),
+                         "bytes_per_launch": int(bytes_launch),
+                         "aabb_tests": int(st["aabb_tests"]), "tri_tests": int(st["tri_tests"])},
+            "cpu_baseline": cpu,
+            "build_ms": {"blas": [round(b.build_ms, 3) for b in binfo], "tlas": round(tinfo.build_ms, 3)},
+        }
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

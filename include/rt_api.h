@@ -1,0 +1,244 @@
+/*
+ * rt_api.h — C-ABI drop-in boundary of the MI355X ray tracer.
+ *
+ * This is the boundary the reference's DXR path sits behind (D3D12 + nv_helpers_dx12).
+ * Each entry point names the reference interface it replaces (file:line, relative to the
+ * reference tree UtkuGokalp/RealTimeRayTracing_GradProject).
+ *
+ * Rules:
+ *   - extern "C", plain pointers and sizes, no exceptions cross the boundary.
+ *   - Non-zero rt_status == FAILED(hr) in the reference (ThrowIfFailed, DXSampleHelper.h:16-22).
+ *     rt_last_error(ctx) returns the message of the last failure on that context.
+ *   - Host inputs are copied during the call. Output device buffers are owned by the caller.
+ *   - GPU work is stream-ordered on the hip_stream passed in (NULL = the context's stream),
+ *     like command-list recording; synchronise with hipStreamSynchronize (== fence wait,
+ *     D3D12HelloTriangle.cpp:627-647).
+ *   - One context per host thread (the reference records on a single thread).
+ *   - Functions in the "host services" section never touch the GPU: they run without one.
+ */
+#ifndef RT_API_H
+#define RT_API_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_API_VERSION 1
+
+typedef struct rt_ctx* rt_ctx_t;
+typedef struct rt_mesh* rt_mesh_t;
+typedef uint32_t rt_blas_t;
+
+typedef enum {
+  RT_OK = 0,
+  RT_E_INVALID = -1,     /* bad argument / misuse (reference: std::logic_error) */
+  RT_E_OOM = -2,         /* device or host allocation failed */
+  RT_E_HIP = -3,         /* a HIP runtime call failed (reference: FAILED(hr)) */
+  RT_E_RCCL = -4,        /* reserved: collective failure */
+  RT_E_UNSUPPORTED = -5, /* no gfx950 device / feature not built */
+  RT_E_IO = -6           /* file could not be opened (reference: LoadObjFile returns false) */
+} rt_status;
+
+/* Hit groups, in the reference's SBT order (D3D12HelloTriangle.cpp:1064-1080). */
+enum { RT_HITGROUP_MODEL = 0, RT_HITGROUP_SHADOW = 1, RT_HITGROUP_PLANE = 2 };
+
+/* Shading modes of the trace kernel. */
+enum {
+  RT_SHADE_REF = 0,            /* exact reference: ClosestHit (Lambert+PBR over the lights) for models,
+                                  PlaneClosestHit (light 0 + one shadow ray) for the plane, Miss sky
+                                  (Hit.hlsl:183-241, Miss.hlsl:3-10, ShadowRay.hlsl:10-20) */
+  RT_SHADE_LAMBERT_SHADOW = 1, /* perf configs: every hit, one shadow ray per light */
+  RT_SHADE_PRIMARY = 2         /* primary rays only: Lambert over the lights, no shadow rays (config C1) */
+};
+
+/* Dispatch variants (same image, different kernel schedule). */
+enum {
+  RT_SCHED_MEGAKERNEL = 0, /* one launch: raygen + traversal + shading + shadow rays per lane */
+  RT_SCHED_WAVEFRONT = 1   /* primary/shade kernel -> ballot-compacted shadow queue -> shadow kernel -> resolve */
+};
+
+/* One TLAS instance (TopLevelASGenerator::AddInstance, TopLevelASGenerator.h:88-99,
+ * instance desc fill TopLevelASGenerator.cpp:180-198). xform = object-to-world 3x4, row-major,
+ * column-vector convention: world = M * (x,y,z,1). instance_id = InstanceID() (the list index in
+ * the reference, D3D12HelloTriangle.cpp:749). */
+typedef struct {
+  rt_blas_t blas;
+  float xform3x4_rowmajor[12];
+  uint32_t instance_id;
+  uint32_t hit_group; /* RT_HITGROUP_MODEL or RT_HITGROUP_PLANE */
+} rt_instance;
+
+/* == Hit.hlsl Light (Hit.hlsl:25-30) */
+typedef struct {
+  float color[3];
+  float position[3];
+  float intensity;
+} rt_light;
+
+/* == Hit.hlsl Material (Hit.hlsl:10-16), 24 B */
+typedef struct {
+  float albedo[3];
+  float roughness, metallic, reflectivity;
+} rt_material;
+
+/* BVH summary returned by rt_blas_info / rt_tlas_info. */
+typedef struct {
+  uint32_t prim_count;   /* triangles (BLAS) or instances (TLAS) */
+  uint32_t node_count;   /* internal child-pair nodes (max(prim_count-1,1)) */
+  uint32_t depth;        /* max root-to-leaf edges */
+  uint32_t reserved;
+  float bounds_lo[3];
+  float bounds_hi[3];
+  double build_ms;       /* device time of the last build (HIP events) */
+} rt_bvh_info;
+
+/* Counters reported by rt_stats (accumulated over dispatches launched while stats are on). */
+enum {
+  RT_STAT_PRIMARY_RAYS = 0,
+  RT_STAT_SHADOW_RAYS = 1,
+  RT_STAT_AABB_TESTS = 2,  /* child-box slab tests (2 per node visit) */
+  RT_STAT_TRI_TESTS = 3,   /* Moller-Trumbore tests */
+  RT_STAT_INSTANCE_ENTRIES = 4,
+  RT_STAT_STACK_OVERFLOWS = 5,
+  RT_STAT_PIXELS = 6,
+  RT_STAT_DISPATCHES = 7,
+  RT_STAT_COUNT = 8
+};
+
+/* ------------------------------------------------------------------------------------------ */
+/* Context                                                                                     */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Replaces device/queue creation in D3D12HelloTriangle::LoadPipeline (D3D12HelloTriangle.cpp:85-198)
+ * and CheckRaytracingSupport (:649). Fails with RT_E_UNSUPPORTED unless the device is gfx950. */
+rt_status rt_create(int hip_device, rt_ctx_t* out);
+/* Replaces OnDestroy + ComPtr release (D3D12HelloTriangle.cpp OnDestroy). */
+rt_status rt_destroy(rt_ctx_t ctx);
+const char* rt_last_error(rt_ctx_t ctx);
+const char* rt_status_string(rt_status st);
+int rt_api_version(void);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Acceleration structures                                                                     */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Replaces BottomLevelASGenerator::AddVertexBuffer + ComputeASBufferSizes + Generate
+ * (BottomLevelASGenerator.h:106-153, .cpp:74-245; call site D3D12HelloTriangle.cpp:682-732).
+ * vtx: host array, vcount vertices of `stride` bytes with float3 position at offset 0 and, when
+ * stride >= 24, float3 normal at offset 12 (the reference Vertex, D3D12HelloTriangle.h:51-56).
+ * idx: host uint32 triangle list (icount % 3 == 0) or NULL for non-indexed geometry
+ * (vcount % 3 == 0). Builds an LBVH on the device (Morton codes, LDS radix sort, Karras
+ * hierarchy, bottom-up refit). Synchronous: returns after the build has completed. */
+rt_status rt_blas_build(rt_ctx_t ctx, const void* vtx, uint32_t vcount, uint32_t stride,
+                        const uint32_t* idx, uint32_t icount, rt_blas_t* out);
+/* Model hot-reload (D3D12HelloTriangle.cpp:1482-1596): rebuild an existing BLAS in place with new
+ * geometry. Instances that reference it pick it up at the next rt_tlas_build. */
+rt_status rt_blas_rebuild(rt_ctx_t ctx, rt_blas_t blas, const void* vtx, uint32_t vcount,
+                          uint32_t stride, const uint32_t* idx, uint32_t icount);
+rt_status rt_blas_info(rt_ctx_t ctx, rt_blas_t blas, rt_bvh_info* out);
+/* Copies the BLAS to host memory for parity checks: nodes (node_count x 64 B child-pair nodes),
+ * tris (prim_count x 48 B: v0.xyz,prim | e1.xyz,0 | e2.xyz,0 in leaf order). Either may be NULL. */
+rt_status rt_blas_export(rt_ctx_t ctx, rt_blas_t blas, void* nodes, size_t nodes_bytes, void* tris,
+                         size_t tris_bytes);
+
+/* Replaces TopLevelASGenerator::AddInstance + ComputeASBufferSizes + Generate
+ * (TopLevelASGenerator.h:88-130, .cpp:64-249; call site D3D12HelloTriangle.cpp:734-776), and
+ * UpdateInstancePropertiesBuffer (D3D12HelloTriangle.cpp:1181-1204): the per-instance normal
+ * matrix transpose(inverse(upper3x3)) is derived here. update_only != 0 refits the existing TLAS
+ * (same instance count and BLAS ids; new transforms), as TopLevelASGenerator.cpp:202-222.
+ * Synchronous. */
+rt_status rt_tlas_build(rt_ctx_t ctx, const rt_instance* instances, uint32_t n, int update_only);
+rt_status rt_tlas_info(rt_ctx_t ctx, rt_bvh_info* out);
+/* nodes: node_count x 64 B; leaf refs are ~instance_index. */
+rt_status rt_tlas_export(rt_ctx_t ctx, void* nodes, size_t nodes_bytes);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Per-frame state                                                                             */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Replaces UpdateCameraBuffer (D3D12HelloTriangle.cpp:1144-1170): cb = view, proj, viewInv,
+ * projInv, 4 x 16 floats, each in XMMATRIX memory order (the exact 256-B constant buffer). */
+rt_status rt_set_camera(rt_ctx_t ctx, const float cb[64]);
+/* Replaces the Hit.hlsl light table (Hit.hlsl:48-57) and UpdateMaterialsBuffer/OnUpdate
+ * (D3D12HelloTriangle.cpp:424-428). nlights in [1, 16]. spp in {1, 4, 9, 16} (k x k stratified). */
+rt_status rt_set_shading(rt_ctx_t ctx, const rt_light* lights, uint32_t nlights,
+                         const rt_material* material, int shade_mode, int spp);
+/* RT_SCHED_MEGAKERNEL (default) or RT_SCHED_WAVEFRONT. */
+rt_status rt_set_schedule(rt_ctx_t ctx, int schedule);
+/* Enables device counters (rt_stats). Costs time: off for timed runs. */
+rt_status rt_set_stats(rt_ctx_t ctx, int enable);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Launch                                                                                      */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Replaces DispatchRays (D3D12HelloTriangle.cpp:558-592) + RayGen/Hit/Miss/ShadowRay programs.
+ * Renders an image of W x H. rows: host list of global row indices to render (NULL = all H
+ * rows, in order); the output is compact: row r of the output is global row rows[r].
+ * rgba8_dev: device buffer of nrows*W*4 bytes, R8G8B8A8_UNORM (D3D12HelloTriangle.cpp:971).
+ * rgba32f_dev: optional device buffer of nrows*W*4 floats (the pre-quantisation float4), or NULL.
+ * hip_stream: hipStream_t or NULL (context stream). Asynchronous. */
+rt_status rt_dispatch_rays(rt_ctx_t ctx, uint32_t W, uint32_t H, const uint32_t* rows,
+                           uint32_t nrows, void* rgba8_dev, float* rgba32f_dev, void* hip_stream);
+
+/* Batch TraceRay (Common.hlsl:44-82 semantics) for parity tests and external callers.
+ * rays_dev: n x 8 floats (o.x,o.y,o.z,tmin, d.x,d.y,d.z,tmax), direction used as given.
+ * any_hit != 0: terminate on the first accepted hit (shadow rays).
+ * hits_dev: n x 4 x 32-bit: (t as float, instance_id, primitive index, hit flag) with u,v written
+ * to uv_dev (n x 2 floats) when uv_dev != NULL. A miss has hit flag 0 and t = tmax. Asynchronous. */
+rt_status rt_trace_rays(rt_ctx_t ctx, const float* rays_dev, uint32_t n, int any_hit,
+                        uint32_t* hits_dev, float* uv_dev, void* hip_stream);
+
+/* Multi-GPU frame assembly: un-interleaves `nranks` compact strip images gathered back to back in
+ * `gathered_dev` (rank-major; rank k holds strips s with s % nranks == k, strip_rows rows each)
+ * into a full W x H RGBA8 image. Asynchronous. */
+rt_status rt_assemble_strips(rt_ctx_t ctx, uint32_t W, uint32_t H, uint32_t nranks,
+                             uint32_t strip_rows, const void* gathered_dev, void* rgba8_dev,
+                             void* hip_stream);
+/* Host helper: the row list rank `rank` of `nranks` renders with interleaved strips of
+ * strip_rows rows. Writes up to cap rows to rows_out; returns the row count (0 on bad args). */
+uint32_t rt_strip_rows(uint32_t H, uint32_t nranks, uint32_t rank, uint32_t strip_rows,
+                       uint32_t* rows_out, uint32_t cap);
+
+/* Copies the counters (RT_STAT_*) to out[RT_STAT_COUNT]; synchronises the context. */
+rt_status rt_stats(rt_ctx_t ctx, uint64_t out[8]);
+rt_status rt_stats_reset(rt_ctx_t ctx);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Host services (no GPU): mesh ingest, normals, plane, camera                                 */
+/* ------------------------------------------------------------------------------------------ */
+
+/* OBJFileManager::LoadObjFile (OBJ_FileManager.cpp:10-71): `v x y z` and `f i j k` lines only,
+ * 1-based -> 0-based unsigned indices. RT_E_IO if the file cannot be opened. */
+rt_status rt_mesh_load_obj(const char* path, rt_mesh_t* out);
+/* Same parser over an in-memory text buffer. */
+rt_status rt_mesh_parse_obj(const char* text, size_t len, rt_mesh_t* out);
+void rt_mesh_free(rt_mesh_t mesh);
+uint32_t rt_mesh_vertex_count(rt_mesh_t mesh);
+uint32_t rt_mesh_index_count(rt_mesh_t mesh);
+/* Vertex array, 6 floats per vertex {pos.xyz, normal.xyz} (reference Vertex, stride 24). Normals
+ * are the default (0,1,0) until rt_mesh_compute_vertex_normals. */
+const float* rt_mesh_vertices(rt_mesh_t mesh);
+const uint32_t* rt_mesh_indices(rt_mesh_t mesh);
+/* D3D12HelloTriangle::ComputeVertexNormals (D3D12HelloTriangle.cpp:1430-1462). */
+rt_status rt_mesh_compute_vertex_normals(rt_mesh_t mesh);
+
+/* CreatePlaneVB (D3D12HelloTriangle.cpp:1237-1271): 6 vertices x {pos, normal} = 36 floats. */
+void rt_plane_vertices(float out[36]);
+
+/* Manipulator::setLookat + update (manipulator.cpp:26-32, 305-314) == glm::lookAtRH
+ * (glm/gtc/matrix_transform.inl:519-545): view matrix in glm column-major memory order. */
+void rt_camera_lookat(const float eye[3], const float center[3], const float up[3], float view[16]);
+/* UpdateCameraBuffer (D3D12HelloTriangle.cpp:1144-1170): cb = {view (as given), proj =
+ * XMMatrixPerspectiveFovRH(fov_deg, W/H, znear, zfar), inverse(view), inverse(proj)}. */
+void rt_camera_buffer(const float view[16], uint32_t W, uint32_t H, float fov_deg, float znear,
+                      float zfar, float cb[64]);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_API_H */

@@ -1,0 +1,991 @@
+/*
+ * rt_oracle.c — CPU ORACLE (test infrastructure; see rt_oracle.h for the parity status).
+ *
+ * Scalar C restatement of the reference's DXR path. Every function cites the reference
+ * (paths relative to UtkuGokalp/RealTimeRayTracing_GradProject) it follows. Floating-point
+ * expressions are written operand by operand in the reference's evaluation order and compiled
+ * with -ffp-contract=off; the only fused multiply-adds are the explicit fmaf() of the slab test.
+ * The BVH is an LBVH built by the same deterministic algorithm as the device builder, so the
+ * device tree can be compared node for node; the rendered image does not depend on the tree
+ * (conservative culling + (t, instance, primitive) tie-break), which brute_force=1 verifies.
+ */
+#include "rt_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ---------------------------------------------------------------------------------------- */
+/* small vector helpers                                                                      */
+/* ---------------------------------------------------------------------------------------- */
+typedef struct { float x, y, z; } vec3;
+static inline vec3 mk(float x, float y, float z) { vec3 r = {x, y, z}; return r; }
+static inline vec3 vadd(vec3 a, vec3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline vec3 vsub(vec3 a, vec3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline vec3 vmul(vec3 a, vec3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline vec3 vscale(vec3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+static inline vec3 vneg(vec3 a) { return mk(-a.x, -a.y, -a.z); }
+static inline float vdot(vec3 a, vec3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+static inline vec3 vcross(vec3 a, vec3 b) {
+  return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+/* HLSL normalize, pinned as v * (1/sqrt(dot)) */
+static inline vec3 vnorm(vec3 a) { float inv = 1.0f / sqrtf(vdot(a, a)); return vscale(a, inv); }
+static inline float fmax2(float a, float b) { return a > b ? a : b; }
+static inline float fmin2(float a, float b) { return a < b ? a : b; }
+static inline vec3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
+
+/* ---------------------------------------------------------------------------------------- */
+/* ingest: OBJFileManager::LoadObjFile (src/OBJ_FileManager.cpp:10-71)                       */
+/* ---------------------------------------------------------------------------------------- */
+static int is_ws(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\v' || c == '\f'; }
+
+static int o_parse_float(const char** pp, const char* end, float* out) {
+  const char* p = *pp;
+  while (p < end && is_ws(*p)) ++p;
+  const char* b = p;
+  while (p < end && ((*p >= '0' && *p <= '9') || *p == '+' || *p == '-' || *p == '.' || *p == 'e' || *p == 'E')) ++p;
+  *pp = p;
+  if (p == b) { *out = 0.0f; return 0; }
+  char buf[128];
+  size_t n = (size_t)(p - b);
+  if (n > 127) n = 127;
+  memcpy(buf, b, n);
+  buf[n] = 0;
+  char* ep = NULL;
+  float v = strtof(buf, &ep);
+  if (ep == buf) { *out = 0.0f; return 0; }
+  *out = v;
+  return 1;
+}
+
+static int o_parse_uint(const char** pp, const char* end, uint32_t* out) {
+  const char* p = *pp;
+  while (p < end && is_ws(*p)) ++p;
+  int neg = 0;
+  if (p < end && (*p == '+' || *p == '-')) { neg = *p == '-'; ++p; }
+  if (p >= end || *p < '0' || *p > '9') { *pp = p; *out = 0; return 0; }
+  uint64_t v = 0;
+  int ovf = 0;
+  while (p < end && *p >= '0' && *p <= '9') { v = v * 10 + (uint64_t)(*p - '0'); if (v > 0xffffffffull) ovf = 1; ++p; }
+  *pp = p;
+  if (ovf) { *out = 0xffffffffu; return 0; }
+  *out = neg ? (uint32_t)(0u - (uint32_t)v) : (uint32_t)v;
+  return 1;
+}
+
+int oracle_obj_parse(const char* text, size_t len, float** vtx6, uint32_t* nv, uint32_t** idx, uint32_t* ni) {
+  size_t cv = 1024, ci = 1024, v = 0, i = 0;
+  float* V = (float*)malloc(cv * 6 * sizeof(float));
+  uint32_t* I = (uint32_t*)malloc(ci * sizeof(uint32_t));
+  if (!V || !I) { free(V); free(I); return -1; }
+  const char* p = text;
+  const char* end = text + len;
+  while (p < end) {
+    const char* ls = p;
+    while (p < end && *p != '\n') ++p;
+    const char* le = p;
+    if (p < end) ++p;
+    if (le - ls < 2) continue;
+    const char* q = ls + 1;
+    if (ls[0] == 'v' && ls[1] == ' ') {
+      float xyz[3] = {0, 0, 0};
+      int ok = 1;
+      for (int k = 0; k < 3 && ok; ++k) ok = o_parse_float(&q, le, &xyz[k]);
+      if (v == cv) { cv *= 2; V = (float*)realloc(V, cv * 6 * sizeof(float)); }
+      float* d = V + v * 6;
+      d[0] = xyz[0]; d[1] = xyz[1]; d[2] = xyz[2]; d[3] = 0.0f; d[4] = 1.0f; d[5] = 0.0f;
+      ++v;
+    } else if (ls[0] == 'f' && ls[1] == ' ') {
+      uint32_t f[3] = {0, 0, 0};
+      int ok = 1;
+      for (int k = 0; k < 3 && ok; ++k) ok = o_parse_uint(&q, le, &f[k]);
+      if (i + 3 > ci) { ci *= 2; I = (uint32_t*)realloc(I, ci * sizeof(uint32_t)); }
+      for (int k = 0; k < 3; ++k) I[i++] = f[k] - 1u;
+    }
+  }
+  *vtx6 = V; *nv = (uint32_t)v; *idx = I; *ni = (uint32_t)i;
+  return 0;
+}
+
+void oracle_free(void* p) { free(p); }
+
+/* ComputeVertexNormals (src/D3D12HelloTriangle.cpp:1430-1462); XMVector3Normalize as v/len. */
+static void xm_norm(const float* v, float* o) {
+  float len = sqrtf((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]);
+  if (len > 0.0f) { o[0] = v[0] / len; o[1] = v[1] / len; o[2] = v[2] / len; }
+  else { o[0] = o[1] = o[2] = 0.0f; }
+}
+
+int oracle_vertex_normals(float* V, uint32_t nv, const uint32_t* I, uint32_t ni) {
+  if (ni % 3) return -1;
+  for (uint32_t k = 0; k < ni; ++k) if (I[k] >= nv) return -1;
+  float* acc = (float*)calloc((size_t)nv * 3 + 1, sizeof(float));
+  for (uint32_t t = 0; t + 2 < ni; t += 3) {
+    uint32_t a = I[t], b = I[t + 1], c = I[t + 2];
+    const float *p0 = V + a * 6, *p1 = V + b * 6, *p2 = V + c * 6;
+    float e1[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};
+    float e2[3] = {p2[0] - p0[0], p2[1] - p0[1], p2[2] - p0[2]};
+    float cr[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+    float n[3];
+    xm_norm(cr, n);
+    uint32_t ids[3] = {a, b, c};
+    for (int k = 0; k < 3; ++k) {
+      acc[ids[k] * 3 + 0] = acc[ids[k] * 3 + 0] + n[0];
+      acc[ids[k] * 3 + 1] = acc[ids[k] * 3 + 1] + n[1];
+      acc[ids[k] * 3 + 2] = acc[ids[k] * 3 + 2] + n[2];
+    }
+  }
+  for (uint32_t v = 0; v < nv; ++v) {
+    float n[3];
+    xm_norm(acc + v * 3, n);
+    V[v * 6 + 3] = -n[0]; V[v * 6 + 4] = -n[1]; V[v * 6 + 5] = -n[2];
+  }
+  free(acc);
+  return 0;
+}
+
+/* glm::lookAtRH (glm/gtc/matrix_transform.inl:519-545), glm column-major memory. */
+void oracle_camera_lookat(const float eye[3], const float center[3], const float up[3], float view[16]) {
+  vec3 e = ld3(eye), c = ld3(center), u0 = ld3(up);
+  vec3 f = vnorm(vsub(c, e));
+  vec3 s = vnorm(vcross(f, u0));
+  vec3 u = vcross(s, f);
+  float r[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+  r[0] = s.x; r[4] = s.y; r[8] = s.z;
+  r[1] = u.x; r[5] = u.y; r[9] = u.z;
+  r[2] = -f.x; r[6] = -f.y; r[10] = -f.z;
+  r[12] = -vdot(s, e); r[13] = -vdot(u, e); r[14] = vdot(f, e);
+  memcpy(view, r, sizeof(r));
+}
+
+/* general 4x4 inverse in double (XMMatrixInverse semantics; rounding pinned, parity unpinned) */
+static void inv4(const float* mf, float* out) {
+  double m[16], a[16];
+  for (int i = 0; i < 16; ++i) m[i] = mf[i];
+  /* Gauss-Jordan with partial pivoting on an augmented copy (independent of the product's cofactor form) */
+  double A[4][8];
+  for (int r = 0; r < 4; ++r) for (int c = 0; c < 8; ++c) A[r][c] = c < 4 ? m[r * 4 + c] : (c - 4 == r ? 1.0 : 0.0);
+  for (int col = 0; col < 4; ++col) {
+    int piv = col;
+    for (int r = col + 1; r < 4; ++r) if (fabs(A[r][col]) > fabs(A[piv][col])) piv = r;
+    if (A[piv][col] == 0.0) { for (int i = 0; i < 16; ++i) out[i] = 0.0f; return; }
+    if (piv != col) for (int c = 0; c < 8; ++c) { double t = A[col][c]; A[col][c] = A[piv][c]; A[piv][c] = t; }
+    double d = A[col][col];
+    for (int c = 0; c < 8; ++c) A[col][c] /= d;
+    for (int r = 0; r < 4; ++r) if (r != col) { double f = A[r][col]; for (int c = 0; c < 8; ++c) A[r][c] -= f * A[col][c]; }
+  }
+  for (int r = 0; r < 4; ++r) for (int c = 0; c < 4; ++c) a[r * 4 + c] = A[r][c + 4];
+  for (int i = 0; i < 16; ++i) out[i] = (float)a[i];
+}
+
+/* UpdateCameraBuffer (src/D3D12HelloTriangle.cpp:1144-1170) */
+void oracle_camera_buffer(const float view[16], uint32_t W, uint32_t H, float fov_deg, float zn, float zf, float cb[64]) {
+  const float pi = 3.141592654f;
+  float aspect = (float)W / (float)H;
+  float fov = fov_deg * pi / 180.0f;
+  float half = 0.5f * fov;
+  float sn = (float)sin((double)half), cs = (float)cos((double)half);
+  float h = cs / sn, w = h / aspect, fr = zf / (zn - zf);
+  float proj[16] = {w, 0, 0, 0, 0, h, 0, 0, 0, 0, fr, -1.0f, 0, 0, fr * zn, 0};
+  memcpy(cb, view, 64);
+  memcpy(cb + 16, proj, 64);
+  inv4(cb, cb + 32);
+  inv4(cb + 16, cb + 48);
+}
+
+/* ---------------------------------------------------------------------------------------- */
+/* LBVH (same algorithm as realtimeraytracing_gradproject_amd/csrc/rt_lbvh.hip)               */
+/* ---------------------------------------------------------------------------------------- */
+typedef struct {
+  float lo0[3], hi0[3], lo1[3], hi1[3];
+  int32_t c0, c1;
+  uint32_t pad0, pad1;
+} onode;
+typedef struct {
+  float v0[3]; uint32_t prim;
+  float e1[3]; uint32_t pad1;
+  float e2[3]; uint32_t pad2;
+} otri;
+
+typedef struct {
+  onode* nodes;
+  otri* tris; /* leaf order */
+  float* vtx; /* {pos, normal} */
+  uint32_t* idx; /* NULL for non-indexed */
+  uint32_t ntri, nnodes, depth, nv;
+  float bounds[6];
+} oblas;
+
+typedef struct {
+  float w2o[12], o2w[12], nrm[9];
+  uint32_t instance_id, hit_group, blas;
+} oinst;
+
+struct oracle_scene {
+  oblas* blas;
+  int nblas, cblas;
+  oinst* inst;
+  uint32_t ninst;
+  onode* tlas;
+  uint32_t tlas_nodes, tlas_depth;
+};
+
+static uint32_t expand10(uint32_t x) {
+  x = (x * 0x00010001u) & 0xFF0000FFu;
+  x = (x * 0x00000101u) & 0x0F00F00Fu;
+  x = (x * 0x00000011u) & 0xC30C30C3u;
+  x = (x * 0x00000005u) & 0x49249249u;
+  return x;
+}
+
+static int clz64(uint64_t v) { return v ? __builtin_clzll(v) : 64; }
+static int odelta(const uint32_t* keys, int n, int i, int j) {
+  if (j < 0 || j >= n) return -1;
+  uint64_t a = ((uint64_t)keys[i] << 32) | (uint32_t)i;
+  uint64_t b = ((uint64_t)keys[j] << 32) | (uint32_t)j;
+  return clz64(a ^ b);
+}
+
+static void box_of(int c, const float* nbox, const float* primbox, const uint32_t* sorted, float* b) {
+  const float* p = c >= 0 ? nbox + (size_t)c * 6 : primbox + (size_t)sorted[~c] * 6;
+  memcpy(b, p, 24);
+}
+
+/* builds nodes over n prim boxes; sorted receives leaf order; returns depth */
+static uint32_t lbvh(const float* primbox, uint32_t n, onode* nodes, uint32_t* sorted, int leaf_ref_is_prim) {
+  float cb[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  for (uint32_t i = 0; i < n; ++i)
+    for (int k = 0; k < 3; ++k) {
+      float c = (primbox[i * 6 + k] + primbox[i * 6 + 3 + k]) * 0.5f;
+      cb[k] = fmin2(cb[k], c);
+      cb[3 + k] = fmax2(cb[3 + k], c);
+    }
+  uint32_t* keys = (uint32_t*)malloc((size_t)n * 4);
+  uint32_t* k2 = (uint32_t*)malloc((size_t)n * 4);
+  uint32_t* v2 = (uint32_t*)malloc((size_t)n * 4);
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t q[3];
+    for (int k = 0; k < 3; ++k) {
+      float ext = cb[3 + k] - cb[k];
+      float inv = ext > 0.0f ? 1.0f / ext : 0.0f;
+      float c = (primbox[i * 6 + k] + primbox[i * 6 + 3 + k]) * 0.5f;
+      float s = ((c - cb[k]) * inv) * 1024.0f;
+      s = fminf(fmaxf(s, 0.0f), 1023.0f);
+      q[k] = (uint32_t)s;
+    }
+    keys[i] = (expand10(q[0]) << 2) | (expand10(q[1]) << 1) | expand10(q[2]);
+    sorted[i] = i;
+  }
+  /* stable LSD counting sort, 4 x 8 bits */
+  for (int pass = 0; pass < 4; ++pass) {
+    int sh = pass * 8;
+    uint32_t cnt[257];
+    memset(cnt, 0, sizeof(cnt));
+    for (uint32_t i = 0; i < n; ++i) cnt[((keys[i] >> sh) & 255u) + 1]++;
+    for (int d = 0; d < 256; ++d) cnt[d + 1] += cnt[d];
+    for (uint32_t i = 0; i < n; ++i) {
+      uint32_t d = (keys[i] >> sh) & 255u;
+      k2[cnt[d]] = keys[i];
+      v2[cnt[d]] = sorted[i];
+      cnt[d]++;
+    }
+    memcpy(keys, k2, (size_t)n * 4);
+    memcpy(sorted, v2, (size_t)n * 4);
+  }
+  uint32_t depth = 1;
+  if (n == 1) {
+    onode nd;
+    memset(&nd, 0, sizeof(nd));
+    for (int k = 0; k < 3; ++k) {
+      nd.lo0[k] = nd.lo1[k] = primbox[k];
+      nd.hi0[k] = nd.hi1[k] = primbox[3 + k];
+    }
+    nd.c0 = nd.c1 = ~0;
+    nodes[0] = nd;
+  } else {
+    int ni = (int)n - 1;
+    int* child = (int*)malloc((size_t)ni * 8);
+    int* pint = (int*)malloc((size_t)ni * 4);
+    int* pleaf = (int*)malloc((size_t)n * 4);
+    float* nbox = (float*)malloc((size_t)ni * 24);
+    /* Karras 2012 (identical integer procedure to k_karras) */
+    for (int i = 0; i < ni; ++i) {
+      int d = (odelta(keys, (int)n, i, i + 1) - odelta(keys, (int)n, i, i - 1)) >= 0 ? 1 : -1;
+      int dmin = odelta(keys, (int)n, i, i - d);
+      int lmax = 2;
+      while (odelta(keys, (int)n, i, i + lmax * d) > dmin) lmax <<= 1;
+      int l = 0;
+      for (int t = lmax >> 1; t >= 1; t >>= 1)
+        if (odelta(keys, (int)n, i, i + (l + t) * d) > dmin) l += t;
+      int j = i + l * d;
+      int dn = odelta(keys, (int)n, i, j);
+      int s = 0, t = l;
+      for (;;) {
+        t = (t + 1) >> 1;
+        if (odelta(keys, (int)n, i, i + (s + t) * d) > dn) s += t;
+        if (t <= 1) break;
+      }
+      int g = i + s * d + (d < 0 ? d : 0);
+      int lo = i < j ? i : j, hi = i < j ? j : i;
+      int left = lo == g ? ~g : g, right = hi == g + 1 ? ~(g + 1) : g + 1;
+      child[2 * i] = left;
+      child[2 * i + 1] = right;
+      if (left >= 0) pint[left] = i; else pleaf[~left] = i;
+      if (right >= 0) pint[right] = i; else pleaf[~right] = i;
+    }
+    pint[0] = -1;
+    /* refit: post-order over internal nodes (children before parents) */
+    int* order = (int*)malloc((size_t)ni * 4);
+    int* stack = (int*)malloc((size_t)ni * 4 + 4);
+    int no = 0, sp = 0;
+    stack[sp++] = 0;
+    while (sp) {  /* pre-order, reversed later gives children-first for every parent */
+      int v = stack[--sp];
+      order[no++] = v;
+      for (int k = 0; k < 2; ++k) if (child[2 * v + k] >= 0) stack[sp++] = child[2 * v + k];
+    }
+    for (int q = no - 1; q >= 0; --q) {
+      int v = order[q];
+      float a[6], b[6];
+      box_of(child[2 * v], nbox, primbox, sorted, a);
+      box_of(child[2 * v + 1], nbox, primbox, sorted, b);
+      for (int k = 0; k < 3; ++k) {
+        nbox[v * 6 + k] = fminf(a[k], b[k]);
+        nbox[v * 6 + 3 + k] = fmaxf(a[3 + k], b[3 + k]);
+      }
+    }
+    for (int i = 0; i < ni; ++i) {
+      onode nd;
+      int c[2] = {child[2 * i], child[2 * i + 1]};
+      float b[2][6];
+      for (int k = 0; k < 2; ++k) box_of(c[k], nbox, primbox, sorted, b[k]);
+      for (int k = 0; k < 3; ++k) {
+        nd.lo0[k] = b[0][k]; nd.hi0[k] = b[0][3 + k];
+        nd.lo1[k] = b[1][k]; nd.hi1[k] = b[1][3 + k];
+      }
+      for (int k = 0; k < 2; ++k) if (c[k] < 0 && leaf_ref_is_prim) c[k] = ~(int)sorted[~c[k]];
+      nd.c0 = c[0]; nd.c1 = c[1]; nd.pad0 = nd.pad1 = 0;
+      nodes[i] = nd;
+    }
+    depth = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      uint32_t d = 1;
+      int node = pleaf[i];
+      while (pint[node] >= 0) { node = pint[node]; ++d; }
+      if (d > depth) depth = d;
+    }
+    free(order); free(stack); free(child); free(pint); free(pleaf); free(nbox);
+  }
+  free(keys); free(k2); free(v2);
+  return depth;
+}
+
+oracle_scene* oracle_scene_create(void) { return (oracle_scene*)calloc(1, sizeof(oracle_scene)); }
+
+void oracle_scene_destroy(oracle_scene* s) {
+  if (!s) return;
+  for (int i = 0; i < s->nblas; ++i) {
+    free(s->blas[i].nodes); free(s->blas[i].tris); free(s->blas[i].vtx); free(s->blas[i].idx);
+  }
+  free(s->blas); free(s->inst); free(s->tlas); free(s);
+}
+
+/* BottomLevelASGenerator semantics (nv_helpers_dx12/BottomLevelASGenerator.cpp:74-245) */
+int oracle_add_blas(oracle_scene* s, const float* vtx6, uint32_t nv, const uint32_t* idx, uint32_t icount) {
+  uint32_t ntri;
+  if (!vtx6 || nv == 0) return -1;
+  if (idx) {
+    if (icount == 0 || icount % 3) return -1;
+    for (uint32_t i = 0; i < icount; ++i) if (idx[i] >= nv) return -1;
+    ntri = icount / 3;
+  } else {
+    if (nv % 3) return -1;
+    ntri = nv / 3;
+  }
+  if (s->nblas == s->cblas) {
+    s->cblas = s->cblas ? s->cblas * 2 : 4;
+    s->blas = (oblas*)realloc(s->blas, (size_t)s->cblas * sizeof(oblas));
+  }
+  oblas* b = &s->blas[s->nblas];
+  memset(b, 0, sizeof(*b));
+  b->vtx = (float*)malloc((size_t)nv * 24);
+  memcpy(b->vtx, vtx6, (size_t)nv * 24);
+  if (idx) { b->idx = (uint32_t*)malloc((size_t)icount * 4); memcpy(b->idx, idx, (size_t)icount * 4); }
+  b->nv = nv;
+  b->ntri = ntri;
+  b->nnodes = ntri > 1 ? ntri - 1 : 1;
+  float* box = (float*)malloc((size_t)ntri * 24);
+  otri* un = (otri*)malloc((size_t)ntri * sizeof(otri));
+  for (uint32_t p = 0; p < ntri; ++p) {
+    uint32_t i0 = idx ? idx[3 * p] : 3 * p, i1 = idx ? idx[3 * p + 1] : 3 * p + 1, i2 = idx ? idx[3 * p + 2] : 3 * p + 2;
+    const float *a = vtx6 + (size_t)i0 * 6, *bb = vtx6 + (size_t)i1 * 6, *c = vtx6 + (size_t)i2 * 6;
+    otri t;
+    for (int k = 0; k < 3; ++k) {
+      t.v0[k] = a[k]; t.e1[k] = bb[k] - a[k]; t.e2[k] = c[k] - a[k];
+      box[p * 6 + k] = fminf(fminf(a[k], bb[k]), c[k]) + 0.0f; /* canonical +0 */
+      box[p * 6 + 3 + k] = fmaxf(fmaxf(a[k], bb[k]), c[k]) + 0.0f;
+    }
+    t.prim = p; t.pad1 = t.pad2 = 0;
+    un[p] = t;
+  }
+  uint32_t* sorted = (uint32_t*)malloc((size_t)ntri * 4);
+  b->nodes = (onode*)malloc((size_t)b->nnodes * sizeof(onode));
+  b->depth = lbvh(box, ntri, b->nodes, sorted, 0);
+  b->tris = (otri*)malloc((size_t)ntri * sizeof(otri));
+  for (uint32_t i = 0; i < ntri; ++i) b->tris[i] = un[sorted[i]];
+  for (int k = 0; k < 3; ++k) { b->bounds[k] = INFINITY; b->bounds[3 + k] = -INFINITY; }
+  for (uint32_t p = 0; p < ntri; ++p)
+    for (int k = 0; k < 3; ++k) {
+      b->bounds[k] = fminf(b->bounds[k], box[p * 6 + k]);
+      b->bounds[3 + k] = fmaxf(b->bounds[3 + k], box[p * 6 + 3 + k]);
+    }
+  free(box); free(un); free(sorted);
+  return s->nblas++;
+}
+
+static int inv3d(const double m[9], double inv[9]) {
+  double c00 = m[4] * m[8] - m[5] * m[7];
+  double c01 = m[5] * m[6] - m[3] * m[8];
+  double c02 = m[3] * m[7] - m[4] * m[6];
+  double det = m[0] * c00 + m[1] * c01 + m[2] * c02;
+  if (det == 0.0) return 0;
+  double r = 1.0 / det;
+  inv[0] = c00 * r; inv[1] = (m[2] * m[7] - m[1] * m[8]) * r; inv[2] = (m[1] * m[5] - m[2] * m[4]) * r;
+  inv[3] = c01 * r; inv[4] = (m[0] * m[8] - m[2] * m[6]) * r; inv[5] = (m[2] * m[3] - m[0] * m[5]) * r;
+  inv[6] = c02 * r; inv[7] = (m[1] * m[6] - m[0] * m[7]) * r; inv[8] = (m[0] * m[4] - m[1] * m[3]) * r;
+  return 1;
+}
+
+static vec3 xpoint(const float* m, vec3 p) {
+  return mk(((m[0] * p.x + m[1] * p.y) + m[2] * p.z) + m[3], ((m[4] * p.x + m[5] * p.y) + m[6] * p.z) + m[7],
+            ((m[8] * p.x + m[9] * p.y) + m[10] * p.z) + m[11]);
+}
+static vec3 xdir(const float* m, vec3 d) {
+  return mk((m[0] * d.x + m[1] * d.y) + m[2] * d.z, (m[4] * d.x + m[5] * d.y) + m[6] * d.z,
+            (m[8] * d.x + m[9] * d.y) + m[10] * d.z);
+}
+static vec3 m3mul(const float* m, vec3 d) {
+  return mk((m[0] * d.x + m[1] * d.y) + m[2] * d.z, (m[3] * d.x + m[4] * d.y) + m[5] * d.z,
+            (m[6] * d.x + m[7] * d.y) + m[8] * d.z);
+}
+
+/* TopLevelASGenerator (nv_helpers_dx12/TopLevelASGenerator.cpp:64-249) +
+ * UpdateInstancePropertiesBuffer (src/D3D12HelloTriangle.cpp:1181-1204) */
+int oracle_set_instances(oracle_scene* s, const oracle_instance* in, uint32_t n) {
+  if (!n) return -1;
+  free(s->inst); free(s->tlas);
+  s->inst = (oinst*)calloc(n, sizeof(oinst));
+  s->ninst = n;
+  float* box = (float*)malloc((size_t)n * 24);
+  for (uint32_t i = 0; i < n; ++i) {
+    if ((int)in[i].blas >= s->nblas) return -1;
+    oinst* r = &s->inst[i];
+    const float* M = in[i].xform;
+    double L[9] = {M[0], M[1], M[2], M[4], M[5], M[6], M[8], M[9], M[10]}, Li[9];
+    if (!inv3d(L, Li)) return -1;
+    double t[3] = {M[3], M[7], M[11]};
+    for (int a = 0; a < 3; ++a) {
+      r->w2o[a * 4 + 0] = (float)Li[a * 3 + 0];
+      r->w2o[a * 4 + 1] = (float)Li[a * 3 + 1];
+      r->w2o[a * 4 + 2] = (float)Li[a * 3 + 2];
+      r->w2o[a * 4 + 3] = (float)(-(Li[a * 3 + 0] * t[0] + Li[a * 3 + 1] * t[1] + Li[a * 3 + 2] * t[2]));
+    }
+    memcpy(r->o2w, M, 48);
+    for (int a = 0; a < 3; ++a) for (int b = 0; b < 3; ++b) r->nrm[a * 3 + b] = (float)Li[b * 3 + a];
+    r->instance_id = in[i].instance_id;
+    r->hit_group = in[i].hit_group;
+    r->blas = in[i].blas;
+    const float* bb = s->blas[in[i].blas].bounds;
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int c = 0; c < 8; ++c) {
+      vec3 p = mk((c & 1) ? bb[3] : bb[0], (c & 2) ? bb[4] : bb[1], (c & 4) ? bb[5] : bb[2]);
+      vec3 w = xpoint(M, p);
+      lo[0] = fminf(lo[0], w.x); lo[1] = fminf(lo[1], w.y); lo[2] = fminf(lo[2], w.z);
+      hi[0] = fmaxf(hi[0], w.x); hi[1] = fmaxf(hi[1], w.y); hi[2] = fmaxf(hi[2], w.z);
+    }
+    for (int k = 0; k < 3; ++k) { box[i * 6 + k] = lo[k] + 0.0f; box[i * 6 + 3 + k] = hi[k] + 0.0f; }
+  }
+  s->tlas_nodes = n > 1 ? n - 1 : 1;
+  s->tlas = (onode*)malloc((size_t)s->tlas_nodes * sizeof(onode));
+  uint32_t* sorted = (uint32_t*)malloc((size_t)n * 4);
+  s->tlas_depth = lbvh(box, n, s->tlas, sorted, 1);
+  free(sorted); free(box);
+  return 0;
+}
+
+int oracle_blas_info(const oracle_scene* s, int b, uint32_t out[3]) {
+  if (b < 0 || b >= s->nblas) return -1;
+  out[0] = s->blas[b].ntri; out[1] = s->blas[b].nnodes; out[2] = s->blas[b].depth;
+  return 0;
+}
+int oracle_tlas_info(const oracle_scene* s, uint32_t out[3]) {
+  if (!s->tlas) return -1;
+  out[0] = s->ninst; out[1] = s->tlas_nodes; out[2] = s->tlas_depth;
+  return 0;
+}
+int oracle_export_blas(const oracle_scene* s, int b, void* nodes, void* tris) {
+  if (b < 0 || b >= s->nblas) return -1;
+  if (nodes) memcpy(nodes, s->blas[b].nodes, (size_t)s->blas[b].nnodes * sizeof(onode));
+  if (tris) memcpy(tris, s->blas[b].tris, (size_t)s->blas[b].ntri * sizeof(otri));
+  return 0;
+}
+int oracle_export_tlas(const oracle_scene* s, void* nodes) {
+  if (!s->tlas) return -1;
+  memcpy(nodes, s->tlas, (size_t)s->tlas_nodes * sizeof(onode));
+  return 0;
+}
+
+/* ---------------------------------------------------------------------------------------- */
+/* traversal: DXR TraceRay semantics (closest hit / any hit), Common.hlsl:44-82               */
+/* ---------------------------------------------------------------------------------------- */
+typedef struct { uint64_t v[8]; } ostats;
+typedef struct { float t, u, v; uint32_t inst, prim; } ohit;
+
+static inline float sinv(float d) { return fabsf(d) > 1e-20f ? 1.0f / d : (d < 0.0f ? -1e20f : 1e20f); }
+
+static inline int oslab(const float* lo, const float* hi, vec3 invd, vec3 noinv, float tmin, float tbest, float* tnear) {
+  float tlx = fmaf(lo[0], invd.x, noinv.x), thx = fmaf(hi[0], invd.x, noinv.x);
+  float tly = fmaf(lo[1], invd.y, noinv.y), thy = fmaf(hi[1], invd.y, noinv.y);
+  float tlz = fmaf(lo[2], invd.z, noinv.z), thz = fmaf(hi[2], invd.z, noinv.z);
+  float tn = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), tmin));
+  float tf = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tbest));
+  *tnear = tn;
+  return tn <= tf * 1.0000004f;
+}
+
+/* Moller-Trumbore (the ray/triangle test DXR performs in hardware; formula pinned here) */
+static inline int omt(vec3 o, vec3 d, const otri* tr, float* t, float* u, float* v) {
+  vec3 v0 = ld3(tr->v0), e1 = ld3(tr->e1), e2 = ld3(tr->e2);
+  vec3 p = vcross(d, e2);
+  float det = vdot(e1, p);
+  if (det == 0.0f) return 0;
+  float inv = 1.0f / det;
+  vec3 s = vsub(o, v0);
+  *u = vdot(s, p) * inv;
+  if (!(*u >= 0.0f && *u <= 1.0f)) return 0;
+  vec3 q = vcross(s, e1);
+  *v = vdot(d, q) * inv;
+  if (!(*v >= 0.0f && *u + *v <= 1.0f)) return 0;
+  *t = vdot(e2, q) * inv;
+  return 1;
+}
+
+static inline int better(float t, uint32_t inst, uint32_t prim, const ohit* h) {
+  return t < h->t || (t == h->t && (inst < h->inst || (inst == h->inst && prim < h->prim)));
+}
+
+#define SENT INT32_MIN
+
+static int otrace(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax, int any, ohit* h, ostats* st) {
+  int stack[512];
+  int cap = (int)(s->tlas_depth + 2);
+  uint32_t maxb = 0;
+  for (int b = 0; b < s->nblas; ++b) if (s->blas[b].depth > maxb) maxb = s->blas[b].depth;
+  cap += (int)maxb;
+  if (cap > 512) cap = 512;
+  vec3 winvd = mk(sinv(d.x), sinv(d.y), sinv(d.z));
+  vec3 wno = vneg(vmul(o, winvd));
+  vec3 ro = o, rd = d, rinvd = winvd, rno = wno;
+  const onode* nodes = s->tlas;
+  const otri* tris = NULL;
+  uint32_t cur = 0;
+  int in_blas = 0, found = 0, sp = 0, ref = 0;
+  h->t = tmax; h->inst = 0xffffffffu; h->prim = 0xffffffffu; h->u = h->v = 0.0f;
+  for (;;) {
+    if (ref >= 0) {
+      const onode* nd = nodes + ref;
+      float tn0, tn1;
+      int h0 = oslab(nd->lo0, nd->hi0, rinvd, rno, tmin, h->t, &tn0);
+      int h1 = oslab(nd->lo1, nd->hi1, rinvd, rno, tmin, h->t, &tn1);
+      st->v[2] += 2;
+      if (h0 && h1) {
+        int sw = tn1 < tn0;
+        int nearc = sw ? nd->c1 : nd->c0, farc = sw ? nd->c0 : nd->c1;
+        if (sp < cap) stack[sp++] = farc; else st->v[5]++;
+        ref = nearc;
+        continue;
+      }
+      if (h0) { ref = nd->c0; continue; }
+      if (h1) { ref = nd->c1; continue; }
+    } else if (!in_blas) {
+      cur = (uint32_t)(~ref);
+      const oinst* ir = &s->inst[cur];
+      ro = xpoint(ir->w2o, o);
+      rd = xdir(ir->w2o, d);
+      rinvd = mk(sinv(rd.x), sinv(rd.y), sinv(rd.z));
+      rno = vneg(vmul(ro, rinvd));
+      nodes = s->blas[ir->blas].nodes;
+      tris = s->blas[ir->blas].tris;
+      in_blas = 1;
+      st->v[4]++;
+      if (sp < cap) { stack[sp++] = SENT; ref = 0; continue; }
+      st->v[5]++;
+      in_blas = 0; nodes = s->tlas; ro = o; rd = d; rinvd = winvd; rno = wno;
+    } else {
+      const otri* tr = tris + (~ref);
+      float t, u, v;
+      st->v[3]++;
+      if (omt(ro, rd, tr, &t, &u, &v) && t >= tmin && better(t, cur, tr->prim, h)) {
+        h->t = t; h->u = u; h->v = v; h->inst = cur; h->prim = tr->prim;
+        found = 1;
+        if (any) return 1;
+      }
+    }
+    for (;;) {
+      if (sp == 0) return found;
+      ref = stack[--sp];
+      if (ref != SENT) break;
+      in_blas = 0; nodes = s->tlas; ro = o; rd = d; rinvd = winvd; rno = wno;
+    }
+  }
+}
+
+/* every triangle of every instance, original primitive order */
+static int obrute(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax, int any, ohit* h, ostats* st) {
+  int found = 0;
+  h->t = tmax; h->inst = 0xffffffffu; h->prim = 0xffffffffu; h->u = h->v = 0.0f;
+  for (uint32_t i = 0; i < s->ninst; ++i) {
+    const oinst* ir = &s->inst[i];
+    const oblas* b = &s->blas[ir->blas];
+    vec3 ro = xpoint(ir->w2o, o), rd = xdir(ir->w2o, d);
+    for (uint32_t k = 0; k < b->ntri; ++k) {
+      const otri* tr = &b->tris[k];
+      float t, u, v;
+      st->v[3]++;
+      if (omt(ro, rd, tr, &t, &u, &v) && t >= tmin && better(t, i, tr->prim, h)) {
+        h->t = t; h->u = u; h->v = v; h->inst = i; h->prim = tr->prim;
+        found = 1;
+        if (any) return 1;
+      }
+    }
+  }
+  return found;
+}
+
+/* ---------------------------------------------------------------------------------------- */
+/* shading (shaders/Hit.hlsl, Miss.hlsl, ShadowRay.hlsl)                                     */
+/* ---------------------------------------------------------------------------------------- */
+static float olog2(float x) {
+  uint32_t b; memcpy(&b, &x, 4);
+  int e = (int)((b >> 23) & 0xffu) - 127;
+  uint32_t mb = (b & 0x7fffffu) | 0x3f800000u;
+  float m; memcpy(&m, &mb, 4);
+  if (m > 1.41421356f) { m = m * 0.5f; e = e + 1; }
+  float f = m - 1.0f;
+  float s = f / (2.0f + f);
+  float s2 = s * s;
+  float p = 1.0f / 11.0f;
+  p = p * s2 + 1.0f / 9.0f;
+  p = p * s2 + 1.0f / 7.0f;
+  p = p * s2 + 1.0f / 5.0f;
+  p = p * s2 + 1.0f / 3.0f;
+  p = p * s2 + 1.0f;
+  float ln = (2.0f * s) * p;
+  return (float)e + ln * 1.44269504f;
+}
+static float oexp2(float y) {
+  if (y < -126.0f) return 0.0f;
+  if (y > 127.0f) y = 127.0f;
+  float fi = floorf(y + 0.5f);
+  float f = y - fi;
+  float a = f * 0.693147181f;
+  float p = 1.0f / 40320.0f;
+  p = p * a + 1.0f / 5040.0f;
+  p = p * a + 1.0f / 720.0f;
+  p = p * a + 1.0f / 120.0f;
+  p = p * a + 1.0f / 24.0f;
+  p = p * a + 1.0f / 6.0f;
+  p = p * a + 0.5f;
+  p = p * a + 1.0f;
+  p = p * a + 1.0f;
+  int i = (int)fi;
+  uint32_t sb = (uint32_t)(i + 127) << 23;
+  float sc; memcpy(&sc, &sb, 4);
+  return p * sc;
+}
+/* HLSL pow(x, y) for x >= 0, pinned to a deterministic exp2(y log2 x) */
+float oracle_pow(float x, float y) { if (!(x > 1e-30f)) return 0.0f; return oexp2(y * olog2(x)); }
+
+static const float OPI = 3.14159265359f; /* Common.hlsl:1 */
+
+/* CalculateDirectLighting (Hit.hlsl:83-95) */
+static vec3 odirect(vec3 P, vec3 n, vec3 albedo, const oracle_light* L, uint32_t nl) {
+  vec3 c = mk(0, 0, 0);
+  for (uint32_t l = 0; l < nl; ++l) {
+    vec3 lp = ld3(L[l].position), lc = ld3(L[l].color);
+    vec3 tl = vneg(vnorm(vsub(lp, P)));
+    float f = vdot(n, tl);
+    float ti = fmax2(0.0f, f * L[l].intensity);
+    c = vadd(c, vscale(vmul(albedo, lc), ti));
+  }
+  return c;
+}
+
+/* CalculatePBRShading (Hit.hlsl:97-174) with FresnelSchlick :97-100, GGX :102-113,
+ * SchlickGGX :115-122, Smith :124-130 */
+static vec3 opbr(vec3 n, vec3 cam, vec3 P, const oracle_light* Ls, uint32_t nl, const float* mat) {
+  vec3 albedo = ld3(mat);
+  float rough = mat[3], metal = mat[4];
+  vec3 N = vneg(vnorm(n));
+  vec3 V = vnorm(vsub(cam, P));
+  vec3 L0 = mk(0, 0, 0);
+  for (uint32_t l = 0; l < nl; ++l) {
+    vec3 lp = ld3(Ls[l].position), lc = ld3(Ls[l].color);
+    vec3 L = vnorm(vsub(lp, P));
+    vec3 H = vnorm(vadd(V, L));
+    vec3 dv = vsub(lp, P);
+    float dist = sqrtf(vdot(dv, dv));
+    float att = 1.0f / fmax2(dist * dist, 1.0f);
+    vec3 radiance = vscale(lc, att);
+    vec3 F0 = mk(0.04f + metal * (albedo.x - 0.04f), 0.04f + metal * (albedo.y - 0.04f), 0.04f + metal * (albedo.z - 0.04f));
+    float x = 1.0f - fmax2(vdot(H, V), 0.0f);
+    x = fmin2(fmax2(x, 0.0f), 1.0f);
+    float x5 = ((x * x) * (x * x)) * x;
+    vec3 F = mk(F0.x + (1.0f - F0.x) * x5, F0.y + (1.0f - F0.y) * x5, F0.z + (1.0f - F0.z) * x5);
+    float a = rough * rough, a2 = a * a;
+    float NdotH = fmax2(vdot(N, H), 0.0f);
+    float NdotH2 = NdotH * NdotH;
+    float denom = NdotH2 * (a2 - 1.0f) + 1.0f;
+    denom = (OPI * denom) * denom;
+    float NDF = a2 / denom;
+    float r = rough + 1.0f;
+    float k = (r * r) / 8.0f;
+    float NdotV = fmax2(vdot(N, V), 0.0f);
+    float NdotL = fmax2(vdot(N, L), 0.0f);
+    float ggx2 = NdotV / (NdotV * (1.0f - k) + k);
+    float ggx1 = NdotL / (NdotL * (1.0f - k) + k);
+    float G = ggx1 * ggx2;
+    vec3 num = vscale(F, NDF * G);
+    float den = (4.0f * fmax2(vdot(N, V), 0.0f)) * fmax2(vdot(N, L), 0.0f) + 0.0001f;
+    vec3 spec = mk(num.x / den, num.y / den, num.z / den);
+    vec3 kD = mk(1.0f - F.x, 1.0f - F.y, 1.0f - F.z);
+    float km = 1.0f - metal;
+    kD = mk(kD.x * km, kD.y * km, kD.z * km);
+    vec3 diff = mk((kD.x * albedo.x) / OPI, (kD.y * albedo.y) / OPI, (kD.z * albedo.z) / OPI);
+    float NdL = fmax2(vdot(N, L), 0.0f);
+    L0 = vadd(L0, vscale(vmul(vadd(diff, spec), radiance), NdL));
+  }
+  vec3 c = vscale(L0, 0.2f);
+  c = mk(c.x / (c.x + 1.0f), c.y / (c.y + 1.0f), c.z / (c.z + 1.0f));
+  float g = 1.0f / 2.2f;
+  return mk(oracle_pow(c.x, g), oracle_pow(c.y, g), oracle_pow(c.z, g));
+}
+
+void oracle_pbr(const float n[3], const float cam[3], const float P[3], const oracle_light* lights, uint32_t nl,
+                const float material[6], float out[3]) {
+  vec3 r = opbr(ld3(n), ld3(cam), ld3(P), lights, nl, material);
+  out[0] = r.x; out[1] = r.y; out[2] = r.z;
+}
+void oracle_direct(const float n[3], const float P[3], const oracle_light* lights, uint32_t nl, const float albedo[3], float out[3]) {
+  vec3 r = odirect(ld3(P), ld3(n), ld3(albedo), lights, nl);
+  out[0] = r.x; out[1] = r.y; out[2] = r.z;
+}
+
+static void tri_ids(const oblas* b, uint32_t prim, uint32_t* i0, uint32_t* i1, uint32_t* i2) {
+  if (b->idx) { *i0 = b->idx[3 * prim]; *i1 = b->idx[3 * prim + 1]; *i2 = b->idx[3 * prim + 2]; }
+  else { *i0 = 3 * prim; *i1 = 3 * prim + 1; *i2 = 3 * prim + 2; }
+}
+
+/* CalculateInterpolatedWorldNormal (Hit.hlsl:67-81) */
+static vec3 o_interp_normal(const oracle_scene* s, uint32_t inst, uint32_t prim, float u, float v) {
+  const oinst* ir = &s->inst[inst];
+  const oblas* b = &s->blas[ir->blas];
+  uint32_t i0, i1, i2;
+  tri_ids(b, prim, &i0, &i1, &i2);
+  vec3 n0 = ld3(b->vtx + (size_t)i1 * 6 + 3), n1 = ld3(b->vtx + (size_t)i2 * 6 + 3), n2 = ld3(b->vtx + (size_t)i0 * 6 + 3);
+  float bz = (1.0f - u) - v;
+  vec3 n = vnorm(vadd(vadd(vscale(n0, u), vscale(n1, v)), vscale(n2, bz)));
+  n = m3mul(ir->nrm, n);
+  return vnorm(n);
+}
+
+/* PlaneClosestHit face normal (Hit.hlsl:218-222) */
+static vec3 o_face_normal(const oracle_scene* s, uint32_t inst, uint32_t prim) {
+  const oinst* ir = &s->inst[inst];
+  const oblas* b = &s->blas[ir->blas];
+  uint32_t i0, i1, i2;
+  tri_ids(b, prim, &i0, &i1, &i2);
+  vec3 p0 = ld3(b->vtx + (size_t)i0 * 6), p1 = ld3(b->vtx + (size_t)i1 * 6), p2 = ld3(b->vtx + (size_t)i2 * 6);
+  vec3 n = vnorm(vcross(vsub(p1, p0), vsub(p2, p0)));
+  return m3mul(ir->nrm, n);
+}
+
+typedef struct {
+  const oracle_scene* s;
+  const float* cb;
+  const oracle_light* L;
+  uint32_t nl;
+  const float* mat;
+  int mode, k, brute;
+  uint32_t W, H;
+} octx;
+
+static int trace_any(const octx* c, vec3 P, vec3 dir, ostats* st) {
+  ohit h;
+  st->v[1]++;
+  vec3 d = vnorm(dir); /* CastShadowRay normalises (Common.hlsl:73) */
+  return c->brute ? obrute(c->s, P, d, 0.01f, 100000.0f, 1, &h, st) : otrace(c->s, P, d, 0.01f, 100000.0f, 1, &h, st);
+}
+
+static void hlsl_mul4(const float* m, const float v[4], float r[4]) {
+  for (int i = 0; i < 4; ++i) r[i] = ((m[i] * v[0] + m[4 + i] * v[1]) + m[8 + i] * v[2]) + m[12 + i] * v[3];
+}
+
+/* RayGen (RayGen.hlsl:28-43) + hit/miss programs for one camera sample */
+static vec3 osample(const octx* c, uint32_t px, uint32_t py, float ox, float oy, ostats* st) {
+  float dx = (((float)px + ox) / (float)c->W) * 2.0f - 1.0f;
+  float dy = (((float)py + oy) / (float)c->H) * 2.0f - 1.0f;
+  float org[4], dcam[4], dw[4];
+  const float z1[4] = {0, 0, 0, 1};
+  hlsl_mul4(c->cb + 32, z1, org);
+  const float ndc[4] = {dx, -dy, 1.0f, 1.0f};
+  hlsl_mul4(c->cb + 48, ndc, dcam);
+  const float dc4[4] = {dcam[0], dcam[1], dcam[2], 0.0f};
+  hlsl_mul4(c->cb + 32, dc4, dw);
+  vec3 O = mk(org[0], org[1], org[2]);
+  vec3 D = vnorm(mk(dw[0], dw[1], dw[2]));
+  ohit h;
+  st->v[0]++;
+  int f = c->brute ? obrute(c->s, O, D, 0.0f, 100000.0f, 0, &h, st) : otrace(c->s, O, D, 0.0f, 100000.0f, 0, &h, st);
+  if (!f) {
+    float ramp = (float)py / (float)c->H; /* Miss.hlsl:8-9 */
+    return mk(0.0f, 0.2f, 0.7f - 0.3f * ramp);
+  }
+  const oinst* ir = &c->s->inst[h.inst];
+  vec3 P = vadd(O, vscale(D, h.t));
+  int plane = ir->hit_group == 2u;
+  if (c->mode == 0) {
+    if (plane) { /* PlaneClosestHit (Hit.hlsl:207-241) */
+      vec3 lp = ld3(c->L[0].position);
+      vec3 ld = vnorm(vsub(lp, P));
+      vec3 n = o_face_normal(c->s, h.inst, h.prim);
+      int shadowed = vdot(n, ld) < 0.0f;
+      int occ = trace_any(c, P, ld, st);
+      if (!shadowed) shadowed = occ;
+      float factor = shadowed ? 0.3f : 1.0f;
+      float li = fmax2(0.0f, vdot(n, ld));
+      float v = (1.0f * li) * factor;
+      return mk(v, v, v);
+    }
+    /* ClosestHit (Hit.hlsl:183-204), reflectivity pinned to 0 */
+    vec3 n = o_interp_normal(c->s, h.inst, h.prim, h.u, h.v);
+    vec3 direct = odirect(P, n, ld3(c->mat), c->L, c->nl);
+    return vadd(direct, opbr(n, O, P, c->L, c->nl, c->mat));
+  }
+  vec3 n = plane ? o_face_normal(c->s, h.inst, h.prim) : vneg(o_interp_normal(c->s, h.inst, h.prim, h.u, h.v));
+  float sum = 0.0f;
+  for (uint32_t l = 0; l < c->nl; ++l) {
+    vec3 L = vnorm(vsub(ld3(c->L[l].position), P));
+    float nl = vdot(n, L);
+    if (nl > 0.0f) {
+      float factor = 1.0f;
+      if (c->mode == 1 && trace_any(c, P, L, st)) factor = 0.3f;
+      sum = sum + nl * factor;
+    }
+  }
+  sum = sum / (float)c->nl;
+  return mk(sum, sum, sum);
+}
+
+static uint32_t unorm8(float x) {
+  if (!(x > 0.0f)) return 0u;
+  if (x >= 1.0f) return 255u;
+  return (uint32_t)(x * 255.0f + 0.5f);
+}
+
+typedef struct {
+  const octx* c;
+  const uint32_t* rows;
+  uint32_t nrows, tid, nthreads;
+  uint8_t* rgba8;
+  float* rgba32f;
+  ostats st;
+} ojob;
+
+static void* render_rows(void* arg) {
+  ojob* j = (ojob*)arg;
+  const octx* c = j->c;
+  for (uint32_t r = j->tid; r < j->nrows; r += j->nthreads) {
+    uint32_t py = j->rows ? j->rows[r] : r;
+    for (uint32_t px = 0; px < c->W; ++px) {
+      vec3 acc = mk(0, 0, 0);
+      for (int sy = 0; sy < c->k; ++sy)
+        for (int sx = 0; sx < c->k; ++sx) {
+          float ox = ((float)sx + 0.5f) / (float)c->k, oy = ((float)sy + 0.5f) / (float)c->k;
+          acc = vadd(acc, osample(c, px, py, ox, oy, &j->st));
+        }
+      if (c->k > 1) {
+        float ns = (float)(c->k * c->k);
+        acc = mk(acc.x / ns, acc.y / ns, acc.z / ns);
+      }
+      size_t o = (size_t)r * c->W + px;
+      if (j->rgba8) {
+        j->rgba8[o * 4 + 0] = (uint8_t)unorm8(acc.x);
+        j->rgba8[o * 4 + 1] = (uint8_t)unorm8(acc.y);
+        j->rgba8[o * 4 + 2] = (uint8_t)unorm8(acc.z);
+        j->rgba8[o * 4 + 3] = 255;
+      }
+      if (j->rgba32f) {
+        j->rgba32f[o * 4 + 0] = acc.x; j->rgba32f[o * 4 + 1] = acc.y;
+        j->rgba32f[o * 4 + 2] = acc.z; j->rgba32f[o * 4 + 3] = 1.0f;
+      }
+    }
+  }
+  return NULL;
+}
+
+int oracle_render(const oracle_scene* s, const float cb[64], const oracle_light* lights, uint32_t nlights,
+                  const float material[6], int mode, int spp, uint32_t W, uint32_t H, const uint32_t* rows,
+                  uint32_t nrows, uint8_t* rgba8, float* rgba32f, int nthreads, uint64_t* stats, int brute) {
+  if (!s || !s->tlas || !cb || !lights || nlights < 1 || nlights > 16 || W == 0 || H == 0) return -1;
+  int k = 0;
+  for (int q = 1; q <= 4; ++q) if (q * q == spp) k = q;
+  if (!k || mode < 0 || mode > 2) return -1;
+  if (!rows) nrows = H;
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  octx c = {s, cb, lights, nlights, material, mode, k, brute, W, H};
+  ojob jobs[256];
+  pthread_t th[256];
+  for (int t = 0; t < nthreads; ++t) {
+    memset(&jobs[t], 0, sizeof(ojob));
+    jobs[t].c = &c; jobs[t].rows = rows; jobs[t].nrows = nrows;
+    jobs[t].tid = (uint32_t)t; jobs[t].nthreads = (uint32_t)nthreads;
+    jobs[t].rgba8 = rgba8; jobs[t].rgba32f = rgba32f;
+  }
+  if (nthreads == 1) render_rows(&jobs[0]);
+  else {
+    for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, render_rows, &jobs[t]);
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+  }
+  if (stats)
+    for (int t = 0; t < nthreads; ++t)
+      for (int q = 0; q < 6; ++q) stats[q] += jobs[t].st.v[q];
+  if (stats) { stats[6] += (uint64_t)W * nrows; stats[7] += 1; }
+  return 0;
+}
+
+int oracle_trace_rays(const oracle_scene* s, const float* rays, uint32_t n, int any, uint32_t* hits, float* uv,
+                      int brute, uint64_t* stats) {
+  if (!s || !s->tlas) return -1;
+  ostats st;
+  memset(&st, 0, sizeof(st));
+  for (uint32_t i = 0; i < n; ++i) {
+    const float* r = rays + (size_t)i * 8;
+    ohit h;
+    int f = brute ? obrute(s, ld3(r), ld3(r + 4), r[3], r[7], any, &h, &st)
+                  : otrace(s, ld3(r), ld3(r + 4), r[3], r[7], any, &h, &st);
+    st.v[0]++;
+    float t = f ? h.t : r[7];
+    uint32_t tb; memcpy(&tb, &t, 4);
+    hits[i * 4 + 0] = tb;
+    hits[i * 4 + 1] = f ? h.inst : 0xffffffffu;
+    hits[i * 4 + 2] = f ? h.prim : 0xffffffffu;
+    hits[i * 4 + 3] = f ? 1u : 0u;
+    if (uv) { uv[i * 2] = f ? h.u : 0.0f; uv[i * 2 + 1] = f ? h.v : 0.0f; }
+  }
+  if (stats) for (int q = 0; q < 6; ++q) stats[q] += st.v[q];
+  return 0;
+}

@@ -1,0 +1,80 @@
+/*
+ * rt_oracle.h — CPU ORACLE (test infrastructure, not product code).
+ *
+ * Scalar C restatement of the reference's ray-tracing path, used only by tests/, by
+ * __graft_entry__.smoke() and by bench.py's cpu_baseline leg, as the checker. Nothing in the
+ * product (realtimeraytracing_gradproject_amd/) links or calls it.
+ *
+ * Parity status (see DESIGN.md "Oracle"):
+ *   - OBJ ingest and camera lookAt: pinned against outputs of the reference's own C++ (glm
+ *     harness in oracle/_ref, counts/first-vertex/first-face goldens recorded in SURVEY.md §8c).
+ *   - HLSL shading, DXR traversal/intersection, DirectXMath inverse/normalize/SinCos: the reference
+ *     runs only under D3D12/DXR on Windows, so these are parity unpinned against reference
+ *     execution; they are restated from the source text (file:line cited per function in
+ *     rt_oracle.c) and cross-checked by an independent numpy restatement (oracle/np_reference.py).
+ */
+#ifndef RT_ORACLE_H
+#define RT_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct oracle_scene oracle_scene;
+
+typedef struct {
+  uint32_t blas;
+  float xform[12]; /* object-to-world 3x4 row-major */
+  uint32_t instance_id;
+  uint32_t hit_group; /* 0 model, 2 plane */
+} oracle_instance;
+
+typedef struct {
+  float color[3];
+  float position[3];
+  float intensity;
+} oracle_light;
+
+/* ingest / host math */
+int oracle_obj_parse(const char* text, size_t len, float** vtx6, uint32_t* nv, uint32_t** idx, uint32_t* ni);
+void oracle_free(void* p);
+int oracle_vertex_normals(float* vtx6, uint32_t nv, const uint32_t* idx, uint32_t ni);
+void oracle_camera_lookat(const float eye[3], const float center[3], const float up[3], float view[16]);
+void oracle_camera_buffer(const float view[16], uint32_t W, uint32_t H, float fov_deg, float znear, float zfar, float cb[64]);
+
+/* scene */
+oracle_scene* oracle_scene_create(void);
+void oracle_scene_destroy(oracle_scene* s);
+/* returns BLAS id >= 0, or < 0 on error. vtx6: {pos, normal} per vertex. idx NULL = non-indexed. */
+int oracle_add_blas(oracle_scene* s, const float* vtx6, uint32_t nv, const uint32_t* idx, uint32_t icount);
+int oracle_set_instances(oracle_scene* s, const oracle_instance* inst, uint32_t n);
+/* info: out[0] prims, out[1] nodes, out[2] depth */
+int oracle_blas_info(const oracle_scene* s, int blas, uint32_t out[3]);
+int oracle_tlas_info(const oracle_scene* s, uint32_t out[3]);
+int oracle_export_blas(const oracle_scene* s, int blas, void* nodes, void* tris);
+int oracle_export_tlas(const oracle_scene* s, void* nodes);
+
+/* render W x H (rows NULL = all). stats[8] accumulates (same slots as RT_STAT_*), may be NULL.
+ * brute_force != 0: closest hit by testing every triangle of every instance (no BVH). */
+int oracle_render(const oracle_scene* s, const float cb[64], const oracle_light* lights, uint32_t nlights,
+                  const float material[6], int mode, int spp, uint32_t W, uint32_t H, const uint32_t* rows,
+                  uint32_t nrows, uint8_t* rgba8, float* rgba32f, int nthreads, uint64_t* stats,
+                  int brute_force);
+/* batch trace: rays n x 8 floats, hits n x 4 u32 (t bits, instance, prim, flag), uv n x 2 (may be NULL) */
+int oracle_trace_rays(const oracle_scene* s, const float* rays, uint32_t n, int any_hit, uint32_t* hits,
+                      float* uv, int brute_force, uint64_t* stats);
+
+/* shading building blocks exposed for known-answer tests */
+void oracle_pbr(const float n[3], const float cam[3], const float P[3], const oracle_light* lights,
+                uint32_t nlights, const float material[6], float out[3]);
+void oracle_direct(const float n[3], const float P[3], const oracle_light* lights, uint32_t nlights,
+                   const float albedo[3], float out[3]);
+float oracle_pow(float x, float y);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

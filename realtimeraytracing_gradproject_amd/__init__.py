@@ -1,0 +1,392 @@
+"""MI355X-native ray tracer — Python view of the C-ABI in include/rt_api.h.
+
+The product is the HIP library ``lib/librtamd.so`` (gfx950 kernels + host C++). This module only
+binds its C entry points with ctypes for tests and the bench; it never computes a frame itself and
+there is no CPU fallback: if the library is missing, importing the package raises.
+
+torch is imported first on purpose: it loads the HIP runtime that the library then shares, so
+device pointers and hipStream_t handles from torch tensors are valid in the library.
+"""
+from __future__ import annotations
+
+import ctypes
+import gzip
+import os
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+
+try:  # share torch's HIP runtime when torch is present
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is part of the image
+    torch = None
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "librtamd.so")
+ASSETS = os.path.join(_HERE, "assets")
+
+RT_OK, RT_E_INVALID, RT_E_OOM, RT_E_HIP, RT_E_RCCL, RT_E_UNSUPPORTED, RT_E_IO = 0, -1, -2, -3, -4, -5, -6
+RT_HITGROUP_MODEL, RT_HITGROUP_SHADOW, RT_HITGROUP_PLANE = 0, 1, 2
+RT_SHADE_REF, RT_SHADE_LAMBERT_SHADOW, RT_SHADE_PRIMARY = 0, 1, 2
+RT_SCHED_MEGAKERNEL, RT_SCHED_WAVEFRONT = 0, 1
+STAT_NAMES = ("primary_rays", "shadow_rays", "aabb_tests", "tri_tests", "instance_entries",
+              "stack_overflows", "pixels", "dispatches")
+
+
+class RtError(RuntimeError):
+    """Non-zero rt_status (the reference's ThrowIfFailed, DXSampleHelper.h:16-22)."""
+
+    def __init__(self, status: int, msg: str = ""):
+        self.status = status
+        super().__init__(f"{_status_name(status)}: {msg}" if msg else _status_name(status))
+
+
+class rt_instance(ctypes.Structure):
+    _fields_ = [("blas", ctypes.c_uint32), ("xform3x4_rowmajor", ctypes.c_float * 12),
+                ("instance_id", ctypes.c_uint32), ("hit_group", ctypes.c_uint32)]
+
+
+class rt_light(ctypes.Structure):
+    _fields_ = [("color", ctypes.c_float * 3), ("position", ctypes.c_float * 3),
+                ("intensity", ctypes.c_float)]
+
+
+class rt_material(ctypes.Structure):
+    _fields_ = [("albedo", ctypes.c_float * 3), ("roughness", ctypes.c_float),
+                ("metallic", ctypes.c_float), ("reflectivity", ctypes.c_float)]
+
+
+class rt_bvh_info(ctypes.Structure):
+    _fields_ = [("prim_count", ctypes.c_uint32), ("node_count", ctypes.c_uint32),
+                ("depth", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("bounds_lo", ctypes.c_float * 3), ("bounds_hi", ctypes.c_float * 3),
+                ("build_ms", ctypes.c_double)]
+
+
+_P = ctypes.c_void_p
+_U32 = ctypes.c_uint32
+_I = ctypes.c_int
+_FP = ctypes.POINTER(ctypes.c_float)
+_UP = ctypes.POINTER(ctypes.c_uint32)
+
+# (name, restype, argtypes) — every function declared in include/rt_api.h
+SIGNATURES = [
+    ("rt_api_version", _I, []),
+    ("rt_status_string", ctypes.c_char_p, [_I]),
+    ("rt_last_error", ctypes.c_char_p, [_P]),
+    ("rt_create", _I, [_I, ctypes.POINTER(_P)]),
+    ("rt_destroy", _I, [_P]),
+    ("rt_blas_build", _I, [_P, _P, _U32, _U32, _P, _U32, _UP]),
+    ("rt_blas_rebuild", _I, [_P, _U32, _P, _U32, _U32, _P, _U32]),
+    ("rt_blas_info", _I, [_P, _U32, ctypes.POINTER(rt_bvh_info)]),
+    ("rt_blas_export", _I, [_P, _U32, _P, ctypes.c_size_t, _P, ctypes.c_size_t]),
+    ("rt_tlas_build", _I, [_P, ctypes.POINTER(rt_instance), _U32, _I]),
+    ("rt_tlas_info", _I, [_P, ctypes.POINTER(rt_bvh_info)]),
+    ("rt_tlas_export", _I, [_P, _P, ctypes.c_size_t]),
+    ("rt_set_camera", _I, [_P, _FP]),
+    ("rt_set_shading", _I, [_P, ctypes.POINTER(rt_light), _U32, ctypes.POINTER(rt_material), _I, _I]),
+    ("rt_set_schedule", _I, [_P, _I]),
+    ("rt_set_stats", _I, [_P, _I]),
+    ("rt_dispatch_rays", _I, [_P, _U32, _U32, _P, _U32, _P, _P, _P]),
+    ("rt_trace_rays", _I, [_P, _P, _U32, _I, _P, _P, _P]),
+    ("rt_assemble_strips", _I, [_P, _U32, _U32, _U32, _U32, _P, _P, _P]),
+    ("rt_strip_rows", _U32, [_U32, _U32, _U32, _U32, _P, _U32]),
+    ("rt_stats", _I, [_P, ctypes.POINTER(ctypes.c_uint64)]),
+    ("rt_stats_reset", _I, [_P]),
+    ("rt_mesh_load_obj", _I, [ctypes.c_char_p, ctypes.POINTER(_P)]),
+    ("rt_mesh_parse_obj", _I, [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(_P)]),
+    ("rt_mesh_free", None, [_P]),
+    ("rt_mesh_vertex_count", _U32, [_P]),
+    ("rt_mesh_index_count", _U32, [_P]),
+    ("rt_mesh_vertices", _FP, [_P]),
+    ("rt_mesh_indices", _UP, [_P]),
+    ("rt_mesh_compute_vertex_normals", _I, [_P]),
+    ("rt_plane_vertices", None, [_FP]),
+    ("rt_camera_lookat", None, [_FP, _FP, _FP, _FP]),
+    ("rt_camera_buffer", None, [_FP, _U32, _U32, ctypes.c_float, ctypes.c_float, ctypes.c_float, _FP]),
+]
+
+
+def _load() -> ctypes.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build the HIP library first "
+            "(python -c 'import __graft_entry__ as g; g.build()' or `make`). There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def _status_name(st: int) -> str:
+    return lib.rt_status_string(st).decode()
+
+
+def _fptr(a: np.ndarray):
+    return a.ctypes.data_as(_FP)
+
+
+def _f32(x, n=None) -> np.ndarray:
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.float32))
+    if n is not None and a.size != n:
+        raise ValueError(f"expected {n} floats, got {a.size}")
+    return a
+
+
+# ---------------------------------------------------------------------------------------------
+# host services (no GPU)
+# ---------------------------------------------------------------------------------------------
+
+class Mesh:
+    """OBJFileManager::LoadObjFile result (OBJ_FileManager.cpp:10-71) held by the C library."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @classmethod
+    def load_obj(cls, path: str) -> "Mesh":
+        h = _P()
+        st = lib.rt_mesh_load_obj(path.encode(), ctypes.byref(h))
+        if st != RT_OK:
+            raise RtError(st, f"cannot load {path}")
+        return cls(h)
+
+    @classmethod
+    def parse_obj(cls, text: bytes) -> "Mesh":
+        h = _P()
+        st = lib.rt_mesh_parse_obj(text, len(text), ctypes.byref(h))
+        if st != RT_OK:
+            raise RtError(st, "parse failed")
+        return cls(h)
+
+    @classmethod
+    def asset(cls, name: str) -> "Mesh":
+        """A model shipped with the package (teapot, rabbit), stored gzip-compressed."""
+        with gzip.open(os.path.join(ASSETS, f"{name}.obj.gz"), "rb") as f:
+            return cls.parse_obj(f.read())
+
+    def __del__(self):
+        if getattr(self, "_h", None) and lib is not None:
+            lib.rt_mesh_free(self._h)
+            self._h = None
+
+    @property
+    def vertex_count(self) -> int:
+        return lib.rt_mesh_vertex_count(self._h)
+
+    @property
+    def index_count(self) -> int:
+        return lib.rt_mesh_index_count(self._h)
+
+    @property
+    def vertices(self) -> np.ndarray:
+        n = self.vertex_count
+        if n == 0:
+            return np.zeros((0, 6), np.float32)
+        return np.ctypeslib.as_array(lib.rt_mesh_vertices(self._h), shape=(n * 6,)).reshape(n, 6).copy()
+
+    @property
+    def indices(self) -> np.ndarray:
+        n = self.index_count
+        if n == 0:
+            return np.zeros((0,), np.uint32)
+        return np.ctypeslib.as_array(lib.rt_mesh_indices(self._h), shape=(n,)).copy()
+
+    def compute_vertex_normals(self) -> "Mesh":
+        st = lib.rt_mesh_compute_vertex_normals(self._h)
+        if st != RT_OK:
+            raise RtError(st, "ComputeVertexNormals")
+        return self
+
+
+def plane_vertices() -> np.ndarray:
+    out = np.zeros(36, np.float32)
+    lib.rt_plane_vertices(_fptr(out))
+    return out.reshape(6, 6)
+
+
+def camera_lookat(eye, center, up) -> np.ndarray:
+    e, c, u = _f32(eye, 3), _f32(center, 3), _f32(up, 3)
+    out = np.zeros(16, np.float32)
+    lib.rt_camera_lookat(_fptr(e), _fptr(c), _fptr(u), _fptr(out))
+    return out
+
+
+def camera_buffer(view, width: int, height: int, fov_deg: float = 45.0, znear: float = 0.1,
+                  zfar: float = 1000.0) -> np.ndarray:
+    v = _f32(view, 16)
+    out = np.zeros(64, np.float32)
+    lib.rt_camera_buffer(_fptr(v), width, height, fov_deg, znear, zfar, _fptr(out))
+    return out
+
+
+def strip_rows(height: int, nranks: int, rank: int, strip_rows_: int = 8) -> np.ndarray:
+    n = lib.rt_strip_rows(height, nranks, rank, strip_rows_, None, 0)
+    out = np.zeros(n, np.uint32)
+    lib.rt_strip_rows(height, nranks, rank, strip_rows_, out.ctypes.data_as(_P), n)
+    return out
+
+
+def strip_rows_per_rank(height: int, nranks: int, strip_rows_: int = 8) -> int:
+    """Rows of the padded per-rank buffer that rt_assemble_strips expects (rank-major blocks)."""
+    nstrips = (height + strip_rows_ - 1) // strip_rows_
+    return ((nstrips + nranks - 1) // nranks) * strip_rows_
+
+
+# ---------------------------------------------------------------------------------------------
+# device context
+# ---------------------------------------------------------------------------------------------
+
+def _ptr(x) -> Optional[int]:
+    """Device pointer of a torch tensor, an int address, or None."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    return x.data_ptr()
+
+
+class Context:
+    """One rt_ctx (one HIP device, one host thread)."""
+
+    def __init__(self, device: int = 0):
+        h = _P()
+        st = lib.rt_create(device, ctypes.byref(h))
+        if st != RT_OK:
+            raise RtError(st, f"rt_create(device={device})")
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None) and lib is not None:
+            lib.rt_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, st: int, what: str):
+        if st != RT_OK:
+            raise RtError(st, f"{what}: {lib.rt_last_error(self._h).decode()}")
+
+    # acceleration structures ------------------------------------------------------------------
+    def blas_build(self, vertices: np.ndarray, indices: Optional[np.ndarray] = None) -> int:
+        v = np.ascontiguousarray(vertices, dtype=np.float32)
+        stride = v.shape[1] * 4 if v.ndim == 2 else 24
+        nv = v.shape[0] if v.ndim == 2 else v.size // 6
+        out = _U32()
+        if indices is None:
+            st = lib.rt_blas_build(self._h, v.ctypes.data_as(_P), nv, stride, None, 0, ctypes.byref(out))
+        else:
+            i = np.ascontiguousarray(indices, dtype=np.uint32)
+            st = lib.rt_blas_build(self._h, v.ctypes.data_as(_P), nv, stride, i.ctypes.data_as(_P), i.size,
+                                   ctypes.byref(out))
+        self._check(st, "rt_blas_build")
+        return out.value
+
+    def blas_rebuild(self, blas: int, vertices: np.ndarray, indices: Optional[np.ndarray] = None):
+        v = np.ascontiguousarray(vertices, dtype=np.float32)
+        stride = v.shape[1] * 4
+        if indices is None:
+            st = lib.rt_blas_rebuild(self._h, blas, v.ctypes.data_as(_P), v.shape[0], stride, None, 0)
+        else:
+            i = np.ascontiguousarray(indices, dtype=np.uint32)
+            st = lib.rt_blas_rebuild(self._h, blas, v.ctypes.data_as(_P), v.shape[0], stride,
+                                     i.ctypes.data_as(_P), i.size)
+        self._check(st, "rt_blas_rebuild")
+
+    def blas_info(self, blas: int) -> rt_bvh_info:
+        info = rt_bvh_info()
+        self._check(lib.rt_blas_info(self._h, blas, ctypes.byref(info)), "rt_blas_info")
+        return info
+
+    def blas_export(self, blas: int):
+        info = self.blas_info(blas)
+        nodes = np.zeros(info.node_count * 16, np.uint32)
+        tris = np.zeros(info.prim_count * 12, np.uint32)
+        self._check(lib.rt_blas_export(self._h, blas, nodes.ctypes.data_as(_P), nodes.nbytes,
+                                       tris.ctypes.data_as(_P), tris.nbytes), "rt_blas_export")
+        return nodes.reshape(-1, 16), tris.reshape(-1, 12)
+
+    def tlas_build(self, instances: Sequence[tuple], update_only: bool = False):
+        """instances: (blas, xform3x4 (12 floats), instance_id, hit_group) tuples."""
+        arr = (rt_instance * len(instances))()
+        for k, (b, x, iid, hg) in enumerate(instances):
+            arr[k].blas = b
+            arr[k].xform3x4_rowmajor[:] = [float(v) for v in np.asarray(x, np.float32).ravel()]
+            arr[k].instance_id = iid
+            arr[k].hit_group = hg
+        self._check(lib.rt_tlas_build(self._h, arr, len(instances), 1 if update_only else 0), "rt_tlas_build")
+
+    def tlas_info(self) -> rt_bvh_info:
+        info = rt_bvh_info()
+        self._check(lib.rt_tlas_info(self._h, ctypes.byref(info)), "rt_tlas_info")
+        return info
+
+    def tlas_export(self) -> np.ndarray:
+        info = self.tlas_info()
+        nodes = np.zeros(info.node_count * 16, np.uint32)
+        self._check(lib.rt_tlas_export(self._h, nodes.ctypes.data_as(_P), nodes.nbytes), "rt_tlas_export")
+        return nodes.reshape(-1, 16)
+
+    # frame state ------------------------------------------------------------------------------
+    def set_camera(self, cb: np.ndarray):
+        c = _f32(cb, 64)
+        self._check(lib.rt_set_camera(self._h, _fptr(c)), "rt_set_camera")
+
+    def set_shading(self, lights: Iterable, material, mode: int, spp: int = 1):
+        lights = list(lights)
+        arr = (rt_light * len(lights))()
+        for k, (col, pos, inten) in enumerate(lights):
+            arr[k].color[:] = [float(v) for v in col]
+            arr[k].position[:] = [float(v) for v in pos]
+            arr[k].intensity = float(inten)
+        m = rt_material()
+        m.albedo[:] = [float(v) for v in material[0:3]]
+        m.roughness, m.metallic, m.reflectivity = (float(v) for v in material[3:6])
+        self._check(lib.rt_set_shading(self._h, arr, len(lights), ctypes.byref(m), mode, spp), "rt_set_shading")
+
+    def set_schedule(self, schedule: int):
+        self._check(lib.rt_set_schedule(self._h, schedule), "rt_set_schedule")
+
+    def set_stats(self, on: bool):
+        self._check(lib.rt_set_stats(self._h, 1 if on else 0), "rt_set_stats")
+
+    def stats(self) -> dict:
+        out = (ctypes.c_uint64 * 8)()
+        self._check(lib.rt_stats(self._h, out), "rt_stats")
+        return dict(zip(STAT_NAMES, list(out)))
+
+    def stats_reset(self):
+        self._check(lib.rt_stats_reset(self._h), "rt_stats_reset")
+
+    # launches ---------------------------------------------------------------------------------
+    def dispatch(self, width: int, height: int, rgba8, rgba32f=None, rows: Optional[np.ndarray] = None,
+                 stream: Optional[int] = None):
+        if rows is not None:
+            r = np.ascontiguousarray(rows, dtype=np.uint32)
+            rp, nr = r.ctypes.data_as(_P), r.size
+        else:
+            rp, nr = None, height
+        self._check(lib.rt_dispatch_rays(self._h, width, height, rp, nr, _ptr(rgba8), _ptr(rgba32f), stream),
+                    "rt_dispatch_rays")
+
+    def trace_rays(self, rays, n: int, any_hit: bool, hits, uv=None, stream: Optional[int] = None):
+        self._check(lib.rt_trace_rays(self._h, _ptr(rays), n, 1 if any_hit else 0, _ptr(hits), _ptr(uv), stream),
+                    "rt_trace_rays")
+
+    def assemble_strips(self, width: int, height: int, nranks: int, strip_rows_: int, gathered, out,
+                        stream: Optional[int] = None):
+        self._check(lib.rt_assemble_strips(self._h, width, height, nranks, strip_rows_, _ptr(gathered), _ptr(out),
+                                           stream), "rt_assemble_strips")

@@ -1,0 +1,545 @@
+// rt_api.cpp — C-ABI implementation: contexts, BLAS/TLAS lifetimes, frame state and launches.
+// No exception crosses the boundary; every failure returns an rt_status and sets rt_last_error.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_api.h"
+#include "rt_internal.hpp"
+
+namespace {
+
+struct DeviceBlas {
+  rt::BvhNode* nodes = nullptr;
+  rt::TriRec* tris = nullptr;
+  float* vtx = nullptr;
+  uint32_t* idx = nullptr;
+  uint32_t ntri = 0, nnodes = 0, depth = 0, nvtx = 0;
+  float bounds[6] = {0, 0, 0, 0, 0, 0};
+  double build_ms = 0.0;
+  void release() {
+    if (nodes) (void)hipFree(nodes);
+    if (tris) (void)hipFree(tris);
+    if (vtx) (void)hipFree(vtx);
+    if (idx) (void)hipFree(idx);
+    nodes = nullptr;
+    tris = nullptr;
+    vtx = nullptr;
+    idx = nullptr;
+  }
+};
+
+}  // namespace
+
+struct rt_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  std::vector<DeviceBlas> blas;
+  // TLAS
+  rt::BvhNode* tlas_nodes = nullptr;
+  rt::InstanceRec* inst = nullptr;
+  uint32_t* tlas_sorted = nullptr;
+  uint32_t ninst = 0, tlas_nodes_n = 0, tlas_depth = 0;
+  float tlas_bounds[6] = {0, 0, 0, 0, 0, 0};
+  double tlas_ms = 0.0;
+  std::vector<rt_instance> inst_host;
+  // frame state
+  rt::FrameParams fp{};
+  bool have_camera = false, have_shading = false;
+  int schedule = RT_SCHED_MEGAKERNEL;
+  bool stats_on = false;
+  unsigned long long* d_stats = nullptr;
+  uint64_t dispatches = 0, pixels = 0;
+  // cached row list
+  uint32_t* d_rows = nullptr;
+  size_t rows_cap = 0;
+  std::vector<uint32_t> rows_host;
+  rt::WavefrontBuffers wf;
+};
+
+namespace {
+
+rt_status fail(rt_ctx* c, rt_status st, const std::string& msg) {
+  if (c) c->err = msg;
+  return st;
+}
+
+rt_status hip_fail(rt_ctx* c, hipError_t e, const char* what) {
+  std::string m = std::string(what) + ": " + hipGetErrorString(e);
+  return fail(c, e == hipErrorOutOfMemory ? RT_E_OOM : RT_E_HIP, m);
+}
+
+#define HIPCHK(ctx, x, what)                       \
+  do {                                             \
+    hipError_t e_ = (x);                           \
+    if (e_ != hipSuccess) return hip_fail(ctx, e_, what); \
+  } while (0)
+
+// inverse of a 3x3 (row-major) in double, rounded to float; returns false if singular.
+bool inverse3(const double m[9], double inv[9]) {
+  double c00 = m[4] * m[8] - m[5] * m[7];
+  double c01 = m[5] * m[6] - m[3] * m[8];
+  double c02 = m[3] * m[7] - m[4] * m[6];
+  double det = m[0] * c00 + m[1] * c01 + m[2] * c02;
+  if (det == 0.0) return false;
+  double r = 1.0 / det;
+  inv[0] = c00 * r;
+  inv[1] = (m[2] * m[7] - m[1] * m[8]) * r;
+  inv[2] = (m[1] * m[5] - m[2] * m[4]) * r;
+  inv[3] = c01 * r;
+  inv[4] = (m[0] * m[8] - m[2] * m[6]) * r;
+  inv[5] = (m[2] * m[3] - m[0] * m[5]) * r;
+  inv[6] = c02 * r;
+  inv[7] = (m[1] * m[6] - m[0] * m[7]) * r;
+  inv[8] = (m[0] * m[4] - m[1] * m[3]) * r;
+  return true;
+}
+
+// Fills the transform part of an InstanceRec (world-to-object, normal matrix) from a 3x4
+// object-to-world transform. Same double-precision formulas as oracle/rt_oracle.c.
+bool fill_instance_xform(const float* o2w, rt::InstanceRec& r) {
+  double L[9] = {o2w[0], o2w[1], o2w[2], o2w[4], o2w[5], o2w[6], o2w[8], o2w[9], o2w[10]};
+  double Li[9];
+  if (!inverse3(L, Li)) return false;
+  double t[3] = {o2w[3], o2w[7], o2w[11]};
+  for (int i = 0; i < 3; ++i) {
+    r.w2o[i * 4 + 0] = (float)Li[i * 3 + 0];
+    r.w2o[i * 4 + 1] = (float)Li[i * 3 + 1];
+    r.w2o[i * 4 + 2] = (float)Li[i * 3 + 2];
+    r.w2o[i * 4 + 3] = (float)(-(Li[i * 3 + 0] * t[0] + Li[i * 3 + 1] * t[1] + Li[i * 3 + 2] * t[2]));
+  }
+  for (int i = 0; i < 12; ++i) r.o2w[i] = o2w[i];
+  // objectToWorldNormal = transpose(inverse(upper3x3)) (D3D12HelloTriangle.cpp:1190-1200)
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) r.nrm[i * 3 + j] = (float)Li[j * 3 + i];
+  return true;
+}
+
+rt_status upload_blas(rt_ctx* c, DeviceBlas& b, const void* vtx, uint32_t vcount, uint32_t stride,
+                      const uint32_t* idx, uint32_t icount) {
+  if (!vtx || vcount == 0 || stride < 12 || (stride % 4)) return fail(c, RT_E_INVALID, "rt_blas_build: bad vertex buffer");
+  uint32_t ntri;
+  if (idx) {
+    if (icount == 0 || icount % 3) return fail(c, RT_E_INVALID, "rt_blas_build: index count must be a positive multiple of 3");
+    for (uint32_t i = 0; i < icount; ++i)
+      if (idx[i] >= vcount) return fail(c, RT_E_INVALID, "rt_blas_build: index out of range");
+    ntri = icount / 3;
+  } else {
+    if (vcount % 3) return fail(c, RT_E_INVALID, "rt_blas_build: non-indexed vertex count must be a multiple of 3");
+    ntri = vcount / 3;
+  }
+  // repack to {pos, normal} (normal default (0,1,0) when the stride carries none)
+  std::vector<float> v6((size_t)vcount * 6);
+  const unsigned char* src = (const unsigned char*)vtx;
+  for (uint32_t i = 0; i < vcount; ++i) {
+    const float* p = (const float*)(src + (size_t)i * stride);
+    v6[i * 6 + 0] = p[0];
+    v6[i * 6 + 1] = p[1];
+    v6[i * 6 + 2] = p[2];
+    if (stride >= 24) {
+      v6[i * 6 + 3] = p[3];
+      v6[i * 6 + 4] = p[4];
+      v6[i * 6 + 5] = p[5];
+    } else {
+      v6[i * 6 + 3] = 0.0f;
+      v6[i * 6 + 4] = 1.0f;
+      v6[i * 6 + 5] = 0.0f;
+    }
+  }
+  b.release();
+  hipStream_t s = c->stream;
+  HIPCHK(c, hipMalloc(&b.vtx, v6.size() * sizeof(float)), "hipMalloc(vtx)");
+  HIPCHK(c, hipMemcpyAsync(b.vtx, v6.data(), v6.size() * sizeof(float), hipMemcpyHostToDevice, s), "upload vtx");
+  if (idx) {
+    HIPCHK(c, hipMalloc(&b.idx, (size_t)icount * 4), "hipMalloc(idx)");
+    HIPCHK(c, hipMemcpyAsync(b.idx, idx, (size_t)icount * 4, hipMemcpyHostToDevice, s), "upload idx");
+  }
+  const uint32_t nn = ntri > 1 ? ntri - 1 : 1;
+  rt::TriRec* unsorted = nullptr;
+  float* primbox = nullptr;
+  uint32_t* sorted = nullptr;
+  HIPCHK(c, hipMalloc(&b.nodes, (size_t)nn * sizeof(rt::BvhNode)), "hipMalloc(nodes)");
+  HIPCHK(c, hipMalloc(&b.tris, (size_t)ntri * sizeof(rt::TriRec)), "hipMalloc(tris)");
+  HIPCHK(c, hipMalloc(&unsorted, (size_t)ntri * sizeof(rt::TriRec)), "hipMalloc(scratch)");
+  HIPCHK(c, hipMalloc(&primbox, (size_t)ntri * 24), "hipMalloc(scratch)");
+  HIPCHK(c, hipMalloc(&sorted, (size_t)ntri * 4), "hipMalloc(scratch)");
+  hipError_t e = rt::blas_prepare(b.vtx, b.idx, ntri, unsorted, primbox, s);
+  float ms = 0.0f;
+  if (e == hipSuccess) e = rt::lbvh_build(primbox, ntri, b.nodes, sorted, false, &b.depth, b.bounds, &ms, s);
+  if (e == hipSuccess) e = rt::blas_reorder(unsorted, sorted, ntri, b.tris, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipFree(unsorted);
+  (void)hipFree(primbox);
+  (void)hipFree(sorted);
+  if (e != hipSuccess) return hip_fail(c, e, "BLAS build");
+  b.ntri = ntri;
+  b.nnodes = nn;
+  b.nvtx = vcount;
+  b.build_ms = ms;
+  return RT_OK;
+}
+
+hipStream_t pick_stream(rt_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
+
+}  // namespace
+
+extern "C" {
+
+int rt_api_version(void) { return RT_API_VERSION; }
+
+const char* rt_status_string(rt_status st) {
+  switch (st) {
+    case RT_OK: return "RT_OK";
+    case RT_E_INVALID: return "RT_E_INVALID";
+    case RT_E_OOM: return "RT_E_OOM";
+    case RT_E_HIP: return "RT_E_HIP";
+    case RT_E_RCCL: return "RT_E_RCCL";
+    case RT_E_UNSUPPORTED: return "RT_E_UNSUPPORTED";
+    case RT_E_IO: return "RT_E_IO";
+  }
+  return "RT_E_UNKNOWN";
+}
+
+const char* rt_last_error(rt_ctx_t ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+rt_status rt_create(int hip_device, rt_ctx_t* out) {
+  if (!out) return RT_E_INVALID;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return RT_E_UNSUPPORTED;
+  if (hip_device < 0 || hip_device >= n) return RT_E_INVALID;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, hip_device) != hipSuccess) return RT_E_HIP;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return RT_E_UNSUPPORTED;
+  if (hipSetDevice(hip_device) != hipSuccess) return RT_E_HIP;
+  rt_ctx* c = new (std::nothrow) rt_ctx();
+  if (!c) return RT_E_OOM;
+  c->device = hip_device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&c->d_stats, RT_STAT_COUNT * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(c->d_stats, 0, RT_STAT_COUNT * sizeof(unsigned long long)) != hipSuccess) {
+    delete c;
+    return RT_E_HIP;
+  }
+  *out = c;
+  return RT_OK;
+}
+
+rt_status rt_destroy(rt_ctx_t c) {
+  if (!c) return RT_E_INVALID;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  for (auto& b : c->blas) b.release();
+  if (c->tlas_nodes) (void)hipFree(c->tlas_nodes);
+  if (c->inst) (void)hipFree(c->inst);
+  if (c->tlas_sorted) (void)hipFree(c->tlas_sorted);
+  if (c->d_stats) (void)hipFree(c->d_stats);
+  if (c->d_rows) (void)hipFree(c->d_rows);
+  if (c->wf.surf) (void)hipFree(c->wf.surf);
+  if (c->wf.shadow_bits) (void)hipFree(c->wf.shadow_bits);
+  if (c->wf.queue) (void)hipFree(c->wf.queue);
+  if (c->wf.queue_count) (void)hipFree(c->wf.queue_count);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+  return RT_OK;
+}
+
+rt_status rt_blas_build(rt_ctx_t c, const void* vtx, uint32_t vcount, uint32_t stride,
+                        const uint32_t* idx, uint32_t icount, rt_blas_t* out) {
+  if (!c || !out) return fail(c, RT_E_INVALID, "rt_blas_build: null argument");
+  (void)hipSetDevice(c->device);
+  DeviceBlas b;
+  rt_status st = upload_blas(c, b, vtx, vcount, stride, idx, icount);
+  if (st != RT_OK) {
+    b.release();
+    return st;
+  }
+  c->blas.push_back(b);
+  *out = (rt_blas_t)(c->blas.size() - 1);
+  return RT_OK;
+}
+
+rt_status rt_blas_rebuild(rt_ctx_t c, rt_blas_t id, const void* vtx, uint32_t vcount, uint32_t stride,
+                          const uint32_t* idx, uint32_t icount) {
+  if (!c || id >= c->blas.size()) return fail(c, RT_E_INVALID, "rt_blas_rebuild: unknown BLAS");
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  DeviceBlas b;
+  rt_status st = upload_blas(c, b, vtx, vcount, stride, idx, icount);
+  if (st != RT_OK) {
+    b.release();
+    return st;
+  }
+  c->blas[id].release();
+  c->blas[id] = b;
+  return RT_OK;
+}
+
+rt_status rt_blas_info(rt_ctx_t c, rt_blas_t id, rt_bvh_info* out) {
+  if (!c || !out || id >= c->blas.size()) return fail(c, RT_E_INVALID, "rt_blas_info: bad argument");
+  const DeviceBlas& b = c->blas[id];
+  out->prim_count = b.ntri;
+  out->node_count = b.nnodes;
+  out->depth = b.depth;
+  out->reserved = 0;
+  for (int k = 0; k < 3; ++k) {
+    out->bounds_lo[k] = b.bounds[k];
+    out->bounds_hi[k] = b.bounds[3 + k];
+  }
+  out->build_ms = b.build_ms;
+  return RT_OK;
+}
+
+rt_status rt_blas_export(rt_ctx_t c, rt_blas_t id, void* nodes, size_t nodes_bytes, void* tris,
+                         size_t tris_bytes) {
+  if (!c || id >= c->blas.size()) return fail(c, RT_E_INVALID, "rt_blas_export: unknown BLAS");
+  const DeviceBlas& b = c->blas[id];
+  (void)hipSetDevice(c->device);
+  if (nodes) {
+    if (nodes_bytes < (size_t)b.nnodes * 64) return fail(c, RT_E_INVALID, "rt_blas_export: nodes buffer too small");
+    HIPCHK(c, hipMemcpy(nodes, b.nodes, (size_t)b.nnodes * 64, hipMemcpyDeviceToHost), "export nodes");
+  }
+  if (tris) {
+    if (tris_bytes < (size_t)b.ntri * 48) return fail(c, RT_E_INVALID, "rt_blas_export: tris buffer too small");
+    HIPCHK(c, hipMemcpy(tris, b.tris, (size_t)b.ntri * 48, hipMemcpyDeviceToHost), "export tris");
+  }
+  return RT_OK;
+}
+
+rt_status rt_tlas_build(rt_ctx_t c, const rt_instance* in, uint32_t n, int update_only) {
+  if (!c || !in || n == 0) return fail(c, RT_E_INVALID, "rt_tlas_build: need at least one instance");
+  (void)hipSetDevice(c->device);
+  if (update_only) {
+    if (!c->inst || n != c->ninst) return fail(c, RT_E_INVALID, "rt_tlas_build: update needs the same instance count");
+    for (uint32_t i = 0; i < n; ++i)
+      if (in[i].blas != c->inst_host[i].blas) return fail(c, RT_E_INVALID, "rt_tlas_build: update cannot change BLAS");
+  }
+  std::vector<rt::InstanceRec> recs(n);
+  std::vector<float> bb((size_t)n * 6);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (in[i].blas >= c->blas.size()) return fail(c, RT_E_INVALID, "rt_tlas_build: unknown BLAS id");
+    if (in[i].hit_group != RT_HITGROUP_MODEL && in[i].hit_group != RT_HITGROUP_PLANE)
+      return fail(c, RT_E_INVALID, "rt_tlas_build: hit_group must be 0 (model) or 2 (plane)");
+    rt::InstanceRec& r = recs[i];
+    std::memset(&r, 0, sizeof(r));
+    if (!fill_instance_xform(in[i].xform3x4_rowmajor, r)) return fail(c, RT_E_INVALID, "rt_tlas_build: singular transform");
+    const DeviceBlas& b = c->blas[in[i].blas];
+    r.instance_id = in[i].instance_id;
+    r.hit_group = in[i].hit_group;
+    r.blas = in[i].blas;
+    r.nodes = b.nodes;
+    r.tris = b.tris;
+    r.vtx = b.vtx;
+    r.idx = b.idx;
+    for (int k = 0; k < 6; ++k) bb[i * 6 + k] = b.bounds[k];
+  }
+  hipStream_t s = c->stream;
+  (void)hipStreamSynchronize(s);
+  if (!update_only || !c->inst) {
+    if (c->tlas_nodes) (void)hipFree(c->tlas_nodes);
+    if (c->inst) (void)hipFree(c->inst);
+    if (c->tlas_sorted) (void)hipFree(c->tlas_sorted);
+    c->tlas_nodes = nullptr;
+    c->inst = nullptr;
+    c->tlas_sorted = nullptr;
+    const uint32_t nn = n > 1 ? n - 1 : 1;
+    HIPCHK(c, hipMalloc(&c->tlas_nodes, (size_t)nn * sizeof(rt::BvhNode)), "hipMalloc(tlas)");
+    HIPCHK(c, hipMalloc(&c->inst, (size_t)n * sizeof(rt::InstanceRec)), "hipMalloc(instances)");
+    HIPCHK(c, hipMalloc(&c->tlas_sorted, (size_t)n * 4), "hipMalloc(tlas order)");
+    c->tlas_nodes_n = nn;
+  }
+  float* d_bb = nullptr;
+  float* d_box = nullptr;
+  HIPCHK(c, hipMalloc(&d_bb, bb.size() * 4), "hipMalloc(scratch)");
+  HIPCHK(c, hipMalloc(&d_box, bb.size() * 4), "hipMalloc(scratch)");
+  hipError_t e = hipMemcpyAsync(c->inst, recs.data(), recs.size() * sizeof(rt::InstanceRec), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_bb, bb.data(), bb.size() * 4, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = rt::tlas_prepare(c->inst, d_bb, n, d_box, s);
+  float ms = 0.0f;
+  // update_only rebuilds the hierarchy over the new boxes: an LBVH rebuild costs the same
+  // launches as a refit at these sizes and keeps the tree identical to a fresh build.
+  if (e == hipSuccess) e = rt::lbvh_build(d_box, n, c->tlas_nodes, c->tlas_sorted, true, &c->tlas_depth, c->tlas_bounds, &ms, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipFree(d_bb);
+  (void)hipFree(d_box);
+  if (e != hipSuccess) return hip_fail(c, e, "TLAS build");
+  c->ninst = n;
+  c->tlas_ms = ms;
+  c->inst_host.assign(in, in + n);
+  return RT_OK;
+}
+
+rt_status rt_tlas_info(rt_ctx_t c, rt_bvh_info* out) {
+  if (!c || !out || !c->inst) return fail(c, RT_E_INVALID, "rt_tlas_info: no TLAS");
+  out->prim_count = c->ninst;
+  out->node_count = c->tlas_nodes_n;
+  out->depth = c->tlas_depth;
+  out->reserved = 0;
+  for (int k = 0; k < 3; ++k) {
+    out->bounds_lo[k] = c->tlas_bounds[k];
+    out->bounds_hi[k] = c->tlas_bounds[3 + k];
+  }
+  out->build_ms = c->tlas_ms;
+  return RT_OK;
+}
+
+rt_status rt_tlas_export(rt_ctx_t c, void* nodes, size_t nodes_bytes) {
+  if (!c || !nodes || !c->inst) return fail(c, RT_E_INVALID, "rt_tlas_export: no TLAS");
+  if (nodes_bytes < (size_t)c->tlas_nodes_n * 64) return fail(c, RT_E_INVALID, "rt_tlas_export: buffer too small");
+  (void)hipSetDevice(c->device);
+  HIPCHK(c, hipMemcpy(nodes, c->tlas_nodes, (size_t)c->tlas_nodes_n * 64, hipMemcpyDeviceToHost), "export tlas");
+  return RT_OK;
+}
+
+rt_status rt_set_camera(rt_ctx_t c, const float cb[64]) {
+  if (!c || !cb) return fail(c, RT_E_INVALID, "rt_set_camera: null argument");
+  std::memcpy(c->fp.cb, cb, 64 * sizeof(float));
+  c->have_camera = true;
+  return RT_OK;
+}
+
+rt_status rt_set_shading(rt_ctx_t c, const rt_light* lights, uint32_t nlights, const rt_material* m,
+                         int shade_mode, int spp) {
+  if (!c || !lights || !m) return fail(c, RT_E_INVALID, "rt_set_shading: null argument");
+  if (nlights < 1 || nlights > (uint32_t)rt::kMaxLights) return fail(c, RT_E_INVALID, "rt_set_shading: nlights must be in [1,16]");
+  if (shade_mode < RT_SHADE_REF || shade_mode > RT_SHADE_PRIMARY) return fail(c, RT_E_INVALID, "rt_set_shading: unknown shade mode");
+  int k = 0;
+  for (int s = 1; s <= 4; ++s)
+    if (s * s == spp) k = s;
+  if (!k) return fail(c, RT_E_INVALID, "rt_set_shading: spp must be 1, 4, 9 or 16");
+  for (uint32_t l = 0; l < nlights; ++l) std::memcpy(&c->fp.lights[l], &lights[l], sizeof(rt::LightRec));
+  std::memcpy(&c->fp.material, m, sizeof(rt::MaterialRec));
+  c->fp.nlights = nlights;
+  c->fp.shade_mode = (uint32_t)shade_mode;
+  c->fp.spp_side = (uint32_t)k;
+  c->have_shading = true;
+  return RT_OK;
+}
+
+rt_status rt_set_schedule(rt_ctx_t c, int schedule) {
+  if (!c) return RT_E_INVALID;
+  if (schedule != RT_SCHED_MEGAKERNEL && schedule != RT_SCHED_WAVEFRONT) return fail(c, RT_E_INVALID, "rt_set_schedule: unknown schedule");
+  c->schedule = schedule;
+  return RT_OK;
+}
+
+rt_status rt_set_stats(rt_ctx_t c, int enable) {
+  if (!c) return RT_E_INVALID;
+  c->stats_on = enable != 0;
+  return RT_OK;
+}
+
+static rt::SceneView scene_view(rt_ctx* c) {
+  rt::SceneView sv;
+  sv.tlas = c->tlas_nodes;
+  sv.inst = c->inst;
+  uint32_t maxb = 0;
+  for (const auto& b : c->blas) maxb = b.depth > maxb ? b.depth : maxb;
+  sv.stack_cap = (int)(c->tlas_depth + maxb + 2);
+  return sv;
+}
+
+rt_status rt_dispatch_rays(rt_ctx_t c, uint32_t W, uint32_t H, const uint32_t* rows, uint32_t nrows,
+                           void* rgba8, float* rgba32f, void* stream) {
+  if (!c) return RT_E_INVALID;
+  if (!c->inst) return fail(c, RT_E_INVALID, "rt_dispatch_rays: no TLAS built");
+  if (!c->have_camera || !c->have_shading) return fail(c, RT_E_INVALID, "rt_dispatch_rays: camera/shading not set");
+  if (W == 0 || H == 0 || !rgba8) return fail(c, RT_E_INVALID, "rt_dispatch_rays: bad size or output");
+  if (!rows) nrows = H;
+  if (nrows == 0 || nrows > H) return fail(c, RT_E_INVALID, "rt_dispatch_rays: bad row count");
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  const uint32_t* d_rows = nullptr;
+  if (rows) {
+    for (uint32_t r = 0; r < nrows; ++r)
+      if (rows[r] >= H) return fail(c, RT_E_INVALID, "rt_dispatch_rays: row index out of range");
+    bool same = c->rows_host.size() == nrows && std::memcmp(c->rows_host.data(), rows, (size_t)nrows * 4) == 0;
+    if (!same) {
+      if (c->rows_cap < nrows) {
+        (void)hipStreamSynchronize(s);
+        if (c->d_rows) (void)hipFree(c->d_rows);
+        c->d_rows = nullptr;
+        HIPCHK(c, hipMalloc(&c->d_rows, (size_t)nrows * 4), "hipMalloc(rows)");
+        c->rows_cap = nrows;
+      }
+      HIPCHK(c, hipMemcpyAsync(c->d_rows, rows, (size_t)nrows * 4, hipMemcpyHostToDevice, s), "upload rows");
+      HIPCHK(c, hipStreamSynchronize(s), "upload rows");
+      c->rows_host.assign(rows, rows + nrows);
+    }
+    d_rows = c->d_rows;
+  }
+  c->fp.width = W;
+  c->fp.height = H;
+  c->fp.nrows = nrows;
+  rt::SceneView sv = scene_view(c);
+  hipError_t e = rt::launch_trace_frame(sv, c->fp, d_rows, rgba8, rgba32f, c->d_stats, c->stats_on,
+                                        c->schedule, &c->wf, s);
+  if (e != hipSuccess) return hip_fail(c, e, "trace launch");
+  if (c->stats_on) {
+    c->dispatches += 1;
+    c->pixels += (uint64_t)W * nrows;
+  }
+  return RT_OK;
+}
+
+rt_status rt_trace_rays(rt_ctx_t c, const float* rays, uint32_t n, int any_hit, uint32_t* hits, float* uv,
+                        void* stream) {
+  if (!c || (!rays && n) || (!hits && n)) return fail(c, RT_E_INVALID, "rt_trace_rays: null argument");
+  if (!c->inst) return fail(c, RT_E_INVALID, "rt_trace_rays: no TLAS built");
+  (void)hipSetDevice(c->device);
+  rt::SceneView sv = scene_view(c);
+  hipError_t e = rt::launch_trace_rays(sv, rays, n, any_hit, hits, uv, c->d_stats, c->stats_on, pick_stream(c, stream));
+  if (e != hipSuccess) return hip_fail(c, e, "trace_rays launch");
+  return RT_OK;
+}
+
+rt_status rt_assemble_strips(rt_ctx_t c, uint32_t W, uint32_t H, uint32_t nranks, uint32_t strip_rows,
+                             const void* gathered, void* out, void* stream) {
+  if (!c || !gathered || !out || W == 0 || H == 0 || nranks == 0 || strip_rows == 0)
+    return fail(c, RT_E_INVALID, "rt_assemble_strips: bad argument");
+  (void)hipSetDevice(c->device);
+  hipError_t e = rt::launch_assemble_strips(W, H, nranks, strip_rows, gathered, out, pick_stream(c, stream));
+  if (e != hipSuccess) return hip_fail(c, e, "assemble launch");
+  return RT_OK;
+}
+
+uint32_t rt_strip_rows(uint32_t H, uint32_t nranks, uint32_t rank, uint32_t strip_rows, uint32_t* rows_out,
+                       uint32_t cap) {
+  if (nranks == 0 || rank >= nranks || strip_rows == 0) return 0;
+  uint32_t n = 0;
+  const uint32_t nstrips = (H + strip_rows - 1) / strip_rows;
+  for (uint32_t s = rank; s < nstrips; s += nranks)
+    for (uint32_t r = s * strip_rows; r < H && r < (s + 1) * strip_rows; ++r) {
+      if (rows_out && n < cap) rows_out[n] = r;
+      ++n;
+    }
+  return n;
+}
+
+rt_status rt_stats(rt_ctx_t c, uint64_t out[8]) {
+  if (!c || !out) return RT_E_INVALID;
+  (void)hipSetDevice(c->device);
+  HIPCHK(c, hipDeviceSynchronize(), "stats sync");
+  unsigned long long h[RT_STAT_COUNT];
+  HIPCHK(c, hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost), "stats copy");
+  for (int k = 0; k < 6; ++k) out[k] = h[k];
+  out[RT_STAT_PIXELS] = c->pixels;
+  out[RT_STAT_DISPATCHES] = c->dispatches;
+  return RT_OK;
+}
+
+rt_status rt_stats_reset(rt_ctx_t c) {
+  if (!c) return RT_E_INVALID;
+  (void)hipSetDevice(c->device);
+  HIPCHK(c, hipMemset(c->d_stats, 0, RT_STAT_COUNT * sizeof(unsigned long long)), "stats reset");
+  c->pixels = 0;
+  c->dispatches = 0;
+  return RT_OK;
+}
+
+}  // extern "C"

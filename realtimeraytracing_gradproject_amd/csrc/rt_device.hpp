@@ -1,0 +1,231 @@
+// rt_device.hpp — HBM data layout and the per-ray arithmetic of the MI355X trace path.
+//
+// Everything here is compiled with -ffp-contract=off: the image must be bit-identical to the CPU
+// oracle (oracle/rt_oracle.c), which restates the same formulas independently. The only fused
+// multiply-adds are the explicit __builtin_fmaf in the slab test, mirrored by the oracle.
+//
+// Reference semantics (relative to the reference tree):
+//   RayGen            shaders/RayGen.hlsl:28-43
+//   ray wrappers      shaders/Common.hlsl:44-82
+//   ClosestHit & co.  shaders/Hit.hlsl:48-241
+//   Miss              shaders/Miss.hlsl:3-10
+//   Shadow programs   shaders/ShadowRay.hlsl:10-20
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define RT_HD __host__ __device__ __forceinline__
+
+namespace rt {
+
+// ------------------------------------------------------------------------------------------
+// HBM layout
+// ------------------------------------------------------------------------------------------
+
+// Child-pair BVH node, 64 B (one half of a 128-B L2 line; 64-B aligned). The node stores the
+// boxes of BOTH children so one node fetch decides which children to visit.
+// Child refs: >= 0 internal node index, < 0 leaf: ~slot (BLAS: triangle slot in leaf order,
+// TLAS: instance index).
+struct alignas(64) BvhNode {
+  float lo0[3], hi0[3];
+  float lo1[3], hi1[3];
+  int32_t c0, c1;
+  uint32_t pad0, pad1;
+};
+static_assert(sizeof(BvhNode) == 64, "BvhNode must be 64 B");
+
+// Moller-Trumbore-ready triangle in leaf order, 48 B: v0, e1 = v1 - v0, e2 = v2 - v0, and the
+// original PrimitiveIndex().
+struct alignas(16) TriRec {
+  float v0[3];
+  uint32_t prim;
+  float e1[3];
+  uint32_t pad1;
+  float e2[3];
+  uint32_t pad2;
+};
+static_assert(sizeof(TriRec) == 48, "TriRec must be 48 B");
+
+// Per-instance record read by the trace kernel (instance desc + InstanceProperties,
+// TopLevelASGenerator.cpp:180-198, Hit.hlsl:19-23).
+struct alignas(16) InstanceRec {
+  float w2o[12];     // world-to-object 3x4 row-major (inverse of the instance transform)
+  float o2w[12];     // object-to-world 3x4 row-major (as given)
+  float nrm[9];      // objectToWorldNormal = transpose(inverse(upper3x3)), row-major 3x3
+  uint32_t instance_id;
+  uint32_t hit_group;
+  uint32_t blas;
+  const BvhNode* nodes;
+  const TriRec* tris;
+  const float* vtx;       // 6 floats per vertex: pos.xyz, normal.xyz (stride 24 B)
+  const uint32_t* idx;    // triangle list, or nullptr for non-indexed geometry
+};
+
+constexpr int kMaxLights = 16;
+constexpr int32_t kStackSentinel = INT32_MIN;  // TLAS -> BLAS transition marker
+
+struct LightRec {
+  float color[3];
+  float position[3];
+  float intensity;
+};
+
+struct MaterialRec {
+  float albedo[3];
+  float roughness, metallic, reflectivity;
+};
+
+// Everything a frame needs besides the scene buffers; passed by value as a kernel argument.
+struct FrameParams {
+  float cb[64];  // view, proj, viewInv, projInv in XMMATRIX memory order
+  LightRec lights[kMaxLights];
+  MaterialRec material;
+  uint32_t nlights;
+  uint32_t shade_mode;
+  uint32_t spp_side;  // k for k x k stratified samples
+  uint32_t width, height;
+  uint32_t nrows;
+};
+
+struct SceneView {
+  const BvhNode* tlas;
+  const InstanceRec* inst;
+  int stack_cap;
+};
+
+// ------------------------------------------------------------------------------------------
+// Scalar float helpers (no contraction; identical to oracle/rt_oracle.c)
+// ------------------------------------------------------------------------------------------
+
+struct V3 {
+  float x, y, z;
+};
+
+RT_HD V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+RT_HD V3 add(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+RT_HD V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+RT_HD V3 mul(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+RT_HD V3 muls(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
+RT_HD V3 neg(V3 a) { return v3(-a.x, -a.y, -a.z); }
+RT_HD float dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+RT_HD V3 cross(V3 a, V3 b) {
+  return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+// HLSL normalize pinned as v * (1 / sqrt(dot(v, v))) (glm's compute_normalize form).
+RT_HD V3 normalize(V3 a) {
+  float inv = 1.0f / sqrtf(dot(a, a));
+  return muls(a, inv);
+}
+RT_HD float length(V3 a) { return sqrtf(dot(a, a)); }
+RT_HD float maxf(float a, float b) { return a > b ? a : b; }
+RT_HD float minf(float a, float b) { return a < b ? a : b; }
+RT_HD float clamp01(float x) { return minf(maxf(x, 0.0f), 1.0f); }
+
+// 3x4 row-major affine transform of a point / a direction, summed left to right.
+RT_HD V3 xform_point(const float* m, V3 p) {
+  return v3(((m[0] * p.x + m[1] * p.y) + m[2] * p.z) + m[3],
+            ((m[4] * p.x + m[5] * p.y) + m[6] * p.z) + m[7],
+            ((m[8] * p.x + m[9] * p.y) + m[10] * p.z) + m[11]);
+}
+RT_HD V3 xform_dir(const float* m, V3 d) {
+  return v3((m[0] * d.x + m[1] * d.y) + m[2] * d.z, (m[4] * d.x + m[5] * d.y) + m[6] * d.z,
+            (m[8] * d.x + m[9] * d.y) + m[10] * d.z);
+}
+RT_HD V3 mat3_mul(const float* m, V3 d) {
+  return v3((m[0] * d.x + m[1] * d.y) + m[2] * d.z, (m[3] * d.x + m[4] * d.y) + m[5] * d.z,
+            (m[6] * d.x + m[7] * d.y) + m[8] * d.z);
+}
+
+// HLSL mul(M, v) with M read column-major from XMMATRIX memory: r_i = sum_j mem[4j+i] v_j.
+RT_HD void hlsl_mul4(const float* mem, const float v[4], float r[4]) {
+  for (int i = 0; i < 4; ++i)
+    r[i] = ((mem[i] * v[0] + mem[4 + i] * v[1]) + mem[8 + i] * v[2]) + mem[12 + i] * v[3];
+}
+
+// 1/d with zero components replaced by +-1e20 so slab products never form inf*0.
+RT_HD float safe_inv(float d) { return fabsf(d) > 1e-20f ? 1.0f / d : (d < 0.0f ? -1e20f : 1e20f); }
+
+// Deterministic log2 / exp2 / pow for x in [0, inf): pure +,-,*,/ and bit operations so the GPU
+// and the oracle agree to the bit. |rel err| ~ 2e-7.
+RT_HD float det_log2(float x) {
+  uint32_t b = __builtin_bit_cast(uint32_t, x);
+  int e = (int)((b >> 23) & 0xffu) - 127;
+  float m = __builtin_bit_cast(float, (b & 0x7fffffu) | 0x3f800000u);
+  if (m > 1.41421356f) {
+    m = m * 0.5f;
+    e = e + 1;
+  }
+  float f = m - 1.0f;
+  float s = f / (2.0f + f);
+  float s2 = s * s;
+  float p = 1.0f / 11.0f;
+  p = p * s2 + 1.0f / 9.0f;
+  p = p * s2 + 1.0f / 7.0f;
+  p = p * s2 + 1.0f / 5.0f;
+  p = p * s2 + 1.0f / 3.0f;
+  p = p * s2 + 1.0f;
+  float ln = (2.0f * s) * p;
+  return (float)e + ln * 1.44269504f;
+}
+RT_HD float det_exp2(float y) {
+  if (y < -126.0f) return 0.0f;
+  if (y > 127.0f) y = 127.0f;
+  float fi = floorf(y + 0.5f);
+  float f = y - fi;  // [-0.5, 0.5]
+  float a = f * 0.693147181f;
+  float p = 1.0f / 40320.0f;
+  p = p * a + 1.0f / 5040.0f;
+  p = p * a + 1.0f / 720.0f;
+  p = p * a + 1.0f / 120.0f;
+  p = p * a + 1.0f / 24.0f;
+  p = p * a + 1.0f / 6.0f;
+  p = p * a + 0.5f;
+  p = p * a + 1.0f;
+  p = p * a + 1.0f;
+  int i = (int)fi;
+  float scale = __builtin_bit_cast(float, (uint32_t)(i + 127) << 23);
+  return p * scale;
+}
+RT_HD float det_pow(float x, float y) {
+  if (!(x > 1e-30f)) return 0.0f;
+  return det_exp2(y * det_log2(x));
+}
+
+// float -> UNORM8 (D3D conversion: saturate, x255, round to nearest; NaN -> 0).
+RT_HD uint32_t unorm8(float c) {
+  if (!(c > 0.0f)) return 0u;
+  if (c >= 1.0f) return 255u;
+  return (uint32_t)(c * 255.0f + 0.5f);
+}
+
+// Slab test of one child box against the current ray segment [tmin, tbest]. Conservative
+// (tfar widened by 1 + 4e-7) so BVH culling never rejects a triangle Moller-Trumbore accepts.
+RT_HD bool slab(const float* lo, const float* hi, V3 invd, V3 noinv, float tmin, float tbest,
+                float& tnear) {
+  float tlx = __builtin_fmaf(lo[0], invd.x, noinv.x), thx = __builtin_fmaf(hi[0], invd.x, noinv.x);
+  float tly = __builtin_fmaf(lo[1], invd.y, noinv.y), thy = __builtin_fmaf(hi[1], invd.y, noinv.y);
+  float tlz = __builtin_fmaf(lo[2], invd.z, noinv.z), thz = __builtin_fmaf(hi[2], invd.z, noinv.z);
+  float tn = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), tmin));
+  float tf = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tbest));
+  tnear = tn;
+  return tn <= tf * 1.0000004f;
+}
+
+// Moller-Trumbore. Accepts u >= 0, v >= 0, u + v <= 1, det != 0; returns t (not yet range checked).
+RT_HD bool moller_trumbore(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float& t, float& u, float& v) {
+  V3 p = cross(d, e2);
+  float det = dot(e1, p);
+  if (det == 0.0f) return false;
+  float inv = 1.0f / det;
+  V3 s = sub(o, v0);
+  u = dot(s, p) * inv;
+  if (!(u >= 0.0f && u <= 1.0f)) return false;
+  V3 q = cross(s, e1);
+  v = dot(d, q) * inv;
+  if (!(v >= 0.0f && u + v <= 1.0f)) return false;
+  t = dot(e2, q) * inv;
+  return true;
+}
+
+}  // namespace rt

@@ -1,0 +1,53 @@
+// rt_internal.hpp — launchers shared between the C-ABI (rt_api.cpp) and the HIP translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "rt_device.hpp"
+
+namespace rt {
+
+// --- LBVH build (rt_lbvh.hip) ---------------------------------------------------------------
+
+// Builds a child-pair LBVH over n primitive boxes (d_primbox: n x {lo.xyz, hi.xyz}).
+// d_nodes receives max(n-1, 1) nodes, d_sorted the leaf-order -> primitive permutation.
+// Leaf refs are ~leaf_slot (BLAS, primitives reordered afterwards) or ~primitive (TLAS).
+// Returns the depth (root-to-leaf edges) and the root box in host memory. Synchronous.
+hipError_t lbvh_build(const float* d_primbox, uint32_t n, BvhNode* d_nodes, uint32_t* d_sorted,
+                      bool leaf_ref_is_prim, uint32_t* depth, float bounds[6], float* build_ms,
+                      hipStream_t stream);
+
+// Triangle setup: prim boxes + unsorted MT records from a {pos, normal} vertex array.
+hipError_t blas_prepare(const float* d_vtx, const uint32_t* d_idx, uint32_t ntri, TriRec* d_tris,
+                        float* d_primbox, hipStream_t stream);
+// Gathers triangles into leaf order.
+hipError_t blas_reorder(const TriRec* d_in, const uint32_t* d_sorted, uint32_t n, TriRec* d_out,
+                        hipStream_t stream);
+// World boxes of instances: the 8 corners of each BLAS root box through the instance transform.
+hipError_t tlas_prepare(const InstanceRec* d_inst, const float* d_blas_bounds, uint32_t n,
+                        float* d_primbox, hipStream_t stream);
+
+// --- Trace (rt_trace.hip) -------------------------------------------------------------------
+
+struct WavefrontBuffers {
+  // Per output pixel: hit record for the resolve pass (P.xyz, n.xyz, kind) and shadow bits.
+  float* surf = nullptr;        // nrows*W*8 floats
+  uint32_t* shadow_bits = nullptr;  // nrows*W
+  uint32_t* queue = nullptr;    // shadow ray queue: (pixel, light) packed, capacity nrows*W*nlights
+  uint32_t* queue_count = nullptr;
+  size_t pixel_cap = 0;
+  size_t queue_cap = 0;
+};
+
+hipError_t launch_trace_frame(const SceneView& scene, const FrameParams& fp, const uint32_t* d_rows,
+                              void* rgba8, float* rgba32f, unsigned long long* d_stats, bool stats,
+                              int schedule, WavefrontBuffers* wf, hipStream_t stream);
+
+hipError_t launch_trace_rays(const SceneView& scene, const float* rays, uint32_t n, int any_hit,
+                             uint32_t* hits, float* uv, unsigned long long* d_stats, bool stats,
+                             hipStream_t stream);
+
+hipError_t launch_assemble_strips(uint32_t W, uint32_t H, uint32_t nranks, uint32_t strip_rows,
+                                  const void* gathered, void* out, hipStream_t stream);
+
+}  // namespace rt

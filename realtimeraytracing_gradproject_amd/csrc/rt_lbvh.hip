@@ -1,0 +1,467 @@
+// rt_lbvh.hip — on-device LBVH build for BLAS and TLAS on gfx950.
+//
+// Replaces the driver acceleration-structure builds behind
+//   BottomLevelASGenerator::Generate  nv_helpers_dx12/BottomLevelASGenerator.cpp:177-245 (build :234)
+//   TopLevelASGenerator::Generate     nv_helpers_dx12/TopLevelASGenerator.cpp:148-249 (build :239)
+//
+// Pipeline (all deterministic, so oracle/rt_oracle.c rebuilds the bit-identical tree):
+//   1. centroid bounds      one 1024-thread workgroup, LDS min/max reduction (exact)
+//   2. Morton codes         30-bit (10 bits/axis) of box centroids
+//   3. LSD radix sort       4 passes x 8 bits; per pass: block digit histogram (LDS atomics),
+//                           exclusive scan, stable scatter with wave64 ballot match + popcount
+//                           ranks (keys tie-break on primitive index: stable)
+//   4. Karras hierarchy     Karras 2012 over key64 = morton << 32 | leaf position
+//   5. bottom-up refit      one thread per leaf, agent-scope release/acquire arrival counters
+//   6. pack                 64-B child-pair nodes (both child boxes per node)
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "rt_internal.hpp"
+
+namespace rt {
+namespace {
+
+constexpr int kRsThreads = 256;
+constexpr int kRsRounds = 4;
+constexpr int kRsTile = kRsThreads * kRsRounds;  // keys per workgroup per pass
+
+__device__ __forceinline__ uint32_t expand_bits10(uint32_t x) {
+  x = (x * 0x00010001u) & 0xFF0000FFu;
+  x = (x * 0x00000101u) & 0x0F00F00Fu;
+  x = (x * 0x00000011u) & 0xC30C30C3u;
+  x = (x * 0x00000005u) & 0x49249249u;
+  return x;
+}
+
+__device__ __forceinline__ uint32_t quantize10(float c, float lo, float inv_ext) {
+  float q = (c - lo) * inv_ext;
+  float s = q * 1024.0f;
+  s = fminf(fmaxf(s, 0.0f), 1023.0f);
+  return (uint32_t)s;
+}
+
+// 1. centroid bounds + union of prim boxes. out[0..5] centroid lo/hi, out[6..11] box lo/hi.
+__global__ __launch_bounds__(1024) void k_bounds(const float* __restrict__ box, uint32_t n,
+                                                 float* __restrict__ out) {
+  __shared__ float red[12][1024 / 64];
+  float v[12];
+  for (int k = 0; k < 3; ++k) {
+    v[k] = INFINITY;
+    v[3 + k] = -INFINITY;
+    v[6 + k] = INFINITY;
+    v[9 + k] = -INFINITY;
+  }
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const float* b = box + (size_t)i * 6;
+    for (int k = 0; k < 3; ++k) {
+      float c = (b[k] + b[3 + k]) * 0.5f;
+      v[k] = fminf(v[k], c);
+      v[3 + k] = fmaxf(v[3 + k], c);
+      v[6 + k] = fminf(v[6 + k], b[k]);
+      v[9 + k] = fmaxf(v[9 + k], b[3 + k]);
+    }
+  }
+  // wave64 reduction, then across the 16 waves
+  for (int off = 32; off >= 1; off >>= 1) {
+    for (int k = 0; k < 12; ++k) {
+      float o = __shfl_xor(v[k], off, 64);
+      bool is_min = (k % 6) < 3;
+      v[k] = is_min ? fminf(v[k], o) : fmaxf(v[k], o);
+    }
+  }
+  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0)
+    for (int k = 0; k < 12; ++k) red[k][w] = v[k];
+  __syncthreads();
+  if (threadIdx.x < 12) {
+    int k = threadIdx.x;
+    bool is_min = (k % 6) < 3;
+    float r = red[k][0];
+    for (int j = 1; j < (int)(blockDim.x / 64); ++j) r = is_min ? fminf(r, red[k][j]) : fmaxf(r, red[k][j]);
+    out[k] = r;
+  }
+}
+
+// 2. Morton codes of box centroids; values = primitive index.
+__global__ void k_morton(const float* __restrict__ box, uint32_t n, const float* __restrict__ cb,
+                         uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* b = box + (size_t)i * 6;
+  uint32_t q[3];
+  for (int k = 0; k < 3; ++k) {
+    float ext = cb[3 + k] - cb[k];
+    float inv = ext > 0.0f ? 1.0f / ext : 0.0f;
+    float c = (b[k] + b[3 + k]) * 0.5f;
+    q[k] = quantize10(c, cb[k], inv);
+  }
+  keys[i] = (expand_bits10(q[0]) << 2) | (expand_bits10(q[1]) << 1) | expand_bits10(q[2]);
+  vals[i] = i;
+}
+
+// 3a. per-workgroup digit histogram, stored digit-major: hist[d * nblocks + b].
+__global__ __launch_bounds__(kRsThreads) void k_rs_hist(const uint32_t* __restrict__ keys, uint32_t n,
+                                                         int shift, uint32_t* __restrict__ hist,
+                                                         uint32_t nblocks) {
+  __shared__ uint32_t h[256];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t base = blockIdx.x * kRsTile;
+  for (int r = 0; r < kRsRounds; ++r) {
+    uint32_t i = base + r * kRsThreads + threadIdx.x;
+    if (i < n) atomicAdd(&h[(keys[i] >> shift) & 255u], 1u);
+  }
+  __syncthreads();
+  hist[threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+}
+
+// 3b. exclusive scan of len values in place, one 1024-thread workgroup.
+__global__ __launch_bounds__(1024) void k_rs_scan(uint32_t* __restrict__ data, uint32_t len) {
+  __shared__ uint32_t sums[1024];
+  uint32_t per = (len + 1023u) / 1024u;
+  uint32_t b = threadIdx.x * per, e = min(b + per, len);
+  uint32_t s = 0;
+  for (uint32_t i = b; i < e; ++i) s += data[i];
+  sums[threadIdx.x] = s;
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024; off <<= 1) {
+    uint32_t add = threadIdx.x >= off ? sums[threadIdx.x - off] : 0u;
+    __syncthreads();
+    sums[threadIdx.x] += add;
+    __syncthreads();
+  }
+  uint32_t run = sums[threadIdx.x] - s;  // exclusive
+  for (uint32_t i = b; i < e; ++i) {
+    uint32_t v = data[i];
+    data[i] = run;
+    run += v;
+  }
+}
+
+// 3c. stable scatter. Each round a wave ranks its 64 keys by digit with 8 ballots (peer mask of
+// equal digits) + popcount of lower peers; waves of a workgroup are ordered through LDS counts.
+__global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const uint32_t* __restrict__ kin,
+                                                            const uint32_t* __restrict__ vin,
+                                                            uint32_t* __restrict__ kout,
+                                                            uint32_t* __restrict__ vout, uint32_t n,
+                                                            int shift, const uint32_t* __restrict__ scan,
+                                                            uint32_t nblocks) {
+  __shared__ uint32_t offs[256];
+  __shared__ uint32_t wcnt[kRsThreads / 64][256];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  offs[tid] = scan[tid * nblocks + blockIdx.x];
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64u - lane));
+  const uint32_t base = blockIdx.x * kRsTile;
+  for (int r = 0; r < kRsRounds; ++r) {
+    for (int k = 0; k < kRsThreads / 64; ++k) wcnt[k][tid] = 0;
+    __syncthreads();
+    uint32_t i = base + r * kRsThreads + tid;
+    bool valid = i < n;
+    uint32_t key = valid ? kin[i] : 0u;
+    uint32_t val = valid ? vin[i] : 0u;
+    uint32_t digit = (key >> shift) & 255u;
+    uint64_t peers = __ballot(valid);
+    for (int b = 0; b < 8; ++b) {
+      bool bit = (digit >> b) & 1u;
+      uint64_t m = __ballot(valid && bit);
+      peers &= bit ? m : ~m;
+    }
+    uint32_t rank = (uint32_t)__popcll(peers & lt);
+    if (valid && rank == 0) wcnt[w][digit] = (uint32_t)__popcll(peers);
+    __syncthreads();
+    if (valid) {
+      uint32_t pre = 0;
+      for (uint32_t k = 0; k < w; ++k) pre += wcnt[k][digit];
+      uint32_t pos = offs[digit] + pre + rank;
+      kout[pos] = key;
+      vout[pos] = val;
+    }
+    __syncthreads();
+    uint32_t tot = 0;
+    for (int k = 0; k < kRsThreads / 64; ++k) tot += wcnt[k][tid];
+    offs[tid] += tot;
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ int delta(const uint32_t* __restrict__ keys, int n, int i, int j) {
+  if (j < 0 || j >= n) return -1;
+  uint64_t a = ((uint64_t)keys[i] << 32) | (uint32_t)i;
+  uint64_t b = ((uint64_t)keys[j] << 32) | (uint32_t)j;
+  return __clzll(a ^ b);
+}
+
+// 4. Karras 2012 hierarchy: internal node i, children encoded >= 0 internal / ~leaf.
+__global__ void k_karras(const uint32_t* __restrict__ keys, int n, int* __restrict__ child,
+                         int* __restrict__ parent_int, int* __restrict__ parent_leaf) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n - 1) return;
+  int d = (delta(keys, n, i, i + 1) - delta(keys, n, i, i - 1)) >= 0 ? 1 : -1;
+  int dmin = delta(keys, n, i, i - d);
+  int lmax = 2;
+  while (delta(keys, n, i, i + lmax * d) > dmin) lmax <<= 1;
+  int l = 0;
+  for (int t = lmax >> 1; t >= 1; t >>= 1)
+    if (delta(keys, n, i, i + (l + t) * d) > dmin) l += t;
+  int j = i + l * d;
+  int dnode = delta(keys, n, i, j);
+  int s = 0, t = l;
+  while (true) {
+    t = (t + 1) >> 1;
+    if (delta(keys, n, i, i + (s + t) * d) > dnode) s += t;
+    if (t <= 1) break;
+  }
+  int gamma = i + s * d + (d < 0 ? d : 0);
+  int lo = i < j ? i : j, hi = i < j ? j : i;
+  int left = (lo == gamma) ? ~gamma : gamma;
+  int right = (hi == gamma + 1) ? ~(gamma + 1) : gamma + 1;
+  child[2 * i] = left;
+  child[2 * i + 1] = right;
+  if (left >= 0) parent_int[left] = i; else parent_leaf[~left] = i;
+  if (right >= 0) parent_int[right] = i; else parent_leaf[~right] = i;
+  if (i == 0) parent_int[0] = -1;
+}
+
+__device__ __forceinline__ void load_box(int c, const float* __restrict__ nbox,
+                                         const float* __restrict__ primbox,
+                                         const uint32_t* __restrict__ sorted, float b[6]) {
+  const float* p = c >= 0 ? nbox + (size_t)c * 6 : primbox + (size_t)sorted[~c] * 6;
+  for (int k = 0; k < 6; ++k) b[k] = p[k];
+}
+
+// 5. bottom-up refit. The second arrival at a node computes its box. Hand-off follows the
+// agent-scope release -> counter -> acquire protocol (node boxes may be cached on other XCDs).
+__global__ void k_refit(int n, const int* __restrict__ parent_leaf, const int* __restrict__ parent_int,
+                        const int* __restrict__ child, const float* __restrict__ primbox,
+                        const uint32_t* __restrict__ sorted, float* nbox, uint32_t* flags) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int node = parent_leaf[i];
+  while (node >= 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t old = __hip_atomic_fetch_add(&flags[node], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == 0) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    float a[6], b[6];
+    load_box(child[2 * node], nbox, primbox, sorted, a);
+    load_box(child[2 * node + 1], nbox, primbox, sorted, b);
+    float* o = nbox + (size_t)node * 6;
+    for (int k = 0; k < 3; ++k) {
+      o[k] = fminf(a[k], b[k]);
+      o[3 + k] = fmaxf(a[3 + k], b[3 + k]);
+    }
+    node = parent_int[node];
+  }
+}
+
+// 6. pack child-pair nodes.
+__global__ void k_pack(int n, const int* __restrict__ child, const float* __restrict__ nbox,
+                       const float* __restrict__ primbox, const uint32_t* __restrict__ sorted,
+                       bool leaf_ref_is_prim, BvhNode* __restrict__ nodes) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n - 1) return;
+  BvhNode nd;
+  int c[2] = {child[2 * i], child[2 * i + 1]};
+  float b[2][6];
+  for (int k = 0; k < 2; ++k) load_box(c[k], nbox, primbox, sorted, b[k]);
+  for (int k = 0; k < 3; ++k) {
+    nd.lo0[k] = b[0][k];
+    nd.hi0[k] = b[0][3 + k];
+    nd.lo1[k] = b[1][k];
+    nd.hi1[k] = b[1][3 + k];
+  }
+  for (int k = 0; k < 2; ++k)
+    if (c[k] < 0 && leaf_ref_is_prim) c[k] = ~(int)sorted[~c[k]];
+  nd.c0 = c[0];
+  nd.c1 = c[1];
+  nd.pad0 = nd.pad1 = 0;
+  nodes[i] = nd;
+}
+
+// n == 1: a root whose two children are the single leaf (tested twice; ties keep the result).
+__global__ void k_single(const float* __restrict__ primbox, bool leaf_ref_is_prim, BvhNode* nodes) {
+  BvhNode nd;
+  for (int k = 0; k < 3; ++k) {
+    nd.lo0[k] = nd.lo1[k] = primbox[k];
+    nd.hi0[k] = nd.hi1[k] = primbox[3 + k];
+  }
+  nd.c0 = nd.c1 = ~0;
+  (void)leaf_ref_is_prim;  // ~slot 0 == ~prim 0
+  nd.pad0 = nd.pad1 = 0;
+  nodes[0] = nd;
+}
+
+__global__ void k_depth(int n, const int* __restrict__ parent_leaf, const int* __restrict__ parent_int,
+                        uint32_t* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t d = 1;
+  int node = parent_leaf[i];
+  while (parent_int[node] >= 0) {
+    node = parent_int[node];
+    ++d;
+  }
+  atomicMax(out, d);
+}
+
+__global__ void k_tri_setup(const float* __restrict__ vtx, const uint32_t* __restrict__ idx,
+                            uint32_t ntri, TriRec* __restrict__ tris, float* __restrict__ box) {
+  uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= ntri) return;
+  uint32_t i0 = idx ? idx[3 * p] : 3 * p, i1 = idx ? idx[3 * p + 1] : 3 * p + 1,
+           i2 = idx ? idx[3 * p + 2] : 3 * p + 2;
+  const float* a = vtx + (size_t)i0 * 6;
+  const float* b = vtx + (size_t)i1 * 6;
+  const float* c = vtx + (size_t)i2 * 6;
+  TriRec t;
+  for (int k = 0; k < 3; ++k) {
+    t.v0[k] = a[k];
+    t.e1[k] = b[k] - a[k];
+    t.e2[k] = c[k] - a[k];
+    // "+ 0.0f" turns -0 into +0: min/max of +-0 may return either sign, boxes must be canonical
+    box[(size_t)p * 6 + k] = fminf(fminf(a[k], b[k]), c[k]) + 0.0f;
+    box[(size_t)p * 6 + 3 + k] = fmaxf(fmaxf(a[k], b[k]), c[k]) + 0.0f;
+  }
+  t.prim = p;
+  t.pad1 = t.pad2 = 0;
+  tris[p] = t;
+}
+
+__global__ void k_tri_reorder(const TriRec* __restrict__ in, const uint32_t* __restrict__ sorted,
+                              uint32_t n, TriRec* __restrict__ out) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = in[sorted[i]];
+}
+
+__global__ void k_inst_boxes(const InstanceRec* __restrict__ inst, const float* __restrict__ bb,
+                             uint32_t n, float* __restrict__ box) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* m = inst[i].o2w;
+  const float* b = bb + (size_t)i * 6;
+  float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int c = 0; c < 8; ++c) {
+    V3 p = v3((c & 1) ? b[3] : b[0], (c & 2) ? b[4] : b[1], (c & 4) ? b[5] : b[2]);
+    V3 w = xform_point(m, p);
+    lo[0] = fminf(lo[0], w.x);
+    lo[1] = fminf(lo[1], w.y);
+    lo[2] = fminf(lo[2], w.z);
+    hi[0] = fmaxf(hi[0], w.x);
+    hi[1] = fmaxf(hi[1], w.y);
+    hi[2] = fmaxf(hi[2], w.z);
+  }
+  for (int k = 0; k < 3; ++k) {
+    box[(size_t)i * 6 + k] = lo[k] + 0.0f;  // canonical +0
+    box[(size_t)i * 6 + 3 + k] = hi[k] + 0.0f;
+  }
+}
+
+inline unsigned grid1(uint32_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
+struct DevBuf {
+  void* p = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+#define RT_TRY(x)                         \
+  do {                                    \
+    hipError_t e_ = (x);                  \
+    if (e_ != hipSuccess) return e_;      \
+  } while (0)
+
+}  // namespace
+
+hipError_t lbvh_build(const float* d_primbox, uint32_t n, BvhNode* d_nodes, uint32_t* d_sorted,
+                      bool leaf_ref_is_prim, uint32_t* depth, float bounds[6], float* build_ms,
+                      hipStream_t s) {
+  if (n == 0) return hipErrorInvalidValue;
+  hipEvent_t e0, e1;
+  RT_TRY(hipEventCreate(&e0));
+  RT_TRY(hipEventCreate(&e1));
+  RT_TRY(hipEventRecord(e0, s));
+  const uint32_t nblocks = (n + kRsTile - 1) / kRsTile;
+  DevBuf stats, keys0, keys1, vals1, hist, child, pint, pleaf, nbox, flags, dep;
+  RT_TRY(hipMalloc(&stats.p, 12 * sizeof(float)));
+  RT_TRY(hipMalloc(&keys0.p, (size_t)n * 4));
+  RT_TRY(hipMalloc(&keys1.p, (size_t)n * 4));
+  RT_TRY(hipMalloc(&vals1.p, (size_t)n * 4));
+  RT_TRY(hipMalloc(&hist.p, (size_t)256 * nblocks * 4));
+  RT_TRY(hipMalloc(&dep.p, 4));
+  RT_TRY(hipMemsetAsync(dep.p, 0, 4, s));
+  float* cb = (float*)stats.p;
+  k_bounds<<<1, 1024, 0, s>>>(d_primbox, n, cb);
+  RT_TRY(hipGetLastError());
+  uint32_t* ka = (uint32_t*)keys0.p;
+  uint32_t* va = d_sorted;  // values ping-pong between d_sorted and vals1; 4 passes end in d_sorted
+  uint32_t* kb = (uint32_t*)keys1.p;
+  uint32_t* vb = (uint32_t*)vals1.p;
+  k_morton<<<grid1(n, 256), 256, 0, s>>>(d_primbox, n, cb, ka, va);
+  RT_TRY(hipGetLastError());
+  for (int pass = 0; pass < 4; ++pass) {
+    int shift = pass * 8;
+    k_rs_hist<<<nblocks, kRsThreads, 0, s>>>(ka, n, shift, (uint32_t*)hist.p, nblocks);
+    k_rs_scan<<<1, 1024, 0, s>>>((uint32_t*)hist.p, 256 * nblocks);
+    k_rs_scatter<<<nblocks, kRsThreads, 0, s>>>(ka, va, kb, vb, n, shift, (uint32_t*)hist.p, nblocks);
+    RT_TRY(hipGetLastError());
+    std::swap(ka, kb);
+    std::swap(va, vb);
+  }
+  // after 4 swaps: va == d_sorted, ka == keys0 (sorted keys)
+  if (n == 1) {
+    k_single<<<1, 1, 0, s>>>(d_primbox, leaf_ref_is_prim, d_nodes);
+    RT_TRY(hipGetLastError());
+    uint32_t one = 1;
+    RT_TRY(hipMemcpyAsync(dep.p, &one, 4, hipMemcpyHostToDevice, s));
+  } else {
+    RT_TRY(hipMalloc(&child.p, (size_t)(n - 1) * 8));
+    RT_TRY(hipMalloc(&pint.p, (size_t)(n - 1) * 4));
+    RT_TRY(hipMalloc(&pleaf.p, (size_t)n * 4));
+    RT_TRY(hipMalloc(&nbox.p, (size_t)(n - 1) * 24));
+    RT_TRY(hipMalloc(&flags.p, (size_t)(n - 1) * 4));
+    RT_TRY(hipMemsetAsync(flags.p, 0, (size_t)(n - 1) * 4, s));
+    k_karras<<<grid1(n - 1, 256), 256, 0, s>>>(ka, (int)n, (int*)child.p, (int*)pint.p, (int*)pleaf.p);
+    k_refit<<<grid1(n, 256), 256, 0, s>>>((int)n, (int*)pleaf.p, (int*)pint.p, (int*)child.p, d_primbox,
+                                          d_sorted, (float*)nbox.p, (uint32_t*)flags.p);
+    k_pack<<<grid1(n - 1, 256), 256, 0, s>>>((int)n, (int*)child.p, (float*)nbox.p, d_primbox, d_sorted,
+                                             leaf_ref_is_prim, d_nodes);
+    k_depth<<<grid1(n, 256), 256, 0, s>>>((int)n, (int*)pleaf.p, (int*)pint.p, (uint32_t*)dep.p);
+    RT_TRY(hipGetLastError());
+  }
+  RT_TRY(hipEventRecord(e1, s));
+  float hb[12];
+  RT_TRY(hipMemcpyAsync(hb, cb, sizeof(hb), hipMemcpyDeviceToHost, s));
+  RT_TRY(hipMemcpyAsync(depth, dep.p, 4, hipMemcpyDeviceToHost, s));
+  RT_TRY(hipStreamSynchronize(s));
+  for (int k = 0; k < 6; ++k) bounds[k] = hb[6 + k];
+  float ms = 0.0f;
+  RT_TRY(hipEventElapsedTime(&ms, e0, e1));
+  if (build_ms) *build_ms = ms;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return hipSuccess;
+}
+
+hipError_t blas_prepare(const float* d_vtx, const uint32_t* d_idx, uint32_t ntri, TriRec* d_tris,
+                        float* d_primbox, hipStream_t s) {
+  k_tri_setup<<<grid1(ntri, 256), 256, 0, s>>>(d_vtx, d_idx, ntri, d_tris, d_primbox);
+  return hipGetLastError();
+}
+
+hipError_t blas_reorder(const TriRec* d_in, const uint32_t* d_sorted, uint32_t n, TriRec* d_out,
+                        hipStream_t s) {
+  k_tri_reorder<<<grid1(n, 256), 256, 0, s>>>(d_in, d_sorted, n, d_out);
+  return hipGetLastError();
+}
+
+hipError_t tlas_prepare(const InstanceRec* d_inst, const float* d_blas_bounds, uint32_t n,
+                        float* d_primbox, hipStream_t s) {
+  k_inst_boxes<<<grid1(n, 64), 64, 0, s>>>(d_inst, d_blas_bounds, n, d_primbox);
+  return hipGetLastError();
+}
+
+}  // namespace rt

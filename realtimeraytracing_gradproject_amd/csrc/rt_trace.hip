@@ -1,0 +1,463 @@
+// rt_trace.hip — the trace megakernel: RayGen -> TLAS/BLAS traversal + Moller-Trumbore ->
+// ClosestHit / PlaneClosestHit (+ shadow rays) / Miss -> RGBA8, in one launch on gfx950.
+//
+// Replaces DispatchRays (D3D12HelloTriangle.cpp:558-592) and the DXR programs:
+//   RayGen            shaders/RayGen.hlsl:28-43
+//   CastDefaultRay    shaders/Common.hlsl:44-56   (TMin 0, TMax 1e5, no culling)
+//   CastShadowRay     shaders/Common.hlsl:71-82   (TMin 0.01, TMax 1e5, any hit terminates)
+//   ClosestHit        shaders/Hit.hlsl:183-204    (+ :67-174 normal, Lambert, PBR)
+//   PlaneClosestHit   shaders/Hit.hlsl:207-241
+//   Miss              shaders/Miss.hlsl:3-10
+//   ShadowClosestHit / ShadowMiss  shaders/ShadowRay.hlsl:10-20
+// SBT dispatch (D3D12HelloTriangle.cpp:1064-1080) becomes a switch on the instance hit group.
+//
+// Execution model: one lane = one pixel, a wave64 = an 8x8 pixel tile, a 256-thread workgroup =
+// 16x16 pixels. Per-lane traversal stack in LDS laid out [entry][lane] (bank = lane: conflict
+// free). Child-pair nodes: one 64-B node fetch tests both children; near child first.
+#include <hip/hip_runtime.h>
+
+#include "rt_internal.hpp"
+
+namespace rt {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr float kPi = 3.14159265359f;  // Common.hlsl:1
+
+struct Counters {
+  uint32_t primary = 0, shadow = 0, aabb = 0, tri = 0, inst = 0, overflow = 0;
+};
+
+struct HitRec {
+  float t, u, v;
+  uint32_t inst;  // instance index (== InstanceID() of the reference list)
+  uint32_t prim;  // PrimitiveIndex()
+};
+
+__device__ __forceinline__ V3 ld3(const float* p) { return v3(p[0], p[1], p[2]); }
+
+// Two-level stack traversal. ANY_HIT: first accepted hit terminates (shadow rays). Closest hit
+// keeps the lexicographic minimum of (t, instance, primitive): independent of traversal order.
+template <bool ANY_HIT, bool STATS>
+__device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, HitRec& hit,
+                      int* __restrict__ stk, Counters& cnt) {
+  const V3 winvd = v3(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
+  const V3 wnoinv = neg(mul(o, winvd));
+  V3 ro = o, rd = d, rinvd = winvd, rnoinv = wnoinv;
+  const BvhNode* nodes = sc.tlas;
+  const TriRec* tris = nullptr;
+  uint32_t cur = 0;
+  bool in_blas = false;
+  bool found = false;
+  int sp = 0;
+  int ref = 0;
+  hit.t = tmax;
+  hit.inst = 0xffffffffu;
+  hit.prim = 0xffffffffu;
+  hit.u = hit.v = 0.0f;
+  while (true) {
+    if (ref >= 0) {
+      const float4* np = reinterpret_cast<const float4*>(nodes + ref);
+      const float4 a = np[0], b = np[1], c = np[2], e = np[3];
+      const float lo0[3] = {a.x, a.y, a.z}, hi0[3] = {a.w, b.x, b.y};
+      const float lo1[3] = {b.z, b.w, c.x}, hi1[3] = {c.y, c.z, c.w};
+      const int c0 = __float_as_int(e.x), c1 = __float_as_int(e.y);
+      float tn0, tn1;
+      const bool h0 = slab(lo0, hi0, rinvd, rnoinv, tmin, hit.t, tn0);
+      const bool h1 = slab(lo1, hi1, rinvd, rnoinv, tmin, hit.t, tn1);
+      if (STATS) cnt.aabb += 2;
+      if (h0 && h1) {
+        const bool swap = tn1 < tn0;
+        const int nearc = swap ? c1 : c0, farc = swap ? c0 : c1;
+        if (sp < sc.stack_cap) {
+          stk[sp * kBlock] = farc;
+          ++sp;
+        } else if (STATS) {
+          ++cnt.overflow;
+        }
+        ref = nearc;
+        continue;
+      }
+      if (h0) {
+        ref = c0;
+        continue;
+      }
+      if (h1) {
+        ref = c1;
+        continue;
+      }
+    } else if (!in_blas) {
+      cur = (uint32_t)(~ref);
+      const InstanceRec* ir = sc.inst + cur;
+      ro = xform_point(ir->w2o, o);
+      rd = xform_dir(ir->w2o, d);
+      rinvd = v3(safe_inv(rd.x), safe_inv(rd.y), safe_inv(rd.z));
+      rnoinv = neg(mul(ro, rinvd));
+      nodes = ir->nodes;
+      tris = ir->tris;
+      in_blas = true;
+      if (STATS) ++cnt.inst;
+      if (sp < sc.stack_cap) {
+        stk[sp * kBlock] = kStackSentinel;
+        ++sp;
+        ref = 0;
+        continue;
+      }
+      if (STATS) ++cnt.overflow;
+      in_blas = false;  // cannot enter without a way back: skip this instance
+      nodes = sc.tlas;
+      ro = o;
+      rd = d;
+      rinvd = winvd;
+      rnoinv = wnoinv;
+    } else {
+      const float4* tp = reinterpret_cast<const float4*>(tris + (~ref));
+      const float4 a = tp[0], b = tp[1], c = tp[2];
+      if (STATS) ++cnt.tri;
+      float t, u, v;
+      if (moller_trumbore(ro, rd, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), v3(c.x, c.y, c.z), t, u, v) &&
+          t >= tmin) {
+        const uint32_t prim = __float_as_uint(a.w);
+        const bool better =
+            t < hit.t || (t == hit.t && (cur < hit.inst || (cur == hit.inst && prim < hit.prim)));
+        if (better) {
+          hit.t = t;
+          hit.u = u;
+          hit.v = v;
+          hit.inst = cur;
+          hit.prim = prim;
+          found = true;
+          if (ANY_HIT) return true;
+        }
+      }
+    }
+    // pop
+    while (true) {
+      if (sp == 0) return found;
+      --sp;
+      ref = stk[sp * kBlock];
+      if (ref != kStackSentinel) break;
+      in_blas = false;
+      nodes = sc.tlas;
+      ro = o;
+      rd = d;
+      rinvd = winvd;
+      rnoinv = wnoinv;
+    }
+  }
+}
+
+__device__ __forceinline__ void tri_vertex_ids(const InstanceRec* ir, uint32_t prim, uint32_t& i0,
+                                               uint32_t& i1, uint32_t& i2) {
+  if (ir->idx) {
+    i0 = ir->idx[3 * prim];
+    i1 = ir->idx[3 * prim + 1];
+    i2 = ir->idx[3 * prim + 2];
+  } else {
+    i0 = 3 * prim;
+    i1 = 3 * prim + 1;
+    i2 = 3 * prim + 2;
+  }
+}
+
+// CalculateInterpolatedWorldNormal (Hit.hlsl:67-81): vertex order 1,2,0 against (u, v, 1-u-v).
+__device__ V3 interpolated_world_normal(const InstanceRec* ir, uint32_t prim, float u, float v) {
+  uint32_t i0, i1, i2;
+  tri_vertex_ids(ir, prim, i0, i1, i2);
+  const V3 n0 = ld3(ir->vtx + (size_t)i1 * 6 + 3);
+  const V3 n1 = ld3(ir->vtx + (size_t)i2 * 6 + 3);
+  const V3 n2 = ld3(ir->vtx + (size_t)i0 * 6 + 3);
+  const float bz = (1.0f - u) - v;
+  V3 n = normalize(add(add(muls(n0, u), muls(n1, v)), muls(n2, bz)));
+  n = mat3_mul(ir->nrm, n);
+  return normalize(n);
+}
+
+// PlaneClosestHit face normal (Hit.hlsl:218-222): normalize(cross(e1, e2)), then the instance
+// normal matrix without renormalisation.
+__device__ V3 face_world_normal(const InstanceRec* ir, uint32_t prim) {
+  uint32_t i0, i1, i2;
+  tri_vertex_ids(ir, prim, i0, i1, i2);
+  const V3 p0 = ld3(ir->vtx + (size_t)i0 * 6);
+  const V3 p1 = ld3(ir->vtx + (size_t)i1 * 6);
+  const V3 p2 = ld3(ir->vtx + (size_t)i2 * 6);
+  V3 n = normalize(cross(sub(p1, p0), sub(p2, p0)));
+  return mat3_mul(ir->nrm, n);
+}
+
+// CalculateDirectLighting (Hit.hlsl:83-95).
+__device__ V3 direct_lighting(const FrameParams& fp, V3 P, V3 n, V3 albedo) {
+  V3 color = v3(0.0f, 0.0f, 0.0f);
+  for (uint32_t l = 0; l < fp.nlights; ++l) {
+    const LightRec& L = fp.lights[l];
+    const V3 lp = v3(L.position[0], L.position[1], L.position[2]);
+    const V3 lc = v3(L.color[0], L.color[1], L.color[2]);
+    const V3 to_light = neg(normalize(sub(lp, P)));
+    const float f = dot(n, to_light);
+    const float ti = maxf(0.0f, f * L.intensity);
+    color = add(color, muls(mul(albedo, lc), ti));
+  }
+  return color;
+}
+
+// CalculatePBRShading (Hit.hlsl:97-174).
+__device__ V3 pbr_shading(const FrameParams& fp, V3 n, V3 cam, V3 P) {
+  const MaterialRec& m = fp.material;
+  const V3 albedo = v3(m.albedo[0], m.albedo[1], m.albedo[2]);
+  const V3 N = neg(normalize(n));
+  const V3 V = normalize(sub(cam, P));
+  V3 L0 = v3(0.0f, 0.0f, 0.0f);
+  const float r = m.roughness;
+  const float a = r * r;
+  const float a2 = a * a;
+  const float rp1 = r + 1.0f;
+  const float k = (rp1 * rp1) / 8.0f;
+  const V3 F0 = v3(0.04f + m.metallic * (albedo.x - 0.04f), 0.04f + m.metallic * (albedo.y - 0.04f),
+                   0.04f + m.metallic * (albedo.z - 0.04f));
+  for (uint32_t l = 0; l < fp.nlights; ++l) {
+    const LightRec& Lr = fp.lights[l];
+    const V3 lp = v3(Lr.position[0], Lr.position[1], Lr.position[2]);
+    const V3 lc = v3(Lr.color[0], Lr.color[1], Lr.color[2]);
+    const V3 L = normalize(sub(lp, P));
+    const V3 H = normalize(add(V, L));
+    const float dist = length(sub(lp, P));
+    const float att = 1.0f / maxf(dist * dist, 1.0f);
+    const V3 radiance = muls(lc, att);
+    const float x = clamp01(1.0f - maxf(dot(H, V), 0.0f));
+    const float x2 = x * x;
+    const float x5 = (x2 * x2) * x;
+    const V3 F = v3(F0.x + (1.0f - F0.x) * x5, F0.y + (1.0f - F0.y) * x5, F0.z + (1.0f - F0.z) * x5);
+    const float NdotH = maxf(dot(N, H), 0.0f);
+    const float NdotH2 = NdotH * NdotH;
+    float denom = NdotH2 * (a2 - 1.0f) + 1.0f;
+    denom = (kPi * denom) * denom;
+    const float NDF = a2 / denom;
+    const float NdotV = maxf(dot(N, V), 0.0f);
+    const float NdotL = maxf(dot(N, L), 0.0f);
+    const float ggx2 = NdotV / (NdotV * (1.0f - k) + k);
+    const float ggx1 = NdotL / (NdotL * (1.0f - k) + k);
+    const float G = ggx1 * ggx2;
+    const V3 numerator = muls(F, NDF * G);
+    const float denominator = (4.0f * NdotV) * NdotL + 0.0001f;
+    const V3 spec = v3(numerator.x / denominator, numerator.y / denominator, numerator.z / denominator);
+    const float km = 1.0f - m.metallic;
+    const V3 kD = v3((1.0f - F.x) * km, (1.0f - F.y) * km, (1.0f - F.z) * km);
+    const V3 diff = v3((kD.x * albedo.x) / kPi, (kD.y * albedo.y) / kPi, (kD.z * albedo.z) / kPi);
+    L0 = add(L0, muls(mul(add(diff, spec), radiance), NdotL));
+  }
+  V3 c = muls(L0, 0.2f);
+  c = v3(c.x / (c.x + 1.0f), c.y / (c.y + 1.0f), c.z / (c.z + 1.0f));
+  const float g = 1.0f / 2.2f;
+  return v3(det_pow(c.x, g), det_pow(c.y, g), det_pow(c.z, g));
+}
+
+template <bool STATS>
+__device__ bool shadow_ray(const SceneView& sc, V3 P, V3 dir, int* stk, Counters& cnt) {
+  HitRec h;
+  if (STATS) ++cnt.shadow;
+  return trace<true, STATS>(sc, P, normalize(dir), 0.01f, 100000.0f, h, stk, cnt);
+}
+
+// One camera sample -> color (RayGen.hlsl:28-43 and the hit/miss programs).
+template <int MODE, bool STATS>
+__device__ V3 shade_sample(const SceneView& sc, const FrameParams& fp, uint32_t px, uint32_t py,
+                           float ox, float oy, int* stk, Counters& cnt) {
+  const float dx = (((float)px + ox) / (float)fp.width) * 2.0f - 1.0f;
+  const float dy = (((float)py + oy) / (float)fp.height) * 2.0f - 1.0f;
+  float org4[4], dc[4], dw[4];
+  const float zero_one[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+  hlsl_mul4(fp.cb + 32, zero_one, org4);
+  const float ndc[4] = {dx, -dy, 1.0f, 1.0f};
+  hlsl_mul4(fp.cb + 48, ndc, dc);
+  const float dcam[4] = {dc[0], dc[1], dc[2], 0.0f};
+  hlsl_mul4(fp.cb + 32, dcam, dw);
+  const V3 O = v3(org4[0], org4[1], org4[2]);
+  const V3 D = normalize(v3(dw[0], dw[1], dw[2]));  // CastDefaultRay
+  HitRec hit;
+  if (STATS) ++cnt.primary;
+  if (!trace<false, STATS>(sc, O, D, 0.0f, 100000.0f, hit, stk, cnt)) {
+    const float ramp = (float)py / (float)fp.height;  // Miss.hlsl:8
+    return v3(0.0f, 0.2f, 0.7f - 0.3f * ramp);
+  }
+  const InstanceRec* ir = sc.inst + hit.inst;
+  const V3 P = add(O, muls(D, hit.t));  // GetWorldHitPoint, Common.hlsl:24-27
+  const bool plane = ir->hit_group == 2u;
+  if (MODE == 0) {
+    if (plane) {
+      const LightRec& L0 = fp.lights[0];
+      const V3 lp = v3(L0.position[0], L0.position[1], L0.position[2]);
+      const V3 ldir = normalize(sub(lp, P));
+      const V3 n = face_world_normal(ir, hit.prim);
+      bool shadowed = dot(n, ldir) < 0.0f;
+      const bool occl = shadow_ray<STATS>(sc, P, ldir, stk, cnt);
+      if (!shadowed) shadowed = occl;
+      const float factor = shadowed ? 0.3f : 1.0f;
+      const float li = maxf(0.0f, dot(n, ldir));
+      const float c = (1.0f * li) * factor;
+      return v3(c, c, c);
+    }
+    const V3 n = interpolated_world_normal(ir, hit.prim, hit.u, hit.v);
+    const V3 albedo = v3(fp.material.albedo[0], fp.material.albedo[1], fp.material.albedo[2]);
+    const V3 direct = direct_lighting(fp, P, n, albedo);
+    // reflectivity is pinned to 0: lerp(final, refl, 0) == final; no reflection ray.
+    return add(direct, pbr_shading(fp, n, O, P));
+  }
+  // RT_SHADE_LAMBERT_SHADOW (MODE 1) and RT_SHADE_PRIMARY (MODE 2)
+  const V3 n = plane ? face_world_normal(ir, hit.prim) : neg(interpolated_world_normal(ir, hit.prim, hit.u, hit.v));
+  float c = 0.0f;
+  for (uint32_t l = 0; l < fp.nlights; ++l) {
+    const LightRec& Lr = fp.lights[l];
+    const V3 L = normalize(sub(v3(Lr.position[0], Lr.position[1], Lr.position[2]), P));
+    const float nl = dot(n, L);
+    if (nl > 0.0f) {
+      float factor = 1.0f;
+      if (MODE == 1 && shadow_ray<STATS>(sc, P, L, stk, cnt)) factor = 0.3f;
+      c = c + nl * factor;
+    }
+  }
+  c = c / (float)fp.nlights;
+  return v3(c, c, c);
+}
+
+__device__ __forceinline__ void flush_stats(const Counters& c, unsigned long long* stats) {
+  uint32_t v[6] = {c.primary, c.shadow, c.aabb, c.tri, c.inst, c.overflow};
+  const int slot[6] = {0, 1, 2, 3, 4, 5};
+  for (int k = 0; k < 6; ++k) {
+    unsigned long long x = v[k];
+    for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, 64);
+    if ((threadIdx.x & 63) == 0 && x) atomicAdd(stats + slot[k], x);
+  }
+}
+
+template <int MODE, bool STATS>
+__global__ __launch_bounds__(kBlock) void k_trace_frame(SceneView sc, FrameParams fp,
+                                                        const uint32_t* __restrict__ rows,
+                                                        uint32_t* __restrict__ rgba8,
+                                                        float4* __restrict__ rgba32f,
+                                                        unsigned long long* __restrict__ stats) {
+  extern __shared__ int s_stack[];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint32_t px = blockIdx.x * 16u + (w & 1u) * 8u + (lane & 7u);
+  const uint32_t orow = blockIdx.y * 16u + (w >> 1) * 8u + (lane >> 3);
+  Counters cnt;
+  if (px < fp.width && orow < fp.nrows) {
+    const uint32_t py = rows ? rows[orow] : orow;
+    int* stk = s_stack + threadIdx.x;
+    const uint32_t k = fp.spp_side;
+    V3 acc = v3(0.0f, 0.0f, 0.0f);
+    for (uint32_t sy = 0; sy < k; ++sy)
+      for (uint32_t sx = 0; sx < k; ++sx) {
+        const float ox = ((float)sx + 0.5f) / (float)k;
+        const float oy = ((float)sy + 0.5f) / (float)k;
+        acc = add(acc, shade_sample<MODE, STATS>(sc, fp, px, py, ox, oy, stk, cnt));
+      }
+    if (k > 1) {
+      const float ns = (float)(k * k);
+      acc = v3(acc.x / ns, acc.y / ns, acc.z / ns);
+    }
+    const size_t o = (size_t)orow * fp.width + px;
+    rgba8[o] = unorm8(acc.x) | (unorm8(acc.y) << 8) | (unorm8(acc.z) << 16) | (255u << 24);
+    if (rgba32f) rgba32f[o] = make_float4(acc.x, acc.y, acc.z, 1.0f);
+  }
+  if (STATS) flush_stats(cnt, stats);
+}
+
+template <bool ANY_HIT, bool STATS>
+__global__ __launch_bounds__(kBlock) void k_trace_rays(SceneView sc, const float4* __restrict__ rays,
+                                                       uint32_t n, uint4* __restrict__ hits,
+                                                       float2* __restrict__ uv,
+                                                       unsigned long long* __restrict__ stats) {
+  extern __shared__ int s_stack[];
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  Counters cnt;
+  if (i < n) {
+    const float4 a = rays[2 * i], b = rays[2 * i + 1];
+    HitRec h;
+    const bool f = trace<ANY_HIT, STATS>(sc, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), a.w, b.w, h,
+                                         s_stack + threadIdx.x, cnt);
+    if (STATS) ++cnt.primary;
+    hits[i] = make_uint4(__float_as_uint(f ? h.t : b.w), f ? h.inst : 0xffffffffu,
+                         f ? h.prim : 0xffffffffu, f ? 1u : 0u);
+    if (uv) uv[i] = make_float2(f ? h.u : 0.0f, f ? h.v : 0.0f);
+  }
+  if (STATS) flush_stats(cnt, stats);
+}
+
+__global__ void k_assemble(uint32_t W, uint32_t H, uint32_t nranks, uint32_t strip_rows,
+                           const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                           uint32_t rows_per_rank) {
+  // one thread per output pixel (4 B), coalesced along x
+  const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t y = blockIdx.y;
+  if (x >= W || y >= H) return;
+  const uint32_t s = y / strip_rows, within = y % strip_rows;
+  const uint32_t rank = s % nranks, local_strip = s / nranks;
+  const uint32_t lrow = local_strip * strip_rows + within;
+  out[(size_t)y * W + x] = in[((size_t)rank * rows_per_rank + lrow) * W + x];
+}
+
+template <int MODE, bool STATS>
+hipError_t launch_mode(const SceneView& sc, const FrameParams& fp, const uint32_t* rows, void* rgba8,
+                       float* rgba32f, unsigned long long* stats, hipStream_t s) {
+  dim3 grid((fp.width + 15) / 16, (fp.nrows + 15) / 16);
+  size_t lds = (size_t)sc.stack_cap * kBlock * sizeof(int);
+  hipLaunchKernelGGL((k_trace_frame<MODE, STATS>), grid, dim3(kBlock), lds, s, sc, fp, rows,
+                     (uint32_t*)rgba8, (float4*)rgba32f, stats);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_trace_frame(const SceneView& sc, const FrameParams& fp, const uint32_t* d_rows,
+                              void* rgba8, float* rgba32f, unsigned long long* d_stats, bool stats,
+                              int schedule, WavefrontBuffers* wf, hipStream_t s) {
+  (void)schedule;
+  (void)wf;
+  switch (fp.shade_mode) {
+    case 0:
+      return stats ? launch_mode<0, true>(sc, fp, d_rows, rgba8, rgba32f, d_stats, s)
+                   : launch_mode<0, false>(sc, fp, d_rows, rgba8, rgba32f, d_stats, s);
+    case 1:
+      return stats ? launch_mode<1, true>(sc, fp, d_rows, rgba8, rgba32f, d_stats, s)
+                   : launch_mode<1, false>(sc, fp, d_rows, rgba8, rgba32f, d_stats, s);
+    case 2:
+      return stats ? launch_mode<2, true>(sc, fp, d_rows, rgba8, rgba32f, d_stats, s)
+                   : launch_mode<2, false>(sc, fp, d_rows, rgba8, rgba32f, d_stats, s);
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_trace_rays(const SceneView& sc, const float* rays, uint32_t n, int any_hit,
+                             uint32_t* hits, float* uv, unsigned long long* d_stats, bool stats,
+                             hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  dim3 grid((n + kBlock - 1) / kBlock);
+  size_t lds = (size_t)sc.stack_cap * kBlock * sizeof(int);
+  const float4* r = (const float4*)rays;
+  if (any_hit) {
+    if (stats)
+      hipLaunchKernelGGL((k_trace_rays<true, true>), grid, dim3(kBlock), lds, s, sc, r, n, (uint4*)hits, (float2*)uv, d_stats);
+    else
+      hipLaunchKernelGGL((k_trace_rays<true, false>), grid, dim3(kBlock), lds, s, sc, r, n, (uint4*)hits, (float2*)uv, d_stats);
+  } else {
+    if (stats)
+      hipLaunchKernelGGL((k_trace_rays<false, true>), grid, dim3(kBlock), lds, s, sc, r, n, (uint4*)hits, (float2*)uv, d_stats);
+    else
+      hipLaunchKernelGGL((k_trace_rays<false, false>), grid, dim3(kBlock), lds, s, sc, r, n, (uint4*)hits, (float2*)uv, d_stats);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_assemble_strips(uint32_t W, uint32_t H, uint32_t nranks, uint32_t strip_rows,
+                                  const void* gathered, void* out, hipStream_t s) {
+  const uint32_t nstrips = (H + strip_rows - 1) / strip_rows;
+  const uint32_t strips_per_rank = (nstrips + nranks - 1) / nranks;
+  const uint32_t rows_per_rank = strips_per_rank * strip_rows;
+  dim3 grid((W + 255) / 256, H);
+  hipLaunchKernelGGL(k_assemble, grid, dim3(256), 0, s, W, H, nranks, strip_rows, (const uint32_t*)gathered,
+                     (uint32_t*)out, rows_per_rank);
+  return hipGetLastError();
+}
+
+}  // namespace rt

@@ -1,0 +1,149 @@
+"""Scene descriptions: the reference scene and the BASELINE configs C1..C5.
+
+Reference scene (D3D12HelloTriangle::CreateAccelerationStructures, D3D12HelloTriangle.cpp:778-810):
+teapot.obj with vertex normals (:335-346), 6 model instances (identity, (-5,0,5) twice, (-5,0,-5),
+(5,0,-5), (5,0,5)) with hit group 0 and the ground plane (CreatePlaneVB :1237-1271) with hit group 2;
+InstanceID = list index (:749). Lights: Hit.hlsl:48-57. Material: UIConstructor defaults
+(UIConstructor.cpp:13-17) with reflectivity pinned to 0. Camera: setLookat((1.5,1.5,1.5),
+(0,0,0), (0,1,0)) (D3D12HelloTriangle.cpp:45), 45 deg, near 0.1, far 1000 (:1154-1156), 1280x720
+(Main.cpp:18).
+
+BASELINE configs: C1 teapot 512^2 primary only; C2 teapot 1080p primary+shadow;
+C3 rabbit 1080p; C4 rabbit x64 grid, 2 lights; C5 rabbit x256 grid, 4 lights, 4K, 4 spp.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+from . import (RT_HITGROUP_MODEL, RT_HITGROUP_PLANE, RT_SHADE_LAMBERT_SHADOW, RT_SHADE_PRIMARY, RT_SHADE_REF,
+               Mesh, camera_buffer, camera_lookat, plane_vertices)
+
+# Hit.hlsl:51-56 — colour, position, intensity
+REFERENCE_LIGHTS = [
+    ((1.0, 1.0, 1.0), (0.0, 10.0, 0.0), 0.2),
+    ((1.0, 1.0, 1.0), (10.0, 10.0, 0.0), 0.2),
+    ((1.0, 1.0, 1.0), (-10.0, 10.0, 0.0), 0.2),
+    ((1.0, 1.0, 1.0), (0.0, 10.0, 10.0), 0.2),
+    ((1.0, 1.0, 1.0), (0.0, 10.0, -10.0), 0.2),
+    ((1.0, 1.0, 1.0), (0.0, -10.0, 0.0), 0.2),
+]
+# albedo rgb, roughness, metallic, reflectivity (UIConstructor.cpp:13-17; reflectivity pinned 0)
+REFERENCE_MATERIAL = (1.0, 1.0, 1.0, 0.5, 0.5, 0.0)
+REFERENCE_CAMERA = ((1.5, 1.5, 1.5), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0))
+
+
+def translation(tx: float, ty: float, tz: float) -> np.ndarray:
+    return np.array([1, 0, 0, tx, 0, 1, 0, ty, 0, 0, 1, tz], np.float32)
+
+
+IDENTITY = translation(0, 0, 0)
+
+
+@dataclass
+class SceneSpec:
+    name: str
+    meshes: List[Tuple[np.ndarray, Optional[np.ndarray]]]  # (vertices N x 6, indices or None)
+    instances: List[Tuple[int, np.ndarray, int, int]]      # (mesh index, 3x4 xform, instance id, hit group)
+    lights: list
+    material: tuple
+    camera: tuple
+    width: int
+    height: int
+    mode: int
+    spp: int = 1
+    fov_deg: float = 45.0
+    model: str = "teapot"
+
+    def camera_buffer(self) -> np.ndarray:
+        view = camera_lookat(*self.camera)
+        return camera_buffer(view, self.width, self.height, self.fov_deg, 0.1, 1000.0)
+
+    def with_size(self, width: int, height: int) -> "SceneSpec":
+        s = SceneSpec(**{**self.__dict__})
+        s.width, s.height = width, height
+        return s
+
+    @property
+    def triangles(self) -> int:
+        return sum((m[1].size // 3 if m[1] is not None else m[0].shape[0] // 3) for m in self.meshes)
+
+
+def load_model(name: str) -> Tuple[np.ndarray, np.ndarray]:
+    """OBJ ingest + ComputeVertexNormals, as LoadAssets does (D3D12HelloTriangle.cpp:335-346)."""
+    m = Mesh.asset(name).compute_vertex_normals()
+    return m.vertices, m.indices
+
+
+_model_cache = {}
+
+
+def _model(name: str):
+    if name not in _model_cache:
+        _model_cache[name] = load_model(name)
+    return _model_cache[name]
+
+
+def reference_scene() -> SceneSpec:
+    model = _model("teapot")
+    inst = [
+        (0, translation(0, 0, 0), 0, RT_HITGROUP_MODEL),
+        (0, translation(-5, 0, 5), 1, RT_HITGROUP_MODEL),
+        (0, translation(-5, 0, 5), 2, RT_HITGROUP_MODEL),
+        (0, translation(-5, 0, -5), 3, RT_HITGROUP_MODEL),
+        (0, translation(5, 0, -5), 4, RT_HITGROUP_MODEL),
+        (0, translation(5, 0, 5), 5, RT_HITGROUP_MODEL),
+        (1, IDENTITY, 6, RT_HITGROUP_PLANE),
+    ]
+    return SceneSpec("reference", [model, (plane_vertices(), None)], inst, REFERENCE_LIGHTS,
+                     REFERENCE_MATERIAL, REFERENCE_CAMERA, 1280, 720, RT_SHADE_REF)
+
+
+def _single(name: str, tag: str, w: int, h: int, mode: int, nlights: int = 1) -> SceneSpec:
+    model = _model(name)
+    inst = [(0, IDENTITY, 0, RT_HITGROUP_MODEL), (1, IDENTITY, 1, RT_HITGROUP_PLANE)]
+    return SceneSpec(tag, [model, (plane_vertices(), None)], inst, REFERENCE_LIGHTS[:nlights],
+                     REFERENCE_MATERIAL, REFERENCE_CAMERA, w, h, mode, model=name)
+
+
+def _grid(name: str, tag: str, side: int, nlights: int, w: int, h: int, spp: int, camera) -> SceneSpec:
+    model = _model(name)
+    inst = []
+    half = (side - 1) / 2.0
+    for i in range(side):
+        for j in range(side):
+            inst.append((0, translation((i - half) * 3.0, 0.0, (j - half) * 3.0), len(inst), RT_HITGROUP_MODEL))
+    inst.append((1, IDENTITY, len(inst), RT_HITGROUP_PLANE))
+    return SceneSpec(tag, [model, (plane_vertices(), None)], inst, REFERENCE_LIGHTS[:nlights], REFERENCE_MATERIAL,
+                     camera, w, h, RT_SHADE_LAMBERT_SHADOW, spp, model=name)
+
+
+def config(name: str) -> SceneSpec:
+    name = name.upper()
+    if name == "REF":
+        return reference_scene()
+    if name == "C1":
+        return _single("teapot", "C1", 512, 512, RT_SHADE_PRIMARY)
+    if name == "C2":
+        return _single("teapot", "C2", 1920, 1080, RT_SHADE_LAMBERT_SHADOW)
+    if name == "C3":
+        return _single("rabbit", "C3", 1920, 1080, RT_SHADE_LAMBERT_SHADOW)
+    if name == "C4":
+        return _grid("rabbit", "C4", 8, 2, 1920, 1080, 1, ((18.0, 14.0, 18.0), (0.0, 1.0, 0.0), (0.0, 1.0, 0.0)))
+    if name == "C5":
+        return _grid("rabbit", "C5", 16, 4, 3840, 2160, 4, ((30.0, 22.0, 30.0), (0.0, 1.0, 0.0), (0.0, 1.0, 0.0)))
+    raise KeyError(name)
+
+
+CONFIGS = ("REF", "C1", "C2", "C3", "C4", "C5")
+
+
+def upload(ctx, spec: SceneSpec) -> List[int]:
+    """Builds BLAS/TLAS and frame state of `spec` on a Context; returns the BLAS ids."""
+    ids = [ctx.blas_build(v, i) for (v, i) in spec.meshes]
+    ctx.tlas_build([(ids[m], x, iid, hg) for (m, x, iid, hg) in spec.instances])
+    ctx.set_camera(spec.camera_buffer())
+    ctx.set_shading(spec.lights, spec.material, spec.mode, spec.spp)
+    return ids

@@ -1,0 +1,287 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle on the same inputs.
+
+Integer/index work (BVH nodes, leaf order, hit ids, RGBA8) must match bit for bit; the float32
+frame too, because the kernel and the oracle evaluate the same expressions in the same order with
+correctly rounded IEEE operations (-ffp-contract=off on both sides). The tolerance written into the
+float checks below is 0 for that reason; BASELINE's north-star bound (L-inf < 1e-3) is far looser.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import realtimeraytracing_gradproject_amd as rt  # noqa: E402
+from realtimeraytracing_gradproject_amd import scenes  # noqa: E402
+
+import oracle  # noqa: E402
+
+FLOAT_TOL = 0.0  # bit-identical float32 frame expected (north-star bound: 1e-3)
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = rt.Context(0)
+    yield c
+    c.close()
+
+
+def fresh_ctx():
+    return rt.Context(0)
+
+
+def gpu_render(c, spec, rows=None, schedule=rt.RT_SCHED_MEGAKERNEL):
+    nrows = spec.height if rows is None else len(rows)
+    out8 = torch.empty((nrows, spec.width, 4), dtype=torch.uint8, device="cuda")
+    out32 = torch.empty((nrows, spec.width, 4), dtype=torch.float32, device="cuda")
+    c.set_schedule(schedule)
+    c.dispatch(spec.width, spec.height, out8, out32, rows=rows, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return out8.cpu().numpy(), out32.cpu().numpy()
+
+
+def load_both(spec):
+    c = fresh_ctx()
+    scenes.upload(c, spec)
+    o = oracle.Scene(spec)
+    return c, o
+
+
+def assert_images_equal(g8, g32, o8, o32, what):
+    d = np.abs(g32.astype(np.float64) - o32.astype(np.float64))
+    bad = np.argwhere(d > FLOAT_TOL)
+    assert d.max() <= FLOAT_TOL, f"{what}: float L-inf {d.max()} at {bad[:5].tolist()} ({len(bad)} values)"
+    n8 = int((g8 != o8).sum())
+    assert n8 == 0, f"{what}: {n8} RGBA8 channels differ"
+
+
+# ------------------------------------------------------------------------------------------
+# acceleration structures
+# ------------------------------------------------------------------------------------------
+
+@pytest.mark.parametrize("model", ["teapot", "rabbit"])
+def test_blas_bitwise_equal_to_oracle(model):
+    v, i = scenes.load_model(model)
+    c = fresh_ctx()
+    b = c.blas_build(v, i)
+    gn, gt = c.blas_export(b)
+    o = oracle.Scene()
+    ob = o.add_blas(v, i)
+    on, ot = o.export_blas(ob)
+    assert np.array_equal(gn, on), f"{model}: {int((gn != on).any(axis=1).sum())} nodes differ"
+    assert np.array_equal(gt, ot)
+    info = c.blas_info(b)
+    prims, nn, depth = o.blas_info(ob)
+    assert (info.prim_count, info.node_count, info.depth) == (prims, nn, depth)
+    # every primitive exactly once in leaf order
+    assert np.array_equal(np.sort(gt[:, 3]), np.arange(prims, dtype=np.uint32))
+    c.close()
+
+
+@pytest.mark.parametrize("ntri", [1, 2, 3, 7, 1000, 1025, 5000])
+def test_blas_edge_sizes(ntri):
+    rng = np.random.default_rng(1234 + ntri)
+    v = np.zeros((ntri * 3, 6), np.float32)
+    v[:, :3] = rng.uniform(-5, 5, size=(ntri * 3, 3)).astype(np.float32)
+    v[:, 4] = 1.0
+    c = fresh_ctx()
+    b = c.blas_build(v)  # non-indexed
+    gn, gt = c.blas_export(b)
+    o = oracle.Scene()
+    ob = o.add_blas(v)
+    on, ot = o.export_blas(ob)
+    assert np.array_equal(gn, on)
+    assert np.array_equal(gt, ot)
+    c.close()
+
+
+def test_blas_duplicate_centroids():
+    # many triangles with identical Morton codes: Karras tie-break on leaf position
+    v = np.zeros((300 * 3, 6), np.float32)
+    base = np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0]], np.float32)
+    for k in range(300):
+        v[k * 3:(k + 1) * 3, :3] = base
+    c = fresh_ctx()
+    b = c.blas_build(v)
+    gn, gt = c.blas_export(b)
+    o = oracle.Scene()
+    ob = o.add_blas(v)
+    on, ot = o.export_blas(ob)
+    assert np.array_equal(gn, on) and np.array_equal(gt, ot)
+    c.close()
+
+
+@pytest.mark.parametrize("name", ["REF", "C4"])
+def test_tlas_bitwise_equal_to_oracle(name):
+    spec = scenes.config(name)
+    c, o = load_both(spec)
+    assert np.array_equal(c.tlas_export(), o.export_tlas())
+    info = c.tlas_info()
+    assert (info.prim_count, info.node_count, info.depth) == tuple(o.tlas_info())
+    c.close()
+
+
+# ------------------------------------------------------------------------------------------
+# frames
+# ------------------------------------------------------------------------------------------
+
+SMALL = {"REF": (160, 90), "C1": (128, 128), "C2": (192, 108), "C3": (192, 108), "C4": (192, 108),
+         "C5": (96, 54)}
+
+
+@pytest.mark.parametrize("name", list(SMALL))
+def test_frame_parity_small(name):
+    spec = scenes.config(name).with_size(*SMALL[name])
+    c, o = load_both(spec)
+    g8, g32 = gpu_render(c, spec)
+    o8, o32, _ = o.render_spec(spec, nthreads=8)
+    assert_images_equal(g8, g32, o8, o32, name)
+    c.close()
+
+
+@pytest.mark.parametrize("name", ["REF", "C2", "C4"])
+def test_counters_match_oracle(name):
+    spec = scenes.config(name).with_size(*SMALL[name])
+    c, o = load_both(spec)
+    c.set_stats(True)
+    c.stats_reset()
+    gpu_render(c, spec)
+    s = c.stats()
+    _, _, ost = o.render_spec(spec, nthreads=4)
+    keys = ["primary_rays", "shadow_rays", "aabb_tests", "tri_tests", "instance_entries", "stack_overflows"]
+    assert [s[k] for k in keys] == [int(x) for x in ost[:6]]
+    assert s["stack_overflows"] == 0
+    c.close()
+
+
+def test_rows_subset_matches_full_frame():
+    spec = scenes.config("C2").with_size(160, 96)
+    c, o = load_both(spec)
+    f8, f32 = gpu_render(c, spec)
+    rows = np.array([0, 5, 17, 18, 50, 95], np.uint32)
+    r8, r32 = gpu_render(c, spec, rows=rows)
+    assert np.array_equal(r8, f8[rows]) and np.array_equal(r32, f32[rows])
+    c.close()
+
+
+def test_full_size_c2_sampled_rows():
+    """Full BASELINE size (1920x1080): GPU frame vs oracle on a deterministic row sample."""
+    spec = scenes.config("C2")
+    c, o = load_both(spec)
+    g8, g32 = gpu_render(c, spec)
+    rows = np.arange(0, spec.height, 41, dtype=np.uint32)
+    o8, o32, _ = o.render_spec(spec, rows=rows, nthreads=8)
+    assert_images_equal(g8[rows], g32[rows], o8, o32, "C2 1080p sampled rows")
+    # size-independent property: alpha channel is opaque everywhere
+    assert (g8[..., 3] == 255).all()
+    c.close()
+
+
+def test_strip_partition_and_assemble():
+    """Multi-GPU frame assembly on one device: render per-rank strips, gather, un-interleave."""
+    spec = scenes.config("C2").with_size(200, 123)
+    c, o = load_both(spec)
+    full8, _ = gpu_render(c, spec)
+    nranks, strip = 3, 8
+    per = [rt.strip_rows(spec.height, nranks, r, strip) for r in range(nranks)]
+    rows_per_rank = rt.strip_rows_per_rank(spec.height, nranks, strip)
+    gathered = torch.zeros((nranks, rows_per_rank, spec.width, 4), dtype=torch.uint8, device="cuda")
+    for r, rows in enumerate(per):
+        part8, _ = gpu_render(c, spec, rows=rows)
+        gathered[r, :len(rows)] = torch.from_numpy(part8).cuda()
+    out = torch.empty((spec.height, spec.width, 4), dtype=torch.uint8, device="cuda")
+    c.assemble_strips(spec.width, spec.height, nranks, strip, gathered, out)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), full8)
+    c.close()
+
+
+# ------------------------------------------------------------------------------------------
+# TraceRay semantics: BVH closest hit == brute force over every triangle
+# ------------------------------------------------------------------------------------------
+
+def random_rays(n, seed, center=(0.0, 1.0, 0.0), radius=12.0):
+    rng = np.random.default_rng(seed)
+    o = rng.normal(size=(n, 3))
+    o = o / np.linalg.norm(o, axis=1, keepdims=True) * radius + np.asarray(center)
+    tgt = rng.uniform(-6, 6, size=(n, 3)) + np.asarray(center)
+    d = tgt - o
+    d = d / np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.zeros((n, 8), np.float32)
+    rays[:, :3] = o
+    rays[:, 3] = 0.0
+    rays[:, 4:7] = d
+    rays[:, 7] = 100000.0
+    return rays
+
+
+@pytest.mark.parametrize("any_hit", [False, True])
+def test_trace_rays_equals_bruteforce(any_hit):
+    spec = scenes.config("REF")
+    c, o = load_both(spec)
+    n = 100000
+    rays = random_rays(n, 0x5EED)
+    d_rays = torch.from_numpy(rays).cuda()
+    d_hits = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+    d_uv = torch.zeros((n, 2), dtype=torch.float32, device="cuda")
+    c.trace_rays(d_rays, n, any_hit, d_hits, d_uv)
+    torch.cuda.synchronize()
+    g = d_hits.cpu().numpy().view(np.uint32)
+    guv = d_uv.cpu().numpy()
+    ob, ouv, _ = o.trace_rays(rays, any_hit=any_hit, brute_force=False)
+    assert np.array_equal(g, ob), "GPU BVH traversal differs from oracle BVH traversal"
+    assert np.array_equal(guv, ouv)
+    if not any_hit:
+        sub = slice(0, 20000)  # brute force is O(rays x triangles) on the CPU
+        bb, buv, _ = o.trace_rays(rays[sub], any_hit=False, brute_force=True)
+        assert np.array_equal(g[sub], bb), "BVH closest hit differs from brute force"
+        assert np.array_equal(guv[sub], buv)
+    else:
+        bb, _, _ = o.trace_rays(rays[:20000], any_hit=True, brute_force=True)
+        assert np.array_equal(g[:20000, 3], bb[:, 3]), "occlusion flag differs from brute force"
+    assert g[:, 3].sum() > n // 10  # the sample actually hits geometry
+    c.close()
+
+
+# ------------------------------------------------------------------------------------------
+# dynamic scenes and error behaviour
+# ------------------------------------------------------------------------------------------
+
+def test_blas_rebuild_and_tlas_update():
+    spec = scenes.config("REF").with_size(128, 72)
+    c, o = load_both(spec)  # BLAS ids on the device == mesh indices of the spec (0 model, 1 plane)
+    rv, ri = scenes.load_model("rabbit")
+    c.blas_rebuild(0, rv, ri)  # model hot-reload (D3D12HelloTriangle.cpp:1482-1596)
+    c.tlas_build(spec.instances)
+    spec2 = scenes.SceneSpec(**{**spec.__dict__})
+    spec2.meshes = [(rv, ri), spec.meshes[1]]
+    g8, g32 = gpu_render(c, spec2)
+    o8, o32, _ = oracle.Scene(spec2).render_spec(spec2, nthreads=4)
+    assert_images_equal(g8, g32, o8, o32, "after rebuild")
+    # update_only: move instance 0, same BLAS ids (TopLevelASGenerator.cpp:202-222)
+    inst = list(spec.instances)
+    inst[0] = (0, scenes.translation(0.5, 0.25, -0.5), 0, rt.RT_HITGROUP_MODEL)
+    c.tlas_build(inst, update_only=True)
+    spec3 = scenes.SceneSpec(**{**spec2.__dict__})
+    spec3.instances = inst
+    g8, g32 = gpu_render(c, spec3)
+    o8, o32, _ = oracle.Scene(spec3).render_spec(spec3, nthreads=4)
+    assert_images_equal(g8, g32, o8, o32, "after TLAS update")
+    with pytest.raises(rt.RtError):
+        c.tlas_build(inst[:3], update_only=True)  # count change is not an update
+    c.close()
+
+
+def test_invalid_arguments_raise():
+    c = fresh_ctx()
+    v = np.zeros((4, 6), np.float32)
+    with pytest.raises(rt.RtError):
+        c.blas_build(v)  # non-indexed count not a multiple of 3
+    with pytest.raises(rt.RtError):
+        c.blas_build(v, np.array([0, 1, 9], np.uint32))  # index out of range
+    out = torch.empty((4, 4, 4), dtype=torch.uint8, device="cuda")
+    with pytest.raises(rt.RtError):
+        c.dispatch(4, 4, out)  # nothing built yet
+    with pytest.raises(rt.RtError):
+        c.set_shading(scenes.REFERENCE_LIGHTS[:1], scenes.REFERENCE_MATERIAL, 0, spp=3)
+    c.close()
