@@ -34,6 +34,7 @@ import realtimeraytracing_gradproject_amd as rt  # noqa: E402
 from realtimeraytracing_gradproject_amd import scenes  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+L2_PEAK_GBS = 34500.0  # aggregate L2 bandwidth, 8 XCDs (MI355X_MICROARCH.md, L2 section)
 BYTES_PER_AABB_TEST = 24  # one child box (6 floats) per slab test
 BYTES_PER_TRI_TEST = 36   # v0, e1, e2 (9 floats) per Moller-Trumbore test
 BYTES_PER_PIXEL = 4       # RGBA8 write
@@ -50,6 +51,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=2.0, help="minimum wall time of the CPU baseline sample")
     p.add_argument("--save-image", default="", help="write the rank-0 frame as .npy")
+    p.add_argument("--extra", default="C2F,C3,C4,C5",
+                   help="comma list of further configs timed on one GPU (N=1 only; '' to skip)")
     return p.parse_args()
 
 
@@ -85,6 +88,40 @@ def cpu_baseline(spec, seconds: float):
     return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"{frames} full {spec.name} frame(s) {spec.width}x{spec.height} by oracle/rt_oracle.c "
                       f"({threads} threads, {dt:.1f} s wall)"}
+
+
+def measure_config(name: str, steps: int, warmup: int, schedule: int) -> dict:
+    """Single-GPU frame rate of another BASELINE config (reported under "extra", not the headline)."""
+    spec = scenes.config(name)
+    W, H = spec.width, spec.height
+    with rt.Context(torch.cuda.current_device()) as ctx:
+        scenes.upload(ctx, spec)
+        ctx.set_schedule(schedule)
+        stream = torch.cuda.Stream()
+        out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+        ctx.set_stats(True)
+        ctx.stats_reset()
+        ctx.dispatch(W, H, out, None, stream=stream.cuda_stream)
+        torch.cuda.synchronize()
+        st = ctx.stats()
+        ctx.set_stats(False)
+        for _ in range(warmup):
+            ctx.dispatch(W, H, out, None, stream=stream.cuda_stream)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(stream)
+        for _ in range(steps):
+            ctx.dispatch(W, H, out, None, stream=stream.cuda_stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        ms = e0.elapsed_time(e1) / steps
+    rays = st["primary_rays"] + st["shadow_rays"]
+    return {"config": name, "Mrays_s": round(rays * steps / wall / 1e6, 1), "frame_ms": round(wall / steps * 1e3, 4),
+            "kernel_ms": round(ms, 4), "rays_per_frame": int(rays), "resolution": f"{W}x{H}", "spp": spec.spp,
+            "aabb_tests_per_ray": round(st["aabb_tests"] / max(rays, 1), 2),
+            "tri_tests_per_ray": round(st["tri_tests"] / max(rays, 1), 2)}
 
 
 def main():
@@ -179,6 +216,11 @@ def main():
         cpu = None
         if not distributed and not a.no_cpu_baseline:
             cpu = cpu_baseline(spec, a.cpu_seconds)
+        extra = []
+        if not distributed and a.extra:
+            sched = rt.RT_SCHED_WAVEFRONT if a.schedule == "wavefront" else rt.RT_SCHED_MEGAKERNEL
+            for name in a.extra.split(","):
+                extra.append(measure_config(name, max(5, a.steps // 2), 2, sched))
         out = {
             "metric": "Mrays/sec (primary+shadow) at 1080p",
             "value": round(value, 2),
@@ -202,9 +244,13 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "k_trace_frame", "kernel_ms": round(kernel_ms, 4),
                          "bytes_per_launch": int(bytes_launch),
-                         "aabb_tests": int(st["aabb_tests"]), "tri_tests": int(st["tri_tests"])},
+                         "aabb_tests": int(st["aabb_tests"]), "tri_tests": int(st["tri_tests"]),
+                         # the BVH (~1 MB) is L2-resident: algorithmic bytes are served by L2/L1, so
+                         # frac vs HBM can exceed 1; the L2 roof (MI355X_MICROARCH.md) is the cache bound
+                         "l2_peak": L2_PEAK_GBS, "l2_frac": round(achieved / L2_PEAK_GBS, 4)},
             "cpu_baseline": cpu,
             "build_ms": {"blas": [round(b.build_ms, 3) for b in binfo], "tlas": round(tinfo.build_ms, 3)},
+            "extra": extra,
         }
         print(json.dumps(out), flush=True)
     ctx.close()

@@ -128,6 +128,11 @@ def config(name: str) -> SceneSpec:
         return _single("teapot", "C1", 512, 512, RT_SHADE_PRIMARY)
     if name == "C2":
         return _single("teapot", "C2", 1920, 1080, RT_SHADE_LAMBERT_SHADOW)
+    if name == "C2F":
+        # C2 with the teapot framed from outside (the reference camera sits inside the teapot body)
+        s = _single("teapot", "C2F", 1920, 1080, RT_SHADE_LAMBERT_SHADOW)
+        s.camera = ((7.0, 5.0, 9.0), (0.2, 1.3, 0.0), (0.0, 1.0, 0.0))
+        return s
     if name == "C3":
         return _single("rabbit", "C3", 1920, 1080, RT_SHADE_LAMBERT_SHADOW)
     if name == "C4":
@@ -137,7 +142,7 @@ def config(name: str) -> SceneSpec:
     raise KeyError(name)
 
 
-CONFIGS = ("REF", "C1", "C2", "C3", "C4", "C5")
+CONFIGS = ("REF", "C1", "C2", "C2F", "C3", "C4", "C5")
 
 
 def upload(ctx, spec: SceneSpec) -> List[int]:
