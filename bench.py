@@ -31,14 +31,14 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import realtimeraytracing_gradproject_amd as rt  # noqa: E402
-from realtimeraytracing_gradproject_amd import scenes  # noqa: E402
+from realtimeraytracing_gradproject_amd import distributed as D, scenes  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 L2_PEAK_GBS = 34500.0  # aggregate L2 bandwidth, 8 XCDs (MI355X_MICROARCH.md, L2 section)
 BYTES_PER_AABB_TEST = 24  # one child box (6 floats) per slab test
 BYTES_PER_TRI_TEST = 36   # v0, e1, e2 (9 floats) per Moller-Trumbore test
 BYTES_PER_PIXEL = 4       # RGBA8 write
-STRIP_ROWS = 8
+STRIP_ROWS = D.STRIP_ROWS
 
 
 def parse():
@@ -144,9 +144,9 @@ def main():
     binfo = [ctx.blas_info(b) for b in range(len(spec.meshes))]
     tinfo = ctx.tlas_info()
 
-    rows = rt.strip_rows(H, world, rank, STRIP_ROWS) if distributed else None
+    rows = D.rank_rows(H, world, rank) if distributed else None
     nrows = H if rows is None else len(rows)
-    rows_per_rank = rt.strip_rows_per_rank(H, world, STRIP_ROWS) if distributed else H
+    rows_per_rank = D.padded_rows(H, world) if distributed else H
     stream = torch.cuda.Stream()
     sp = stream.cuda_stream
     local8 = torch.zeros((rows_per_rank, W, 4), dtype=torch.uint8, device="cuda")
@@ -157,7 +157,7 @@ def main():
         ctx.dispatch(W, H, local8, None, rows=rows, stream=sp)
         if distributed:
             with torch.cuda.stream(stream):
-                dist.gather(local8, [gathered[r] for r in range(world)] if rank == 0 else None, dst=0)
+                D.gather_strips(local8, world, rank, gathered)
                 if rank == 0:
                     ctx.assemble_strips(W, H, world, STRIP_ROWS, gathered, frame, stream=sp)
 
@@ -189,7 +189,7 @@ def main():
         ev[k][1].record(stream)
         if distributed:
             with torch.cuda.stream(stream):
-                dist.gather(local8, [gathered[r] for r in range(world)] if rank == 0 else None, dst=0)
+                D.gather_strips(local8, world, rank, gathered)
                 if rank == 0:
                     ctx.assemble_strips(W, H, world, STRIP_ROWS, gathered, frame, stream=sp)
     torch.cuda.synchronize()

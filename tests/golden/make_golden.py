@@ -1,0 +1,64 @@
+"""Regenerates the committed golden fixtures in tests/golden/ (run in the dev container).
+
+camera_glm.json   glm::lookAt / glm::rotate from the reference's vendored glm, via the harness
+                  oracle/ref_glm_camera.cpp built into oracle/_ref/ (`make ref`).
+frames_small.npz  oracle frames (RGBA8 + float32) of every config at small sizes; each is first
+                  cross-checked against the independent float64 numpy restatement
+                  (oracle/np_reference.py) and the script refuses to write on disagreement.
+
+The reference itself (HLSL under DXR) cannot run here: the frames pin the oracle against drift and
+give the GPU tests a fixed target; their link to the reference is the restatement + numpy check.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+import realtimeraytracing_gradproject_amd as rt  # noqa: E402,F401
+from realtimeraytracing_gradproject_amd import scenes  # noqa: E402
+
+import oracle  # noqa: E402
+from oracle import np_reference  # noqa: E402
+
+SIZES = {"REF": (96, 54), "C1": (64, 64), "C2": (96, 54), "C2F": (96, 54), "C3": (96, 54), "C4": (96, 54),
+         "C5": (48, 27)}
+NUMPY_CHECK = {"REF", "C1", "C2", "C2F", "C3", "C4"}  # C5 (257 instances x 4 spp) is too slow in numpy
+NUMPY_TOL = 1e-4
+
+
+def camera():
+    exe = os.path.join(ROOT, "oracle", "_ref", "glm_camera")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", ROOT, "ref"], check=True)
+    out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout
+    json.loads(out)
+    with open(os.path.join(HERE, "camera_glm.json"), "w") as f:
+        f.write(out)
+
+
+def frames():
+    data = {}
+    for name, (w, h) in SIZES.items():
+        spec = scenes.config(name).with_size(w, h)
+        o8, o32, st = oracle.Scene(spec).render_spec(spec, nthreads=8)
+        if name in NUMPY_CHECK:
+            img, _ = np_reference.Scene(spec).render(spec.camera_buffer())
+            d = float(np.abs(img - o32[..., :3]).max())
+            print(f"{name}: numpy float64 vs oracle L-inf {d:.3g}")
+            if d > NUMPY_TOL:
+                raise SystemExit(f"{name}: oracle disagrees with the numpy restatement ({d})")
+        data[f"{name}_rgba8"] = o8
+        data[f"{name}_rgba32f"] = o32
+        data[f"{name}_stats"] = st
+    np.savez_compressed(os.path.join(HERE, "frames_small.npz"), **data)
+
+
+if __name__ == "__main__":
+    camera()
+    frames()
