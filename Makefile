@@ -23,7 +23,7 @@ ORACLE    := oracle/liboracle.so
 
 HDRS      := include/rt_api.h $(SRC)/rt_device.hpp $(SRC)/rt_internal.hpp
 
-all: $(LIB) $(ORACLE)
+all: $(LIB) $(APP) $(ORACLE)
 
 $(BUILD)/%.o: $(SRC)/%.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
