@@ -87,9 +87,9 @@ typedef struct {
 /* BVH summary returned by rt_blas_info / rt_tlas_info. */
 typedef struct {
   uint32_t prim_count;   /* triangles (BLAS) or instances (TLAS) */
-  uint32_t node_count;   /* internal child-pair nodes (max(prim_count-1,1)) */
-  uint32_t depth;        /* max root-to-leaf edges */
-  uint32_t reserved;
+  uint32_t node_count;   /* 4-wide nodes (BFS order, root 0) */
+  uint32_t depth;        /* levels of 4-wide nodes */
+  uint32_t max_stack;    /* worst-case traversal-stack entries a path through this tree needs */
   float bounds_lo[3];
   float bounds_hi[3];
   double build_ms;       /* device time of the last build (HIP events) */
@@ -99,7 +99,7 @@ typedef struct {
 enum {
   RT_STAT_PRIMARY_RAYS = 0,
   RT_STAT_SHADOW_RAYS = 1,
-  RT_STAT_AABB_TESTS = 2,  /* child-box slab tests (2 per node visit) */
+  RT_STAT_AABB_TESTS = 2,  /* child-box slab tests (one per valid child of a visited node) */
   RT_STAT_TRI_TESTS = 3,   /* Moller-Trumbore tests */
   RT_STAT_INSTANCE_ENTRIES = 4,
   RT_STAT_STACK_OVERFLOWS = 5,
@@ -139,7 +139,7 @@ rt_status rt_blas_build(rt_ctx_t ctx, const void* vtx, uint32_t vcount, uint32_t
 rt_status rt_blas_rebuild(rt_ctx_t ctx, rt_blas_t blas, const void* vtx, uint32_t vcount,
                           uint32_t stride, const uint32_t* idx, uint32_t icount);
 rt_status rt_blas_info(rt_ctx_t ctx, rt_blas_t blas, rt_bvh_info* out);
-/* Copies the BLAS to host memory for parity checks: nodes (node_count x 64 B child-pair nodes),
+/* Copies the BLAS to host memory for parity checks: nodes (node_count x 128 B 4-wide nodes, BFS order),
  * tris (prim_count x 48 B: v0.xyz,prim | e1.xyz,0 | e2.xyz,0 in leaf order). Either may be NULL. */
 rt_status rt_blas_export(rt_ctx_t ctx, rt_blas_t blas, void* nodes, size_t nodes_bytes, void* tris,
                          size_t tris_bytes);
@@ -152,7 +152,7 @@ rt_status rt_blas_export(rt_ctx_t ctx, rt_blas_t blas, void* nodes, size_t nodes
  * Synchronous. */
 rt_status rt_tlas_build(rt_ctx_t ctx, const rt_instance* instances, uint32_t n, int update_only);
 rt_status rt_tlas_info(rt_ctx_t ctx, rt_bvh_info* out);
-/* nodes: node_count x 64 B; leaf refs are ~instance_index. */
+/* nodes: node_count x 128 B 4-wide nodes; leaf refs are ~instance_index. */
 rt_status rt_tlas_export(rt_ctx_t ctx, void* nodes, size_t nodes_bytes);
 
 /* ------------------------------------------------------------------------------------------ */

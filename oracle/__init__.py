@@ -183,27 +183,27 @@ class Scene:
         self.set_instances([(self.blas_ids[m], x, iid, hg) for (m, x, iid, hg) in spec.instances])
 
     def blas_info(self, b):
-        out = np.zeros(3, np.uint32)
+        out = np.zeros(4, np.uint32)
         lib.oracle_blas_info(self._h, b, out.ctypes.data_as(_P))
         return out
 
     def tlas_info(self):
-        out = np.zeros(3, np.uint32)
+        out = np.zeros(4, np.uint32)
         lib.oracle_tlas_info(self._h, out.ctypes.data_as(_P))
         return out
 
     def export_blas(self, b):
-        prims, nn, _ = self.blas_info(b)
-        nodes = np.zeros(nn * 16, np.uint32)
+        prims, nn, _, _ = self.blas_info(b)
+        nodes = np.zeros(nn * 32, np.uint32)  # 128-B 4-wide nodes
         tris = np.zeros(prims * 12, np.uint32)
         lib.oracle_export_blas(self._h, b, nodes.ctypes.data_as(_P), tris.ctypes.data_as(_P))
-        return nodes.reshape(-1, 16), tris.reshape(-1, 12)
+        return nodes.reshape(-1, 32), tris.reshape(-1, 12)
 
     def export_tlas(self):
-        _, nn, _ = self.tlas_info()
-        nodes = np.zeros(nn * 16, np.uint32)
+        _, nn, _, _ = self.tlas_info()
+        nodes = np.zeros(nn * 32, np.uint32)
         lib.oracle_export_tlas(self._h, nodes.ctypes.data_as(_P))
-        return nodes.reshape(-1, 16)
+        return nodes.reshape(-1, 32)
 
     def render(self, cb, lights, material, mode, spp, W, H, rows: Optional[np.ndarray] = None, nthreads=1,
                brute_force=False, want_float=True):

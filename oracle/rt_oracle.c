@@ -202,7 +202,14 @@ typedef struct {
   float lo0[3], hi0[3], lo1[3], hi1[3];
   int32_t c0, c1;
   uint32_t pad0, pad1;
-} onode;
+} onode; /* binary LBVH node: build intermediate */
+/* traversal node: 4-wide, BFS order, SoA child boxes (== Bvh4Node of the device) */
+#define O_EMPTY ((int32_t)(INT32_MIN + 1))
+typedef struct {
+  float lox[4], hix[4], loy[4], hiy[4], loz[4], hiz[4];
+  int32_t child[4];
+  uint32_t count, pad[3];
+} o4node;
 typedef struct {
   float v0[3]; uint32_t prim;
   float e1[3]; uint32_t pad1;
@@ -210,11 +217,11 @@ typedef struct {
 } otri;
 
 typedef struct {
-  onode* nodes;
+  o4node* nodes;
   otri* tris; /* leaf order */
   float* vtx; /* {pos, normal} */
   uint32_t* idx; /* NULL for non-indexed */
-  uint32_t ntri, nnodes, depth, nv;
+  uint32_t ntri, nnodes, depth, nv, max_stack;
   float bounds[6];
 } oblas;
 
@@ -228,8 +235,8 @@ struct oracle_scene {
   int nblas, cblas;
   oinst* inst;
   uint32_t ninst;
-  onode* tlas;
-  uint32_t tlas_nodes, tlas_depth;
+  o4node* tlas;
+  uint32_t tlas_nodes, tlas_depth, tlas_max_stack;
 };
 
 static uint32_t expand10(uint32_t x) {
@@ -254,7 +261,71 @@ static void box_of(int c, const float* nbox, const float* primbox, const uint32_
 }
 
 /* builds nodes over n prim boxes; sorted receives leaf order; returns depth */
-static uint32_t lbvh(const float* primbox, uint32_t n, onode* nodes, uint32_t* sorted, int leaf_ref_is_prim) {
+/* collapse every other level of the binary tree into 4-wide nodes, BFS order (k_collapse) */
+static uint32_t collapse(const onode* bin, uint32_t nbin, o4node* out, uint32_t* count, uint32_t* max_stack) {
+  int* q = (int*)malloc((size_t)nbin * sizeof(int) + sizeof(int));
+  int* ps = (int*)calloc((size_t)nbin + 1, sizeof(int)); /* siblings left on the stack above a node */
+  int best = 0;
+  int head = 0, tail = 1, level_end = 1;
+  uint32_t depth = 0;
+  q[0] = 0;
+  while (head < level_end) {
+    ++depth;
+    for (; head < level_end; ++head) {
+      const onode* b = &bin[q[head]];
+      int ref[4];
+      float box[4][6];
+      int cnt = 0;
+      for (int k = 0; k < 2; ++k) {
+        int c = k ? b->c1 : b->c0;
+        const float* lo = k ? b->lo1 : b->lo0;
+        const float* hi = k ? b->hi1 : b->hi0;
+        if (c < 0) {
+          ref[cnt] = c;
+          for (int a = 0; a < 3; ++a) { box[cnt][a] = lo[a]; box[cnt][3 + a] = hi[a]; }
+          ++cnt;
+        } else {
+          const onode* g = &bin[c];
+          for (int qq = 0; qq < 2; ++qq) {
+            ref[cnt] = qq ? g->c1 : g->c0;
+            for (int a = 0; a < 3; ++a) {
+              box[cnt][a] = qq ? g->lo1[a] : g->lo0[a];
+              box[cnt][3 + a] = qq ? g->hi1[a] : g->hi0[a];
+            }
+            ++cnt;
+          }
+        }
+      }
+      o4node nd;
+      memset(&nd, 0, sizeof(nd));
+      for (int j = 0; j < 4; ++j) {
+        int32_t r = O_EMPTY;
+        if (j < cnt) {
+          nd.lox[j] = box[j][0]; nd.loy[j] = box[j][1]; nd.loz[j] = box[j][2];
+          nd.hix[j] = box[j][3]; nd.hiy[j] = box[j][4]; nd.hiz[j] = box[j][5];
+          if (ref[j] >= 0) { q[tail] = ref[j]; r = tail; ps[tail] = ps[head] + cnt - 1; ++tail; }
+          else r = ref[j];
+        }
+        nd.child[j] = r;
+      }
+      nd.count = (uint32_t)cnt;
+      if (ps[head] + cnt - 1 > best) best = ps[head] + cnt - 1;
+      out[head] = nd;
+    }
+    level_end = tail;
+  }
+  *count = (uint32_t)tail;
+  *max_stack = (uint32_t)best;
+  free(ps);
+  free(q);
+  return depth;
+}
+
+/* LBVH over n prim boxes -> 4-wide nodes (caller frees *out); returns levels */
+static uint32_t lbvh(const float* primbox, uint32_t n, o4node** out4, uint32_t* count4, uint32_t* max_stack,
+                     uint32_t* sorted, int leaf_ref_is_prim) {
+  const uint32_t nbin = n > 1 ? n - 1 : 1;
+  onode* nodes = (onode*)malloc((size_t)nbin * sizeof(onode));
   float cb[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
   for (uint32_t i = 0; i < n; ++i)
     for (int k = 0; k < 3; ++k) {
@@ -379,7 +450,11 @@ static uint32_t lbvh(const float* primbox, uint32_t n, onode* nodes, uint32_t* s
     free(order); free(stack); free(child); free(pint); free(pleaf); free(nbox);
   }
   free(keys); free(k2); free(v2);
-  return depth;
+  (void)depth;
+  *out4 = (o4node*)malloc((size_t)nbin * sizeof(o4node));
+  uint32_t levels = collapse(nodes, nbin, *out4, count4, max_stack);
+  free(nodes);
+  return levels;
 }
 
 oracle_scene* oracle_scene_create(void) { return (oracle_scene*)calloc(1, sizeof(oracle_scene)); }
@@ -415,7 +490,6 @@ int oracle_add_blas(oracle_scene* s, const float* vtx6, uint32_t nv, const uint3
   if (idx) { b->idx = (uint32_t*)malloc((size_t)icount * 4); memcpy(b->idx, idx, (size_t)icount * 4); }
   b->nv = nv;
   b->ntri = ntri;
-  b->nnodes = ntri > 1 ? ntri - 1 : 1;
   float* box = (float*)malloc((size_t)ntri * 24);
   otri* un = (otri*)malloc((size_t)ntri * sizeof(otri));
   for (uint32_t p = 0; p < ntri; ++p) {
@@ -431,8 +505,7 @@ int oracle_add_blas(oracle_scene* s, const float* vtx6, uint32_t nv, const uint3
     un[p] = t;
   }
   uint32_t* sorted = (uint32_t*)malloc((size_t)ntri * 4);
-  b->nodes = (onode*)malloc((size_t)b->nnodes * sizeof(onode));
-  b->depth = lbvh(box, ntri, b->nodes, sorted, 0);
+  b->depth = lbvh(box, ntri, &b->nodes, &b->nnodes, &b->max_stack, sorted, 0);
   b->tris = (otri*)malloc((size_t)ntri * sizeof(otri));
   for (uint32_t i = 0; i < ntri; ++i) b->tris[i] = un[sorted[i]];
   for (int k = 0; k < 3; ++k) { b->bounds[k] = INFINITY; b->bounds[3 + k] = -INFINITY; }
@@ -507,33 +580,31 @@ int oracle_set_instances(oracle_scene* s, const oracle_instance* in, uint32_t n)
     }
     for (int k = 0; k < 3; ++k) { box[i * 6 + k] = lo[k] + 0.0f; box[i * 6 + 3 + k] = hi[k] + 0.0f; }
   }
-  s->tlas_nodes = n > 1 ? n - 1 : 1;
-  s->tlas = (onode*)malloc((size_t)s->tlas_nodes * sizeof(onode));
   uint32_t* sorted = (uint32_t*)malloc((size_t)n * 4);
-  s->tlas_depth = lbvh(box, n, s->tlas, sorted, 1);
+  s->tlas_depth = lbvh(box, n, &s->tlas, &s->tlas_nodes, &s->tlas_max_stack, sorted, 1);
   free(sorted); free(box);
   return 0;
 }
 
-int oracle_blas_info(const oracle_scene* s, int b, uint32_t out[3]) {
+int oracle_blas_info(const oracle_scene* s, int b, uint32_t out[4]) {
   if (b < 0 || b >= s->nblas) return -1;
-  out[0] = s->blas[b].ntri; out[1] = s->blas[b].nnodes; out[2] = s->blas[b].depth;
+  out[0] = s->blas[b].ntri; out[1] = s->blas[b].nnodes; out[2] = s->blas[b].depth; out[3] = s->blas[b].max_stack;
   return 0;
 }
-int oracle_tlas_info(const oracle_scene* s, uint32_t out[3]) {
+int oracle_tlas_info(const oracle_scene* s, uint32_t out[4]) {
   if (!s->tlas) return -1;
-  out[0] = s->ninst; out[1] = s->tlas_nodes; out[2] = s->tlas_depth;
+  out[0] = s->ninst; out[1] = s->tlas_nodes; out[2] = s->tlas_depth; out[3] = s->tlas_max_stack;
   return 0;
 }
 int oracle_export_blas(const oracle_scene* s, int b, void* nodes, void* tris) {
   if (b < 0 || b >= s->nblas) return -1;
-  if (nodes) memcpy(nodes, s->blas[b].nodes, (size_t)s->blas[b].nnodes * sizeof(onode));
+  if (nodes) memcpy(nodes, s->blas[b].nodes, (size_t)s->blas[b].nnodes * sizeof(o4node));
   if (tris) memcpy(tris, s->blas[b].tris, (size_t)s->blas[b].ntri * sizeof(otri));
   return 0;
 }
 int oracle_export_tlas(const oracle_scene* s, void* nodes) {
   if (!s->tlas) return -1;
-  memcpy(nodes, s->tlas, (size_t)s->tlas_nodes * sizeof(onode));
+  memcpy(nodes, s->tlas, (size_t)s->tlas_nodes * sizeof(o4node));
   return 0;
 }
 
@@ -545,14 +616,24 @@ typedef struct { float t, u, v; uint32_t inst, prim; } ohit;
 
 static inline float sinv(float d) { return fabsf(d) > 1e-20f ? 1.0f / d : (d < 0.0f ? -1e20f : 1e20f); }
 
-static inline int oslab(const float* lo, const float* hi, vec3 invd, vec3 noinv, float tmin, float tbest, float* tnear) {
-  float tlx = fmaf(lo[0], invd.x, noinv.x), thx = fmaf(hi[0], invd.x, noinv.x);
-  float tly = fmaf(lo[1], invd.y, noinv.y), thy = fmaf(hi[1], invd.y, noinv.y);
-  float tlz = fmaf(lo[2], invd.z, noinv.z), thz = fmaf(hi[2], invd.z, noinv.z);
-  float tn = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), tmin));
-  float tf = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tbest));
-  *tnear = tn;
-  return tn <= tf * 1.0000004f;
+/* slab tests of the 4 children of a node against [tmin, tbest]; +inf = missed or empty */
+static inline void oslab4(const o4node* nd, vec3 invd, vec3 noinv, float tmin, float tbest, float tn[4]) {
+  for (int k = 0; k < 4; ++k) {
+    float tlx = fmaf(nd->lox[k], invd.x, noinv.x), thx = fmaf(nd->hix[k], invd.x, noinv.x);
+    float tly = fmaf(nd->loy[k], invd.y, noinv.y), thy = fmaf(nd->hiy[k], invd.y, noinv.y);
+    float tlz = fmaf(nd->loz[k], invd.z, noinv.z), thz = fmaf(nd->hiz[k], invd.z, noinv.z);
+    float n = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), tmin));
+    float f = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tbest));
+    tn[k] = (nd->child[k] != O_EMPTY && n <= f * 1.0000004f) ? n : INFINITY;
+  }
+}
+
+/* nearest-first order: comparator network (0,1)(2,3)(0,2)(1,3)(1,2), swap only when strictly nearer */
+static inline void ocswap(float* t, int32_t* r, int a, int b) {
+  if (t[b] < t[a]) { float tt = t[a]; t[a] = t[b]; t[b] = tt; int32_t rr = r[a]; r[a] = r[b]; r[b] = rr; }
+}
+static inline void osort4(float* t, int32_t* r) {
+  ocswap(t, r, 0, 1); ocswap(t, r, 2, 3); ocswap(t, r, 0, 2); ocswap(t, r, 1, 3); ocswap(t, r, 1, 2);
 }
 
 /* Moller-Trumbore (the ray/triangle test DXR performs in hardware; formula pinned here) */
@@ -578,51 +659,54 @@ static inline int better(float t, uint32_t inst, uint32_t prim, const ohit* h) {
 
 #define SENT INT32_MIN
 
+#define OPUSH(X) do { if (sp < cap) stack[sp++] = (X); else st->v[5]++; } while (0)
+
 static int otrace(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax, int any, ohit* h, ostats* st) {
-  int stack[512];
-  int cap = (int)(s->tlas_depth + 2);
+  int stack[256];
   uint32_t maxb = 0;
-  for (int b = 0; b < s->nblas; ++b) if (s->blas[b].depth > maxb) maxb = s->blas[b].depth;
-  cap += (int)maxb;
-  if (cap > 512) cap = 512;
+  for (int b = 0; b < s->nblas; ++b) if (s->blas[b].max_stack > maxb) maxb = s->blas[b].max_stack;
+  int cap = (int)(s->tlas_max_stack + 1 + maxb); /* same exact bound as the device (rt_api.cpp) */
+  if (cap > 256) cap = 256;
   vec3 winvd = mk(sinv(d.x), sinv(d.y), sinv(d.z));
   vec3 wno = vneg(vmul(o, winvd));
   vec3 ro = o, rd = d, rinvd = winvd, rno = wno;
-  const onode* nodes = s->tlas;
+  const o4node* nodes = s->tlas;
   const otri* tris = NULL;
   uint32_t cur = 0;
   int in_blas = 0, found = 0, sp = 0, ref = 0;
   h->t = tmax; h->inst = 0xffffffffu; h->prim = 0xffffffffu; h->u = h->v = 0.0f;
   for (;;) {
     if (ref >= 0) {
-      const onode* nd = nodes + ref;
-      float tn0, tn1;
-      int h0 = oslab(nd->lo0, nd->hi0, rinvd, rno, tmin, h->t, &tn0);
-      int h1 = oslab(nd->lo1, nd->hi1, rinvd, rno, tmin, h->t, &tn1);
-      st->v[2] += 2;
-      if (h0 && h1) {
-        int sw = tn1 < tn0;
-        int nearc = sw ? nd->c1 : nd->c0, farc = sw ? nd->c0 : nd->c1;
-        if (sp < cap) stack[sp++] = farc; else st->v[5]++;
-        ref = nearc;
+      const o4node* nd = nodes + ref;
+      float tn[4];
+      int32_t r[4] = {nd->child[0], nd->child[1], nd->child[2], nd->child[3]};
+      oslab4(nd, rinvd, rno, tmin, h->t, tn);
+      for (int k = 0; k < 4; ++k) st->v[2] += r[k] != O_EMPTY;
+      osort4(tn, r);
+      if (tn[0] != INFINITY) {
+        if (tn[3] != INFINITY) OPUSH(r[3]);
+        if (tn[2] != INFINITY) OPUSH(r[2]);
+        if (tn[1] != INFINITY) OPUSH(r[1]);
+        ref = r[0];
         continue;
       }
-      if (h0) { ref = nd->c0; continue; }
-      if (h1) { ref = nd->c1; continue; }
     } else if (!in_blas) {
       cur = (uint32_t)(~ref);
       const oinst* ir = &s->inst[cur];
-      ro = xpoint(ir->w2o, o);
-      rd = xdir(ir->w2o, d);
-      rinvd = mk(sinv(rd.x), sinv(rd.y), sinv(rd.z));
-      rno = vneg(vmul(ro, rinvd));
-      nodes = s->blas[ir->blas].nodes;
-      tris = s->blas[ir->blas].tris;
-      in_blas = 1;
       st->v[4]++;
-      if (sp < cap) { stack[sp++] = SENT; ref = 0; continue; }
+      if (sp < cap) {
+        stack[sp++] = SENT;
+        ro = xpoint(ir->w2o, o);
+        rd = xdir(ir->w2o, d);
+        rinvd = mk(sinv(rd.x), sinv(rd.y), sinv(rd.z));
+        rno = vneg(vmul(ro, rinvd));
+        nodes = s->blas[ir->blas].nodes;
+        tris = s->blas[ir->blas].tris;
+        in_blas = 1;
+        ref = 0;
+        continue;
+      }
       st->v[5]++;
-      in_blas = 0; nodes = s->tlas; ro = o; rd = d; rinvd = winvd; rno = wno;
     } else {
       const otri* tr = tris + (~ref);
       float t, u, v;

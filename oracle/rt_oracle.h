@@ -51,9 +51,9 @@ void oracle_scene_destroy(oracle_scene* s);
 /* returns BLAS id >= 0, or < 0 on error. vtx6: {pos, normal} per vertex. idx NULL = non-indexed. */
 int oracle_add_blas(oracle_scene* s, const float* vtx6, uint32_t nv, const uint32_t* idx, uint32_t icount);
 int oracle_set_instances(oracle_scene* s, const oracle_instance* inst, uint32_t n);
-/* info: out[0] prims, out[1] nodes, out[2] depth */
-int oracle_blas_info(const oracle_scene* s, int blas, uint32_t out[3]);
-int oracle_tlas_info(const oracle_scene* s, uint32_t out[3]);
+/* info: out[0] prims, out[1] nodes, out[2] levels, out[3] worst-case traversal stack */
+int oracle_blas_info(const oracle_scene* s, int blas, uint32_t out[4]);
+int oracle_tlas_info(const oracle_scene* s, uint32_t out[4]);
 int oracle_export_blas(const oracle_scene* s, int blas, void* nodes, void* tris);
 int oracle_export_tlas(const oracle_scene* s, void* nodes);
 

@@ -58,7 +58,7 @@ class rt_material(ctypes.Structure):
 
 class rt_bvh_info(ctypes.Structure):
     _fields_ = [("prim_count", ctypes.c_uint32), ("node_count", ctypes.c_uint32),
-                ("depth", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("depth", ctypes.c_uint32), ("max_stack", ctypes.c_uint32),
                 ("bounds_lo", ctypes.c_float * 3), ("bounds_hi", ctypes.c_float * 3),
                 ("build_ms", ctypes.c_double)]
 
@@ -107,12 +107,13 @@ SIGNATURES = [
 ]
 
 
-def _load() -> ctypes.CDLL:
-    if not os.path.exists(LIB_PATH):
+def _load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Loads the C-ABI library (a variant build may be given for A/B timing in one process)."""
+    if not os.path.exists(path):
         raise ImportError(
-            f"{LIB_PATH} is missing: build the HIP library first "
+            f"{path} is missing: build the HIP library first "
             "(python -c 'import __graft_entry__ as g; g.build()' or `make`). There is no CPU fallback.")
-    lib = ctypes.CDLL(LIB_PATH)
+    lib = ctypes.CDLL(path)
     for name, res, args in SIGNATURES:
         fn = getattr(lib, name)
         fn.restype = res
@@ -254,17 +255,18 @@ def _ptr(x) -> Optional[int]:
 class Context:
     """One rt_ctx (one HIP device, one host thread)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, library: Optional[ctypes.CDLL] = None):
+        self._lib = library if library is not None else lib
         h = _P()
-        st = lib.rt_create(device, ctypes.byref(h))
+        st = self._lib.rt_create(device, ctypes.byref(h))
         if st != RT_OK:
             raise RtError(st, f"rt_create(device={device})")
         self._h = h
         self.device = device
 
     def close(self):
-        if getattr(self, "_h", None) and lib is not None:
-            lib.rt_destroy(self._h)
+        if getattr(self, "_h", None) and getattr(self, "_lib", None) is not None:
+            self._lib.rt_destroy(self._h)
             self._h = None
 
     def __del__(self):
@@ -278,7 +280,7 @@ class Context:
 
     def _check(self, st: int, what: str):
         if st != RT_OK:
-            raise RtError(st, f"{what}: {lib.rt_last_error(self._h).decode()}")
+            raise RtError(st, f"{what}: {self._lib.rt_last_error(self._h).decode()}")
 
     # acceleration structures ------------------------------------------------------------------
     def blas_build(self, vertices: np.ndarray, indices: Optional[np.ndarray] = None) -> int:
@@ -287,10 +289,10 @@ class Context:
         nv = v.shape[0] if v.ndim == 2 else v.size // 6
         out = _U32()
         if indices is None:
-            st = lib.rt_blas_build(self._h, v.ctypes.data_as(_P), nv, stride, None, 0, ctypes.byref(out))
+            st = self._lib.rt_blas_build(self._h, v.ctypes.data_as(_P), nv, stride, None, 0, ctypes.byref(out))
         else:
             i = np.ascontiguousarray(indices, dtype=np.uint32)
-            st = lib.rt_blas_build(self._h, v.ctypes.data_as(_P), nv, stride, i.ctypes.data_as(_P), i.size,
+            st = self._lib.rt_blas_build(self._h, v.ctypes.data_as(_P), nv, stride, i.ctypes.data_as(_P), i.size,
                                    ctypes.byref(out))
         self._check(st, "rt_blas_build")
         return out.value
@@ -299,25 +301,25 @@ class Context:
         v = np.ascontiguousarray(vertices, dtype=np.float32)
         stride = v.shape[1] * 4
         if indices is None:
-            st = lib.rt_blas_rebuild(self._h, blas, v.ctypes.data_as(_P), v.shape[0], stride, None, 0)
+            st = self._lib.rt_blas_rebuild(self._h, blas, v.ctypes.data_as(_P), v.shape[0], stride, None, 0)
         else:
             i = np.ascontiguousarray(indices, dtype=np.uint32)
-            st = lib.rt_blas_rebuild(self._h, blas, v.ctypes.data_as(_P), v.shape[0], stride,
+            st = self._lib.rt_blas_rebuild(self._h, blas, v.ctypes.data_as(_P), v.shape[0], stride,
                                      i.ctypes.data_as(_P), i.size)
         self._check(st, "rt_blas_rebuild")
 
     def blas_info(self, blas: int) -> rt_bvh_info:
         info = rt_bvh_info()
-        self._check(lib.rt_blas_info(self._h, blas, ctypes.byref(info)), "rt_blas_info")
+        self._check(self._lib.rt_blas_info(self._h, blas, ctypes.byref(info)), "rt_blas_info")
         return info
 
     def blas_export(self, blas: int):
         info = self.blas_info(blas)
-        nodes = np.zeros(info.node_count * 16, np.uint32)
+        nodes = np.zeros(info.node_count * 32, np.uint32)  # 128-B 4-wide nodes
         tris = np.zeros(info.prim_count * 12, np.uint32)
-        self._check(lib.rt_blas_export(self._h, blas, nodes.ctypes.data_as(_P), nodes.nbytes,
-                                       tris.ctypes.data_as(_P), tris.nbytes), "rt_blas_export")
-        return nodes.reshape(-1, 16), tris.reshape(-1, 12)
+        self._check(self._lib.rt_blas_export(self._h, blas, nodes.ctypes.data_as(_P), nodes.nbytes,
+                                             tris.ctypes.data_as(_P), tris.nbytes), "rt_blas_export")
+        return nodes.reshape(-1, 32), tris.reshape(-1, 12)
 
     def tlas_build(self, instances: Sequence[tuple], update_only: bool = False):
         """instances: (blas, xform3x4 (12 floats), instance_id, hit_group) tuples."""
@@ -327,23 +329,23 @@ class Context:
             arr[k].xform3x4_rowmajor[:] = [float(v) for v in np.asarray(x, np.float32).ravel()]
             arr[k].instance_id = iid
             arr[k].hit_group = hg
-        self._check(lib.rt_tlas_build(self._h, arr, len(instances), 1 if update_only else 0), "rt_tlas_build")
+        self._check(self._lib.rt_tlas_build(self._h, arr, len(instances), 1 if update_only else 0), "rt_tlas_build")
 
     def tlas_info(self) -> rt_bvh_info:
         info = rt_bvh_info()
-        self._check(lib.rt_tlas_info(self._h, ctypes.byref(info)), "rt_tlas_info")
+        self._check(self._lib.rt_tlas_info(self._h, ctypes.byref(info)), "rt_tlas_info")
         return info
 
     def tlas_export(self) -> np.ndarray:
         info = self.tlas_info()
-        nodes = np.zeros(info.node_count * 16, np.uint32)
-        self._check(lib.rt_tlas_export(self._h, nodes.ctypes.data_as(_P), nodes.nbytes), "rt_tlas_export")
-        return nodes.reshape(-1, 16)
+        nodes = np.zeros(info.node_count * 32, np.uint32)
+        self._check(self._lib.rt_tlas_export(self._h, nodes.ctypes.data_as(_P), nodes.nbytes), "rt_tlas_export")
+        return nodes.reshape(-1, 32)
 
     # frame state ------------------------------------------------------------------------------
     def set_camera(self, cb: np.ndarray):
         c = _f32(cb, 64)
-        self._check(lib.rt_set_camera(self._h, _fptr(c)), "rt_set_camera")
+        self._check(self._lib.rt_set_camera(self._h, _fptr(c)), "rt_set_camera")
 
     def set_shading(self, lights: Iterable, material, mode: int, spp: int = 1):
         lights = list(lights)
@@ -355,21 +357,21 @@ class Context:
         m = rt_material()
         m.albedo[:] = [float(v) for v in material[0:3]]
         m.roughness, m.metallic, m.reflectivity = (float(v) for v in material[3:6])
-        self._check(lib.rt_set_shading(self._h, arr, len(lights), ctypes.byref(m), mode, spp), "rt_set_shading")
+        self._check(self._lib.rt_set_shading(self._h, arr, len(lights), ctypes.byref(m), mode, spp), "rt_set_shading")
 
     def set_schedule(self, schedule: int):
-        self._check(lib.rt_set_schedule(self._h, schedule), "rt_set_schedule")
+        self._check(self._lib.rt_set_schedule(self._h, schedule), "rt_set_schedule")
 
     def set_stats(self, on: bool):
-        self._check(lib.rt_set_stats(self._h, 1 if on else 0), "rt_set_stats")
+        self._check(self._lib.rt_set_stats(self._h, 1 if on else 0), "rt_set_stats")
 
     def stats(self) -> dict:
         out = (ctypes.c_uint64 * 8)()
-        self._check(lib.rt_stats(self._h, out), "rt_stats")
+        self._check(self._lib.rt_stats(self._h, out), "rt_stats")
         return dict(zip(STAT_NAMES, list(out)))
 
     def stats_reset(self):
-        self._check(lib.rt_stats_reset(self._h), "rt_stats_reset")
+        self._check(self._lib.rt_stats_reset(self._h), "rt_stats_reset")
 
     # launches ---------------------------------------------------------------------------------
     def dispatch(self, width: int, height: int, rgba8, rgba32f=None, rows: Optional[np.ndarray] = None,
@@ -379,14 +381,14 @@ class Context:
             rp, nr = r.ctypes.data_as(_P), r.size
         else:
             rp, nr = None, height
-        self._check(lib.rt_dispatch_rays(self._h, width, height, rp, nr, _ptr(rgba8), _ptr(rgba32f), stream),
+        self._check(self._lib.rt_dispatch_rays(self._h, width, height, rp, nr, _ptr(rgba8), _ptr(rgba32f), stream),
                     "rt_dispatch_rays")
 
     def trace_rays(self, rays, n: int, any_hit: bool, hits, uv=None, stream: Optional[int] = None):
-        self._check(lib.rt_trace_rays(self._h, _ptr(rays), n, 1 if any_hit else 0, _ptr(hits), _ptr(uv), stream),
+        self._check(self._lib.rt_trace_rays(self._h, _ptr(rays), n, 1 if any_hit else 0, _ptr(hits), _ptr(uv), stream),
                     "rt_trace_rays")
 
     def assemble_strips(self, width: int, height: int, nranks: int, strip_rows_: int, gathered, out,
                         stream: Optional[int] = None):
-        self._check(lib.rt_assemble_strips(self._h, width, height, nranks, strip_rows_, _ptr(gathered), _ptr(out),
+        self._check(self._lib.rt_assemble_strips(self._h, width, height, nranks, strip_rows_, _ptr(gathered), _ptr(out),
                                            stream), "rt_assemble_strips")

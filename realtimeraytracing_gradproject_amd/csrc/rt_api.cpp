@@ -14,11 +14,11 @@
 namespace {
 
 struct DeviceBlas {
-  rt::BvhNode* nodes = nullptr;
+  rt::Bvh4Node* nodes = nullptr;
   rt::TriRec* tris = nullptr;
   float* vtx = nullptr;
   uint32_t* idx = nullptr;
-  uint32_t ntri = 0, nnodes = 0, depth = 0, nvtx = 0;
+  uint32_t ntri = 0, nnodes = 0, depth = 0, nvtx = 0, max_stack = 0;
   float bounds[6] = {0, 0, 0, 0, 0, 0};
   double build_ms = 0.0;
   void release() {
@@ -41,10 +41,10 @@ struct rt_ctx {
   std::string err;
   std::vector<DeviceBlas> blas;
   // TLAS
-  rt::BvhNode* tlas_nodes = nullptr;
+  rt::Bvh4Node* tlas_nodes = nullptr;
   rt::InstanceRec* inst = nullptr;
   uint32_t* tlas_sorted = nullptr;
-  uint32_t ninst = 0, tlas_nodes_n = 0, tlas_depth = 0;
+  uint32_t ninst = 0, tlas_nodes_n = 0, tlas_depth = 0, tlas_max_stack = 0;
   float tlas_bounds[6] = {0, 0, 0, 0, 0, 0};
   double tlas_ms = 0.0;
   std::vector<rt_instance> inst_host;
@@ -60,6 +60,9 @@ struct rt_ctx {
   size_t rows_cap = 0;
   std::vector<uint32_t> rows_host;
   rt::WavefrontBuffers wf;
+  // traversal-stack overflow area in HBM for lanes whose path outgrows the LDS part
+  int* d_ovf = nullptr;
+  size_t ovf_cap = 0;
 };
 
 namespace {
@@ -163,14 +166,16 @@ rt_status upload_blas(rt_ctx* c, DeviceBlas& b, const void* vtx, uint32_t vcount
   rt::TriRec* unsorted = nullptr;
   float* primbox = nullptr;
   uint32_t* sorted = nullptr;
-  HIPCHK(c, hipMalloc(&b.nodes, (size_t)nn * sizeof(rt::BvhNode)), "hipMalloc(nodes)");
+  HIPCHK(c, hipMalloc(&b.nodes, (size_t)nn * sizeof(rt::Bvh4Node)), "hipMalloc(nodes)");
   HIPCHK(c, hipMalloc(&b.tris, (size_t)ntri * sizeof(rt::TriRec)), "hipMalloc(tris)");
   HIPCHK(c, hipMalloc(&unsorted, (size_t)ntri * sizeof(rt::TriRec)), "hipMalloc(scratch)");
   HIPCHK(c, hipMalloc(&primbox, (size_t)ntri * 24), "hipMalloc(scratch)");
   HIPCHK(c, hipMalloc(&sorted, (size_t)ntri * 4), "hipMalloc(scratch)");
   hipError_t e = rt::blas_prepare(b.vtx, b.idx, ntri, unsorted, primbox, s);
   float ms = 0.0f;
-  if (e == hipSuccess) e = rt::lbvh_build(primbox, ntri, b.nodes, sorted, false, &b.depth, b.bounds, &ms, s);
+  uint32_t nnodes4 = 0;
+  if (e == hipSuccess)
+    e = rt::lbvh_build(primbox, ntri, b.nodes, sorted, false, &nnodes4, &b.depth, &b.max_stack, b.bounds, &ms, s);
   if (e == hipSuccess) e = rt::blas_reorder(unsorted, sorted, ntri, b.tris, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   (void)hipFree(unsorted);
@@ -178,7 +183,7 @@ rt_status upload_blas(rt_ctx* c, DeviceBlas& b, const void* vtx, uint32_t vcount
   (void)hipFree(sorted);
   if (e != hipSuccess) return hip_fail(c, e, "BLAS build");
   b.ntri = ntri;
-  b.nnodes = nn;
+  b.nnodes = nnodes4;
   b.nvtx = vcount;
   b.build_ms = ms;
   return RT_OK;
@@ -241,6 +246,7 @@ rt_status rt_destroy(rt_ctx_t c) {
   if (c->d_stats) (void)hipFree(c->d_stats);
   if (c->d_rows) (void)hipFree(c->d_rows);
   if (c->wf.surf) (void)hipFree(c->wf.surf);
+  if (c->d_ovf) (void)hipFree(c->d_ovf);
   if (c->wf.shadow_bits) (void)hipFree(c->wf.shadow_bits);
   if (c->wf.queue) (void)hipFree(c->wf.queue);
   if (c->wf.queue_count) (void)hipFree(c->wf.queue_count);
@@ -286,7 +292,7 @@ rt_status rt_blas_info(rt_ctx_t c, rt_blas_t id, rt_bvh_info* out) {
   out->prim_count = b.ntri;
   out->node_count = b.nnodes;
   out->depth = b.depth;
-  out->reserved = 0;
+  out->max_stack = b.max_stack;
   for (int k = 0; k < 3; ++k) {
     out->bounds_lo[k] = b.bounds[k];
     out->bounds_hi[k] = b.bounds[3 + k];
@@ -301,8 +307,9 @@ rt_status rt_blas_export(rt_ctx_t c, rt_blas_t id, void* nodes, size_t nodes_byt
   const DeviceBlas& b = c->blas[id];
   (void)hipSetDevice(c->device);
   if (nodes) {
-    if (nodes_bytes < (size_t)b.nnodes * 64) return fail(c, RT_E_INVALID, "rt_blas_export: nodes buffer too small");
-    HIPCHK(c, hipMemcpy(nodes, b.nodes, (size_t)b.nnodes * 64, hipMemcpyDeviceToHost), "export nodes");
+    if (nodes_bytes < (size_t)b.nnodes * sizeof(rt::Bvh4Node))
+      return fail(c, RT_E_INVALID, "rt_blas_export: nodes buffer too small");
+    HIPCHK(c, hipMemcpy(nodes, b.nodes, (size_t)b.nnodes * sizeof(rt::Bvh4Node), hipMemcpyDeviceToHost), "export nodes");
   }
   if (tris) {
     if (tris_bytes < (size_t)b.ntri * 48) return fail(c, RT_E_INVALID, "rt_blas_export: tris buffer too small");
@@ -348,10 +355,9 @@ rt_status rt_tlas_build(rt_ctx_t c, const rt_instance* in, uint32_t n, int updat
     c->inst = nullptr;
     c->tlas_sorted = nullptr;
     const uint32_t nn = n > 1 ? n - 1 : 1;
-    HIPCHK(c, hipMalloc(&c->tlas_nodes, (size_t)nn * sizeof(rt::BvhNode)), "hipMalloc(tlas)");
+    HIPCHK(c, hipMalloc(&c->tlas_nodes, (size_t)nn * sizeof(rt::Bvh4Node)), "hipMalloc(tlas)");
     HIPCHK(c, hipMalloc(&c->inst, (size_t)n * sizeof(rt::InstanceRec)), "hipMalloc(instances)");
     HIPCHK(c, hipMalloc(&c->tlas_sorted, (size_t)n * 4), "hipMalloc(tlas order)");
-    c->tlas_nodes_n = nn;
   }
   float* d_bb = nullptr;
   float* d_box = nullptr;
@@ -363,7 +369,9 @@ rt_status rt_tlas_build(rt_ctx_t c, const rt_instance* in, uint32_t n, int updat
   float ms = 0.0f;
   // update_only rebuilds the hierarchy over the new boxes: an LBVH rebuild costs the same
   // launches as a refit at these sizes and keeps the tree identical to a fresh build.
-  if (e == hipSuccess) e = rt::lbvh_build(d_box, n, c->tlas_nodes, c->tlas_sorted, true, &c->tlas_depth, c->tlas_bounds, &ms, s);
+  if (e == hipSuccess)
+    e = rt::lbvh_build(d_box, n, c->tlas_nodes, c->tlas_sorted, true, &c->tlas_nodes_n, &c->tlas_depth, &c->tlas_max_stack,
+                       c->tlas_bounds, &ms, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   (void)hipFree(d_bb);
   (void)hipFree(d_box);
@@ -379,7 +387,7 @@ rt_status rt_tlas_info(rt_ctx_t c, rt_bvh_info* out) {
   out->prim_count = c->ninst;
   out->node_count = c->tlas_nodes_n;
   out->depth = c->tlas_depth;
-  out->reserved = 0;
+  out->max_stack = c->tlas_max_stack;
   for (int k = 0; k < 3; ++k) {
     out->bounds_lo[k] = c->tlas_bounds[k];
     out->bounds_hi[k] = c->tlas_bounds[3 + k];
@@ -390,9 +398,10 @@ rt_status rt_tlas_info(rt_ctx_t c, rt_bvh_info* out) {
 
 rt_status rt_tlas_export(rt_ctx_t c, void* nodes, size_t nodes_bytes) {
   if (!c || !nodes || !c->inst) return fail(c, RT_E_INVALID, "rt_tlas_export: no TLAS");
-  if (nodes_bytes < (size_t)c->tlas_nodes_n * 64) return fail(c, RT_E_INVALID, "rt_tlas_export: buffer too small");
+  const size_t bytes = (size_t)c->tlas_nodes_n * sizeof(rt::Bvh4Node);
+  if (nodes_bytes < bytes) return fail(c, RT_E_INVALID, "rt_tlas_export: buffer too small");
   (void)hipSetDevice(c->device);
-  HIPCHK(c, hipMemcpy(nodes, c->tlas_nodes, (size_t)c->tlas_nodes_n * 64, hipMemcpyDeviceToHost), "export tlas");
+  HIPCHK(c, hipMemcpy(nodes, c->tlas_nodes, bytes, hipMemcpyDeviceToHost), "export tlas");
   return RT_OK;
 }
 
@@ -439,9 +448,30 @@ static rt::SceneView scene_view(rt_ctx* c) {
   sv.tlas = c->tlas_nodes;
   sv.inst = c->inst;
   uint32_t maxb = 0;
-  for (const auto& b : c->blas) maxb = b.depth > maxb ? b.depth : maxb;
-  sv.stack_cap = (int)(c->tlas_depth + maxb + 2);
+  for (const auto& b : c->blas) maxb = b.max_stack > maxb ? b.max_stack : maxb;
+  // worst case: the TLAS path's siblings, the TLAS->BLAS sentinel, the BLAS path's siblings
+  sv.stack_cap = (int)(c->tlas_max_stack + 1 + maxb);
+  sv.lds_cap = sv.stack_cap < rt::kLdsStackEntries ? sv.stack_cap : rt::kLdsStackEntries;
+  sv.ovf = nullptr;
+  sv.ovf_lanes = 0;
   return sv;
+}
+
+// Sizes the HBM overflow stack for `lanes` lanes when the trees are deeper than the LDS part.
+static rt_status ensure_overflow(rt_ctx* c, rt::SceneView& sv, size_t lanes, hipStream_t s) {
+  if (sv.stack_cap <= sv.lds_cap) return RT_OK;
+  const size_t need = lanes * (size_t)(sv.stack_cap - sv.lds_cap);
+  if (need > c->ovf_cap) {
+    (void)hipStreamSynchronize(s);
+    if (c->d_ovf) (void)hipFree(c->d_ovf);
+    c->d_ovf = nullptr;
+    c->ovf_cap = 0;
+    HIPCHK(c, hipMalloc(&c->d_ovf, need * sizeof(int)), "hipMalloc(stack overflow area)");
+    c->ovf_cap = need;
+  }
+  sv.ovf = c->d_ovf;
+  sv.ovf_lanes = (uint32_t)lanes;
+  return RT_OK;
 }
 
 rt_status rt_dispatch_rays(rt_ctx_t c, uint32_t W, uint32_t H, const uint32_t* rows, uint32_t nrows,
@@ -477,6 +507,13 @@ rt_status rt_dispatch_rays(rt_ctx_t c, uint32_t W, uint32_t H, const uint32_t* r
   c->fp.height = H;
   c->fp.nrows = nrows;
   rt::SceneView sv = scene_view(c);
+  if (sv.stack_cap > rt::kMaxTraversalStack)
+    return fail(c, RT_E_UNSUPPORTED, "rt_dispatch_rays: BVH too deep for the traversal stack");
+  {
+    const size_t lanes = (size_t)((W + 15) / 16) * ((nrows + 15) / 16) * 256;
+    rt_status st = ensure_overflow(c, sv, lanes, s);
+    if (st != RT_OK) return st;
+  }
   hipError_t e = rt::launch_trace_frame(sv, c->fp, d_rows, rgba8, rgba32f, c->d_stats, c->stats_on,
                                         c->schedule, &c->wf, s);
   if (e != hipSuccess) return hip_fail(c, e, "trace launch");
@@ -493,6 +530,12 @@ rt_status rt_trace_rays(rt_ctx_t c, const float* rays, uint32_t n, int any_hit, 
   if (!c->inst) return fail(c, RT_E_INVALID, "rt_trace_rays: no TLAS built");
   (void)hipSetDevice(c->device);
   rt::SceneView sv = scene_view(c);
+  if (sv.stack_cap > rt::kMaxTraversalStack)
+    return fail(c, RT_E_UNSUPPORTED, "rt_trace_rays: BVH too deep for the traversal stack");
+  {
+    rt_status st = ensure_overflow(c, sv, (size_t)((n + 255) / 256) * 256, pick_stream(c, stream));
+    if (st != RT_OK) return st;
+  }
   hipError_t e = rt::launch_trace_rays(sv, rays, n, any_hit, hits, uv, c->d_stats, c->stats_on, pick_stream(c, stream));
   if (e != hipSuccess) return hip_fail(c, e, "trace_rays launch");
   return RT_OK;

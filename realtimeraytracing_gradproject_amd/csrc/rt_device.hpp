@@ -17,23 +17,50 @@
 
 #define RT_HD __host__ __device__ __forceinline__
 
+// Code-shape knobs, A/B-timed in one process with tools/ab.py (results in DESIGN.md §3.2). They
+// change instruction schedules only: every setting renders the identical image.
+#ifndef RT_MT_EARLY_EXIT
+#define RT_MT_EARLY_EXIT 1  // Moller-Trumbore with early rejects (vs one final predicate)
+#endif
+#ifndef RT_COND_PUSH
+#define RT_COND_PUSH 1      // push only hit children (vs unconditional LDS writes, predicated sp)
+#endif
+#ifndef RT_ARGMIN_ORDER
+#define RT_ARGMIN_ORDER 0   // nearest child only (vs the full 4-sort; the sort culls better)
+#endif
+
 namespace rt {
 
 // ------------------------------------------------------------------------------------------
 // HBM layout
 // ------------------------------------------------------------------------------------------
 
-// Child-pair BVH node, 64 B (one half of a 128-B L2 line; 64-B aligned). The node stores the
-// boxes of BOTH children so one node fetch decides which children to visit.
+// Binary child-pair node of the Karras LBVH: a build intermediate only (collapsed into Bvh4Node).
 // Child refs: >= 0 internal node index, < 0 leaf: ~slot (BLAS: triangle slot in leaf order,
 // TLAS: instance index).
-struct alignas(64) BvhNode {
+struct alignas(64) BinNode {
   float lo0[3], hi0[3];
   float lo1[3], hi1[3];
   int32_t c0, c1;
   uint32_t pad0, pad1;
 };
-static_assert(sizeof(BvhNode) == 64, "BvhNode must be 64 B");
+static_assert(sizeof(BinNode) == 64, "BinNode must be 64 B");
+
+// Traversal node: 4-wide, 128 B = one cache line, nodes in BFS order (root 0, then level by
+// level: the top of the tree is a contiguous prefix). Child boxes are stored SoA so one node is
+// 8 x 16-B loads and the 4 slab tests share per-axis FMAs. Built on the device by collapsing
+// every other level of the binary LBVH (each node has 2..4 children).
+// child[k]: >= 0 node index, < 0 leaf (~slot / ~instance), kEmptyChild = unused slot.
+constexpr int32_t kEmptyChild = INT32_MIN + 1;
+struct alignas(128) Bvh4Node {
+  float lox[4], hix[4];
+  float loy[4], hiy[4];
+  float loz[4], hiz[4];
+  int32_t child[4];
+  uint32_t count;  // valid children
+  uint32_t pad[3];
+};
+static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node must be 128 B");
 
 // Moller-Trumbore-ready triangle in leaf order, 48 B: v0, e1 = v1 - v0, e2 = v2 - v0, and the
 // original PrimitiveIndex().
@@ -56,7 +83,7 @@ struct alignas(16) InstanceRec {
   uint32_t instance_id;
   uint32_t hit_group;
   uint32_t blas;
-  const BvhNode* nodes;
+  const Bvh4Node* nodes;  // BLAS root = node 0
   const TriRec* tris;
   const float* vtx;       // 6 floats per vertex: pos.xyz, normal.xyz (stride 24 B)
   const uint32_t* idx;    // triangle list, or nullptr for non-indexed geometry
@@ -64,6 +91,8 @@ struct alignas(16) InstanceRec {
 
 constexpr int kMaxLights = 16;
 constexpr int32_t kStackSentinel = INT32_MIN;  // TLAS -> BLAS transition marker
+constexpr int kMaxTraversalStack = 256;        // entries per lane (LDS part + HBM overflow)
+constexpr int kLdsStackEntries = 32;           // LDS part: 32 KB per 256-lane workgroup
 
 struct LightRec {
   float color[3];
@@ -89,9 +118,12 @@ struct FrameParams {
 };
 
 struct SceneView {
-  const BvhNode* tlas;
+  const Bvh4Node* tlas;
   const InstanceRec* inst;
-  int stack_cap;
+  int stack_cap;       // worst-case entries per lane (exact bound from the trees)
+  int lds_cap;         // entries kept in LDS ([entry][lane])
+  int* ovf;            // HBM overflow area, [entry - lds_cap][global lane], or null
+  uint32_t ovf_lanes;  // lanes of the launch (overflow row pitch)
 };
 
 // ------------------------------------------------------------------------------------------
@@ -199,21 +231,47 @@ RT_HD uint32_t unorm8(float c) {
   return (uint32_t)(c * 255.0f + 0.5f);
 }
 
-// Slab test of one child box against the current ray segment [tmin, tbest]. Conservative
-// (tfar widened by 1 + 4e-7) so BVH culling never rejects a triangle Moller-Trumbore accepts.
-RT_HD bool slab(const float* lo, const float* hi, V3 invd, V3 noinv, float tmin, float tbest,
-                float& tnear) {
-  float tlx = __builtin_fmaf(lo[0], invd.x, noinv.x), thx = __builtin_fmaf(hi[0], invd.x, noinv.x);
-  float tly = __builtin_fmaf(lo[1], invd.y, noinv.y), thy = __builtin_fmaf(hi[1], invd.y, noinv.y);
-  float tlz = __builtin_fmaf(lo[2], invd.z, noinv.z), thz = __builtin_fmaf(hi[2], invd.z, noinv.z);
-  float tn = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), tmin));
-  float tf = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tbest));
-  tnear = tn;
-  return tn <= tf * 1.0000004f;
+// Slab tests of the 4 children of a Bvh4Node against the ray segment [tmin, tbest].
+// tn[k] = entry distance of child k, or +inf if it is missed or empty. Conservative (tfar
+// widened by 1 + 4e-7) so BVH culling never rejects a triangle Moller-Trumbore accepts.
+RT_HD void slab4(const float* lox, const float* hix, const float* loy, const float* hiy,
+                 const float* loz, const float* hiz, const int32_t* child, V3 invd, V3 noinv,
+                 float tmin, float tbest, float tn[4]) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float tlx = __builtin_fmaf(lox[k], invd.x, noinv.x), thx = __builtin_fmaf(hix[k], invd.x, noinv.x);
+    float tly = __builtin_fmaf(loy[k], invd.y, noinv.y), thy = __builtin_fmaf(hiy[k], invd.y, noinv.y);
+    float tlz = __builtin_fmaf(loz[k], invd.z, noinv.z), thz = __builtin_fmaf(hiz[k], invd.z, noinv.z);
+    float n = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), tmin));
+    float f = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tbest));
+    tn[k] = (child[k] != kEmptyChild && n <= f * 1.0000004f) ? n : __builtin_inff();
+  }
+}
+
+// Orders 4 (distance, ref) pairs ascending with the 5-comparator network (0,1)(2,3)(0,2)(1,3)(1,2);
+// a pair moves only when strictly nearer, so equal distances keep a fixed, shared order.
+RT_HD void cswap(float& ta, int32_t& ra, float& tb, int32_t& rb) {
+  const bool s = tb < ta;
+  const float t = s ? tb : ta;
+  const int32_t r = s ? rb : ra;
+  tb = s ? ta : tb;
+  rb = s ? ra : rb;
+  ta = t;
+  ra = r;
+}
+RT_HD void sort4(float t[4], int32_t r[4]) {
+  cswap(t[0], r[0], t[1], r[1]);
+  cswap(t[2], r[2], t[3], r[3]);
+  cswap(t[0], r[0], t[2], r[2]);
+  cswap(t[1], r[1], t[3], r[3]);
+  cswap(t[1], r[1], t[2], r[2]);
 }
 
 // Moller-Trumbore. Accepts u >= 0, v >= 0, u + v <= 1, det != 0; returns t (not yet range checked).
+// Evaluated without early exits (one predicate at the end): fewer divergent branches per wave;
+// the values are those of the early-exit form whenever it accepts.
 RT_HD bool moller_trumbore(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float& t, float& u, float& v) {
+#if RT_MT_EARLY_EXIT
   V3 p = cross(d, e2);
   float det = dot(e1, p);
   if (det == 0.0f) return false;
@@ -226,6 +284,17 @@ RT_HD bool moller_trumbore(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float& t, float& u, 
   if (!(v >= 0.0f && u + v <= 1.0f)) return false;
   t = dot(e2, q) * inv;
   return true;
+#else
+  const V3 p = cross(d, e2);
+  const float det = dot(e1, p);
+  const float inv = 1.0f / det;
+  const V3 s = sub(o, v0);
+  u = dot(s, p) * inv;
+  const V3 q = cross(s, e1);
+  v = dot(d, q) * inv;
+  t = dot(e2, q) * inv;
+  return det != 0.0f && u >= 0.0f && u <= 1.0f && v >= 0.0f && u + v <= 1.0f;
+#endif
 }
 
 }  // namespace rt

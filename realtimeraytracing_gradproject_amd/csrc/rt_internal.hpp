@@ -9,13 +9,15 @@ namespace rt {
 
 // --- LBVH build (rt_lbvh.hip) ---------------------------------------------------------------
 
-// Builds a child-pair LBVH over n primitive boxes (d_primbox: n x {lo.xyz, hi.xyz}).
-// d_nodes receives max(n-1, 1) nodes, d_sorted the leaf-order -> primitive permutation.
-// Leaf refs are ~leaf_slot (BLAS, primitives reordered afterwards) or ~primitive (TLAS).
-// Returns the depth (root-to-leaf edges) and the root box in host memory. Synchronous.
-hipError_t lbvh_build(const float* d_primbox, uint32_t n, BvhNode* d_nodes, uint32_t* d_sorted,
-                      bool leaf_ref_is_prim, uint32_t* depth, float bounds[6], float* build_ms,
-                      hipStream_t stream);
+// Builds an LBVH over n primitive boxes (d_primbox: n x {lo.xyz, hi.xyz}) and collapses it into
+// 4-wide BFS-ordered nodes. d_nodes needs room for max(n-1, 1) nodes (an upper bound); the count
+// used, the number of levels and the worst-case traversal stack of the tree are returned, with
+// the root box, in host memory. d_sorted
+// receives the leaf-order -> primitive permutation. Leaf refs are ~leaf_slot (BLAS, primitives
+// reordered afterwards) or ~primitive (TLAS). Synchronous.
+hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uint32_t* d_sorted,
+                      bool leaf_ref_is_prim, uint32_t* node_count, uint32_t* depth, uint32_t* max_stack,
+                      float bounds[6], float* build_ms, hipStream_t stream);
 
 // Triangle setup: prim boxes + unsorted MT records from a {pos, normal} vertex array.
 hipError_t blas_prepare(const float* d_vtx, const uint32_t* d_idx, uint32_t ntri, TriRec* d_tris,

@@ -260,10 +260,10 @@ __global__ void k_refit(int n, const int* __restrict__ parent_leaf, const int* _
 // 6. pack child-pair nodes.
 __global__ void k_pack(int n, const int* __restrict__ child, const float* __restrict__ nbox,
                        const float* __restrict__ primbox, const uint32_t* __restrict__ sorted,
-                       bool leaf_ref_is_prim, BvhNode* __restrict__ nodes) {
+                       bool leaf_ref_is_prim, BinNode* __restrict__ nodes) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n - 1) return;
-  BvhNode nd;
+  BinNode nd;
   int c[2] = {child[2 * i], child[2 * i + 1]};
   float b[2][6];
   for (int k = 0; k < 2; ++k) load_box(c[k], nbox, primbox, sorted, b[k]);
@@ -282,8 +282,8 @@ __global__ void k_pack(int n, const int* __restrict__ child, const float* __rest
 }
 
 // n == 1: a root whose two children are the single leaf (tested twice; ties keep the result).
-__global__ void k_single(const float* __restrict__ primbox, bool leaf_ref_is_prim, BvhNode* nodes) {
-  BvhNode nd;
+__global__ void k_single(const float* __restrict__ primbox, bool leaf_ref_is_prim, BinNode* nodes) {
+  BinNode nd;
   for (int k = 0; k < 3; ++k) {
     nd.lo0[k] = nd.lo1[k] = primbox[k];
     nd.hi0[k] = nd.hi1[k] = primbox[3 + k];
@@ -294,17 +294,123 @@ __global__ void k_single(const float* __restrict__ primbox, bool leaf_ref_is_pri
   nodes[0] = nd;
 }
 
-__global__ void k_depth(int n, const int* __restrict__ parent_leaf, const int* __restrict__ parent_int,
-                        uint32_t* out) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t d = 1;
-  int node = parent_leaf[i];
-  while (parent_int[node] >= 0) {
-    node = parent_int[node];
-    ++d;
+// 7. collapse the binary tree into 4-wide nodes in BFS order: a 4-wide node at binary depth 2k
+// takes its children's children (a leaf child stays a child). One workgroup walks the levels;
+// each level's new node indices come from a block-wide exclusive scan of per-node internal-child
+// counts (deterministic, no atomics), so the oracle's sequential BFS yields the same array.
+// It also bounds the traversal stack: a visited node pushes (count - 1) siblings, so the most a
+// root-to-node path can leave on the stack is ps[node] + count(node) - 1, ps = sum over the
+// ancestors. info[0] = node count, info[1] = levels, info[2] = that maximum.
+__global__ __launch_bounds__(1024) void k_collapse(const BinNode* __restrict__ bin, Bvh4Node* __restrict__ out,
+                                                   int* la, int* lb, int* ps, uint32_t* __restrict__ info) {
+  __shared__ int scan[1024];
+  __shared__ int s_maxstack;
+  const int tid = threadIdx.x;
+  int* cur = la;
+  int* nxt = lb;
+  if (tid == 0) {
+    cur[0] = 0;
+    ps[0] = 0;
+    s_maxstack = 0;
   }
-  atomicMax(out, d);
+  __syncthreads();
+  int lmax = 0;
+  int cur_n = 1, base = 0, depth = 0;
+  while (cur_n > 0) {
+    ++depth;
+    int next_total = 0;
+    for (int cs = 0; cs < cur_n; cs += 1024) {
+      const int i = cs + tid;
+      const bool valid = i < cur_n;
+      int ref[4];
+      float box[4][6];
+      int cnt = 0;
+      if (valid) {
+        const BinNode& b = bin[cur[i]];
+        for (int k = 0; k < 2; ++k) {
+          const int c = k ? b.c1 : b.c0;
+          const float* lo = k ? b.lo1 : b.lo0;
+          const float* hi = k ? b.hi1 : b.hi0;
+          if (c < 0) {
+            ref[cnt] = c;
+            for (int a = 0; a < 3; ++a) {
+              box[cnt][a] = lo[a];
+              box[cnt][3 + a] = hi[a];
+            }
+            ++cnt;
+          } else {
+            const BinNode& g = bin[c];
+            for (int q = 0; q < 2; ++q) {
+              ref[cnt] = q ? g.c1 : g.c0;
+              for (int a = 0; a < 3; ++a) {
+                box[cnt][a] = q ? g.lo1[a] : g.lo0[a];
+                box[cnt][3 + a] = q ? g.hi1[a] : g.hi0[a];
+              }
+              ++cnt;
+            }
+          }
+        }
+      }
+      int m = 0;
+      for (int j = 0; j < cnt; ++j) m += ref[j] >= 0;
+      scan[tid] = m;
+      __syncthreads();
+      for (int off = 1; off < 1024; off <<= 1) {
+        const int add = tid >= off ? scan[tid - off] : 0;
+        __syncthreads();
+        scan[tid] += add;
+        __syncthreads();
+      }
+      const int excl = scan[tid] - m;
+      const int chunk_total = scan[1023];
+      if (valid) {
+        Bvh4Node nd;
+        int o = excl;
+        const int below = ps[base + i] + cnt - 1;
+        lmax = below > lmax ? below : lmax;
+        for (int j = 0; j < 4; ++j) {
+          float b6[6] = {0, 0, 0, 0, 0, 0};
+          int32_t r = kEmptyChild;
+          if (j < cnt) {
+            for (int a = 0; a < 6; ++a) b6[a] = box[j][a];
+            if (ref[j] >= 0) {
+              const int pos = next_total + o;
+              nxt[pos] = ref[j];
+              r = base + cur_n + pos;
+              ps[r] = below;
+              ++o;
+            } else {
+              r = ref[j];
+            }
+          }
+          nd.lox[j] = b6[0];
+          nd.loy[j] = b6[1];
+          nd.loz[j] = b6[2];
+          nd.hix[j] = b6[3];
+          nd.hiy[j] = b6[4];
+          nd.hiz[j] = b6[5];
+          nd.child[j] = r;
+        }
+        nd.count = (uint32_t)cnt;
+        nd.pad[0] = nd.pad[1] = nd.pad[2] = 0;
+        out[base + i] = nd;
+      }
+      next_total += chunk_total;
+      __syncthreads();
+    }
+    int* t = cur;
+    cur = nxt;
+    nxt = t;
+    base += cur_n;
+    cur_n = next_total;
+  }
+  atomicMax(&s_maxstack, lmax);
+  __syncthreads();
+  if (tid == 0) {
+    info[0] = (uint32_t)base;
+    info[1] = (uint32_t)depth;
+    info[2] = (uint32_t)s_maxstack;
+  }
 }
 
 __global__ void k_tri_setup(const float* __restrict__ vtx, const uint32_t* __restrict__ idx,
@@ -376,23 +482,27 @@ struct DevBuf {
 
 }  // namespace
 
-hipError_t lbvh_build(const float* d_primbox, uint32_t n, BvhNode* d_nodes, uint32_t* d_sorted,
-                      bool leaf_ref_is_prim, uint32_t* depth, float bounds[6], float* build_ms,
-                      hipStream_t s) {
+hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uint32_t* d_sorted,
+                      bool leaf_ref_is_prim, uint32_t* node_count, uint32_t* depth, uint32_t* max_stack,
+                      float bounds[6], float* build_ms, hipStream_t s) {
   if (n == 0) return hipErrorInvalidValue;
   hipEvent_t e0, e1;
   RT_TRY(hipEventCreate(&e0));
   RT_TRY(hipEventCreate(&e1));
   RT_TRY(hipEventRecord(e0, s));
   const uint32_t nblocks = (n + kRsTile - 1) / kRsTile;
-  DevBuf stats, keys0, keys1, vals1, hist, child, pint, pleaf, nbox, flags, dep;
+  const uint32_t nbin = n > 1 ? n - 1 : 1;
+  DevBuf stats, keys0, keys1, vals1, hist, child, pint, pleaf, nbox, flags, info, bin, la, lb, ps;
   RT_TRY(hipMalloc(&stats.p, 12 * sizeof(float)));
   RT_TRY(hipMalloc(&keys0.p, (size_t)n * 4));
   RT_TRY(hipMalloc(&keys1.p, (size_t)n * 4));
   RT_TRY(hipMalloc(&vals1.p, (size_t)n * 4));
   RT_TRY(hipMalloc(&hist.p, (size_t)256 * nblocks * 4));
-  RT_TRY(hipMalloc(&dep.p, 4));
-  RT_TRY(hipMemsetAsync(dep.p, 0, 4, s));
+  RT_TRY(hipMalloc(&info.p, 12));
+  RT_TRY(hipMalloc(&ps.p, (size_t)nbin * 4));
+  RT_TRY(hipMalloc(&bin.p, (size_t)nbin * sizeof(BinNode)));
+  RT_TRY(hipMalloc(&la.p, (size_t)nbin * 4));
+  RT_TRY(hipMalloc(&lb.p, (size_t)nbin * 4));
   float* cb = (float*)stats.p;
   k_bounds<<<1, 1024, 0, s>>>(d_primbox, n, cb);
   RT_TRY(hipGetLastError());
@@ -412,11 +522,10 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, BvhNode* d_nodes, uint
     std::swap(va, vb);
   }
   // after 4 swaps: va == d_sorted, ka == keys0 (sorted keys)
+  BinNode* d_bin = (BinNode*)bin.p;
   if (n == 1) {
-    k_single<<<1, 1, 0, s>>>(d_primbox, leaf_ref_is_prim, d_nodes);
+    k_single<<<1, 1, 0, s>>>(d_primbox, leaf_ref_is_prim, d_bin);
     RT_TRY(hipGetLastError());
-    uint32_t one = 1;
-    RT_TRY(hipMemcpyAsync(dep.p, &one, 4, hipMemcpyHostToDevice, s));
   } else {
     RT_TRY(hipMalloc(&child.p, (size_t)(n - 1) * 8));
     RT_TRY(hipMalloc(&pint.p, (size_t)(n - 1) * 4));
@@ -428,16 +537,21 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, BvhNode* d_nodes, uint
     k_refit<<<grid1(n, 256), 256, 0, s>>>((int)n, (int*)pleaf.p, (int*)pint.p, (int*)child.p, d_primbox,
                                           d_sorted, (float*)nbox.p, (uint32_t*)flags.p);
     k_pack<<<grid1(n - 1, 256), 256, 0, s>>>((int)n, (int*)child.p, (float*)nbox.p, d_primbox, d_sorted,
-                                             leaf_ref_is_prim, d_nodes);
-    k_depth<<<grid1(n, 256), 256, 0, s>>>((int)n, (int*)pleaf.p, (int*)pint.p, (uint32_t*)dep.p);
+                                             leaf_ref_is_prim, d_bin);
     RT_TRY(hipGetLastError());
   }
+  k_collapse<<<1, 1024, 0, s>>>(d_bin, d_nodes, (int*)la.p, (int*)lb.p, (int*)ps.p, (uint32_t*)info.p);
+  RT_TRY(hipGetLastError());
   RT_TRY(hipEventRecord(e1, s));
   float hb[12];
+  uint32_t hinfo[3];
   RT_TRY(hipMemcpyAsync(hb, cb, sizeof(hb), hipMemcpyDeviceToHost, s));
-  RT_TRY(hipMemcpyAsync(depth, dep.p, 4, hipMemcpyDeviceToHost, s));
+  RT_TRY(hipMemcpyAsync(hinfo, info.p, 12, hipMemcpyDeviceToHost, s));
   RT_TRY(hipStreamSynchronize(s));
   for (int k = 0; k < 6; ++k) bounds[k] = hb[6 + k];
+  *node_count = hinfo[0];
+  *depth = hinfo[1];
+  *max_stack = hinfo[2];
   float ms = 0.0f;
   RT_TRY(hipEventElapsedTime(&ms, e0, e1));
   if (build_ms) *build_ms = ms;

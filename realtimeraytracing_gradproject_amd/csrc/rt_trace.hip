@@ -36,19 +36,63 @@ struct HitRec {
 
 __device__ __forceinline__ V3 ld3(const float* p) { return v3(p[0], p[1], p[2]); }
 
-// Two-level stack traversal. ANY_HIT: first accepted hit terminates (shadow rays). Closest hit
-// keeps the lexicographic minimum of (t, instance, primitive): independent of traversal order.
+// Scene data is read through explicit global (address space 1) pointers: pointers loaded from
+// memory (instance records) would otherwise become flat accesses, which wait on both vmcnt and
+// lgkmcnt and serialise the node fetch against LDS stack traffic.
+#define RT_GLOBAL __attribute__((address_space(1)))
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef int i4v __attribute__((ext_vector_type(4)));
+template <typename T>
+__device__ __forceinline__ const RT_GLOBAL T* gp(const T* p) {
+  return (const RT_GLOBAL T*)p;
+}
+
+// Two-level stack traversal over 4-wide nodes. ANY_HIT: first accepted hit terminates (shadow
+// rays). Closest hit keeps the lexicographic minimum of (t, instance, primitive): independent of
+// traversal order. Children are visited nearest first (sort4); the oracle mirrors the order, so
+// the box/triangle test counters match it exactly. The per-lane stack lives in LDS as
+// [entry][lane] (bank = lane: conflict free), sized to the worst case of the scene's trees.
+// Per-lane stack: entries [0, lds_cap) in LDS ([entry][lane], bank = lane), deeper entries in
+// the HBM overflow area ([entry - lds_cap][lane]), touched only by paths deeper than lds_cap.
+struct LaneStack {
+  int* lds;                 // s_stack + threadIdx.x
+  RT_GLOBAL int* ovf;       // overflow base + global lane (null when stack_cap <= lds_cap)
+  uint32_t pitch;           // lanes of the launch
+  int lds_cap, cap;
+  __device__ __forceinline__ void put(int slot, int v) const {
+    if (slot < lds_cap) lds[slot * kBlock] = v;
+    else if (slot < cap) ovf[(size_t)(slot - lds_cap) * pitch] = v;
+  }
+  __device__ __forceinline__ int get(int slot) const {
+    int v;
+    if (slot < lds_cap) v = lds[slot * kBlock];
+    else v = ovf[(size_t)(slot - lds_cap) * pitch];
+    return v;
+  }
+};
+
+__device__ __forceinline__ LaneStack lane_stack(const SceneView& sc, int* s_stack, uint32_t global_lane) {
+  LaneStack st;
+  st.lds = s_stack + threadIdx.x;
+  st.ovf = sc.ovf ? (RT_GLOBAL int*)sc.ovf + global_lane : nullptr;
+  st.pitch = sc.ovf_lanes;
+  st.lds_cap = sc.lds_cap;
+  st.cap = sc.stack_cap;
+  return st;
+}
+
 template <bool ANY_HIT, bool STATS>
 __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, HitRec& hit,
-                      int* __restrict__ stk, Counters& cnt) {
+                      const LaneStack& stk, Counters& cnt) {
   const V3 winvd = v3(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
   const V3 wnoinv = neg(mul(o, winvd));
   V3 ro = o, rd = d, rinvd = winvd, rnoinv = wnoinv;
-  const BvhNode* nodes = sc.tlas;
-  const TriRec* tris = nullptr;
+  const RT_GLOBAL Bvh4Node* nodes = gp(sc.tlas);
+  const RT_GLOBAL TriRec* tris = nullptr;
   uint32_t cur = 0;
   bool in_blas = false;
   bool found = false;
+  const int cap = stk.cap;
   int sp = 0;
   int ref = 0;
   hit.t = tmax;
@@ -57,62 +101,80 @@ __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, H
   hit.u = hit.v = 0.0f;
   while (true) {
     if (ref >= 0) {
-      const float4* np = reinterpret_cast<const float4*>(nodes + ref);
-      const float4 a = np[0], b = np[1], c = np[2], e = np[3];
-      const float lo0[3] = {a.x, a.y, a.z}, hi0[3] = {a.w, b.x, b.y};
-      const float lo1[3] = {b.z, b.w, c.x}, hi1[3] = {c.y, c.z, c.w};
-      const int c0 = __float_as_int(e.x), c1 = __float_as_int(e.y);
-      float tn0, tn1;
-      const bool h0 = slab(lo0, hi0, rinvd, rnoinv, tmin, hit.t, tn0);
-      const bool h1 = slab(lo1, hi1, rinvd, rnoinv, tmin, hit.t, tn1);
-      if (STATS) cnt.aabb += 2;
-      if (h0 && h1) {
-        const bool swap = tn1 < tn0;
-        const int nearc = swap ? c1 : c0, farc = swap ? c0 : c1;
-        if (sp < sc.stack_cap) {
-          stk[sp * kBlock] = farc;
-          ++sp;
-        } else if (STATS) {
-          ++cnt.overflow;
+      const RT_GLOBAL f4v* np = reinterpret_cast<const RT_GLOBAL f4v*>(nodes + ref);
+      const f4v a0 = np[0], a1 = np[1], a2 = np[2], a3 = np[3], a4 = np[4], a5 = np[5];
+      const i4v ch = reinterpret_cast<const RT_GLOBAL i4v*>(np)[6];
+      const float lox[4] = {a0.x, a0.y, a0.z, a0.w}, hix[4] = {a1.x, a1.y, a1.z, a1.w};
+      const float loy[4] = {a2.x, a2.y, a2.z, a2.w}, hiy[4] = {a3.x, a3.y, a3.z, a3.w};
+      const float loz[4] = {a4.x, a4.y, a4.z, a4.w}, hiz[4] = {a5.x, a5.y, a5.z, a5.w};
+      int32_t r[4] = {ch.x, ch.y, ch.z, ch.w};
+      float tn[4];
+      slab4(lox, hix, loy, hiy, loz, hiz, r, rinvd, rnoinv, tmin, hit.t, tn);
+      if (STATS)
+        cnt.aabb += (uint32_t)(r[0] != kEmptyChild) + (uint32_t)(r[1] != kEmptyChild) +
+                    (uint32_t)(r[2] != kEmptyChild) + (uint32_t)(r[3] != kEmptyChild);
+#if RT_ARGMIN_ORDER
+      // nearest child first; the others keep slot order
+      {
+        int b = 0;
+#pragma unroll
+        for (int k = 1; k < 4; ++k) b = tn[k] < tn[b] ? k : b;
+        const float tb = tn[b];
+        const int32_t rb = r[b];
+        tn[b] = tn[0];
+        r[b] = r[0];
+        tn[0] = tb;
+        r[0] = rb;
+      }
+#else
+      sort4(tn, r);
+#endif
+      if (tn[0] != __builtin_inff()) {
+#pragma unroll
+        for (int k = 3; k >= 1; --k) {
+          const bool h = tn[k] != __builtin_inff();
+#if RT_COND_PUSH
+          if (h) {
+            if (sp < cap) {
+              stk.put(sp, r[k]);
+              ++sp;
+            } else if (STATS) {
+              ++cnt.overflow;
+            }
+          }
+#else
+          // unconditional write (a miss leaves a dead value above the top), predicated sp
+          stk.put(sp, r[k]);
+          if (STATS && h && sp >= cap) ++cnt.overflow;
+          sp += (h && sp < cap) ? 1 : 0;
+#endif
         }
-        ref = nearc;
-        continue;
-      }
-      if (h0) {
-        ref = c0;
-        continue;
-      }
-      if (h1) {
-        ref = c1;
+        ref = r[0];
         continue;
       }
     } else if (!in_blas) {
       cur = (uint32_t)(~ref);
-      const InstanceRec* ir = sc.inst + cur;
-      ro = xform_point(ir->w2o, o);
-      rd = xform_dir(ir->w2o, d);
-      rinvd = v3(safe_inv(rd.x), safe_inv(rd.y), safe_inv(rd.z));
-      rnoinv = neg(mul(ro, rinvd));
-      nodes = ir->nodes;
-      tris = ir->tris;
-      in_blas = true;
+      const RT_GLOBAL InstanceRec* ir = gp(sc.inst) + cur;
       if (STATS) ++cnt.inst;
-      if (sp < sc.stack_cap) {
-        stk[sp * kBlock] = kStackSentinel;
+      if (sp < cap) {
+        stk.put(sp, kStackSentinel);
         ++sp;
+        float m[12];
+        for (int k = 0; k < 12; ++k) m[k] = ir->w2o[k];
+        ro = xform_point(m, o);
+        rd = xform_dir(m, d);
+        rinvd = v3(safe_inv(rd.x), safe_inv(rd.y), safe_inv(rd.z));
+        rnoinv = neg(mul(ro, rinvd));
+        nodes = gp(ir->nodes);
+        tris = gp(ir->tris);
+        in_blas = true;
         ref = 0;
         continue;
       }
-      if (STATS) ++cnt.overflow;
-      in_blas = false;  // cannot enter without a way back: skip this instance
-      nodes = sc.tlas;
-      ro = o;
-      rd = d;
-      rinvd = winvd;
-      rnoinv = wnoinv;
+      if (STATS) ++cnt.overflow;  // no room for the way back: skip this instance
     } else {
-      const float4* tp = reinterpret_cast<const float4*>(tris + (~ref));
-      const float4 a = tp[0], b = tp[1], c = tp[2];
+      const RT_GLOBAL f4v* tp = reinterpret_cast<const RT_GLOBAL f4v*>(tris + (~ref));
+      const f4v a = tp[0], b = tp[1], c = tp[2];
       if (STATS) ++cnt.tri;
       float t, u, v;
       if (moller_trumbore(ro, rd, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), v3(c.x, c.y, c.z), t, u, v) &&
@@ -135,10 +197,10 @@ __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, H
     while (true) {
       if (sp == 0) return found;
       --sp;
-      ref = stk[sp * kBlock];
+      ref = stk.get(sp);
       if (ref != kStackSentinel) break;
       in_blas = false;
-      nodes = sc.tlas;
+      nodes = gp(sc.tlas);
       ro = o;
       rd = d;
       rinvd = winvd;
@@ -147,12 +209,32 @@ __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, H
   }
 }
 
-__device__ __forceinline__ void tri_vertex_ids(const InstanceRec* ir, uint32_t prim, uint32_t& i0,
-                                               uint32_t& i1, uint32_t& i2) {
-  if (ir->idx) {
-    i0 = ir->idx[3 * prim];
-    i1 = ir->idx[3 * prim + 1];
-    i2 = ir->idx[3 * prim + 2];
+// Hit-instance data the shaders read (the reference binds it per hit group through the SBT).
+struct HitInstance {
+  const RT_GLOBAL float* vtx;
+  const RT_GLOBAL uint32_t* idx;
+  float nrm[9];
+  uint32_t hit_group;
+};
+
+__device__ __forceinline__ HitInstance load_hit_instance(const SceneView& sc, uint32_t inst) {
+  const RT_GLOBAL InstanceRec* ir = gp(sc.inst) + inst;
+  HitInstance h;
+  h.vtx = gp(ir->vtx);
+  h.idx = gp(ir->idx);
+  for (int k = 0; k < 9; ++k) h.nrm[k] = ir->nrm[k];
+  h.hit_group = ir->hit_group;
+  return h;
+}
+
+__device__ __forceinline__ V3 ldg3(const RT_GLOBAL float* p) { return v3(p[0], p[1], p[2]); }
+
+__device__ __forceinline__ void tri_vertex_ids(const HitInstance& hi, uint32_t prim, uint32_t& i0, uint32_t& i1,
+                                               uint32_t& i2) {
+  if (hi.idx) {
+    i0 = hi.idx[3 * prim];
+    i1 = hi.idx[3 * prim + 1];
+    i2 = hi.idx[3 * prim + 2];
   } else {
     i0 = 3 * prim;
     i1 = 3 * prim + 1;
@@ -161,28 +243,28 @@ __device__ __forceinline__ void tri_vertex_ids(const InstanceRec* ir, uint32_t p
 }
 
 // CalculateInterpolatedWorldNormal (Hit.hlsl:67-81): vertex order 1,2,0 against (u, v, 1-u-v).
-__device__ V3 interpolated_world_normal(const InstanceRec* ir, uint32_t prim, float u, float v) {
+__device__ V3 interpolated_world_normal(const HitInstance& hi, uint32_t prim, float u, float v) {
   uint32_t i0, i1, i2;
-  tri_vertex_ids(ir, prim, i0, i1, i2);
-  const V3 n0 = ld3(ir->vtx + (size_t)i1 * 6 + 3);
-  const V3 n1 = ld3(ir->vtx + (size_t)i2 * 6 + 3);
-  const V3 n2 = ld3(ir->vtx + (size_t)i0 * 6 + 3);
+  tri_vertex_ids(hi, prim, i0, i1, i2);
+  const V3 n0 = ldg3(hi.vtx + (size_t)i1 * 6 + 3);
+  const V3 n1 = ldg3(hi.vtx + (size_t)i2 * 6 + 3);
+  const V3 n2 = ldg3(hi.vtx + (size_t)i0 * 6 + 3);
   const float bz = (1.0f - u) - v;
   V3 n = normalize(add(add(muls(n0, u), muls(n1, v)), muls(n2, bz)));
-  n = mat3_mul(ir->nrm, n);
+  n = mat3_mul(hi.nrm, n);
   return normalize(n);
 }
 
 // PlaneClosestHit face normal (Hit.hlsl:218-222): normalize(cross(e1, e2)), then the instance
 // normal matrix without renormalisation.
-__device__ V3 face_world_normal(const InstanceRec* ir, uint32_t prim) {
+__device__ V3 face_world_normal(const HitInstance& hi, uint32_t prim) {
   uint32_t i0, i1, i2;
-  tri_vertex_ids(ir, prim, i0, i1, i2);
-  const V3 p0 = ld3(ir->vtx + (size_t)i0 * 6);
-  const V3 p1 = ld3(ir->vtx + (size_t)i1 * 6);
-  const V3 p2 = ld3(ir->vtx + (size_t)i2 * 6);
+  tri_vertex_ids(hi, prim, i0, i1, i2);
+  const V3 p0 = ldg3(hi.vtx + (size_t)i0 * 6);
+  const V3 p1 = ldg3(hi.vtx + (size_t)i1 * 6);
+  const V3 p2 = ldg3(hi.vtx + (size_t)i2 * 6);
   V3 n = normalize(cross(sub(p1, p0), sub(p2, p0)));
-  return mat3_mul(ir->nrm, n);
+  return mat3_mul(hi.nrm, n);
 }
 
 // CalculateDirectLighting (Hit.hlsl:83-95).
@@ -252,7 +334,7 @@ __device__ V3 pbr_shading(const FrameParams& fp, V3 n, V3 cam, V3 P) {
 }
 
 template <bool STATS>
-__device__ bool shadow_ray(const SceneView& sc, V3 P, V3 dir, int* stk, Counters& cnt) {
+__device__ bool shadow_ray(const SceneView& sc, V3 P, V3 dir, const LaneStack& stk, Counters& cnt) {
   HitRec h;
   if (STATS) ++cnt.shadow;
   return trace<true, STATS>(sc, P, normalize(dir), 0.01f, 100000.0f, h, stk, cnt);
@@ -261,7 +343,7 @@ __device__ bool shadow_ray(const SceneView& sc, V3 P, V3 dir, int* stk, Counters
 // One camera sample -> color (RayGen.hlsl:28-43 and the hit/miss programs).
 template <int MODE, bool STATS>
 __device__ V3 shade_sample(const SceneView& sc, const FrameParams& fp, uint32_t px, uint32_t py,
-                           float ox, float oy, int* stk, Counters& cnt) {
+                           float ox, float oy, const LaneStack& stk, Counters& cnt) {
   const float dx = (((float)px + ox) / (float)fp.width) * 2.0f - 1.0f;
   const float dy = (((float)py + oy) / (float)fp.height) * 2.0f - 1.0f;
   float org4[4], dc[4], dw[4];
@@ -279,9 +361,9 @@ __device__ V3 shade_sample(const SceneView& sc, const FrameParams& fp, uint32_t 
     const float ramp = (float)py / (float)fp.height;  // Miss.hlsl:8
     return v3(0.0f, 0.2f, 0.7f - 0.3f * ramp);
   }
-  const InstanceRec* ir = sc.inst + hit.inst;
+  const HitInstance ir = load_hit_instance(sc, hit.inst);
   const V3 P = add(O, muls(D, hit.t));  // GetWorldHitPoint, Common.hlsl:24-27
-  const bool plane = ir->hit_group == 2u;
+  const bool plane = ir.hit_group == 2u;
   if (MODE == 0) {
     if (plane) {
       const LightRec& L0 = fp.lights[0];
@@ -329,8 +411,14 @@ __device__ __forceinline__ void flush_stats(const Counters& c, unsigned long lon
   }
 }
 
+#ifdef RT_TRACE_MIN_WAVES
+#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_MIN_WAVES, 8)))
+#else
+#define RT_TRACE_ATTR
+#endif
+
 template <int MODE, bool STATS>
-__global__ __launch_bounds__(kBlock) void k_trace_frame(SceneView sc, FrameParams fp,
+__global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void k_trace_frame(SceneView sc, FrameParams fp,
                                                         const uint32_t* __restrict__ rows,
                                                         uint32_t* __restrict__ rgba8,
                                                         float4* __restrict__ rgba32f,
@@ -342,7 +430,7 @@ __global__ __launch_bounds__(kBlock) void k_trace_frame(SceneView sc, FrameParam
   Counters cnt;
   if (px < fp.width && orow < fp.nrows) {
     const uint32_t py = rows ? rows[orow] : orow;
-    int* stk = s_stack + threadIdx.x;
+    const LaneStack stk = lane_stack(sc, s_stack, (blockIdx.y * gridDim.x + blockIdx.x) * kBlock + threadIdx.x);
     const uint32_t k = fp.spp_side;
     V3 acc = v3(0.0f, 0.0f, 0.0f);
     for (uint32_t sy = 0; sy < k; ++sy)
@@ -374,7 +462,7 @@ __global__ __launch_bounds__(kBlock) void k_trace_rays(SceneView sc, const float
     const float4 a = rays[2 * i], b = rays[2 * i + 1];
     HitRec h;
     const bool f = trace<ANY_HIT, STATS>(sc, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), a.w, b.w, h,
-                                         s_stack + threadIdx.x, cnt);
+                                         lane_stack(sc, s_stack, i), cnt);
     if (STATS) ++cnt.primary;
     hits[i] = make_uint4(__float_as_uint(f ? h.t : b.w), f ? h.inst : 0xffffffffu,
                          f ? h.prim : 0xffffffffu, f ? 1u : 0u);
@@ -400,7 +488,7 @@ template <int MODE, bool STATS>
 hipError_t launch_mode(const SceneView& sc, const FrameParams& fp, const uint32_t* rows, void* rgba8,
                        float* rgba32f, unsigned long long* stats, hipStream_t s) {
   dim3 grid((fp.width + 15) / 16, (fp.nrows + 15) / 16);
-  size_t lds = (size_t)sc.stack_cap * kBlock * sizeof(int);
+  size_t lds = (size_t)sc.lds_cap * kBlock * sizeof(int);
   hipLaunchKernelGGL((k_trace_frame<MODE, STATS>), grid, dim3(kBlock), lds, s, sc, fp, rows,
                      (uint32_t*)rgba8, (float4*)rgba32f, stats);
   return hipGetLastError();
@@ -433,7 +521,7 @@ hipError_t launch_trace_rays(const SceneView& sc, const float* rays, uint32_t n,
                              hipStream_t s) {
   if (n == 0) return hipSuccess;
   dim3 grid((n + kBlock - 1) / kBlock);
-  size_t lds = (size_t)sc.stack_cap * kBlock * sizeof(int);
+  size_t lds = (size_t)sc.lds_cap * kBlock * sizeof(int);
   const float4* r = (const float4*)rays;
   if (any_hit) {
     if (stats)

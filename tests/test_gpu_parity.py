@@ -71,8 +71,8 @@ def test_blas_bitwise_equal_to_oracle(model):
     assert np.array_equal(gn, on), f"{model}: {int((gn != on).any(axis=1).sum())} nodes differ"
     assert np.array_equal(gt, ot)
     info = c.blas_info(b)
-    prims, nn, depth = o.blas_info(ob)
-    assert (info.prim_count, info.node_count, info.depth) == (prims, nn, depth)
+    prims, nn, depth, mstack = o.blas_info(ob)
+    assert (info.prim_count, info.node_count, info.depth, info.max_stack) == (prims, nn, depth, mstack)
     # every primitive exactly once in leaf order
     assert np.array_equal(np.sort(gt[:, 3]), np.arange(prims, dtype=np.uint32))
     c.close()
@@ -117,7 +117,7 @@ def test_tlas_bitwise_equal_to_oracle(name):
     c, o = load_both(spec)
     assert np.array_equal(c.tlas_export(), o.export_tlas())
     info = c.tlas_info()
-    assert (info.prim_count, info.node_count, info.depth) == tuple(o.tlas_info())
+    assert (info.prim_count, info.node_count, info.depth, info.max_stack) == tuple(o.tlas_info())
     c.close()
 
 

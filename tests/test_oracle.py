@@ -15,9 +15,15 @@ SIZES = {"REF": (96, 54), "C1": (64, 64), "C2": (96, 54), "C2F": (96, 54), "C3":
          "C5": (48, 27)}
 
 
-def node_boxes(nodes):
+EMPTY = np.int32(-2**31 + 1)
+
+
+def unpack4(nodes):
+    """128-B 4-wide nodes -> lo (n,4,3), hi (n,4,3), child (n,4), count (n,)."""
     f = nodes.view(np.float32)
-    return f[:, 0:3], f[:, 3:6], f[:, 6:9], f[:, 9:12], nodes[:, 12].view(np.int32), nodes[:, 13].view(np.int32)
+    lo = np.stack([f[:, 0:4], f[:, 8:12], f[:, 16:20]], -1)
+    hi = np.stack([f[:, 4:8], f[:, 12:16], f[:, 20:24]], -1)
+    return lo, hi, nodes[:, 24:28].view(np.int32), nodes[:, 28]
 
 
 @pytest.mark.parametrize("model", ["teapot", "rabbit"])
@@ -26,27 +32,33 @@ def test_lbvh_invariants(model):
     o = oracle.Scene()
     b = o.add_blas(v, i)
     nodes, tris = o.export_blas(b)
-    lo0, hi0, lo1, hi1, c0, c1 = node_boxes(nodes)
+    lo, hi, ch, count = unpack4(nodes)
     n = tris.shape[0]
+    valid = ch != EMPTY
+    assert (valid.sum(1) == count).all() and (count >= 2).all() and (count <= 4).all()
     # every primitive exactly once in leaf order; every leaf slot referenced exactly once
     assert np.array_equal(np.sort(tris[:, 3]), np.arange(n))
-    leaves = np.concatenate([~c0[c0 < 0], ~c1[c1 < 0]])
+    leaves = ~ch[valid & (ch < 0)]
     assert np.array_equal(np.sort(leaves), np.arange(n))
-    internal = np.concatenate([c0[c0 >= 0], c1[c1 >= 0]])
-    assert np.array_equal(np.sort(internal), np.arange(1, n - 1))  # every node but the root has one parent
-    # parent box of a child == union of the child's two boxes (refit exactness)
-    for k, c in enumerate(c0):
-        if c >= 0:
-            assert np.array_equal(lo0[k], np.minimum(lo0[c], lo1[c])) and np.array_equal(hi0[k], np.maximum(hi0[c], hi1[c]))
+    # every node but the root has exactly one parent, and BFS order puts children after parents
+    internal = ch[valid & (ch >= 0)]
+    assert np.array_equal(np.sort(internal), np.arange(1, len(nodes)))
+    parents = np.repeat(np.arange(len(nodes))[:, None], 4, 1)[valid & (ch >= 0)]
+    assert (internal > parents).all()
+    # a child box is exactly the union of that child's own child boxes (refit exactness)
+    for k in range(len(nodes)):
+        for j in range(4):
+            c = ch[k, j]
+            if c >= 0:
+                m = ch[c] != EMPTY
+                assert np.array_equal(lo[k, j], lo[c][m].min(0)) and np.array_equal(hi[k, j], hi[c][m].max(0))
     # leaf boxes contain their triangle
     tf = tris.view(np.float32)
     v0, e1, e2 = tf[:, 0:3], tf[:, 4:7], tf[:, 8:11]
     pts = np.stack([v0, v0 + e1, v0 + e2], 1)
-    for k in range(len(c0)):
-        for c, lo, hi in ((c0[k], lo0[k], hi0[k]), (c1[k], lo1[k], hi1[k])):
-            if c < 0:
-                p = pts[~c]
-                assert (p >= lo - 1e-6).all() and (p <= hi + 1e-6).all()
+    for k, j in zip(*np.nonzero(valid & (ch < 0))):
+        p = pts[~ch[k, j]]
+        assert (p >= lo[k, j] - 1e-6).all() and (p <= hi[k, j] + 1e-6).all()
 
 
 @pytest.mark.parametrize("name", ["REF", "C1", "C2F", "C3", "C4"])

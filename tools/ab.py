@@ -1,0 +1,75 @@
+"""Interleaved A/B timing of library variants in ONE process (cdna guide §5.4 rule 24).
+
+python tools/ab.py --configs C2,C4 --rounds 7 --steps 20 base=realtimeraytracing_gradproject_amd/lib/librtamd.so \
+       w6=realtimeraytracing_gradproject_amd/lib/variants/w6/librtamd.so
+Each variant's frame must equal the first variant's bit for bit (RGBA8 and float) or the run fails.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import realtimeraytracing_gradproject_amd as rt  # noqa: E402
+from realtimeraytracing_gradproject_amd import scenes  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("variants", nargs="+")
+    ap.add_argument("--configs", default="C2")
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--schedule", type=int, default=0)
+    ap.add_argument("--mode", type=int, default=-1, help="override the shade mode (2 = primary rays only)")
+    a = ap.parse_args()
+    libs = {}
+    for v in a.variants:
+        name, path = v.split("=", 1)
+        libs[name] = rt._load(path)
+    res = {}
+    for cfg in a.configs.split(","):
+        spec = scenes.config(cfg)
+        if a.mode >= 0:
+            spec.mode = a.mode
+        W, H = spec.width, spec.height
+        stream = torch.cuda.Stream()
+        ctxs, outs = {}, {}
+        for name, lib in libs.items():
+            c = rt.Context(0, library=lib)
+            scenes.upload(c, spec)
+            c.set_schedule(a.schedule)
+            ctxs[name] = c
+            outs[name] = (torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda"),
+                          torch.zeros((H, W, 4), dtype=torch.float32, device="cuda"))
+            c.dispatch(W, H, outs[name][0], outs[name][1], stream=stream.cuda_stream)
+        torch.cuda.synchronize()
+        first = next(iter(libs))
+        for name in libs:
+            if not (torch.equal(outs[name][0], outs[first][0]) and
+                    torch.equal(outs[name][1].view(torch.int32), outs[first][1].view(torch.int32))):
+                raise SystemExit(f"{cfg}: variant {name} differs from {first}")
+        times = {n: [] for n in libs}
+        for r in range(a.rounds):
+            for name, c in ctxs.items():
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(a.steps):
+                    c.dispatch(W, H, outs[name][0], None, stream=stream.cuda_stream)
+                e1.record(stream)
+                torch.cuda.synchronize()
+                times[name].append(e0.elapsed_time(e1) / a.steps)
+        res[cfg] = {n: {"median_ms": round(statistics.median(t), 4), "min_ms": round(min(t), 4)} for n, t in times.items()}
+        for c in ctxs.values():
+            c.close()
+        print(cfg, json.dumps(res[cfg]), flush=True)
+
+
+if __name__ == "__main__":
+    main()
