@@ -63,6 +63,11 @@ struct rt_ctx {
   // traversal-stack overflow area in HBM for lanes whose path outgrows the LDS part
   int* d_ovf = nullptr;
   size_t ovf_cap = 0;
+  // scene pools read by the trace kernels (rebuilt by every rt_tlas_build)
+  rt::Bvh4Node* pool_nodes = nullptr;
+  rt::TriRec* pool_tris = nullptr;
+  size_t pool_nodes_cap = 0, pool_tris_cap = 0;
+  bool tlas_stale = false;  // a BLAS was rebuilt after the last rt_tlas_build
 };
 
 namespace {
@@ -247,6 +252,8 @@ rt_status rt_destroy(rt_ctx_t c) {
   if (c->d_rows) (void)hipFree(c->d_rows);
   if (c->wf.surf) (void)hipFree(c->wf.surf);
   if (c->d_ovf) (void)hipFree(c->d_ovf);
+  if (c->pool_nodes) (void)hipFree(c->pool_nodes);
+  if (c->pool_tris) (void)hipFree(c->pool_tris);
   if (c->wf.shadow_bits) (void)hipFree(c->wf.shadow_bits);
   if (c->wf.queue) (void)hipFree(c->wf.queue);
   if (c->wf.queue_count) (void)hipFree(c->wf.queue_count);
@@ -283,6 +290,7 @@ rt_status rt_blas_rebuild(rt_ctx_t c, rt_blas_t id, const void* vtx, uint32_t vc
   }
   c->blas[id].release();
   c->blas[id] = b;
+  c->tlas_stale = c->inst != nullptr;  // the scene pool holds the old tree until rt_tlas_build
   return RT_OK;
 }
 
@@ -328,6 +336,19 @@ rt_status rt_tlas_build(rt_ctx_t c, const rt_instance* in, uint32_t n, int updat
   }
   std::vector<rt::InstanceRec> recs(n);
   std::vector<float> bb((size_t)n * 6);
+  // scene pool layout: [TLAS (room for max(n-1,1) nodes) | BLAS 0 | BLAS 1 | ...], triangles
+  // [BLAS 0 | BLAS 1 | ...]
+  const uint32_t tlas_cap = n > 1 ? n - 1 : 1;
+  std::vector<uint32_t> node_base(c->blas.size()), tri_base(c->blas.size());
+  size_t pool_n = tlas_cap, pool_t = 0;
+  for (size_t k = 0; k < c->blas.size(); ++k) {
+    node_base[k] = (uint32_t)pool_n;
+    tri_base[k] = (uint32_t)pool_t;
+    pool_n += c->blas[k].nnodes;
+    pool_t += c->blas[k].ntri;
+  }
+  if (pool_n > 0x7fffffffull / sizeof(rt::Bvh4Node) || pool_t > 0x7fffffffull / sizeof(rt::TriRec))
+    return fail(c, RT_E_UNSUPPORTED, "rt_tlas_build: scene pool exceeds 2 GB of nodes or triangles");
   for (uint32_t i = 0; i < n; ++i) {
     if (in[i].blas >= c->blas.size()) return fail(c, RT_E_INVALID, "rt_tlas_build: unknown BLAS id");
     if (in[i].hit_group != RT_HITGROUP_MODEL && in[i].hit_group != RT_HITGROUP_PLANE)
@@ -343,6 +364,7 @@ rt_status rt_tlas_build(rt_ctx_t c, const rt_instance* in, uint32_t n, int updat
     r.tris = b.tris;
     r.vtx = b.vtx;
     r.idx = b.idx;
+    r.pool_root = node_base[in[i].blas];
     for (int k = 0; k < 6; ++k) bb[i * 6 + k] = b.bounds[k];
   }
   hipStream_t s = c->stream;
@@ -376,6 +398,32 @@ rt_status rt_tlas_build(rt_ctx_t c, const rt_instance* in, uint32_t n, int updat
   (void)hipFree(d_bb);
   (void)hipFree(d_box);
   if (e != hipSuccess) return hip_fail(c, e, "TLAS build");
+  // scene pools (rebased copies; the per-BLAS arrays stay for export and rebuilds)
+  if (pool_n > c->pool_nodes_cap) {
+    if (c->pool_nodes) (void)hipFree(c->pool_nodes);
+    c->pool_nodes = nullptr;
+    c->pool_nodes_cap = 0;
+    HIPCHK(c, hipMalloc(&c->pool_nodes, pool_n * sizeof(rt::Bvh4Node)), "hipMalloc(node pool)");
+    c->pool_nodes_cap = pool_n;
+  }
+  if (pool_t > c->pool_tris_cap) {
+    if (c->pool_tris) (void)hipFree(c->pool_tris);
+    c->pool_tris = nullptr;
+    c->pool_tris_cap = 0;
+    HIPCHK(c, hipMalloc(&c->pool_tris, pool_t * sizeof(rt::TriRec)), "hipMalloc(triangle pool)");
+    c->pool_tris_cap = pool_t;
+  }
+  e = rt::pool_rebase(c->tlas_nodes, c->tlas_nodes_n, 0, -1, c->pool_nodes, s);
+  for (size_t k = 0; k < c->blas.size() && e == hipSuccess; ++k) {
+    const DeviceBlas& b = c->blas[k];
+    e = rt::pool_rebase(b.nodes, b.nnodes, node_base[k], tri_base[k], c->pool_nodes + node_base[k], s);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(c->pool_tris + tri_base[k], b.tris, (size_t)b.ntri * sizeof(rt::TriRec),
+                         hipMemcpyDeviceToDevice, s);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hip_fail(c, e, "scene pool");
+  c->tlas_stale = false;
   c->ninst = n;
   c->tlas_ms = ms;
   c->inst_host.assign(in, in + n);
@@ -445,6 +493,8 @@ rt_status rt_set_stats(rt_ctx_t c, int enable) {
 
 static rt::SceneView scene_view(rt_ctx* c) {
   rt::SceneView sv;
+  sv.pool_nodes = c->pool_nodes;
+  sv.pool_tris = c->pool_tris;
   sv.tlas = c->tlas_nodes;
   sv.inst = c->inst;
   uint32_t maxb = 0;
@@ -478,6 +528,7 @@ rt_status rt_dispatch_rays(rt_ctx_t c, uint32_t W, uint32_t H, const uint32_t* r
                            void* rgba8, float* rgba32f, void* stream) {
   if (!c) return RT_E_INVALID;
   if (!c->inst) return fail(c, RT_E_INVALID, "rt_dispatch_rays: no TLAS built");
+  if (c->tlas_stale) return fail(c, RT_E_INVALID, "rt_dispatch_rays: BLAS rebuilt since the last rt_tlas_build");
   if (!c->have_camera || !c->have_shading) return fail(c, RT_E_INVALID, "rt_dispatch_rays: camera/shading not set");
   if (W == 0 || H == 0 || !rgba8) return fail(c, RT_E_INVALID, "rt_dispatch_rays: bad size or output");
   if (!rows) nrows = H;
@@ -528,6 +579,7 @@ rt_status rt_trace_rays(rt_ctx_t c, const float* rays, uint32_t n, int any_hit, 
                         void* stream) {
   if (!c || (!rays && n) || (!hits && n)) return fail(c, RT_E_INVALID, "rt_trace_rays: null argument");
   if (!c->inst) return fail(c, RT_E_INVALID, "rt_trace_rays: no TLAS built");
+  if (c->tlas_stale) return fail(c, RT_E_INVALID, "rt_trace_rays: BLAS rebuilt since the last rt_tlas_build");
   (void)hipSetDevice(c->device);
   rt::SceneView sv = scene_view(c);
   if (sv.stack_cap > rt::kMaxTraversalStack)

@@ -83,8 +83,10 @@ struct alignas(16) InstanceRec {
   uint32_t instance_id;
   uint32_t hit_group;
   uint32_t blas;
-  const Bvh4Node* nodes;  // BLAS root = node 0
+  const Bvh4Node* nodes;  // the BLAS's own arrays (root = node 0)
   const TriRec* tris;
+  uint32_t pool_root;     // the BLAS root's index in the scene pool (see SceneView)
+  uint32_t pad_[3];
   const float* vtx;       // 6 floats per vertex: pos.xyz, normal.xyz (stride 24 B)
   const uint32_t* idx;    // triangle list, or nullptr for non-indexed geometry
 };
@@ -117,7 +119,14 @@ struct FrameParams {
   uint32_t nrows;
 };
 
+// The trace kernels read one node pool and one triangle pool per scene: [TLAS | BLAS 0 | BLAS 1 ..]
+// with child refs rebased to pool indices (BLAS leaves -> ~(global triangle slot)). A uniform base
+// (SGPR) plus a 32-bit per-lane byte offset is the global_load saddr form: one VALU add per load
+// address instead of 64-bit pointer arithmetic, and per-lane octant offsets pick the near/far
+// planes of a node with no min/max.
 struct SceneView {
+  const Bvh4Node* pool_nodes;
+  const TriRec* pool_tris;
   const Bvh4Node* tlas;
   const InstanceRec* inst;
   int stack_cap;       // worst-case entries per lane (exact bound from the trees)
@@ -231,19 +240,23 @@ RT_HD uint32_t unorm8(float c) {
   return (uint32_t)(c * 255.0f + 0.5f);
 }
 
-// Slab tests of the 4 children of a Bvh4Node against the ray segment [tmin, tbest].
+// Slab tests of the 4 children of a Bvh4Node against the ray segment [tmin, tbest], given each
+// axis's near and far planes (the ray's octant picks them: near = lo where invd >= 0, else hi).
 // tn[k] = entry distance of child k, or +inf if it is missed or empty. Conservative (tfar
 // widened by 1 + 4e-7) so BVH culling never rejects a triangle Moller-Trumbore accepts.
-RT_HD void slab4(const float* lox, const float* hix, const float* loy, const float* hiy,
-                 const float* loz, const float* hiz, const int32_t* child, V3 invd, V3 noinv,
-                 float tmin, float tbest, float tn[4]) {
+// Bitwise equal to the min/max form of oracle oslab4: for invd > 0 the exact products lo*invd <=
+// hi*invd and the fma rounding is monotone, so fma(lo,..) <= fma(hi,..) (reversed for invd < 0;
+// safe_inv never returns 0), i.e. min/max of the two plane distances is the near/far plane.
+RT_HD void slab4_octant(const float* nx, const float* fx, const float* ny, const float* fy,
+                        const float* nz, const float* fz, const int32_t* child, V3 invd, V3 noinv,
+                        float tmin, float tbest, float tn[4]) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    float tlx = __builtin_fmaf(lox[k], invd.x, noinv.x), thx = __builtin_fmaf(hix[k], invd.x, noinv.x);
-    float tly = __builtin_fmaf(loy[k], invd.y, noinv.y), thy = __builtin_fmaf(hiy[k], invd.y, noinv.y);
-    float tlz = __builtin_fmaf(loz[k], invd.z, noinv.z), thz = __builtin_fmaf(hiz[k], invd.z, noinv.z);
-    float n = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), tmin));
-    float f = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tbest));
+    const float tnx = __builtin_fmaf(nx[k], invd.x, noinv.x), tfx = __builtin_fmaf(fx[k], invd.x, noinv.x);
+    const float tny = __builtin_fmaf(ny[k], invd.y, noinv.y), tfy = __builtin_fmaf(fy[k], invd.y, noinv.y);
+    const float tnz = __builtin_fmaf(nz[k], invd.z, noinv.z), tfz = __builtin_fmaf(fz[k], invd.z, noinv.z);
+    const float n = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
+    const float f = fminf(fminf(tfx, tfy), fminf(tfz, tbest));
     tn[k] = (child[k] != kEmptyChild && n <= f * 1.0000004f) ? n : __builtin_inff();
   }
 }

@@ -25,6 +25,10 @@ hipError_t blas_prepare(const float* d_vtx, const uint32_t* d_idx, uint32_t ntri
 // Gathers triangles into leaf order.
 hipError_t blas_reorder(const TriRec* d_in, const uint32_t* d_sorted, uint32_t n, TriRec* d_out,
                         hipStream_t stream);
+// Copies n nodes into the scene pool at dst, rebasing internal refs by node_base and leaf refs
+// (~slot) by tri_base (TLAS: node_base = 0, tri_base = -1 keeps ~instance refs).
+hipError_t pool_rebase(const Bvh4Node* src, uint32_t n, uint32_t node_base, int64_t tri_base, Bvh4Node* dst,
+                       hipStream_t stream);
 // World boxes of instances: the 8 corners of each BLAS root box through the instance transform.
 hipError_t tlas_prepare(const InstanceRec* d_inst, const float* d_blas_bounds, uint32_t n,
                         float* d_primbox, hipStream_t stream);

@@ -560,6 +560,28 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
   return hipSuccess;
 }
 
+namespace {
+__global__ void k_pool_rebase(const Bvh4Node* __restrict__ src, uint32_t n, uint32_t node_base, int64_t tri_base,
+                              Bvh4Node* __restrict__ dst) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Bvh4Node nd = src[i];
+  for (int k = 0; k < 4; ++k) {
+    const int32_t c = nd.child[k];
+    if (c == kEmptyChild) continue;
+    if (c >= 0) nd.child[k] = c + (int32_t)node_base;
+    else if (tri_base >= 0) nd.child[k] = ~(int32_t)((int64_t)(~c) + tri_base);
+  }
+  dst[i] = nd;
+}
+}  // namespace
+
+hipError_t pool_rebase(const Bvh4Node* src, uint32_t n, uint32_t node_base, int64_t tri_base, Bvh4Node* dst,
+                       hipStream_t s) {
+  k_pool_rebase<<<grid1(n, 256), 256, 0, s>>>(src, n, node_base, tri_base, dst);
+  return hipGetLastError();
+}
+
 hipError_t blas_prepare(const float* d_vtx, const uint32_t* d_idx, uint32_t ntri, TriRec* d_tris,
                         float* d_primbox, hipStream_t s) {
   k_tri_setup<<<grid1(ntri, 256), 256, 0, s>>>(d_vtx, d_idx, ntri, d_tris, d_primbox);

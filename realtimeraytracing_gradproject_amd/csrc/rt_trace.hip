@@ -12,8 +12,9 @@
 // SBT dispatch (D3D12HelloTriangle.cpp:1064-1080) becomes a switch on the instance hit group.
 //
 // Execution model: one lane = one pixel, a wave64 = an 8x8 pixel tile, a 256-thread workgroup =
-// 16x16 pixels. Per-lane traversal stack in LDS laid out [entry][lane] (bank = lane: conflict
-// free). Child-pair nodes: one 64-B node fetch tests both children; near child first.
+// 16x16 pixels. 4-wide BVH nodes (128 B, one cache line) from the scene pool: one node fetch
+// tests four children, visited nearest first. Per-lane traversal stack in LDS laid out
+// [entry][lane] (bank = lane: conflict free) with an HBM overflow for deep paths.
 #include <hip/hip_runtime.h>
 
 #include "rt_internal.hpp"
@@ -47,13 +48,9 @@ __device__ __forceinline__ const RT_GLOBAL T* gp(const T* p) {
   return (const RT_GLOBAL T*)p;
 }
 
-// Two-level stack traversal over 4-wide nodes. ANY_HIT: first accepted hit terminates (shadow
-// rays). Closest hit keeps the lexicographic minimum of (t, instance, primitive): independent of
-// traversal order. Children are visited nearest first (sort4); the oracle mirrors the order, so
-// the box/triangle test counters match it exactly. The per-lane stack lives in LDS as
-// [entry][lane] (bank = lane: conflict free), sized to the worst case of the scene's trees.
 // Per-lane stack: entries [0, lds_cap) in LDS ([entry][lane], bank = lane), deeper entries in
 // the HBM overflow area ([entry - lds_cap][lane]), touched only by paths deeper than lds_cap.
+// The capacity is the exact worst case of the scene's trees, so nothing is ever dropped.
 struct LaneStack {
   int* lds;                 // s_stack + threadIdx.x
   RT_GLOBAL int* ovf;       // overflow base + global lane (null when stack_cap <= lds_cap)
@@ -81,14 +78,42 @@ __device__ __forceinline__ LaneStack lane_stack(const SceneView& sc, int* s_stac
   return st;
 }
 
+// Pool loads: uniform (SGPR) base + 32-bit per-lane byte offset, the global_load saddr form.
+__device__ __forceinline__ f4v ldf4(const RT_GLOBAL char* base, uint32_t off) {
+  return *reinterpret_cast<const RT_GLOBAL f4v*>(base + off);
+}
+__device__ __forceinline__ i4v ldi4(const RT_GLOBAL char* base, uint32_t off) {
+  return *reinterpret_cast<const RT_GLOBAL i4v*>(base + off);
+}
+
+// Byte offsets of the near planes inside a Bvh4Node for the ray's octant (the far plane of an
+// axis is the near one ^ 16): lox 0, hix 16, loy 32, hiy 48, loz 64, hiz 80.
+struct Octant {
+  uint32_t x, y, z;
+};
+__device__ __forceinline__ Octant octant(V3 invd) {
+  Octant q;
+  q.x = invd.x < 0.0f ? 16u : 0u;
+  q.y = invd.y < 0.0f ? 48u : 32u;
+  q.z = invd.z < 0.0f ? 80u : 64u;
+  return q;
+}
+
+// Two-level stack traversal over the scene pool. ANY_HIT: first accepted hit terminates (shadow
+// rays). Closest hit keeps the lexicographic minimum of (t, instance, primitive): independent of
+// traversal order. Children are visited nearest first (sort4); the oracle mirrors the order, so
+// the box/triangle test counters match it exactly. Entering an instance pushes a sentinel and
+// moves to the BLAS root in the pool; popping the sentinel restores the world-space ray.
 template <bool ANY_HIT, bool STATS>
 __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, HitRec& hit,
                       const LaneStack& stk, Counters& cnt) {
   const V3 winvd = v3(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
   const V3 wnoinv = neg(mul(o, winvd));
+  const Octant woct = octant(winvd);
   V3 ro = o, rd = d, rinvd = winvd, rnoinv = wnoinv;
-  const RT_GLOBAL Bvh4Node* nodes = gp(sc.tlas);
-  const RT_GLOBAL TriRec* tris = nullptr;
+  Octant oct = woct;
+  const RT_GLOBAL char* pn = (const RT_GLOBAL char*)sc.pool_nodes;
+  const RT_GLOBAL char* pt = (const RT_GLOBAL char*)sc.pool_tris;
   uint32_t cur = 0;
   bool in_blas = false;
   bool found = false;
@@ -101,15 +126,17 @@ __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, H
   hit.u = hit.v = 0.0f;
   while (true) {
     if (ref >= 0) {
-      const RT_GLOBAL f4v* np = reinterpret_cast<const RT_GLOBAL f4v*>(nodes + ref);
-      const f4v a0 = np[0], a1 = np[1], a2 = np[2], a3 = np[3], a4 = np[4], a5 = np[5];
-      const i4v ch = reinterpret_cast<const RT_GLOBAL i4v*>(np)[6];
-      const float lox[4] = {a0.x, a0.y, a0.z, a0.w}, hix[4] = {a1.x, a1.y, a1.z, a1.w};
-      const float loy[4] = {a2.x, a2.y, a2.z, a2.w}, hiy[4] = {a3.x, a3.y, a3.z, a3.w};
-      const float loz[4] = {a4.x, a4.y, a4.z, a4.w}, hiz[4] = {a5.x, a5.y, a5.z, a5.w};
+      const uint32_t off = (uint32_t)ref << 7;
+      const f4v a0 = ldf4(pn, off + oct.x), a1 = ldf4(pn, off + (oct.x ^ 16u));
+      const f4v a2 = ldf4(pn, off + oct.y), a3 = ldf4(pn, off + (oct.y ^ 16u));
+      const f4v a4 = ldf4(pn, off + oct.z), a5 = ldf4(pn, off + (oct.z ^ 16u));
+      const i4v ch = ldi4(pn, off + 96u);
+      const float nx[4] = {a0.x, a0.y, a0.z, a0.w}, fx[4] = {a1.x, a1.y, a1.z, a1.w};
+      const float ny[4] = {a2.x, a2.y, a2.z, a2.w}, fy[4] = {a3.x, a3.y, a3.z, a3.w};
+      const float nz[4] = {a4.x, a4.y, a4.z, a4.w}, fz[4] = {a5.x, a5.y, a5.z, a5.w};
       int32_t r[4] = {ch.x, ch.y, ch.z, ch.w};
       float tn[4];
-      slab4(lox, hix, loy, hiy, loz, hiz, r, rinvd, rnoinv, tmin, hit.t, tn);
+      slab4_octant(nx, fx, ny, fy, nz, fz, r, rinvd, rnoinv, tmin, hit.t, tn);
       if (STATS)
         cnt.aabb += (uint32_t)(r[0] != kEmptyChild) + (uint32_t)(r[1] != kEmptyChild) +
                     (uint32_t)(r[2] != kEmptyChild) + (uint32_t)(r[3] != kEmptyChild);
@@ -165,16 +192,15 @@ __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, H
         rd = xform_dir(m, d);
         rinvd = v3(safe_inv(rd.x), safe_inv(rd.y), safe_inv(rd.z));
         rnoinv = neg(mul(ro, rinvd));
-        nodes = gp(ir->nodes);
-        tris = gp(ir->tris);
+        oct = octant(rinvd);
         in_blas = true;
-        ref = 0;
+        ref = (int)ir->pool_root;
         continue;
       }
       if (STATS) ++cnt.overflow;  // no room for the way back: skip this instance
     } else {
-      const RT_GLOBAL f4v* tp = reinterpret_cast<const RT_GLOBAL f4v*>(tris + (~ref));
-      const f4v a = tp[0], b = tp[1], c = tp[2];
+      const uint32_t toff = (uint32_t)(~ref) * (uint32_t)sizeof(TriRec);
+      const f4v a = ldf4(pt, toff), b = ldf4(pt, toff + 16u), c = ldf4(pt, toff + 32u);
       if (STATS) ++cnt.tri;
       float t, u, v;
       if (moller_trumbore(ro, rd, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), v3(c.x, c.y, c.z), t, u, v) &&
@@ -200,11 +226,11 @@ __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, H
       ref = stk.get(sp);
       if (ref != kStackSentinel) break;
       in_blas = false;
-      nodes = gp(sc.tlas);
       ro = o;
       rd = d;
       rinvd = winvd;
       rnoinv = wnoinv;
+      oct = woct;
     }
   }
 }
