@@ -47,7 +47,7 @@ def parse():
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="C2", choices=[c for c in scenes.CONFIGS])
-    p.add_argument("--schedule", default="megakernel", choices=["megakernel", "wavefront"])
+    p.add_argument("--schedule", default="packet", choices=["packet", "lane"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=2.0, help="minimum wall time of the CPU baseline sample")
     p.add_argument("--save-image", default="", help="write the rank-0 frame as .npy")
@@ -79,7 +79,7 @@ def cpu_baseline(spec, seconds: float):
     frames = 0
     t0 = time.perf_counter()
     while True:
-        _, _, st = o.render_spec(spec, nthreads=threads, want_float=False)
+        _, _, st = o.render_spec(spec, nthreads=threads, want_float=False, schedule=1)  # per-ray: the CPU form
         rays += int(st[0] + st[1])
         frames += 1
         dt = time.perf_counter() - t0
@@ -140,7 +140,7 @@ def main():
     W, H = spec.width, spec.height
     ctx = rt.Context(local)
     scenes.upload(ctx, spec)
-    ctx.set_schedule(rt.RT_SCHED_WAVEFRONT if a.schedule == "wavefront" else rt.RT_SCHED_MEGAKERNEL)
+    ctx.set_schedule(rt.RT_SCHED_LANE if a.schedule == "lane" else rt.RT_SCHED_PACKET)
     binfo = [ctx.blas_info(b) for b in range(len(spec.meshes))]
     tinfo = ctx.tlas_info()
 
@@ -218,7 +218,7 @@ def main():
             cpu = cpu_baseline(spec, a.cpu_seconds)
         extra = []
         if not distributed and a.extra:
-            sched = rt.RT_SCHED_WAVEFRONT if a.schedule == "wavefront" else rt.RT_SCHED_MEGAKERNEL
+            sched = rt.RT_SCHED_LANE if a.schedule == "lane" else rt.RT_SCHED_PACKET
             for name in a.extra.split(","):
                 extra.append(measure_config(name, max(5, a.steps // 2), 2, sched))
         out = {

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RT_API_VERSION 1
+#define RT_API_VERSION 2
 
 typedef struct rt_ctx* rt_ctx_t;
 typedef struct rt_mesh* rt_mesh_t;
@@ -54,10 +54,13 @@ enum {
   RT_SHADE_PRIMARY = 2         /* primary rays only: Lambert over the lights, no shadow rays (config C1) */
 };
 
-/* Dispatch variants (same image, different kernel schedule). */
+/* Trace schedules of the one-launch frame kernel (raygen + traversal + shading + shadow rays).
+ * Same image; the traversal counters (rt_stats) follow the schedule. */
 enum {
-  RT_SCHED_MEGAKERNEL = 0, /* one launch: raygen + traversal + shading + shadow rays per lane */
-  RT_SCHED_WAVEFRONT = 1   /* primary/shade kernel -> ballot-compacted shadow queue -> shadow kernel -> resolve */
+  RT_SCHED_PACKET = 0, /* default: each wave (8 x 8 pixels) walks the trees as one packet: scalar
+                          node fetches, ballot child decisions, a wave-uniform stack. Runs when the
+                          scene's worst-case stack is below 64 entries, else falls back to LANE */
+  RT_SCHED_LANE = 1    /* one independent traversal per lane (LDS stack + HBM overflow) */
 };
 
 /* One TLAS instance (TopLevelASGenerator::AddInstance, TopLevelASGenerator.h:88-99,
@@ -166,7 +169,7 @@ rt_status rt_set_camera(rt_ctx_t ctx, const float cb[64]);
  * (D3D12HelloTriangle.cpp:424-428). nlights in [1, 16]. spp in {1, 4, 9, 16} (k x k stratified). */
 rt_status rt_set_shading(rt_ctx_t ctx, const rt_light* lights, uint32_t nlights,
                          const rt_material* material, int shade_mode, int spp);
-/* RT_SCHED_MEGAKERNEL (default) or RT_SCHED_WAVEFRONT. */
+/* RT_SCHED_PACKET (default) or RT_SCHED_LANE. */
 rt_status rt_set_schedule(rt_ctx_t ctx, int schedule);
 /* Enables device counters (rt_stats). Costs time: off for timed runs. */
 rt_status rt_set_stats(rt_ctx_t ctx, int enable);

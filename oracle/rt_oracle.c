@@ -261,7 +261,45 @@ static void box_of(int c, const float* nbox, const float* primbox, const uint32_
 }
 
 /* builds nodes over n prim boxes; sorted receives leaf order; returns depth */
-/* collapse every other level of the binary tree into 4-wide nodes, BFS order (k_collapse) */
+static float half_area(const float* b) {
+  const float dx = b[3] - b[0], dy = b[4] - b[1], dz = b[5] - b[2];
+  return (dx * dy + dy * dz) + dz * dx;
+}
+
+/* children of the 4-wide node rooted at binary node `root`: its two children, then the internal
+ * candidate with the largest surface area (lowest slot on ties) is opened until there are four
+ * (gather4 in rt_lbvh.hip) */
+static int gather4(const onode* bin, int root, int ref[4], float box[4][6]) {
+  const onode* b = &bin[root];
+  ref[0] = b->c0;
+  ref[1] = b->c1;
+  for (int a = 0; a < 3; ++a) {
+    box[0][a] = b->lo0[a]; box[0][3 + a] = b->hi0[a];
+    box[1][a] = b->lo1[a]; box[1][3 + a] = b->hi1[a];
+  }
+  int cnt = 2;
+  while (cnt < 4) {
+    int best = -1;
+    float bsa = 0.0f;
+    for (int j = 0; j < cnt; ++j) {
+      if (ref[j] < 0) continue;
+      const float sa = half_area(box[j]);
+      if (best < 0 || sa > bsa) { best = j; bsa = sa; }
+    }
+    if (best < 0) break;
+    const onode* g = &bin[ref[best]];
+    ref[best] = g->c0;
+    ref[cnt] = g->c1;
+    for (int a = 0; a < 3; ++a) {
+      box[best][a] = g->lo0[a]; box[best][3 + a] = g->hi0[a];
+      box[cnt][a] = g->lo1[a]; box[cnt][3 + a] = g->hi1[a];
+    }
+    ++cnt;
+  }
+  return cnt;
+}
+
+/* collapse the binary tree into 4-wide nodes (greedy largest-area opening), BFS order (k_collapse) */
 static uint32_t collapse(const onode* bin, uint32_t nbin, o4node* out, uint32_t* count, uint32_t* max_stack) {
   int* q = (int*)malloc((size_t)nbin * sizeof(int) + sizeof(int));
   int* ps = (int*)calloc((size_t)nbin + 1, sizeof(int)); /* siblings left on the stack above a node */
@@ -272,30 +310,9 @@ static uint32_t collapse(const onode* bin, uint32_t nbin, o4node* out, uint32_t*
   while (head < level_end) {
     ++depth;
     for (; head < level_end; ++head) {
-      const onode* b = &bin[q[head]];
       int ref[4];
       float box[4][6];
-      int cnt = 0;
-      for (int k = 0; k < 2; ++k) {
-        int c = k ? b->c1 : b->c0;
-        const float* lo = k ? b->lo1 : b->lo0;
-        const float* hi = k ? b->hi1 : b->hi0;
-        if (c < 0) {
-          ref[cnt] = c;
-          for (int a = 0; a < 3; ++a) { box[cnt][a] = lo[a]; box[cnt][3 + a] = hi[a]; }
-          ++cnt;
-        } else {
-          const onode* g = &bin[c];
-          for (int qq = 0; qq < 2; ++qq) {
-            ref[cnt] = qq ? g->c1 : g->c0;
-            for (int a = 0; a < 3; ++a) {
-              box[cnt][a] = qq ? g->lo1[a] : g->lo0[a];
-              box[cnt][3 + a] = qq ? g->hi1[a] : g->hi0[a];
-            }
-            ++cnt;
-          }
-        }
-      }
+      const int cnt = gather4(bin, q[head], ref, box);
       o4node nd;
       memset(&nd, 0, sizeof(nd));
       for (int j = 0; j < 4; ++j) {
@@ -726,6 +743,127 @@ static int otrace(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax,
   }
 }
 
+/* ---------------------------------------------------------------------------------------- */
+/* Wave-packet traversal (trace_packet in rt_trace.hip): the 64 lanes of a wave walk one path */
+/* together; a child is entered when any live lane's slab test accepts it. Emulated lane by   */
+/* lane so the traversal order and the per-lane counters are those of the device.            */
+/* ---------------------------------------------------------------------------------------- */
+#define OPK 64
+
+typedef struct {
+  vec3 o[OPK], d[OPK], invd[OPK], no[OPK];
+} opkray;
+
+static uint32_t f2bits(float x) { uint32_t b; memcpy(&b, &x, 4); return b; }
+
+/* one node: returns 0 when no child is entered, else pushes the others and sets *next */
+static int opk_node(const o4node* nd, const opkray* ry, float tmin, const ohit* h, const int* live, int lead,
+                    int* stack, int* sp, int cap, int* next, ostats* st) {
+  uint64_t hm[4] = {0, 0, 0, 0};
+  uint32_t vkey[OPK][4];
+  int nvalid = 0;
+  for (int k = 0; k < 4; ++k) nvalid += nd->child[k] != O_EMPTY;
+  for (int l = 0; l < OPK; ++l) {
+    for (int k = 0; k < 4; ++k) {
+      float tlx = fmaf(nd->lox[k], ry->invd[l].x, ry->no[l].x), thx = fmaf(nd->hix[k], ry->invd[l].x, ry->no[l].x);
+      float tly = fmaf(nd->loy[k], ry->invd[l].y, ry->no[l].y), thy = fmaf(nd->hiy[k], ry->invd[l].y, ry->no[l].y);
+      float tlz = fmaf(nd->loz[k], ry->invd[l].z, ry->no[l].z), thz = fmaf(nd->hiz[k], ry->invd[l].z, ry->no[l].z);
+      float n = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), tmin));
+      float f = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), h[l].t));
+      int hit = live[l] && n <= f * 1.0000004f;
+      if (hit && nd->child[k] != O_EMPTY) hm[k] |= 1ull << l;
+      vkey[l][k] = hit ? (f2bits(n) & 0x7fffffffu) : 0x7f800000u;
+    }
+    if (live[l]) st->v[2] += (uint64_t)nvalid;
+  }
+  if ((hm[0] | hm[1] | hm[2] | hm[3]) == 0) return 0;
+  uint32_t key[4];
+  for (int k = 0; k < 4; ++k) key[k] = hm[k] ? vkey[lead][k] : 0xffffffffu;
+  /* nearest first (lowest slot on ties), the other entered children pushed in descending slot order */
+  uint32_t kb = key[0];
+  int rb = nd->child[0], ib = 0;
+  for (int k = 1; k < 4; ++k)
+    if (key[k] < kb) { kb = key[k]; rb = nd->child[k]; ib = k; }
+  for (int k = 3; k >= 0; --k) {
+    if (key[k] == 0xffffffffu || k == ib) continue;
+    if (*sp >= cap) /* never: cap is the exact worst case; counted per live lane like the device */
+      for (int l = 0; l < OPK; ++l) st->v[5] += live[l] ? 1u : 0u;
+    if (*sp < OPK) stack[*sp] = nd->child[k];
+    ++*sp;
+  }
+  *next = rb;
+  return 1;
+}
+
+static int olead(const int* live) {
+  for (int l = 0; l < OPK; ++l) if (live[l]) return l;
+  return -1;
+}
+
+static void opacket(const oracle_scene* s, const vec3* o, const vec3* d, float tmin, float tmax, int any,
+                    const int* alive, ohit* h, int* found, ostats* st) {
+  int live[OPK];
+  opkray w, b;
+  for (int l = 0; l < OPK; ++l) {
+    live[l] = alive[l];
+    found[l] = 0;
+    h[l].t = tmax; h[l].inst = 0xffffffffu; h[l].prim = 0xffffffffu; h[l].u = h[l].v = 0.0f;
+    w.o[l] = o[l]; w.d[l] = d[l];
+    w.invd[l] = mk(sinv(d[l].x), sinv(d[l].y), sinv(d[l].z));
+    w.no[l] = vneg(vmul(o[l], w.invd[l]));
+  }
+  int lead = olead(live);
+  if (lead < 0) return;
+  uint32_t maxb = 0;
+  for (int q = 0; q < s->nblas; ++q) if (s->blas[q].max_stack > maxb) maxb = s->blas[q].max_stack;
+  const int cap = (int)(s->tlas_max_stack + 1 + maxb); /* < 64 whenever the packet path runs */
+  int stack[OPK];
+  int sp = 0, ref = 0, next;
+  for (;;) {
+    if (ref >= 0) {
+      if (opk_node(s->tlas + ref, &w, tmin, h, live, lead, stack, &sp, cap, &next, st)) { ref = next; continue; }
+    } else {
+      const uint32_t cur = (uint32_t)(~ref);
+      const oinst* ir = &s->inst[cur];
+      const oblas* bl = &s->blas[ir->blas];
+      for (int l = 0; l < OPK; ++l) {
+        if (live[l]) st->v[4]++;
+        b.o[l] = xpoint(ir->w2o, o[l]);
+        b.d[l] = xdir(ir->w2o, d[l]);
+        b.invd[l] = mk(sinv(b.d[l].x), sinv(b.d[l].y), sinv(b.d[l].z));
+        b.no[l] = vneg(vmul(b.o[l], b.invd[l]));
+      }
+      const int base = sp;
+      int bref = 0;
+      for (;;) {
+        if (bref >= 0) {
+          if (opk_node(bl->nodes + bref, &b, tmin, h, live, lead, stack, &sp, cap, &next, st)) { bref = next; continue; }
+        } else {
+          const otri* tr = bl->tris + (~bref);
+          for (int l = 0; l < OPK; ++l) {
+            if (!live[l]) continue;
+            float t, u, v;
+            st->v[3]++;
+            if (omt(b.o[l], b.d[l], tr, &t, &u, &v) && t >= tmin && better(t, cur, tr->prim, &h[l])) {
+              h[l].t = t; h[l].u = u; h[l].v = v; h[l].inst = cur; h[l].prim = tr->prim;
+              found[l] = 1;
+              if (any) live[l] = 0;
+            }
+          }
+          if (any) {
+            lead = olead(live);
+            if (lead < 0) return;
+          }
+        }
+        if (sp == base) break;
+        bref = stack[--sp];
+      }
+    }
+    if (sp == 0) return;
+    ref = stack[--sp];
+  }
+}
+
 /* every triangle of every instance, original primitive order */
 static int obrute(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax, int any, ohit* h, ostats* st) {
   int found = 0;
@@ -917,8 +1055,8 @@ static void hlsl_mul4(const float* m, const float v[4], float r[4]) {
   for (int i = 0; i < 4; ++i) r[i] = ((m[i] * v[0] + m[4 + i] * v[1]) + m[8 + i] * v[2]) + m[12 + i] * v[3];
 }
 
-/* RayGen (RayGen.hlsl:28-43) + hit/miss programs for one camera sample */
-static vec3 osample(const octx* c, uint32_t px, uint32_t py, float ox, float oy, ostats* st) {
+/* RayGen (RayGen.hlsl:28-43): camera ray of one sample */
+static void oraygen(const octx* c, uint32_t px, uint32_t py, float ox, float oy, vec3* O, vec3* D) {
   float dx = (((float)px + ox) / (float)c->W) * 2.0f - 1.0f;
   float dy = (((float)py + oy) / (float)c->H) * 2.0f - 1.0f;
   float org[4], dcam[4], dw[4];
@@ -928,8 +1066,14 @@ static vec3 osample(const octx* c, uint32_t px, uint32_t py, float ox, float oy,
   hlsl_mul4(c->cb + 48, ndc, dcam);
   const float dc4[4] = {dcam[0], dcam[1], dcam[2], 0.0f};
   hlsl_mul4(c->cb + 32, dc4, dw);
-  vec3 O = mk(org[0], org[1], org[2]);
-  vec3 D = vnorm(mk(dw[0], dw[1], dw[2]));
+  *O = mk(org[0], org[1], org[2]);
+  *D = vnorm(mk(dw[0], dw[1], dw[2]));
+}
+
+/* RayGen + hit/miss programs for one camera sample, one independent ray per pixel */
+static vec3 osample(const octx* c, uint32_t px, uint32_t py, float ox, float oy, ostats* st) {
+  vec3 O, D;
+  oraygen(c, px, py, ox, oy, &O, &D);
   ohit h;
   st->v[0]++;
   int f = c->brute ? obrute(c->s, O, D, 0.0f, 100000.0f, 0, &h, st) : otrace(c->s, O, D, 0.0f, 100000.0f, 0, &h, st);
@@ -979,6 +1123,82 @@ static uint32_t unorm8(float x) {
   return (uint32_t)(x * 255.0f + 0.5f);
 }
 
+/* One camera sample for the 64 lanes of a wave tile, traces as wave packets
+ * (shade_sample_packet in rt_trace.hip): lanes without a ray of a kind join that packet dead. */
+static void osample_packet(const octx* c, const uint32_t* px, const uint32_t* py, const int* inimg, float ox,
+                           float oy, vec3* color, ostats* st) {
+  vec3 O[OPK], D[OPK], P[OPK], sd[OPK];
+  ohit h[OPK], hs[OPK];
+  int found[OPK], occl[OPK], need[OPK];
+  for (int l = 0; l < OPK; ++l) {
+    oraygen(c, px[l], py[l], ox, oy, &O[l], &D[l]);
+    if (inimg[l]) st->v[0]++;
+  }
+  opacket(c->s, O, D, 0.0f, 100000.0f, 0, inimg, h, found, st);
+  for (int l = 0; l < OPK; ++l) {
+    float ramp = (float)py[l] / (float)c->H; /* Miss.hlsl:8-9 */
+    color[l] = mk(0.0f, 0.2f, 0.7f - 0.3f * ramp);
+    P[l] = vadd(O[l], vscale(D[l], h[l].t));
+  }
+  if (c->mode == 0) {
+    vec3 ldir[OPK], nf[OPK];
+    for (int l = 0; l < OPK; ++l) {
+      need[l] = 0;
+      ldir[l] = nf[l] = mk(0, 0, 0);
+      if (!found[l]) continue;
+      if (c->s->inst[h[l].inst].hit_group == 2u) {
+        ldir[l] = vnorm(vsub(ld3(c->L[0].position), P[l]));
+        nf[l] = o_face_normal(c->s, h[l].inst, h[l].prim);
+        need[l] = 1;
+        st->v[1]++;
+      } else {
+        vec3 n = o_interp_normal(c->s, h[l].inst, h[l].prim, h[l].u, h[l].v);
+        color[l] = vadd(odirect(P[l], n, ld3(c->mat), c->L, c->nl), opbr(n, O[l], P[l], c->L, c->nl, c->mat));
+      }
+      sd[l] = vnorm(ldir[l]);
+    }
+    for (int l = 0; l < OPK; ++l) if (!need[l]) sd[l] = mk(0, 0, 1);
+    opacket(c->s, P, sd, 0.01f, 100000.0f, 1, need, hs, occl, st);
+    for (int l = 0; l < OPK; ++l) {
+      if (!need[l]) continue;
+      int shadowed = vdot(nf[l], ldir[l]) < 0.0f;
+      if (!shadowed) shadowed = occl[l];
+      float factor = shadowed ? 0.3f : 1.0f;
+      float li = fmax2(0.0f, vdot(nf[l], ldir[l]));
+      float v = (1.0f * li) * factor;
+      color[l] = mk(v, v, v);
+    }
+    return;
+  }
+  vec3 n[OPK], Ld[OPK];
+  float sum[OPK], nl[OPK];
+  for (int l = 0; l < OPK; ++l) {
+    sum[l] = 0.0f;
+    n[l] = mk(0, 0, 0);
+    if (!found[l]) continue;
+    n[l] = c->s->inst[h[l].inst].hit_group == 2u ? o_face_normal(c->s, h[l].inst, h[l].prim)
+                                                 : vneg(o_interp_normal(c->s, h[l].inst, h[l].prim, h[l].u, h[l].v));
+  }
+  for (uint32_t li = 0; li < c->nl; ++li) {
+    for (int l = 0; l < OPK; ++l) {
+      Ld[l] = vnorm(vsub(ld3(c->L[li].position), P[l]));
+      nl[l] = vdot(n[l], Ld[l]);
+      need[l] = found[l] && nl[l] > 0.0f;
+      occl[l] = 0;
+      sd[l] = need[l] ? vnorm(Ld[l]) : mk(0, 0, 1);
+      if (c->mode == 1 && need[l]) st->v[1]++;
+    }
+    if (c->mode == 1) opacket(c->s, P, sd, 0.01f, 100000.0f, 1, need, hs, occl, st);
+    for (int l = 0; l < OPK; ++l)
+      if (need[l]) sum[l] = sum[l] + nl[l] * (occl[l] ? 0.3f : 1.0f);
+  }
+  for (int l = 0; l < OPK; ++l)
+    if (found[l]) {
+      float v = sum[l] / (float)c->nl;
+      color[l] = mk(v, v, v);
+    }
+}
+
 typedef struct {
   const octx* c;
   const uint32_t* rows;
@@ -987,6 +1207,55 @@ typedef struct {
   float* rgba32f;
   ostats st;
 } ojob;
+
+static void store_px(const ojob* j, size_t o, vec3 acc) {
+  if (j->rgba8) {
+    j->rgba8[o * 4 + 0] = (uint8_t)unorm8(acc.x);
+    j->rgba8[o * 4 + 1] = (uint8_t)unorm8(acc.y);
+    j->rgba8[o * 4 + 2] = (uint8_t)unorm8(acc.z);
+    j->rgba8[o * 4 + 3] = 255;
+  }
+  if (j->rgba32f) {
+    j->rgba32f[o * 4 + 0] = acc.x; j->rgba32f[o * 4 + 1] = acc.y;
+    j->rgba32f[o * 4 + 2] = acc.z; j->rgba32f[o * 4 + 3] = 1.0f;
+  }
+}
+
+/* wave tiles of 8 x 8 (pixel column, row-list entry), lane = 8 * (row % 8) + column % 8 */
+static void* render_tiles(void* arg) {
+  ojob* j = (ojob*)arg;
+  const octx* c = j->c;
+  const uint32_t tw = (c->W + 7) / 8, th = (j->nrows + 7) / 8;
+  for (uint32_t t = j->tid; t < tw * th; t += j->nthreads) {
+    const uint32_t tx = t % tw, ty = t / tw;
+    uint32_t px[OPK], py[OPK];
+    int inimg[OPK];
+    vec3 acc[OPK], col[OPK];
+    for (int l = 0; l < OPK; ++l) {
+      px[l] = tx * 8 + (uint32_t)(l & 7);
+      const uint32_t orow = ty * 8 + (uint32_t)(l >> 3);
+      inimg[l] = px[l] < c->W && orow < j->nrows;
+      py[l] = inimg[l] ? (j->rows ? j->rows[orow] : orow) : 0;
+      acc[l] = mk(0, 0, 0);
+    }
+    for (int sy = 0; sy < c->k; ++sy)
+      for (int sx = 0; sx < c->k; ++sx) {
+        float ox = ((float)sx + 0.5f) / (float)c->k, oy = ((float)sy + 0.5f) / (float)c->k;
+        osample_packet(c, px, py, inimg, ox, oy, col, &j->st);
+        for (int l = 0; l < OPK; ++l) acc[l] = vadd(acc[l], col[l]);
+      }
+    for (int l = 0; l < OPK; ++l) {
+      if (!inimg[l]) continue;
+      vec3 a = acc[l];
+      if (c->k > 1) {
+        float ns = (float)(c->k * c->k);
+        a = mk(a.x / ns, a.y / ns, a.z / ns);
+      }
+      store_px(j, (size_t)(ty * 8 + (uint32_t)(l >> 3)) * c->W + px[l], a);
+    }
+  }
+  return NULL;
+}
 
 static void* render_rows(void* arg) {
   ojob* j = (ojob*)arg;
@@ -1004,17 +1273,7 @@ static void* render_rows(void* arg) {
         float ns = (float)(c->k * c->k);
         acc = mk(acc.x / ns, acc.y / ns, acc.z / ns);
       }
-      size_t o = (size_t)r * c->W + px;
-      if (j->rgba8) {
-        j->rgba8[o * 4 + 0] = (uint8_t)unorm8(acc.x);
-        j->rgba8[o * 4 + 1] = (uint8_t)unorm8(acc.y);
-        j->rgba8[o * 4 + 2] = (uint8_t)unorm8(acc.z);
-        j->rgba8[o * 4 + 3] = 255;
-      }
-      if (j->rgba32f) {
-        j->rgba32f[o * 4 + 0] = acc.x; j->rgba32f[o * 4 + 1] = acc.y;
-        j->rgba32f[o * 4 + 2] = acc.z; j->rgba32f[o * 4 + 3] = 1.0f;
-      }
+      store_px(j, (size_t)r * c->W + px, acc);
     }
   }
   return NULL;
@@ -1022,7 +1281,8 @@ static void* render_rows(void* arg) {
 
 int oracle_render(const oracle_scene* s, const float cb[64], const oracle_light* lights, uint32_t nlights,
                   const float material[6], int mode, int spp, uint32_t W, uint32_t H, const uint32_t* rows,
-                  uint32_t nrows, uint8_t* rgba8, float* rgba32f, int nthreads, uint64_t* stats, int brute) {
+                  uint32_t nrows, uint8_t* rgba8, float* rgba32f, int nthreads, uint64_t* stats, int brute,
+                  int schedule) {
   if (!s || !s->tlas || !cb || !lights || nlights < 1 || nlights > 16 || W == 0 || H == 0) return -1;
   int k = 0;
   for (int q = 1; q <= 4; ++q) if (q * q == spp) k = q;
@@ -1039,9 +1299,15 @@ int oracle_render(const oracle_scene* s, const float cb[64], const oracle_light*
     jobs[t].tid = (uint32_t)t; jobs[t].nthreads = (uint32_t)nthreads;
     jobs[t].rgba8 = rgba8; jobs[t].rgba32f = rgba32f;
   }
-  if (nthreads == 1) render_rows(&jobs[0]);
+  /* the device runs wave packets unless asked for per-lane rays or the trees are too deep for
+   * its one-VGPR stack (rt_trace.hip launch_mode) */
+  uint32_t maxb = 0;
+  for (int q = 0; q < s->nblas; ++q) if (s->blas[q].max_stack > maxb) maxb = s->blas[q].max_stack;
+  const int packet = !brute && schedule == 0 && (s->tlas_max_stack + 1 + maxb) < OPK;
+  void* (*fn)(void*) = packet ? render_tiles : render_rows;
+  if (nthreads == 1) fn(&jobs[0]);
   else {
-    for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, render_rows, &jobs[t]);
+    for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, fn, &jobs[t]);
     for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
   }
   if (stats)

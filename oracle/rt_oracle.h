@@ -58,11 +58,13 @@ int oracle_export_blas(const oracle_scene* s, int blas, void* nodes, void* tris)
 int oracle_export_tlas(const oracle_scene* s, void* nodes);
 
 /* render W x H (rows NULL = all). stats[8] accumulates (same slots as RT_STAT_*), may be NULL.
- * brute_force != 0: closest hit by testing every triangle of every instance (no BVH). */
+ * brute_force != 0: closest hit by testing every triangle of every instance (no BVH).
+ * schedule: RT_SCHED_PACKET (0: 8 x 8 wave packets, as the device) or RT_SCHED_LANE (1: one
+ * independent traversal per pixel). The image is the same; the traversal counters follow it. */
 int oracle_render(const oracle_scene* s, const float cb[64], const oracle_light* lights, uint32_t nlights,
                   const float material[6], int mode, int spp, uint32_t W, uint32_t H, const uint32_t* rows,
                   uint32_t nrows, uint8_t* rgba8, float* rgba32f, int nthreads, uint64_t* stats,
-                  int brute_force);
+                  int brute_force, int schedule);
 /* batch trace: rays n x 8 floats, hits n x 4 u32 (t bits, instance, prim, flag), uv n x 2 (may be NULL) */
 int oracle_trace_rays(const oracle_scene* s, const float* rays, uint32_t n, int any_hit, uint32_t* hits,
                       float* uv, int brute_force, uint64_t* stats);

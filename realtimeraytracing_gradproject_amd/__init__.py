@@ -28,7 +28,7 @@ ASSETS = os.path.join(_HERE, "assets")
 RT_OK, RT_E_INVALID, RT_E_OOM, RT_E_HIP, RT_E_RCCL, RT_E_UNSUPPORTED, RT_E_IO = 0, -1, -2, -3, -4, -5, -6
 RT_HITGROUP_MODEL, RT_HITGROUP_SHADOW, RT_HITGROUP_PLANE = 0, 1, 2
 RT_SHADE_REF, RT_SHADE_LAMBERT_SHADOW, RT_SHADE_PRIMARY = 0, 1, 2
-RT_SCHED_MEGAKERNEL, RT_SCHED_WAVEFRONT = 0, 1
+RT_SCHED_PACKET, RT_SCHED_LANE = 0, 1
 STAT_NAMES = ("primary_rays", "shadow_rays", "aabb_tests", "tri_tests", "instance_entries",
               "stack_overflows", "pixels", "dispatches")
 

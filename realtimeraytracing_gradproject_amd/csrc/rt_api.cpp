@@ -51,7 +51,7 @@ struct rt_ctx {
   // frame state
   rt::FrameParams fp{};
   bool have_camera = false, have_shading = false;
-  int schedule = RT_SCHED_MEGAKERNEL;
+  int schedule = RT_SCHED_PACKET;
   bool stats_on = false;
   unsigned long long* d_stats = nullptr;
   uint64_t dispatches = 0, pixels = 0;
@@ -59,7 +59,6 @@ struct rt_ctx {
   uint32_t* d_rows = nullptr;
   size_t rows_cap = 0;
   std::vector<uint32_t> rows_host;
-  rt::WavefrontBuffers wf;
   // traversal-stack overflow area in HBM for lanes whose path outgrows the LDS part
   int* d_ovf = nullptr;
   size_t ovf_cap = 0;
@@ -250,13 +249,9 @@ rt_status rt_destroy(rt_ctx_t c) {
   if (c->tlas_sorted) (void)hipFree(c->tlas_sorted);
   if (c->d_stats) (void)hipFree(c->d_stats);
   if (c->d_rows) (void)hipFree(c->d_rows);
-  if (c->wf.surf) (void)hipFree(c->wf.surf);
   if (c->d_ovf) (void)hipFree(c->d_ovf);
   if (c->pool_nodes) (void)hipFree(c->pool_nodes);
   if (c->pool_tris) (void)hipFree(c->pool_tris);
-  if (c->wf.shadow_bits) (void)hipFree(c->wf.shadow_bits);
-  if (c->wf.queue) (void)hipFree(c->wf.queue);
-  if (c->wf.queue_count) (void)hipFree(c->wf.queue_count);
   (void)hipStreamDestroy(c->stream);
   delete c;
   return RT_OK;
@@ -480,7 +475,7 @@ rt_status rt_set_shading(rt_ctx_t c, const rt_light* lights, uint32_t nlights, c
 
 rt_status rt_set_schedule(rt_ctx_t c, int schedule) {
   if (!c) return RT_E_INVALID;
-  if (schedule != RT_SCHED_MEGAKERNEL && schedule != RT_SCHED_WAVEFRONT) return fail(c, RT_E_INVALID, "rt_set_schedule: unknown schedule");
+  if (schedule != RT_SCHED_PACKET && schedule != RT_SCHED_LANE) return fail(c, RT_E_INVALID, "rt_set_schedule: unknown schedule");
   c->schedule = schedule;
   return RT_OK;
 }
@@ -566,7 +561,7 @@ rt_status rt_dispatch_rays(rt_ctx_t c, uint32_t W, uint32_t H, const uint32_t* r
     if (st != RT_OK) return st;
   }
   hipError_t e = rt::launch_trace_frame(sv, c->fp, d_rows, rgba8, rgba32f, c->d_stats, c->stats_on,
-                                        c->schedule, &c->wf, s);
+                                        c->schedule, s);
   if (e != hipSuccess) return hip_fail(c, e, "trace launch");
   if (c->stats_on) {
     c->dispatches += 1;

@@ -49,7 +49,8 @@ static_assert(sizeof(BinNode) == 64, "BinNode must be 64 B");
 // Traversal node: 4-wide, 128 B = one cache line, nodes in BFS order (root 0, then level by
 // level: the top of the tree is a contiguous prefix). Child boxes are stored SoA so one node is
 // 8 x 16-B loads and the 4 slab tests share per-axis FMAs. Built on the device by collapsing
-// every other level of the binary LBVH (each node has 2..4 children).
+// the binary LBVH: each wide node opens its largest-area internal descendants until it has 4
+// children (fewer only where the subtree runs out of internal nodes).
 // child[k]: >= 0 node index, < 0 leaf (~slot / ~instance), kEmptyChild = unused slot.
 constexpr int32_t kEmptyChild = INT32_MIN + 1;
 struct alignas(128) Bvh4Node {

@@ -35,19 +35,9 @@ hipError_t tlas_prepare(const InstanceRec* d_inst, const float* d_blas_bounds, u
 
 // --- Trace (rt_trace.hip) -------------------------------------------------------------------
 
-struct WavefrontBuffers {
-  // Per output pixel: hit record for the resolve pass (P.xyz, n.xyz, kind) and shadow bits.
-  float* surf = nullptr;        // nrows*W*8 floats
-  uint32_t* shadow_bits = nullptr;  // nrows*W
-  uint32_t* queue = nullptr;    // shadow ray queue: (pixel, light) packed, capacity nrows*W*nlights
-  uint32_t* queue_count = nullptr;
-  size_t pixel_cap = 0;
-  size_t queue_cap = 0;
-};
-
 hipError_t launch_trace_frame(const SceneView& scene, const FrameParams& fp, const uint32_t* d_rows,
                               void* rgba8, float* rgba32f, unsigned long long* d_stats, bool stats,
-                              int schedule, WavefrontBuffers* wf, hipStream_t stream);
+                              int schedule, hipStream_t stream);
 
 hipError_t launch_trace_rays(const SceneView& scene, const float* rays, uint32_t n, int any_hit,
                              uint32_t* hits, float* uv, unsigned long long* d_stats, bool stats,

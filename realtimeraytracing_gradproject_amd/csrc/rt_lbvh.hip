@@ -301,6 +301,52 @@ __global__ void k_single(const float* __restrict__ primbox, bool leaf_ref_is_pri
 // It also bounds the traversal stack: a visited node pushes (count - 1) siblings, so the most a
 // root-to-node path can leave on the stack is ps[node] + count(node) - 1, ps = sum over the
 // ancestors. info[0] = node count, info[1] = levels, info[2] = that maximum.
+// Half surface area of a box (the SAH weight), summed in a fixed order (mirrored by the oracle).
+__device__ __forceinline__ float half_area(const float* b) {
+  const float dx = b[3] - b[0], dy = b[4] - b[1], dz = b[5] - b[2];
+  return (dx * dy + dy * dz) + dz * dx;
+}
+
+// Children of one 4-wide node rooted at binary node `root`: start from its two children and
+// open the internal candidate with the largest surface area (lowest slot on ties) until there
+// are four, so the wide nodes come out full and the large boxes are split first.
+__device__ __forceinline__ int gather4(const BinNode* __restrict__ bin, int root, int ref[4], float box[4][6]) {
+  const BinNode& b = bin[root];
+  ref[0] = b.c0;
+  ref[1] = b.c1;
+  for (int a = 0; a < 3; ++a) {
+    box[0][a] = b.lo0[a];
+    box[0][3 + a] = b.hi0[a];
+    box[1][a] = b.lo1[a];
+    box[1][3 + a] = b.hi1[a];
+  }
+  int cnt = 2;
+  while (cnt < 4) {
+    int best = -1;
+    float bsa = 0.0f;
+    for (int j = 0; j < cnt; ++j) {
+      if (ref[j] < 0) continue;
+      const float sa = half_area(box[j]);
+      if (best < 0 || sa > bsa) {
+        best = j;
+        bsa = sa;
+      }
+    }
+    if (best < 0) break;
+    const BinNode& g = bin[ref[best]];
+    ref[best] = g.c0;
+    ref[cnt] = g.c1;
+    for (int a = 0; a < 3; ++a) {
+      box[best][a] = g.lo0[a];
+      box[best][3 + a] = g.hi0[a];
+      box[cnt][a] = g.lo1[a];
+      box[cnt][3 + a] = g.hi1[a];
+    }
+    ++cnt;
+  }
+  return cnt;
+}
+
 __global__ __launch_bounds__(1024) void k_collapse(const BinNode* __restrict__ bin, Bvh4Node* __restrict__ out,
                                                    int* la, int* lb, int* ps, uint32_t* __restrict__ info) {
   __shared__ int scan[1024];
@@ -325,32 +371,7 @@ __global__ __launch_bounds__(1024) void k_collapse(const BinNode* __restrict__ b
       int ref[4];
       float box[4][6];
       int cnt = 0;
-      if (valid) {
-        const BinNode& b = bin[cur[i]];
-        for (int k = 0; k < 2; ++k) {
-          const int c = k ? b.c1 : b.c0;
-          const float* lo = k ? b.lo1 : b.lo0;
-          const float* hi = k ? b.hi1 : b.hi0;
-          if (c < 0) {
-            ref[cnt] = c;
-            for (int a = 0; a < 3; ++a) {
-              box[cnt][a] = lo[a];
-              box[cnt][3 + a] = hi[a];
-            }
-            ++cnt;
-          } else {
-            const BinNode& g = bin[c];
-            for (int q = 0; q < 2; ++q) {
-              ref[cnt] = q ? g.c1 : g.c0;
-              for (int a = 0; a < 3; ++a) {
-                box[cnt][a] = q ? g.lo1[a] : g.lo0[a];
-                box[cnt][3 + a] = q ? g.hi1[a] : g.hi0[a];
-              }
-              ++cnt;
-            }
-          }
-        }
-      }
+      if (valid) cnt = gather4(bin, cur[i], ref, box);
       int m = 0;
       for (int j = 0; j < cnt; ++j) m += ref[j] >= 0;
       scan[tid] = m;

@@ -19,6 +19,10 @@
 
 #include "rt_internal.hpp"
 
+// v_writelane_b32 (the LLVM intrinsic; this clang has no builtin for it): writes the uniform x
+// into lane l of v, whatever EXEC holds.
+__device__ int amdgcn_writelane(int x, int l, int v) __asm("llvm.amdgcn.writelane.i32");
+
 namespace rt {
 namespace {
 
@@ -235,6 +239,231 @@ __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, H
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Wave-packet traversal: the 64 lanes of a wave (an 8x8 pixel tile) walk ONE path through the
+// trees together. The current node / triangle / instance is wave-uniform, so it is fetched with
+// scalar loads into SGPRs (one fetch per wave instead of 64 lane loads) and every lane tests its
+// own ray against it; a child is entered when any live lane's slab test accepts it (ballot). The
+// traversal stack is wave-uniform and lives in the 64 lanes of one VGPR (v_writelane /
+// v_readlane): no LDS and no per-lane stack traffic. Children are ordered by the entry distance
+// of the lowest live lane (a uniform key, sorted in SALU). When every live lane's ray has the
+// same direction octant (the common case for camera and shadow tiles) the near and far planes
+// of each axis are picked by the load address, as in the per-lane path.
+// Results are those of the per-ray traversal: the closest hit is the lexicographic minimum of
+// (t, instance, primitive) over every triangle a lane's ray reaches, and every triangle whose
+// root path the ray's slab tests accept is visited, whatever the order.
+// ------------------------------------------------------------------------------------------
+#define RT_CONST __attribute__((address_space(4)))
+
+constexpr int kPacketStack = 64;  // wave-uniform stack entries: one VGPR, entry i in lane i
+
+
+struct WaveStack {
+  int v = 0;
+  __device__ __forceinline__ void put(int slot, int x) { v = amdgcn_writelane(x, slot, v); }
+  __device__ __forceinline__ int get(int slot) const { return __builtin_amdgcn_readlane(v, slot); }
+};
+
+__device__ __forceinline__ uint64_t wave_ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ uint32_t lead_lane(uint64_t m) { return (uint32_t)__builtin_ctzll(m); }
+
+// Octant shared by every live lane (bit k set: component k of the direction is negative), or 8
+// when the live lanes disagree.
+__device__ __forceinline__ uint32_t wave_octant(V3 invd, bool live, uint32_t lead) {
+  const uint32_t o = (invd.x < 0.0f ? 1u : 0u) | (invd.y < 0.0f ? 2u : 0u) | (invd.z < 0.0f ? 4u : 0u);
+  const uint32_t ol = (uint32_t)__builtin_amdgcn_readlane((int)o, (int)lead);
+  return wave_ballot(live && o != ol) ? 8u : ol;
+}
+
+__device__ __forceinline__ f4v cld4(const RT_CONST char* p) { return *(const RT_CONST f4v*)p; }
+
+// Per-wave ray state of one traversal level (world rays in the TLAS, object rays in a BLAS).
+struct PacketRay {
+  V3 o, d, invd, noinv;
+  uint32_t oct;  // octant shared by the live lanes, or 8
+};
+
+// One node of the packet walk: slab tests of the 4 children for every live lane, then the
+// entered children (any live lane accepts) go nearest first (the lead lane's entry distance,
+// lowest slot on ties); the other entered ones are pushed in descending slot order, so the
+// lowest slot pops next. Pushes that do not happen write the spare lane kPacketStack - 1, and
+// the bookkeeping is plain integer SALU work. Returns false when no child is entered.
+template <bool STATS>
+__device__ __forceinline__ bool packet_node(const RT_CONST char* pool, int ref, const PacketRay& ry, float tmin,
+                                            float tbest, bool live, uint32_t lead, WaveStack& stk, int& sp,
+                                            int cap, int& next, Counters& cnt) {
+  const RT_CONST char* nb = pool + ((size_t)(uint32_t)ref << 7);
+  const i4v ch = *(const RT_CONST i4v*)(nb + 96);
+  const int cref[4] = {ch.x, ch.y, ch.z, ch.w};
+  uint64_t hm[4];
+  uint32_t vkey[4];  // per lane: |entry distance| if this lane's test accepted the child, else +inf
+  if (ry.oct < 8u) {
+    // shared octant: near/far planes by address (bitwise equal to the min/max form)
+    const uint32_t ox = (ry.oct & 1u) ? 16u : 0u, oy = (ry.oct & 2u) ? 48u : 32u, oz = (ry.oct & 4u) ? 80u : 64u;
+    const f4v a0 = cld4(nb + ox), a1 = cld4(nb + (ox ^ 16u));
+    const f4v a2 = cld4(nb + oy), a3 = cld4(nb + (oy ^ 16u));
+    const f4v a4 = cld4(nb + oz), a5 = cld4(nb + (oz ^ 16u));
+    const float nx[4] = {a0.x, a0.y, a0.z, a0.w}, fx[4] = {a1.x, a1.y, a1.z, a1.w};
+    const float ny[4] = {a2.x, a2.y, a2.z, a2.w}, fy[4] = {a3.x, a3.y, a3.z, a3.w};
+    const float nz[4] = {a4.x, a4.y, a4.z, a4.w}, fz[4] = {a5.x, a5.y, a5.z, a5.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float tnx = __builtin_fmaf(nx[k], ry.invd.x, ry.noinv.x), tfx = __builtin_fmaf(fx[k], ry.invd.x, ry.noinv.x);
+      const float tny = __builtin_fmaf(ny[k], ry.invd.y, ry.noinv.y), tfy = __builtin_fmaf(fy[k], ry.invd.y, ry.noinv.y);
+      const float tnz = __builtin_fmaf(nz[k], ry.invd.z, ry.noinv.z), tfz = __builtin_fmaf(fz[k], ry.invd.z, ry.noinv.z);
+      const float n = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
+      const float f = fminf(fminf(tfx, tfy), fminf(tfz, tbest));
+      const bool h = live && n <= f * 1.0000004f;
+      hm[k] = cref[k] != kEmptyChild ? wave_ballot(h) : 0ull;
+      vkey[k] = h ? (__float_as_uint(n) & 0x7fffffffu) : 0x7f800000u;
+    }
+  } else {
+    const f4v a0 = cld4(nb), a1 = cld4(nb + 16), a2 = cld4(nb + 32);
+    const f4v a3 = cld4(nb + 48), a4 = cld4(nb + 64), a5 = cld4(nb + 80);
+    const float lox[4] = {a0.x, a0.y, a0.z, a0.w}, hix[4] = {a1.x, a1.y, a1.z, a1.w};
+    const float loy[4] = {a2.x, a2.y, a2.z, a2.w}, hiy[4] = {a3.x, a3.y, a3.z, a3.w};
+    const float loz[4] = {a4.x, a4.y, a4.z, a4.w}, hiz[4] = {a5.x, a5.y, a5.z, a5.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float tlx = __builtin_fmaf(lox[k], ry.invd.x, ry.noinv.x), thx = __builtin_fmaf(hix[k], ry.invd.x, ry.noinv.x);
+      const float tly = __builtin_fmaf(loy[k], ry.invd.y, ry.noinv.y), thy = __builtin_fmaf(hiy[k], ry.invd.y, ry.noinv.y);
+      const float tlz = __builtin_fmaf(loz[k], ry.invd.z, ry.noinv.z), thz = __builtin_fmaf(hiz[k], ry.invd.z, ry.noinv.z);
+      const float n = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), tmin));
+      const float f = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tbest));
+      const bool h = live && n <= f * 1.0000004f;
+      hm[k] = cref[k] != kEmptyChild ? wave_ballot(h) : 0ull;
+      vkey[k] = h ? (__float_as_uint(n) & 0x7fffffffu) : 0x7f800000u;
+    }
+  }
+  if (STATS && live)
+    cnt.aabb += (uint32_t)(cref[0] != kEmptyChild) + (uint32_t)(cref[1] != kEmptyChild) +
+                (uint32_t)(cref[2] != kEmptyChild) + (uint32_t)(cref[3] != kEmptyChild);
+  if ((hm[0] | hm[1] | hm[2] | hm[3]) == 0) return false;
+  // uniform keys: the lead lane's key, all-ones where no lane entered the child
+  uint32_t key[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    key[k] = hm[k] ? (uint32_t)__builtin_amdgcn_readlane((int)vkey[k], (int)lead) : 0xffffffffu;
+  uint32_t kb = key[0];
+  int rb = cref[0];
+  uint32_t ib = 0;
+#pragma unroll
+  for (int k = 1; k < 4; ++k) {
+    const bool s = key[k] < kb;
+    kb = s ? key[k] : kb;
+    rb = s ? cref[k] : rb;
+    ib = s ? (uint32_t)k : ib;
+  }
+#pragma unroll
+  for (int k = 3; k >= 0; --k) {
+    // e = entered and not the nearest, as 0/1 integers (no lane masks)
+    const uint32_t e = __builtin_elementwise_min(~key[k], 1u) & __builtin_elementwise_min((uint32_t)k ^ ib, 1u);
+    if (STATS && live && e && sp >= cap) ++cnt.overflow;
+    const int lane = (int)(((uint32_t)(sp - (kPacketStack - 1)) & (0u - e)) + (kPacketStack - 1));
+    stk.put(lane, cref[k]);
+    sp += (int)e;
+  }
+  next = rb;
+  return true;
+}
+
+// Triangle leaf for every live lane (uniform triangle, scalar loads). ANY_HIT: a lane that
+// accepts a hit leaves the packet.
+template <bool ANY_HIT, bool STATS>
+__device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref, const PacketRay& ry, float tmin,
+                                           uint32_t cur, bool& live, bool& found, HitRec& hit, Counters& cnt) {
+  const RT_CONST f4v* tq = (const RT_CONST f4v*)(tpool + (~ref));
+  const f4v ta = tq[0], tb = tq[1], tc = tq[2];
+  if (STATS && live) ++cnt.tri;
+  float t, u, v;
+  const bool ok = moller_trumbore(ry.o, ry.d, v3(ta.x, ta.y, ta.z), v3(tb.x, tb.y, tb.z), v3(tc.x, tc.y, tc.z), t, u, v);
+  if (live && ok && t >= tmin) {
+    const uint32_t prim = __float_as_uint(ta.w);
+    const bool better = t < hit.t || (t == hit.t && (cur < hit.inst || (cur == hit.inst && prim < hit.prim)));
+    if (better) {
+      hit.t = t;
+      hit.u = u;
+      hit.v = v;
+      hit.inst = cur;
+      hit.prim = prim;
+      found = true;
+      if (ANY_HIT) live = false;
+    }
+  }
+}
+
+template <bool ANY_HIT, bool STATS>
+__device__ bool trace_packet(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, bool alive, HitRec& hit,
+                             Counters& cnt) {
+  const RT_CONST char* pool = (const RT_CONST char*)sc.pool_nodes;
+  const RT_CONST TriRec* tpool = (const RT_CONST TriRec*)sc.pool_tris;
+  const RT_CONST InstanceRec* ipool = (const RT_CONST InstanceRec*)sc.inst;
+  hit.t = tmax;
+  hit.inst = 0xffffffffu;
+  hit.prim = 0xffffffffu;
+  hit.u = hit.v = 0.0f;
+  bool found = false;
+  bool live = alive;
+  uint64_t livemask = wave_ballot(live);
+  if (livemask == 0) return false;
+  uint32_t lead = lead_lane(livemask);
+  PacketRay w;
+  w.o = o;
+  w.d = d;
+  w.invd = v3(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
+  w.noinv = neg(mul(o, w.invd));
+  w.oct = wave_octant(w.invd, live, lead);
+  WaveStack stk;
+  const int cap = sc.stack_cap;  // < kPacketStack (checked at launch): lane 63 stays spare
+  int sp = 0;
+  int ref = 0;
+  // TLAS walk; each instance leaf runs a nested BLAS walk on the stack above the TLAS entries
+  // (the world ray is invariant here, the object ray inside: no ray state is carried around).
+  while (true) {
+    int next;
+    if (ref >= 0) {
+      if (packet_node<STATS>(pool, ref, w, tmin, hit.t, live, lead, stk, sp, cap, next, cnt)) {
+        ref = next;
+        continue;
+      }
+    } else {
+      const uint32_t cur = (uint32_t)(~ref);
+      const RT_CONST InstanceRec& ir = ipool[cur];
+      if (STATS && live) ++cnt.inst;
+      const RT_CONST f4v* mq = (const RT_CONST f4v*)ir.w2o;
+      const f4v m0 = mq[0], m1 = mq[1], m2 = mq[2];
+      const float m[12] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w, m2.x, m2.y, m2.z, m2.w};
+      PacketRay b;
+      b.o = xform_point(m, o);
+      b.d = xform_dir(m, d);
+      b.invd = v3(safe_inv(b.d.x), safe_inv(b.d.y), safe_inv(b.d.z));
+      b.noinv = neg(mul(b.o, b.invd));
+      b.oct = wave_octant(b.invd, live, lead);
+      const int base = sp;
+      int bref = (int)ir.pool_root;
+      while (true) {
+        if (bref >= 0) {
+          if (packet_node<STATS>(pool, bref, b, tmin, hit.t, live, lead, stk, sp, cap, next, cnt)) {
+            bref = next;
+            continue;
+          }
+        } else {
+          packet_tri<ANY_HIT, STATS>(tpool, bref, b, tmin, cur, live, found, hit, cnt);
+          if (ANY_HIT) {
+            livemask = wave_ballot(live);
+            if (livemask == 0) return found;
+            lead = lead_lane(livemask);
+          }
+        }
+        if (sp == base) break;
+        bref = stk.get(--sp);
+      }
+    }
+    if (sp == 0) return found;
+    ref = stk.get(--sp);
+  }
+}
+
 // Hit-instance data the shaders read (the reference binds it per hit group through the SBT).
 struct HitInstance {
   const RT_GLOBAL float* vtx;
@@ -427,6 +656,84 @@ __device__ V3 shade_sample(const SceneView& sc, const FrameParams& fp, uint32_t 
   return v3(c, c, c);
 }
 
+// shade_sample for the wave-packet traversal: identical arithmetic, with every trace hoisted to
+// wave-uniform control flow (lanes without a ray of that kind join the packet dead).
+template <int MODE, bool STATS>
+__device__ V3 shade_sample_packet(const SceneView& sc, const FrameParams& fp, uint32_t px, uint32_t py,
+                                  float ox, float oy, bool inimg, Counters& cnt) {
+  const float dx = (((float)px + ox) / (float)fp.width) * 2.0f - 1.0f;
+  const float dy = (((float)py + oy) / (float)fp.height) * 2.0f - 1.0f;
+  float org4[4], dc[4], dw[4];
+  const float zero_one[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+  hlsl_mul4(fp.cb + 32, zero_one, org4);
+  const float ndc[4] = {dx, -dy, 1.0f, 1.0f};
+  hlsl_mul4(fp.cb + 48, ndc, dc);
+  const float dcam[4] = {dc[0], dc[1], dc[2], 0.0f};
+  hlsl_mul4(fp.cb + 32, dcam, dw);
+  const V3 O = v3(org4[0], org4[1], org4[2]);
+  const V3 D = normalize(v3(dw[0], dw[1], dw[2]));  // CastDefaultRay
+  HitRec hit;
+  if (STATS && inimg) ++cnt.primary;
+  const bool found = trace_packet<false, STATS>(sc, O, D, 0.0f, 100000.0f, inimg, hit, cnt);
+  const float ramp = (float)py / (float)fp.height;  // Miss.hlsl:8
+  const V3 miss = v3(0.0f, 0.2f, 0.7f - 0.3f * ramp);
+  const V3 P = add(O, muls(D, hit.t));  // GetWorldHitPoint, Common.hlsl:24-27
+  HitInstance ir;
+  bool plane = false;
+  if (found) {
+    ir = load_hit_instance(sc, hit.inst);
+    plane = ir.hit_group == 2u;
+  }
+  if (MODE == 0) {
+    V3 color = miss, ldir = v3(0.0f, 0.0f, 0.0f), nf = v3(0.0f, 0.0f, 0.0f);
+    bool need = false;
+    if (found) {
+      if (plane) {
+        const LightRec& L0 = fp.lights[0];
+        ldir = normalize(sub(v3(L0.position[0], L0.position[1], L0.position[2]), P));
+        nf = face_world_normal(ir, hit.prim);
+        need = true;
+      } else {
+        const V3 n = interpolated_world_normal(ir, hit.prim, hit.u, hit.v);
+        const V3 albedo = v3(fp.material.albedo[0], fp.material.albedo[1], fp.material.albedo[2]);
+        // reflectivity is pinned to 0: lerp(final, refl, 0) == final; no reflection ray.
+        color = add(direct_lighting(fp, P, n, albedo), pbr_shading(fp, n, O, P));
+      }
+    }
+    HitRec sh;
+    if (STATS && need) ++cnt.shadow;
+    const bool occl = trace_packet<true, STATS>(sc, P, normalize(ldir), 0.01f, 100000.0f, need, sh, cnt);
+    if (need) {
+      bool shadowed = dot(nf, ldir) < 0.0f;
+      if (!shadowed) shadowed = occl;
+      const float factor = shadowed ? 0.3f : 1.0f;
+      const float li = maxf(0.0f, dot(nf, ldir));
+      const float c = (1.0f * li) * factor;
+      color = v3(c, c, c);
+    }
+    return color;
+  }
+  // RT_SHADE_LAMBERT_SHADOW (MODE 1) and RT_SHADE_PRIMARY (MODE 2)
+  V3 n = v3(0.0f, 0.0f, 0.0f);
+  if (found) n = plane ? face_world_normal(ir, hit.prim) : neg(interpolated_world_normal(ir, hit.prim, hit.u, hit.v));
+  float c = 0.0f;
+  for (uint32_t l = 0; l < fp.nlights; ++l) {
+    const LightRec& Lr = fp.lights[l];
+    const V3 L = normalize(sub(v3(Lr.position[0], Lr.position[1], Lr.position[2]), P));
+    const float nl = dot(n, L);
+    const bool lit = found && nl > 0.0f;
+    float factor = 1.0f;
+    if (MODE == 1) {
+      HitRec sh;
+      if (STATS && lit) ++cnt.shadow;
+      if (trace_packet<true, STATS>(sc, P, normalize(L), 0.01f, 100000.0f, lit, sh, cnt)) factor = 0.3f;
+    }
+    if (lit) c = c + nl * factor;
+  }
+  c = c / (float)fp.nlights;
+  return found ? v3(c, c, c) : miss;
+}
+
 __device__ __forceinline__ void flush_stats(const Counters& c, unsigned long long* stats) {
   uint32_t v[6] = {c.primary, c.shadow, c.aabb, c.tri, c.inst, c.overflow};
   const int slot[6] = {0, 1, 2, 3, 4, 5};
@@ -476,6 +783,41 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void k_trace_frame(SceneView 
   if (STATS) flush_stats(cnt, stats);
 }
 
+// Wave-packet frame kernel: same pixel mapping as k_trace_frame; every lane runs the sample loop
+// (lanes outside the image or the row list join the packets dead) and stores only in-image pixels.
+template <int MODE, bool STATS>
+__global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void k_trace_frame_packet(SceneView sc, FrameParams fp,
+                                                               const uint32_t* __restrict__ rows,
+                                                               uint32_t* __restrict__ rgba8,
+                                                               float4* __restrict__ rgba32f,
+                                                               unsigned long long* __restrict__ stats) {
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint32_t px = blockIdx.x * 16u + (w & 1u) * 8u + (lane & 7u);
+  const uint32_t orow = blockIdx.y * 16u + (w >> 1) * 8u + (lane >> 3);
+  const bool inimg = px < fp.width && orow < fp.nrows;
+  Counters cnt;
+  uint32_t py = 0;
+  if (inimg) py = rows ? rows[orow] : orow;
+  const uint32_t k = fp.spp_side;
+  V3 acc = v3(0.0f, 0.0f, 0.0f);
+  for (uint32_t sy = 0; sy < k; ++sy)
+    for (uint32_t sx = 0; sx < k; ++sx) {
+      const float ox = ((float)sx + 0.5f) / (float)k;
+      const float oy = ((float)sy + 0.5f) / (float)k;
+      acc = add(acc, shade_sample_packet<MODE, STATS>(sc, fp, px, py, ox, oy, inimg, cnt));
+    }
+  if (k > 1) {
+    const float ns = (float)(k * k);
+    acc = v3(acc.x / ns, acc.y / ns, acc.z / ns);
+  }
+  if (inimg) {
+    const size_t o = (size_t)orow * fp.width + px;
+    rgba8[o] = unorm8(acc.x) | (unorm8(acc.y) << 8) | (unorm8(acc.z) << 16) | (255u << 24);
+    if (rgba32f) rgba32f[o] = make_float4(acc.x, acc.y, acc.z, 1.0f);
+  }
+  if (STATS) flush_stats(cnt, stats);
+}
+
 template <bool ANY_HIT, bool STATS>
 __global__ __launch_bounds__(kBlock) void k_trace_rays(SceneView sc, const float4* __restrict__ rays,
                                                        uint32_t n, uint4* __restrict__ hits,
@@ -512,11 +854,16 @@ __global__ void k_assemble(uint32_t W, uint32_t H, uint32_t nranks, uint32_t str
 
 template <int MODE, bool STATS>
 hipError_t launch_mode(const SceneView& sc, const FrameParams& fp, const uint32_t* rows, void* rgba8,
-                       float* rgba32f, unsigned long long* stats, hipStream_t s) {
+                       float* rgba32f, unsigned long long* stats, int schedule, hipStream_t s) {
   dim3 grid((fp.width + 15) / 16, (fp.nrows + 15) / 16);
-  size_t lds = (size_t)sc.lds_cap * kBlock * sizeof(int);
-  hipLaunchKernelGGL((k_trace_frame<MODE, STATS>), grid, dim3(kBlock), lds, s, sc, fp, rows,
-                     (uint32_t*)rgba8, (float4*)rgba32f, stats);
+  if (schedule == 0 && sc.stack_cap < kPacketStack) {
+    hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS>), grid, dim3(kBlock), 0, s, sc, fp, rows,
+                       (uint32_t*)rgba8, (float4*)rgba32f, stats);
+  } else {
+    size_t lds = (size_t)sc.lds_cap * kBlock * sizeof(int);
+    hipLaunchKernelGGL((k_trace_frame<MODE, STATS>), grid, dim3(kBlock), lds, s, sc, fp, rows,
+                       (uint32_t*)rgba8, (float4*)rgba32f, stats);
+  }
   return hipGetLastError();
 }
 
@@ -524,19 +871,17 @@ hipError_t launch_mode(const SceneView& sc, const FrameParams& fp, const uint32_
 
 hipError_t launch_trace_frame(const SceneView& sc, const FrameParams& fp, const uint32_t* d_rows,
                               void* rgba8, float* rgba32f, unsigned long long* d_stats, bool stats,
-                              int schedule, WavefrontBuffers* wf, hipStream_t s) {
-  (void)schedule;
-  (void)wf;
+                              int schedule, hipStream_t s) {
   switch (fp.shade_mode) {
     case 0:
-      return stats ? launch_mode<0, true>(sc, fp, d_rows, rgba8, rgba32f, d_stats, s)
-                   : launch_mode<0, false>(sc, fp, d_rows, rgba8, rgba32f, d_stats, s);
+      return stats ? launch_mode<0, true>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, s)
+                   : launch_mode<0, false>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, s);
     case 1:
-      return stats ? launch_mode<1, true>(sc, fp, d_rows, rgba8, rgba32f, d_stats, s)
-                   : launch_mode<1, false>(sc, fp, d_rows, rgba8, rgba32f, d_stats, s);
+      return stats ? launch_mode<1, true>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, s)
+                   : launch_mode<1, false>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, s);
     case 2:
-      return stats ? launch_mode<2, true>(sc, fp, d_rows, rgba8, rgba32f, d_stats, s)
-                   : launch_mode<2, false>(sc, fp, d_rows, rgba8, rgba32f, d_stats, s);
+      return stats ? launch_mode<2, true>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, s)
+                   : launch_mode<2, false>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, s);
     default:
       return hipErrorInvalidValue;
   }

@@ -5,6 +5,9 @@ camera_glm.json   glm::lookAt / glm::rotate from the reference's vendored glm, v
 frames_small.npz  oracle frames (RGBA8 + float32) of every config at small sizes; each is first
                   cross-checked against the independent float64 numpy restatement
                   (oracle/np_reference.py) and the script refuses to write on disagreement.
+                  Traversal counters for both schedules: <cfg>_stats (wave packets, the device
+                  default) and <cfg>_stats_lane (one traversal per pixel); the two schedules
+                  must render the identical image.
 
 The reference itself (HLSL under DXR) cannot run here: the frames pin the oracle against drift and
 give the GPU tests a fixed target; their link to the reference is the restatement + numpy check.
@@ -46,7 +49,11 @@ def frames():
     data = {}
     for name, (w, h) in SIZES.items():
         spec = scenes.config(name).with_size(w, h)
-        o8, o32, st = oracle.Scene(spec).render_spec(spec, nthreads=8)
+        sc = oracle.Scene(spec)
+        o8, o32, st = sc.render_spec(spec, nthreads=8)
+        l8, l32, st_lane = sc.render_spec(spec, nthreads=8, schedule=1)
+        if not (np.array_equal(o8, l8) and np.array_equal(o32.view(np.uint32), l32.view(np.uint32))):
+            raise SystemExit(f"{name}: packet and per-lane schedules render different images")
         if name in NUMPY_CHECK:
             img, _ = np_reference.Scene(spec).render(spec.camera_buffer())
             d = float(np.abs(img - o32[..., :3]).max())
@@ -56,9 +63,11 @@ def frames():
         data[f"{name}_rgba8"] = o8
         data[f"{name}_rgba32f"] = o32
         data[f"{name}_stats"] = st
+        data[f"{name}_stats_lane"] = st_lane
     np.savez_compressed(os.path.join(HERE, "frames_small.npz"), **data)
 
 
 if __name__ == "__main__":
-    camera()
+    if "--frames-only" not in sys.argv:
+        camera()
     frames()

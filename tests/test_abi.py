@@ -32,7 +32,7 @@ def test_python_binding_covers_header():
 
 
 def test_status_strings_and_version():
-    assert rt.lib.rt_api_version() == 1
+    assert rt.lib.rt_api_version() == 2
     assert rt.lib.rt_status_string(rt.RT_E_IO) == b"RT_E_IO"
     assert rt.lib.rt_status_string(rt.RT_OK) == b"RT_OK"
 

@@ -30,7 +30,7 @@ def fresh_ctx():
     return rt.Context(0)
 
 
-def gpu_render(c, spec, rows=None, schedule=rt.RT_SCHED_MEGAKERNEL):
+def gpu_render(c, spec, rows=None, schedule=rt.RT_SCHED_PACKET):
     nrows = spec.height if rows is None else len(rows)
     out8 = torch.empty((nrows, spec.width, 4), dtype=torch.uint8, device="cuda")
     out32 = torch.empty((nrows, spec.width, 4), dtype=torch.float32, device="cuda")
@@ -129,28 +129,49 @@ SMALL = {"REF": (160, 90), "C1": (128, 128), "C2": (192, 108), "C3": (192, 108),
          "C5": (96, 54)}
 
 
+SCHEDULES = {"packet": rt.RT_SCHED_PACKET, "lane": rt.RT_SCHED_LANE}
+
+
+@pytest.mark.parametrize("sched", list(SCHEDULES))
 @pytest.mark.parametrize("name", list(SMALL))
-def test_frame_parity_small(name):
+def test_frame_parity_small(name, sched):
     spec = scenes.config(name).with_size(*SMALL[name])
     c, o = load_both(spec)
-    g8, g32 = gpu_render(c, spec)
+    g8, g32 = gpu_render(c, spec, schedule=SCHEDULES[sched])
     o8, o32, _ = o.render_spec(spec, nthreads=8)
-    assert_images_equal(g8, g32, o8, o32, name)
+    assert_images_equal(g8, g32, o8, o32, f"{name}/{sched}")
     c.close()
 
 
-@pytest.mark.parametrize("name", ["REF", "C2", "C4"])
-def test_counters_match_oracle(name):
-    spec = scenes.config(name).with_size(*SMALL[name])
+@pytest.mark.parametrize("sched", list(SCHEDULES))
+@pytest.mark.parametrize("name", ["REF", "C2", "C2F", "C4", "C5"])
+def test_counters_match_oracle(name, sched):
+    """Traversal counters equal the oracle's emulation of the same schedule: same visit order."""
+    spec = scenes.config(name).with_size(*SMALL.get(name, (192, 108)))
     c, o = load_both(spec)
     c.set_stats(True)
     c.stats_reset()
-    gpu_render(c, spec)
+    gpu_render(c, spec, schedule=SCHEDULES[sched])
     s = c.stats()
-    _, _, ost = o.render_spec(spec, nthreads=4)
+    _, _, ost = o.render_spec(spec, nthreads=8, schedule=SCHEDULES[sched])
     keys = ["primary_rays", "shadow_rays", "aabb_tests", "tri_tests", "instance_entries", "stack_overflows"]
     assert [s[k] for k in keys] == [int(x) for x in ost[:6]]
     assert s["stack_overflows"] == 0
+    c.close()
+
+
+def test_packet_counters_on_row_subset():
+    """Packet tiles follow the row list (8 list entries per tile row), as the oracle emulates."""
+    spec = scenes.config("C2").with_size(160, 96)
+    c, o = load_both(spec)
+    rows = np.array([1, 2, 3, 7, 11, 12, 40, 41, 42, 60, 61, 90, 95], np.uint32)
+    c.set_stats(True)
+    c.stats_reset()
+    g8, g32 = gpu_render(c, spec, rows=rows)
+    s = c.stats()
+    o8, o32, ost = o.render_spec(spec, rows=rows, nthreads=4)
+    assert_images_equal(g8, g32, o8, o32, "row subset")
+    assert [s[k] for k in ["primary_rays", "shadow_rays", "aabb_tests", "tri_tests"]] == [int(x) for x in ost[:4]]
     c.close()
 
 
@@ -335,7 +356,13 @@ def test_gpu_frames_equal_committed_goldens(name):
     spec = scenes.config(name).with_size(*GOLDEN_SIZES[name])
     c = fresh_ctx()
     scenes.upload(c, spec)
-    g8, g32 = gpu_render(c, spec)
-    assert np.array_equal(g8, gold[f"{name}_rgba8"])
-    assert np.array_equal(g32.view(np.uint32), gold[f"{name}_rgba32f"].view(np.uint32))
+    for sched, key in ((rt.RT_SCHED_PACKET, "stats"), (rt.RT_SCHED_LANE, "stats_lane")):
+        c.set_stats(True)
+        c.stats_reset()
+        g8, g32 = gpu_render(c, spec, schedule=sched)
+        s = c.stats()
+        assert np.array_equal(g8, gold[f"{name}_rgba8"])
+        assert np.array_equal(g32.view(np.uint32), gold[f"{name}_rgba32f"].view(np.uint32))
+        assert [s[k] for k in ["primary_rays", "shadow_rays", "aabb_tests", "tri_tests"]] == \
+            [int(x) for x in gold[f"{name}_{key}"][:4]]
     c.close()

@@ -109,10 +109,12 @@ def test_tie_break_duplicate_instances():
 @pytest.mark.parametrize("name", list(SIZES))
 def test_oracle_matches_golden_frames(name):
     spec = scenes.config(name).with_size(*SIZES[name])
-    o8, o32, st = oracle.Scene(spec).render_spec(spec, nthreads=8)
-    assert np.array_equal(o8, GOLD[f"{name}_rgba8"])
-    assert np.array_equal(o32.view(np.uint32), GOLD[f"{name}_rgba32f"].view(np.uint32))
-    assert np.array_equal(st, GOLD[f"{name}_stats"])
+    sc = oracle.Scene(spec)
+    for sched, key in ((0, "stats"), (1, "stats_lane")):
+        o8, o32, st = sc.render_spec(spec, nthreads=8, schedule=sched)
+        assert np.array_equal(o8, GOLD[f"{name}_rgba8"])
+        assert np.array_equal(o32.view(np.uint32), GOLD[f"{name}_rgba32f"].view(np.uint32))
+        assert np.array_equal(st, GOLD[f"{name}_{key}"])
 
 
 @pytest.mark.parametrize("name", ["REF", "C1", "C2F", "C3"])

@@ -1,7 +1,8 @@
 """Interleaved A/B timing of library variants in ONE process (cdna guide §5.4 rule 24).
 
 python tools/ab.py --configs C2,C4 --rounds 7 --steps 20 base=realtimeraytracing_gradproject_amd/lib/librtamd.so \
-       w6=realtimeraytracing_gradproject_amd/lib/variants/w6/librtamd.so
+       w6=realtimeraytracing_gradproject_amd/lib/variants/w6/librtamd.so lane=realtimeraytracing_gradproject_amd/lib/librtamd.so@1
+A variant is name=library[@schedule] (schedule: 0 packet, 1 per-lane; default --schedule).
 Each variant's frame must equal the first variant's bit for bit (RGBA8 and float) or the run fails.
 """
 import argparse
@@ -29,10 +30,12 @@ def main():
     ap.add_argument("--schedule", type=int, default=0)
     ap.add_argument("--mode", type=int, default=-1, help="override the shade mode (2 = primary rays only)")
     a = ap.parse_args()
-    libs = {}
+    libs, scheds = {}, {}
     for v in a.variants:
         name, path = v.split("=", 1)
+        path, _, sch = path.partition("@")
         libs[name] = rt._load(path)
+        scheds[name] = int(sch) if sch else a.schedule
     res = {}
     for cfg in a.configs.split(","):
         spec = scenes.config(cfg)
@@ -44,7 +47,7 @@ def main():
         for name, lib in libs.items():
             c = rt.Context(0, library=lib)
             scenes.upload(c, spec)
-            c.set_schedule(a.schedule)
+            c.set_schedule(scheds[name])
             ctxs[name] = c
             outs[name] = (torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda"),
                           torch.zeros((H, W, 4), dtype=torch.float32, device="cuda"))
