@@ -315,9 +315,13 @@ static uint32_t collapse(const onode* bin, uint32_t nbin, o4node* out, uint32_t*
       const int cnt = gather4(bin, q[head], ref, box);
       o4node nd;
       memset(&nd, 0, sizeof(nd));
+      uint32_t valid = 0;
       for (int j = 0; j < 4; ++j) {
         int32_t r = O_EMPTY;
-        if (j < cnt) {
+        /* unused slots: lo = hi = +inf, rejected by every slab test */
+        nd.lox[j] = nd.loy[j] = nd.loz[j] = nd.hix[j] = nd.hiy[j] = nd.hiz[j] = INFINITY;
+        if (j < cnt && ref[j] != O_EMPTY) {
+          ++valid;
           nd.lox[j] = box[j][0]; nd.loy[j] = box[j][1]; nd.loz[j] = box[j][2];
           nd.hix[j] = box[j][3]; nd.hiy[j] = box[j][4]; nd.hiz[j] = box[j][5];
           if (ref[j] >= 0) { q[tail] = ref[j]; r = tail; ps[tail] = ps[head] + cnt - 1; ++tail; }
@@ -325,7 +329,7 @@ static uint32_t collapse(const onode* bin, uint32_t nbin, o4node* out, uint32_t*
         }
         nd.child[j] = r;
       }
-      nd.count = (uint32_t)cnt;
+      nd.count = valid;
       if (ps[head] + cnt - 1 > best) best = ps[head] + cnt - 1;
       out[head] = nd;
     }
@@ -390,7 +394,8 @@ static uint32_t lbvh(const float* primbox, uint32_t n, o4node** out4, uint32_t* 
       nd.lo0[k] = nd.lo1[k] = primbox[k];
       nd.hi0[k] = nd.hi1[k] = primbox[3 + k];
     }
-    nd.c0 = nd.c1 = ~0;
+    nd.c0 = ~0;
+    nd.c1 = O_EMPTY;
     nodes[0] = nd;
   } else {
     int ni = (int)n - 1;

@@ -25,6 +25,9 @@
 #ifndef RT_COND_PUSH
 #define RT_COND_PUSH 1      // push only hit children (vs unconditional LDS writes, predicated sp)
 #endif
+#ifndef RT_PACKET_OCTANT
+#define RT_PACKET_OCTANT 0  // packet: near/far plane loads when the live lanes share an octant
+#endif
 #ifndef RT_ARGMIN_ORDER
 #define RT_ARGMIN_ORDER 0   // nearest child only (vs the full 4-sort; the sort culls better)
 #endif
@@ -258,7 +261,8 @@ RT_HD void slab4_octant(const float* nx, const float* fx, const float* ny, const
     const float tnz = __builtin_fmaf(nz[k], invd.z, noinv.z), tfz = __builtin_fmaf(fz[k], invd.z, noinv.z);
     const float n = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
     const float f = fminf(fminf(tfx, tfy), fminf(tfz, tbest));
-    tn[k] = (child[k] != kEmptyChild && n <= f * 1.0000004f) ? n : __builtin_inff();
+    (void)child;  // unused slots carry +inf boxes, rejected here like any missed child
+    tn[k] = n <= f * 1.0000004f ? n : __builtin_inff();
   }
 }
 

@@ -288,16 +288,19 @@ __global__ void k_single(const float* __restrict__ primbox, bool leaf_ref_is_pri
     nd.lo0[k] = nd.lo1[k] = primbox[k];
     nd.hi0[k] = nd.hi1[k] = primbox[3 + k];
   }
-  nd.c0 = nd.c1 = ~0;
-  (void)leaf_ref_is_prim;  // ~slot 0 == ~prim 0
+  nd.c0 = ~0;  // ~slot 0 == ~prim 0
+  nd.c1 = kEmptyChild;
+  (void)leaf_ref_is_prim;
   nd.pad0 = nd.pad1 = 0;
   nodes[0] = nd;
 }
 
-// 7. collapse the binary tree into 4-wide nodes in BFS order: a 4-wide node at binary depth 2k
-// takes its children's children (a leaf child stays a child). One workgroup walks the levels;
-// each level's new node indices come from a block-wide exclusive scan of per-node internal-child
-// counts (deterministic, no atomics), so the oracle's sequential BFS yields the same array.
+// 7. collapse the binary tree into 4-wide nodes in BFS order (children chosen by gather4). One
+// workgroup walks the levels; each level's new node indices come from a block-wide exclusive
+// scan of per-node internal-child counts (deterministic, no atomics), so the oracle's sequential
+// BFS yields the same array. Unused slots get kEmptyChild and the box lo = hi = +inf, which
+// every slab test rejects (min/max and near/far forms alike: t is +inf or -inf on every axis),
+// so traversal needs no per-slot validity mask.
 // It also bounds the traversal stack: a visited node pushes (count - 1) siblings, so the most a
 // root-to-node path can leave on the stack is ps[node] + count(node) - 1, ps = sum over the
 // ancestors. info[0] = node count, info[1] = levels, info[2] = that maximum.
@@ -389,10 +392,13 @@ __global__ __launch_bounds__(1024) void k_collapse(const BinNode* __restrict__ b
         int o = excl;
         const int below = ps[base + i] + cnt - 1;
         lmax = below > lmax ? below : lmax;
+        uint32_t valid = 0;
         for (int j = 0; j < 4; ++j) {
-          float b6[6] = {0, 0, 0, 0, 0, 0};
+          const float inf = __builtin_inff();
+          float b6[6] = {inf, inf, inf, inf, inf, inf};
           int32_t r = kEmptyChild;
-          if (j < cnt) {
+          if (j < cnt && ref[j] != kEmptyChild) {
+            ++valid;
             for (int a = 0; a < 6; ++a) b6[a] = box[j][a];
             if (ref[j] >= 0) {
               const int pos = next_total + o;
@@ -412,7 +418,7 @@ __global__ __launch_bounds__(1024) void k_collapse(const BinNode* __restrict__ b
           nd.hiz[j] = b6[5];
           nd.child[j] = r;
         }
-        nd.count = (uint32_t)cnt;
+        nd.count = valid;
         nd.pad[0] = nd.pad[1] = nd.pad[2] = 0;
         out[base + i] = nd;
       }

@@ -297,6 +297,7 @@ __device__ __forceinline__ bool packet_node(const RT_CONST char* pool, int ref, 
   const int cref[4] = {ch.x, ch.y, ch.z, ch.w};
   uint64_t hm[4];
   uint32_t vkey[4];  // per lane: |entry distance| if this lane's test accepted the child, else +inf
+#if RT_PACKET_OCTANT
   if (ry.oct < 8u) {
     // shared octant: near/far planes by address (bitwise equal to the min/max form)
     const uint32_t ox = (ry.oct & 1u) ? 16u : 0u, oy = (ry.oct & 2u) ? 48u : 32u, oz = (ry.oct & 4u) ? 80u : 64u;
@@ -314,10 +315,13 @@ __device__ __forceinline__ bool packet_node(const RT_CONST char* pool, int ref, 
       const float n = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
       const float f = fminf(fminf(tfx, tfy), fminf(tfz, tbest));
       const bool h = live && n <= f * 1.0000004f;
-      hm[k] = cref[k] != kEmptyChild ? wave_ballot(h) : 0ull;
+      hm[k] = wave_ballot(h);
       vkey[k] = h ? (__float_as_uint(n) & 0x7fffffffu) : 0x7f800000u;
     }
-  } else {
+  } else
+#endif
+  {
+    // unused slots hold lo = hi = +inf boxes that every lane rejects: no validity mask
     const f4v a0 = cld4(nb), a1 = cld4(nb + 16), a2 = cld4(nb + 32);
     const f4v a3 = cld4(nb + 48), a4 = cld4(nb + 64), a5 = cld4(nb + 80);
     const float lox[4] = {a0.x, a0.y, a0.z, a0.w}, hix[4] = {a1.x, a1.y, a1.z, a1.w};
@@ -331,13 +335,11 @@ __device__ __forceinline__ bool packet_node(const RT_CONST char* pool, int ref, 
       const float n = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), tmin));
       const float f = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tbest));
       const bool h = live && n <= f * 1.0000004f;
-      hm[k] = cref[k] != kEmptyChild ? wave_ballot(h) : 0ull;
+      hm[k] = wave_ballot(h);
       vkey[k] = h ? (__float_as_uint(n) & 0x7fffffffu) : 0x7f800000u;
     }
   }
-  if (STATS && live)
-    cnt.aabb += (uint32_t)(cref[0] != kEmptyChild) + (uint32_t)(cref[1] != kEmptyChild) +
-                (uint32_t)(cref[2] != kEmptyChild) + (uint32_t)(cref[3] != kEmptyChild);
+  if (STATS && live) cnt.aabb += *(const RT_CONST uint32_t*)(nb + 112);  // Bvh4Node::count
   if ((hm[0] | hm[1] | hm[2] | hm[3]) == 0) return false;
   // uniform keys: the lead lane's key, all-ones where no lane entered the child
   uint32_t key[4];
@@ -412,7 +414,7 @@ __device__ bool trace_packet(const SceneView& sc, V3 o, V3 d, float tmin, float 
   w.d = d;
   w.invd = v3(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
   w.noinv = neg(mul(o, w.invd));
-  w.oct = wave_octant(w.invd, live, lead);
+  w.oct = RT_PACKET_OCTANT ? wave_octant(w.invd, live, lead) : 8u;
   WaveStack stk;
   const int cap = sc.stack_cap;  // < kPacketStack (checked at launch): lane 63 stays spare
   int sp = 0;
@@ -438,7 +440,7 @@ __device__ bool trace_packet(const SceneView& sc, V3 o, V3 d, float tmin, float 
       b.d = xform_dir(m, d);
       b.invd = v3(safe_inv(b.d.x), safe_inv(b.d.y), safe_inv(b.d.z));
       b.noinv = neg(mul(b.o, b.invd));
-      b.oct = wave_octant(b.invd, live, lead);
+      b.oct = RT_PACKET_OCTANT ? wave_octant(b.invd, live, lead) : 8u;
       const int base = sp;
       int bref = (int)ir.pool_root;
       while (true) {
