@@ -290,8 +290,8 @@ struct PacketRay {
 // the bookkeeping is plain integer SALU work. Returns false when no child is entered.
 template <bool STATS>
 __device__ __forceinline__ bool packet_node(const RT_CONST char* pool, int ref, const PacketRay& ry, float tmin,
-                                            float tbest, bool live, uint32_t lead, WaveStack& stk, int& sp,
-                                            int cap, int& next, Counters& cnt) {
+                                            float tbest, bool live, uint64_t livemask, uint32_t lead,
+                                            WaveStack& stk, int& sp, int cap, int& next, Counters& cnt) {
   const RT_CONST char* nb = pool + ((size_t)(uint32_t)ref << 7);
   const i4v ch = *(const RT_CONST i4v*)(nb + 96);
   const int cref[4] = {ch.x, ch.y, ch.z, ch.w};
@@ -314,8 +314,8 @@ __device__ __forceinline__ bool packet_node(const RT_CONST char* pool, int ref, 
       const float tnz = __builtin_fmaf(nz[k], ry.invd.z, ry.noinv.z), tfz = __builtin_fmaf(fz[k], ry.invd.z, ry.noinv.z);
       const float n = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
       const float f = fminf(fminf(tfx, tfy), fminf(tfz, tbest));
-      const bool h = live && n <= f * 1.0000004f;
-      hm[k] = wave_ballot(h);
+      const bool h = n <= f * 1.0000004f;  // dead lanes are masked out of the ballot; only the lead's key is read
+      hm[k] = wave_ballot(h) & livemask;
       vkey[k] = h ? (__float_as_uint(n) & 0x7fffffffu) : 0x7f800000u;
     }
   } else
@@ -334,8 +334,8 @@ __device__ __forceinline__ bool packet_node(const RT_CONST char* pool, int ref, 
       const float tlz = __builtin_fmaf(loz[k], ry.invd.z, ry.noinv.z), thz = __builtin_fmaf(hiz[k], ry.invd.z, ry.noinv.z);
       const float n = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), tmin));
       const float f = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tbest));
-      const bool h = live && n <= f * 1.0000004f;
-      hm[k] = wave_ballot(h);
+      const bool h = n <= f * 1.0000004f;  // dead lanes are masked out of the ballot; only the lead's key is read
+      hm[k] = wave_ballot(h) & livemask;
       vkey[k] = h ? (__float_as_uint(n) & 0x7fffffffu) : 0x7f800000u;
     }
   }
@@ -344,8 +344,10 @@ __device__ __forceinline__ bool packet_node(const RT_CONST char* pool, int ref, 
   // uniform keys: the lead lane's key, all-ones where no lane entered the child
   uint32_t key[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k)
-    key[k] = hm[k] ? (uint32_t)__builtin_amdgcn_readlane((int)vkey[k], (int)lead) : 0xffffffffu;
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)vkey[k], (int)lead);
+    key[k] = hm[k] ? kl : 0xffffffffu;
+  }
   uint32_t kb = key[0];
   int rb = cref[0];
   uint32_t ib = 0;
@@ -356,15 +358,17 @@ __device__ __forceinline__ bool packet_node(const RT_CONST char* pool, int ref, 
     rb = s ? cref[k] : rb;
     ib = s ? (uint32_t)k : ib;
   }
+  // pushed set P (entered, not the nearest) as a 4-bit mask; descending slot order puts child k
+  // at sp + popcount(P >> (k + 1)), so the four writes are independent of each other
+  const uint32_t ent = (hm[0] ? 1u : 0u) | (hm[1] ? 2u : 0u) | (hm[2] ? 4u : 0u) | (hm[3] ? 8u : 0u);
+  const uint32_t P = ent & ~(1u << ib);
+  if (STATS && live && sp + __builtin_popcount(P) > cap) ++cnt.overflow;
 #pragma unroll
-  for (int k = 3; k >= 0; --k) {
-    // e = entered and not the nearest, as 0/1 integers (no lane masks)
-    const uint32_t e = __builtin_elementwise_min(~key[k], 1u) & __builtin_elementwise_min((uint32_t)k ^ ib, 1u);
-    if (STATS && live && e && sp >= cap) ++cnt.overflow;
-    const int lane = (int)(((uint32_t)(sp - (kPacketStack - 1)) & (0u - e)) + (kPacketStack - 1));
-    stk.put(lane, cref[k]);
-    sp += (int)e;
+  for (int k = 0; k < 4; ++k) {
+    const int pos = sp + __builtin_popcount(P >> (k + 1));
+    stk.put(((P >> k) & 1u) ? pos : kPacketStack - 1, cref[k]);
   }
+  sp = __builtin_amdgcn_readfirstlane(sp + __builtin_popcount(P));  // uniform by construction: an SGPR
   next = rb;
   return true;
 }
@@ -424,7 +428,7 @@ __device__ bool trace_packet(const SceneView& sc, V3 o, V3 d, float tmin, float 
   while (true) {
     int next;
     if (ref >= 0) {
-      if (packet_node<STATS>(pool, ref, w, tmin, hit.t, live, lead, stk, sp, cap, next, cnt)) {
+      if (packet_node<STATS>(pool, ref, w, tmin, hit.t, live, livemask, lead, stk, sp, cap, next, cnt)) {
         ref = next;
         continue;
       }
@@ -445,7 +449,7 @@ __device__ bool trace_packet(const SceneView& sc, V3 o, V3 d, float tmin, float 
       int bref = (int)ir.pool_root;
       while (true) {
         if (bref >= 0) {
-          if (packet_node<STATS>(pool, bref, b, tmin, hit.t, live, lead, stk, sp, cap, next, cnt)) {
+          if (packet_node<STATS>(pool, bref, b, tmin, hit.t, live, livemask, lead, stk, sp, cap, next, cnt)) {
             bref = next;
             continue;
           }
