@@ -761,13 +761,19 @@ typedef struct {
 
 static uint32_t f2bits(float x) { uint32_t b; memcpy(&b, &x, 4); return b; }
 
-/* one node: returns 0 when no child is entered, else pushes the others and sets *next */
-static int opk_node(const o4node* nd, const opkray* ry, float tmin, const ohit* h, const int* live, int lead,
-                    int* stack, int* sp, int cap, int* next, ostats* st) {
+static int olead(const int* live) {
+  for (int l = 0; l < OPK; ++l) if (live[l]) return l;
+  return -1;
+}
+
+/* one node (packet_node in rt_trace.hip): returns 1 with *next set, 0 when nothing is left to
+ * descend into, 2 when an any-hit packet has no live lane left. leaves != NULL (BLAS level):
+ * entered triangle children are tested here, in slot order, and never pushed. */
+static int opk_node(const o4node* nd, const opkray* ry, float tmin, ohit* h, int* live, int* lead,
+                    const otri* leaves, uint32_t cur, int any, int* found, int* stack, int* sp, int cap,
+                    int* next, ostats* st) {
   uint64_t hm[4] = {0, 0, 0, 0};
   uint32_t vkey[OPK][4];
-  int nvalid = 0;
-  for (int k = 0; k < 4; ++k) nvalid += nd->child[k] != O_EMPTY;
   for (int l = 0; l < OPK; ++l) {
     for (int k = 0; k < 4; ++k) {
       float tlx = fmaf(nd->lox[k], ry->invd[l].x, ry->no[l].x), thx = fmaf(nd->hix[k], ry->invd[l].x, ry->no[l].x);
@@ -775,34 +781,60 @@ static int opk_node(const o4node* nd, const opkray* ry, float tmin, const ohit* 
       float tlz = fmaf(nd->loz[k], ry->invd[l].z, ry->no[l].z), thz = fmaf(nd->hiz[k], ry->invd[l].z, ry->no[l].z);
       float n = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), tmin));
       float f = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), h[l].t));
-      int hit = live[l] && n <= f * 1.0000004f;
-      if (hit && nd->child[k] != O_EMPTY) hm[k] |= 1ull << l;
+      int hit = n <= f * 1.0000004f; /* empty slots hold +inf boxes: never accepted */
+      if (hit && live[l]) hm[k] |= 1ull << l;
       vkey[l][k] = hit ? (f2bits(n) & 0x7fffffffu) : 0x7f800000u;
     }
-    if (live[l]) st->v[2] += (uint64_t)nvalid;
+    if (live[l]) st->v[2] += nd->count;
   }
-  if ((hm[0] | hm[1] | hm[2] | hm[3]) == 0) return 0;
+  uint32_t ent = 0;
+  for (int k = 0; k < 4; ++k) if (hm[k]) ent |= 1u << k;
+  if (!ent) return 0;
+  if (leaves) {
+    uint32_t leafbits = 0;
+    for (int k = 0; k < 4; ++k) if (nd->child[k] < 0) leafbits |= 1u << k;
+    const uint32_t tl = ent & leafbits;
+    ent &= ~leafbits;
+    for (int k = 0; k < 4; ++k) {
+      if (!((tl >> k) & 1u)) continue;
+      const otri* tr = leaves + (~nd->child[k]);
+      for (int l = 0; l < OPK; ++l) {
+        if (!live[l]) continue;
+        float t, u, v;
+        st->v[3]++;
+        if (omt(ry->o[l], ry->d[l], tr, &t, &u, &v) && t >= tmin && better(t, cur, tr->prim, &h[l])) {
+          h[l].t = t; h[l].u = u; h[l].v = v; h[l].inst = cur; h[l].prim = tr->prim;
+          found[l] = 1;
+          if (any) live[l] = 0;
+        }
+      }
+    }
+    if (any) {
+      *lead = olead(live);
+      if (*lead < 0) return 2;
+      uint64_t lm = 0;
+      for (int l = 0; l < OPK; ++l) if (live[l]) lm |= 1ull << l;
+      for (int k = 0; k < 4; ++k) if (!(hm[k] & lm)) ent &= ~(1u << k);
+    }
+    if (!ent) return 0;
+  }
   uint32_t key[4];
-  for (int k = 0; k < 4; ++k) key[k] = hm[k] ? vkey[lead][k] : 0xffffffffu;
+  for (int k = 0; k < 4; ++k) key[k] = ((ent >> k) & 1u) ? vkey[*lead][k] : 0xffffffffu;
   /* nearest first (lowest slot on ties), the other entered children pushed in descending slot order */
   uint32_t kb = key[0];
   int rb = nd->child[0], ib = 0;
   for (int k = 1; k < 4; ++k)
     if (key[k] < kb) { kb = key[k]; rb = nd->child[k]; ib = k; }
+  const uint32_t P = ent & ~(1u << ib);
+  if (*sp + __builtin_popcount(P) > cap) /* never: cap is the exact worst case; counted per live lane */
+    for (int l = 0; l < OPK; ++l) st->v[5] += live[l] ? 1u : 0u;
   for (int k = 3; k >= 0; --k) {
-    if (key[k] == 0xffffffffu || k == ib) continue;
-    if (*sp >= cap) /* never: cap is the exact worst case; counted per live lane like the device */
-      for (int l = 0; l < OPK; ++l) st->v[5] += live[l] ? 1u : 0u;
+    if (!((P >> k) & 1u)) continue;
     if (*sp < OPK) stack[*sp] = nd->child[k];
     ++*sp;
   }
   *next = rb;
   return 1;
-}
-
-static int olead(const int* live) {
-  for (int l = 0; l < OPK; ++l) if (live[l]) return l;
-  return -1;
 }
 
 static void opacket(const oracle_scene* s, const vec3* o, const vec3* d, float tmin, float tmax, int any,
@@ -826,7 +858,10 @@ static void opacket(const oracle_scene* s, const vec3* o, const vec3* d, float t
   int sp = 0, ref = 0, next;
   for (;;) {
     if (ref >= 0) {
-      if (opk_node(s->tlas + ref, &w, tmin, h, live, lead, stack, &sp, cap, &next, st)) { ref = next; continue; }
+      if (opk_node(s->tlas + ref, &w, tmin, h, live, &lead, NULL, 0u, any, found, stack, &sp, cap, &next, st) == 1) {
+        ref = next;
+        continue;
+      }
     } else {
       const uint32_t cur = (uint32_t)(~ref);
       const oinst* ir = &s->inst[cur];
@@ -841,25 +876,11 @@ static void opacket(const oracle_scene* s, const vec3* o, const vec3* d, float t
       const int base = sp;
       int bref = 0;
       for (;;) {
-        if (bref >= 0) {
-          if (opk_node(bl->nodes + bref, &b, tmin, h, live, lead, stack, &sp, cap, &next, st)) { bref = next; continue; }
-        } else {
-          const otri* tr = bl->tris + (~bref);
-          for (int l = 0; l < OPK; ++l) {
-            if (!live[l]) continue;
-            float t, u, v;
-            st->v[3]++;
-            if (omt(b.o[l], b.d[l], tr, &t, &u, &v) && t >= tmin && better(t, cur, tr->prim, &h[l])) {
-              h[l].t = t; h[l].u = u; h[l].v = v; h[l].inst = cur; h[l].prim = tr->prim;
-              found[l] = 1;
-              if (any) live[l] = 0;
-            }
-          }
-          if (any) {
-            lead = olead(live);
-            if (lead < 0) return;
-          }
-        }
+        /* only internal nodes reach here: triangle children are tested inside opk_node */
+        const int r = opk_node(bl->nodes + bref, &b, tmin, h, live, &lead, bl->tris, cur, any, found, stack, &sp,
+                               cap, &next, st);
+        if (r == 1) { bref = next; continue; }
+        if (r == 2) return;
         if (sp == base) break;
         bref = stack[--sp];
       }

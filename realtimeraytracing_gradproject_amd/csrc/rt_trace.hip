@@ -283,15 +283,45 @@ struct PacketRay {
   uint32_t oct;  // octant shared by the live lanes, or 8
 };
 
-// One node of the packet walk: slab tests of the 4 children for every live lane, then the
-// entered children (any live lane accepts) go nearest first (the lead lane's entry distance,
-// lowest slot on ties); the other entered ones are pushed in descending slot order, so the
-// lowest slot pops next. Pushes that do not happen write the spare lane kPacketStack - 1, and
-// the bookkeeping is plain integer SALU work. Returns false when no child is entered.
-template <bool STATS>
-__device__ __forceinline__ bool packet_node(const RT_CONST char* pool, int ref, const PacketRay& ry, float tmin,
-                                            float tbest, bool live, uint64_t livemask, uint32_t lead,
-                                            WaveStack& stk, int& sp, int cap, int& next, Counters& cnt) {
+// Triangle leaf for every live lane (uniform triangle, scalar loads). ANY_HIT: a lane that
+// accepts a hit leaves the packet.
+template <bool ANY_HIT, bool STATS>
+__device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref, const PacketRay& ry, float tmin,
+                                           uint32_t cur, bool& live, bool& found, HitRec& hit, Counters& cnt) {
+  const RT_CONST f4v* tq = (const RT_CONST f4v*)(tpool + (~ref));
+  const f4v ta = tq[0], tb = tq[1], tc = tq[2];
+  if (STATS && live) ++cnt.tri;
+  float t, u, v;
+  const bool ok = moller_trumbore(ry.o, ry.d, v3(ta.x, ta.y, ta.z), v3(tb.x, tb.y, tb.z), v3(tc.x, tc.y, tc.z), t, u, v);
+  if (live && ok && t >= tmin) {
+    const uint32_t prim = __float_as_uint(ta.w);
+    const bool better = t < hit.t || (t == hit.t && (cur < hit.inst || (cur == hit.inst && prim < hit.prim)));
+    if (better) {
+      hit.t = t;
+      hit.u = u;
+      hit.v = v;
+      hit.inst = cur;
+      hit.prim = prim;
+      found = true;
+      if (ANY_HIT) live = false;
+    }
+  }
+}
+
+// One node of the packet walk: slab tests of the 4 children for every live lane; a child is
+// entered when any live lane accepts it. LEAVES (BLAS level): entered triangle children are
+// tested right here, in slot order, instead of going through the stack. The entered internal
+// children (TLAS: also instance leaves) go nearest first by the lead lane's entry distance
+// (lowest slot on ties); the others are pushed in descending slot order, so the lowest slot pops
+// next. Pushes that do not happen write the spare lane kPacketStack - 1; the bookkeeping is
+// plain integer SALU work. Returns 1 with *next set, 0 when nothing is left to descend into,
+// 2 when an any-hit packet has no live lane left.
+template <bool ANY_HIT, bool STATS, bool LEAVES>
+__device__ __forceinline__ int packet_node(const RT_CONST char* pool, const RT_CONST TriRec* tpool, int ref,
+                                           const PacketRay& ry, float tmin, uint32_t cur, bool& live,
+                                           uint64_t& livemask, uint32_t& lead, bool& found, HitRec& hit,
+                                           WaveStack& stk, int& sp, int cap, int& next, Counters& cnt) {
+  const float tbest = hit.t;
   const RT_CONST char* nb = pool + ((size_t)(uint32_t)ref << 7);
   const i4v ch = *(const RT_CONST i4v*)(nb + 96);
   const int cref[4] = {ch.x, ch.y, ch.z, ch.w};
@@ -340,13 +370,35 @@ __device__ __forceinline__ bool packet_node(const RT_CONST char* pool, int ref, 
     }
   }
   if (STATS && live) cnt.aabb += *(const RT_CONST uint32_t*)(nb + 112);  // Bvh4Node::count
-  if ((hm[0] | hm[1] | hm[2] | hm[3]) == 0) return false;
-  // uniform keys: the lead lane's key, all-ones where no lane entered the child
+  uint32_t ent = (hm[0] ? 1u : 0u) | (hm[1] ? 2u : 0u) | (hm[2] ? 4u : 0u) | (hm[3] ? 8u : 0u);
+  if (ent == 0) return 0;
+  if (LEAVES) {
+    const uint32_t leafbits = (cref[0] < 0 ? 1u : 0u) | (cref[1] < 0 ? 2u : 0u) | (cref[2] < 0 ? 4u : 0u) |
+                              (cref[3] < 0 ? 8u : 0u);
+    uint32_t tl = ent & leafbits;
+    ent &= ~leafbits;
+    while (tl) {
+      const uint32_t k = (uint32_t)__builtin_ctz(tl);
+      tl &= tl - 1u;
+      const int tr = k == 0 ? cref[0] : k == 1 ? cref[1] : k == 2 ? cref[2] : cref[3];
+      packet_tri<ANY_HIT, STATS>(tpool, tr, ry, tmin, cur, live, found, hit, cnt);
+    }
+    if (ANY_HIT) {
+      livemask = wave_ballot(live);
+      if (livemask == 0) return 2;
+      lead = lead_lane(livemask);
+      // children only finished lanes wanted are dropped
+      ent &= ((hm[0] & livemask) ? 1u : 0u) | ((hm[1] & livemask) ? 2u : 0u) | ((hm[2] & livemask) ? 4u : 0u) |
+             ((hm[3] & livemask) ? 8u : 0u);
+    }
+    if (ent == 0) return 0;
+  }
+  // uniform keys: the lead lane's key, all-ones where the child is not descended into
   uint32_t key[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)vkey[k], (int)lead);
-    key[k] = hm[k] ? kl : 0xffffffffu;
+    key[k] = ((ent >> k) & 1u) ? kl : 0xffffffffu;
   }
   uint32_t kb = key[0];
   int rb = cref[0];
@@ -360,7 +412,6 @@ __device__ __forceinline__ bool packet_node(const RT_CONST char* pool, int ref, 
   }
   // pushed set P (entered, not the nearest) as a 4-bit mask; descending slot order puts child k
   // at sp + popcount(P >> (k + 1)), so the four writes are independent of each other
-  const uint32_t ent = (hm[0] ? 1u : 0u) | (hm[1] ? 2u : 0u) | (hm[2] ? 4u : 0u) | (hm[3] ? 8u : 0u);
   const uint32_t P = ent & ~(1u << ib);
   if (STATS && live && sp + __builtin_popcount(P) > cap) ++cnt.overflow;
 #pragma unroll
@@ -370,32 +421,7 @@ __device__ __forceinline__ bool packet_node(const RT_CONST char* pool, int ref, 
   }
   sp = __builtin_amdgcn_readfirstlane(sp + __builtin_popcount(P));  // uniform by construction: an SGPR
   next = rb;
-  return true;
-}
-
-// Triangle leaf for every live lane (uniform triangle, scalar loads). ANY_HIT: a lane that
-// accepts a hit leaves the packet.
-template <bool ANY_HIT, bool STATS>
-__device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref, const PacketRay& ry, float tmin,
-                                           uint32_t cur, bool& live, bool& found, HitRec& hit, Counters& cnt) {
-  const RT_CONST f4v* tq = (const RT_CONST f4v*)(tpool + (~ref));
-  const f4v ta = tq[0], tb = tq[1], tc = tq[2];
-  if (STATS && live) ++cnt.tri;
-  float t, u, v;
-  const bool ok = moller_trumbore(ry.o, ry.d, v3(ta.x, ta.y, ta.z), v3(tb.x, tb.y, tb.z), v3(tc.x, tc.y, tc.z), t, u, v);
-  if (live && ok && t >= tmin) {
-    const uint32_t prim = __float_as_uint(ta.w);
-    const bool better = t < hit.t || (t == hit.t && (cur < hit.inst || (cur == hit.inst && prim < hit.prim)));
-    if (better) {
-      hit.t = t;
-      hit.u = u;
-      hit.v = v;
-      hit.inst = cur;
-      hit.prim = prim;
-      found = true;
-      if (ANY_HIT) live = false;
-    }
-  }
+  return 1;
 }
 
 template <bool ANY_HIT, bool STATS>
@@ -428,7 +454,8 @@ __device__ bool trace_packet(const SceneView& sc, V3 o, V3 d, float tmin, float 
   while (true) {
     int next;
     if (ref >= 0) {
-      if (packet_node<STATS>(pool, ref, w, tmin, hit.t, live, livemask, lead, stk, sp, cap, next, cnt)) {
+      if (packet_node<ANY_HIT, STATS, false>(pool, tpool, ref, w, tmin, 0u, live, livemask, lead, found, hit, stk,
+                                             sp, cap, next, cnt)) {
         ref = next;
         continue;
       }
@@ -448,19 +475,14 @@ __device__ bool trace_packet(const SceneView& sc, V3 o, V3 d, float tmin, float 
       const int base = sp;
       int bref = (int)ir.pool_root;
       while (true) {
-        if (bref >= 0) {
-          if (packet_node<STATS>(pool, bref, b, tmin, hit.t, live, livemask, lead, stk, sp, cap, next, cnt)) {
-            bref = next;
-            continue;
-          }
-        } else {
-          packet_tri<ANY_HIT, STATS>(tpool, bref, b, tmin, cur, live, found, hit, cnt);
-          if (ANY_HIT) {
-            livemask = wave_ballot(live);
-            if (livemask == 0) return found;
-            lead = lead_lane(livemask);
-          }
+        // only internal nodes reach here: triangle children are tested inside packet_node
+        const int st = packet_node<ANY_HIT, STATS, true>(pool, tpool, bref, b, tmin, cur, live, livemask, lead,
+                                                         found, hit, stk, sp, cap, next, cnt);
+        if (st == 1) {
+          bref = next;
+          continue;
         }
+        if (ANY_HIT && st == 2) return found;
         if (sp == base) break;
         bref = stk.get(--sp);
       }
