@@ -371,6 +371,9 @@ __device__ __forceinline__ int packet_node(const RT_CONST char* pool, const RT_C
   }
   if (STATS && live) cnt.aabb += *(const RT_CONST uint32_t*)(nb + 112);  // Bvh4Node::count
   uint32_t ent = (hm[0] ? 1u : 0u) | (hm[1] ? 2u : 0u) | (hm[2] ? 4u : 0u) | (hm[3] ? 8u : 0u);
+  // pin the child-ref load before the early exit: issued with the plane loads, it shares their
+  // scalar-cache round trip instead of starting a second one after the slab tests
+  asm volatile("" ::"s"(ch.x), "s"(ch.y), "s"(ch.z), "s"(ch.w));
   if (ent == 0) return 0;
   if (LEAVES) {
     const uint32_t leafbits = (cref[0] < 0 ? 1u : 0u) | (cref[1] < 0 ? 2u : 0u) | (cref[2] < 0 ? 4u : 0u) |
