@@ -315,4 +315,19 @@ RT_HD bool moller_trumbore(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float& t, float& u, 
 #endif
 }
 
+// Moller-Trumbore without early exits: every lane runs the same instructions (the wave-packet
+// path, where a divergent early exit costs exec-mask SALU work on the busiest pipe). Accepts
+// exactly what moller_trumbore accepts, with the same u, v, t.
+RT_HD bool moller_trumbore_flat(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float& t, float& u, float& v) {
+  const V3 p = cross(d, e2);
+  const float det = dot(e1, p);
+  const float inv = 1.0f / det;
+  const V3 s = sub(o, v0);
+  u = dot(s, p) * inv;
+  const V3 q = cross(s, e1);
+  v = dot(d, q) * inv;
+  t = dot(e2, q) * inv;
+  return det != 0.0f && u >= 0.0f && u <= 1.0f && v >= 0.0f && u + v <= 1.0f;
+}
+
 }  // namespace rt

@@ -292,20 +292,19 @@ __device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref
   const f4v ta = tq[0], tb = tq[1], tc = tq[2];
   if (STATS && live) ++cnt.tri;
   float t, u, v;
-  const bool ok = moller_trumbore(ry.o, ry.d, v3(ta.x, ta.y, ta.z), v3(tb.x, tb.y, tb.z), v3(tc.x, tc.y, tc.z), t, u, v);
-  if (live && ok && t >= tmin) {
-    const uint32_t prim = __float_as_uint(ta.w);
-    const bool better = t < hit.t || (t == hit.t && (cur < hit.inst || (cur == hit.inst && prim < hit.prim)));
-    if (better) {
-      hit.t = t;
-      hit.u = u;
-      hit.v = v;
-      hit.inst = cur;
-      hit.prim = prim;
-      found = true;
-      if (ANY_HIT) live = false;
-    }
-  }
+  const bool ok =
+      moller_trumbore_flat(ry.o, ry.d, v3(ta.x, ta.y, ta.z), v3(tb.x, tb.y, tb.z), v3(tc.x, tc.y, tc.z), t, u, v);
+  const uint32_t prim = __float_as_uint(ta.w);
+  const bool better = t < hit.t || (t == hit.t && (cur < hit.inst || (cur == hit.inst && prim < hit.prim)));
+  // branch-free update: selects instead of exec-mask regions
+  const bool take = live && ok && t >= tmin && better;
+  hit.t = take ? t : hit.t;
+  hit.u = take ? u : hit.u;
+  hit.v = take ? v : hit.v;
+  hit.inst = take ? cur : hit.inst;
+  hit.prim = take ? prim : hit.prim;
+  found = found || take;
+  if (ANY_HIT) live = live && !take;
 }
 
 // One node of the packet walk: slab tests of the 4 children for every live lane; a child is
