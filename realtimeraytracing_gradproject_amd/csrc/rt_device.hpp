@@ -25,8 +25,8 @@
 #ifndef RT_COND_PUSH
 #define RT_COND_PUSH 1      // push only hit children (vs unconditional LDS writes, predicated sp)
 #endif
-#ifndef RT_PACKET_OCTANT
-#define RT_PACKET_OCTANT 0  // packet: near/far plane loads when the live lanes share an octant
+#ifndef RT_PACKET_RAYS
+#define RT_PACKET_RAYS 1    // rays per lane in a packet (2: 128-ray packets, 8 x 16 pixels per wave)
 #endif
 #ifndef RT_ARGMIN_ORDER
 #define RT_ARGMIN_ORDER 0   // nearest child only (vs the full 4-sort; the sort culls better)

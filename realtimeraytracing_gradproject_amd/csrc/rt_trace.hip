@@ -17,6 +17,7 @@
 // [entry][lane] (bank = lane: conflict free) with an HBM overflow for deep paths.
 #include <hip/hip_runtime.h>
 
+#include "../../include/rt_api.h"
 #include "rt_internal.hpp"
 
 // v_writelane_b32 (the LLVM intrinsic; this clang has no builtin for it): writes the uniform x
@@ -240,23 +241,22 @@ __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, H
 }
 
 // ------------------------------------------------------------------------------------------
-// Wave-packet traversal: the 64 lanes of a wave (an 8x8 pixel tile) walk ONE path through the
-// trees together. The current node / triangle / instance is wave-uniform, so it is fetched with
-// scalar loads into SGPRs (one fetch per wave instead of 64 lane loads) and every lane tests its
-// own ray against it; a child is entered when any live lane's slab test accepts it (ballot). The
-// traversal stack is wave-uniform and lives in the 64 lanes of one VGPR (v_writelane /
-// v_readlane): no LDS and no per-lane stack traffic. Children are ordered by the entry distance
-// of the lowest live lane (a uniform key, sorted in SALU). When every live lane's ray has the
-// same direction octant (the common case for camera and shadow tiles) the near and far planes
-// of each axis are picked by the load address, as in the per-lane path.
+// Wave-packet traversal: the rays of a wave walk ONE path through the trees together. A packet
+// is 64 x R rays: each lane carries R rays (R = 1: an 8x8 pixel tile per wave; R = 2: 8x16).
+// The current node / triangle / instance is wave-uniform, so it is fetched with scalar loads
+// into SGPRs (one fetch per wave instead of one per lane) and every lane tests its own rays
+// against it; a child is entered when any live ray accepts it (ballots). The traversal stack is
+// wave-uniform and lives in the 64 lanes of one VGPR (v_writelane / v_readlane): no LDS and no
+// per-lane stack traffic. Children are ordered by the entry distance of the lead ray (the first
+// live ray in slot order r * 64 + lane). All per-node decisions are scalar (SALU) work shared by
+// the packet's 64 x R rays: R > 1 spends more VALU per node to amortise the SALU further.
 // Results are those of the per-ray traversal: the closest hit is the lexicographic minimum of
-// (t, instance, primitive) over every triangle a lane's ray reaches, and every triangle whose
-// root path the ray's slab tests accept is visited, whatever the order.
+// (t, instance, primitive) over every triangle a ray reaches, and every triangle whose root
+// path the ray's slab tests accept is visited, whatever the order.
 // ------------------------------------------------------------------------------------------
 #define RT_CONST __attribute__((address_space(4)))
 
 constexpr int kPacketStack = 64;  // wave-uniform stack entries: one VGPR, entry i in lane i
-
 
 struct WaveStack {
   int v = 0;
@@ -265,111 +265,116 @@ struct WaveStack {
 };
 
 __device__ __forceinline__ uint64_t wave_ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
-__device__ __forceinline__ uint32_t lead_lane(uint64_t m) { return (uint32_t)__builtin_ctzll(m); }
-
-// Octant shared by every live lane (bit k set: component k of the direction is negative), or 8
-// when the live lanes disagree.
-__device__ __forceinline__ uint32_t wave_octant(V3 invd, bool live, uint32_t lead) {
-  const uint32_t o = (invd.x < 0.0f ? 1u : 0u) | (invd.y < 0.0f ? 2u : 0u) | (invd.z < 0.0f ? 4u : 0u);
-  const uint32_t ol = (uint32_t)__builtin_amdgcn_readlane((int)o, (int)lead);
-  return wave_ballot(live && o != ol) ? 8u : ol;
-}
 
 __device__ __forceinline__ f4v cld4(const RT_CONST char* p) { return *(const RT_CONST f4v*)p; }
 
-// Per-wave ray state of one traversal level (world rays in the TLAS, object rays in a BLAS).
-struct PacketRay {
-  V3 o, d, invd, noinv;
-  uint32_t oct;  // octant shared by the live lanes, or 8
+// Live rays of the packet: one ballot mask per ray slot r, and the lead ray (lowest r, then
+// lowest lane).
+template <int R>
+struct PacketLive {
+  bool live[R];
+  uint64_t mask[R];
+  uint32_t lead_r, lead_l;
+  __device__ __forceinline__ bool update() {  // false when no ray is live
+    bool any = false;
+    lead_r = 0;
+    lead_l = 0;
+#pragma unroll
+    for (int r = R - 1; r >= 0; --r) {
+      mask[r] = wave_ballot(live[r]);
+      if (mask[r]) {
+        any = true;
+        lead_r = (uint32_t)r;
+        lead_l = (uint32_t)__builtin_ctzll(mask[r]);
+      }
+    }
+    return any;
+  }
 };
 
-// Triangle leaf for every live lane (uniform triangle, scalar loads). ANY_HIT: a lane that
-// accepts a hit leaves the packet.
-template <bool ANY_HIT, bool STATS>
-__device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref, const PacketRay& ry, float tmin,
-                                           uint32_t cur, bool& live, bool& found, HitRec& hit, Counters& cnt) {
+// Per-wave ray state of one traversal level (world rays in the TLAS, object rays in a BLAS).
+template <int R>
+struct PacketRay {
+  V3 o[R], d[R], invd[R], noinv[R];
+};
+
+// Triangle leaf for every live ray (uniform triangle, scalar loads). ANY_HIT: a ray that accepts
+// a hit leaves the packet. Branch-free: selects instead of exec-mask regions.
+template <bool ANY_HIT, bool STATS, int R>
+__device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref, const PacketRay<R>& ry,
+                                           float tmin, uint32_t cur, PacketLive<R>& pl, bool* found, HitRec* hit,
+                                           Counters& cnt) {
   const RT_CONST f4v* tq = (const RT_CONST f4v*)(tpool + (~ref));
   const f4v ta = tq[0], tb = tq[1], tc = tq[2];
-  if (STATS && live) ++cnt.tri;
-  float t, u, v;
-  const bool ok =
-      moller_trumbore_flat(ry.o, ry.d, v3(ta.x, ta.y, ta.z), v3(tb.x, tb.y, tb.z), v3(tc.x, tc.y, tc.z), t, u, v);
   const uint32_t prim = __float_as_uint(ta.w);
-  const bool better = t < hit.t || (t == hit.t && (cur < hit.inst || (cur == hit.inst && prim < hit.prim)));
-  // branch-free update: selects instead of exec-mask regions
-  const bool take = live && ok && t >= tmin && better;
-  hit.t = take ? t : hit.t;
-  hit.u = take ? u : hit.u;
-  hit.v = take ? v : hit.v;
-  hit.inst = take ? cur : hit.inst;
-  hit.prim = take ? prim : hit.prim;
-  found = found || take;
-  if (ANY_HIT) live = live && !take;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (STATS && pl.live[r]) ++cnt.tri;
+    float t, u, v;
+    const bool ok = moller_trumbore_flat(ry.o[r], ry.d[r], v3(ta.x, ta.y, ta.z), v3(tb.x, tb.y, tb.z),
+                                         v3(tc.x, tc.y, tc.z), t, u, v);
+    HitRec& h = hit[r];
+    const bool better = t < h.t || (t == h.t && (cur < h.inst || (cur == h.inst && prim < h.prim)));
+    const bool take = pl.live[r] && ok && t >= tmin && better;
+    h.t = take ? t : h.t;
+    h.u = take ? u : h.u;
+    h.v = take ? v : h.v;
+    h.inst = take ? cur : h.inst;
+    h.prim = take ? prim : h.prim;
+    found[r] = found[r] || take;
+    if (ANY_HIT) pl.live[r] = pl.live[r] && !take;
+  }
 }
 
-// One node of the packet walk: slab tests of the 4 children for every live lane; a child is
-// entered when any live lane accepts it. LEAVES (BLAS level): entered triangle children are
+// One node of the packet walk: slab tests of the 4 children for every live ray; a child is
+// entered when any live ray accepts it. LEAVES (BLAS level): entered triangle children are
 // tested right here, in slot order, instead of going through the stack. The entered internal
-// children (TLAS: also instance leaves) go nearest first by the lead lane's entry distance
+// children (TLAS: also instance leaves) go nearest first by the lead ray's entry distance
 // (lowest slot on ties); the others are pushed in descending slot order, so the lowest slot pops
 // next. Pushes that do not happen write the spare lane kPacketStack - 1; the bookkeeping is
 // plain integer SALU work. Returns 1 with *next set, 0 when nothing is left to descend into,
-// 2 when an any-hit packet has no live lane left.
-template <bool ANY_HIT, bool STATS, bool LEAVES>
+// 2 when an any-hit packet has no live ray left.
+template <bool ANY_HIT, bool STATS, bool LEAVES, int R>
 __device__ __forceinline__ int packet_node(const RT_CONST char* pool, const RT_CONST TriRec* tpool, int ref,
-                                           const PacketRay& ry, float tmin, uint32_t cur, bool& live,
-                                           uint64_t& livemask, uint32_t& lead, bool& found, HitRec& hit,
-                                           WaveStack& stk, int& sp, int cap, int& next, Counters& cnt) {
-  const float tbest = hit.t;
+                                           const PacketRay<R>& ry, float tmin, uint32_t cur, PacketLive<R>& pl,
+                                           bool* found, HitRec* hit, WaveStack& stk, int& sp, int cap, int& next,
+                                           Counters& cnt) {
   const RT_CONST char* nb = pool + ((size_t)(uint32_t)ref << 7);
   const i4v ch = *(const RT_CONST i4v*)(nb + 96);
   const int cref[4] = {ch.x, ch.y, ch.z, ch.w};
-  uint64_t hm[4];
-  uint32_t vkey[4];  // per lane: |entry distance| if this lane's test accepted the child, else +inf
-#if RT_PACKET_OCTANT
-  if (ry.oct < 8u) {
-    // shared octant: near/far planes by address (bitwise equal to the min/max form)
-    const uint32_t ox = (ry.oct & 1u) ? 16u : 0u, oy = (ry.oct & 2u) ? 48u : 32u, oz = (ry.oct & 4u) ? 80u : 64u;
-    const f4v a0 = cld4(nb + ox), a1 = cld4(nb + (ox ^ 16u));
-    const f4v a2 = cld4(nb + oy), a3 = cld4(nb + (oy ^ 16u));
-    const f4v a4 = cld4(nb + oz), a5 = cld4(nb + (oz ^ 16u));
-    const float nx[4] = {a0.x, a0.y, a0.z, a0.w}, fx[4] = {a1.x, a1.y, a1.z, a1.w};
-    const float ny[4] = {a2.x, a2.y, a2.z, a2.w}, fy[4] = {a3.x, a3.y, a3.z, a3.w};
-    const float nz[4] = {a4.x, a4.y, a4.z, a4.w}, fz[4] = {a5.x, a5.y, a5.z, a5.w};
+  // unused slots hold lo = hi = +inf boxes that every ray rejects: no validity mask
+  const f4v a0 = cld4(nb), a1 = cld4(nb + 16), a2 = cld4(nb + 32);
+  const f4v a3 = cld4(nb + 48), a4 = cld4(nb + 64), a5 = cld4(nb + 80);
+  const float lox[4] = {a0.x, a0.y, a0.z, a0.w}, hix[4] = {a1.x, a1.y, a1.z, a1.w};
+  const float loy[4] = {a2.x, a2.y, a2.z, a2.w}, hiy[4] = {a3.x, a3.y, a3.z, a3.w};
+  const float loz[4] = {a4.x, a4.y, a4.z, a4.w}, hiz[4] = {a5.x, a5.y, a5.z, a5.w};
+  uint64_t hm[R][4];
+  uint32_t vkey[R][4];  // per ray: |entry distance| if its test accepted the child, else +inf
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const V3 iv = ry.invd[r], no = ry.noinv[r];
+    const float tbest = hit[r].t;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const float tnx = __builtin_fmaf(nx[k], ry.invd.x, ry.noinv.x), tfx = __builtin_fmaf(fx[k], ry.invd.x, ry.noinv.x);
-      const float tny = __builtin_fmaf(ny[k], ry.invd.y, ry.noinv.y), tfy = __builtin_fmaf(fy[k], ry.invd.y, ry.noinv.y);
-      const float tnz = __builtin_fmaf(nz[k], ry.invd.z, ry.noinv.z), tfz = __builtin_fmaf(fz[k], ry.invd.z, ry.noinv.z);
-      const float n = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
-      const float f = fminf(fminf(tfx, tfy), fminf(tfz, tbest));
-      const bool h = n <= f * 1.0000004f;  // dead lanes are masked out of the ballot; only the lead's key is read
-      hm[k] = wave_ballot(h) & livemask;
-      vkey[k] = h ? (__float_as_uint(n) & 0x7fffffffu) : 0x7f800000u;
-    }
-  } else
-#endif
-  {
-    // unused slots hold lo = hi = +inf boxes that every lane rejects: no validity mask
-    const f4v a0 = cld4(nb), a1 = cld4(nb + 16), a2 = cld4(nb + 32);
-    const f4v a3 = cld4(nb + 48), a4 = cld4(nb + 64), a5 = cld4(nb + 80);
-    const float lox[4] = {a0.x, a0.y, a0.z, a0.w}, hix[4] = {a1.x, a1.y, a1.z, a1.w};
-    const float loy[4] = {a2.x, a2.y, a2.z, a2.w}, hiy[4] = {a3.x, a3.y, a3.z, a3.w};
-    const float loz[4] = {a4.x, a4.y, a4.z, a4.w}, hiz[4] = {a5.x, a5.y, a5.z, a5.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float tlx = __builtin_fmaf(lox[k], ry.invd.x, ry.noinv.x), thx = __builtin_fmaf(hix[k], ry.invd.x, ry.noinv.x);
-      const float tly = __builtin_fmaf(loy[k], ry.invd.y, ry.noinv.y), thy = __builtin_fmaf(hiy[k], ry.invd.y, ry.noinv.y);
-      const float tlz = __builtin_fmaf(loz[k], ry.invd.z, ry.noinv.z), thz = __builtin_fmaf(hiz[k], ry.invd.z, ry.noinv.z);
+      const float tlx = __builtin_fmaf(lox[k], iv.x, no.x), thx = __builtin_fmaf(hix[k], iv.x, no.x);
+      const float tly = __builtin_fmaf(loy[k], iv.y, no.y), thy = __builtin_fmaf(hiy[k], iv.y, no.y);
+      const float tlz = __builtin_fmaf(loz[k], iv.z, no.z), thz = __builtin_fmaf(hiz[k], iv.z, no.z);
       const float n = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), tmin));
       const float f = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tbest));
-      const bool h = n <= f * 1.0000004f;  // dead lanes are masked out of the ballot; only the lead's key is read
-      hm[k] = wave_ballot(h) & livemask;
-      vkey[k] = h ? (__float_as_uint(n) & 0x7fffffffu) : 0x7f800000u;
+      const bool h = n <= f * 1.0000004f;  // dead rays are masked out of the ballot; only the lead's key is read
+      hm[r][k] = wave_ballot(h) & pl.mask[r];
+      vkey[r][k] = h ? (__float_as_uint(n) & 0x7fffffffu) : 0x7f800000u;
     }
+    if (STATS && pl.live[r]) cnt.aabb += *(const RT_CONST uint32_t*)(nb + 112);  // Bvh4Node::count
   }
-  if (STATS && live) cnt.aabb += *(const RT_CONST uint32_t*)(nb + 112);  // Bvh4Node::count
-  uint32_t ent = (hm[0] ? 1u : 0u) | (hm[1] ? 2u : 0u) | (hm[2] ? 4u : 0u) | (hm[3] ? 8u : 0u);
+  uint32_t ent = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint64_t any = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) any |= hm[r][k];
+    ent |= any ? (1u << k) : 0u;
+  }
   // pin the child-ref load before the early exit: issued with the plane loads, it shares their
   // scalar-cache round trip instead of starting a second one after the slab tests
   asm volatile("" ::"s"(ch.x), "s"(ch.y), "s"(ch.z), "s"(ch.w));
@@ -383,23 +388,31 @@ __device__ __forceinline__ int packet_node(const RT_CONST char* pool, const RT_C
       const uint32_t k = (uint32_t)__builtin_ctz(tl);
       tl &= tl - 1u;
       const int tr = k == 0 ? cref[0] : k == 1 ? cref[1] : k == 2 ? cref[2] : cref[3];
-      packet_tri<ANY_HIT, STATS>(tpool, tr, ry, tmin, cur, live, found, hit, cnt);
+      packet_tri<ANY_HIT, STATS, R>(tpool, tr, ry, tmin, cur, pl, found, hit, cnt);
     }
     if (ANY_HIT) {
-      livemask = wave_ballot(live);
-      if (livemask == 0) return 2;
-      lead = lead_lane(livemask);
-      // children only finished lanes wanted are dropped
-      ent &= ((hm[0] & livemask) ? 1u : 0u) | ((hm[1] & livemask) ? 2u : 0u) | ((hm[2] & livemask) ? 4u : 0u) |
-             ((hm[3] & livemask) ? 8u : 0u);
+      if (!pl.update()) return 2;
+      // children only finished rays wanted are dropped
+      uint32_t still = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint64_t any = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) any |= hm[r][k] & pl.mask[r];
+        still |= any ? (1u << k) : 0u;
+      }
+      ent &= still;
     }
     if (ent == 0) return 0;
   }
-  // uniform keys: the lead lane's key, all-ones where the child is not descended into
+  // uniform keys: the lead ray's key, all-ones where the child is not descended into
   uint32_t key[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)vkey[k], (int)lead);
+    uint32_t vk = vkey[0][k];
+#pragma unroll
+    for (int r = 1; r < R; ++r) vk = pl.lead_r == (uint32_t)r ? vkey[r][k] : vk;
+    const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)vk, (int)pl.lead_l);
     key[k] = ((ent >> k) & 1u) ? kl : 0xffffffffu;
   }
   uint32_t kb = key[0];
@@ -415,7 +428,9 @@ __device__ __forceinline__ int packet_node(const RT_CONST char* pool, const RT_C
   // pushed set P (entered, not the nearest) as a 4-bit mask; descending slot order puts child k
   // at sp + popcount(P >> (k + 1)), so the four writes are independent of each other
   const uint32_t P = ent & ~(1u << ib);
-  if (STATS && live && sp + __builtin_popcount(P) > cap) ++cnt.overflow;
+  if (STATS && sp + __builtin_popcount(P) > cap)  // never: cap is the exact worst case
+#pragma unroll
+    for (int r = 0; r < R; ++r) cnt.overflow += pl.live[r] ? 1u : 0u;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int pos = sp + __builtin_popcount(P >> (k + 1));
@@ -426,70 +441,74 @@ __device__ __forceinline__ int packet_node(const RT_CONST char* pool, const RT_C
   return 1;
 }
 
-template <bool ANY_HIT, bool STATS>
-__device__ bool trace_packet(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, bool alive, HitRec& hit,
-                             Counters& cnt) {
+// Traces the R rays of every lane (o, d, alive per slot) as one packet; found[r] / hit[r] per ray.
+template <bool ANY_HIT, bool STATS, int R>
+__device__ void trace_packet(const SceneView& sc, const V3* o, const V3* d, float tmin, float tmax,
+                             const bool* alive, bool* found, HitRec* hit, Counters& cnt) {
   const RT_CONST char* pool = (const RT_CONST char*)sc.pool_nodes;
   const RT_CONST TriRec* tpool = (const RT_CONST TriRec*)sc.pool_tris;
   const RT_CONST InstanceRec* ipool = (const RT_CONST InstanceRec*)sc.inst;
-  hit.t = tmax;
-  hit.inst = 0xffffffffu;
-  hit.prim = 0xffffffffu;
-  hit.u = hit.v = 0.0f;
-  bool found = false;
-  bool live = alive;
-  uint64_t livemask = wave_ballot(live);
-  if (livemask == 0) return false;
-  uint32_t lead = lead_lane(livemask);
-  PacketRay w;
-  w.o = o;
-  w.d = d;
-  w.invd = v3(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
-  w.noinv = neg(mul(o, w.invd));
-  w.oct = RT_PACKET_OCTANT ? wave_octant(w.invd, live, lead) : 8u;
+  PacketLive<R> pl;
+  PacketRay<R> w;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    hit[r].t = tmax;
+    hit[r].inst = 0xffffffffu;
+    hit[r].prim = 0xffffffffu;
+    hit[r].u = hit[r].v = 0.0f;
+    found[r] = false;
+    pl.live[r] = alive[r];
+    w.o[r] = o[r];
+    w.d[r] = d[r];
+    w.invd[r] = v3(safe_inv(d[r].x), safe_inv(d[r].y), safe_inv(d[r].z));
+    w.noinv[r] = neg(mul(o[r], w.invd[r]));
+  }
+  if (!pl.update()) return;
   WaveStack stk;
   const int cap = sc.stack_cap;  // < kPacketStack (checked at launch): lane 63 stays spare
   int sp = 0;
   int ref = 0;
   // TLAS walk; each instance leaf runs a nested BLAS walk on the stack above the TLAS entries
-  // (the world ray is invariant here, the object ray inside: no ray state is carried around).
+  // (the world rays are invariant here, the object rays inside: no ray state moves around).
   while (true) {
     int next;
     if (ref >= 0) {
-      if (packet_node<ANY_HIT, STATS, false>(pool, tpool, ref, w, tmin, 0u, live, livemask, lead, found, hit, stk,
-                                             sp, cap, next, cnt)) {
+      if (packet_node<ANY_HIT, STATS, false, R>(pool, tpool, ref, w, tmin, 0u, pl, found, hit, stk, sp, cap, next,
+                                                cnt)) {
         ref = next;
         continue;
       }
     } else {
       const uint32_t cur = (uint32_t)(~ref);
       const RT_CONST InstanceRec& ir = ipool[cur];
-      if (STATS && live) ++cnt.inst;
       const RT_CONST f4v* mq = (const RT_CONST f4v*)ir.w2o;
       const f4v m0 = mq[0], m1 = mq[1], m2 = mq[2];
       const float m[12] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w, m2.x, m2.y, m2.z, m2.w};
-      PacketRay b;
-      b.o = xform_point(m, o);
-      b.d = xform_dir(m, d);
-      b.invd = v3(safe_inv(b.d.x), safe_inv(b.d.y), safe_inv(b.d.z));
-      b.noinv = neg(mul(b.o, b.invd));
-      b.oct = RT_PACKET_OCTANT ? wave_octant(b.invd, live, lead) : 8u;
+      PacketRay<R> b;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (STATS && pl.live[r]) ++cnt.inst;
+        b.o[r] = xform_point(m, o[r]);
+        b.d[r] = xform_dir(m, d[r]);
+        b.invd[r] = v3(safe_inv(b.d[r].x), safe_inv(b.d[r].y), safe_inv(b.d[r].z));
+        b.noinv[r] = neg(mul(b.o[r], b.invd[r]));
+      }
       const int base = sp;
       int bref = (int)ir.pool_root;
       while (true) {
         // only internal nodes reach here: triangle children are tested inside packet_node
-        const int st = packet_node<ANY_HIT, STATS, true>(pool, tpool, bref, b, tmin, cur, live, livemask, lead,
-                                                         found, hit, stk, sp, cap, next, cnt);
+        const int st = packet_node<ANY_HIT, STATS, true, R>(pool, tpool, bref, b, tmin, cur, pl, found, hit, stk, sp,
+                                                            cap, next, cnt);
         if (st == 1) {
           bref = next;
           continue;
         }
-        if (ANY_HIT && st == 2) return found;
+        if (ANY_HIT && st == 2) return;
         if (sp == base) break;
         bref = stk.get(--sp);
       }
     }
-    if (sp == 0) return found;
+    if (sp == 0) return;
     ref = stk.get(--sp);
   }
 }
@@ -686,82 +705,115 @@ __device__ V3 shade_sample(const SceneView& sc, const FrameParams& fp, uint32_t 
   return v3(c, c, c);
 }
 
-// shade_sample for the wave-packet traversal: identical arithmetic, with every trace hoisted to
-// wave-uniform control flow (lanes without a ray of that kind join the packet dead).
-template <int MODE, bool STATS>
-__device__ V3 shade_sample_packet(const SceneView& sc, const FrameParams& fp, uint32_t px, uint32_t py,
-                                  float ox, float oy, bool inimg, Counters& cnt) {
-  const float dx = (((float)px + ox) / (float)fp.width) * 2.0f - 1.0f;
-  const float dy = (((float)py + oy) / (float)fp.height) * 2.0f - 1.0f;
-  float org4[4], dc[4], dw[4];
-  const float zero_one[4] = {0.0f, 0.0f, 0.0f, 1.0f};
-  hlsl_mul4(fp.cb + 32, zero_one, org4);
-  const float ndc[4] = {dx, -dy, 1.0f, 1.0f};
-  hlsl_mul4(fp.cb + 48, ndc, dc);
-  const float dcam[4] = {dc[0], dc[1], dc[2], 0.0f};
-  hlsl_mul4(fp.cb + 32, dcam, dw);
-  const V3 O = v3(org4[0], org4[1], org4[2]);
-  const V3 D = normalize(v3(dw[0], dw[1], dw[2]));  // CastDefaultRay
-  HitRec hit;
-  if (STATS && inimg) ++cnt.primary;
-  const bool found = trace_packet<false, STATS>(sc, O, D, 0.0f, 100000.0f, inimg, hit, cnt);
-  const float ramp = (float)py / (float)fp.height;  // Miss.hlsl:8
-  const V3 miss = v3(0.0f, 0.2f, 0.7f - 0.3f * ramp);
-  const V3 P = add(O, muls(D, hit.t));  // GetWorldHitPoint, Common.hlsl:24-27
-  HitInstance ir;
-  bool plane = false;
-  if (found) {
-    ir = load_hit_instance(sc, hit.inst);
-    plane = ir.hit_group == 2u;
+// shade_sample for the wave-packet traversal: identical arithmetic per ray, with every trace
+// hoisted to wave-uniform control flow (rays without a trace of that kind join the packet dead).
+// Each lane shades R camera samples (R pixels) at once.
+template <int MODE, bool STATS, int R>
+__device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, const uint32_t* px,
+                                    const uint32_t* py, float ox, float oy, const bool* inimg, V3* color,
+                                    Counters& cnt) {
+  V3 O[R], D[R], P[R], sd[R];
+  HitRec hit[R], sh[R];
+  bool found[R], occl[R], need[R];
+  HitInstance ir[R];
+  bool plane[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const float dx = (((float)px[r] + ox) / (float)fp.width) * 2.0f - 1.0f;
+    const float dy = (((float)py[r] + oy) / (float)fp.height) * 2.0f - 1.0f;
+    float org4[4], dc[4], dw[4];
+    const float zero_one[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+    hlsl_mul4(fp.cb + 32, zero_one, org4);
+    const float ndc[4] = {dx, -dy, 1.0f, 1.0f};
+    hlsl_mul4(fp.cb + 48, ndc, dc);
+    const float dcam[4] = {dc[0], dc[1], dc[2], 0.0f};
+    hlsl_mul4(fp.cb + 32, dcam, dw);
+    O[r] = v3(org4[0], org4[1], org4[2]);
+    D[r] = normalize(v3(dw[0], dw[1], dw[2]));  // CastDefaultRay
+    if (STATS && inimg[r]) ++cnt.primary;
+  }
+  trace_packet<false, STATS, R>(sc, O, D, 0.0f, 100000.0f, inimg, found, hit, cnt);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const float ramp = (float)py[r] / (float)fp.height;  // Miss.hlsl:8
+    color[r] = v3(0.0f, 0.2f, 0.7f - 0.3f * ramp);
+    P[r] = add(O[r], muls(D[r], hit[r].t));  // GetWorldHitPoint, Common.hlsl:24-27
+    plane[r] = false;
+    if (found[r]) {
+      ir[r] = load_hit_instance(sc, hit[r].inst);
+      plane[r] = ir[r].hit_group == 2u;
+    }
   }
   if (MODE == 0) {
-    V3 color = miss, ldir = v3(0.0f, 0.0f, 0.0f), nf = v3(0.0f, 0.0f, 0.0f);
-    bool need = false;
-    if (found) {
-      if (plane) {
-        const LightRec& L0 = fp.lights[0];
-        ldir = normalize(sub(v3(L0.position[0], L0.position[1], L0.position[2]), P));
-        nf = face_world_normal(ir, hit.prim);
-        need = true;
-      } else {
-        const V3 n = interpolated_world_normal(ir, hit.prim, hit.u, hit.v);
-        const V3 albedo = v3(fp.material.albedo[0], fp.material.albedo[1], fp.material.albedo[2]);
-        // reflectivity is pinned to 0: lerp(final, refl, 0) == final; no reflection ray.
-        color = add(direct_lighting(fp, P, n, albedo), pbr_shading(fp, n, O, P));
+    V3 ldir[R], nf[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      ldir[r] = nf[r] = v3(0.0f, 0.0f, 0.0f);
+      need[r] = false;
+      if (found[r]) {
+        if (plane[r]) {
+          const LightRec& L0 = fp.lights[0];
+          ldir[r] = normalize(sub(v3(L0.position[0], L0.position[1], L0.position[2]), P[r]));
+          nf[r] = face_world_normal(ir[r], hit[r].prim);
+          need[r] = true;
+        } else {
+          const V3 n = interpolated_world_normal(ir[r], hit[r].prim, hit[r].u, hit[r].v);
+          const V3 albedo = v3(fp.material.albedo[0], fp.material.albedo[1], fp.material.albedo[2]);
+          // reflectivity is pinned to 0: lerp(final, refl, 0) == final; no reflection ray.
+          color[r] = add(direct_lighting(fp, P[r], n, albedo), pbr_shading(fp, n, O[r], P[r]));
+        }
+      }
+      if (STATS && need[r]) ++cnt.shadow;
+      sd[r] = normalize(ldir[r]);
+    }
+    trace_packet<true, STATS, R>(sc, P, sd, 0.01f, 100000.0f, need, occl, sh, cnt);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (need[r]) {
+        bool shadowed = dot(nf[r], ldir[r]) < 0.0f;
+        if (!shadowed) shadowed = occl[r];
+        const float factor = shadowed ? 0.3f : 1.0f;
+        const float li = maxf(0.0f, dot(nf[r], ldir[r]));
+        const float c = (1.0f * li) * factor;
+        color[r] = v3(c, c, c);
       }
     }
-    HitRec sh;
-    if (STATS && need) ++cnt.shadow;
-    const bool occl = trace_packet<true, STATS>(sc, P, normalize(ldir), 0.01f, 100000.0f, need, sh, cnt);
-    if (need) {
-      bool shadowed = dot(nf, ldir) < 0.0f;
-      if (!shadowed) shadowed = occl;
-      const float factor = shadowed ? 0.3f : 1.0f;
-      const float li = maxf(0.0f, dot(nf, ldir));
-      const float c = (1.0f * li) * factor;
-      color = v3(c, c, c);
-    }
-    return color;
+    return;
   }
   // RT_SHADE_LAMBERT_SHADOW (MODE 1) and RT_SHADE_PRIMARY (MODE 2)
-  V3 n = v3(0.0f, 0.0f, 0.0f);
-  if (found) n = plane ? face_world_normal(ir, hit.prim) : neg(interpolated_world_normal(ir, hit.prim, hit.u, hit.v));
-  float c = 0.0f;
+  V3 n[R];
+  float c[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    n[r] = v3(0.0f, 0.0f, 0.0f);
+    c[r] = 0.0f;
+    if (found[r])
+      n[r] = plane[r] ? face_world_normal(ir[r], hit[r].prim)
+                      : neg(interpolated_world_normal(ir[r], hit[r].prim, hit[r].u, hit[r].v));
+  }
   for (uint32_t l = 0; l < fp.nlights; ++l) {
     const LightRec& Lr = fp.lights[l];
-    const V3 L = normalize(sub(v3(Lr.position[0], Lr.position[1], Lr.position[2]), P));
-    const float nl = dot(n, L);
-    const bool lit = found && nl > 0.0f;
-    float factor = 1.0f;
-    if (MODE == 1) {
-      HitRec sh;
-      if (STATS && lit) ++cnt.shadow;
-      if (trace_packet<true, STATS>(sc, P, normalize(L), 0.01f, 100000.0f, lit, sh, cnt)) factor = 0.3f;
+    float nl[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const V3 L = normalize(sub(v3(Lr.position[0], Lr.position[1], Lr.position[2]), P[r]));
+      nl[r] = dot(n[r], L);
+      need[r] = found[r] && nl[r] > 0.0f;
+      sd[r] = normalize(L);
+      occl[r] = false;
+      if (MODE == 1 && STATS && need[r]) ++cnt.shadow;
     }
-    if (lit) c = c + nl * factor;
+    if (MODE == 1) trace_packet<true, STATS, R>(sc, P, sd, 0.01f, 100000.0f, need, occl, sh, cnt);
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (need[r]) c[r] = c[r] + nl[r] * (occl[r] ? 0.3f : 1.0f);
   }
-  c = c / (float)fp.nlights;
-  return found ? v3(c, c, c) : miss;
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    if (found[r]) {
+      const float v = c[r] / (float)fp.nlights;
+      color[r] = v3(v, v, v);
+    }
 }
 
 __device__ __forceinline__ void flush_stats(const Counters& c, unsigned long long* stats) {
@@ -813,37 +865,52 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void k_trace_frame(SceneView 
   if (STATS) flush_stats(cnt, stats);
 }
 
-// Wave-packet frame kernel: same pixel mapping as k_trace_frame; every lane runs the sample loop
-// (lanes outside the image or the row list join the packets dead) and stores only in-image pixels.
-template <int MODE, bool STATS>
+// Wave-packet frame kernel. A wave covers an 8 x 8R tile (ray r of lane l: column l % 8, row
+// entry 8r + l / 8 of the tile), a 256-thread workgroup 16 x 16R pixels. Every lane runs the
+// sample loop (rays outside the image or the row list join the packets dead) and stores only
+// in-image pixels.
+template <int MODE, bool STATS, int R>
 __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void k_trace_frame_packet(SceneView sc, FrameParams fp,
                                                                const uint32_t* __restrict__ rows,
                                                                uint32_t* __restrict__ rgba8,
                                                                float4* __restrict__ rgba32f,
                                                                unsigned long long* __restrict__ stats) {
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-  const uint32_t px = blockIdx.x * 16u + (w & 1u) * 8u + (lane & 7u);
-  const uint32_t orow = blockIdx.y * 16u + (w >> 1) * 8u + (lane >> 3);
-  const bool inimg = px < fp.width && orow < fp.nrows;
+  const uint32_t x = blockIdx.x * 16u + (w & 1u) * 8u + (lane & 7u);
+  uint32_t px[R], py[R], orow[R];
+  bool inimg[R];
+  V3 acc[R], col[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    px[r] = x;
+    orow[r] = blockIdx.y * (16u * R) + (w >> 1) * (8u * R) + 8u * r + (lane >> 3);
+    inimg[r] = x < fp.width && orow[r] < fp.nrows;
+    py[r] = 0;
+    if (inimg[r]) py[r] = rows ? rows[orow[r]] : orow[r];
+    acc[r] = v3(0.0f, 0.0f, 0.0f);
+  }
   Counters cnt;
-  uint32_t py = 0;
-  if (inimg) py = rows ? rows[orow] : orow;
   const uint32_t k = fp.spp_side;
-  V3 acc = v3(0.0f, 0.0f, 0.0f);
   for (uint32_t sy = 0; sy < k; ++sy)
     for (uint32_t sx = 0; sx < k; ++sx) {
       const float ox = ((float)sx + 0.5f) / (float)k;
       const float oy = ((float)sy + 0.5f) / (float)k;
-      acc = add(acc, shade_sample_packet<MODE, STATS>(sc, fp, px, py, ox, oy, inimg, cnt));
+      shade_sample_packet<MODE, STATS, R>(sc, fp, px, py, ox, oy, inimg, col, cnt);
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r] = add(acc[r], col[r]);
     }
-  if (k > 1) {
-    const float ns = (float)(k * k);
-    acc = v3(acc.x / ns, acc.y / ns, acc.z / ns);
-  }
-  if (inimg) {
-    const size_t o = (size_t)orow * fp.width + px;
-    rgba8[o] = unorm8(acc.x) | (unorm8(acc.y) << 8) | (unorm8(acc.z) << 16) | (255u << 24);
-    if (rgba32f) rgba32f[o] = make_float4(acc.x, acc.y, acc.z, 1.0f);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    V3 a = acc[r];
+    if (k > 1) {
+      const float ns = (float)(k * k);
+      a = v3(a.x / ns, a.y / ns, a.z / ns);
+    }
+    if (inimg[r]) {
+      const size_t o = (size_t)orow[r] * fp.width + px[r];
+      rgba8[o] = unorm8(a.x) | (unorm8(a.y) << 8) | (unorm8(a.z) << 16) | (255u << 24);
+      if (rgba32f) rgba32f[o] = make_float4(a.x, a.y, a.z, 1.0f);
+    }
   }
   if (STATS) flush_stats(cnt, stats);
 }
@@ -886,8 +953,10 @@ template <int MODE, bool STATS>
 hipError_t launch_mode(const SceneView& sc, const FrameParams& fp, const uint32_t* rows, void* rgba8,
                        float* rgba32f, unsigned long long* stats, int schedule, hipStream_t s) {
   dim3 grid((fp.width + 15) / 16, (fp.nrows + 15) / 16);
-  if (schedule == 0 && sc.stack_cap < kPacketStack) {
-    hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS>), grid, dim3(kBlock), 0, s, sc, fp, rows,
+  if (schedule == RT_SCHED_PACKET && sc.stack_cap < kPacketStack) {
+    constexpr int R = RT_PACKET_RAYS;
+    dim3 gp((fp.width + 15) / 16, (fp.nrows + 16 * R - 1) / (16 * R));
+    hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R>), gp, dim3(kBlock), 0, s, sc, fp, rows,
                        (uint32_t*)rgba8, (float4*)rgba32f, stats);
   } else {
     size_t lds = (size_t)sc.lds_cap * kBlock * sizeof(int);
