@@ -108,7 +108,8 @@ enum {
   RT_STAT_STACK_OVERFLOWS = 5,
   RT_STAT_PIXELS = 6,
   RT_STAT_DISPATCHES = 7,
-  RT_STAT_COUNT = 8
+  RT_STAT_REFLECTION_RAYS = 8, /* RT_SHADE_REF with reflectivity != 0 (Hit.hlsl:176-203) */
+  RT_STAT_COUNT = 9
 };
 
 /* ------------------------------------------------------------------------------------------ */
@@ -187,12 +188,20 @@ rt_status rt_set_stats(rt_ctx_t ctx, int enable);
 rt_status rt_dispatch_rays(rt_ctx_t ctx, uint32_t W, uint32_t H, const uint32_t* rows,
                            uint32_t nrows, void* rgba8_dev, float* rgba32f_dev, void* hip_stream);
 
+/* TraceRay ray flags (the D3D12_RAY_FLAG values the reference passes, Common.hlsl:44-82). */
+enum {
+  RT_RAY_FLAG_NONE = 0x00,
+  RT_RAY_FLAG_ACCEPT_FIRST_HIT_AND_END_SEARCH = 0x04, /* any hit: first accepted hit ends the ray */
+  RT_RAY_FLAG_CULL_BACK_FACING_TRIANGLES = 0x10       /* CastReflectionRay (Common.hlsl:58-69) */
+};
+
 /* Batch TraceRay (Common.hlsl:44-82 semantics) for parity tests and external callers.
  * rays_dev: n x 8 floats (o.x,o.y,o.z,tmin, d.x,d.y,d.z,tmax), direction used as given.
- * any_hit != 0: terminate on the first accepted hit (shadow rays).
+ * ray_flags: RT_RAY_FLAG_* (other bits: RT_E_INVALID). Front faces are clockwise seen from the
+ * ray origin (DXR's default), flipped by an instance transform with a negative determinant.
  * hits_dev: n x 4 x 32-bit: (t as float, instance_id, primitive index, hit flag) with u,v written
  * to uv_dev (n x 2 floats) when uv_dev != NULL. A miss has hit flag 0 and t = tmax. Asynchronous. */
-rt_status rt_trace_rays(rt_ctx_t ctx, const float* rays_dev, uint32_t n, int any_hit,
+rt_status rt_trace_rays(rt_ctx_t ctx, const float* rays_dev, uint32_t n, uint32_t ray_flags,
                         uint32_t* hits_dev, float* uv_dev, void* hip_stream);
 
 /* Multi-GPU frame assembly: un-interleaves `nranks` compact strip images gathered back to back in
@@ -207,7 +216,7 @@ uint32_t rt_strip_rows(uint32_t H, uint32_t nranks, uint32_t rank, uint32_t stri
                        uint32_t* rows_out, uint32_t cap);
 
 /* Copies the counters (RT_STAT_*) to out[RT_STAT_COUNT]; synchronises the context. */
-rt_status rt_stats(rt_ctx_t ctx, uint64_t out[8]);
+rt_status rt_stats(rt_ctx_t ctx, uint64_t out[RT_STAT_COUNT]);
 rt_status rt_stats_reset(rt_ctx_t ctx);
 
 /* ------------------------------------------------------------------------------------------ */

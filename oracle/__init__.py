@@ -46,7 +46,7 @@ _SIGS = [
     ("oracle_export_tlas", _I, [_P, _P]),
     ("oracle_render", _I, [_P, _FP, ctypes.POINTER(oracle_light), _U32, _FP, _I, _I, _U32, _U32, _P, _U32, _P, _P,
                            _I, _P, _I, _I]),
-    ("oracle_trace_rays", _I, [_P, _P, _U32, _I, _P, _P, _I, _P]),
+    ("oracle_trace_rays", _I, [_P, _P, _U32, _U32, _P, _P, _I, _P]),
     ("oracle_pbr", None, [_FP, _FP, _FP, ctypes.POINTER(oracle_light), _U32, _FP, _FP]),
     ("oracle_direct", None, [_FP, _FP, ctypes.POINTER(oracle_light), _U32, _FP, _FP]),
     ("oracle_pow", ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
@@ -212,7 +212,7 @@ class Scene:
         nrows = H if rows is None else len(rows)
         rgba8 = np.zeros((nrows, W, 4), np.uint8)
         rgba32 = np.zeros((nrows, W, 4), np.float32) if want_float else None
-        stats = np.zeros(8, np.uint64)
+        stats = np.zeros(9, np.uint64)
         rp = None
         if rows is not None:
             r = np.ascontiguousarray(rows, dtype=np.uint32)
@@ -228,12 +228,13 @@ class Scene:
         return self.render(spec.camera_buffer(), spec.lights, spec.material, spec.mode, spec.spp, spec.width,
                            spec.height, rows, nthreads, brute_force, want_float, schedule)
 
-    def trace_rays(self, rays: np.ndarray, any_hit=False, brute_force=False):
+    def trace_rays(self, rays: np.ndarray, any_hit=False, brute_force=False, cull_back=False):
         r = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
         n = r.shape[0]
         hits = np.zeros((n, 4), np.uint32)
         uv = np.zeros((n, 2), np.float32)
-        stats = np.zeros(8, np.uint64)
-        lib.oracle_trace_rays(self._h, r.ctypes.data_as(_P), n, 1 if any_hit else 0, hits.ctypes.data_as(_P),
+        stats = np.zeros(9, np.uint64)
+        flags = (0x04 if any_hit else 0) | (0x10 if cull_back else 0)  # D3D12_RAY_FLAG values
+        lib.oracle_trace_rays(self._h, r.ctypes.data_as(_P), n, flags, hits.ctypes.data_as(_P),
                               uv.ctypes.data_as(_P), 1 if brute_force else 0, stats.ctypes.data_as(_P))
         return hits, uv, stats

@@ -228,6 +228,7 @@ typedef struct {
 typedef struct {
   float w2o[12], o2w[12], nrm[9];
   uint32_t instance_id, hit_group, blas;
+  float face; /* +1, or -1 when the transform mirrors (front-face sense flipped for culling) */
 } oinst;
 
 struct oracle_scene {
@@ -580,6 +581,9 @@ int oracle_set_instances(oracle_scene* s, const oracle_instance* in, uint32_t n)
     const float* M = in[i].xform;
     double L[9] = {M[0], M[1], M[2], M[4], M[5], M[6], M[8], M[9], M[10]}, Li[9];
     if (!inv3d(L, Li)) return -1;
+    const double det = L[0] * (L[4] * L[8] - L[5] * L[7]) + L[1] * (L[5] * L[6] - L[3] * L[8]) +
+                       L[2] * (L[3] * L[7] - L[4] * L[6]);
+    r->face = det < 0.0 ? -1.0f : 1.0f;
     double t[3] = {M[3], M[7], M[11]};
     for (int a = 0; a < 3; ++a) {
       r->w2o[a * 4 + 0] = (float)Li[a * 3 + 0];
@@ -633,7 +637,7 @@ int oracle_export_tlas(const oracle_scene* s, void* nodes) {
 /* ---------------------------------------------------------------------------------------- */
 /* traversal: DXR TraceRay semantics (closest hit / any hit), Common.hlsl:44-82               */
 /* ---------------------------------------------------------------------------------------- */
-typedef struct { uint64_t v[8]; } ostats;
+typedef struct { uint64_t v[9]; } ostats;
 typedef struct { float t, u, v; uint32_t inst, prim; } ohit;
 
 static inline float sinv(float d) { return fabsf(d) > 1e-20f ? 1.0f / d : (d < 0.0f ? -1e20f : 1e20f); }
@@ -658,12 +662,14 @@ static inline void osort4(float* t, int32_t* r) {
   ocswap(t, r, 0, 1); ocswap(t, r, 2, 3); ocswap(t, r, 0, 2); ocswap(t, r, 1, 3); ocswap(t, r, 1, 2);
 }
 
-/* Moller-Trumbore (the ray/triangle test DXR performs in hardware; formula pinned here) */
-static inline int omt(vec3 o, vec3 d, const otri* tr, float* t, float* u, float* v) {
+/* Moller-Trumbore (the ray/triangle test DXR performs in hardware; formula pinned here).
+ * face 0: both sides; +1/-1: RAY_FLAG_CULL_BACK_FACING_TRIANGLES, front = det * face > 0
+ * (clockwise seen from the ray origin, DXR's default; face = -1 under a mirroring transform). */
+static inline int omt(vec3 o, vec3 d, const otri* tr, float face, float* t, float* u, float* v) {
   vec3 v0 = ld3(tr->v0), e1 = ld3(tr->e1), e2 = ld3(tr->e2);
   vec3 p = vcross(d, e2);
   float det = vdot(e1, p);
-  if (det == 0.0f) return 0;
+  if (det == 0.0f || det * face < 0.0f) return 0;
   float inv = 1.0f / det;
   vec3 s = vsub(o, v0);
   *u = vdot(s, p) * inv;
@@ -683,7 +689,8 @@ static inline int better(float t, uint32_t inst, uint32_t prim, const ohit* h) {
 
 #define OPUSH(X) do { if (sp < cap) stack[sp++] = (X); else st->v[5]++; } while (0)
 
-static int otrace(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax, int any, ohit* h, ostats* st) {
+static int otrace(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax, int any, int cull, ohit* h,
+                  ostats* st) {
   int stack[256];
   uint32_t maxb = 0;
   for (int b = 0; b < s->nblas; ++b) if (s->blas[b].max_stack > maxb) maxb = s->blas[b].max_stack;
@@ -733,7 +740,7 @@ static int otrace(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax,
       const otri* tr = tris + (~ref);
       float t, u, v;
       st->v[3]++;
-      if (omt(ro, rd, tr, &t, &u, &v) && t >= tmin && better(t, cur, tr->prim, h)) {
+      if (omt(ro, rd, tr, cull ? s->inst[cur].face : 0.0f, &t, &u, &v) && t >= tmin && better(t, cur, tr->prim, h)) {
         h->t = t; h->u = u; h->v = v; h->inst = cur; h->prim = tr->prim;
         found = 1;
         if (any) return 1;
@@ -770,8 +777,8 @@ static int olead(const int* live) {
  * descend into, 2 when an any-hit packet has no live lane left. leaves != NULL (BLAS level):
  * entered triangle children are tested here, in slot order, and never pushed. */
 static int opk_node(const o4node* nd, const opkray* ry, float tmin, ohit* h, int* live, int* lead,
-                    const otri* leaves, uint32_t cur, int any, int* found, int* stack, int* sp, int cap,
-                    int* next, ostats* st) {
+                    const otri* leaves, uint32_t cur, float face, int any, int* found, int* stack, int* sp,
+                    int cap, int* next, ostats* st) {
   uint64_t hm[4] = {0, 0, 0, 0};
   uint32_t vkey[OPK][4];
   for (int l = 0; l < OPK; ++l) {
@@ -802,7 +809,7 @@ static int opk_node(const o4node* nd, const opkray* ry, float tmin, ohit* h, int
         if (!live[l]) continue;
         float t, u, v;
         st->v[3]++;
-        if (omt(ry->o[l], ry->d[l], tr, &t, &u, &v) && t >= tmin && better(t, cur, tr->prim, &h[l])) {
+        if (omt(ry->o[l], ry->d[l], tr, face, &t, &u, &v) && t >= tmin && better(t, cur, tr->prim, &h[l])) {
           h[l].t = t; h[l].u = u; h[l].v = v; h[l].inst = cur; h[l].prim = tr->prim;
           found[l] = 1;
           if (any) live[l] = 0;
@@ -838,7 +845,7 @@ static int opk_node(const o4node* nd, const opkray* ry, float tmin, ohit* h, int
 }
 
 static void opacket(const oracle_scene* s, const vec3* o, const vec3* d, float tmin, float tmax, int any,
-                    const int* alive, ohit* h, int* found, ostats* st) {
+                    int cull, const int* alive, ohit* h, int* found, ostats* st) {
   int live[OPK];
   opkray w, b;
   for (int l = 0; l < OPK; ++l) {
@@ -858,7 +865,8 @@ static void opacket(const oracle_scene* s, const vec3* o, const vec3* d, float t
   int sp = 0, ref = 0, next;
   for (;;) {
     if (ref >= 0) {
-      if (opk_node(s->tlas + ref, &w, tmin, h, live, &lead, NULL, 0u, any, found, stack, &sp, cap, &next, st) == 1) {
+      if (opk_node(s->tlas + ref, &w, tmin, h, live, &lead, NULL, 0u, 0.0f, any, found, stack, &sp, cap, &next,
+                   st) == 1) {
         ref = next;
         continue;
       }
@@ -877,8 +885,8 @@ static void opacket(const oracle_scene* s, const vec3* o, const vec3* d, float t
       int bref = 0;
       for (;;) {
         /* only internal nodes reach here: triangle children are tested inside opk_node */
-        const int r = opk_node(bl->nodes + bref, &b, tmin, h, live, &lead, bl->tris, cur, any, found, stack, &sp,
-                               cap, &next, st);
+        const int r = opk_node(bl->nodes + bref, &b, tmin, h, live, &lead, bl->tris, cur, cull ? ir->face : 0.0f,
+                               any, found, stack, &sp, cap, &next, st);
         if (r == 1) { bref = next; continue; }
         if (r == 2) return;
         if (sp == base) break;
@@ -891,7 +899,8 @@ static void opacket(const oracle_scene* s, const vec3* o, const vec3* d, float t
 }
 
 /* every triangle of every instance, original primitive order */
-static int obrute(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax, int any, ohit* h, ostats* st) {
+static int obrute(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax, int any, int cull, ohit* h,
+                  ostats* st) {
   int found = 0;
   h->t = tmax; h->inst = 0xffffffffu; h->prim = 0xffffffffu; h->u = h->v = 0.0f;
   for (uint32_t i = 0; i < s->ninst; ++i) {
@@ -902,7 +911,7 @@ static int obrute(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax,
       const otri* tr = &b->tris[k];
       float t, u, v;
       st->v[3]++;
-      if (omt(ro, rd, tr, &t, &u, &v) && t >= tmin && better(t, i, tr->prim, h)) {
+      if (omt(ro, rd, tr, cull ? ir->face : 0.0f, &t, &u, &v) && t >= tmin && better(t, i, tr->prim, h)) {
         h->t = t; h->u = u; h->v = v; h->inst = i; h->prim = tr->prim;
         found = 1;
         if (any) return 1;
@@ -1074,7 +1083,75 @@ static int trace_any(const octx* c, vec3 P, vec3 dir, ostats* st) {
   ohit h;
   st->v[1]++;
   vec3 d = vnorm(dir); /* CastShadowRay normalises (Common.hlsl:73) */
-  return c->brute ? obrute(c->s, P, d, 0.01f, 100000.0f, 1, &h, st) : otrace(c->s, P, d, 0.01f, 100000.0f, 1, &h, st);
+  return c->brute ? obrute(c->s, P, d, 0.01f, 100000.0f, 1, 0, &h, st)
+                  : otrace(c->s, P, d, 0.01f, 100000.0f, 1, 0, &h, st);
+}
+
+#define O_MAX_REFLECT 18 /* kMaxReflectDepth (rt_device.hpp): 20 TraceRay levels (D3D12HelloTriangle.cpp:954) */
+
+static vec3 vreflect(vec3 i, vec3 n) { /* HLSL reflect: i - 2 n dot(i, n) */
+  float t = vdot(i, n);
+  return mk(i.x - (2.0f * n.x) * t, i.y - (2.0f * n.y) * t, i.z - (2.0f * n.z) * t);
+}
+
+static vec3 omiss(const octx* c, uint32_t py) {
+  float ramp = (float)py / (float)c->H; /* Miss.hlsl:8-9 (DispatchRaysIndex: the pixel row at every depth) */
+  return mk(0.0f, 0.2f, 0.7f - 0.3f * ramp);
+}
+
+/* PlaneClosestHit (Hit.hlsl:207-241) for a hit at P (one shadow ray) */
+static vec3 oplane(const octx* c, vec3 P, const ohit* h, ostats* st) {
+  vec3 ld = vnorm(vsub(ld3(c->L[0].position), P));
+  vec3 n = o_face_normal(c->s, h->inst, h->prim);
+  int shadowed = vdot(n, ld) < 0.0f;
+  int occ = trace_any(c, P, ld, st);
+  if (!shadowed) shadowed = occ;
+  float factor = shadowed ? 0.3f : 1.0f;
+  float li = fmax2(0.0f, vdot(n, ld));
+  float v = (1.0f * li) * factor;
+  return mk(v, v, v);
+}
+
+/* RT_SHADE_REF for one camera ray: ClosestHit (Hit.hlsl:183-204) / PlaneClosestHit / Miss, with
+ * the reflection rays of InstanceID 0 and 1 (ReflectRay :176-181, CastReflectionRay
+ * Common.hlsl:58-69: origin offset 0.001, TMin 0.001, TMax 1000, back faces culled) when the
+ * material's reflectivity r != 0. The nested lerp(s_k, c_{k+1}, r) chain is evaluated front to
+ * back: acc += (w (1 - r)) s_k, w *= r, ending with acc + w c_N (mathematically the same sum;
+ * this float order is the pinned one). r == 0 traces no reflection. */
+static vec3 oshade_ref(const octx* c, uint32_t py, vec3 O, vec3 D, int f, ohit h, ostats* st) {
+  const float refl = c->mat[5];
+  vec3 acc = mk(0, 0, 0), ro = O, rd = D;
+  float w = 1.0f;
+  int chain = 0;
+  for (int depth = 0;; ++depth) {
+    vec3 term;
+    if (!f) {
+      term = omiss(c, py);
+    } else {
+      const oinst* ir = &c->s->inst[h.inst];
+      vec3 P = vadd(ro, vscale(rd, h.t));
+      if (ir->hit_group == 2u) {
+        term = oplane(c, P, &h, st);
+      } else {
+        vec3 n = o_interp_normal(c->s, h.inst, h.prim, h.u, h.v);
+        vec3 s = vadd(odirect(P, n, ld3(c->mat), c->L, c->nl), opbr(n, ro, P, c->L, c->nl, c->mat));
+        if (refl != 0.0f && (ir->instance_id == 0u || ir->instance_id == 1u) && depth < O_MAX_REFLECT) {
+          acc = vadd(acc, vscale(s, w * (1.0f - refl)));
+          w = w * refl;
+          chain = 1;
+          vec3 dir = vnorm(vnorm(vreflect(vnorm(rd), n)));
+          ro = vadd(P, vscale(dir, 0.001f));
+          rd = dir;
+          st->v[8]++;
+          f = c->brute ? obrute(c->s, ro, rd, 0.001f, 1000.0f, 0, 1, &h, st)
+                       : otrace(c->s, ro, rd, 0.001f, 1000.0f, 0, 1, &h, st);
+          continue;
+        }
+        term = s;
+      }
+    }
+    return chain ? vadd(acc, vscale(term, w)) : term;
+  }
 }
 
 static void hlsl_mul4(const float* m, const float v[4], float r[4]) {
@@ -1102,32 +1179,13 @@ static vec3 osample(const octx* c, uint32_t px, uint32_t py, float ox, float oy,
   oraygen(c, px, py, ox, oy, &O, &D);
   ohit h;
   st->v[0]++;
-  int f = c->brute ? obrute(c->s, O, D, 0.0f, 100000.0f, 0, &h, st) : otrace(c->s, O, D, 0.0f, 100000.0f, 0, &h, st);
-  if (!f) {
-    float ramp = (float)py / (float)c->H; /* Miss.hlsl:8-9 */
-    return mk(0.0f, 0.2f, 0.7f - 0.3f * ramp);
-  }
+  int f = c->brute ? obrute(c->s, O, D, 0.0f, 100000.0f, 0, 0, &h, st)
+                   : otrace(c->s, O, D, 0.0f, 100000.0f, 0, 0, &h, st);
+  if (c->mode == 0) return oshade_ref(c, py, O, D, f, h, st);
+  if (!f) return omiss(c, py);
   const oinst* ir = &c->s->inst[h.inst];
   vec3 P = vadd(O, vscale(D, h.t));
   int plane = ir->hit_group == 2u;
-  if (c->mode == 0) {
-    if (plane) { /* PlaneClosestHit (Hit.hlsl:207-241) */
-      vec3 lp = ld3(c->L[0].position);
-      vec3 ld = vnorm(vsub(lp, P));
-      vec3 n = o_face_normal(c->s, h.inst, h.prim);
-      int shadowed = vdot(n, ld) < 0.0f;
-      int occ = trace_any(c, P, ld, st);
-      if (!shadowed) shadowed = occ;
-      float factor = shadowed ? 0.3f : 1.0f;
-      float li = fmax2(0.0f, vdot(n, ld));
-      float v = (1.0f * li) * factor;
-      return mk(v, v, v);
-    }
-    /* ClosestHit (Hit.hlsl:183-204), reflectivity pinned to 0 */
-    vec3 n = o_interp_normal(c->s, h.inst, h.prim, h.u, h.v);
-    vec3 direct = odirect(P, n, ld3(c->mat), c->L, c->nl);
-    return vadd(direct, opbr(n, O, P, c->L, c->nl, c->mat));
-  }
   vec3 n = plane ? o_face_normal(c->s, h.inst, h.prim) : vneg(o_interp_normal(c->s, h.inst, h.prim, h.u, h.v));
   float sum = 0.0f;
   for (uint32_t l = 0; l < c->nl; ++l) {
@@ -1160,41 +1218,77 @@ static void osample_packet(const octx* c, const uint32_t* px, const uint32_t* py
     oraygen(c, px[l], py[l], ox, oy, &O[l], &D[l]);
     if (inimg[l]) st->v[0]++;
   }
-  opacket(c->s, O, D, 0.0f, 100000.0f, 0, inimg, h, found, st);
+  opacket(c->s, O, D, 0.0f, 100000.0f, 0, 0, inimg, h, found, st);
   for (int l = 0; l < OPK; ++l) {
-    float ramp = (float)py[l] / (float)c->H; /* Miss.hlsl:8-9 */
-    color[l] = mk(0.0f, 0.2f, 0.7f - 0.3f * ramp);
+    color[l] = omiss(c, py[l]);
     P[l] = vadd(O[l], vscale(D[l], h[l].t));
   }
   if (c->mode == 0) {
-    vec3 ldir[OPK], nf[OPK];
+    /* oshade_ref, level by level for the whole tile: each level's shadow rays and next
+     * reflection rays are one packet each */
+    const float refl = c->mat[5];
+    vec3 acc[OPK], ro[OPK], rd[OPK], ldir[OPK], nf[OPK];
+    float w[OPK];
+    int chain[OPK], act[OPK], nxt[OPK];
     for (int l = 0; l < OPK; ++l) {
-      need[l] = 0;
-      ldir[l] = nf[l] = mk(0, 0, 0);
-      if (!found[l]) continue;
-      if (c->s->inst[h[l].inst].hit_group == 2u) {
-        ldir[l] = vnorm(vsub(ld3(c->L[0].position), P[l]));
-        nf[l] = o_face_normal(c->s, h[l].inst, h[l].prim);
-        need[l] = 1;
-        st->v[1]++;
-      } else {
-        vec3 n = o_interp_normal(c->s, h[l].inst, h[l].prim, h[l].u, h[l].v);
-        color[l] = vadd(odirect(P[l], n, ld3(c->mat), c->L, c->nl), opbr(n, O[l], P[l], c->L, c->nl, c->mat));
+      acc[l] = mk(0, 0, 0); ro[l] = O[l]; rd[l] = D[l]; w[l] = 1.0f; chain[l] = 0; act[l] = inimg[l];
+    }
+    for (int depth = 0;; ++depth) {
+      int any_next = 0;
+      for (int l = 0; l < OPK; ++l) {
+        need[l] = 0;
+        nxt[l] = 0;
+        sd[l] = mk(0, 0, 1);
+        if (!act[l]) continue;
+        vec3 term;
+        if (!found[l]) {
+          term = omiss(c, py[l]);
+        } else {
+          const oinst* ir = &c->s->inst[h[l].inst];
+          P[l] = vadd(ro[l], vscale(rd[l], h[l].t));
+          if (ir->hit_group == 2u) {
+            ldir[l] = vnorm(vsub(ld3(c->L[0].position), P[l]));
+            nf[l] = o_face_normal(c->s, h[l].inst, h[l].prim);
+            need[l] = 1;
+            sd[l] = vnorm(ldir[l]);
+            st->v[1]++;
+            continue;
+          }
+          vec3 n = o_interp_normal(c->s, h[l].inst, h[l].prim, h[l].u, h[l].v);
+          vec3 s = vadd(odirect(P[l], n, ld3(c->mat), c->L, c->nl), opbr(n, ro[l], P[l], c->L, c->nl, c->mat));
+          if (refl != 0.0f && (ir->instance_id == 0u || ir->instance_id == 1u) && depth < O_MAX_REFLECT) {
+            acc[l] = vadd(acc[l], vscale(s, w[l] * (1.0f - refl)));
+            w[l] = w[l] * refl;
+            chain[l] = 1;
+            vec3 dir = vnorm(vnorm(vreflect(vnorm(rd[l]), n)));
+            ro[l] = vadd(P[l], vscale(dir, 0.001f));
+            rd[l] = dir;
+            nxt[l] = 1;
+            any_next = 1;
+            st->v[8]++;
+            continue;
+          }
+          term = s;
+        }
+        color[l] = chain[l] ? vadd(acc[l], vscale(term, w[l])) : term;
+        act[l] = 0;
       }
-      sd[l] = vnorm(ldir[l]);
+      opacket(c->s, P, sd, 0.01f, 100000.0f, 1, 0, need, hs, occl, st);
+      for (int l = 0; l < OPK; ++l) {
+        if (!need[l]) continue;
+        int shadowed = vdot(nf[l], ldir[l]) < 0.0f;
+        if (!shadowed) shadowed = occl[l];
+        float factor = shadowed ? 0.3f : 1.0f;
+        float li = fmax2(0.0f, vdot(nf[l], ldir[l]));
+        float v = (1.0f * li) * factor;
+        vec3 term = mk(v, v, v);
+        color[l] = chain[l] ? vadd(acc[l], vscale(term, w[l])) : term;
+        act[l] = 0;
+      }
+      if (!any_next) return;
+      for (int l = 0; l < OPK; ++l) act[l] = nxt[l];
+      opacket(c->s, ro, rd, 0.001f, 1000.0f, 0, 1, act, h, found, st);
     }
-    for (int l = 0; l < OPK; ++l) if (!need[l]) sd[l] = mk(0, 0, 1);
-    opacket(c->s, P, sd, 0.01f, 100000.0f, 1, need, hs, occl, st);
-    for (int l = 0; l < OPK; ++l) {
-      if (!need[l]) continue;
-      int shadowed = vdot(nf[l], ldir[l]) < 0.0f;
-      if (!shadowed) shadowed = occl[l];
-      float factor = shadowed ? 0.3f : 1.0f;
-      float li = fmax2(0.0f, vdot(nf[l], ldir[l]));
-      float v = (1.0f * li) * factor;
-      color[l] = mk(v, v, v);
-    }
-    return;
   }
   vec3 n[OPK], Ld[OPK];
   float sum[OPK], nl[OPK];
@@ -1214,7 +1308,7 @@ static void osample_packet(const octx* c, const uint32_t* px, const uint32_t* py
       sd[l] = need[l] ? vnorm(Ld[l]) : mk(0, 0, 1);
       if (c->mode == 1 && need[l]) st->v[1]++;
     }
-    if (c->mode == 1) opacket(c->s, P, sd, 0.01f, 100000.0f, 1, need, hs, occl, st);
+    if (c->mode == 1) opacket(c->s, P, sd, 0.01f, 100000.0f, 1, 0, need, hs, occl, st);
     for (int l = 0; l < OPK; ++l)
       if (need[l]) sum[l] = sum[l] + nl[l] * (occl[l] ? 0.3f : 1.0f);
   }
@@ -1339,20 +1433,23 @@ int oracle_render(const oracle_scene* s, const float cb[64], const oracle_light*
   if (stats)
     for (int t = 0; t < nthreads; ++t)
       for (int q = 0; q < 6; ++q) stats[q] += jobs[t].st.v[q];
+  if (stats)
+    for (int t = 0; t < nthreads; ++t) stats[8] += jobs[t].st.v[8];
   if (stats) { stats[6] += (uint64_t)W * nrows; stats[7] += 1; }
   return 0;
 }
 
-int oracle_trace_rays(const oracle_scene* s, const float* rays, uint32_t n, int any, uint32_t* hits, float* uv,
-                      int brute, uint64_t* stats) {
+int oracle_trace_rays(const oracle_scene* s, const float* rays, uint32_t n, uint32_t flags, uint32_t* hits,
+                      float* uv, int brute, uint64_t* stats) {
   if (!s || !s->tlas) return -1;
+  const int any = (flags & 0x04u) != 0, cull = (flags & 0x10u) != 0; /* D3D12_RAY_FLAG values */
   ostats st;
   memset(&st, 0, sizeof(st));
   for (uint32_t i = 0; i < n; ++i) {
     const float* r = rays + (size_t)i * 8;
     ohit h;
-    int f = brute ? obrute(s, ld3(r), ld3(r + 4), r[3], r[7], any, &h, &st)
-                  : otrace(s, ld3(r), ld3(r + 4), r[3], r[7], any, &h, &st);
+    int f = brute ? obrute(s, ld3(r), ld3(r + 4), r[3], r[7], any, cull, &h, &st)
+                  : otrace(s, ld3(r), ld3(r + 4), r[3], r[7], any, cull, &h, &st);
     st.v[0]++;
     float t = f ? h.t : r[7];
     uint32_t tb; memcpy(&tb, &t, 4);

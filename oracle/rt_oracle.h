@@ -57,7 +57,7 @@ int oracle_tlas_info(const oracle_scene* s, uint32_t out[4]);
 int oracle_export_blas(const oracle_scene* s, int blas, void* nodes, void* tris);
 int oracle_export_tlas(const oracle_scene* s, void* nodes);
 
-/* render W x H (rows NULL = all). stats[8] accumulates (same slots as RT_STAT_*), may be NULL.
+/* render W x H (rows NULL = all). stats[9] accumulates (same slots as RT_STAT_*), may be NULL.
  * brute_force != 0: closest hit by testing every triangle of every instance (no BVH).
  * schedule: RT_SCHED_PACKET (0: 8 x 8 wave packets, as the device) or RT_SCHED_LANE (1: one
  * independent traversal per pixel). The image is the same; the traversal counters follow it. */
@@ -65,8 +65,9 @@ int oracle_render(const oracle_scene* s, const float cb[64], const oracle_light*
                   const float material[6], int mode, int spp, uint32_t W, uint32_t H, const uint32_t* rows,
                   uint32_t nrows, uint8_t* rgba8, float* rgba32f, int nthreads, uint64_t* stats,
                   int brute_force, int schedule);
-/* batch trace: rays n x 8 floats, hits n x 4 u32 (t bits, instance, prim, flag), uv n x 2 (may be NULL) */
-int oracle_trace_rays(const oracle_scene* s, const float* rays, uint32_t n, int any_hit, uint32_t* hits,
+/* batch trace: rays n x 8 floats, ray_flags = D3D12_RAY_FLAG bits (0x04 first hit ends, 0x10 cull back
+ * faces), hits n x 4 u32 (t bits, instance, prim, flag), uv n x 2 (may be NULL) */
+int oracle_trace_rays(const oracle_scene* s, const float* rays, uint32_t n, uint32_t ray_flags, uint32_t* hits,
                       float* uv, int brute_force, uint64_t* stats);
 
 /* shading building blocks exposed for known-answer tests */

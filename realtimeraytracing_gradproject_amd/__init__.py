@@ -29,8 +29,9 @@ RT_OK, RT_E_INVALID, RT_E_OOM, RT_E_HIP, RT_E_RCCL, RT_E_UNSUPPORTED, RT_E_IO = 
 RT_HITGROUP_MODEL, RT_HITGROUP_SHADOW, RT_HITGROUP_PLANE = 0, 1, 2
 RT_SHADE_REF, RT_SHADE_LAMBERT_SHADOW, RT_SHADE_PRIMARY = 0, 1, 2
 RT_SCHED_PACKET, RT_SCHED_LANE = 0, 1
+RT_RAY_FLAG_ACCEPT_FIRST_HIT_AND_END_SEARCH, RT_RAY_FLAG_CULL_BACK_FACING_TRIANGLES = 0x04, 0x10
 STAT_NAMES = ("primary_rays", "shadow_rays", "aabb_tests", "tri_tests", "instance_entries",
-              "stack_overflows", "pixels", "dispatches")
+              "stack_overflows", "pixels", "dispatches", "reflection_rays")
 
 
 class RtError(RuntimeError):
@@ -88,7 +89,7 @@ SIGNATURES = [
     ("rt_set_schedule", _I, [_P, _I]),
     ("rt_set_stats", _I, [_P, _I]),
     ("rt_dispatch_rays", _I, [_P, _U32, _U32, _P, _U32, _P, _P, _P]),
-    ("rt_trace_rays", _I, [_P, _P, _U32, _I, _P, _P, _P]),
+    ("rt_trace_rays", _I, [_P, _P, _U32, _U32, _P, _P, _P]),
     ("rt_assemble_strips", _I, [_P, _U32, _U32, _U32, _U32, _P, _P, _P]),
     ("rt_strip_rows", _U32, [_U32, _U32, _U32, _U32, _P, _U32]),
     ("rt_stats", _I, [_P, ctypes.POINTER(ctypes.c_uint64)]),
@@ -366,7 +367,7 @@ class Context:
         self._check(self._lib.rt_set_stats(self._h, 1 if on else 0), "rt_set_stats")
 
     def stats(self) -> dict:
-        out = (ctypes.c_uint64 * 8)()
+        out = (ctypes.c_uint64 * len(STAT_NAMES))()
         self._check(self._lib.rt_stats(self._h, out), "rt_stats")
         return dict(zip(STAT_NAMES, list(out)))
 
@@ -384,8 +385,11 @@ class Context:
         self._check(self._lib.rt_dispatch_rays(self._h, width, height, rp, nr, _ptr(rgba8), _ptr(rgba32f), stream),
                     "rt_dispatch_rays")
 
-    def trace_rays(self, rays, n: int, any_hit: bool, hits, uv=None, stream: Optional[int] = None):
-        self._check(self._lib.rt_trace_rays(self._h, _ptr(rays), n, 1 if any_hit else 0, _ptr(hits), _ptr(uv), stream),
+    def trace_rays(self, rays, n: int, any_hit: bool, hits, uv=None, stream: Optional[int] = None,
+                   cull_back: bool = False):
+        flags = (RT_RAY_FLAG_ACCEPT_FIRST_HIT_AND_END_SEARCH if any_hit else 0) | \
+            (RT_RAY_FLAG_CULL_BACK_FACING_TRIANGLES if cull_back else 0)
+        self._check(self._lib.rt_trace_rays(self._h, _ptr(rays), n, flags, _ptr(hits), _ptr(uv), stream),
                     "rt_trace_rays")
 
     def assemble_strips(self, width: int, height: int, nranks: int, strip_rows_: int, gathered, out,

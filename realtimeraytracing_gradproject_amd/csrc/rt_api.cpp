@@ -113,6 +113,10 @@ bool fill_instance_xform(const float* o2w, rt::InstanceRec& r) {
   double L[9] = {o2w[0], o2w[1], o2w[2], o2w[4], o2w[5], o2w[6], o2w[8], o2w[9], o2w[10]};
   double Li[9];
   if (!inverse3(L, Li)) return false;
+  // winding sense for back-face culling: a mirroring transform swaps front and back
+  const double det = L[0] * (L[4] * L[8] - L[5] * L[7]) + L[1] * (L[5] * L[6] - L[3] * L[8]) +
+                     L[2] * (L[3] * L[7] - L[4] * L[6]);
+  r.flip = det < 0.0 ? 1u : 0u;
   double t[3] = {o2w[3], o2w[7], o2w[11]};
   for (int i = 0; i < 3; ++i) {
     r.w2o[i * 4 + 0] = (float)Li[i * 3 + 0];
@@ -570,9 +574,11 @@ rt_status rt_dispatch_rays(rt_ctx_t c, uint32_t W, uint32_t H, const uint32_t* r
   return RT_OK;
 }
 
-rt_status rt_trace_rays(rt_ctx_t c, const float* rays, uint32_t n, int any_hit, uint32_t* hits, float* uv,
+rt_status rt_trace_rays(rt_ctx_t c, const float* rays, uint32_t n, uint32_t ray_flags, uint32_t* hits, float* uv,
                         void* stream) {
   if (!c || (!rays && n) || (!hits && n)) return fail(c, RT_E_INVALID, "rt_trace_rays: null argument");
+  if (ray_flags & ~(uint32_t)(RT_RAY_FLAG_ACCEPT_FIRST_HIT_AND_END_SEARCH | RT_RAY_FLAG_CULL_BACK_FACING_TRIANGLES))
+    return fail(c, RT_E_INVALID, "rt_trace_rays: unsupported ray flags");
   if (!c->inst) return fail(c, RT_E_INVALID, "rt_trace_rays: no TLAS built");
   if (c->tlas_stale) return fail(c, RT_E_INVALID, "rt_trace_rays: BLAS rebuilt since the last rt_tlas_build");
   (void)hipSetDevice(c->device);
@@ -583,7 +589,9 @@ rt_status rt_trace_rays(rt_ctx_t c, const float* rays, uint32_t n, int any_hit, 
     rt_status st = ensure_overflow(c, sv, (size_t)((n + 255) / 256) * 256, pick_stream(c, stream));
     if (st != RT_OK) return st;
   }
-  hipError_t e = rt::launch_trace_rays(sv, rays, n, any_hit, hits, uv, c->d_stats, c->stats_on, pick_stream(c, stream));
+  hipError_t e = rt::launch_trace_rays(sv, rays, n, (ray_flags & RT_RAY_FLAG_ACCEPT_FIRST_HIT_AND_END_SEARCH) != 0,
+                                       (ray_flags & RT_RAY_FLAG_CULL_BACK_FACING_TRIANGLES) != 0, hits, uv, c->d_stats,
+                                       c->stats_on, pick_stream(c, stream));
   if (e != hipSuccess) return hip_fail(c, e, "trace_rays launch");
   return RT_OK;
 }
@@ -611,7 +619,7 @@ uint32_t rt_strip_rows(uint32_t H, uint32_t nranks, uint32_t rank, uint32_t stri
   return n;
 }
 
-rt_status rt_stats(rt_ctx_t c, uint64_t out[8]) {
+rt_status rt_stats(rt_ctx_t c, uint64_t out[RT_STAT_COUNT]) {
   if (!c || !out) return RT_E_INVALID;
   (void)hipSetDevice(c->device);
   HIPCHK(c, hipDeviceSynchronize(), "stats sync");
@@ -620,6 +628,7 @@ rt_status rt_stats(rt_ctx_t c, uint64_t out[8]) {
   for (int k = 0; k < 6; ++k) out[k] = h[k];
   out[RT_STAT_PIXELS] = c->pixels;
   out[RT_STAT_DISPATCHES] = c->dispatches;
+  out[RT_STAT_REFLECTION_RAYS] = h[RT_STAT_REFLECTION_RAYS];
   return RT_OK;
 }
 

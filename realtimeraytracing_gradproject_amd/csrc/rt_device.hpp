@@ -90,7 +90,8 @@ struct alignas(16) InstanceRec {
   const Bvh4Node* nodes;  // the BLAS's own arrays (root = node 0)
   const TriRec* tris;
   uint32_t pool_root;     // the BLAS root's index in the scene pool (see SceneView)
-  uint32_t pad_[3];
+  uint32_t flip;          // instance transform has a negative determinant (front-face sense flipped)
+  uint32_t pad_[2];
   const float* vtx;       // 6 floats per vertex: pos.xyz, normal.xyz (stride 24 B)
   const uint32_t* idx;    // triangle list, or nullptr for non-indexed geometry
 };
@@ -99,6 +100,10 @@ constexpr int kMaxLights = 16;
 constexpr int32_t kStackSentinel = INT32_MIN;  // TLAS -> BLAS transition marker
 constexpr int kMaxTraversalStack = 256;        // entries per lane (LDS part + HBM overflow)
 constexpr int kLdsStackEntries = 32;           // LDS part: 32 KB per 256-lane workgroup
+// Reflection bounces per camera sample in RT_SHADE_REF: the reference pipeline allows 20 nested
+// TraceRay levels (D3D12HelloTriangle.cpp:954) = camera ray + 18 reflections + the plane's
+// shadow ray. A reflective hit at the limit shades as non-reflective (pinned; DXR would fail).
+constexpr int kMaxReflectDepth = 18;
 
 struct LightRec {
   float color[3];
@@ -286,13 +291,14 @@ RT_HD void sort4(float t[4], int32_t r[4]) {
 }
 
 // Moller-Trumbore. Accepts u >= 0, v >= 0, u + v <= 1, det != 0; returns t (not yet range checked).
-// Evaluated without early exits (one predicate at the end): fewer divergent branches per wave;
-// the values are those of the early-exit form whenever it accepts.
-RT_HD bool moller_trumbore(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float& t, float& u, float& v) {
+// face: 0 accepts both sides; +1 / -1 accepts only det * face > 0, i.e. front faces under DXR's
+// RAY_FLAG_CULL_BACK_FACING_TRIANGLES (front = clockwise seen from the ray origin = det > 0 with
+// det = e1 . (d x e2), the sense flipped by a negative instance-transform determinant: face = -1).
+RT_HD bool moller_trumbore(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, float& t, float& u, float& v) {
 #if RT_MT_EARLY_EXIT
   V3 p = cross(d, e2);
   float det = dot(e1, p);
-  if (det == 0.0f) return false;
+  if (det == 0.0f || det * face < 0.0f) return false;
   float inv = 1.0f / det;
   V3 s = sub(o, v0);
   u = dot(s, p) * inv;
@@ -311,14 +317,14 @@ RT_HD bool moller_trumbore(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float& t, float& u, 
   const V3 q = cross(s, e1);
   v = dot(d, q) * inv;
   t = dot(e2, q) * inv;
-  return det != 0.0f && u >= 0.0f && u <= 1.0f && v >= 0.0f && u + v <= 1.0f;
+  return det != 0.0f && !(det * face < 0.0f) && u >= 0.0f && u <= 1.0f && v >= 0.0f && u + v <= 1.0f;
 #endif
 }
 
 // Moller-Trumbore without early exits: every lane runs the same instructions (the wave-packet
 // path, where a divergent early exit costs exec-mask SALU work on the busiest pipe). Accepts
 // exactly what moller_trumbore accepts, with the same u, v, t.
-RT_HD bool moller_trumbore_flat(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float& t, float& u, float& v) {
+RT_HD bool moller_trumbore_flat(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, float& t, float& u, float& v) {
   const V3 p = cross(d, e2);
   const float det = dot(e1, p);
   const float inv = 1.0f / det;
@@ -327,7 +333,13 @@ RT_HD bool moller_trumbore_flat(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float& t, float
   const V3 q = cross(s, e1);
   v = dot(d, q) * inv;
   t = dot(e2, q) * inv;
-  return det != 0.0f && u >= 0.0f && u <= 1.0f && v >= 0.0f && u + v <= 1.0f;
+  return det != 0.0f && !(det * face < 0.0f) && u >= 0.0f && u <= 1.0f && v >= 0.0f && u + v <= 1.0f;
+}
+
+// HLSL reflect(i, n) = i - 2 * n * dot(i, n), evaluated as i - (2 n) * dot(i, n).
+RT_HD V3 reflect_dir(V3 i, V3 n) {
+  const float t = dot(i, n);
+  return v3(i.x - (2.0f * n.x) * t, i.y - (2.0f * n.y) * t, i.z - (2.0f * n.z) * t);
 }
 
 }  // namespace rt

@@ -39,7 +39,7 @@ hipError_t launch_trace_frame(const SceneView& scene, const FrameParams& fp, con
                               void* rgba8, float* rgba32f, unsigned long long* d_stats, bool stats,
                               int schedule, hipStream_t stream);
 
-hipError_t launch_trace_rays(const SceneView& scene, const float* rays, uint32_t n, int any_hit,
+hipError_t launch_trace_rays(const SceneView& scene, const float* rays, uint32_t n, bool any_hit, bool cull,
                              uint32_t* hits, float* uv, unsigned long long* d_stats, bool stats,
                              hipStream_t stream);
 

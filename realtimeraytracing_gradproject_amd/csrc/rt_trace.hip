@@ -31,7 +31,7 @@ constexpr int kBlock = 256;
 constexpr float kPi = 3.14159265359f;  // Common.hlsl:1
 
 struct Counters {
-  uint32_t primary = 0, shadow = 0, aabb = 0, tri = 0, inst = 0, overflow = 0;
+  uint32_t primary = 0, shadow = 0, aabb = 0, tri = 0, inst = 0, overflow = 0, refl = 0;
 };
 
 struct HitRec {
@@ -109,7 +109,7 @@ __device__ __forceinline__ Octant octant(V3 invd) {
 // traversal order. Children are visited nearest first (sort4); the oracle mirrors the order, so
 // the box/triangle test counters match it exactly. Entering an instance pushes a sentinel and
 // moves to the BLAS root in the pool; popping the sentinel restores the world-space ray.
-template <bool ANY_HIT, bool STATS>
+template <bool ANY_HIT, bool STATS, bool CULL = false>
 __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, HitRec& hit,
                       const LaneStack& stk, Counters& cnt) {
   const V3 winvd = v3(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
@@ -120,6 +120,7 @@ __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, H
   const RT_GLOBAL char* pn = (const RT_GLOBAL char*)sc.pool_nodes;
   const RT_GLOBAL char* pt = (const RT_GLOBAL char*)sc.pool_tris;
   uint32_t cur = 0;
+  float face = 0.0f;  // CULL: +1 / -1 (mirroring instance) for the current BLAS
   bool in_blas = false;
   bool found = false;
   const int cap = stk.cap;
@@ -198,6 +199,7 @@ __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, H
         rinvd = v3(safe_inv(rd.x), safe_inv(rd.y), safe_inv(rd.z));
         rnoinv = neg(mul(ro, rinvd));
         oct = octant(rinvd);
+        if (CULL) face = ir->flip ? -1.0f : 1.0f;
         in_blas = true;
         ref = (int)ir->pool_root;
         continue;
@@ -208,7 +210,7 @@ __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, H
       const f4v a = ldf4(pt, toff), b = ldf4(pt, toff + 16u), c = ldf4(pt, toff + 32u);
       if (STATS) ++cnt.tri;
       float t, u, v;
-      if (moller_trumbore(ro, rd, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), v3(c.x, c.y, c.z), t, u, v) &&
+      if (moller_trumbore(ro, rd, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), v3(c.x, c.y, c.z), face, t, u, v) &&
           t >= tmin) {
         const uint32_t prim = __float_as_uint(a.w);
         const bool better =
@@ -302,8 +304,8 @@ struct PacketRay {
 // a hit leaves the packet. Branch-free: selects instead of exec-mask regions.
 template <bool ANY_HIT, bool STATS, int R>
 __device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref, const PacketRay<R>& ry,
-                                           float tmin, uint32_t cur, PacketLive<R>& pl, bool* found, HitRec* hit,
-                                           Counters& cnt) {
+                                           float tmin, uint32_t cur, float face, PacketLive<R>& pl, bool* found,
+                                           HitRec* hit, Counters& cnt) {
   const RT_CONST f4v* tq = (const RT_CONST f4v*)(tpool + (~ref));
   const f4v ta = tq[0], tb = tq[1], tc = tq[2];
   const uint32_t prim = __float_as_uint(ta.w);
@@ -312,7 +314,7 @@ __device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref
     if (STATS && pl.live[r]) ++cnt.tri;
     float t, u, v;
     const bool ok = moller_trumbore_flat(ry.o[r], ry.d[r], v3(ta.x, ta.y, ta.z), v3(tb.x, tb.y, tb.z),
-                                         v3(tc.x, tc.y, tc.z), t, u, v);
+                                         v3(tc.x, tc.y, tc.z), face, t, u, v);
     HitRec& h = hit[r];
     const bool better = t < h.t || (t == h.t && (cur < h.inst || (cur == h.inst && prim < h.prim)));
     const bool take = pl.live[r] && ok && t >= tmin && better;
@@ -336,9 +338,9 @@ __device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref
 // 2 when an any-hit packet has no live ray left.
 template <bool ANY_HIT, bool STATS, bool LEAVES, int R>
 __device__ __forceinline__ int packet_node(const RT_CONST char* pool, const RT_CONST TriRec* tpool, int ref,
-                                           const PacketRay<R>& ry, float tmin, uint32_t cur, PacketLive<R>& pl,
-                                           bool* found, HitRec* hit, WaveStack& stk, int& sp, int cap, int& next,
-                                           Counters& cnt) {
+                                           const PacketRay<R>& ry, float tmin, uint32_t cur, float face,
+                                           PacketLive<R>& pl, bool* found, HitRec* hit, WaveStack& stk, int& sp,
+                                           int cap, int& next, Counters& cnt) {
   const RT_CONST char* nb = pool + ((size_t)(uint32_t)ref << 7);
   const i4v ch = *(const RT_CONST i4v*)(nb + 96);
   const int cref[4] = {ch.x, ch.y, ch.z, ch.w};
@@ -388,7 +390,7 @@ __device__ __forceinline__ int packet_node(const RT_CONST char* pool, const RT_C
       const uint32_t k = (uint32_t)__builtin_ctz(tl);
       tl &= tl - 1u;
       const int tr = k == 0 ? cref[0] : k == 1 ? cref[1] : k == 2 ? cref[2] : cref[3];
-      packet_tri<ANY_HIT, STATS, R>(tpool, tr, ry, tmin, cur, pl, found, hit, cnt);
+      packet_tri<ANY_HIT, STATS, R>(tpool, tr, ry, tmin, cur, face, pl, found, hit, cnt);
     }
     if (ANY_HIT) {
       if (!pl.update()) return 2;
@@ -442,7 +444,7 @@ __device__ __forceinline__ int packet_node(const RT_CONST char* pool, const RT_C
 }
 
 // Traces the R rays of every lane (o, d, alive per slot) as one packet; found[r] / hit[r] per ray.
-template <bool ANY_HIT, bool STATS, int R>
+template <bool ANY_HIT, bool STATS, int R, bool CULL = false>
 __device__ void trace_packet(const SceneView& sc, const V3* o, const V3* d, float tmin, float tmax,
                              const bool* alive, bool* found, HitRec* hit, Counters& cnt) {
   const RT_CONST char* pool = (const RT_CONST char*)sc.pool_nodes;
@@ -473,8 +475,8 @@ __device__ void trace_packet(const SceneView& sc, const V3* o, const V3* d, floa
   while (true) {
     int next;
     if (ref >= 0) {
-      if (packet_node<ANY_HIT, STATS, false, R>(pool, tpool, ref, w, tmin, 0u, pl, found, hit, stk, sp, cap, next,
-                                                cnt)) {
+      if (packet_node<ANY_HIT, STATS, false, R>(pool, tpool, ref, w, tmin, 0u, 0.0f, pl, found, hit, stk, sp, cap,
+                                                next, cnt)) {
         ref = next;
         continue;
       }
@@ -493,12 +495,13 @@ __device__ void trace_packet(const SceneView& sc, const V3* o, const V3* d, floa
         b.invd[r] = v3(safe_inv(b.d[r].x), safe_inv(b.d[r].y), safe_inv(b.d[r].z));
         b.noinv[r] = neg(mul(b.o[r], b.invd[r]));
       }
+      const float face = CULL ? (ir.flip ? -1.0f : 1.0f) : 0.0f;
       const int base = sp;
       int bref = (int)ir.pool_root;
       while (true) {
         // only internal nodes reach here: triangle children are tested inside packet_node
-        const int st = packet_node<ANY_HIT, STATS, true, R>(pool, tpool, bref, b, tmin, cur, pl, found, hit, stk, sp,
-                                                            cap, next, cnt);
+        const int st = packet_node<ANY_HIT, STATS, true, R>(pool, tpool, bref, b, tmin, cur, face, pl, found, hit,
+                                                            stk, sp, cap, next, cnt);
         if (st == 1) {
           bref = next;
           continue;
@@ -519,6 +522,7 @@ struct HitInstance {
   const RT_GLOBAL uint32_t* idx;
   float nrm[9];
   uint32_t hit_group;
+  uint32_t instance_id;  // InstanceID(): reflective when 0 or 1 (Hit.hlsl:196)
 };
 
 __device__ __forceinline__ HitInstance load_hit_instance(const SceneView& sc, uint32_t inst) {
@@ -528,6 +532,7 @@ __device__ __forceinline__ HitInstance load_hit_instance(const SceneView& sc, ui
   h.idx = gp(ir->idx);
   for (int k = 0; k < 9; ++k) h.nrm[k] = ir->nrm[k];
   h.hit_group = ir->hit_group;
+  h.instance_id = ir->instance_id;
   return h;
 }
 
@@ -644,6 +649,74 @@ __device__ bool shadow_ray(const SceneView& sc, V3 P, V3 dir, const LaneStack& s
   return trace<true, STATS>(sc, P, normalize(dir), 0.01f, 100000.0f, h, stk, cnt);
 }
 
+__device__ __forceinline__ V3 miss_color(const FrameParams& fp, uint32_t py) {
+  const float ramp = (float)py / (float)fp.height;  // Miss.hlsl:8 (DispatchRaysIndex: the pixel row at every depth)
+  return v3(0.0f, 0.2f, 0.7f - 0.3f * ramp);
+}
+
+// ReflectRay + CastReflectionRay (Hit.hlsl:176-181, Common.hlsl:58-69): the reflected direction
+// (normalised three times, as the HLSL does) and the offset origin.
+__device__ __forceinline__ void reflection_ray(V3 P, V3 n, V3 rd, V3& ro_next, V3& rd_next) {
+  const V3 dir = normalize(normalize(reflect_dir(normalize(rd), n)));
+  ro_next = add(P, muls(dir, 0.001f));
+  rd_next = dir;
+}
+
+__device__ __forceinline__ bool reflective(const FrameParams& fp, const HitInstance& ir, int depth) {
+  return fp.material.reflectivity != 0.0f && (ir.instance_id == 0u || ir.instance_id == 1u) &&
+         depth < kMaxReflectDepth;
+}
+
+// RT_SHADE_REF for one camera ray, one lane: ClosestHit (Hit.hlsl:183-204) / PlaneClosestHit
+// (:207-241) / Miss, with the reflection rays of InstanceID 0 and 1 when the material's
+// reflectivity r != 0 (back faces culled). The nested lerp(s_k, c_{k+1}, r) chain is evaluated
+// front to back: acc += (w (1 - r)) s_k, w *= r, ending with acc + w c_N (the pinned order,
+// mirrored by oracle/rt_oracle.c oshade_ref). r == 0 traces no reflection.
+template <bool STATS>
+__device__ V3 shade_ref(const SceneView& sc, const FrameParams& fp, uint32_t py, V3 O, V3 D, bool f, HitRec hit,
+                        const LaneStack& stk, Counters& cnt) {
+  const float refl = fp.material.reflectivity;
+  const V3 albedo = v3(fp.material.albedo[0], fp.material.albedo[1], fp.material.albedo[2]);
+  V3 acc = v3(0.0f, 0.0f, 0.0f), ro = O, rd = D;
+  float w = 1.0f;
+  bool chain = false;
+  for (int depth = 0;; ++depth) {
+    V3 term;
+    if (!f) {
+      term = miss_color(fp, py);
+    } else {
+      const HitInstance ir = load_hit_instance(sc, hit.inst);
+      const V3 P = add(ro, muls(rd, hit.t));  // GetWorldHitPoint, Common.hlsl:24-27
+      if (ir.hit_group == 2u) {
+        const LightRec& L0 = fp.lights[0];
+        const V3 ldir = normalize(sub(v3(L0.position[0], L0.position[1], L0.position[2]), P));
+        const V3 n = face_world_normal(ir, hit.prim);
+        bool shadowed = dot(n, ldir) < 0.0f;
+        const bool occl = shadow_ray<STATS>(sc, P, ldir, stk, cnt);
+        if (!shadowed) shadowed = occl;
+        const float factor = shadowed ? 0.3f : 1.0f;
+        const float li = maxf(0.0f, dot(n, ldir));
+        const float c = (1.0f * li) * factor;
+        term = v3(c, c, c);
+      } else {
+        const V3 n = interpolated_world_normal(ir, hit.prim, hit.u, hit.v);
+        const V3 s = add(direct_lighting(fp, P, n, albedo), pbr_shading(fp, n, ro, P));
+        if (reflective(fp, ir, depth)) {
+          acc = add(acc, muls(s, w * (1.0f - refl)));
+          w = w * refl;
+          chain = true;
+          reflection_ray(P, n, rd, ro, rd);
+          if (STATS) ++cnt.refl;
+          f = trace<false, STATS, true>(sc, ro, rd, 0.001f, 1000.0f, hit, stk, cnt);
+          continue;
+        }
+        term = s;
+      }
+    }
+    return chain ? add(acc, muls(term, w)) : term;
+  }
+}
+
 // One camera sample -> color (RayGen.hlsl:28-43 and the hit/miss programs).
 template <int MODE, bool STATS>
 __device__ V3 shade_sample(const SceneView& sc, const FrameParams& fp, uint32_t px, uint32_t py,
@@ -661,33 +734,12 @@ __device__ V3 shade_sample(const SceneView& sc, const FrameParams& fp, uint32_t 
   const V3 D = normalize(v3(dw[0], dw[1], dw[2]));  // CastDefaultRay
   HitRec hit;
   if (STATS) ++cnt.primary;
-  if (!trace<false, STATS>(sc, O, D, 0.0f, 100000.0f, hit, stk, cnt)) {
-    const float ramp = (float)py / (float)fp.height;  // Miss.hlsl:8
-    return v3(0.0f, 0.2f, 0.7f - 0.3f * ramp);
-  }
+  const bool f = trace<false, STATS>(sc, O, D, 0.0f, 100000.0f, hit, stk, cnt);
+  if (MODE == 0) return shade_ref<STATS>(sc, fp, py, O, D, f, hit, stk, cnt);
+  if (!f) return miss_color(fp, py);
   const HitInstance ir = load_hit_instance(sc, hit.inst);
   const V3 P = add(O, muls(D, hit.t));  // GetWorldHitPoint, Common.hlsl:24-27
   const bool plane = ir.hit_group == 2u;
-  if (MODE == 0) {
-    if (plane) {
-      const LightRec& L0 = fp.lights[0];
-      const V3 lp = v3(L0.position[0], L0.position[1], L0.position[2]);
-      const V3 ldir = normalize(sub(lp, P));
-      const V3 n = face_world_normal(ir, hit.prim);
-      bool shadowed = dot(n, ldir) < 0.0f;
-      const bool occl = shadow_ray<STATS>(sc, P, ldir, stk, cnt);
-      if (!shadowed) shadowed = occl;
-      const float factor = shadowed ? 0.3f : 1.0f;
-      const float li = maxf(0.0f, dot(n, ldir));
-      const float c = (1.0f * li) * factor;
-      return v3(c, c, c);
-    }
-    const V3 n = interpolated_world_normal(ir, hit.prim, hit.u, hit.v);
-    const V3 albedo = v3(fp.material.albedo[0], fp.material.albedo[1], fp.material.albedo[2]);
-    const V3 direct = direct_lighting(fp, P, n, albedo);
-    // reflectivity is pinned to 0: lerp(final, refl, 0) == final; no reflection ray.
-    return add(direct, pbr_shading(fp, n, O, P));
-  }
   // RT_SHADE_LAMBERT_SHADOW (MODE 1) and RT_SHADE_PRIMARY (MODE 2)
   const V3 n = plane ? face_world_normal(ir, hit.prim) : neg(interpolated_world_normal(ir, hit.prim, hit.u, hit.v));
   float c = 0.0f;
@@ -715,8 +767,6 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
   V3 O[R], D[R], P[R], sd[R];
   HitRec hit[R], sh[R];
   bool found[R], occl[R], need[R];
-  HitInstance ir[R];
-  bool plane[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const float dx = (((float)px[r] + ox) / (float)fp.width) * 2.0f - 1.0f;
@@ -735,50 +785,86 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
   trace_packet<false, STATS, R>(sc, O, D, 0.0f, 100000.0f, inimg, found, hit, cnt);
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const float ramp = (float)py[r] / (float)fp.height;  // Miss.hlsl:8
-    color[r] = v3(0.0f, 0.2f, 0.7f - 0.3f * ramp);
+    color[r] = miss_color(fp, py[r]);
     P[r] = add(O[r], muls(D[r], hit[r].t));  // GetWorldHitPoint, Common.hlsl:24-27
-    plane[r] = false;
-    if (found[r]) {
-      ir[r] = load_hit_instance(sc, hit[r].inst);
-      plane[r] = ir[r].hit_group == 2u;
-    }
   }
   if (MODE == 0) {
-    V3 ldir[R], nf[R];
+    // shade_ref level by level for the whole packet: each level's shadow rays and next
+    // reflection rays are one packet each (mirrored by oracle osample_packet)
+    const float refl = fp.material.reflectivity;
+    const V3 albedo = v3(fp.material.albedo[0], fp.material.albedo[1], fp.material.albedo[2]);
+    V3 acc[R], ro[R], rd[R], ldir[R], nf[R];
+    float w[R];
+    bool chain[R], act[R], nxt[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      ldir[r] = nf[r] = v3(0.0f, 0.0f, 0.0f);
-      need[r] = false;
-      if (found[r]) {
-        if (plane[r]) {
-          const LightRec& L0 = fp.lights[0];
-          ldir[r] = normalize(sub(v3(L0.position[0], L0.position[1], L0.position[2]), P[r]));
-          nf[r] = face_world_normal(ir[r], hit[r].prim);
-          need[r] = true;
-        } else {
-          const V3 n = interpolated_world_normal(ir[r], hit[r].prim, hit[r].u, hit[r].v);
-          const V3 albedo = v3(fp.material.albedo[0], fp.material.albedo[1], fp.material.albedo[2]);
-          // reflectivity is pinned to 0: lerp(final, refl, 0) == final; no reflection ray.
-          color[r] = add(direct_lighting(fp, P[r], n, albedo), pbr_shading(fp, n, O[r], P[r]));
-        }
-      }
-      if (STATS && need[r]) ++cnt.shadow;
-      sd[r] = normalize(ldir[r]);
+      acc[r] = v3(0.0f, 0.0f, 0.0f);
+      ro[r] = O[r];
+      rd[r] = D[r];
+      w[r] = 1.0f;
+      chain[r] = false;
+      act[r] = inimg[r];
     }
-    trace_packet<true, STATS, R>(sc, P, sd, 0.01f, 100000.0f, need, occl, sh, cnt);
+    for (int depth = 0;; ++depth) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (need[r]) {
+      for (int r = 0; r < R; ++r) {
+        need[r] = false;
+        nxt[r] = false;
+        sd[r] = v3(0.0f, 0.0f, 1.0f);
+        if (!act[r]) continue;
+        V3 term;
+        if (!found[r]) {
+          term = miss_color(fp, py[r]);
+        } else {
+          const HitInstance ir = load_hit_instance(sc, hit[r].inst);
+          P[r] = add(ro[r], muls(rd[r], hit[r].t));
+          if (ir.hit_group == 2u) {
+            const LightRec& L0 = fp.lights[0];
+            ldir[r] = normalize(sub(v3(L0.position[0], L0.position[1], L0.position[2]), P[r]));
+            nf[r] = face_world_normal(ir, hit[r].prim);
+            need[r] = true;
+            sd[r] = normalize(ldir[r]);
+            if (STATS) ++cnt.shadow;
+            continue;
+          }
+          const V3 n = interpolated_world_normal(ir, hit[r].prim, hit[r].u, hit[r].v);
+          const V3 s = add(direct_lighting(fp, P[r], n, albedo), pbr_shading(fp, n, ro[r], P[r]));
+          if (reflective(fp, ir, depth)) {
+            acc[r] = add(acc[r], muls(s, w[r] * (1.0f - refl)));
+            w[r] = w[r] * refl;
+            chain[r] = true;
+            reflection_ray(P[r], n, rd[r], ro[r], rd[r]);
+            nxt[r] = true;
+            if (STATS) ++cnt.refl;
+            continue;
+          }
+          term = s;
+        }
+        color[r] = chain[r] ? add(acc[r], muls(term, w[r])) : term;
+        act[r] = false;
+      }
+      trace_packet<true, STATS, R>(sc, P, sd, 0.01f, 100000.0f, need, occl, sh, cnt);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (!need[r]) continue;
         bool shadowed = dot(nf[r], ldir[r]) < 0.0f;
         if (!shadowed) shadowed = occl[r];
         const float factor = shadowed ? 0.3f : 1.0f;
         const float li = maxf(0.0f, dot(nf[r], ldir[r]));
         const float c = (1.0f * li) * factor;
-        color[r] = v3(c, c, c);
+        const V3 term = v3(c, c, c);
+        color[r] = chain[r] ? add(acc[r], muls(term, w[r])) : term;
+        act[r] = false;
       }
+      // uniform exit: no ray of the packet reflects further
+      bool more = false;
+#pragma unroll
+      for (int r = 0; r < R; ++r) more = more || wave_ballot(nxt[r]) != 0;
+      if (!more) return;
+#pragma unroll
+      for (int r = 0; r < R; ++r) act[r] = nxt[r];
+      trace_packet<false, STATS, R, true>(sc, ro, rd, 0.001f, 1000.0f, act, found, hit, cnt);
     }
-    return;
   }
   // RT_SHADE_LAMBERT_SHADOW (MODE 1) and RT_SHADE_PRIMARY (MODE 2)
   V3 n[R];
@@ -787,9 +873,11 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
   for (int r = 0; r < R; ++r) {
     n[r] = v3(0.0f, 0.0f, 0.0f);
     c[r] = 0.0f;
-    if (found[r])
-      n[r] = plane[r] ? face_world_normal(ir[r], hit[r].prim)
-                      : neg(interpolated_world_normal(ir[r], hit[r].prim, hit[r].u, hit[r].v));
+    if (found[r]) {
+      const HitInstance ir = load_hit_instance(sc, hit[r].inst);
+      n[r] = ir.hit_group == 2u ? face_world_normal(ir, hit[r].prim)
+                                : neg(interpolated_world_normal(ir, hit[r].prim, hit[r].u, hit[r].v));
+    }
   }
   for (uint32_t l = 0; l < fp.nlights; ++l) {
     const LightRec& Lr = fp.lights[l];
@@ -817,9 +905,9 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
 }
 
 __device__ __forceinline__ void flush_stats(const Counters& c, unsigned long long* stats) {
-  uint32_t v[6] = {c.primary, c.shadow, c.aabb, c.tri, c.inst, c.overflow};
-  const int slot[6] = {0, 1, 2, 3, 4, 5};
-  for (int k = 0; k < 6; ++k) {
+  uint32_t v[7] = {c.primary, c.shadow, c.aabb, c.tri, c.inst, c.overflow, c.refl};
+  const int slot[7] = {0, 1, 2, 3, 4, 5, 8};
+  for (int k = 0; k < 7; ++k) {
     unsigned long long x = v[k];
     for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, 64);
     if ((threadIdx.x & 63) == 0 && x) atomicAdd(stats + slot[k], x);
@@ -915,7 +1003,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void k_trace_frame_packet(Sce
   if (STATS) flush_stats(cnt, stats);
 }
 
-template <bool ANY_HIT, bool STATS>
+template <bool ANY_HIT, bool STATS, bool CULL>
 __global__ __launch_bounds__(kBlock) void k_trace_rays(SceneView sc, const float4* __restrict__ rays,
                                                        uint32_t n, uint4* __restrict__ hits,
                                                        float2* __restrict__ uv,
@@ -926,7 +1014,7 @@ __global__ __launch_bounds__(kBlock) void k_trace_rays(SceneView sc, const float
   if (i < n) {
     const float4 a = rays[2 * i], b = rays[2 * i + 1];
     HitRec h;
-    const bool f = trace<ANY_HIT, STATS>(sc, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), a.w, b.w, h,
+    const bool f = trace<ANY_HIT, STATS, CULL>(sc, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), a.w, b.w, h,
                                          lane_stack(sc, s_stack, i), cnt);
     if (STATS) ++cnt.primary;
     hits[i] = make_uint4(__float_as_uint(f ? h.t : b.w), f ? h.inst : 0xffffffffu,
@@ -986,24 +1074,24 @@ hipError_t launch_trace_frame(const SceneView& sc, const FrameParams& fp, const 
   }
 }
 
-hipError_t launch_trace_rays(const SceneView& sc, const float* rays, uint32_t n, int any_hit,
+hipError_t launch_trace_rays(const SceneView& sc, const float* rays, uint32_t n, bool any_hit, bool cull,
                              uint32_t* hits, float* uv, unsigned long long* d_stats, bool stats,
                              hipStream_t s) {
   if (n == 0) return hipSuccess;
   dim3 grid((n + kBlock - 1) / kBlock);
   size_t lds = (size_t)sc.lds_cap * kBlock * sizeof(int);
   const float4* r = (const float4*)rays;
+#define RT_LAUNCH_RAYS(A, C, S)                                                                          \
+  hipLaunchKernelGGL((k_trace_rays<A, S, C>), grid, dim3(kBlock), lds, s, sc, r, n, (uint4*)hits, (float2*)uv, \
+                     d_stats)
   if (any_hit) {
-    if (stats)
-      hipLaunchKernelGGL((k_trace_rays<true, true>), grid, dim3(kBlock), lds, s, sc, r, n, (uint4*)hits, (float2*)uv, d_stats);
-    else
-      hipLaunchKernelGGL((k_trace_rays<true, false>), grid, dim3(kBlock), lds, s, sc, r, n, (uint4*)hits, (float2*)uv, d_stats);
+    if (cull) { if (stats) RT_LAUNCH_RAYS(true, true, true); else RT_LAUNCH_RAYS(true, true, false); }
+    else { if (stats) RT_LAUNCH_RAYS(true, false, true); else RT_LAUNCH_RAYS(true, false, false); }
   } else {
-    if (stats)
-      hipLaunchKernelGGL((k_trace_rays<false, true>), grid, dim3(kBlock), lds, s, sc, r, n, (uint4*)hits, (float2*)uv, d_stats);
-    else
-      hipLaunchKernelGGL((k_trace_rays<false, false>), grid, dim3(kBlock), lds, s, sc, r, n, (uint4*)hits, (float2*)uv, d_stats);
+    if (cull) { if (stats) RT_LAUNCH_RAYS(false, true, true); else RT_LAUNCH_RAYS(false, true, false); }
+    else { if (stats) RT_LAUNCH_RAYS(false, false, true); else RT_LAUNCH_RAYS(false, false, false); }
   }
+#undef RT_LAUNCH_RAYS
   return hipGetLastError();
 }
 

@@ -139,10 +139,21 @@ def config(name: str) -> SceneSpec:
         return _grid("rabbit", "C4", 8, 2, 1920, 1080, 1, ((18.0, 14.0, 18.0), (0.0, 1.0, 0.0), (0.0, 1.0, 0.0)))
     if name == "C5":
         return _grid("rabbit", "C5", 16, 4, 3840, 2160, 4, ((30.0, 22.0, 30.0), (0.0, 1.0, 0.0), (0.0, 1.0, 0.0)))
+    if name in ("REFL", "REFLO"):
+        # the reference scene with a reflective material (reflectivity is never
+        # initialised in the reference, UIConstructor.h:41; 0.5 here): InstanceID 0 and 1 trace
+        # reflection rays. REFL keeps the reference camera (inside teapot 0: long mirror chains),
+        # REFLO looks at the scene from outside.
+        s = reference_scene()
+        s.name = name
+        s.material = REFERENCE_MATERIAL[:5] + (0.5,)
+        if name == "REFLO":
+            s.camera = ((9.0, 6.0, 11.0), (-1.5, 0.5, 0.0), (0.0, 1.0, 0.0))
+        return s
     raise KeyError(name)
 
 
-CONFIGS = ("REF", "C1", "C2", "C2F", "C3", "C4", "C5")
+CONFIGS = ("REF", "C1", "C2", "C2F", "C3", "C4", "C5", "REFL", "REFLO")
 
 
 def upload(ctx, spec: SceneSpec) -> List[int]:

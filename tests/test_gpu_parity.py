@@ -126,7 +126,7 @@ def test_tlas_bitwise_equal_to_oracle(name):
 # ------------------------------------------------------------------------------------------
 
 SMALL = {"REF": (160, 90), "C1": (128, 128), "C2": (192, 108), "C3": (192, 108), "C4": (192, 108),
-         "C5": (96, 54)}
+         "C5": (96, 54), "REFL": (160, 90), "REFLO": (160, 90)}
 
 
 SCHEDULES = {"packet": rt.RT_SCHED_PACKET, "lane": rt.RT_SCHED_LANE}
@@ -144,7 +144,7 @@ def test_frame_parity_small(name, sched):
 
 
 @pytest.mark.parametrize("sched", list(SCHEDULES))
-@pytest.mark.parametrize("name", ["REF", "C2", "C2F", "C4", "C5"])
+@pytest.mark.parametrize("name", ["REF", "C2", "C2F", "C4", "C5", "REFL", "REFLO"])
 def test_counters_match_oracle(name, sched):
     """Traversal counters equal the oracle's emulation of the same schedule: same visit order."""
     spec = scenes.config(name).with_size(*SMALL.get(name, (192, 108)))
@@ -156,6 +156,7 @@ def test_counters_match_oracle(name, sched):
     _, _, ost = o.render_spec(spec, nthreads=8, schedule=SCHEDULES[sched])
     keys = ["primary_rays", "shadow_rays", "aabb_tests", "tri_tests", "instance_entries", "stack_overflows"]
     assert [s[k] for k in keys] == [int(x) for x in ost[:6]]
+    assert s["reflection_rays"] == int(ost[8])
     assert s["stack_overflows"] == 0
     c.close()
 
@@ -236,8 +237,8 @@ def random_rays(n, seed, center=(0.0, 1.0, 0.0), radius=12.0):
     return rays
 
 
-@pytest.mark.parametrize("any_hit", [False, True])
-def test_trace_rays_equals_bruteforce(any_hit):
+@pytest.mark.parametrize("any_hit,cull", [(False, False), (True, False), (False, True)])
+def test_trace_rays_equals_bruteforce(any_hit, cull):
     spec = scenes.config("REF")
     c, o = load_both(spec)
     n = 100000
@@ -245,16 +246,16 @@ def test_trace_rays_equals_bruteforce(any_hit):
     d_rays = torch.from_numpy(rays).cuda()
     d_hits = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
     d_uv = torch.zeros((n, 2), dtype=torch.float32, device="cuda")
-    c.trace_rays(d_rays, n, any_hit, d_hits, d_uv)
+    c.trace_rays(d_rays, n, any_hit, d_hits, d_uv, cull_back=cull)
     torch.cuda.synchronize()
     g = d_hits.cpu().numpy().view(np.uint32)
     guv = d_uv.cpu().numpy()
-    ob, ouv, _ = o.trace_rays(rays, any_hit=any_hit, brute_force=False)
+    ob, ouv, _ = o.trace_rays(rays, any_hit=any_hit, brute_force=False, cull_back=cull)
     assert np.array_equal(g, ob), "GPU BVH traversal differs from oracle BVH traversal"
     assert np.array_equal(guv, ouv)
     if not any_hit:
         sub = slice(0, 20000)  # brute force is O(rays x triangles) on the CPU
-        bb, buv, _ = o.trace_rays(rays[sub], any_hit=False, brute_force=True)
+        bb, buv, _ = o.trace_rays(rays[sub], any_hit=False, brute_force=True, cull_back=cull)
         assert np.array_equal(g[sub], bb), "BVH closest hit differs from brute force"
         assert np.array_equal(guv[sub], buv)
     else:
@@ -346,7 +347,7 @@ def test_assemble_kernel_equals_host_twin():
 
 
 GOLDEN_SIZES = {"REF": (96, 54), "C1": (64, 64), "C2": (96, 54), "C2F": (96, 54), "C3": (96, 54), "C4": (96, 54),
-                "C5": (48, 27)}
+                "C5": (48, 27), "REFL": (96, 54), "REFLO": (96, 54)}
 
 
 @pytest.mark.parametrize("name", list(GOLDEN_SIZES))

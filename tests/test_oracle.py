@@ -12,7 +12,7 @@ from oracle import np_reference
 
 GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "frames_small.npz"))
 SIZES = {"REF": (96, 54), "C1": (64, 64), "C2": (96, 54), "C2F": (96, 54), "C3": (96, 54), "C4": (96, 54),
-         "C5": (48, 27)}
+         "C5": (48, 27), "REFL": (96, 54), "REFLO": (96, 54)}
 
 
 EMPTY = np.int32(-2**31 + 1)
@@ -187,3 +187,81 @@ def test_deterministic_pow_accuracy():
         got = oracle.pow_(float(x), 1.0 / 2.2)
         exp = float(np.float64(np.float32(x)) ** np.float64(np.float32(1 / 2.2))) if x > 1e-30 else 0.0
         assert abs(got - exp) <= 1e-6 * max(exp, 1e-3), (x, got, exp)
+
+
+# ------------------------------------------------------------------------------------------
+# reflection rays: back-face culling convention and the reflection chain
+# ------------------------------------------------------------------------------------------
+
+def _one_triangle_scene(xform):
+    """One triangle v0=(0,0,1), v1=(0,1,1), v2=(1,0,1): seen from the origin looking +z its
+    vertices run clockwise (x right, y up), i.e. it is FRONT-facing for DXR's default."""
+    v = np.array([[0, 0, 1, 0, 0, -1], [0, 1, 1, 0, 0, -1], [1, 0, 1, 0, 0, -1]], np.float32)
+    o = oracle.Scene()
+    o.add_blas(v, None)
+    o.set_instances([(0, xform, 0, rt.RT_HITGROUP_MODEL)])
+    return o
+
+
+def _rays(o, d):
+    r = np.zeros((1, 8), np.float32)
+    r[0, :3] = o
+    r[0, 4:7] = d
+    r[0, 7] = 100.0
+    return r
+
+
+def test_backface_cull_kat():
+    """RAY_FLAG_CULL_BACK_FACING_TRIANGLES: clockwise-from-origin = front (DXR default); a mirroring
+    instance transform (negative determinant) swaps the sides."""
+    front = _rays((0.2, 0.2, 0.0), (0, 0, 1))   # sees v0, v1, v2 clockwise
+    back = _rays((0.2, 0.2, 2.0), (0, 0, -1))   # sees them counter-clockwise
+    o = _one_triangle_scene(scenes.IDENTITY)
+    for r, expect in ((front, 1), (back, 0)):
+        h, _, _ = o.trace_rays(r, cull_back=True)
+        assert h[0, 3] == expect
+        h, _, _ = o.trace_rays(r)  # no culling: both sides hit
+        assert h[0, 3] == 1
+    mirror = np.array([-1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0], np.float32)
+    o = _one_triangle_scene(mirror)
+    front_m = _rays((-0.2, 0.2, 0.0), (0, 0, 1))
+    back_m = _rays((-0.2, 0.2, 2.0), (0, 0, -1))
+    assert o.trace_rays(front_m, cull_back=True)[0][0, 3] == 0
+    assert o.trace_rays(back_m, cull_back=True)[0][0, 3] == 1
+
+
+@pytest.mark.parametrize("name", ["REFL", "REFLO"])
+def test_reflection_chain_schedules_agree(name):
+    spec = scenes.config(name).with_size(80, 45)
+    sc = oracle.Scene(spec)
+    a8, a32, sa = sc.render_spec(spec, nthreads=8, schedule=0)
+    b8, b32, sb = sc.render_spec(spec, nthreads=8, schedule=1)
+    c8, c32, _ = sc.render_spec(spec, nthreads=8, brute_force=True)
+    assert np.array_equal(a32.view(np.uint32), b32.view(np.uint32))
+    assert np.array_equal(a32.view(np.uint32), c32.view(np.uint32))
+    assert sa[8] == sb[8] > 0  # reflection rays, same count either way
+    # reflectivity 0 renders the reference image exactly (no reflection ray at all)
+    ref = scenes.config("REF").with_size(80, 45)
+    r8, r32, rs = oracle.Scene(ref).render_spec(ref, nthreads=8)
+    if name == "REFL":
+        assert rs[8] == 0 and not np.array_equal(a32, r32)
+
+
+def test_reflection_chain_kat():
+    """One mirror bounce by hand: camera above the plane looking down at a reflective model
+    instance (InstanceID 0) whose reflection ray misses: c = (1 - r) s + r miss."""
+    spec = scenes.config("REFLO").with_size(1, 1)
+    spec.instances = [spec.instances[0]]  # teapot at the origin only
+    spec.camera = ((0.0, 10.0, 0.001), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0))  # straight down onto the lid
+    sc = oracle.Scene(spec)
+    _, o32, st = sc.render_spec(spec)
+    r = spec.material[5]
+    # no-reflection surface colour of the same pixel and the miss colour of row 0
+    plain = scenes.config("REFLO").with_size(1, 1)
+    plain.instances, plain.camera = spec.instances, spec.camera
+    plain.material = spec.material[:5] + (0.0,)
+    _, s32, _ = oracle.Scene(plain).render_spec(plain)
+    miss = np.array([0.0, 0.2, 0.7])
+    assert st[8] == 1
+    expect = (1.0 - r) * s32[0, 0, :3].astype(np.float64) + r * miss
+    assert np.abs(o32[0, 0, :3] - expect).max() < 1e-6
