@@ -957,8 +957,12 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void k_trace_frame(SceneView 
 // entry 8r + l / 8 of the tile), a 256-thread workgroup 16 x 16R pixels. Every lane runs the
 // sample loop (rays outside the image or the row list join the packets dead) and stores only
 // in-image pixels.
+// Occupancy: LAMBERT_SHADOW (the perf configs) runs at 6 waves per SIMD (the register allocator
+// keeps it to 80 VGPRs with 28 B of scratch); A/B: -2..6 % frame time on C2, C3, C4, C5 (+3 % on
+// C2F). REF and PRIMARY keep the allocator's choice (REF would spill hundreds of bytes; PRIMARY
+// measured neutral).
 template <int MODE, bool STATS, int R>
-__global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void k_trace_frame_packet(SceneView sc, FrameParams fp,
+__global__ __launch_bounds__(kBlock, (MODE == 1 && !STATS) ? 6 : 1) RT_TRACE_ATTR void k_trace_frame_packet(SceneView sc, FrameParams fp,
                                                                const uint32_t* __restrict__ rows,
                                                                uint32_t* __restrict__ rgba8,
                                                                float4* __restrict__ rgba32f,
