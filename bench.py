@@ -6,12 +6,14 @@ A step is one frame: RayGen -> TLAS/BLAS traversal -> shading + shadow rays -> R
 reference's DispatchRays, D3D12HelloTriangle.cpp:558-592). The scene is static: the LBVH build
 runs once before the timed region and is reported separately (build_ms).
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): the frame is
-split into interleaved 8-row strips (strip s -> rank s mod N), every rank renders its strips into
-a compact buffer, one gather over RCCL brings them to rank 0, which un-interleaves them
-(rt_assemble_strips). Total work per step is fixed (one frame): scaling "strong".
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): every pixel is an
+independent unit, so the job shards with no data-path collective. Default ("frames"): a step is a
+batch of N frames of the configured view, one per rank, each left in its rank's HBM (per-GPU work
+fixed: scaling "weak"). --assemble instead splits ONE frame into interleaved 8-row strips (strip s
+-> rank s mod N), gathers them to rank 0 over RCCL and un-interleaves them there
+(rt_assemble_strips): scaling "strong", the presentation path of a single-view frame.
 
-value = rays traced in one frame (all ranks, counted by the device counters in an untimed pass)
+value = rays traced in one step (all ranks, counted by the device counters in an untimed pass)
 x steps / max-over-ranks wall time of the timed region.
 """
 from __future__ import annotations
@@ -50,6 +52,8 @@ def parse():
     p.add_argument("--schedule", default="packet", choices=["packet", "lane"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=2.0, help="minimum wall time of the CPU baseline sample")
+    p.add_argument("--assemble", action="store_true",
+                   help="N>1: split one frame into strips and gather it to rank 0 (strong scaling)")
     p.add_argument("--save-image", default="", help="write the rank-0 frame as .npy")
     p.add_argument("--extra", default="C2F,C3,C4,C5",
                    help="comma list of further configs timed on one GPU (N=1 only; '' to skip)")
@@ -132,6 +136,7 @@ def main():
     if world != a.gpus:
         a.gpus = world if world > 1 else a.gpus
     distributed = world > 1
+    strips = distributed and a.assemble  # one frame split over ranks + RCCL gather
     torch.cuda.set_device(local)
     if distributed:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -144,18 +149,18 @@ def main():
     binfo = [ctx.blas_info(b) for b in range(len(spec.meshes))]
     tinfo = ctx.tlas_info()
 
-    rows = D.rank_rows(H, world, rank) if distributed else None
+    rows = D.rank_rows(H, world, rank) if strips else None
     nrows = H if rows is None else len(rows)
-    rows_per_rank = D.padded_rows(H, world) if distributed else H
+    rows_per_rank = D.padded_rows(H, world) if strips else H
     stream = torch.cuda.Stream()
     sp = stream.cuda_stream
     local8 = torch.zeros((rows_per_rank, W, 4), dtype=torch.uint8, device="cuda")
-    gathered = torch.zeros((world, rows_per_rank, W, 4), dtype=torch.uint8, device="cuda") if distributed and rank == 0 else None
-    frame = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") if distributed and rank == 0 else None
+    gathered = torch.zeros((world, rows_per_rank, W, 4), dtype=torch.uint8, device="cuda") if strips and rank == 0 else None
+    frame = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") if strips and rank == 0 else None
 
     def step():
         ctx.dispatch(W, H, local8, None, rows=rows, stream=sp)
-        if distributed:
+        if strips:
             with torch.cuda.stream(stream):
                 D.gather_strips(local8, world, rank, gathered)
                 if rank == 0:
@@ -172,7 +177,7 @@ def main():
     counts = torch.tensor([rays_local, st["primary_rays"], st["shadow_rays"]], dtype=torch.float64, device="cuda")
     if distributed:
         dist.all_reduce(counts)
-    rays_frame = int(counts[0].item())
+    rays_step = int(counts[0].item())  # frames mode: N frames; strips mode: one frame
 
     for _ in range(a.warmup):
         step()
@@ -187,7 +192,7 @@ def main():
         ev[k][0].record(stream)
         ctx.dispatch(W, H, local8, None, rows=rows, stream=sp)
         ev[k][1].record(stream)
-        if distributed:
+        if strips:
             with torch.cuda.stream(stream):
                 D.gather_strips(local8, world, rank, gathered)
                 if rank == 0:
@@ -204,15 +209,15 @@ def main():
     tmax = float(tmax.item())
 
     if a.save_image and rank == 0:
-        img = (frame if distributed else local8[:H]).cpu().numpy()
+        img = (frame if strips else local8[:H]).cpu().numpy()
         np.save(a.save_image, img)
 
     if rank == 0:
-        value = rays_frame * a.steps / tmax / 1e6
+        value = rays_step * a.steps / tmax / 1e6
         bytes_launch = (BYTES_PER_AABB_TEST * st["aabb_tests"] + BYTES_PER_TRI_TEST * st["tri_tests"]
                         + BYTES_PER_PIXEL * W * nrows)
         achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
-        traffic = load_traffic(a.config) if not distributed else None
+        traffic = load_traffic(a.config) if not strips else None
         cpu = None
         if not distributed and not a.no_cpu_baseline:
             cpu = cpu_baseline(spec, a.cpu_seconds)
@@ -230,15 +235,16 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(tmax / a.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "strong" if strips else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic camera/lights of BASELINE config; meshes teapot.obj/rabbit.obj from the reference",
             "config": {"workload": f"{spec.name}: {spec.model}.obj x{len(spec.instances) - 1} + plane, "
                                    f"{len(spec.lights)} light(s), {W}x{H}, {spec.spp} spp, shade "
                                    f"{['ref', 'lambert_shadow', 'primary'][spec.mode]}",
-                       "rays_per_frame": rays_frame, "primary_rays": int(counts[1].item()),
-                       "shadow_rays": int(counts[2].item()), "parallelism": f"strips{world}",
+                       "rays_per_step": rays_step,
+                       "rays_per_frame": rays_step if strips else int(rays_local),
+                       "primary_rays": int(counts[1].item()), "shadow_rays": int(counts[2].item()), "parallelism": (f"strips{world}+gather" if strips else f"frames{world}"),
                        "schedule": a.schedule},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

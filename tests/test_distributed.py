@@ -80,3 +80,45 @@ def test_assemble_host_inverse_of_partition():
             rows = D.rank_rows(H, world, r)
             g[r, : len(rows)] = full[rows]
         assert np.array_equal(D.assemble_host(g, H, world), full)
+
+
+def frames_worker(rank, world, port, name, size, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle
+        from realtimeraytracing_gradproject_amd import scenes
+        spec = scenes.config(name).with_size(*size)
+        o8, _, st = oracle.Scene(spec).render_spec(spec, nthreads=1, want_float=False)
+        # bench.py's default N>1 mode: each rank renders a whole frame, no data-path collective;
+        # only the ray counts (sum) and the timed wall clock (max) are reduced
+        counts = torch.tensor([float(st[0] + st[1])], dtype=torch.float64)
+        dist.all_reduce(counts)
+        t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        q.put((rank, o8, float(st[0] + st[1]), float(counts.item()), float(t.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_frames_mode_weak():
+    """Weak-scaling frames mode: N ranks, N identical frames, rays per step = N x one frame."""
+    import sys
+    sys.path.insert(0, ROOT)
+    world, name, size = 2, "C2F", (48, 27)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=frames_worker, args=(r, world, port, name, size, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert np.array_equal(res[0][1], res[1][1])
+    for _, _, local, total, tmax in res:
+        assert total == world * local
+        assert tmax == float(world)
