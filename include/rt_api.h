@@ -249,6 +249,65 @@ void rt_camera_lookat(const float eye[3], const float center[3], const float up[
 void rt_camera_buffer(const float view[16], uint32_t W, uint32_t H, float fov_deg, float znear,
                       float zfar, float cb[64]);
 
+/* ---- Camera manipulator ------------------------------------------------------------------------
+ * nv_helpers_dx12::Manipulator (include/manipulator.h:33-148, src/manipulator.cpp) as plain data the
+ * caller owns, so any FFI can hold it; every function is host-only arithmetic (no GPU). Float
+ * results are bit-identical to the reference's glm 0.9.8.5 arithmetic (tests/golden/manipulator.json).
+ * `mode` and `speed` are written directly (Manipulator::setMode / setSpeed, :50-53, :91-94);
+ * `matrix` is what getMatrix returns (:83-86), column-major as glm stores it. */
+typedef enum rt_manip_mode {  /* Manipulator::Modes, manipulator.h:37 */
+  RT_MANIP_EXAMINE = 0,
+  RT_MANIP_FLY = 1,
+  RT_MANIP_WALK = 2,
+  RT_MANIP_TRACKBALL = 3
+} rt_manip_mode;
+
+typedef enum rt_manip_action {  /* Manipulator::Actions, manipulator.h:38 */
+  RT_MANIP_NONE = 0,
+  RT_MANIP_ORBIT = 1,
+  RT_MANIP_DOLLY = 2,
+  RT_MANIP_PAN = 3,
+  RT_MANIP_LOOK_AROUND = 4
+} rt_manip_action;
+
+/* Manipulator::Inputs (manipulator.h:39-40) as a bit set. */
+#define RT_INPUT_LMB 0x01u
+#define RT_INPUT_MMB 0x02u
+#define RT_INPUT_RMB 0x04u
+#define RT_INPUT_SHIFT 0x08u
+#define RT_INPUT_CTRL 0x10u
+#define RT_INPUT_ALT 0x20u
+
+typedef struct rt_manipulator {  /* member defaults: manipulator.h:124-144 */
+  float pos[3];      /* m_pos  (10,10,10) */
+  float interest[3]; /* m_int  (0,0,0) */
+  float up[3];       /* m_up   (0,1,0) */
+  float roll;        /* m_roll radians about the view z axis */
+  float matrix[16];  /* m_matrix */
+  int32_t width;     /* m_width  1 */
+  int32_t height;    /* m_height 1 */
+  float speed;       /* m_speed  30 */
+  float mouse[2];    /* m_mouse */
+  float tbsize;      /* m_tbsize 0.8 */
+  int32_t mode;      /* rt_manip_mode */
+} rt_manipulator;    /* 132 bytes */
+
+/* Manipulator::Manipulator (:17-20): member defaults, then update(). */
+void rt_manip_init(rt_manipulator* m);
+/* Manipulator::update (:305-314): matrix = lookAt(pos, interest, up) [* rotate(roll, z)]. */
+void rt_manip_update(rt_manipulator* m);
+/* setLookat (:26-32), setRoll (:66-70), setWindowSize (:125-129), setMousePosition (:107-111). */
+void rt_manip_set_lookat(rt_manipulator* m, const float eye[3], const float center[3], const float up[3]);
+void rt_manip_set_roll(rt_manipulator* m, float roll);
+void rt_manip_set_window_size(rt_manipulator* m, int32_t w, int32_t h);
+void rt_manip_set_mouse_position(rt_manipulator* m, int32_t x, int32_t y);
+/* motion (:135-166): apply `action` for a mouse move to (x, y), update, remember (x, y). */
+void rt_manip_motion(rt_manipulator* m, int32_t x, int32_t y, int32_t action);
+/* mouseMove (:175-198): choose the action from the RT_INPUT_* bits, apply it; returns the action. */
+int32_t rt_manip_mouse_move(rt_manipulator* m, int32_t x, int32_t y, uint32_t inputs);
+/* wheel (:203-214): dolly by value*|value|/width*speed, then update. */
+void rt_manip_wheel(rt_manipulator* m, int32_t value);
+
 #ifdef __cplusplus
 }
 #endif

@@ -64,6 +64,14 @@ class rt_bvh_info(ctypes.Structure):
                 ("build_ms", ctypes.c_double)]
 
 
+class rt_manipulator(ctypes.Structure):
+    """include/rt_api.h rt_manipulator: nv_helpers_dx12::Manipulator state (manipulator.h:124-144)."""
+    _fields_ = [("pos", ctypes.c_float * 3), ("interest", ctypes.c_float * 3), ("up", ctypes.c_float * 3),
+                ("roll", ctypes.c_float), ("matrix", ctypes.c_float * 16), ("width", ctypes.c_int32),
+                ("height", ctypes.c_int32), ("speed", ctypes.c_float), ("mouse", ctypes.c_float * 2),
+                ("tbsize", ctypes.c_float), ("mode", ctypes.c_int32)]
+
+
 _P = ctypes.c_void_p
 _U32 = ctypes.c_uint32
 _I = ctypes.c_int
@@ -105,6 +113,16 @@ SIGNATURES = [
     ("rt_plane_vertices", None, [_FP]),
     ("rt_camera_lookat", None, [_FP, _FP, _FP, _FP]),
     ("rt_camera_buffer", None, [_FP, _U32, _U32, ctypes.c_float, ctypes.c_float, ctypes.c_float, _FP]),
+    ("rt_manip_init", None, [ctypes.POINTER(rt_manipulator)]),
+    ("rt_manip_update", None, [ctypes.POINTER(rt_manipulator)]),
+    ("rt_manip_set_lookat", None, [ctypes.POINTER(rt_manipulator), _FP, _FP, _FP]),
+    ("rt_manip_set_roll", None, [ctypes.POINTER(rt_manipulator), ctypes.c_float]),
+    ("rt_manip_set_window_size", None, [ctypes.POINTER(rt_manipulator), ctypes.c_int32, ctypes.c_int32]),
+    ("rt_manip_set_mouse_position", None, [ctypes.POINTER(rt_manipulator), ctypes.c_int32, ctypes.c_int32]),
+    ("rt_manip_motion", None, [ctypes.POINTER(rt_manipulator), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    ("rt_manip_mouse_move", ctypes.c_int32, [ctypes.POINTER(rt_manipulator), ctypes.c_int32, ctypes.c_int32,
+                                             ctypes.c_uint32]),
+    ("rt_manip_wheel", None, [ctypes.POINTER(rt_manipulator), ctypes.c_int32]),
 ]
 
 
@@ -225,6 +243,78 @@ def camera_buffer(view, width: int, height: int, fov_deg: float = 45.0, znear: f
     out = np.zeros(64, np.float32)
     lib.rt_camera_buffer(_fptr(v), width, height, fov_deg, znear, zfar, _fptr(out))
     return out
+
+
+class Manipulator:
+    """Camera manipulator with the reference's API (nv_helpers_dx12::Manipulator,
+    include/manipulator.h:33-148, src/manipulator.cpp) over the C-ABI rt_manip_* functions.
+    Host-only arithmetic; results are bit-identical to the reference's glm arithmetic."""
+    Examine, Fly, Walk, Trackball = 0, 1, 2, 3          # Modes, manipulator.h:37
+    NoAction, Orbit, Dolly, Pan, LookAround = 0, 1, 2, 3, 4  # Actions, manipulator.h:38
+    LMB, MMB, RMB, SHIFT, CTRL, ALT = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20  # Inputs bits
+
+    def __init__(self):
+        self._m = rt_manipulator()
+        lib.rt_manip_init(ctypes.byref(self._m))
+
+    @staticmethod
+    def inputs(lmb=False, mmb=False, rmb=False, shift=False, ctrl=False, alt=False) -> int:
+        """Manipulator::Inputs (manipulator.h:39-40) -> RT_INPUT_* bits."""
+        return (lmb * 0x01) | (mmb * 0x02) | (rmb * 0x04) | (shift * 0x08) | (ctrl * 0x10) | (alt * 0x20)
+
+    def setLookat(self, eye, center, up):
+        e, c, u = _f32(eye, 3), _f32(center, 3), _f32(up, 3)
+        lib.rt_manip_set_lookat(ctypes.byref(self._m), _fptr(e), _fptr(c), _fptr(u))
+
+    def getLookat(self):
+        m = self._m
+        return (np.array(m.pos[:], np.float32), np.array(m.interest[:], np.float32), np.array(m.up[:], np.float32))
+
+    def setWindowSize(self, w: int, h: int):
+        lib.rt_manip_set_window_size(ctypes.byref(self._m), w, h)
+
+    def getWidth(self) -> int:
+        return self._m.width
+
+    def getHeight(self) -> int:
+        return self._m.height
+
+    def setMousePosition(self, x: int, y: int):
+        lib.rt_manip_set_mouse_position(ctypes.byref(self._m), x, y)
+
+    def getMousePosition(self):
+        return int(self._m.mouse[0]), int(self._m.mouse[1])
+
+    def setMode(self, mode: int):
+        self._m.mode = mode
+
+    def getMode(self) -> int:
+        return self._m.mode
+
+    def setRoll(self, roll: float):
+        lib.rt_manip_set_roll(ctypes.byref(self._m), roll)
+
+    def getRoll(self) -> float:
+        return self._m.roll
+
+    def setSpeed(self, speed: float):
+        self._m.speed = speed
+
+    def getSpeed(self) -> float:
+        return self._m.speed
+
+    def getMatrix(self) -> np.ndarray:
+        """Column-major 4x4 as glm stores it (16 floats)."""
+        return np.array(self._m.matrix[:], np.float32)
+
+    def motion(self, x: int, y: int, action: int = 0):
+        lib.rt_manip_motion(ctypes.byref(self._m), x, y, action)
+
+    def mouseMove(self, x: int, y: int, inputs: int) -> int:
+        return int(lib.rt_manip_mouse_move(ctypes.byref(self._m), x, y, inputs))
+
+    def wheel(self, value: int):
+        lib.rt_manip_wheel(ctypes.byref(self._m), value)
 
 
 def strip_rows(height: int, nranks: int, rank: int, strip_rows_: int = 8) -> np.ndarray:

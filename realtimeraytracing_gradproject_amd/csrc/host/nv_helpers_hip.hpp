@@ -194,37 +194,53 @@ class TopLevelASGenerator {
   bool m_sizesComputed = false;
 };
 
-// Camera manipulator API subset the renderer depends on (manipulator.h:33-148): setLookat /
-// getLookat / setWindowSize / getMatrix / setRoll. getMatrix() == glm::lookAt (column-major).
+// Camera manipulator (manipulator.h:33-148) over the C-ABI rt_manip_* state: same class, enums and
+// methods as nv_helpers_dx12::Manipulator; getMatrix() is the glm column-major view matrix.
 class Manipulator {
  public:
-  Manipulator() { update(); }
+  enum Modes { Examine = RT_MANIP_EXAMINE, Fly = RT_MANIP_FLY, Walk = RT_MANIP_WALK, Trackball = RT_MANIP_TRACKBALL };
+  enum Actions { None = RT_MANIP_NONE, Orbit = RT_MANIP_ORBIT, Dolly = RT_MANIP_DOLLY, Pan = RT_MANIP_PAN,
+                 LookAround = RT_MANIP_LOOK_AROUND };
+  struct Inputs {
+    bool lmb = false, mmb = false, rmb = false, shift = false, ctrl = false, alt = false;
+    uint32_t bits() const {
+      return (lmb ? RT_INPUT_LMB : 0u) | (mmb ? RT_INPUT_MMB : 0u) | (rmb ? RT_INPUT_RMB : 0u) |
+             (shift ? RT_INPUT_SHIFT : 0u) | (ctrl ? RT_INPUT_CTRL : 0u) | (alt ? RT_INPUT_ALT : 0u);
+    }
+  };
+
+  Manipulator() { rt_manip_init(&m_state); }
+  Actions mouseMove(int x, int y, const Inputs& inputs) {
+    return static_cast<Actions>(rt_manip_mouse_move(&m_state, x, y, inputs.bits()));
+  }
   void setLookat(const float eye[3], const float center[3], const float up[3]) {
-    std::memcpy(m_pos, eye, 12);
-    std::memcpy(m_int, center, 12);
-    std::memcpy(m_up, up, 12);
-    update();
+    rt_manip_set_lookat(&m_state, eye, center, up);
   }
   void getLookat(float eye[3], float center[3], float up[3]) const {
-    std::memcpy(eye, m_pos, 12);
-    std::memcpy(center, m_int, 12);
-    std::memcpy(up, m_up, 12);
+    std::memcpy(eye, m_state.pos, 12);
+    std::memcpy(center, m_state.interest, 12);
+    std::memcpy(up, m_state.up, 12);
   }
-  void setWindowSize(int w, int h) {
-    m_width = w;
-    m_height = h;
+  void setWindowSize(int w, int h) { rt_manip_set_window_size(&m_state, w, h); }
+  void setMousePosition(int x, int y) { rt_manip_set_mouse_position(&m_state, x, y); }
+  void getMousePosition(int& x, int& y) const {
+    x = static_cast<int>(m_state.mouse[0]);
+    y = static_cast<int>(m_state.mouse[1]);
   }
-  int getWidth() const { return m_width; }
-  int getHeight() const { return m_height; }
-  const float* getMatrix() const { return m_matrix; }
+  void setMode(Modes mode) { m_state.mode = mode; }
+  Modes getMode() const { return static_cast<Modes>(m_state.mode); }
+  void setRoll(float roll) { rt_manip_set_roll(&m_state, roll); }
+  float getRoll() const { return m_state.roll; }
+  const float* getMatrix() const { return m_state.matrix; }
+  void setSpeed(float speed) { m_state.speed = speed; }
+  float getSpeed() const { return m_state.speed; }
+  void motion(int x, int y, int action = 0) { rt_manip_motion(&m_state, x, y, action); }
+  void wheel(int value) { rt_manip_wheel(&m_state, value); }
+  int getWidth() const { return m_state.width; }
+  int getHeight() const { return m_state.height; }
 
  private:
-  void update() { rt_camera_lookat(m_pos, m_int, m_up, m_matrix); }
-  float m_pos[3] = {10, 10, 10};  // manipulator.h:126-128 defaults
-  float m_int[3] = {0, 0, 0};
-  float m_up[3] = {0, 1, 0};
-  float m_matrix[16];
-  int m_width = 1, m_height = 1;
+  rt_manipulator m_state;
 };
 
 inline Manipulator& CameraManip() {  // manipulator.h:148 singleton

@@ -7,6 +7,13 @@
 //   rt_app --model teapot.obj [--scene ref|single|grid8|grid16] [--width W --height H]
 //          [--lights N] [--mode ref|lambert_shadow|primary] [--spp S] [--frames F]
 //          [--eye x y z --center x y z] [--out frame.ppm] [--raw frame.rgba]
+//          [--drag BUTTONS DX DY] [--out-pattern frame_%03d.ppm]
+//
+// --drag replays a mouse drag through the manipulator, as the reference's window messages do
+// (OnButtonDown / OnMouseMove, D3D12HelloTriangle.cpp:1206-1234): button down at the window
+// centre, then every frame the pointer moves by (DX, DY) pixels with BUTTONS held — a '+'-joined
+// subset of lmb, mmb, rmb, shift, ctrl, alt (e.g. lmb = orbit, rmb = dolly, mmb = pan,
+// lmb+alt = look around). --out-pattern writes every frame (printf pattern with the frame index).
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -27,7 +34,8 @@ const rt_light kLights[6] = {  // Hit.hlsl:51-56
     {{1, 1, 1}, {0, 10, 10}, 0.2f}, {{1, 1, 1}, {0, 10, -10}, 0.2f}, {{1, 1, 1}, {0, -10, 0}, 0.2f}};
 
 struct Options {
-  std::string model = "teapot.obj", scene = "ref", mode = "ref", out, raw;
+  std::string model = "teapot.obj", scene = "ref", mode = "ref", out, raw, drag, out_pattern;
+  int drag_dx = 0, drag_dy = 0;
   int width = 1280, height = 720, lights = 6, spp = 1, frames = 1;
   float eye[3] = {1.5f, 1.5f, 1.5f}, center[3] = {0, 0, 0}, up[3] = {0, 1, 0};
 };
@@ -52,6 +60,15 @@ class RayTracingApp {
     CreateAccelerationStructures();
     hip_check(hipMalloc(&m_output, (size_t)m_opt.width * m_opt.height * 4), "hipMalloc(output)");
     hip_check(hipStreamCreate(&m_stream), "hipStreamCreate");
+  }
+
+  // D3D12HelloTriangle::OnButtonDown (:1206-1212): the reference negates the window coordinates
+  void OnButtonDown(int x, int y) { CameraManip().setMousePosition(-x, -y); }
+
+  // D3D12HelloTriangle::OnMouseMove (:1214-1234): no button held -> ignored
+  void OnMouseMove(const Manipulator::Inputs& in, int x, int y) {
+    if (!in.lmb && !in.rmb && !in.mmb) return;
+    CameraManip().mouseMove(-x, -y, in);
   }
 
   // D3D12HelloTriangle::OnUpdate (:421-433): material from the UI defaults, camera buffer
@@ -82,16 +99,19 @@ class RayTracingApp {
     return ms;
   }
 
-  void Save() {
+  // The swap-chain copy (:599-607) becomes a file dump: PPM (RGB) and/or raw RGBA8.
+  void Save(const std::string& ppm, const std::string& raw) {
     std::vector<unsigned char> px((size_t)m_opt.width * m_opt.height * 4);
     hip_check(hipMemcpy(px.data(), m_output, px.size(), hipMemcpyDeviceToHost), "download");
-    if (!m_opt.raw.empty()) {
-      FILE* f = std::fopen(m_opt.raw.c_str(), "wb");
+    if (!raw.empty()) {
+      FILE* f = std::fopen(raw.c_str(), "wb");
+      if (!f) throw std::runtime_error("cannot write " + raw);
       std::fwrite(px.data(), 1, px.size(), f);
       std::fclose(f);
     }
-    if (!m_opt.out.empty()) {
-      FILE* f = std::fopen(m_opt.out.c_str(), "wb");
+    if (!ppm.empty()) {
+      FILE* f = std::fopen(ppm.c_str(), "wb");
+      if (!f) throw std::runtime_error("cannot write " + ppm);
       std::fprintf(f, "P6\n%d %d\n255\n", m_opt.width, m_opt.height);
       for (size_t i = 0; i < px.size(); i += 4) std::fwrite(&px[i], 1, 3, f);
       std::fclose(f);
@@ -160,6 +180,28 @@ class RayTracingApp {
   std::vector<uint32_t> m_indices;
 };
 
+Manipulator::Inputs parse_buttons(const std::string& spec) {
+  Manipulator::Inputs in;
+  size_t b = 0;
+  while (b <= spec.size()) {
+    size_t e = spec.find('+', b);
+    if (e == std::string::npos) e = spec.size();
+    const std::string k = spec.substr(b, e - b);
+    if (k == "lmb") in.lmb = true;
+    else if (k == "mmb") in.mmb = true;
+    else if (k == "rmb") in.rmb = true;
+    else if (k == "shift") in.shift = true;
+    else if (k == "ctrl") in.ctrl = true;
+    else if (k == "alt") in.alt = true;
+    else {
+      std::fprintf(stderr, "unknown button %s in --drag\n", k.c_str());
+      std::exit(2);
+    }
+    b = e + 1;
+  }
+  return in;
+}
+
 Options parse(int argc, char** argv) {
   Options o;
   for (int i = 1; i < argc; ++i) {
@@ -183,6 +225,11 @@ Options parse(int argc, char** argv) {
     else if (a == "--raw") o.raw = next();
     else if (a == "--eye") for (int k = 0; k < 3; ++k) o.eye[k] = (float)std::atof(next());
     else if (a == "--center") for (int k = 0; k < 3; ++k) o.center[k] = (float)std::atof(next());
+    else if (a == "--drag") {
+      o.drag = next();
+      o.drag_dx = std::atoi(next());
+      o.drag_dy = std::atoi(next());
+    } else if (a == "--out-pattern") o.out_pattern = next();
     else {
       std::fprintf(stderr, "unknown option %s\n", a.c_str());
       std::exit(2);
@@ -198,14 +245,28 @@ int main(int argc, char** argv) {
   RayTracingApp app(o);
   try {
     app.OnInit();
+    const bool drag = !o.drag.empty();
+    const Manipulator::Inputs buttons = drag ? parse_buttons(o.drag) : Manipulator::Inputs();
+    int mx = o.width / 2, my = o.height / 2;
+    if (drag) app.OnButtonDown(mx, my);
     float best = 1e30f, sum = 0.0f;
     for (int f = 0; f < o.frames; ++f) {
+      if (drag && f > 0) {
+        mx += o.drag_dx;
+        my += o.drag_dy;
+        app.OnMouseMove(buttons, mx, my);
+      }
       app.OnUpdate();
       float ms = app.OnRender();
       sum += ms;
       best = ms < best ? ms : best;
+      if (!o.out_pattern.empty()) {
+        char name[1024];
+        std::snprintf(name, sizeof(name), o.out_pattern.c_str(), f);
+        app.Save(name, "");
+      }
     }
-    app.Save();
+    app.Save(o.out, o.raw);
     std::printf("{\"frames\": %d, \"ms_mean\": %.4f, \"ms_best\": %.4f, \"width\": %d, \"height\": %d}\n", o.frames,
                 sum / o.frames, best, o.width, o.height);
     app.OnDestroy();

@@ -2,6 +2,8 @@
 
 camera_glm.json   glm::lookAt / glm::rotate from the reference's vendored glm, via the harness
                   oracle/ref_glm_camera.cpp built into oracle/_ref/ (`make ref`).
+manipulator.json  camera-manipulator trajectories (mouseMove / motion / wheel / roll in every mode)
+                  from oracle/ref_glm_manip.cpp over the reference's vendored glm (oracle/_ref/).
 frames_small.npz  oracle frames (RGBA8 + float32) of every config at small sizes; each is first
                   cross-checked against the independent float64 numpy restatement
                   (oracle/np_reference.py) and the script refuses to write on disagreement.
@@ -35,14 +37,18 @@ NUMPY_CHECK = {"REF", "C1", "C2", "C2F", "C3", "C4"}  # C5 (257 instances x 4 sp
 NUMPY_TOL = 1e-4
 
 
-def camera():
-    exe = os.path.join(ROOT, "oracle", "_ref", "glm_camera")
-    if not os.path.exists(exe):
-        subprocess.run(["make", "-C", ROOT, "ref"], check=True)
+def _harness(name: str, fixture: str):
+    exe = os.path.join(ROOT, "oracle", "_ref", name)
+    subprocess.run(["make", "-C", ROOT, "ref"], check=True)
     out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout
     json.loads(out)
-    with open(os.path.join(HERE, "camera_glm.json"), "w") as f:
+    with open(os.path.join(HERE, fixture), "w") as f:
         f.write(out)
+
+
+def camera():
+    _harness("glm_camera", "camera_glm.json")
+    _harness("glm_manip", "manipulator.json")
 
 
 def frames():
