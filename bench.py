@@ -51,7 +51,7 @@ def parse():
     p.add_argument("--config", default="C2", choices=[c for c in scenes.CONFIGS])
     p.add_argument("--schedule", default="packet", choices=["packet", "lane"])
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=2.0, help="minimum wall time of the CPU baseline sample")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum wall time of the CPU baseline sample")
     p.add_argument("--assemble", action="store_true",
                    help="N>1: split one frame into strips and gather it to rank 0 (strong scaling)")
     p.add_argument("--save-image", default="", help="write the rank-0 frame as .npy")
