@@ -34,15 +34,15 @@ $(BUILD)/rt_api.o: $(SRC)/rt_api.cpp $(HDRS) | $(BUILD)
 $(BUILD)/rt_host.o: $(SRC)/rt_host.cpp include/rt_api.h | $(BUILD)
 	g++ $(CXXFLAGS) -c $< -o $@
 
-$(LIB): $(BUILD)/rt_api.o $(BUILD)/rt_host.o $(BUILD)/rt_lbvh.o $(BUILD)/rt_trace.o | $(LIBDIR)
+$(LIB): $(BUILD)/rt_api.o $(BUILD)/rt_host.o $(BUILD)/rt_lbvh.o $(BUILD)/rt_trace.o $(BUILD)/rt_raster.o | $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-rpath,$(ROCM)/lib
 
 $(APP): $(SRC)/host/rt_app.cpp $(wildcard $(SRC)/host/*.hpp) $(LIB) | $(LIBDIR)
 	g++ $(CXXFLAGS) -I$(ROCM)/include -D__HIP_PLATFORM_AMD__ -o $@ $(SRC)/host/rt_app.cpp \
 	    -L$(LIBDIR) -lrtamd -L$(ROCM)/lib -lamdhip64 -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(ROCM)/lib
 
-$(ORACLE): oracle/rt_oracle.c oracle/rt_oracle.h
-	gcc $(OCFLAGS) -shared -o $@ oracle/rt_oracle.c -lm -lpthread
+$(ORACLE): oracle/rt_oracle.c oracle/rt_raster_oracle.c oracle/rt_oracle.h
+	gcc $(OCFLAGS) -shared -o $@ oracle/rt_oracle.c oracle/rt_raster_oracle.c -lm -lpthread
 
 ref:
 	$(MAKE) -C oracle -f Makefile.ref

@@ -128,6 +128,33 @@ def measure_config(name: str, steps: int, warmup: int, schedule: int) -> dict:
             "tri_tests_per_ray": round(st["tri_tests"] / max(rays, 1), 2)}
 
 
+def measure_raster(name: str, steps: int, warmup: int) -> dict:
+    """Raster fallback (rt_raster_draw: the reference's scrapped raster pipeline, model + plane with
+    instance 0's transform) on one GPU, reported under "extra"."""
+    spec = scenes.config(name)
+    W, H = spec.width, spec.height
+    with rt.Context(torch.cuda.current_device()) as ctx:
+        ids = scenes.upload(ctx, spec)
+        stream = torch.cuda.Stream()
+        out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+        x0 = spec.instances[0][1]
+        for _ in range(warmup):
+            ctx.raster_draw(ids, W, H, out, object_to_world=x0, stream=stream.cuda_stream)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(stream)
+        for _ in range(steps):
+            ctx.raster_draw(ids, W, H, out, object_to_world=x0, stream=stream.cuda_stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        ms = e0.elapsed_time(e1) / steps
+    tris = sum(((v.shape[0] if i is None else len(i)) // 3) for v, i in spec.meshes)
+    return {"config": f"{name} raster", "frame_ms": round(wall / steps * 1e3, 4), "gpu_ms": round(ms, 4),
+            "triangles": int(tris), "resolution": f"{W}x{H}"}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -226,6 +253,7 @@ def main():
             sched = rt.RT_SCHED_LANE if a.schedule == "lane" else rt.RT_SCHED_PACKET
             for name in a.extra.split(","):
                 extra.append(measure_config(name, max(5, a.steps // 2), 2, sched))
+            extra.append(measure_raster("REF", max(5, a.steps // 2), 2))
         out = {
             "metric": "Mrays/sec (primary+shadow) at 1080p",
             "value": round(value, 2),

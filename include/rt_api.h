@@ -192,17 +192,32 @@ rt_status rt_dispatch_rays(rt_ctx_t ctx, uint32_t W, uint32_t H, const uint32_t*
 enum {
   RT_RAY_FLAG_NONE = 0x00,
   RT_RAY_FLAG_ACCEPT_FIRST_HIT_AND_END_SEARCH = 0x04, /* any hit: first accepted hit ends the ray */
-  RT_RAY_FLAG_CULL_BACK_FACING_TRIANGLES = 0x10       /* CastReflectionRay (Common.hlsl:58-69) */
+  RT_RAY_FLAG_CULL_BACK_FACING_TRIANGLES = 0x10,      /* CastReflectionRay (Common.hlsl:58-69) */
+  RT_RAY_FLAG_CULL_FRONT_FACING_TRIANGLES = 0x20      /* DXR flag; not set by the reference's shaders */
 };
 
 /* Batch TraceRay (Common.hlsl:44-82 semantics) for parity tests and external callers.
  * rays_dev: n x 8 floats (o.x,o.y,o.z,tmin, d.x,d.y,d.z,tmax), direction used as given.
- * ray_flags: RT_RAY_FLAG_* (other bits: RT_E_INVALID). Front faces are clockwise seen from the
+ * ray_flags: RT_RAY_FLAG_* (other bits, or both cull flags: RT_E_INVALID). Front faces are clockwise seen from the
  * ray origin (DXR's default), flipped by an instance transform with a negative determinant.
  * hits_dev: n x 4 x 32-bit: (t as float, instance_id, primitive index, hit flag) with u,v written
  * to uv_dev (n x 2 floats) when uv_dev != NULL. A miss has hit flag 0 and t = tmax. Asynchronous. */
 rt_status rt_trace_rays(rt_ctx_t ctx, const float* rays_dev, uint32_t n, uint32_t ray_flags,
                         uint32_t* hits_dev, float* uv_dev, void* hip_stream);
+
+/* Raster fallback: the reference's abandoned rasterization pipeline (shaders/shaders.hlsl:41-59,
+ * recorded at D3D12HelloTriangle.cpp:513-540, pipeline state :248-276). Draws the BLAS vertex
+ * buffers `draws[0..ndraws)` in order (indexed when built with indices; the reference draws the
+ * model, then the plane) through VSMain: pos = projection * view * objectToWorld * (p, 1), with
+ * view = cb[0..15] and projection = cb[16..31] of rt_set_camera and objectToWorld the 3x4
+ * row-major transform given (the reference binds instance 0's; NULL = identity). D3D rules:
+ * clip 0 <= z <= w, 16.8 fixed-point snap, pixel centres, top-left fill rule, back faces culled
+ * (clockwise = front), depth LESS on a D32 buffer cleared to 1.0. PSMain returns the interpolated
+ * COLOR (the reference's input layout: the 16 bytes at offset 12 of each vertex = normal.xyz +
+ * next vertex's position.x; 0 for the last vertex). rgba8: W x H RGBA8 (cleared to
+ * {0.03, 0.35, 0.43, 1}); depth32f: optional W x H floats. Device pointers, async on `stream`. */
+rt_status rt_raster_draw(rt_ctx_t ctx, const rt_blas_t* draws, uint32_t ndraws, const float* object_to_world,
+                         uint32_t W, uint32_t H, void* rgba8, float* depth32f, void* stream);
 
 /* Multi-GPU frame assembly: un-interleaves `nranks` compact strip images gathered back to back in
  * `gathered_dev` (rank-major; rank k holds strips s with s % nranks == k, strip_rows rows each)

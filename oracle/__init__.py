@@ -47,6 +47,7 @@ _SIGS = [
     ("oracle_render", _I, [_P, _FP, ctypes.POINTER(oracle_light), _U32, _FP, _I, _I, _U32, _U32, _P, _U32, _P, _P,
                            _I, _P, _I, _I]),
     ("oracle_trace_rays", _I, [_P, _P, _U32, _U32, _P, _P, _I, _P]),
+    ("oracle_raster", _I, [_P, _P, _P, _P, _U32, _P, _P, _U32, _U32, _P, _P, _P]),
     ("oracle_pbr", None, [_FP, _FP, _FP, ctypes.POINTER(oracle_light), _U32, _FP, _FP]),
     ("oracle_direct", None, [_FP, _FP, ctypes.POINTER(oracle_light), _U32, _FP, _FP]),
     ("oracle_pow", ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
@@ -136,6 +137,30 @@ def direct(n, P, lights, albedo):
     m, mp = _f(albedo)
     lib.oracle_direct(ap, cp, _lights(lights), len(lights), mp, out.ctypes.data_as(_FP))
     return out
+
+
+def raster(draws, cb, W: int, H: int, object_to_world=None):
+    """Raster fallback oracle (rt_raster_oracle.c). draws: sequence of (vtx6 (n, 6) float32, idx or
+    None) in submission order. Returns (rgba8 (H, W, 4), depth (H, W), prim (H, W) uint32)."""
+    vs = [np.ascontiguousarray(v, dtype=np.float32).reshape(-1, 6) for v, _ in draws]
+    ids = [None if i is None else np.ascontiguousarray(i, dtype=np.uint32).ravel() for _, i in draws]
+    n = len(draws)
+    vp = (ctypes.c_void_p * n)(*[v.ctypes.data for v in vs])
+    ip = (ctypes.c_void_p * n)(*[None if i is None else i.ctypes.data for i in ids])
+    nv = np.array([v.shape[0] for v in vs], np.uint32)
+    nt = np.array([(v.shape[0] if i is None else i.size) // 3 for v, i in zip(vs, ids)], np.uint32)
+    x = np.asarray([1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0] if object_to_world is None else object_to_world,
+                   np.float32).ravel()
+    c = np.ascontiguousarray(cb, dtype=np.float32).ravel()
+    rgba8 = np.zeros((H, W, 4), np.uint8)
+    depth = np.zeros((H, W), np.float32)
+    prim = np.zeros((H, W), np.uint32)
+    r = lib.oracle_raster(ctypes.cast(vp, _P), nv.ctypes.data_as(_P), ctypes.cast(ip, _P), nt.ctypes.data_as(_P), n,
+                          x.ctypes.data_as(_P), c.ctypes.data_as(_P), W, H, rgba8.ctypes.data_as(_P),
+                          depth.ctypes.data_as(_P), prim.ctypes.data_as(_P))
+    if r:
+        raise RuntimeError(f"oracle_raster failed ({r})")
+    return rgba8, depth, prim
 
 
 def pow_(x: float, y: float) -> float:
@@ -228,13 +253,14 @@ class Scene:
         return self.render(spec.camera_buffer(), spec.lights, spec.material, spec.mode, spec.spp, spec.width,
                            spec.height, rows, nthreads, brute_force, want_float, schedule)
 
-    def trace_rays(self, rays: np.ndarray, any_hit=False, brute_force=False, cull_back=False):
+    def trace_rays(self, rays: np.ndarray, any_hit=False, brute_force=False, cull_back=False, cull_front=False):
         r = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
         n = r.shape[0]
         hits = np.zeros((n, 4), np.uint32)
         uv = np.zeros((n, 2), np.float32)
         stats = np.zeros(9, np.uint64)
-        flags = (0x04 if any_hit else 0) | (0x10 if cull_back else 0)  # D3D12_RAY_FLAG values
-        lib.oracle_trace_rays(self._h, r.ctypes.data_as(_P), n, flags, hits.ctypes.data_as(_P),
-                              uv.ctypes.data_as(_P), 1 if brute_force else 0, stats.ctypes.data_as(_P))
+        flags = (0x04 if any_hit else 0) | (0x10 if cull_back else 0) | (0x20 if cull_front else 0)  # D3D12_RAY_FLAG
+        if lib.oracle_trace_rays(self._h, r.ctypes.data_as(_P), n, flags, hits.ctypes.data_as(_P),
+                              uv.ctypes.data_as(_P), 1 if brute_force else 0, stats.ctypes.data_as(_P)):
+            raise RuntimeError("oracle_trace_rays failed")
         return hits, uv, stats

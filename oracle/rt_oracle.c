@@ -740,7 +740,7 @@ static int otrace(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax,
       const otri* tr = tris + (~ref);
       float t, u, v;
       st->v[3]++;
-      if (omt(ro, rd, tr, cull ? s->inst[cur].face : 0.0f, &t, &u, &v) && t >= tmin && better(t, cur, tr->prim, h)) {
+      if (omt(ro, rd, tr, cull ? (float)cull * s->inst[cur].face : 0.0f, &t, &u, &v) && t >= tmin && better(t, cur, tr->prim, h)) {
         h->t = t; h->u = u; h->v = v; h->inst = cur; h->prim = tr->prim;
         found = 1;
         if (any) return 1;
@@ -885,7 +885,7 @@ static void opacket(const oracle_scene* s, const vec3* o, const vec3* d, float t
       int bref = 0;
       for (;;) {
         /* only internal nodes reach here: triangle children are tested inside opk_node */
-        const int r = opk_node(bl->nodes + bref, &b, tmin, h, live, &lead, bl->tris, cur, cull ? ir->face : 0.0f,
+        const int r = opk_node(bl->nodes + bref, &b, tmin, h, live, &lead, bl->tris, cur, cull ? (float)cull * ir->face : 0.0f,
                                any, found, stack, &sp, cap, &next, st);
         if (r == 1) { bref = next; continue; }
         if (r == 2) return;
@@ -911,7 +911,7 @@ static int obrute(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax,
       const otri* tr = &b->tris[k];
       float t, u, v;
       st->v[3]++;
-      if (omt(ro, rd, tr, cull ? ir->face : 0.0f, &t, &u, &v) && t >= tmin && better(t, i, tr->prim, h)) {
+      if (omt(ro, rd, tr, cull ? (float)cull * ir->face : 0.0f, &t, &u, &v) && t >= tmin && better(t, i, tr->prim, h)) {
         h->t = t; h->u = u; h->v = v; h->inst = i; h->prim = tr->prim;
         found = 1;
         if (any) return 1;
@@ -1442,7 +1442,9 @@ int oracle_render(const oracle_scene* s, const float cb[64], const oracle_light*
 int oracle_trace_rays(const oracle_scene* s, const float* rays, uint32_t n, uint32_t flags, uint32_t* hits,
                       float* uv, int brute, uint64_t* stats) {
   if (!s || !s->tlas) return -1;
-  const int any = (flags & 0x04u) != 0, cull = (flags & 0x10u) != 0; /* D3D12_RAY_FLAG values */
+  /* D3D12_RAY_FLAG values: 0x04 accept first hit, 0x10 cull back faces, 0x20 cull front faces */
+  if ((flags & 0x30u) == 0x30u) return -1;
+  const int any = (flags & 0x04u) != 0, cull = (flags & 0x10u) ? 1 : ((flags & 0x20u) ? -1 : 0);
   ostats st;
   memset(&st, 0, sizeof(st));
   for (uint32_t i = 0; i < n; ++i) {

@@ -70,6 +70,13 @@ int oracle_render(const oracle_scene* s, const float cb[64], const oracle_light*
 int oracle_trace_rays(const oracle_scene* s, const float* rays, uint32_t n, uint32_t ray_flags, uint32_t* hits,
                       float* uv, int brute_force, uint64_t* stats);
 
+/* raster fallback (rt_raster_draw), rt_raster_oracle.c: draws in order, each vtx6[d] with nvtx[d]
+ * {pos, normal} vertices and ntri[d] triangles (idx[d] NULL = non-indexed). rgba8 W x H x 4;
+ * depth_out (W x H floats) and prim_out (W x H, 0xffffffff = background) may be NULL. */
+int oracle_raster(const float* const* vtx6, const uint32_t* nvtx, const uint32_t* const* idx, const uint32_t* ntri,
+                  uint32_t ndraws, const float o2w3x4[12], const float cb[64], uint32_t W, uint32_t H,
+                  uint8_t* rgba8, float* depth_out, uint32_t* prim_out);
+
 /* shading building blocks exposed for known-answer tests */
 void oracle_pbr(const float n[3], const float cam[3], const float P[3], const oracle_light* lights,
                 uint32_t nlights, const float material[6], float out[3]);

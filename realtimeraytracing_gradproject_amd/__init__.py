@@ -30,6 +30,7 @@ RT_HITGROUP_MODEL, RT_HITGROUP_SHADOW, RT_HITGROUP_PLANE = 0, 1, 2
 RT_SHADE_REF, RT_SHADE_LAMBERT_SHADOW, RT_SHADE_PRIMARY = 0, 1, 2
 RT_SCHED_PACKET, RT_SCHED_LANE = 0, 1
 RT_RAY_FLAG_ACCEPT_FIRST_HIT_AND_END_SEARCH, RT_RAY_FLAG_CULL_BACK_FACING_TRIANGLES = 0x04, 0x10
+RT_RAY_FLAG_CULL_FRONT_FACING_TRIANGLES = 0x20
 STAT_NAMES = ("primary_rays", "shadow_rays", "aabb_tests", "tri_tests", "instance_entries",
               "stack_overflows", "pixels", "dispatches", "reflection_rays")
 
@@ -98,6 +99,7 @@ SIGNATURES = [
     ("rt_set_stats", _I, [_P, _I]),
     ("rt_dispatch_rays", _I, [_P, _U32, _U32, _P, _U32, _P, _P, _P]),
     ("rt_trace_rays", _I, [_P, _P, _U32, _U32, _P, _P, _P]),
+    ("rt_raster_draw", _I, [_P, _UP, _U32, _FP, _U32, _U32, _P, _P, _P]),
     ("rt_assemble_strips", _I, [_P, _U32, _U32, _U32, _U32, _P, _P, _P]),
     ("rt_strip_rows", _U32, [_U32, _U32, _U32, _U32, _P, _U32]),
     ("rt_stats", _I, [_P, ctypes.POINTER(ctypes.c_uint64)]),
@@ -476,11 +478,23 @@ class Context:
                     "rt_dispatch_rays")
 
     def trace_rays(self, rays, n: int, any_hit: bool, hits, uv=None, stream: Optional[int] = None,
-                   cull_back: bool = False):
+                   cull_back: bool = False, cull_front: bool = False):
         flags = (RT_RAY_FLAG_ACCEPT_FIRST_HIT_AND_END_SEARCH if any_hit else 0) | \
-            (RT_RAY_FLAG_CULL_BACK_FACING_TRIANGLES if cull_back else 0)
+            (RT_RAY_FLAG_CULL_BACK_FACING_TRIANGLES if cull_back else 0) | \
+            (RT_RAY_FLAG_CULL_FRONT_FACING_TRIANGLES if cull_front else 0)
         self._check(self._lib.rt_trace_rays(self._h, _ptr(rays), n, flags, _ptr(hits), _ptr(uv), stream),
                     "rt_trace_rays")
+
+    def raster_draw(self, draws: Sequence[int], width: int, height: int, rgba8, depth=None, object_to_world=None,
+                    stream: Optional[int] = None):
+        """Raster fallback (rt_raster_draw; shaders/shaders.hlsl:41-59, D3D12HelloTriangle.cpp:513-540):
+        draws the BLAS vertex buffers in order with the current camera into rgba8 (H x W x 4 device
+        tensor) and optionally depth (H x W float32 device tensor)."""
+        d = np.ascontiguousarray(draws, dtype=np.uint32)
+        x = None if object_to_world is None else _f32(object_to_world, 12)
+        self._check(self._lib.rt_raster_draw(self._h, d.ctypes.data_as(_UP), len(d),
+                                             None if x is None else _fptr(x), width, height, _ptr(rgba8),
+                                             _ptr(depth), stream), "rt_raster_draw")
 
     def assemble_strips(self, width: int, height: int, nranks: int, strip_rows_: int, gathered, out,
                         stream: Optional[int] = None):

@@ -67,6 +67,9 @@ struct rt_ctx {
   rt::TriRec* pool_tris = nullptr;
   size_t pool_nodes_cap = 0, pool_tris_cap = 0;
   bool tlas_stale = false;  // a BLAS was rebuilt after the last rt_tlas_build
+  // raster fallback scratch (grown on demand)
+  rt::RasterScratch raster;
+  size_t raster_px_cap = 0, raster_prim_cap = 0;
 };
 
 namespace {
@@ -256,6 +259,9 @@ rt_status rt_destroy(rt_ctx_t c) {
   if (c->d_ovf) (void)hipFree(c->d_ovf);
   if (c->pool_nodes) (void)hipFree(c->pool_nodes);
   if (c->pool_tris) (void)hipFree(c->pool_tris);
+  for (void* p : {(void*)c->raster.vis, (void*)c->raster.clip, (void*)c->raster.slots, (void*)c->raster.tiles,
+                  (void*)c->raster.offs})
+    if (p) (void)hipFree(p);
   (void)hipStreamDestroy(c->stream);
   delete c;
   return RT_OK;
@@ -503,6 +509,7 @@ static rt::SceneView scene_view(rt_ctx* c) {
   sv.lds_cap = sv.stack_cap < rt::kLdsStackEntries ? sv.stack_cap : rt::kLdsStackEntries;
   sv.ovf = nullptr;
   sv.ovf_lanes = 0;
+  sv.cull_sense = 1.0f;
   return sv;
 }
 
@@ -520,6 +527,71 @@ static rt_status ensure_overflow(rt_ctx* c, rt::SceneView& sv, size_t lanes, hip
   }
   sv.ovf = c->d_ovf;
   sv.ovf_lanes = (uint32_t)lanes;
+  return RT_OK;
+}
+
+rt_status rt_raster_draw(rt_ctx_t c, const rt_blas_t* draws, uint32_t ndraws, const float* object_to_world,
+                         uint32_t W, uint32_t H, void* rgba8, float* depth32f, void* stream) {
+  if (!c) return RT_E_INVALID;
+  if (!draws || ndraws == 0 || ndraws > rt::kRasterMaxDraws)
+    return fail(c, RT_E_INVALID, "rt_raster_draw: 1..8 draws required");
+  if (!c->have_camera) return fail(c, RT_E_INVALID, "rt_raster_draw: camera not set");
+  if (W == 0 || H == 0 || W > 16384 || H > 16384 || !rgba8)
+    return fail(c, RT_E_INVALID, "rt_raster_draw: bad size or output");
+  rt::RasterDraws dr;
+  dr.n = ndraws;
+  uint64_t total = 0;
+  for (uint32_t d = 0; d < ndraws; ++d) {
+    if (draws[d] >= c->blas.size() || !c->blas[draws[d]].vtx) return fail(c, RT_E_INVALID, "rt_raster_draw: unknown BLAS");
+    const DeviceBlas& b = c->blas[draws[d]];
+    dr.first[d] = (uint32_t)total;
+    dr.nvtx[d] = b.nvtx;
+    dr.vtx[d] = b.vtx;
+    dr.idx[d] = b.idx;
+    total += b.ntri;
+  }
+  if (total * 7 >= 0xffffffffull) return fail(c, RT_E_UNSUPPORTED, "rt_raster_draw: too many triangles");
+  dr.total = (uint32_t)total;
+  rt::RasterView rv;
+  // objectToWorld as the instance properties buffer holds it (XMMATRIX memory, row-vector
+  // convention): memory row j = column j of the 3x4 column-vector transform
+  const float I[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+  const float* T = object_to_world ? object_to_world : I;
+  for (int j = 0; j < 4; ++j) {
+    for (int i = 0; i < 3; ++i) rv.o2w[j * 4 + i] = T[i * 4 + j];
+    rv.o2w[j * 4 + 3] = j == 3 ? 1.0f : 0.0f;
+  }
+  std::memcpy(rv.view, c->fp.cb, 16 * sizeof(float));
+  std::memcpy(rv.proj, c->fp.cb + 16, 16 * sizeof(float));
+  rv.width = W;
+  rv.height = H;
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  const size_t npx = (size_t)W * H;
+  if (c->raster_px_cap < npx || c->raster_prim_cap < total) {
+    (void)hipStreamSynchronize(s);
+    if (c->raster_px_cap < npx) {
+      if (c->raster.vis) (void)hipFree(c->raster.vis);
+      c->raster.vis = nullptr;
+      HIPCHK(c, hipMalloc(&c->raster.vis, npx * 8), "hipMalloc(raster vis)");
+      c->raster_px_cap = npx;
+    }
+    if (c->raster_prim_cap < total) {
+      for (void** p : {(void**)&c->raster.clip, (void**)&c->raster.slots, (void**)&c->raster.tiles,
+                       (void**)&c->raster.offs}) {
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+      }
+      const size_t n = (size_t)total;
+      HIPCHK(c, hipMalloc(&c->raster.clip, n * 3 * sizeof(float4)), "hipMalloc(raster clip)");
+      HIPCHK(c, hipMalloc(&c->raster.slots, n * 7 * sizeof(rt::RasterSlot)), "hipMalloc(raster slots)");
+      HIPCHK(c, hipMalloc(&c->raster.tiles, n * 7 * 4), "hipMalloc(raster tiles)");
+      HIPCHK(c, hipMalloc(&c->raster.offs, (n * 7 + 1) * 4), "hipMalloc(raster offs)");
+      c->raster_prim_cap = n;
+    }
+  }
+  hipError_t e = rt::launch_raster(dr, rv, c->raster, rgba8, depth32f, s);
+  if (e != hipSuccess) return hip_fail(c, e, "raster launch");
   return RT_OK;
 }
 
@@ -577,12 +649,17 @@ rt_status rt_dispatch_rays(rt_ctx_t c, uint32_t W, uint32_t H, const uint32_t* r
 rt_status rt_trace_rays(rt_ctx_t c, const float* rays, uint32_t n, uint32_t ray_flags, uint32_t* hits, float* uv,
                         void* stream) {
   if (!c || (!rays && n) || (!hits && n)) return fail(c, RT_E_INVALID, "rt_trace_rays: null argument");
-  if (ray_flags & ~(uint32_t)(RT_RAY_FLAG_ACCEPT_FIRST_HIT_AND_END_SEARCH | RT_RAY_FLAG_CULL_BACK_FACING_TRIANGLES))
+  if (ray_flags & ~(uint32_t)(RT_RAY_FLAG_ACCEPT_FIRST_HIT_AND_END_SEARCH | RT_RAY_FLAG_CULL_BACK_FACING_TRIANGLES |
+                              RT_RAY_FLAG_CULL_FRONT_FACING_TRIANGLES))
     return fail(c, RT_E_INVALID, "rt_trace_rays: unsupported ray flags");
+  const bool cull_back = (ray_flags & RT_RAY_FLAG_CULL_BACK_FACING_TRIANGLES) != 0;
+  const bool cull_front = (ray_flags & RT_RAY_FLAG_CULL_FRONT_FACING_TRIANGLES) != 0;
+  if (cull_back && cull_front) return fail(c, RT_E_INVALID, "rt_trace_rays: both cull flags set");
   if (!c->inst) return fail(c, RT_E_INVALID, "rt_trace_rays: no TLAS built");
   if (c->tlas_stale) return fail(c, RT_E_INVALID, "rt_trace_rays: BLAS rebuilt since the last rt_tlas_build");
   (void)hipSetDevice(c->device);
   rt::SceneView sv = scene_view(c);
+  sv.cull_sense = cull_front ? -1.0f : 1.0f;
   if (sv.stack_cap > rt::kMaxTraversalStack)
     return fail(c, RT_E_UNSUPPORTED, "rt_trace_rays: BVH too deep for the traversal stack");
   {
@@ -590,7 +667,7 @@ rt_status rt_trace_rays(rt_ctx_t c, const float* rays, uint32_t n, uint32_t ray_
     if (st != RT_OK) return st;
   }
   hipError_t e = rt::launch_trace_rays(sv, rays, n, (ray_flags & RT_RAY_FLAG_ACCEPT_FIRST_HIT_AND_END_SEARCH) != 0,
-                                       (ray_flags & RT_RAY_FLAG_CULL_BACK_FACING_TRIANGLES) != 0, hits, uv, c->d_stats,
+                                       cull_back || cull_front, hits, uv, c->d_stats,
                                        c->stats_on, pick_stream(c, stream));
   if (e != hipSuccess) return hip_fail(c, e, "trace_rays launch");
   return RT_OK;

@@ -142,6 +142,7 @@ struct SceneView {
   int lds_cap;         // entries kept in LDS ([entry][lane])
   int* ovf;            // HBM overflow area, [entry - lds_cap][global lane], or null
   uint32_t ovf_lanes;  // lanes of the launch (overflow row pitch)
+  float cull_sense;    // culling traces: +1 culls back faces, -1 front faces (DXR ray flags 0x10 / 0x20)
 };
 
 // ------------------------------------------------------------------------------------------

@@ -46,4 +46,42 @@ hipError_t launch_trace_rays(const SceneView& scene, const float* rays, uint32_t
 hipError_t launch_assemble_strips(uint32_t W, uint32_t H, uint32_t nranks, uint32_t strip_rows,
                                   const void* gathered, void* out, hipStream_t stream);
 
+// --- Raster fallback (rt_raster.hip) -------------------------------------------------------
+
+constexpr uint32_t kRasterMaxDraws = 8;
+constexpr unsigned long long kRasterClear = ~0ull;  // visibility word of an untouched pixel
+
+struct RasterDraws {  // draw list in submission order; primitive id = first[d] + local triangle
+  uint32_t n = 0, total = 0;
+  uint32_t first[kRasterMaxDraws] = {};
+  uint32_t nvtx[kRasterMaxDraws] = {};
+  const float* vtx[kRasterMaxDraws] = {};    // {pos, normal} x nvtx (the reference Vertex)
+  const uint32_t* idx[kRasterMaxDraws] = {};  // nullptr: non-indexed draw
+};
+
+struct RasterView {
+  float o2w[16];   // instance 0 objectToWorld, XMMATRIX memory (row-vector convention)
+  float view[16];  // camera buffer view (cb[0..15])
+  float proj[16];  // camera buffer projection (cb[16..31])
+  uint32_t width, height;
+};
+
+struct RasterSlot {  // one screen-space triangle after clipping (48 B)
+  int32_t x[3], y[3];  // 16.8 fixed point
+  float z[3];
+  uint32_t prim;
+  uint16_t tx0, ty0, tw, th;  // 8x8-pixel tile box
+};
+
+struct RasterScratch {
+  unsigned long long* vis = nullptr;  // W x H (depth bits << 32 | primitive)
+  float4* clip = nullptr;             // 3 clip-space vertices per primitive
+  RasterSlot* slots = nullptr;        // 7 per primitive
+  uint32_t* tiles = nullptr;          // tile count per slot
+  uint32_t* offs = nullptr;           // exclusive scan of tiles, + total
+};
+
+hipError_t launch_raster(const RasterDraws& dr, const RasterView& rv, const RasterScratch& s, void* rgba8,
+                         float* depth, hipStream_t stream);
+
 }  // namespace rt

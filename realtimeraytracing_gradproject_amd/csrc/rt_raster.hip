@@ -1,0 +1,296 @@
+// rt_raster.hip — raster fallback: the reference's abandoned rasterization pipeline
+// (shaders/shaders.hlsl:41-59 VSMain/PSMain; D3D12HelloTriangle.cpp:513-540 draw recording;
+// pipeline state :248-276) as a visibility-buffer rasterizer for gfx950.
+//
+//   1. k_raster_setup   one thread per triangle of every draw: VSMain (objectToWorld, view,
+//                       projection), clip to 0 <= z <= w and a guard band, viewport transform,
+//                       16.8 fixed-point snap, back-face cull (clockwise front), then up to 7 fan
+//                       triangles into fixed slots 7t..7t+6 with their 8x8-pixel tile counts.
+//   2. k_raster_scan    exclusive scan of the slot tile counts (one workgroup) + total.
+//   3. k_raster_tiles   one wave per (slot, 8x8 tile): edge functions with the top-left rule,
+//                       screen-linear depth, depth LESS as a 64-bit atomicMin of (depth, prim):
+//                       the smallest depth wins and equal depths keep the earliest primitive —
+//                       exactly in-order LESS testing, independent of execution order.
+//   4. k_raster_resolve one thread per pixel: PSMain's interpolated COLOR (perspective-correct
+//                       barycentrics of the original triangle) -> RGBA8, or the clear colour.
+//
+// COLOR is read as the reference's input layout reads it (R32G32B32A32_FLOAT at byte 12 of a
+// 24-byte Vertex, :253-257): the normal plus the next vertex's position.x; the element of the
+// last vertex runs past the buffer and reads as 0 in every component (pinned: D3D returns 0 for
+// an out-of-bounds input-assembler fetch).
+#include "rt_internal.hpp"
+
+namespace rt {
+
+namespace {
+
+constexpr float kGuard = 4.0f;  // |x|, |y| <= kGuard * w: keeps 16.8 screen coordinates in int32
+
+struct ClipV {
+  float x, y, z, w;
+};
+
+__device__ inline float plane_dist(const ClipV& v, int p) {
+  switch (p) {
+    case 0: return v.z;                   // near: z >= 0
+    case 1: return v.w - v.z;             // far:  z <= w
+    case 2: return v.x + kGuard * v.w;    // guard band
+    case 3: return kGuard * v.w - v.x;
+    case 4: return v.y + kGuard * v.w;
+    default: return kGuard * v.w - v.y;
+  }
+}
+
+// Point where the edge from the inside vertex a to the outside vertex b meets the plane.
+__device__ inline ClipV clip_lerp(const ClipV& a, float da, const ClipV& b, float db) {
+  const float t = da / (da - db);
+  return {a.x + t * (b.x - a.x), a.y + t * (b.y - a.y), a.z + t * (b.z - a.z), a.w + t * (b.w - a.w)};
+}
+
+__device__ inline int64_t floor_div(int64_t a, int64_t b) {  // b > 0
+  const int64_t q = a / b;
+  return (a % b != 0 && a < 0) ? q - 1 : q;
+}
+
+__device__ inline void clip_of_vertex(const float* vtx, uint32_t v, const float* o2w_mem, const float* view,
+                                      const float* proj, ClipV& out) {
+  const float p[4] = {vtx[v * 6 + 0], vtx[v * 6 + 1], vtx[v * 6 + 2], 1.0f};  // POSITION, w = 1
+  float wpos[4], vpos[4], c[4];
+  hlsl_mul4(o2w_mem, p, wpos);  // mul(instanceProps[0].objectToWorld, position)
+  hlsl_mul4(view, wpos, vpos);  // mul(view, pos)
+  hlsl_mul4(proj, vpos, c);     // mul(projection, pos)
+  out = {c[0], c[1], c[2], c[3]};
+}
+
+__global__ __launch_bounds__(256) void k_raster_setup(RasterDraws dr, RasterView rv, float4* __restrict__ clip,
+                                                      RasterSlot* __restrict__ slots,
+                                                      uint32_t* __restrict__ tiles) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= dr.total) return;
+  uint32_t d = 0;
+  while (d + 1 < dr.n && t >= dr.first[d + 1]) ++d;
+  const uint32_t lt = t - dr.first[d];
+  const float* vtx = dr.vtx[d];
+  uint32_t vi[3];
+  for (int k = 0; k < 3; ++k) vi[k] = dr.idx[d] ? dr.idx[d][lt * 3 + k] : lt * 3 + k;
+  ClipV v[3];
+  for (int k = 0; k < 3; ++k) {
+    clip_of_vertex(vtx, vi[k], rv.o2w, rv.view, rv.proj, v[k]);
+    clip[(size_t)t * 3 + k] = make_float4(v[k].x, v[k].y, v[k].z, v[k].w);
+  }
+  // Sutherland-Hodgman against the 6 planes (at most 9 vertices)
+  ClipV poly[9], tmp[9];
+  int n = 3;
+  for (int k = 0; k < 3; ++k) poly[k] = v[k];
+  for (int p = 0; p < 6 && n > 0; ++p) {
+    bool all_in = true;
+    for (int k = 0; k < n; ++k) all_in = all_in && plane_dist(poly[k], p) >= 0.0f;
+    if (all_in) continue;
+    int m = 0;
+    for (int k = 0; k < n; ++k) {
+      const ClipV& a = poly[k];
+      const ClipV& b = poly[(k + 1) % n];
+      const float da = plane_dist(a, p), db = plane_dist(b, p);
+      if (da >= 0.0f) tmp[m++] = a;
+      if ((da >= 0.0f) != (db >= 0.0f)) tmp[m++] = da >= 0.0f ? clip_lerp(a, da, b, db) : clip_lerp(b, db, a, da);
+    }
+    n = m;
+    for (int k = 0; k < n; ++k) poly[k] = tmp[k];
+  }
+  int32_t X[9], Y[9];
+  float Z[9];
+  bool ok = n >= 3;
+  for (int k = 0; k < n && ok; ++k) {
+    if (!(poly[k].w > 0.0f)) {
+      ok = false;
+      break;
+    }
+    // viewport (0, 0, W, H, 0, 1): X = (x/w + 1) W/2, Y = (1 - y/w) H/2, depth = z/w
+    const float sx = (poly[k].x / poly[k].w + 1.0f) * (0.5f * (float)rv.width);
+    const float sy = (1.0f - poly[k].y / poly[k].w) * (0.5f * (float)rv.height);
+    X[k] = (int32_t)rintf(sx * 256.0f);
+    Y[k] = (int32_t)rintf(sy * 256.0f);
+    Z[k] = poly[k].z / poly[k].w + 0.0f;
+  }
+  for (int s = 0; s < 7; ++s) {
+    const size_t slot = (size_t)t * 7 + s;
+    uint32_t cnt = 0;
+    RasterSlot r{};
+    if (ok && s + 2 < n) {
+      const int a = 0, b = s + 1, c = s + 2;  // fan from vertex 0
+      const int64_t area = (int64_t)(X[b] - X[a]) * (Y[c] - Y[a]) - (int64_t)(Y[b] - Y[a]) * (X[c] - X[a]);
+      if (area > 0) {  // clockwise on screen (y down) = front face; back faces and slivers culled
+        const int32_t xmin = min(X[a], min(X[b], X[c])), xmax = max(X[a], max(X[b], X[c]));
+        const int32_t ymin = min(Y[a], min(Y[b], Y[c])), ymax = max(Y[a], max(Y[b], Y[c]));
+        // pixels whose centre (256 px + 128) can lie inside
+        int64_t px0 = -floor_div(-(int64_t)xmin + 128, 256), px1 = floor_div((int64_t)xmax - 128, 256);
+        int64_t py0 = -floor_div(-(int64_t)ymin + 128, 256), py1 = floor_div((int64_t)ymax - 128, 256);
+        px0 = px0 < 0 ? 0 : px0;
+        py0 = py0 < 0 ? 0 : py0;
+        px1 = px1 > (int64_t)rv.width - 1 ? (int64_t)rv.width - 1 : px1;
+        py1 = py1 > (int64_t)rv.height - 1 ? (int64_t)rv.height - 1 : py1;
+        if (px0 <= px1 && py0 <= py1) {
+          r.x[0] = X[a], r.x[1] = X[b], r.x[2] = X[c];
+          r.y[0] = Y[a], r.y[1] = Y[b], r.y[2] = Y[c];
+          r.z[0] = Z[a], r.z[1] = Z[b], r.z[2] = Z[c];
+          r.prim = t;
+          r.tx0 = (uint16_t)(px0 >> 3);
+          r.ty0 = (uint16_t)(py0 >> 3);
+          r.tw = (uint16_t)((px1 >> 3) - (px0 >> 3) + 1);
+          r.th = (uint16_t)((py1 >> 3) - (py0 >> 3) + 1);
+          cnt = (uint32_t)r.tw * r.th;
+        }
+      }
+    }
+    slots[slot] = r;
+    tiles[slot] = cnt;
+  }
+}
+
+// Exclusive scan of n counts into offs[0..n], offs[n] = total. One 1024-thread workgroup, each
+// thread owning a contiguous chunk.
+__global__ __launch_bounds__(1024) void k_raster_scan(const uint32_t* __restrict__ cnt, uint32_t n,
+                                                      uint32_t* __restrict__ offs) {
+  __shared__ uint32_t part[1024];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t chunk = (n + 1023u) / 1024u;
+  const uint32_t b = min(n, tid * chunk), e = min(n, b + chunk);
+  uint32_t s = 0;
+  for (uint32_t i = b; i < e; ++i) s += cnt[i];
+  part[tid] = s;
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024u; off <<= 1) {
+    const uint32_t add = tid >= off ? part[tid - off] : 0u;
+    __syncthreads();
+    part[tid] += add;
+    __syncthreads();
+  }
+  uint32_t run = part[tid] - s;
+  for (uint32_t i = b; i < e; ++i) {
+    offs[i] = run;
+    run += cnt[i];
+  }
+  if (tid == 1023u) offs[n] = part[1023];
+}
+
+// One wave per (slot, tile); each wave takes a contiguous range of the tile list.
+__global__ __launch_bounds__(256) void k_raster_tiles(const RasterSlot* __restrict__ slots,
+                                                      const uint32_t* __restrict__ offs, uint32_t nslots,
+                                                      uint32_t width, uint32_t height,
+                                                      unsigned long long* __restrict__ vis) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+  const uint32_t total = offs[nslots];
+  const uint32_t per = (total + nwaves - 1) / nwaves;
+  const uint32_t t0 = wave * per, t1 = min(total, t0 + per);
+  if (t0 >= t1) return;
+  // last slot with offs[s] <= t0 (and a nonzero count, skipped below)
+  uint32_t lo = 0, hi = nslots;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (offs[mid] <= t0) lo = mid;
+    else hi = mid;
+  }
+  uint32_t s = lo;
+  for (uint32_t t = t0; t < t1; ++t) {
+    while (offs[s + 1] <= t) ++s;
+    const RasterSlot r = slots[s];
+    const uint32_t k = t - offs[s];
+    const uint32_t tx = r.tx0 + k % r.tw, ty = r.ty0 + k / r.tw;
+    const uint32_t x = tx * 8u + (lane & 7u), y = ty * 8u + (lane >> 3);
+    if (x >= width || y >= height) continue;
+    const int64_t px = (int64_t)x * 256 + 128, py = (int64_t)y * 256 + 128;
+    int64_t e[3];
+    bool in = true;
+    for (int i = 0; i < 3; ++i) {  // E_i: edge from vertex i+1 to i+2 (opposite vertex i)
+      const int a = (i + 1) % 3, b = (i + 2) % 3;
+      const int64_t dx = (int64_t)r.x[b] - r.x[a], dy = (int64_t)r.y[b] - r.y[a];
+      e[i] = dx * (py - r.y[a]) - dy * (px - r.x[a]);
+      const bool top_left = dy < 0 || (dy == 0 && dx > 0);
+      in = in && (e[i] > 0 || (e[i] == 0 && top_left));
+    }
+    if (!in) continue;
+    const double area = (double)(e[0] + e[1] + e[2]);
+    const double b1 = (double)e[1] / area, b2 = (double)e[2] / area;
+    float z = (float)((double)r.z[0] + b1 * ((double)r.z[1] - (double)r.z[0]) +
+                      b2 * ((double)r.z[2] - (double)r.z[0]));
+    z = z < 0.0f ? 0.0f : z;  // viewport depth range [0, 1]
+    if (!(z < 1.0f)) continue;  // LESS against the 1.0 clear
+    const unsigned long long key =
+        ((unsigned long long)__builtin_bit_cast(uint32_t, z + 0.0f) << 32) | (unsigned long long)r.prim;
+    unsigned long long* dst = vis + (size_t)y * width + x;
+    if (key < *dst) atomicMin(dst, key);
+  }
+}
+
+__device__ inline uint32_t raster_unorm8(float c) {  // saturate + round, as the RT path's output
+  return unorm8(c);
+}
+
+__global__ __launch_bounds__(256) void k_raster_resolve(RasterDraws dr, const float4* __restrict__ clip,
+                                                        const unsigned long long* __restrict__ vis,
+                                                        uint32_t width, uint32_t height,
+                                                        uint32_t* __restrict__ rgba8, float* __restrict__ depth) {
+  const uint32_t x = blockIdx.x * 16u + (threadIdx.x & 15u), y = blockIdx.y * 16u + (threadIdx.x >> 4);
+  if (x >= width || y >= height) return;
+  const size_t o = (size_t)y * width + x;
+  const unsigned long long v = vis[o];
+  if (v == kRasterClear) {
+    // ClearRenderTargetView {0.03, 0.35, 0.43, 1} (:529), depth 1.0 (:516)
+    rgba8[o] = unorm8(0.03f) | (unorm8(0.35f) << 8) | (unorm8(0.43f) << 16) | (unorm8(1.0f) << 24);
+    if (depth) depth[o] = 1.0f;
+    return;
+  }
+  const uint32_t t = (uint32_t)(v & 0xffffffffu);
+  uint32_t d = 0;
+  while (d + 1 < dr.n && t >= dr.first[d + 1]) ++d;
+  const uint32_t lt = t - dr.first[d];
+  const float* vtx = dr.vtx[d];
+  float col[3][4];
+  for (int k = 0; k < 3; ++k) {
+    const uint32_t vi = dr.idx[d] ? dr.idx[d][lt * 3 + k] : lt * 3 + k;
+    const bool inside = vi + 1 < dr.nvtx[d];
+    col[k][0] = inside ? vtx[vi * 6 + 3] : 0.0f;
+    col[k][1] = inside ? vtx[vi * 6 + 4] : 0.0f;
+    col[k][2] = inside ? vtx[vi * 6 + 5] : 0.0f;
+    col[k][3] = inside ? vtx[(vi + 1) * 6 + 0] : 0.0f;
+  }
+  const float4 c0 = clip[(size_t)t * 3 + 0], c1 = clip[(size_t)t * 3 + 1], c2 = clip[(size_t)t * 3 + 2];
+  // perspective-correct barycentrics of the pixel centre from the homogeneous (x, y, w) vertices
+  const float qx = (((float)x + 0.5f) / (float)width) * 2.0f - 1.0f;
+  const float qy = 1.0f - (((float)y + 0.5f) / (float)height) * 2.0f;
+  const V3 h0 = v3(c0.x, c0.y, c0.w), h1 = v3(c1.x, c1.y, c1.w), h2 = v3(c2.x, c2.y, c2.w);
+  const V3 q = v3(qx, qy, 1.0f);
+  const float f0 = dot(cross(h1, h2), q), f1 = dot(cross(h2, h0), q), f2 = dot(cross(h0, h1), q);
+  const float sum = (f0 + f1) + f2;
+  const float b0 = f0 / sum, b1 = f1 / sum, b2 = f2 / sum;
+  float out[4];
+  for (int ch = 0; ch < 4; ++ch) out[ch] = (b0 * col[0][ch] + b1 * col[1][ch]) + b2 * col[2][ch];
+  rgba8[o] = raster_unorm8(out[0]) | (raster_unorm8(out[1]) << 8) | (raster_unorm8(out[2]) << 16) |
+             (raster_unorm8(out[3]) << 24);
+  if (depth) depth[o] = __builtin_bit_cast(float, (uint32_t)(v >> 32));
+}
+
+}  // namespace
+
+hipError_t launch_raster(const RasterDraws& dr, const RasterView& rv, const RasterScratch& s, void* rgba8,
+                         float* depth, hipStream_t stream) {
+  const size_t npx = (size_t)rv.width * rv.height;
+  const uint32_t nslots = dr.total * 7u;
+  hipError_t e = hipMemsetD32Async((hipDeviceptr_t)s.vis, 0xffffffffu, npx * 2, stream);
+  if (e != hipSuccess) return e;
+  if (dr.total) {
+    k_raster_setup<<<(dr.total + 255) / 256, 256, 0, stream>>>(dr, rv, s.clip, s.slots, s.tiles);
+    k_raster_scan<<<1, 1024, 0, stream>>>(s.tiles, nslots, s.offs);
+    int dev = 0, ncu = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    k_raster_tiles<<<ncu * 8, 256, 0, stream>>>(s.slots, s.offs, nslots, rv.width, rv.height, s.vis);
+  }
+  dim3 g((rv.width + 15) / 16, (rv.height + 15) / 16);
+  k_raster_resolve<<<g, 256, 0, stream>>>(dr, s.clip, s.vis, rv.width, rv.height, (uint32_t*)rgba8, depth);
+  return hipGetLastError();
+}
+
+}  // namespace rt

@@ -199,7 +199,7 @@ __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, H
         rinvd = v3(safe_inv(rd.x), safe_inv(rd.y), safe_inv(rd.z));
         rnoinv = neg(mul(ro, rinvd));
         oct = octant(rinvd);
-        if (CULL) face = ir->flip ? -1.0f : 1.0f;
+        if (CULL) face = (ir->flip ? -1.0f : 1.0f) * sc.cull_sense;
         in_blas = true;
         ref = (int)ir->pool_root;
         continue;
@@ -495,7 +495,7 @@ __device__ void trace_packet(const SceneView& sc, const V3* o, const V3* d, floa
         b.invd[r] = v3(safe_inv(b.d[r].x), safe_inv(b.d[r].y), safe_inv(b.d[r].z));
         b.noinv[r] = neg(mul(b.o[r], b.invd[r]));
       }
-      const float face = CULL ? (ir.flip ? -1.0f : 1.0f) : 0.0f;
+      const float face = CULL ? (ir.flip ? -1.0f : 1.0f) * sc.cull_sense : 0.0f;
       const int base = sp;
       int bref = (int)ir.pool_root;
       while (true) {
