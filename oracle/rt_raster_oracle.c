@@ -7,8 +7,8 @@
  * :1340-1360) under the Direct3D rasterization rules, processed the way the API defines them:
  * draw after draw, triangle after triangle, every covered pixel depth-tested LESS against a D32
  * buffer cleared to 1.0 and written in submission order. (The device reaches the same image
- * order-independently with a 64-bit atomicMin of (depth, primitive); this in-order form is what
- * proves that equivalence.)
+ * order-independently — per-pixel minimum of (depth, primitive) over tile bins filled in arbitrary
+ * order; this in-order form is what proves that equivalence.)
  *
  * Pinned rules: clip 0 <= z <= w plus a |x|,|y| <= 4w guard band (Sutherland-Hodgman,
  * the inside vertex as the interpolation origin), viewport X = (x/w + 1) W/2, Y = (1 - y/w) H/2,
@@ -19,7 +19,8 @@
  * vertex's position.x, all zero for the last vertex (out-of-bounds fetch).
  *
  * Parity unpinned against reference execution (D3D12 only): restated from the source text and
- * the D3D rules; cross-checked in tests against the ray tracer's back-face-culled primary hits.
+ * the D3D rules; cross-checked in tests against the ray tracer's primary hits traced with
+ * RAY_FLAG_CULL_FRONT_FACING_TRIANGLES (tests/test_raster.py).
  */
 #include <math.h>
 #include <stdint.h>
@@ -169,9 +170,10 @@ int oracle_raster(const float* const* vtx6, const uint32_t* nvtx, const uint32_t
               if (!(e[i] > 0 || (e[i] == 0 && top_left))) covered = 0;
             }
             if (!covered) continue;
+            /* depth linear in screen space: z0 + (E1 (z1 - z0) + E2 (z2 - z0)) / area, in double */
             const double A = (double)(e[0] + e[1] + e[2]);
-            const double w1 = (double)e[1] / A, w2 = (double)e[2] / A;
-            float z = (float)((double)tz[0] + w1 * ((double)tz[1] - (double)tz[0]) + w2 * ((double)tz[2] - (double)tz[0]));
+            const double dz = ((double)e[1] * ((double)tz[1] - (double)tz[0]) + (double)e[2] * ((double)tz[2] - (double)tz[0])) / A;
+            float z = (float)((double)tz[0] + dz);
             if (z < 0.0f) z = 0.0f;
             const size_t o = (size_t)py * W + (size_t)px;
             if (z < depth[o]) { /* DepthFunc LESS, in submission order */

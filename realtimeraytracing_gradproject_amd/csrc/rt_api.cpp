@@ -69,7 +69,7 @@ struct rt_ctx {
   bool tlas_stale = false;  // a BLAS was rebuilt after the last rt_tlas_build
   // raster fallback scratch (grown on demand)
   rt::RasterScratch raster;
-  size_t raster_px_cap = 0, raster_prim_cap = 0;
+  size_t raster_tile_cap = 0, raster_prim_cap = 0, raster_bin_cap = 0;
 };
 
 namespace {
@@ -259,8 +259,8 @@ rt_status rt_destroy(rt_ctx_t c) {
   if (c->d_ovf) (void)hipFree(c->d_ovf);
   if (c->pool_nodes) (void)hipFree(c->pool_nodes);
   if (c->pool_tris) (void)hipFree(c->pool_tris);
-  for (void* p : {(void*)c->raster.vis, (void*)c->raster.clip, (void*)c->raster.slots, (void*)c->raster.tiles,
-                  (void*)c->raster.offs})
+  for (void* p : {(void*)c->raster.clip, (void*)c->raster.slots, (void*)c->raster.tiles, (void*)c->raster.tcount,
+                  (void*)c->raster.toffs, (void*)c->raster.bins})
     if (p) (void)hipFree(p);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -567,30 +567,42 @@ rt_status rt_raster_draw(rt_ctx_t c, const rt_blas_t* draws, uint32_t ndraws, co
   rv.height = H;
   (void)hipSetDevice(c->device);
   hipStream_t s = pick_stream(c, stream);
-  const size_t npx = (size_t)W * H;
-  if (c->raster_px_cap < npx || c->raster_prim_cap < total) {
+  const size_t ntiles = (size_t)((W + 7) / 8) * ((H + 7) / 8);
+  auto regrow = [&](void** p, size_t bytes, const char* what) -> rt_status {
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    HIPCHK(c, hipMalloc(p, bytes), what);
+    return RT_OK;
+  };
+  rt_status st = RT_OK;
+  if (c->raster_tile_cap < ntiles || c->raster_prim_cap < total) {
     (void)hipStreamSynchronize(s);
-    if (c->raster_px_cap < npx) {
-      if (c->raster.vis) (void)hipFree(c->raster.vis);
-      c->raster.vis = nullptr;
-      HIPCHK(c, hipMalloc(&c->raster.vis, npx * 8), "hipMalloc(raster vis)");
-      c->raster_px_cap = npx;
+    if (c->raster_tile_cap < ntiles) {
+      if ((st = regrow((void**)&c->raster.tcount, ntiles * 4, "hipMalloc(raster tile counts)")) != RT_OK) return st;
+      if ((st = regrow((void**)&c->raster.toffs, (ntiles + 1) * 4, "hipMalloc(raster tile offsets)")) != RT_OK) return st;
+      c->raster_tile_cap = ntiles;
     }
     if (c->raster_prim_cap < total) {
-      for (void** p : {(void**)&c->raster.clip, (void**)&c->raster.slots, (void**)&c->raster.tiles,
-                       (void**)&c->raster.offs}) {
-        if (*p) (void)hipFree(*p);
-        *p = nullptr;
-      }
       const size_t n = (size_t)total;
-      HIPCHK(c, hipMalloc(&c->raster.clip, n * 3 * sizeof(float4)), "hipMalloc(raster clip)");
-      HIPCHK(c, hipMalloc(&c->raster.slots, n * 7 * sizeof(rt::RasterSlot)), "hipMalloc(raster slots)");
-      HIPCHK(c, hipMalloc(&c->raster.tiles, n * 7 * 4), "hipMalloc(raster tiles)");
-      HIPCHK(c, hipMalloc(&c->raster.offs, (n * 7 + 1) * 4), "hipMalloc(raster offs)");
+      if ((st = regrow((void**)&c->raster.clip, n * 3 * sizeof(float4), "hipMalloc(raster clip)")) != RT_OK) return st;
+      if ((st = regrow((void**)&c->raster.slots, n * 7 * sizeof(rt::RasterSlot), "hipMalloc(raster slots)")) != RT_OK)
+        return st;
+      if ((st = regrow((void**)&c->raster.tiles, n * 7 * 4, "hipMalloc(raster slot tiles)")) != RT_OK) return st;
       c->raster_prim_cap = n;
     }
   }
-  hipError_t e = rt::launch_raster(dr, rv, c->raster, rgba8, depth32f, s);
+  hipError_t e = rt::launch_raster_bin(dr, rv, c->raster, s);
+  if (e != hipSuccess) return hip_fail(c, e, "raster bin launch");
+  // the bin total sizes the bin array: one 4-byte read-back per draw
+  uint32_t nbins = 0;
+  HIPCHK(c, hipMemcpyAsync(&nbins, c->raster.toffs + ntiles, 4, hipMemcpyDeviceToHost, s), "raster bin count");
+  HIPCHK(c, hipStreamSynchronize(s), "raster bin count");
+  if (c->raster_bin_cap < nbins) {
+    const size_t cap = (size_t)nbins + nbins / 2;
+    if ((st = regrow((void**)&c->raster.bins, cap * 4, "hipMalloc(raster bins)")) != RT_OK) return st;
+    c->raster_bin_cap = cap;
+  }
+  e = rt::launch_raster_draw(dr, rv, c->raster, rgba8, depth32f, s);
   if (e != hipSuccess) return hip_fail(c, e, "raster launch");
   return RT_OK;
 }

@@ -49,7 +49,7 @@ hipError_t launch_assemble_strips(uint32_t W, uint32_t H, uint32_t nranks, uint3
 // --- Raster fallback (rt_raster.hip) -------------------------------------------------------
 
 constexpr uint32_t kRasterMaxDraws = 8;
-constexpr unsigned long long kRasterClear = ~0ull;  // visibility word of an untouched pixel
+constexpr unsigned long long kRasterClear = ~0ull;  // (depth, primitive) of an untouched pixel
 
 struct RasterDraws {  // draw list in submission order; primitive id = first[d] + local triangle
   uint32_t n = 0, total = 0;
@@ -74,14 +74,19 @@ struct RasterSlot {  // one screen-space triangle after clipping (48 B)
 };
 
 struct RasterScratch {
-  unsigned long long* vis = nullptr;  // W x H (depth bits << 32 | primitive)
-  float4* clip = nullptr;             // 3 clip-space vertices per primitive
-  RasterSlot* slots = nullptr;        // 7 per primitive
-  uint32_t* tiles = nullptr;          // tile count per slot
-  uint32_t* offs = nullptr;           // exclusive scan of tiles, + total
+  float4* clip = nullptr;       // 3 clip-space vertices per primitive
+  RasterSlot* slots = nullptr;  // 7 per primitive
+  uint32_t* tiles = nullptr;    // tile-box size per slot
+  uint32_t* tcount = nullptr;   // per screen tile: binned triangles (then the append cursor)
+  uint32_t* toffs = nullptr;    // exclusive scan of tcount, + total (screen tiles + 1)
+  uint32_t* bins = nullptr;     // slot ids grouped by screen tile
 };
 
-hipError_t launch_raster(const RasterDraws& dr, const RasterView& rv, const RasterScratch& s, void* rgba8,
-                         float* depth, hipStream_t stream);
+// Phase 1: vertex stage, clipping, setup and bin counting; toffs[ntiles] = number of bin entries
+// (the caller reads it to size `bins`). Phase 2: bin fill + per-tile raster and shading.
+hipError_t launch_raster_bin(const RasterDraws& dr, const RasterView& rv, const RasterScratch& s,
+                             hipStream_t stream);
+hipError_t launch_raster_draw(const RasterDraws& dr, const RasterView& rv, const RasterScratch& s, void* rgba8,
+                              float* depth, hipStream_t stream);
 
 }  // namespace rt

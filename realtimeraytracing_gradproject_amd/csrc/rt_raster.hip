@@ -1,18 +1,22 @@
 // rt_raster.hip — raster fallback: the reference's abandoned rasterization pipeline
 // (shaders/shaders.hlsl:41-59 VSMain/PSMain; D3D12HelloTriangle.cpp:513-540 draw recording;
-// pipeline state :248-276) as a visibility-buffer rasterizer for gfx950.
+// pipeline state :248-276) as a tile-binned rasterizer for gfx950.
 //
 //   1. k_raster_setup   one thread per triangle of every draw: VSMain (objectToWorld, view,
 //                       projection), clip to 0 <= z <= w and a guard band, viewport transform,
 //                       16.8 fixed-point snap, back-face cull (clockwise front), then up to 7 fan
 //                       triangles into fixed slots 7t..7t+6 with their 8x8-pixel tile counts.
-//   2. k_raster_scan    exclusive scan of the slot tile counts (one workgroup) + total.
-//   3. k_raster_tiles   one wave per (slot, 8x8 tile): edge functions with the top-left rule,
-//                       screen-linear depth, depth LESS as a 64-bit atomicMin of (depth, prim):
-//                       the smallest depth wins and equal depths keep the earliest primitive —
-//                       exactly in-order LESS testing, independent of execution order.
-//   4. k_raster_resolve one thread per pixel: PSMain's interpolated COLOR (perspective-correct
-//                       barycentrics of the original triangle) -> RGBA8, or the clear colour.
+//   2. k_raster_bin<0> one wave per slot: count the 8x8 screen tiles each triangle overlaps;
+//      k_raster_scan   exclusive scan of the per-tile counts -> bin offsets (the host reads the
+//                      total once to size the bins);
+//      k_raster_bin<1> the same walk, appending the slot to each overlapped tile's bin.
+//   3. k_raster_tile   one wave per screen tile, the tile's depth buffer in registers: for every
+//                      binned triangle, edge functions with the top-left rule and screen-linear
+//                      depth; the per-pixel minimum of (depth, primitive) is exactly in-order LESS
+//                      testing (smallest depth, earliest primitive on ties) whatever the bin
+//                      order. Then PSMain's interpolated COLOR (perspective-correct barycentrics
+//                      of the original triangle) -> RGBA8 and depth, written once. No global
+//                      atomics in the depth test.
 //
 // COLOR is read as the reference's input layout reads it (R32G32B32A32_FLOAT at byte 12 of a
 // 24-byte Vertex, :253-257): the normal plus the next vertex's position.x; the element of the
@@ -173,76 +177,95 @@ __global__ __launch_bounds__(1024) void k_raster_scan(const uint32_t* __restrict
   if (tid == 1023u) offs[n] = part[1023];
 }
 
-// One wave per (slot, tile); each wave takes a contiguous range of the tile list.
-__global__ __launch_bounds__(256) void k_raster_tiles(const RasterSlot* __restrict__ slots,
-                                                      const uint32_t* __restrict__ offs, uint32_t nslots,
-                                                      uint32_t width, uint32_t height,
-                                                      unsigned long long* __restrict__ vis) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-  const uint32_t total = offs[nslots];
-  const uint32_t per = (total + nwaves - 1) / nwaves;
-  const uint32_t t0 = wave * per, t1 = min(total, t0 + per);
-  if (t0 >= t1) return;
-  // last slot with offs[s] <= t0 (and a nonzero count, skipped below)
-  uint32_t lo = 0, hi = nslots;
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (offs[mid] <= t0) lo = mid;
-    else hi = mid;
+// Triangle-vs-tile test: false when the 8x8 tile's pixel centres all lie strictly outside one
+// edge (E < 0 at the corner centre that maximises E). Conservative with respect to the fill rule.
+__device__ inline bool tile_overlaps(const RasterSlot& r, uint32_t tx, uint32_t ty) {
+  const int64_t x0 = (int64_t)tx * 2048 + 128, y0 = (int64_t)ty * 2048 + 128;
+  for (int i = 0; i < 3; ++i) {
+    const int a = (i + 1) % 3, b = (i + 2) % 3;
+    const int64_t dx = (int64_t)r.x[b] - r.x[a], dy = (int64_t)r.y[b] - r.y[a];
+    // E = dx (py - ya) - dy (px - xa): largest at py = max if dx > 0, px = max if dy < 0
+    const int64_t py = dx > 0 ? y0 + 7 * 256 : y0, px = dy < 0 ? x0 + 7 * 256 : x0;
+    if (dx * (py - r.y[a]) - dy * (px - r.x[a]) < 0) return false;
   }
-  uint32_t s = lo;
-  for (uint32_t t = t0; t < t1; ++t) {
-    while (offs[s + 1] <= t) ++s;
-    const RasterSlot r = slots[s];
-    const uint32_t k = t - offs[s];
+  return true;
+}
+
+// Binning: one wave per slot, lanes striding over the slot's tile box. PASS 0 counts the
+// overlapping (slot, tile) pairs per screen tile, PASS 1 appends the slot to the tile's bin
+// (order inside a bin is arbitrary: the per-pixel minimum below does not depend on it).
+template <int PASS>
+__global__ __launch_bounds__(256) void k_raster_bin(const RasterSlot* __restrict__ slots,
+                                                    const uint32_t* __restrict__ slot_tiles, uint32_t nslots,
+                                                    uint32_t tiles_x, uint32_t* __restrict__ tcount,
+                                                    const uint32_t* __restrict__ toffs, uint32_t* __restrict__ bins) {
+  const uint32_t s = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (s >= nslots) return;
+  const uint32_t n = slot_tiles[s];
+  if (n == 0) return;
+  const RasterSlot r = slots[s];
+  for (uint32_t k = threadIdx.x & 63u; k < n; k += 64u) {
     const uint32_t tx = r.tx0 + k % r.tw, ty = r.ty0 + k / r.tw;
-    const uint32_t x = tx * 8u + (lane & 7u), y = ty * 8u + (lane >> 3);
-    if (x >= width || y >= height) continue;
-    const int64_t px = (int64_t)x * 256 + 128, py = (int64_t)y * 256 + 128;
+    if (!tile_overlaps(r, tx, ty)) continue;
+    const uint32_t tile = ty * tiles_x + tx;
+    if (PASS == 0) {
+      atomicAdd(&tcount[tile], 1u);
+    } else {
+      bins[toffs[tile] + atomicAdd(&tcount[tile], 1u)] = s;
+    }
+  }
+}
+
+// One wave per 8x8 screen tile: every binned triangle is tested against the wave's 64 pixels
+// (edge functions, top-left rule, screen-linear depth); the per-pixel minimum of
+// (depth bits << 32 | primitive) is exactly in-order LESS testing. The winning primitive is then
+// shaded (PSMain: interpolated COLOR) and written once.
+__global__ __launch_bounds__(256) void k_raster_tile(RasterDraws dr, const float4* __restrict__ clip,
+                                                     const RasterSlot* __restrict__ slots,
+                                                     const uint32_t* __restrict__ toffs,
+                                                     const uint32_t* __restrict__ bins, uint32_t tiles_x,
+                                                     uint32_t ntiles, uint32_t width, uint32_t height,
+                                                     uint32_t* __restrict__ rgba8, float* __restrict__ depth) {
+  const uint32_t tile = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (tile >= ntiles) return;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t x = (tile % tiles_x) * 8u + (lane & 7u), y = (tile / tiles_x) * 8u + (lane >> 3);
+  const int64_t px = (int64_t)x * 256 + 128, py = (int64_t)y * 256 + 128;
+  unsigned long long best = kRasterClear;
+  const uint32_t b0 = toffs[tile], b1 = toffs[tile + 1];
+  for (uint32_t b = b0; b < b1; ++b) {
+    const uint32_t s = __builtin_amdgcn_readfirstlane(bins[b]);
+    const RasterSlot r = slots[s];
     int64_t e[3];
     bool in = true;
     for (int i = 0; i < 3; ++i) {  // E_i: edge from vertex i+1 to i+2 (opposite vertex i)
-      const int a = (i + 1) % 3, b = (i + 2) % 3;
-      const int64_t dx = (int64_t)r.x[b] - r.x[a], dy = (int64_t)r.y[b] - r.y[a];
+      const int a = (i + 1) % 3, c = (i + 2) % 3;
+      const int64_t dx = (int64_t)r.x[c] - r.x[a], dy = (int64_t)r.y[c] - r.y[a];
       e[i] = dx * (py - r.y[a]) - dy * (px - r.x[a]);
       const bool top_left = dy < 0 || (dy == 0 && dx > 0);
       in = in && (e[i] > 0 || (e[i] == 0 && top_left));
     }
     if (!in) continue;
+    // depth, linear in screen space: z0 + (E1 (z1 - z0) + E2 (z2 - z0)) / area, in double
     const double area = (double)(e[0] + e[1] + e[2]);
-    const double b1 = (double)e[1] / area, b2 = (double)e[2] / area;
-    float z = (float)((double)r.z[0] + b1 * ((double)r.z[1] - (double)r.z[0]) +
-                      b2 * ((double)r.z[2] - (double)r.z[0]));
+    const double dz = ((double)e[1] * ((double)r.z[1] - (double)r.z[0]) +
+                       (double)e[2] * ((double)r.z[2] - (double)r.z[0])) / area;
+    float z = (float)((double)r.z[0] + dz);
     z = z < 0.0f ? 0.0f : z;  // viewport depth range [0, 1]
     if (!(z < 1.0f)) continue;  // LESS against the 1.0 clear
     const unsigned long long key =
         ((unsigned long long)__builtin_bit_cast(uint32_t, z + 0.0f) << 32) | (unsigned long long)r.prim;
-    unsigned long long* dst = vis + (size_t)y * width + x;
-    if (key < *dst) atomicMin(dst, key);
+    best = key < best ? key : best;
   }
-}
-
-__device__ inline uint32_t raster_unorm8(float c) {  // saturate + round, as the RT path's output
-  return unorm8(c);
-}
-
-__global__ __launch_bounds__(256) void k_raster_resolve(RasterDraws dr, const float4* __restrict__ clip,
-                                                        const unsigned long long* __restrict__ vis,
-                                                        uint32_t width, uint32_t height,
-                                                        uint32_t* __restrict__ rgba8, float* __restrict__ depth) {
-  const uint32_t x = blockIdx.x * 16u + (threadIdx.x & 15u), y = blockIdx.y * 16u + (threadIdx.x >> 4);
   if (x >= width || y >= height) return;
   const size_t o = (size_t)y * width + x;
-  const unsigned long long v = vis[o];
-  if (v == kRasterClear) {
+  if (best == kRasterClear) {
     // ClearRenderTargetView {0.03, 0.35, 0.43, 1} (:529), depth 1.0 (:516)
     rgba8[o] = unorm8(0.03f) | (unorm8(0.35f) << 8) | (unorm8(0.43f) << 16) | (unorm8(1.0f) << 24);
     if (depth) depth[o] = 1.0f;
     return;
   }
-  const uint32_t t = (uint32_t)(v & 0xffffffffu);
+  const uint32_t t = (uint32_t)(best & 0xffffffffu);
   uint32_t d = 0;
   while (d + 1 < dr.n && t >= dr.first[d + 1]) ++d;
   const uint32_t lt = t - dr.first[d];
@@ -264,32 +287,40 @@ __global__ __launch_bounds__(256) void k_raster_resolve(RasterDraws dr, const fl
   const V3 q = v3(qx, qy, 1.0f);
   const float f0 = dot(cross(h1, h2), q), f1 = dot(cross(h2, h0), q), f2 = dot(cross(h0, h1), q);
   const float sum = (f0 + f1) + f2;
-  const float b0 = f0 / sum, b1 = f1 / sum, b2 = f2 / sum;
+  const float w0 = f0 / sum, w1 = f1 / sum, w2 = f2 / sum;
   float out[4];
-  for (int ch = 0; ch < 4; ++ch) out[ch] = (b0 * col[0][ch] + b1 * col[1][ch]) + b2 * col[2][ch];
-  rgba8[o] = raster_unorm8(out[0]) | (raster_unorm8(out[1]) << 8) | (raster_unorm8(out[2]) << 16) |
-             (raster_unorm8(out[3]) << 24);
-  if (depth) depth[o] = __builtin_bit_cast(float, (uint32_t)(v >> 32));
+  for (int ch = 0; ch < 4; ++ch) out[ch] = (w0 * col[0][ch] + w1 * col[1][ch]) + w2 * col[2][ch];
+  rgba8[o] = unorm8(out[0]) | (unorm8(out[1]) << 8) | (unorm8(out[2]) << 16) | (unorm8(out[3]) << 24);
+  if (depth) depth[o] = __builtin_bit_cast(float, (uint32_t)(best >> 32));
 }
 
 }  // namespace
 
-hipError_t launch_raster(const RasterDraws& dr, const RasterView& rv, const RasterScratch& s, void* rgba8,
-                         float* depth, hipStream_t stream) {
-  const size_t npx = (size_t)rv.width * rv.height;
+hipError_t launch_raster_bin(const RasterDraws& dr, const RasterView& rv, const RasterScratch& s,
+                             hipStream_t stream) {
   const uint32_t nslots = dr.total * 7u;
-  hipError_t e = hipMemsetD32Async((hipDeviceptr_t)s.vis, 0xffffffffu, npx * 2, stream);
+  const uint32_t tx = (rv.width + 7) / 8, ty = (rv.height + 7) / 8, ntiles = tx * ty;
+  hipError_t e = hipMemsetAsync(s.tcount, 0, (size_t)ntiles * 4, stream);
   if (e != hipSuccess) return e;
   if (dr.total) {
     k_raster_setup<<<(dr.total + 255) / 256, 256, 0, stream>>>(dr, rv, s.clip, s.slots, s.tiles);
-    k_raster_scan<<<1, 1024, 0, stream>>>(s.tiles, nslots, s.offs);
-    int dev = 0, ncu = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    k_raster_tiles<<<ncu * 8, 256, 0, stream>>>(s.slots, s.offs, nslots, rv.width, rv.height, s.vis);
+    k_raster_bin<0><<<(nslots + 3) / 4, 256, 0, stream>>>(s.slots, s.tiles, nslots, tx, s.tcount, nullptr, nullptr);
   }
-  dim3 g((rv.width + 15) / 16, (rv.height + 15) / 16);
-  k_raster_resolve<<<g, 256, 0, stream>>>(dr, s.clip, s.vis, rv.width, rv.height, (uint32_t*)rgba8, depth);
+  k_raster_scan<<<1, 1024, 0, stream>>>(s.tcount, ntiles, s.toffs);
+  return hipGetLastError();
+}
+
+hipError_t launch_raster_draw(const RasterDraws& dr, const RasterView& rv, const RasterScratch& s, void* rgba8,
+                              float* depth, hipStream_t stream) {
+  const uint32_t nslots = dr.total * 7u;
+  const uint32_t tx = (rv.width + 7) / 8, ty = (rv.height + 7) / 8, ntiles = tx * ty;
+  if (dr.total) {
+    hipError_t e = hipMemsetAsync(s.tcount, 0, (size_t)ntiles * 4, stream);
+    if (e != hipSuccess) return e;
+    k_raster_bin<1><<<(nslots + 3) / 4, 256, 0, stream>>>(s.slots, s.tiles, nslots, tx, s.tcount, s.toffs, s.bins);
+  }
+  k_raster_tile<<<(ntiles + 3) / 4, 256, 0, stream>>>(dr, s.clip, s.slots, s.toffs, s.bins, tx, ntiles, rv.width,
+                                                      rv.height, (uint32_t*)rgba8, depth);
   return hipGetLastError();
 }
 

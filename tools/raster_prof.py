@@ -1,0 +1,17 @@
+#!/usr/bin/env python3
+"""Times rt_raster_draw on one config (for rocprofv3 --kernel-trace --stats runs)."""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402,F401
+
+import bench  # noqa: E402
+
+p = argparse.ArgumentParser()
+p.add_argument("--config", default="REF")
+p.add_argument("--steps", type=int, default=20)
+a = p.parse_args()
+print(json.dumps(bench.measure_raster(a.config, a.steps, 3)))
