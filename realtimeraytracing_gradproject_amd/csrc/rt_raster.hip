@@ -66,23 +66,48 @@ __device__ inline void clip_of_vertex(const float* vtx, uint32_t v, const float*
   out = {c[0], c[1], c[2], c[3]};
 }
 
-__global__ __launch_bounds__(256) void k_raster_setup(RasterDraws dr, RasterView rv, float4* __restrict__ clip,
-                                                      RasterSlot* __restrict__ slots,
-                                                      uint32_t* __restrict__ tiles) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= dr.total) return;
-  uint32_t d = 0;
-  while (d + 1 < dr.n && t >= dr.first[d + 1]) ++d;
-  const uint32_t lt = t - dr.first[d];
-  const float* vtx = dr.vtx[d];
-  uint32_t vi[3];
-  for (int k = 0; k < 3; ++k) vi[k] = dr.idx[d] ? dr.idx[d][lt * 3 + k] : lt * 3 + k;
-  ClipV v[3];
+// Screen-space record of one (sub)triangle; count = its tile-box size, 0 when culled (counter-
+// clockwise on screen, degenerate) or outside the viewport.
+__device__ inline uint32_t make_slot(const int32_t X[3], const int32_t Y[3], const float Z[3], uint32_t prim,
+                                     uint32_t width, uint32_t height, RasterSlot& r) {
+  const int64_t area = (int64_t)(X[1] - X[0]) * (Y[2] - Y[0]) - (int64_t)(Y[1] - Y[0]) * (X[2] - X[0]);
+  if (area <= 0) return 0;  // clockwise on screen (y down) = front face; back faces and slivers culled
+  const int32_t xmin = min(X[0], min(X[1], X[2])), xmax = max(X[0], max(X[1], X[2]));
+  const int32_t ymin = min(Y[0], min(Y[1], Y[2])), ymax = max(Y[0], max(Y[1], Y[2]));
+  // pixels whose centre (256 px + 128) can lie inside
+  int64_t px0 = -floor_div(-(int64_t)xmin + 128, 256), px1 = floor_div((int64_t)xmax - 128, 256);
+  int64_t py0 = -floor_div(-(int64_t)ymin + 128, 256), py1 = floor_div((int64_t)ymax - 128, 256);
+  px0 = px0 < 0 ? 0 : px0;
+  py0 = py0 < 0 ? 0 : py0;
+  px1 = px1 > (int64_t)width - 1 ? (int64_t)width - 1 : px1;
+  py1 = py1 > (int64_t)height - 1 ? (int64_t)height - 1 : py1;
+  if (px0 > px1 || py0 > py1) return 0;
   for (int k = 0; k < 3; ++k) {
-    clip_of_vertex(vtx, vi[k], rv.o2w, rv.view, rv.proj, v[k]);
-    clip[(size_t)t * 3 + k] = make_float4(v[k].x, v[k].y, v[k].z, v[k].w);
+    r.x[k] = X[k];
+    r.y[k] = Y[k];
+    r.z[k] = Z[k];
   }
-  // Sutherland-Hodgman against the 6 planes (at most 9 vertices)
+  r.prim = prim;
+  r.tx0 = (uint16_t)(px0 >> 3);
+  r.ty0 = (uint16_t)(py0 >> 3);
+  r.tw = (uint16_t)((px1 >> 3) - (px0 >> 3) + 1);
+  r.th = (uint16_t)((py1 >> 3) - (py0 >> 3) + 1);
+  return (uint32_t)r.tw * r.th;
+}
+
+// viewport (0, 0, W, H, 0, 1): X = (x/w + 1) W/2, Y = (1 - y/w) H/2, depth = z/w; 16.8 snap
+__device__ inline void to_screen(const ClipV& v, uint32_t width, uint32_t height, int32_t& X, int32_t& Y, float& Z) {
+  const float sx = (v.x / v.w + 1.0f) * (0.5f * (float)width);
+  const float sy = (1.0f - v.y / v.w) * (0.5f * (float)height);
+  X = (int32_t)rintf(sx * 256.0f);
+  Y = (int32_t)rintf(sy * 256.0f);
+  Z = v.z / v.w + 0.0f;
+}
+
+// Triangles that cross a clip plane: Sutherland-Hodgman against the 6 planes (at most 9
+// vertices), then a fan from vertex 0 into slots 0..6.
+__device__ __noinline__ void setup_clipped(const ClipV* v, uint32_t t, uint32_t width, uint32_t height,
+                                           RasterSlot* __restrict__ slots, uint32_t* __restrict__ tiles) {
   ClipV poly[9], tmp[9];
   int n = 3;
   for (int k = 0; k < 3; ++k) poly[k] = v[k];
@@ -101,80 +126,87 @@ __global__ __launch_bounds__(256) void k_raster_setup(RasterDraws dr, RasterView
     n = m;
     for (int k = 0; k < n; ++k) poly[k] = tmp[k];
   }
-  int32_t X[9], Y[9];
-  float Z[9];
   bool ok = n >= 3;
-  for (int k = 0; k < n && ok; ++k) {
-    if (!(poly[k].w > 0.0f)) {
-      ok = false;
-      break;
-    }
-    // viewport (0, 0, W, H, 0, 1): X = (x/w + 1) W/2, Y = (1 - y/w) H/2, depth = z/w
-    const float sx = (poly[k].x / poly[k].w + 1.0f) * (0.5f * (float)rv.width);
-    const float sy = (1.0f - poly[k].y / poly[k].w) * (0.5f * (float)rv.height);
-    X[k] = (int32_t)rintf(sx * 256.0f);
-    Y[k] = (int32_t)rintf(sy * 256.0f);
-    Z[k] = poly[k].z / poly[k].w + 0.0f;
-  }
+  for (int k = 0; k < n; ++k) ok = ok && poly[k].w > 0.0f;
   for (int s = 0; s < 7; ++s) {
     const size_t slot = (size_t)t * 7 + s;
     uint32_t cnt = 0;
-    RasterSlot r{};
     if (ok && s + 2 < n) {
-      const int a = 0, b = s + 1, c = s + 2;  // fan from vertex 0
-      const int64_t area = (int64_t)(X[b] - X[a]) * (Y[c] - Y[a]) - (int64_t)(Y[b] - Y[a]) * (X[c] - X[a]);
-      if (area > 0) {  // clockwise on screen (y down) = front face; back faces and slivers culled
-        const int32_t xmin = min(X[a], min(X[b], X[c])), xmax = max(X[a], max(X[b], X[c]));
-        const int32_t ymin = min(Y[a], min(Y[b], Y[c])), ymax = max(Y[a], max(Y[b], Y[c]));
-        // pixels whose centre (256 px + 128) can lie inside
-        int64_t px0 = -floor_div(-(int64_t)xmin + 128, 256), px1 = floor_div((int64_t)xmax - 128, 256);
-        int64_t py0 = -floor_div(-(int64_t)ymin + 128, 256), py1 = floor_div((int64_t)ymax - 128, 256);
-        px0 = px0 < 0 ? 0 : px0;
-        py0 = py0 < 0 ? 0 : py0;
-        px1 = px1 > (int64_t)rv.width - 1 ? (int64_t)rv.width - 1 : px1;
-        py1 = py1 > (int64_t)rv.height - 1 ? (int64_t)rv.height - 1 : py1;
-        if (px0 <= px1 && py0 <= py1) {
-          r.x[0] = X[a], r.x[1] = X[b], r.x[2] = X[c];
-          r.y[0] = Y[a], r.y[1] = Y[b], r.y[2] = Y[c];
-          r.z[0] = Z[a], r.z[1] = Z[b], r.z[2] = Z[c];
-          r.prim = t;
-          r.tx0 = (uint16_t)(px0 >> 3);
-          r.ty0 = (uint16_t)(py0 >> 3);
-          r.tw = (uint16_t)((px1 >> 3) - (px0 >> 3) + 1);
-          r.th = (uint16_t)((py1 >> 3) - (py0 >> 3) + 1);
-          cnt = (uint32_t)r.tw * r.th;
-        }
-      }
+      int32_t X[3], Y[3];
+      float Z[3];
+      to_screen(poly[0], width, height, X[0], Y[0], Z[0]);
+      to_screen(poly[s + 1], width, height, X[1], Y[1], Z[1]);
+      to_screen(poly[s + 2], width, height, X[2], Y[2], Z[2]);
+      RasterSlot r;
+      cnt = make_slot(X, Y, Z, t, width, height, r);
+      if (cnt) slots[slot] = r;
     }
-    slots[slot] = r;
     tiles[slot] = cnt;
   }
 }
 
-// Exclusive scan of n counts into offs[0..n], offs[n] = total. One 1024-thread workgroup, each
-// thread owning a contiguous chunk.
+__global__ __launch_bounds__(256) void k_raster_setup(RasterDraws dr, RasterView rv, float4* __restrict__ clip,
+                                                      RasterSlot* __restrict__ slots,
+                                                      uint32_t* __restrict__ tiles) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= dr.total) return;
+  uint32_t d = 0;
+  while (d + 1 < dr.n && t >= dr.first[d + 1]) ++d;
+  const uint32_t lt = t - dr.first[d];
+  const float* vtx = dr.vtx[d];
+  uint32_t vi[3];
+  for (int k = 0; k < 3; ++k) vi[k] = dr.idx[d] ? dr.idx[d][lt * 3 + k] : lt * 3 + k;
+  ClipV v[3];
+  bool inside = true;
+  for (int k = 0; k < 3; ++k) {
+    clip_of_vertex(vtx, vi[k], rv.o2w, rv.view, rv.proj, v[k]);
+    clip[(size_t)t * 3 + k] = make_float4(v[k].x, v[k].y, v[k].z, v[k].w);
+    for (int p = 0; p < 6; ++p) inside = inside && plane_dist(v[k], p) >= 0.0f;
+  }
+  if (!inside) {
+    setup_clipped(v, t, rv.width, rv.height, slots, tiles);
+    return;
+  }
+  // common case: no clipping needed
+  const bool ok = v[0].w > 0.0f && v[1].w > 0.0f && v[2].w > 0.0f;
+  int32_t X[3], Y[3];
+  float Z[3];
+  for (int k = 0; k < 3; ++k) to_screen(v[k], rv.width, rv.height, X[k], Y[k], Z[k]);
+  RasterSlot r;
+  const uint32_t cnt = ok ? make_slot(X, Y, Z, t, rv.width, rv.height, r) : 0u;
+  if (cnt) slots[(size_t)t * 7] = r;
+  tiles[(size_t)t * 7] = cnt;
+  for (int s = 1; s < 7; ++s) tiles[(size_t)t * 7 + s] = 0;
+}
+
+// Exclusive scan of n counts into offs[0..n], offs[n] = total: one 1024-thread workgroup
+// sweeping the array in coalesced 1024-element rows, carrying the running total.
 __global__ __launch_bounds__(1024) void k_raster_scan(const uint32_t* __restrict__ cnt, uint32_t n,
                                                       uint32_t* __restrict__ offs) {
-  __shared__ uint32_t part[1024];
-  const uint32_t tid = threadIdx.x;
-  const uint32_t chunk = (n + 1023u) / 1024u;
-  const uint32_t b = min(n, tid * chunk), e = min(n, b + chunk);
-  uint32_t s = 0;
-  for (uint32_t i = b; i < e; ++i) s += cnt[i];
-  part[tid] = s;
-  __syncthreads();
-  for (uint32_t off = 1; off < 1024u; off <<= 1) {
-    const uint32_t add = tid >= off ? part[tid - off] : 0u;
+  __shared__ uint32_t wsum[16];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < n; base += 1024u) {
+    const uint32_t i = base + tid;
+    const uint32_t v = i < n ? cnt[i] : 0u;
+    uint32_t x = v;  // inclusive scan within the wave
+    for (uint32_t off = 1; off < 64u; off <<= 1) {
+      const uint32_t y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63u) wsum[w] = x;
     __syncthreads();
-    part[tid] += add;
+    uint32_t before = 0, total = 0;
+    for (uint32_t k = 0; k < 16u; ++k) {
+      const uint32_t ws = wsum[k];
+      before += k < w ? ws : 0u;
+      total += ws;
+    }
+    if (i < n) offs[i] = carry + before + x - v;
+    carry += total;
     __syncthreads();
   }
-  uint32_t run = part[tid] - s;
-  for (uint32_t i = b; i < e; ++i) {
-    offs[i] = run;
-    run += cnt[i];
-  }
-  if (tid == 1023u) offs[n] = part[1023];
+  if (tid == 0) offs[n] = carry;
 }
 
 // Triangle-vs-tile test: false when the 8x8 tile's pixel centres all lie strictly outside one
