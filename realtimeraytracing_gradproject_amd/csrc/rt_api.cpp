@@ -260,7 +260,7 @@ rt_status rt_destroy(rt_ctx_t c) {
   if (c->pool_nodes) (void)hipFree(c->pool_nodes);
   if (c->pool_tris) (void)hipFree(c->pool_tris);
   for (void* p : {(void*)c->raster.clip, (void*)c->raster.slots, (void*)c->raster.tiles, (void*)c->raster.tcount,
-                  (void*)c->raster.toffs, (void*)c->raster.bins})
+                  (void*)c->raster.toffs, (void*)c->raster.bins, (void*)c->raster.bsum, (void*)c->raster.draws})
     if (p) (void)hipFree(p);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -580,6 +580,10 @@ rt_status rt_raster_draw(rt_ctx_t c, const rt_blas_t* draws, uint32_t ndraws, co
     if (c->raster_tile_cap < ntiles) {
       if ((st = regrow((void**)&c->raster.tcount, ntiles * 4, "hipMalloc(raster tile counts)")) != RT_OK) return st;
       if ((st = regrow((void**)&c->raster.toffs, (ntiles + 1) * 4, "hipMalloc(raster tile offsets)")) != RT_OK) return st;
+      if ((st = regrow((void**)&c->raster.bsum, (ntiles / 4096 + 2) * 4, "hipMalloc(raster scan)")) != RT_OK) return st;
+      if (!c->raster.draws &&
+          (st = regrow((void**)&c->raster.draws, sizeof(rt::RasterDraws), "hipMalloc(raster draws)")) != RT_OK)
+        return st;
       c->raster_tile_cap = ntiles;
     }
     if (c->raster_prim_cap < total) {

@@ -80,6 +80,8 @@ struct RasterScratch {
   uint32_t* tcount = nullptr;   // per screen tile: binned triangles (then the append cursor)
   uint32_t* toffs = nullptr;    // exclusive scan of tcount, + total (screen tiles + 1)
   uint32_t* bins = nullptr;     // slot ids grouped by screen tile
+  uint32_t* bsum = nullptr;     // scan block sums (screen tiles / 4096 + 1)
+  RasterDraws* draws = nullptr; // device copy of the draw list
 };
 
 // Phase 1: vertex stage, clipping, setup and bin counting; toffs[ntiles] = number of bin entries

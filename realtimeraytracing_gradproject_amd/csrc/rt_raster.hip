@@ -145,17 +145,17 @@ __device__ __noinline__ void setup_clipped(const ClipV* v, uint32_t t, uint32_t 
   }
 }
 
-__global__ __launch_bounds__(256) void k_raster_setup(RasterDraws dr, RasterView rv, float4* __restrict__ clip,
+__global__ __launch_bounds__(256) void k_raster_setup(const RasterDraws* __restrict__ drp, uint32_t total, RasterView rv, float4* __restrict__ clip,
                                                       RasterSlot* __restrict__ slots,
                                                       uint32_t* __restrict__ tiles) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= dr.total) return;
+  if (t >= total) return;
   uint32_t d = 0;
-  while (d + 1 < dr.n && t >= dr.first[d + 1]) ++d;
-  const uint32_t lt = t - dr.first[d];
-  const float* vtx = dr.vtx[d];
+  while (d + 1 < drp->n && t >= drp->first[d + 1]) ++d;
+  const uint32_t lt = t - drp->first[d];
+  const float* vtx = drp->vtx[d];
   uint32_t vi[3];
-  for (int k = 0; k < 3; ++k) vi[k] = dr.idx[d] ? dr.idx[d][lt * 3 + k] : lt * 3 + k;
+  for (int k = 0; k < 3; ++k) vi[k] = drp->idx[d] ? drp->idx[d][lt * 3 + k] : lt * 3 + k;
   ClipV v[3];
   bool inside = true;
   for (int k = 0; k < 3; ++k) {
@@ -179,34 +179,66 @@ __global__ __launch_bounds__(256) void k_raster_setup(RasterDraws dr, RasterView
   for (int s = 1; s < 7; ++s) tiles[(size_t)t * 7 + s] = 0;
 }
 
-// Exclusive scan of n counts into offs[0..n], offs[n] = total: one 1024-thread workgroup
-// sweeping the array in coalesced 1024-element rows, carrying the running total.
-__global__ __launch_bounds__(1024) void k_raster_scan(const uint32_t* __restrict__ cnt, uint32_t n,
-                                                      uint32_t* __restrict__ offs) {
-  __shared__ uint32_t wsum[16];
+// Exclusive scan of n counts into offs[0..n] (offs[n] = total) in three launches:
+// k_scan_blocks scans 4096-element blocks (4 per thread, coalesced uint4 loads) and records each
+// block's sum, k_scan_sums scans the block sums (one workgroup), k_scan_add adds them back.
+constexpr uint32_t kScanBlock = 4096;
+
+__device__ inline uint32_t block_exclusive(uint32_t v, uint32_t* wsum, uint32_t& total) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
-  uint32_t carry = 0;
-  for (uint32_t base = 0; base < n; base += 1024u) {
-    const uint32_t i = base + tid;
-    const uint32_t v = i < n ? cnt[i] : 0u;
-    uint32_t x = v;  // inclusive scan within the wave
-    for (uint32_t off = 1; off < 64u; off <<= 1) {
-      const uint32_t y = __shfl_up(x, off, 64);
-      if (lane >= off) x += y;
-    }
-    if (lane == 63u) wsum[w] = x;
-    __syncthreads();
-    uint32_t before = 0, total = 0;
-    for (uint32_t k = 0; k < 16u; ++k) {
-      const uint32_t ws = wsum[k];
-      before += k < w ? ws : 0u;
-      total += ws;
-    }
-    if (i < n) offs[i] = carry + before + x - v;
-    carry += total;
-    __syncthreads();
+  uint32_t x = v;  // inclusive scan within the wave
+  for (uint32_t off = 1; off < 64u; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
   }
-  if (tid == 0) offs[n] = carry;
+  if (lane == 63u) wsum[w] = x;
+  __syncthreads();
+  uint32_t before = 0;
+  total = 0;
+  for (uint32_t k = 0; k < 16u; ++k) {
+    const uint32_t ws = wsum[k];
+    before += k < w ? ws : 0u;
+    total += ws;
+  }
+  __syncthreads();
+  return before + x - v;
+}
+
+__global__ __launch_bounds__(1024) void k_scan_blocks(const uint32_t* __restrict__ cnt, uint32_t n,
+                                                      uint32_t* __restrict__ offs, uint32_t* __restrict__ bsum) {
+  __shared__ uint32_t wsum[16];
+  const uint32_t i0 = blockIdx.x * kScanBlock + threadIdx.x * 4u;
+  uint32_t v[4];
+  for (int k = 0; k < 4; ++k) v[k] = i0 + k < n ? cnt[i0 + k] : 0u;
+  const uint32_t mine = (v[0] + v[1]) + (v[2] + v[3]);
+  uint32_t total;
+  uint32_t run = block_exclusive(mine, wsum, total);
+  for (int k = 0; k < 4; ++k) {
+    if (i0 + k < n) offs[i0 + k] = run;
+    run += v[k];
+  }
+  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(1024) void k_scan_sums(uint32_t* __restrict__ bsum, uint32_t nb, uint32_t n,
+                                                    uint32_t* __restrict__ offs) {
+  __shared__ uint32_t wsum[16];
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < nb; base += 1024u) {
+    const uint32_t i = base + threadIdx.x;
+    const uint32_t v = i < nb ? bsum[i] : 0u;
+    uint32_t total;
+    const uint32_t ex = block_exclusive(v, wsum, total);
+    if (i < nb) bsum[i] = carry + ex;
+    carry += total;
+  }
+  if (threadIdx.x == 0) offs[n] = carry;
+}
+
+__global__ __launch_bounds__(256) void k_scan_add(uint32_t* __restrict__ offs, uint32_t n,
+                                                  const uint32_t* __restrict__ bsum) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && i >= kScanBlock) offs[i] += bsum[i / kScanBlock];
 }
 
 // Triangle-vs-tile test: false when the 8x8 tile's pixel centres all lie strictly outside one
@@ -252,7 +284,7 @@ __global__ __launch_bounds__(256) void k_raster_bin(const RasterSlot* __restrict
 // (edge functions, top-left rule, screen-linear depth); the per-pixel minimum of
 // (depth bits << 32 | primitive) is exactly in-order LESS testing. The winning primitive is then
 // shaded (PSMain: interpolated COLOR) and written once.
-__global__ __launch_bounds__(256) void k_raster_tile(RasterDraws dr, const float4* __restrict__ clip,
+__global__ __launch_bounds__(256) void k_raster_tile(const RasterDraws* __restrict__ drp, const float4* __restrict__ clip,
                                                      const RasterSlot* __restrict__ slots,
                                                      const uint32_t* __restrict__ toffs,
                                                      const uint32_t* __restrict__ bins, uint32_t tiles_x,
@@ -299,13 +331,13 @@ __global__ __launch_bounds__(256) void k_raster_tile(RasterDraws dr, const float
   }
   const uint32_t t = (uint32_t)(best & 0xffffffffu);
   uint32_t d = 0;
-  while (d + 1 < dr.n && t >= dr.first[d + 1]) ++d;
-  const uint32_t lt = t - dr.first[d];
-  const float* vtx = dr.vtx[d];
+  while (d + 1 < drp->n && t >= drp->first[d + 1]) ++d;
+  const uint32_t lt = t - drp->first[d];
+  const float* vtx = drp->vtx[d];
   float col[3][4];
   for (int k = 0; k < 3; ++k) {
-    const uint32_t vi = dr.idx[d] ? dr.idx[d][lt * 3 + k] : lt * 3 + k;
-    const bool inside = vi + 1 < dr.nvtx[d];
+    const uint32_t vi = drp->idx[d] ? drp->idx[d][lt * 3 + k] : lt * 3 + k;
+    const bool inside = vi + 1 < drp->nvtx[d];
     col[k][0] = inside ? vtx[vi * 6 + 3] : 0.0f;
     col[k][1] = inside ? vtx[vi * 6 + 4] : 0.0f;
     col[k][2] = inside ? vtx[vi * 6 + 5] : 0.0f;
@@ -334,11 +366,16 @@ hipError_t launch_raster_bin(const RasterDraws& dr, const RasterView& rv, const 
   const uint32_t tx = (rv.width + 7) / 8, ty = (rv.height + 7) / 8, ntiles = tx * ty;
   hipError_t e = hipMemsetAsync(s.tcount, 0, (size_t)ntiles * 4, stream);
   if (e != hipSuccess) return e;
+  e = hipMemcpyAsync(s.draws, &dr, sizeof(RasterDraws), hipMemcpyHostToDevice, stream);
+  if (e != hipSuccess) return e;
   if (dr.total) {
-    k_raster_setup<<<(dr.total + 255) / 256, 256, 0, stream>>>(dr, rv, s.clip, s.slots, s.tiles);
+    k_raster_setup<<<(dr.total + 255) / 256, 256, 0, stream>>>(s.draws, dr.total, rv, s.clip, s.slots, s.tiles);
     k_raster_bin<0><<<(nslots + 3) / 4, 256, 0, stream>>>(s.slots, s.tiles, nslots, tx, s.tcount, nullptr, nullptr);
   }
-  k_raster_scan<<<1, 1024, 0, stream>>>(s.tcount, ntiles, s.toffs);
+  const uint32_t nb = (ntiles + kScanBlock - 1) / kScanBlock;
+  k_scan_blocks<<<nb, 1024, 0, stream>>>(s.tcount, ntiles, s.toffs, s.bsum);
+  k_scan_sums<<<1, 1024, 0, stream>>>(s.bsum, nb, ntiles, s.toffs);
+  if (nb > 1) k_scan_add<<<(ntiles + 255) / 256, 256, 0, stream>>>(s.toffs, ntiles, s.bsum);
   return hipGetLastError();
 }
 
@@ -351,7 +388,7 @@ hipError_t launch_raster_draw(const RasterDraws& dr, const RasterView& rv, const
     if (e != hipSuccess) return e;
     k_raster_bin<1><<<(nslots + 3) / 4, 256, 0, stream>>>(s.slots, s.tiles, nslots, tx, s.tcount, s.toffs, s.bins);
   }
-  k_raster_tile<<<(ntiles + 3) / 4, 256, 0, stream>>>(dr, s.clip, s.slots, s.toffs, s.bins, tx, ntiles, rv.width,
+  k_raster_tile<<<(ntiles + 3) / 4, 256, 0, stream>>>(s.draws, s.clip, s.slots, s.toffs, s.bins, tx, ntiles, rv.width,
                                                       rv.height, (uint32_t*)rgba8, depth);
   return hipGetLastError();
 }
