@@ -105,10 +105,13 @@ __device__ inline void to_screen(const ClipV& v, uint32_t width, uint32_t height
 }
 
 // Triangles that cross a clip plane: Sutherland-Hodgman against the 6 planes (at most 9
-// vertices), then a fan from vertex 0 into slots 0..6.
-__device__ __noinline__ void setup_clipped(const ClipV* v, uint32_t t, uint32_t width, uint32_t height,
-                                           RasterSlot* __restrict__ slots, uint32_t* __restrict__ tiles) {
-  ClipV poly[9], tmp[9];
+// vertices, the polygons in LDS so the variable-length lists are not spilled to scratch), then a
+// fan from vertex 0 into slots 0..6.
+constexpr int kSetupBlock = 64;
+
+__device__ void setup_clipped(const ClipV* v, uint32_t t, uint32_t width, uint32_t height,
+                              ClipV* __restrict__ poly, ClipV* __restrict__ tmp,
+                              RasterSlot* __restrict__ slots, uint32_t* __restrict__ tiles) {
   int n = 3;
   for (int k = 0; k < 3; ++k) poly[k] = v[k];
   for (int p = 0; p < 6 && n > 0; ++p) {
@@ -117,8 +120,8 @@ __device__ __noinline__ void setup_clipped(const ClipV* v, uint32_t t, uint32_t 
     if (all_in) continue;
     int m = 0;
     for (int k = 0; k < n; ++k) {
-      const ClipV& a = poly[k];
-      const ClipV& b = poly[(k + 1) % n];
+      const ClipV a = poly[k];
+      const ClipV b = poly[k + 1 < n ? k + 1 : 0];
       const float da = plane_dist(a, p), db = plane_dist(b, p);
       if (da >= 0.0f) tmp[m++] = a;
       if ((da >= 0.0f) != (db >= 0.0f)) tmp[m++] = da >= 0.0f ? clip_lerp(a, da, b, db) : clip_lerp(b, db, a, da);
@@ -145,7 +148,7 @@ __device__ __noinline__ void setup_clipped(const ClipV* v, uint32_t t, uint32_t 
   }
 }
 
-__global__ __launch_bounds__(256) void k_raster_setup(const RasterDraws* __restrict__ drp, uint32_t total, RasterView rv, float4* __restrict__ clip,
+__global__ __launch_bounds__(kSetupBlock) void k_raster_setup(const RasterDraws* __restrict__ drp, uint32_t total, RasterView rv, float4* __restrict__ clip,
                                                       RasterSlot* __restrict__ slots,
                                                       uint32_t* __restrict__ tiles) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -164,7 +167,8 @@ __global__ __launch_bounds__(256) void k_raster_setup(const RasterDraws* __restr
     for (int p = 0; p < 6; ++p) inside = inside && plane_dist(v[k], p) >= 0.0f;
   }
   if (!inside) {
-    setup_clipped(v, t, rv.width, rv.height, slots, tiles);
+    __shared__ ClipV poly[kSetupBlock][9], tmp[kSetupBlock][9];
+    setup_clipped(v, t, rv.width, rv.height, poly[threadIdx.x], tmp[threadIdx.x], slots, tiles);
     return;
   }
   // common case: no clipping needed
@@ -297,29 +301,51 @@ __global__ __launch_bounds__(256) void k_raster_tile(const RasterDraws* __restri
   const int64_t px = (int64_t)x * 256 + 128, py = (int64_t)y * 256 + 128;
   unsigned long long best = kRasterClear;
   const uint32_t b0 = toffs[tile], b1 = toffs[tile + 1];
-  for (uint32_t b = b0; b < b1; ++b) {
-    const uint32_t s = __builtin_amdgcn_readfirstlane(bins[b]);
-    const RasterSlot r = slots[s];
-    int64_t e[3];
-    bool in = true;
-    for (int i = 0; i < 3; ++i) {  // E_i: edge from vertex i+1 to i+2 (opposite vertex i)
-      const int a = (i + 1) % 3, c = (i + 2) % 3;
-      const int64_t dx = (int64_t)r.x[c] - r.x[a], dy = (int64_t)r.y[c] - r.y[a];
-      e[i] = dx * (py - r.y[a]) - dy * (px - r.x[a]);
-      const bool top_left = dy < 0 || (dy == 0 && dx > 0);
-      in = in && (e[i] > 0 || (e[i] == 0 && top_left));
+  // the bin is fetched 64 entries at a time, one slot record per lane, then broadcast lane by lane
+  for (uint32_t base = b0; base < b1; base += 64u) {
+    const uint32_t cnt = min(64u, b1 - base);
+    int32_t lx[3] = {0, 0, 0}, ly[3] = {0, 0, 0};
+    float lz[3] = {0.0f, 0.0f, 0.0f};
+    uint32_t lp = 0;
+    if (lane < cnt) {
+      const RasterSlot& q = slots[bins[base + lane]];
+      for (int k = 0; k < 3; ++k) {
+        lx[k] = q.x[k];
+        ly[k] = q.y[k];
+        lz[k] = q.z[k];
+      }
+      lp = q.prim;
     }
-    if (!in) continue;
-    // depth, linear in screen space: z0 + (E1 (z1 - z0) + E2 (z2 - z0)) / area, in double
-    const double area = (double)(e[0] + e[1] + e[2]);
-    const double dz = ((double)e[1] * ((double)r.z[1] - (double)r.z[0]) +
-                       (double)e[2] * ((double)r.z[2] - (double)r.z[0])) / area;
-    float z = (float)((double)r.z[0] + dz);
-    z = z < 0.0f ? 0.0f : z;  // viewport depth range [0, 1]
-    if (!(z < 1.0f)) continue;  // LESS against the 1.0 clear
-    const unsigned long long key =
-        ((unsigned long long)__builtin_bit_cast(uint32_t, z + 0.0f) << 32) | (unsigned long long)r.prim;
-    best = key < best ? key : best;
+    for (uint32_t j = 0; j < cnt; ++j) {
+      int32_t X[3], Y[3];
+      float Z[3];
+      for (int k = 0; k < 3; ++k) {
+        X[k] = __builtin_amdgcn_readlane(lx[k], j);
+        Y[k] = __builtin_amdgcn_readlane(ly[k], j);
+        Z[k] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int32_t, lz[k]), j));
+      }
+      const uint32_t prim = __builtin_amdgcn_readlane(lp, j);
+      int64_t e[3];
+      bool in = true;
+      for (int i = 0; i < 3; ++i) {  // E_i: edge from vertex i+1 to i+2 (opposite vertex i)
+        const int a = (i + 1) % 3, c = (i + 2) % 3;
+        const int64_t dx = (int64_t)X[c] - X[a], dy = (int64_t)Y[c] - Y[a];
+        e[i] = dx * (py - Y[a]) - dy * (px - X[a]);
+        const bool top_left = dy < 0 || (dy == 0 && dx > 0);
+        in = in && (e[i] > 0 || (e[i] == 0 && top_left));
+      }
+      if (!in) continue;
+      // depth, linear in screen space: z0 + (E1 (z1 - z0) + E2 (z2 - z0)) / area, in double
+      const double area = (double)(e[0] + e[1] + e[2]);
+      const double dz = ((double)e[1] * ((double)Z[1] - (double)Z[0]) +
+                         (double)e[2] * ((double)Z[2] - (double)Z[0])) / area;
+      float z = (float)((double)Z[0] + dz);
+      z = z < 0.0f ? 0.0f : z;  // viewport depth range [0, 1]
+      if (!(z < 1.0f)) continue;  // LESS against the 1.0 clear
+      const unsigned long long key =
+          ((unsigned long long)__builtin_bit_cast(uint32_t, z + 0.0f) << 32) | (unsigned long long)prim;
+      best = key < best ? key : best;
+    }
   }
   if (x >= width || y >= height) return;
   const size_t o = (size_t)y * width + x;
@@ -369,7 +395,8 @@ hipError_t launch_raster_bin(const RasterDraws& dr, const RasterView& rv, const 
   e = hipMemcpyAsync(s.draws, &dr, sizeof(RasterDraws), hipMemcpyHostToDevice, stream);
   if (e != hipSuccess) return e;
   if (dr.total) {
-    k_raster_setup<<<(dr.total + 255) / 256, 256, 0, stream>>>(s.draws, dr.total, rv, s.clip, s.slots, s.tiles);
+    k_raster_setup<<<(dr.total + kSetupBlock - 1) / kSetupBlock, kSetupBlock, 0, stream>>>(s.draws, dr.total, rv,
+                                                                                          s.clip, s.slots, s.tiles);
     k_raster_bin<0><<<(nslots + 3) / 4, 256, 0, stream>>>(s.slots, s.tiles, nslots, tx, s.tcount, nullptr, nullptr);
   }
   const uint32_t nb = (ntiles + kScanBlock - 1) / kScanBlock;
