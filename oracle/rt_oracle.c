@@ -208,7 +208,10 @@ typedef struct {
 typedef struct {
   float lox[4], hix[4], loy[4], hiy[4], loz[4], hiz[4];
   int32_t child[4];
-  uint32_t count, pad[3];
+  uint32_t count;
+  int32_t first_inner; /* ref of the first internal child (consecutive refs in slot order), 0 if none */
+  uint32_t inner_mask; /* bit k: child[k] >= 0 */
+  uint32_t pad;
 } o4node;
 typedef struct {
   float v0[3]; uint32_t prim;
@@ -325,7 +328,11 @@ static uint32_t collapse(const onode* bin, uint32_t nbin, o4node* out, uint32_t*
           ++valid;
           nd.lox[j] = box[j][0]; nd.loy[j] = box[j][1]; nd.loz[j] = box[j][2];
           nd.hix[j] = box[j][3]; nd.hiy[j] = box[j][4]; nd.hiz[j] = box[j][5];
-          if (ref[j] >= 0) { q[tail] = ref[j]; r = tail; ps[tail] = ps[head] + cnt - 1; ++tail; }
+          if (ref[j] >= 0) {
+            if (!nd.inner_mask) nd.first_inner = tail;
+            nd.inner_mask |= 1u << j;
+            q[tail] = ref[j]; r = tail; ps[tail] = ps[head] + cnt - 1; ++tail;
+          }
           else r = ref[j];
         }
         nd.child[j] = r;
@@ -761,6 +768,7 @@ static int otrace(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax,
 /* lane so the traversal order and the per-lane counters are those of the device.            */
 /* ---------------------------------------------------------------------------------------- */
 #define OPK 64
+#define OSTACK 4096 /* emulated per-child stack: its bound is at most 3 entries per tree level */
 
 typedef struct {
   vec3 o[OPK], d[OPK], invd[OPK], no[OPK];
@@ -837,7 +845,7 @@ static int opk_node(const o4node* nd, const opkray* ry, float tmin, ohit* h, int
     for (int l = 0; l < OPK; ++l) st->v[5] += live[l] ? 1u : 0u;
   for (int k = 3; k >= 0; --k) {
     if (!((P >> k) & 1u)) continue;
-    if (*sp < OPK) stack[*sp] = nd->child[k];
+    if (*sp < OSTACK) stack[*sp] = nd->child[k];
     ++*sp;
   }
   *next = rb;
@@ -860,8 +868,10 @@ static void opacket(const oracle_scene* s, const vec3* o, const vec3* d, float t
   if (lead < 0) return;
   uint32_t maxb = 0;
   for (int q = 0; q < s->nblas; ++q) if (s->blas[q].max_stack > maxb) maxb = s->blas[q].max_stack;
-  const int cap = (int)(s->tlas_max_stack + 1 + maxb); /* < 64 whenever the packet path runs */
-  int stack[OPK];
+  /* per-child entries: the exact bound of this (emulated) stack; the device keeps one entry per
+   * BLAS node with pending children, an order-preserving compression of the same stack */
+  const int cap = (int)(s->tlas_max_stack + 1 + maxb);
+  int stack[OSTACK];
   int sp = 0, ref = 0, next;
   for (;;) {
     if (ref >= 0) {
@@ -1421,9 +1431,9 @@ int oracle_render(const oracle_scene* s, const float cb[64], const oracle_light*
   }
   /* the device runs wave packets unless asked for per-lane rays or the trees are too deep for
    * its one-VGPR stack (rt_trace.hip launch_mode) */
-  uint32_t maxb = 0;
-  for (int q = 0; q < s->nblas; ++q) if (s->blas[q].max_stack > maxb) maxb = s->blas[q].max_stack;
-  const int packet = !brute && schedule == 0 && (s->tlas_max_stack + 1 + maxb) < OPK;
+  uint32_t maxd = 0;
+  for (int q = 0; q < s->nblas; ++q) if (s->blas[q].depth > maxd) maxd = s->blas[q].depth;
+  const int packet = !brute && schedule == 0 && (s->tlas_max_stack + maxd) < OPK;
   void* (*fn)(void*) = packet ? render_tiles : render_rows;
   if (nthreads == 1) fn(&jobs[0]);
   else {

@@ -502,10 +502,15 @@ static rt::SceneView scene_view(rt_ctx* c) {
   sv.pool_tris = c->pool_tris;
   sv.tlas = c->tlas_nodes;
   sv.inst = c->inst;
-  uint32_t maxb = 0;
-  for (const auto& b : c->blas) maxb = b.max_stack > maxb ? b.max_stack : maxb;
+  uint32_t maxb = 0, maxd = 0;
+  for (const auto& b : c->blas) {
+    maxb = b.max_stack > maxb ? b.max_stack : maxb;
+    maxd = b.depth > maxd ? b.depth : maxd;
+  }
   // worst case: the TLAS path's siblings, the TLAS->BLAS sentinel, the BLAS path's siblings
   sv.stack_cap = (int)(c->tlas_max_stack + 1 + maxb);
+  // wave packets: the TLAS path's siblings, then at most one entry per BLAS level
+  sv.packet_cap = (int)(c->tlas_max_stack + maxd);
   sv.lds_cap = sv.stack_cap < rt::kLdsStackEntries ? sv.stack_cap : rt::kLdsStackEntries;
   sv.ovf = nullptr;
   sv.ovf_lanes = 0;

@@ -61,8 +61,12 @@ struct alignas(128) Bvh4Node {
   float loy[4], hiy[4];
   float loz[4], hiz[4];
   int32_t child[4];
-  uint32_t count;  // valid children
-  uint32_t pad[3];
+  uint32_t count;       // valid children
+  int32_t first_inner;  // ref of the first internal child (0 when none): the internal children's
+                        // refs are consecutive in slot order (BFS allocation), so internal slot k
+                        // is first_inner + popcount(inner_mask & ((1 << k) - 1))
+  uint32_t inner_mask;  // bit k: child[k] is an internal node (>= 0)
+  uint32_t pad;
 };
 static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node must be 128 B");
 
@@ -139,6 +143,7 @@ struct SceneView {
   const Bvh4Node* tlas;
   const InstanceRec* inst;
   int stack_cap;       // worst-case entries per lane (exact bound from the trees)
+  int packet_cap;      // worst-case entries of the wave-packet stack (TLAS siblings + BLAS levels)
   int lds_cap;         // entries kept in LDS ([entry][lane])
   int* ovf;            // HBM overflow area, [entry - lds_cap][global lane], or null
   uint32_t ovf_lanes;  // lanes of the launch (overflow row pitch)

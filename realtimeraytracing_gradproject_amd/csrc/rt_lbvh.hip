@@ -392,7 +392,8 @@ __global__ __launch_bounds__(1024) void k_collapse(const BinNode* __restrict__ b
         int o = excl;
         const int below = ps[base + i] + cnt - 1;
         lmax = below > lmax ? below : lmax;
-        uint32_t valid = 0;
+        uint32_t valid = 0, inner = 0;
+        nd.first_inner = 0;
         for (int j = 0; j < 4; ++j) {
           const float inf = __builtin_inff();
           float b6[6] = {inf, inf, inf, inf, inf, inf};
@@ -405,6 +406,8 @@ __global__ __launch_bounds__(1024) void k_collapse(const BinNode* __restrict__ b
               nxt[pos] = ref[j];
               r = base + cur_n + pos;
               ps[r] = below;
+              if (o == excl) nd.first_inner = r;
+              inner |= 1u << j;
               ++o;
             } else {
               r = ref[j];
@@ -419,7 +422,8 @@ __global__ __launch_bounds__(1024) void k_collapse(const BinNode* __restrict__ b
           nd.child[j] = r;
         }
         nd.count = valid;
-        nd.pad[0] = nd.pad[1] = nd.pad[2] = 0;
+        nd.inner_mask = inner;
+        nd.pad = 0;
         out[base + i] = nd;
       }
       next_total += chunk_total;
@@ -599,6 +603,7 @@ __global__ void k_pool_rebase(const Bvh4Node* __restrict__ src, uint32_t n, uint
     if (c >= 0) nd.child[k] = c + (int32_t)node_base;
     else if (tri_base >= 0) nd.child[k] = ~(int32_t)((int64_t)(~c) + tri_base);
   }
+  if (nd.inner_mask) nd.first_inner += (int32_t)node_base;
   dst[i] = nd;
 }
 }  // namespace

@@ -48,6 +48,7 @@ __device__ __forceinline__ V3 ld3(const float* p) { return v3(p[0], p[1], p[2]);
 #define RT_GLOBAL __attribute__((address_space(1)))
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef int i4v __attribute__((ext_vector_type(4)));
+typedef int i8v __attribute__((ext_vector_type(8)));
 template <typename T>
 __device__ __forceinline__ const RT_GLOBAL T* gp(const T* p) {
   return (const RT_GLOBAL T*)p;
@@ -328,30 +329,19 @@ __device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref
   }
 }
 
-// One node of the packet walk: slab tests of the 4 children for every live ray; a child is
-// entered when any live ray accepts it. LEAVES (BLAS level): entered triangle children are
-// tested right here, in slot order, instead of going through the stack. The entered internal
-// children (TLAS: also instance leaves) go nearest first by the lead ray's entry distance
-// (lowest slot on ties); the others are pushed in descending slot order, so the lowest slot pops
-// next. Pushes that do not happen write the spare lane kPacketStack - 1; the bookkeeping is
-// plain integer SALU work. Returns 1 with *next set, 0 when nothing is left to descend into,
-// 2 when an any-hit packet has no live ray left.
-template <bool ANY_HIT, bool STATS, bool LEAVES, int R>
-__device__ __forceinline__ int packet_node(const RT_CONST char* pool, const RT_CONST TriRec* tpool, int ref,
-                                           const PacketRay<R>& ry, float tmin, uint32_t cur, float face,
-                                           PacketLive<R>& pl, bool* found, HitRec* hit, WaveStack& stk, int& sp,
-                                           int cap, int& next, Counters& cnt) {
-  const RT_CONST char* nb = pool + ((size_t)(uint32_t)ref << 7);
-  const i4v ch = *(const RT_CONST i4v*)(nb + 96);
-  const int cref[4] = {ch.x, ch.y, ch.z, ch.w};
-  // unused slots hold lo = hi = +inf boxes that every ray rejects: no validity mask
+// Slab tests of the 4 children of one node for every live ray: hm[r][k] = the live lanes whose
+// ray r accepts child k, vkey[r][k] = |entry distance| where accepted, else +inf. Returns the
+// entered set (children some live ray accepts). Unused slots hold lo = hi = +inf boxes that every
+// ray rejects: no validity mask.
+template <bool STATS, int R>
+__device__ __forceinline__ uint32_t packet_slabs(const RT_CONST char* nb, const PacketRay<R>& ry, float tmin,
+                                                 const PacketLive<R>& pl, const HitRec* hit, uint32_t count,
+                                                 uint64_t (&hm)[R][4], uint32_t (&vkey)[R][4], Counters& cnt) {
   const f4v a0 = cld4(nb), a1 = cld4(nb + 16), a2 = cld4(nb + 32);
   const f4v a3 = cld4(nb + 48), a4 = cld4(nb + 64), a5 = cld4(nb + 80);
   const float lox[4] = {a0.x, a0.y, a0.z, a0.w}, hix[4] = {a1.x, a1.y, a1.z, a1.w};
   const float loy[4] = {a2.x, a2.y, a2.z, a2.w}, hiy[4] = {a3.x, a3.y, a3.z, a3.w};
   const float loz[4] = {a4.x, a4.y, a4.z, a4.w}, hiz[4] = {a5.x, a5.y, a5.z, a5.w};
-  uint64_t hm[R][4];
-  uint32_t vkey[R][4];  // per ray: |entry distance| if its test accepted the child, else +inf
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const V3 iv = ry.invd[r], no = ry.noinv[r];
@@ -367,7 +357,7 @@ __device__ __forceinline__ int packet_node(const RT_CONST char* pool, const RT_C
       hm[r][k] = wave_ballot(h) & pl.mask[r];
       vkey[r][k] = h ? (__float_as_uint(n) & 0x7fffffffu) : 0x7f800000u;
     }
-    if (STATS && pl.live[r]) cnt.aabb += *(const RT_CONST uint32_t*)(nb + 112);  // Bvh4Node::count
+    if (STATS && pl.live[r]) cnt.aabb += count;
   }
   uint32_t ent = 0;
 #pragma unroll
@@ -377,36 +367,28 @@ __device__ __forceinline__ int packet_node(const RT_CONST char* pool, const RT_C
     for (int r = 0; r < R; ++r) any |= hm[r][k];
     ent |= any ? (1u << k) : 0u;
   }
+  return ent;
+}
+
+// TLAS node of the packet walk (children: TLAS nodes and instance leaves). The entered children go
+// nearest first by the lead ray's entry distance (lowest slot on ties); the others are pushed in
+// descending slot order, so the lowest slot pops next. Pushes that do not happen write the spare
+// lane kPacketStack - 1; the bookkeeping is plain integer SALU work. Returns 1 with *next set,
+// 0 when nothing is left to descend into.
+template <bool STATS, int R>
+__device__ __forceinline__ int packet_tlas_node(const RT_CONST char* pool, int ref, const PacketRay<R>& ry,
+                                                float tmin, PacketLive<R>& pl, const HitRec* hit, WaveStack& stk,
+                                                int& sp, int cap, int& next, Counters& cnt) {
+  const RT_CONST char* nb = pool + ((size_t)(uint32_t)ref << 7);
+  const i8v ch = *(const RT_CONST i8v*)(nb + 96);  // child[4], count, first_inner, inner_mask, pad
+  const int cref[4] = {ch[0], ch[1], ch[2], ch[3]};
+  uint64_t hm[R][4];
+  uint32_t vkey[R][4];
+  const uint32_t ent = packet_slabs<STATS, R>(nb, ry, tmin, pl, hit, (uint32_t)ch[4], hm, vkey, cnt);
   // pin the child-ref load before the early exit: issued with the plane loads, it shares their
   // scalar-cache round trip instead of starting a second one after the slab tests
-  asm volatile("" ::"s"(ch.x), "s"(ch.y), "s"(ch.z), "s"(ch.w));
+  asm volatile("" ::"s"(ch[0]), "s"(ch[1]), "s"(ch[2]), "s"(ch[3]));
   if (ent == 0) return 0;
-  if (LEAVES) {
-    const uint32_t leafbits = (cref[0] < 0 ? 1u : 0u) | (cref[1] < 0 ? 2u : 0u) | (cref[2] < 0 ? 4u : 0u) |
-                              (cref[3] < 0 ? 8u : 0u);
-    uint32_t tl = ent & leafbits;
-    ent &= ~leafbits;
-    while (tl) {
-      const uint32_t k = (uint32_t)__builtin_ctz(tl);
-      tl &= tl - 1u;
-      const int tr = k == 0 ? cref[0] : k == 1 ? cref[1] : k == 2 ? cref[2] : cref[3];
-      packet_tri<ANY_HIT, STATS, R>(tpool, tr, ry, tmin, cur, face, pl, found, hit, cnt);
-    }
-    if (ANY_HIT) {
-      if (!pl.update()) return 2;
-      // children only finished rays wanted are dropped
-      uint32_t still = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        uint64_t any = 0;
-#pragma unroll
-        for (int r = 0; r < R; ++r) any |= hm[r][k] & pl.mask[r];
-        still |= any ? (1u << k) : 0u;
-      }
-      ent &= still;
-    }
-    if (ent == 0) return 0;
-  }
   // uniform keys: the lead ray's key, all-ones where the child is not descended into
   uint32_t key[4];
 #pragma unroll
@@ -443,6 +425,75 @@ __device__ __forceinline__ int packet_node(const RT_CONST char* pool, const RT_C
   return 1;
 }
 
+// BLAS node of the packet walk. Entered triangle children are tested right here, in slot order.
+// Of the entered internal children the nearest (the lead ray's entry distance, lowest slot on
+// ties; chosen per lane in VALU, one readlane) is descended into; the rest become ONE stack entry
+// (first_inner << 8 | inner_mask << 4 | pending slots) that pops its slots lowest first — exactly
+// the order in which per-child pushes in descending slot order would pop them, so the walk (and
+// every counter) is that of the per-child stack, with a fraction of the scalar bookkeeping.
+// Internal child k's ref is first_inner + popcount(inner_mask below k) (BFS allocation).
+// Returns 1 with *next set, 0 when nothing is left to descend into, 2 when an any-hit packet has
+// no live ray left.
+template <bool ANY_HIT, bool STATS, int R>
+__device__ __forceinline__ int packet_blas_node(const RT_CONST char* pool, const RT_CONST TriRec* tpool, int ref,
+                                                const PacketRay<R>& ry, float tmin, uint32_t cur, float face,
+                                                PacketLive<R>& pl, bool* found, HitRec* hit, WaveStack& stk, int& sp,
+                                                int cap, int& next, Counters& cnt) {
+  const RT_CONST char* nb = pool + ((size_t)(uint32_t)ref << 7);
+  const i8v ch = *(const RT_CONST i8v*)(nb + 96);  // child[4], count, first_inner, inner_mask, pad
+  const int cref[4] = {ch[0], ch[1], ch[2], ch[3]};
+  uint64_t hm[R][4];
+  uint32_t vkey[R][4];
+  uint32_t ent = packet_slabs<STATS, R>(nb, ry, tmin, pl, hit, (uint32_t)ch[4], hm, vkey, cnt);
+  asm volatile("" ::"s"(ch[0]), "s"(ch[1]), "s"(ch[2]), "s"(ch[3]), "s"(ch[5]), "s"(ch[6]));
+  if (ent == 0) return 0;
+  const uint32_t imask = (uint32_t)ch[6];
+  uint32_t tl = ent & ~imask;
+  ent &= imask;
+  while (tl) {
+    const uint32_t k = (uint32_t)__builtin_ctz(tl);
+    tl &= tl - 1u;
+    const int tr = k == 0 ? cref[0] : k == 1 ? cref[1] : k == 2 ? cref[2] : cref[3];
+    packet_tri<ANY_HIT, STATS, R>(tpool, tr, ry, tmin, cur, face, pl, found, hit, cnt);
+  }
+  if (ANY_HIT) {
+    if (!pl.update()) return 2;
+    // children only finished rays wanted are dropped
+    uint32_t still = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint64_t any = 0;
+#pragma unroll
+      for (int r = 0; r < R; ++r) any |= hm[r][k] & pl.mask[r];
+      still |= any ? (1u << k) : 0u;
+    }
+    ent &= still;
+  }
+  if (ent == 0) return 0;
+  // per lane: the slot of its smallest key over the entered internal children (all-ones keys
+  // elsewhere), lowest slot on ties; the lead lane's answer is the packet's
+  uint32_t idx = 0;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    uint32_t kk[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) kk[k] = vkey[r][k] | (((ent >> k) & 1u) - 1u);
+    const uint32_t m = min(min(kk[0], kk[1]), min(kk[2], kk[3]));
+    const uint32_t ir = kk[0] == m ? 0u : kk[1] == m ? 1u : kk[2] == m ? 2u : 3u;
+    idx = (r == 0 || pl.lead_r == (uint32_t)r) ? ir : idx;
+  }
+  const uint32_t ib = (uint32_t)__builtin_amdgcn_readlane((int)idx, (int)pl.lead_l);
+  const uint32_t first = (uint32_t)ch[5];
+  next = (int)(first + (uint32_t)__builtin_popcount(imask & ((1u << ib) - 1u)));
+  const uint32_t P = ent & ~(1u << ib);
+  if (STATS && P && sp + 1 > cap)  // never: cap bounds the entries (one per BLAS level)
+#pragma unroll
+    for (int r = 0; r < R; ++r) cnt.overflow += pl.live[r] ? 1u : 0u;
+  stk.put(P ? sp : kPacketStack - 1, (int)((first << 8) | (imask << 4) | P));
+  sp = __builtin_amdgcn_readfirstlane(sp + (P ? 1 : 0));
+  return 1;
+}
+
 // Traces the R rays of every lane (o, d, alive per slot) as one packet; found[r] / hit[r] per ray.
 template <bool ANY_HIT, bool STATS, int R, bool CULL = false>
 __device__ void trace_packet(const SceneView& sc, const V3* o, const V3* d, float tmin, float tmax,
@@ -467,7 +518,7 @@ __device__ void trace_packet(const SceneView& sc, const V3* o, const V3* d, floa
   }
   if (!pl.update()) return;
   WaveStack stk;
-  const int cap = sc.stack_cap;  // < kPacketStack (checked at launch): lane 63 stays spare
+  const int cap = sc.packet_cap;  // < kPacketStack (checked at launch): lane 63 stays spare
   int sp = 0;
   int ref = 0;
   // TLAS walk; each instance leaf runs a nested BLAS walk on the stack above the TLAS entries
@@ -475,8 +526,7 @@ __device__ void trace_packet(const SceneView& sc, const V3* o, const V3* d, floa
   while (true) {
     int next;
     if (ref >= 0) {
-      if (packet_node<ANY_HIT, STATS, false, R>(pool, tpool, ref, w, tmin, 0u, 0.0f, pl, found, hit, stk, sp, cap,
-                                                next, cnt)) {
+      if (packet_tlas_node<STATS, R>(pool, ref, w, tmin, pl, hit, stk, sp, cap, next, cnt)) {
         ref = next;
         continue;
       }
@@ -500,15 +550,22 @@ __device__ void trace_packet(const SceneView& sc, const V3* o, const V3* d, floa
       int bref = (int)ir.pool_root;
       while (true) {
         // only internal nodes reach here: triangle children are tested inside packet_node
-        const int st = packet_node<ANY_HIT, STATS, true, R>(pool, tpool, bref, b, tmin, cur, face, pl, found, hit,
-                                                            stk, sp, cap, next, cnt);
+        const int st = packet_blas_node<ANY_HIT, STATS, R>(pool, tpool, bref, b, tmin, cur, face, pl, found, hit,
+                                                           stk, sp, cap, next, cnt);
         if (st == 1) {
           bref = next;
           continue;
         }
         if (ANY_HIT && st == 2) return;
         if (sp == base) break;
-        bref = stk.get(--sp);
+        // top entry: its lowest pending slot is next; the entry stays while slots remain
+        const uint32_t e = (uint32_t)stk.get(sp - 1);
+        const uint32_t pend = e & 15u;
+        const uint32_t k = (uint32_t)__builtin_ctz(pend);
+        bref = (int)((e >> 8) + (uint32_t)__builtin_popcount((e >> 4) & ((1u << k) - 1u)));
+        const uint32_t rest = pend & (pend - 1u);
+        stk.put(rest ? sp - 1 : kPacketStack - 1, (int)((e & ~15u) | rest));
+        sp = __builtin_amdgcn_readfirstlane(rest ? sp : sp - 1);
       }
     }
     if (sp == 0) return;
@@ -1045,7 +1102,7 @@ template <int MODE, bool STATS>
 hipError_t launch_mode(const SceneView& sc, const FrameParams& fp, const uint32_t* rows, void* rgba8,
                        float* rgba32f, unsigned long long* stats, int schedule, hipStream_t s) {
   dim3 grid((fp.width + 15) / 16, (fp.nrows + 15) / 16);
-  if (schedule == RT_SCHED_PACKET && sc.stack_cap < kPacketStack) {
+  if (schedule == RT_SCHED_PACKET && sc.packet_cap < kPacketStack) {
     constexpr int R = RT_PACKET_RAYS;
     dim3 gp((fp.width + 15) / 16, (fp.nrows + 16 * R - 1) / (16 * R));
     hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R>), gp, dim3(kBlock), 0, s, sc, fp, rows,
