@@ -271,6 +271,14 @@ __device__ __forceinline__ uint64_t wave_ballot(bool p) { return __builtin_amdgc
 
 __device__ __forceinline__ f4v cld4(const RT_CONST char* p) { return *(const RT_CONST f4v*)p; }
 
+// bit if the uniform 64-bit mask m is nonzero, else 0: s_cmp_lg_u64 + s_cselect_b32 (the
+// compiler otherwise round-trips the boolean through a VGPR and readfirstlane)
+__device__ __forceinline__ uint32_t nonzero_bit(uint64_t m, uint32_t bit) {
+  uint32_t r;
+  asm("s_cmp_lg_u64 %1, 0\n\ts_cselect_b32 %0, %2, 0" : "=s"(r) : "s"(m), "s"(bit) : "scc");
+  return r;
+}
+
 // Live rays of the packet: one ballot mask per ray slot r, and the lead ray (lowest r, then
 // lowest lane).
 template <int R>
@@ -307,7 +315,8 @@ template <bool ANY_HIT, bool STATS, int R>
 __device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref, const PacketRay<R>& ry,
                                            float tmin, uint32_t cur, float face, PacketLive<R>& pl, bool* found,
                                            HitRec* hit, Counters& cnt) {
-  const RT_CONST f4v* tq = (const RT_CONST f4v*)(tpool + (~ref));
+  // 32-bit byte offsets (pools are < 2 GiB): the scalar load takes them as its SGPR offset
+  const RT_CONST f4v* tq = (const RT_CONST f4v*)((const RT_CONST char*)tpool + (uint32_t)(~ref) * 48u);
   const f4v ta = tq[0], tb = tq[1], tc = tq[2];
   const uint32_t prim = __float_as_uint(ta.w);
 #pragma unroll
@@ -365,7 +374,7 @@ __device__ __forceinline__ uint32_t packet_slabs(const RT_CONST char* nb, const 
     uint64_t any = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) any |= hm[r][k];
-    ent |= any ? (1u << k) : 0u;
+    ent |= nonzero_bit(any, 1u << k);
   }
   return ent;
 }
@@ -379,7 +388,7 @@ template <bool STATS, int R>
 __device__ __forceinline__ int packet_tlas_node(const RT_CONST char* pool, int ref, const PacketRay<R>& ry,
                                                 float tmin, PacketLive<R>& pl, const HitRec* hit, WaveStack& stk,
                                                 int& sp, int cap, int& next, Counters& cnt) {
-  const RT_CONST char* nb = pool + ((size_t)(uint32_t)ref << 7);
+  const RT_CONST char* nb = pool + ((uint32_t)ref << 7);
   const i8v ch = *(const RT_CONST i8v*)(nb + 96);  // child[4], count, first_inner, inner_mask, pad
   const int cref[4] = {ch[0], ch[1], ch[2], ch[3]};
   uint64_t hm[R][4];
@@ -439,7 +448,7 @@ __device__ __forceinline__ int packet_blas_node(const RT_CONST char* pool, const
                                                 const PacketRay<R>& ry, float tmin, uint32_t cur, float face,
                                                 PacketLive<R>& pl, bool* found, HitRec* hit, WaveStack& stk, int& sp,
                                                 int cap, int& next, Counters& cnt) {
-  const RT_CONST char* nb = pool + ((size_t)(uint32_t)ref << 7);
+  const RT_CONST char* nb = pool + ((uint32_t)ref << 7);
   const i8v ch = *(const RT_CONST i8v*)(nb + 96);  // child[4], count, first_inner, inner_mask, pad
   const int cref[4] = {ch[0], ch[1], ch[2], ch[3]};
   uint64_t hm[R][4];
@@ -453,8 +462,8 @@ __device__ __forceinline__ int packet_blas_node(const RT_CONST char* pool, const
   while (tl) {
     const uint32_t k = (uint32_t)__builtin_ctz(tl);
     tl &= tl - 1u;
-    const int tr = k == 0 ? cref[0] : k == 1 ? cref[1] : k == 2 ? cref[2] : cref[3];
-    packet_tri<ANY_HIT, STATS, R>(tpool, tr, ry, tmin, cur, face, pl, found, hit, cnt);
+    const i4v c4 = {ch[0], ch[1], ch[2], ch[3]};
+    packet_tri<ANY_HIT, STATS, R>(tpool, c4[k], ry, tmin, cur, face, pl, found, hit, cnt);
   }
   if (ANY_HIT) {
     if (!pl.update()) return 2;
@@ -465,7 +474,7 @@ __device__ __forceinline__ int packet_blas_node(const RT_CONST char* pool, const
       uint64_t any = 0;
 #pragma unroll
       for (int r = 0; r < R; ++r) any |= hm[r][k] & pl.mask[r];
-      still |= any ? (1u << k) : 0u;
+      still |= nonzero_bit(any, 1u << k);
     }
     ent &= still;
   }
@@ -1018,8 +1027,11 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void k_trace_frame(SceneView 
 // keeps it to 80 VGPRs with 28 B of scratch); A/B: -2..6 % frame time on C2, C3, C4, C5 (+3 % on
 // C2F). REF and PRIMARY keep the allocator's choice (REF would spill hundreds of bytes; PRIMARY
 // measured neutral).
+#ifndef RT_LS_WAVES
+#define RT_LS_WAVES 6
+#endif
 template <int MODE, bool STATS, int R>
-__global__ __launch_bounds__(kBlock, (MODE == 1 && !STATS) ? 6 : 1) RT_TRACE_ATTR void k_trace_frame_packet(SceneView sc, FrameParams fp,
+__global__ __launch_bounds__(kBlock, (MODE == 1 && !STATS) ? RT_LS_WAVES : 1) RT_TRACE_ATTR void k_trace_frame_packet(SceneView sc, FrameParams fp,
                                                                const uint32_t* __restrict__ rows,
                                                                uint32_t* __restrict__ rgba8,
                                                                float4* __restrict__ rgba32f,
