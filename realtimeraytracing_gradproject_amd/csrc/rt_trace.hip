@@ -313,8 +313,8 @@ struct PacketRay {
 // a hit leaves the packet. Branch-free: selects instead of exec-mask regions.
 template <bool ANY_HIT, bool STATS, int R>
 __device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref, const PacketRay<R>& ry,
-                                           float tmin, uint32_t cur, float face, PacketLive<R>& pl, bool* found,
-                                           HitRec* hit, Counters& cnt) {
+                                           float tmin, uint32_t cur, float face, PacketLive<R>& pl, HitRec* hit,
+                                           Counters& cnt) {
   // 32-bit byte offsets (pools are < 2 GiB): the scalar load takes them as its SGPR offset
   const RT_CONST f4v* tq = (const RT_CONST f4v*)((const RT_CONST char*)tpool + (uint32_t)(~ref) * 48u);
   const f4v ta = tq[0], tb = tq[1], tc = tq[2];
@@ -328,12 +328,12 @@ __device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref
     HitRec& h = hit[r];
     const bool better = t < h.t || (t == h.t && (cur < h.inst || (cur == h.inst && prim < h.prim)));
     const bool take = pl.live[r] && ok && t >= tmin && better;
-    h.t = take ? t : h.t;
+    // an any-hit ray that accepts leaves the packet with t = -inf: every later slab test rejects it
+    h.t = take ? (ANY_HIT ? -__builtin_inff() : t) : h.t;
     h.u = take ? u : h.u;
     h.v = take ? v : h.v;
     h.inst = take ? cur : h.inst;
     h.prim = take ? prim : h.prim;
-    found[r] = found[r] || take;
     if (ANY_HIT) pl.live[r] = pl.live[r] && !take;
   }
 }
@@ -362,8 +362,8 @@ __device__ __forceinline__ uint32_t packet_slabs(const RT_CONST char* nb, const 
       const float tlz = __builtin_fmaf(loz[k], iv.z, no.z), thz = __builtin_fmaf(hiz[k], iv.z, no.z);
       const float n = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), tmin));
       const float f = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tbest));
-      const bool h = n <= f * 1.0000004f;  // dead rays are masked out of the ballot; only the lead's key is read
-      hm[r][k] = wave_ballot(h) & pl.mask[r];
+      const bool h = n <= f * 1.0000004f;  // only the lead's key is read
+      hm[r][k] = wave_ballot(h);  // dead rays carry tbest = -inf: their h is false
       vkey[r][k] = h ? (__float_as_uint(n) & 0x7fffffffu) : 0x7f800000u;
     }
     if (STATS && pl.live[r]) cnt.aabb += count;
@@ -446,8 +446,8 @@ __device__ __forceinline__ int packet_tlas_node(const RT_CONST char* pool, int r
 template <bool ANY_HIT, bool STATS, int R>
 __device__ __forceinline__ int packet_blas_node(const RT_CONST char* pool, const RT_CONST TriRec* tpool, int ref,
                                                 const PacketRay<R>& ry, float tmin, uint32_t cur, float face,
-                                                PacketLive<R>& pl, bool* found, HitRec* hit, WaveStack& stk, int& sp,
-                                                int cap, int& next, Counters& cnt) {
+                                                PacketLive<R>& pl, HitRec* hit, WaveStack& stk, int& sp, int cap,
+                                                int& next, Counters& cnt) {
   const RT_CONST char* nb = pool + ((uint32_t)ref << 7);
   const i8v ch = *(const RT_CONST i8v*)(nb + 96);  // child[4], count, first_inner, inner_mask, pad
   const int cref[4] = {ch[0], ch[1], ch[2], ch[3]};
@@ -463,7 +463,7 @@ __device__ __forceinline__ int packet_blas_node(const RT_CONST char* pool, const
     const uint32_t k = (uint32_t)__builtin_ctz(tl);
     tl &= tl - 1u;
     const i4v c4 = {ch[0], ch[1], ch[2], ch[3]};
-    packet_tri<ANY_HIT, STATS, R>(tpool, c4[k], ry, tmin, cur, face, pl, found, hit, cnt);
+    packet_tri<ANY_HIT, STATS, R>(tpool, c4[k], ry, tmin, cur, face, pl, hit, cnt);
   }
   if (ANY_HIT) {
     if (!pl.update()) return 2;
@@ -503,10 +503,11 @@ __device__ __forceinline__ int packet_blas_node(const RT_CONST char* pool, const
   return 1;
 }
 
-// Traces the R rays of every lane (o, d, alive per slot) as one packet; found[r] / hit[r] per ray.
-template <bool ANY_HIT, bool STATS, int R, bool CULL = false>
-__device__ void trace_packet(const SceneView& sc, const V3* o, const V3* d, float tmin, float tmax,
-                             const bool* alive, bool* found, HitRec* hit, Counters& cnt) {
+// The walk of trace_packet. Rays that are not alive start with t = -inf, so every slab test
+// rejects them and the ballots need no live mask.
+template <bool ANY_HIT, bool STATS, int R, bool CULL>
+__device__ __forceinline__ void packet_walk(const SceneView& sc, const V3* o, const V3* d, float tmin, float tmax,
+                                            const bool* alive, HitRec* hit, Counters& cnt) {
   const RT_CONST char* pool = (const RT_CONST char*)sc.pool_nodes;
   const RT_CONST TriRec* tpool = (const RT_CONST TriRec*)sc.pool_tris;
   const RT_CONST InstanceRec* ipool = (const RT_CONST InstanceRec*)sc.inst;
@@ -514,11 +515,10 @@ __device__ void trace_packet(const SceneView& sc, const V3* o, const V3* d, floa
   PacketRay<R> w;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    hit[r].t = tmax;
+    hit[r].t = alive[r] ? tmax : -__builtin_inff();
     hit[r].inst = 0xffffffffu;
     hit[r].prim = 0xffffffffu;
     hit[r].u = hit[r].v = 0.0f;
-    found[r] = false;
     pl.live[r] = alive[r];
     w.o[r] = o[r];
     w.d[r] = d[r];
@@ -559,8 +559,8 @@ __device__ void trace_packet(const SceneView& sc, const V3* o, const V3* d, floa
       int bref = (int)ir.pool_root;
       while (true) {
         // only internal nodes reach here: triangle children are tested inside packet_node
-        const int st = packet_blas_node<ANY_HIT, STATS, R>(pool, tpool, bref, b, tmin, cur, face, pl, found, hit,
-                                                           stk, sp, cap, next, cnt);
+        const int st = packet_blas_node<ANY_HIT, STATS, R>(pool, tpool, bref, b, tmin, cur, face, pl, hit, stk,
+                                                           sp, cap, next, cnt);
         if (st == 1) {
           bref = next;
           continue;
@@ -580,6 +580,17 @@ __device__ void trace_packet(const SceneView& sc, const V3* o, const V3* d, floa
     if (sp == 0) return;
     ref = stk.get(--sp);
   }
+}
+
+// Traces the R rays of every lane (o, d, alive per slot) as one packet; found[r] / hit[r] per ray
+// (a ray found a hit iff one was accepted: inst is set on acceptance only). Any-hit rays report
+// acceptance only (t is -inf once accepted).
+template <bool ANY_HIT, bool STATS, int R, bool CULL = false>
+__device__ void trace_packet(const SceneView& sc, const V3* o, const V3* d, float tmin, float tmax,
+                             const bool* alive, bool* found, HitRec* hit, Counters& cnt) {
+  packet_walk<ANY_HIT, STATS, R, CULL>(sc, o, d, tmin, tmax, alive, hit, cnt);
+#pragma unroll
+  for (int r = 0; r < R; ++r) found[r] = hit[r].inst != 0xffffffffu;
 }
 
 // Hit-instance data the shaders read (the reference binds it per hit group through the SBT).
