@@ -211,7 +211,7 @@ typedef struct {
   uint32_t count;
   int32_t first_inner; /* ref of the first internal child (consecutive refs in slot order), 0 if none */
   uint32_t inner_mask; /* bit k: child[k] >= 0 */
-  uint32_t pad;
+  uint32_t entry_base; /* first_inner << 8 | inner_mask << 4 (the device's packet-stack entry) */
 } o4node;
 typedef struct {
   float v0[3]; uint32_t prim;
@@ -338,6 +338,7 @@ static uint32_t collapse(const onode* bin, uint32_t nbin, o4node* out, uint32_t*
         nd.child[j] = r;
       }
       nd.count = valid;
+      nd.entry_base = ((uint32_t)nd.first_inner << 8) | (nd.inner_mask << 4);
       if (ps[head] + cnt - 1 > best) best = ps[head] + cnt - 1;
       out[head] = nd;
     }

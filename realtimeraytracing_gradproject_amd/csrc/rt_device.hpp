@@ -66,7 +66,8 @@ struct alignas(128) Bvh4Node {
                         // refs are consecutive in slot order (BFS allocation), so internal slot k
                         // is first_inner + popcount(inner_mask & ((1 << k) - 1))
   uint32_t inner_mask;  // bit k: child[k] is an internal node (>= 0)
-  uint32_t pad;
+  uint32_t entry_base;  // first_inner << 8 | inner_mask << 4: the packet walk's stack entry for this
+                        // node, OR-ed with the pending slots
 };
 static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node must be 128 B");
 

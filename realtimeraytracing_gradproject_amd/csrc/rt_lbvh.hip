@@ -423,7 +423,7 @@ __global__ __launch_bounds__(1024) void k_collapse(const BinNode* __restrict__ b
         }
         nd.count = valid;
         nd.inner_mask = inner;
-        nd.pad = 0;
+        nd.entry_base = ((uint32_t)nd.first_inner << 8) | (inner << 4);
         out[base + i] = nd;
       }
       next_total += chunk_total;
@@ -604,6 +604,7 @@ __global__ void k_pool_rebase(const Bvh4Node* __restrict__ src, uint32_t n, uint
     else if (tri_base >= 0) nd.child[k] = ~(int32_t)((int64_t)(~c) + tri_base);
   }
   if (nd.inner_mask) nd.first_inner += (int32_t)node_base;
+  nd.entry_base = ((uint32_t)nd.first_inner << 8) | (nd.inner_mask << 4);
   dst[i] = nd;
 }
 }  // namespace

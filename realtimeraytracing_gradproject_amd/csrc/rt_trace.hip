@@ -271,6 +271,58 @@ __device__ __forceinline__ uint64_t wave_ballot(bool p) { return __builtin_amdgc
 
 __device__ __forceinline__ f4v cld4(const RT_CONST char* p) { return *(const RT_CONST f4v*)p; }
 
+// -1 in every lane if bit k of the uniform m is set, else 0 (VALU: v_bfe_i32 on an SGPR operand;
+// keeps this per-child select off the scalar unit, the packet walk's tightest pipe)
+__device__ __forceinline__ uint32_t bit_mask_v(uint32_t m, int k) {
+  uint32_t r;
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(r) : "s"(m), "i"(k));
+  return r;
+}
+
+// Pushes entry_base | P with P = ent & ~nearest when P != 0: the write goes to lane sp, or to the
+// spare lane kPacketStack - 1 when nothing is pending, and sp advances by SCC (= P != 0): four
+// scalar instructions and one v_writelane (its lane select goes through m0, placed by the
+// compiler: gfx9 VOP3 reads one SGPR per instruction, so value and lane cannot both be SGPRs).
+__device__ __forceinline__ int push_entry(int stk, int& sp, uint32_t entry_base, uint32_t ent, uint32_t nearest) {
+  uint32_t p, e, lane;
+  asm volatile(
+      "s_andn2_b32 %0, %4, %5\n\t"
+      "s_cselect_b32 %3, %1, 63\n\t"
+      "s_addc_u32 %1, %1, 0\n\t"
+      "s_or_b32 %2, %6, %0"
+      : "=&s"(p), "+s"(sp), "=&s"(e), "=&s"(lane)
+      : "s"(ent), "s"(nearest), "s"(entry_base)
+      : "scc");
+  return amdgcn_writelane((int)e, (int)lane, stk);
+}
+
+// Pops the packet walk's top BLAS entry (sp > base): returns its lowest pending child
+// (first_inner + the internal children below that slot) and keeps the entry, minus that slot,
+// while slots remain. e & (e - 1) clears the lowest pending bit (the pending bits are the low
+// four and never all zero).
+__device__ __forceinline__ int pop_entry(int& stk, int& sp) {
+  const int top = sp - 1;
+  const uint32_t e = (uint32_t)__builtin_amdgcn_readlane(stk, top);
+  uint32_t ref, rest, lane, t0, t1;
+  asm volatile(
+      "s_ff1_i32_b32 %3, %6\n\t"
+      "s_bfm_b32 %3, %3, 4\n\t"
+      "s_and_b32 %3, %6, %3\n\t"
+      "s_bcnt1_i32_b32 %3, %3\n\t"
+      "s_lshr_b32 %0, %6, 8\n\t"
+      "s_add_u32 %0, %0, %3\n\t"
+      "s_add_u32 %4, %6, -1\n\t"
+      "s_and_b32 %1, %6, %4\n\t"
+      "s_and_b32 %4, %1, 15\n\t"
+      "s_cselect_b32 %2, %7, 63\n\t"
+      "s_cselect_b32 %5, %5, %7"
+      : "=&s"(ref), "=&s"(rest), "=&s"(lane), "=&s"(t0), "=&s"(t1), "+s"(sp)
+      : "s"(e), "s"(top)
+      : "scc");
+  stk = amdgcn_writelane((int)rest, (int)lane, stk);
+  return (int)ref;
+}
+
 // bit if the uniform 64-bit mask m is nonzero, else 0: s_cmp_lg_u64 + s_cselect_b32 (the
 // compiler otherwise round-trips the boolean through a VGPR and readfirstlane)
 __device__ __forceinline__ uint32_t nonzero_bit(uint64_t m, uint32_t bit) {
@@ -454,7 +506,7 @@ __device__ __forceinline__ int packet_blas_node(const RT_CONST char* pool, const
   uint64_t hm[R][4];
   uint32_t vkey[R][4];
   uint32_t ent = packet_slabs<STATS, R>(nb, ry, tmin, pl, hit, (uint32_t)ch[4], hm, vkey, cnt);
-  asm volatile("" ::"s"(ch[0]), "s"(ch[1]), "s"(ch[2]), "s"(ch[3]), "s"(ch[5]), "s"(ch[6]));
+  asm volatile("" ::"s"(ch[0]), "s"(ch[1]), "s"(ch[2]), "s"(ch[3]), "s"(ch[5]), "s"(ch[6]), "s"(ch[7]));
   if (ent == 0) return 0;
   const uint32_t imask = (uint32_t)ch[6];
   uint32_t tl = ent & ~imask;
@@ -481,12 +533,13 @@ __device__ __forceinline__ int packet_blas_node(const RT_CONST char* pool, const
   if (ent == 0) return 0;
   // per lane: the slot of its smallest key over the entered internal children (all-ones keys
   // elsewhere), lowest slot on ties; the lead lane's answer is the packet's
+  const uint32_t nent = ~ent;
   uint32_t idx = 0;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     uint32_t kk[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) kk[k] = vkey[r][k] | (((ent >> k) & 1u) - 1u);
+    for (int k = 0; k < 4; ++k) kk[k] = vkey[r][k] | bit_mask_v(nent, k);
     const uint32_t m = min(min(kk[0], kk[1]), min(kk[2], kk[3]));
     const uint32_t ir = kk[0] == m ? 0u : kk[1] == m ? 1u : kk[2] == m ? 2u : 3u;
     idx = (r == 0 || pl.lead_r == (uint32_t)r) ? ir : idx;
@@ -494,12 +547,10 @@ __device__ __forceinline__ int packet_blas_node(const RT_CONST char* pool, const
   const uint32_t ib = (uint32_t)__builtin_amdgcn_readlane((int)idx, (int)pl.lead_l);
   const uint32_t first = (uint32_t)ch[5];
   next = (int)(first + (uint32_t)__builtin_popcount(imask & ((1u << ib) - 1u)));
-  const uint32_t P = ent & ~(1u << ib);
-  if (STATS && P && sp + 1 > cap)  // never: cap bounds the entries (one per BLAS level)
+  if (STATS && (ent & ~(1u << ib)) && sp + 1 > cap)  // never: cap bounds the entries (one per BLAS level)
 #pragma unroll
     for (int r = 0; r < R; ++r) cnt.overflow += pl.live[r] ? 1u : 0u;
-  stk.put(P ? sp : kPacketStack - 1, (int)((first << 8) | (imask << 4) | P));
-  sp = __builtin_amdgcn_readfirstlane(sp + (P ? 1 : 0));
+  stk.v = push_entry(stk.v, sp, (uint32_t)ch[7], ent, 1u << ib);
   return 1;
 }
 
@@ -568,13 +619,7 @@ __device__ __forceinline__ void packet_walk(const SceneView& sc, const V3* o, co
         if (ANY_HIT && st == 2) return;
         if (sp == base) break;
         // top entry: its lowest pending slot is next; the entry stays while slots remain
-        const uint32_t e = (uint32_t)stk.get(sp - 1);
-        const uint32_t pend = e & 15u;
-        const uint32_t k = (uint32_t)__builtin_ctz(pend);
-        bref = (int)((e >> 8) + (uint32_t)__builtin_popcount((e >> 4) & ((1u << k) - 1u)));
-        const uint32_t rest = pend & (pend - 1u);
-        stk.put(rest ? sp - 1 : kPacketStack - 1, (int)((e & ~15u) | rest));
-        sp = __builtin_amdgcn_readfirstlane(rest ? sp : sp - 1);
+        bref = pop_entry(stk.v, sp);
       }
     }
     if (sp == 0) return;
