@@ -89,9 +89,20 @@ def cpu_baseline(spec, seconds: float):
         dt = time.perf_counter() - t0
         if dt >= seconds:
             break
+    # also one thread, and the host CPU model
+    t1 = time.perf_counter()
+    _, _, st1 = o.render_spec(spec, nthreads=1, want_float=False, schedule=1)
+    dt1 = time.perf_counter() - t1
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), None)
+    except OSError:
+        pass
     return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"{frames} full {spec.name} frame(s) {spec.width}x{spec.height} by oracle/rt_oracle.c "
-                      f"({threads} threads, {dt:.1f} s wall)"}
+                      f"({threads} threads, {dt:.1f} s wall)",
+            "single_thread": round(int(st1[0] + st1[1]) / dt1 / 1e6, 3), "host_cpus": ncpu, "cpu_model": model}
 
 
 def measure_config(name: str, steps: int, warmup: int, schedule: int) -> dict:

@@ -395,11 +395,10 @@ __device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref
 // entered set (children some live ray accepts). Unused slots hold lo = hi = +inf boxes that every
 // ray rejects: no validity mask.
 template <bool STATS, int R>
-__device__ __forceinline__ uint32_t packet_slabs(const RT_CONST char* nb, const PacketRay<R>& ry, float tmin,
+__device__ __forceinline__ uint32_t packet_slabs(const f4v (&pl6)[6], const PacketRay<R>& ry, float tmin,
                                                  const PacketLive<R>& pl, const HitRec* hit, uint32_t count,
                                                  uint64_t (&hm)[R][4], uint32_t (&vkey)[R][4], Counters& cnt) {
-  const f4v a0 = cld4(nb), a1 = cld4(nb + 16), a2 = cld4(nb + 32);
-  const f4v a3 = cld4(nb + 48), a4 = cld4(nb + 64), a5 = cld4(nb + 80);
+  const f4v a0 = pl6[0], a1 = pl6[1], a2 = pl6[2], a3 = pl6[3], a4 = pl6[4], a5 = pl6[5];
   const float lox[4] = {a0.x, a0.y, a0.z, a0.w}, hix[4] = {a1.x, a1.y, a1.z, a1.w};
   const float loy[4] = {a2.x, a2.y, a2.z, a2.w}, hiy[4] = {a3.x, a3.y, a3.z, a3.w};
   const float loz[4] = {a4.x, a4.y, a4.z, a4.w}, hiz[4] = {a5.x, a5.y, a5.z, a5.w};
@@ -445,7 +444,8 @@ __device__ __forceinline__ int packet_tlas_node(const RT_CONST char* pool, int r
   const int cref[4] = {ch[0], ch[1], ch[2], ch[3]};
   uint64_t hm[R][4];
   uint32_t vkey[R][4];
-  const uint32_t ent = packet_slabs<STATS, R>(nb, ry, tmin, pl, hit, (uint32_t)ch[4], hm, vkey, cnt);
+  const f4v planes[6] = {cld4(nb), cld4(nb + 16), cld4(nb + 32), cld4(nb + 48), cld4(nb + 64), cld4(nb + 80)};
+  const uint32_t ent = packet_slabs<STATS, R>(planes, ry, tmin, pl, hit, (uint32_t)ch[4], hm, vkey, cnt);
   // pin the child-ref load before the early exit: issued with the plane loads, it shares their
   // scalar-cache round trip instead of starting a second one after the slab tests
   asm volatile("" ::"s"(ch[0]), "s"(ch[1]), "s"(ch[2]), "s"(ch[3]));
@@ -505,7 +505,8 @@ __device__ __forceinline__ int packet_blas_node(const RT_CONST char* pool, const
   const int cref[4] = {ch[0], ch[1], ch[2], ch[3]};
   uint64_t hm[R][4];
   uint32_t vkey[R][4];
-  uint32_t ent = packet_slabs<STATS, R>(nb, ry, tmin, pl, hit, (uint32_t)ch[4], hm, vkey, cnt);
+  const f4v planes[6] = {cld4(nb), cld4(nb + 16), cld4(nb + 32), cld4(nb + 48), cld4(nb + 64), cld4(nb + 80)};
+  uint32_t ent = packet_slabs<STATS, R>(planes, ry, tmin, pl, hit, (uint32_t)ch[4], hm, vkey, cnt);
   asm volatile("" ::"s"(ch[0]), "s"(ch[1]), "s"(ch[2]), "s"(ch[3]), "s"(ch[5]), "s"(ch[6]), "s"(ch[7]));
   if (ent == 0) return 0;
   const uint32_t imask = (uint32_t)ch[6];
