@@ -1077,31 +1077,39 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void k_trace_frame(SceneView 
 }
 
 // Wave-packet frame kernel. A wave covers an 8 x 8R tile (ray r of lane l: column l % 8, row
-// entry 8r + l / 8 of the tile), a 256-thread workgroup 16 x 16R pixels. Every lane runs the
-// sample loop (rays outside the image or the row list join the packets dead) and stores only
+// entry 8r + l / 8 of the tile), a workgroup RT_PACKET_WX x RT_PACKET_WY tiles (2 x 1: 128
+// threads, 16 x 8R pixels; smaller workgroups shorten the tail of the launch). Every lane runs
+// the sample loop (rays outside the image or the row list join the packets dead) and stores only
 // in-image pixels.
-// Occupancy: LAMBERT_SHADOW (the perf configs) runs at 6 waves per SIMD (the register allocator
-// keeps it to 80 VGPRs with 28 B of scratch); A/B: -2..6 % frame time on C2, C3, C4, C5 (+3 % on
-// C2F). REF and PRIMARY keep the allocator's choice (REF would spill hundreds of bytes; PRIMARY
-// measured neutral).
+// Occupancy: LAMBERT_SHADOW (the perf configs) runs at 6 waves per SIMD (80 VGPRs, 13 spilled
+// outside the traversal loops); 5, 7 and 8 waves measured slower. REF and PRIMARY keep the
+// allocator's choice (REF would spill hundreds of bytes; PRIMARY measured neutral).
 #ifndef RT_LS_WAVES
 #define RT_LS_WAVES 6
 #endif
+#ifndef RT_PACKET_WX
+#define RT_PACKET_WX 2  // waves of a packet workgroup along x (8-pixel tiles)
+#endif
+#ifndef RT_PACKET_WY
+#define RT_PACKET_WY 1  // ... and along y (8R-row tiles); 2 x 1 measured best (C4/C5 -6 % vs 2 x 2)
+#endif
+constexpr int kPacketBlock = 64 * RT_PACKET_WX * RT_PACKET_WY;
 template <int MODE, bool STATS, int R>
-__global__ __launch_bounds__(kBlock, (MODE == 1 && !STATS) ? RT_LS_WAVES : 1) RT_TRACE_ATTR void k_trace_frame_packet(SceneView sc, FrameParams fp,
+__global__ __launch_bounds__(kPacketBlock) __attribute__((amdgpu_waves_per_eu((MODE == 1 && !STATS) ? RT_LS_WAVES : 1)))
+void k_trace_frame_packet(SceneView sc, FrameParams fp,
                                                                const uint32_t* __restrict__ rows,
                                                                uint32_t* __restrict__ rgba8,
                                                                float4* __restrict__ rgba32f,
                                                                unsigned long long* __restrict__ stats) {
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-  const uint32_t x = blockIdx.x * 16u + (w & 1u) * 8u + (lane & 7u);
+  const uint32_t x = blockIdx.x * (8u * RT_PACKET_WX) + (w % RT_PACKET_WX) * 8u + (lane & 7u);
   uint32_t px[R], py[R], orow[R];
   bool inimg[R];
   V3 acc[R], col[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     px[r] = x;
-    orow[r] = blockIdx.y * (16u * R) + (w >> 1) * (8u * R) + 8u * r + (lane >> 3);
+    orow[r] = blockIdx.y * (8u * R * RT_PACKET_WY) + (w / RT_PACKET_WX) * (8u * R) + 8u * r + (lane >> 3);
     inimg[r] = x < fp.width && orow[r] < fp.nrows;
     py[r] = 0;
     if (inimg[r]) py[r] = rows ? rows[orow[r]] : orow[r];
@@ -1173,8 +1181,9 @@ hipError_t launch_mode(const SceneView& sc, const FrameParams& fp, const uint32_
   dim3 grid((fp.width + 15) / 16, (fp.nrows + 15) / 16);
   if (schedule == RT_SCHED_PACKET && sc.packet_cap < kPacketStack) {
     constexpr int R = RT_PACKET_RAYS;
-    dim3 gp((fp.width + 15) / 16, (fp.nrows + 16 * R - 1) / (16 * R));
-    hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R>), gp, dim3(kBlock), 0, s, sc, fp, rows,
+    constexpr uint32_t tw = 8 * RT_PACKET_WX, th = 8 * R * RT_PACKET_WY;
+    dim3 gp((fp.width + tw - 1) / tw, (fp.nrows + th - 1) / th);
+    hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R>), gp, dim3(kPacketBlock), 0, s, sc, fp, rows,
                        (uint32_t*)rgba8, (float4*)rgba32f, stats);
   } else {
     size_t lds = (size_t)sc.lds_cap * kBlock * sizeof(int);
