@@ -49,6 +49,9 @@ __device__ __forceinline__ V3 ld3(const float* p) { return v3(p[0], p[1], p[2]);
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef int i4v __attribute__((ext_vector_type(4)));
 typedef int i8v __attribute__((ext_vector_type(8)));
+#ifndef RT_PACKET_OCT
+#define RT_PACKET_OCT 1  // uniform-octant BLAS walks load near/far planes directly (no min/max pairs)
+#endif
 template <typename T>
 __device__ __forceinline__ const RT_GLOBAL T* gp(const T* p) {
   return (const RT_GLOBAL T*)p;
@@ -394,7 +397,17 @@ __device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref
 // ray r accepts child k, vkey[r][k] = |entry distance| where accepted, else +inf. Returns the
 // entered set (children some live ray accepts). Unused slots hold lo = hi = +inf boxes that every
 // ray rejects: no validity mask.
-template <bool STATS, int R>
+// Byte offsets, inside a node, of the near and far plane rows of each axis for one ray octant.
+struct NodeOct {
+  uint32_t nx, fx, ny, fy, nz, fz;
+};
+
+// OCT: every live ray of the packet has the same direction octant and pl6 holds the planes in
+// {near x, far x, near y, far y, near z, far z} order (loaded through NodeOct offsets): the per-axis
+// min/max pairs disappear. fma is monotone in the plane, so min(fma(lo), fma(hi)) IS the near
+// plane's fma: the entry/exit distances, and so every decision and key, are bitwise those of the
+// min/max form (dead rays, whatever their octant, still carry tbest = -inf and reject).
+template <bool STATS, int R, bool OCT = false>
 __device__ __forceinline__ uint32_t packet_slabs(const f4v (&pl6)[6], const PacketRay<R>& ry, float tmin,
                                                  const PacketLive<R>& pl, const HitRec* hit, uint32_t count,
                                                  uint64_t (&hm)[R][4], uint32_t (&vkey)[R][4], Counters& cnt) {
@@ -411,8 +424,14 @@ __device__ __forceinline__ uint32_t packet_slabs(const f4v (&pl6)[6], const Pack
       const float tlx = __builtin_fmaf(lox[k], iv.x, no.x), thx = __builtin_fmaf(hix[k], iv.x, no.x);
       const float tly = __builtin_fmaf(loy[k], iv.y, no.y), thy = __builtin_fmaf(hiy[k], iv.y, no.y);
       const float tlz = __builtin_fmaf(loz[k], iv.z, no.z), thz = __builtin_fmaf(hiz[k], iv.z, no.z);
-      const float n = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), tmin));
-      const float f = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tbest));
+      float n, f;
+      if (OCT) {  // lo* hold the near planes, hi* the far planes
+        n = fmaxf(fmaxf(tlx, tly), fmaxf(tlz, tmin));
+        f = fminf(fminf(thx, thy), fminf(thz, tbest));
+      } else {
+        n = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), tmin));
+        f = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tbest));
+      }
       const bool h = n <= f * 1.0000004f;  // only the lead's key is read
       hm[r][k] = wave_ballot(h);  // dead rays carry tbest = -inf: their h is false
       vkey[r][k] = h ? (__float_as_uint(n) & 0x7fffffffu) : 0x7f800000u;
@@ -495,18 +514,29 @@ __device__ __forceinline__ int packet_tlas_node(const RT_CONST char* pool, int r
 // Internal child k's ref is first_inner + popcount(inner_mask below k) (BFS allocation).
 // Returns 1 with *next set, 0 when nothing is left to descend into, 2 when an any-hit packet has
 // no live ray left.
-template <bool ANY_HIT, bool STATS, int R>
+template <bool ANY_HIT, bool STATS, int R, bool OCT>
 __device__ __forceinline__ int packet_blas_node(const RT_CONST char* pool, const RT_CONST TriRec* tpool, int ref,
                                                 const PacketRay<R>& ry, float tmin, uint32_t cur, float face,
                                                 PacketLive<R>& pl, HitRec* hit, WaveStack& stk, int& sp, int cap,
-                                                int& next, Counters& cnt) {
+                                                int& next, const NodeOct& oc, Counters& cnt) {
   const RT_CONST char* nb = pool + ((uint32_t)ref << 7);
   const i8v ch = *(const RT_CONST i8v*)(nb + 96);  // child[4], count, first_inner, inner_mask, pad
   const int cref[4] = {ch[0], ch[1], ch[2], ch[3]};
   uint64_t hm[R][4];
   uint32_t vkey[R][4];
-  const f4v planes[6] = {cld4(nb), cld4(nb + 16), cld4(nb + 32), cld4(nb + 48), cld4(nb + 64), cld4(nb + 80)};
-  uint32_t ent = packet_slabs<STATS, R>(planes, ry, tmin, pl, hit, (uint32_t)ch[4], hm, vkey, cnt);
+  f4v planes[6];
+  if (OCT) {
+    planes[0] = cld4(nb + oc.nx);
+    planes[1] = cld4(nb + oc.fx);
+    planes[2] = cld4(nb + oc.ny);
+    planes[3] = cld4(nb + oc.fy);
+    planes[4] = cld4(nb + oc.nz);
+    planes[5] = cld4(nb + oc.fz);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 6; ++q) planes[q] = cld4(nb + 16 * q);
+  }
+  uint32_t ent = packet_slabs<STATS, R, OCT>(planes, ry, tmin, pl, hit, (uint32_t)ch[4], hm, vkey, cnt);
   asm volatile("" ::"s"(ch[0]), "s"(ch[1]), "s"(ch[2]), "s"(ch[3]), "s"(ch[5]), "s"(ch[6]), "s"(ch[7]));
   if (ent == 0) return 0;
   const uint32_t imask = (uint32_t)ch[6];
@@ -553,6 +583,30 @@ __device__ __forceinline__ int packet_blas_node(const RT_CONST char* pool, const
     for (int r = 0; r < R; ++r) cnt.overflow += pl.live[r] ? 1u : 0u;
   stk.v = push_entry(stk.v, sp, (uint32_t)ch[7], ent, 1u << ib);
   return 1;
+}
+
+// One BLAS walk of the packet (instance cur, object rays b) on the stack above `base`. Returns
+// false when an any-hit packet has no live ray left.
+template <bool ANY_HIT, bool STATS, int R, bool OCT>
+__device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, const RT_CONST TriRec* tpool, int bref,
+                                                 const PacketRay<R>& b, float tmin, uint32_t cur, float face,
+                                                 PacketLive<R>& pl, HitRec* hit, WaveStack& stk, int& sp, int cap,
+                                                 const NodeOct& oc, Counters& cnt) {
+  const int base = sp;
+  while (true) {
+    // only internal nodes reach here: triangle children are tested inside packet_blas_node
+    int next;
+    const int st = packet_blas_node<ANY_HIT, STATS, R, OCT>(pool, tpool, bref, b, tmin, cur, face, pl, hit, stk, sp,
+                                                            cap, next, oc, cnt);
+    if (st == 1) {
+      bref = next;
+      continue;
+    }
+    if (ANY_HIT && st == 2) return false;
+    if (sp == base) return true;
+    // top entry: its lowest pending slot is next; the entry stays while slots remain
+    bref = pop_entry(stk.v, sp);
+  }
 }
 
 // The walk of trace_packet. Rays that are not alive start with t = -inf, so every slab test
@@ -607,21 +661,25 @@ __device__ __forceinline__ void packet_walk(const SceneView& sc, const V3* o, co
         b.noinv[r] = neg(mul(b.o[r], b.invd[r]));
       }
       const float face = CULL ? (ir.flip ? -1.0f : 1.0f) * sc.cull_sense : 0.0f;
-      const int base = sp;
-      int bref = (int)ir.pool_root;
-      while (true) {
-        // only internal nodes reach here: triangle children are tested inside packet_node
-        const int st = packet_blas_node<ANY_HIT, STATS, R>(pool, tpool, bref, b, tmin, cur, face, pl, hit, stk,
-                                                           sp, cap, next, cnt);
-        if (st == 1) {
-          bref = next;
-          continue;
-        }
-        if (ANY_HIT && st == 2) return;
-        if (sp == base) break;
-        // top entry: its lowest pending slot is next; the entry stays while slots remain
-        bref = pop_entry(stk.v, sp);
+      // one direction octant for every live object ray: near/far planes picked by load offsets
+      bool uni = false;
+      NodeOct oc{0u, 16u, 32u, 48u, 64u, 80u};
+#if RT_PACKET_OCT
+      if (R == 1) {
+        const uint64_t live = pl.mask[0];
+        const uint64_t sx = wave_ballot((int)__float_as_uint(b.invd[0].x) < 0) & live;
+        const uint64_t sy = wave_ballot((int)__float_as_uint(b.invd[0].y) < 0) & live;
+        const uint64_t sz = wave_ballot((int)__float_as_uint(b.invd[0].z) < 0) & live;
+        uni = (sx == 0 || sx == live) && (sy == 0 || sy == live) && (sz == 0 || sz == live);
+        const uint32_t ox = sx ? 16u : 0u, oy = sy ? 16u : 0u, oz = sz ? 16u : 0u;
+        oc = NodeOct{ox, 16u - ox, 32u + oy, 48u - oy, 64u + oz, 80u - oz};
       }
+#endif
+      const bool more = uni ? packet_blas_walk<ANY_HIT, STATS, R, true>(pool, tpool, (int)ir.pool_root, b, tmin, cur,
+                                                                          face, pl, hit, stk, sp, cap, oc, cnt)
+                            : packet_blas_walk<ANY_HIT, STATS, R, false>(pool, tpool, (int)ir.pool_root, b, tmin,
+                                                                           cur, face, pl, hit, stk, sp, cap, oc, cnt);
+      if (ANY_HIT && !more) return;
     }
     if (sp == 0) return;
     ref = stk.get(--sp);
