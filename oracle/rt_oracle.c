@@ -836,11 +836,17 @@ static int opk_node(const o4node* nd, const opkray* ry, float tmin, ohit* h, int
   }
   uint32_t key[4];
   for (int k = 0; k < 4; ++k) key[k] = ((ent >> k) & 1u) ? vkey[*lead][k] : 0xffffffffu;
-  /* nearest first (lowest slot on ties), the other entered children pushed in descending slot order */
+  /* nearest first (lowest slot on ties), the other entered children pushed in descending slot order;
+   * any-hit BLAS nodes skip the distance order: the lowest entered slot goes first */
   uint32_t kb = key[0];
   int rb = nd->child[0], ib = 0;
-  for (int k = 1; k < 4; ++k)
-    if (key[k] < kb) { kb = key[k]; rb = nd->child[k]; ib = k; }
+  if (leaves && any) {
+    ib = __builtin_ctz(ent);
+    rb = nd->child[ib];
+  } else {
+    for (int k = 1; k < 4; ++k)
+      if (key[k] < kb) { kb = key[k]; rb = nd->child[k]; ib = k; }
+  }
   const uint32_t P = ent & ~(1u << ib);
   if (*sp + __builtin_popcount(P) > cap) /* never: cap is the exact worst case; counted per live lane */
     for (int l = 0; l < OPK; ++l) st->v[5] += live[l] ? 1u : 0u;
