@@ -326,6 +326,24 @@ __device__ __forceinline__ int pop_entry(int& stk, int& sp) {
   return (int)ref;
 }
 
+// Bit k set iff the uniform 64-bit mask m[k] is nonzero: s_cmp_lg_u64 sets SCC and
+// s_addc_u32 acc, acc, acc shifts it in (children 3..0), two scalar instructions per child.
+__device__ __forceinline__ uint32_t nonzero_mask4(const uint64_t (&m)[4]) {
+  uint32_t r;
+  asm("s_cmp_lg_u64 %1, 0\n\t"
+      "s_addc_u32 %0, 0, 0\n\t"
+      "s_cmp_lg_u64 %2, 0\n\t"
+      "s_addc_u32 %0, %0, %0\n\t"
+      "s_cmp_lg_u64 %3, 0\n\t"
+      "s_addc_u32 %0, %0, %0\n\t"
+      "s_cmp_lg_u64 %4, 0\n\t"
+      "s_addc_u32 %0, %0, %0"
+      : "=&s"(r)
+      : "s"(m[3]), "s"(m[2]), "s"(m[1]), "s"(m[0])
+      : "scc");
+  return r;
+}
+
 // bit if the uniform 64-bit mask m is nonzero, else 0: s_cmp_lg_u64 + s_cselect_b32 (the
 // compiler otherwise round-trips the boolean through a VGPR and readfirstlane)
 __device__ __forceinline__ uint32_t nonzero_bit(uint64_t m, uint32_t bit) {
@@ -438,15 +456,14 @@ __device__ __forceinline__ uint32_t packet_slabs(const f4v (&pl6)[6], const Pack
     }
     if (STATS && pl.live[r]) cnt.aabb += count;
   }
-  uint32_t ent = 0;
+  uint64_t any[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    uint64_t any = 0;
+    any[k] = 0;
 #pragma unroll
-    for (int r = 0; r < R; ++r) any |= hm[r][k];
-    ent |= nonzero_bit(any, 1u << k);
+    for (int r = 0; r < R; ++r) any[k] |= hm[r][k];
   }
-  return ent;
+  return nonzero_mask4(any);
 }
 
 // TLAS node of the packet walk (children: TLAS nodes and instance leaves). The entered children go
@@ -541,13 +558,14 @@ __device__ __forceinline__ int packet_blas_node(const RT_CONST char* pool, const
   const uint32_t imask = (uint32_t)ch[6];
   uint32_t tl = ent & ~imask;
   ent &= imask;
+  const bool tested = tl != 0;
   while (tl) {
     const uint32_t k = (uint32_t)__builtin_ctz(tl);
     tl &= tl - 1u;
     const i4v c4 = {ch[0], ch[1], ch[2], ch[3]};
     packet_tri<ANY_HIT, STATS, R>(tpool, c4[k], ry, tmin, cur, face, pl, hit, cnt);
   }
-  if (ANY_HIT) {
+  if (ANY_HIT && tested) {  // rays can only have left the packet in a triangle test
     if (!pl.update()) return 2;
     // children only finished rays wanted are dropped
     uint32_t still = 0;
