@@ -46,8 +46,9 @@ STRIP_ROWS = D.STRIP_ROWS
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=100,
+                   help="untimed frames first: the GPU needs ~20 ms of load to reach steady clocks")
     p.add_argument("--config", default="C2", choices=[c for c in scenes.CONFIGS])
     p.add_argument("--schedule", default="packet", choices=["packet", "lane"])
     p.add_argument("--no-cpu-baseline", action="store_true")
