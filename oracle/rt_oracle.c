@@ -303,8 +303,105 @@ static int gather4(const onode* bin, int root, int ref[4], float box[4][6]) {
   return cnt;
 }
 
-/* collapse the binary tree into 4-wide nodes (greedy largest-area opening), BFS order (k_collapse) */
+/* ---- SAH-optimal collapse (k_refit sah_dp + k_collapse gather4_dp in rt_lbvh.hip) -------------
+ * cost(collapse) = sum of the half areas of its wide nodes: a wide node's visit tests all four
+ * slots, and every triangle is tested under the same conditions in any collapse. C(n, i): least
+ * cost of the subtree of binary node n as at most i slot roots; D(n, i) = min_j C(c0, j) +
+ * C(c1, i - j); C(n, 1) = A(n) + D(n, 4); C(n, i) = min(C(n, 1), D(n, i)); ties keep the lowest j.
+ * ORACLE_GREEDY_COLLAPSE=1 selects the earlier greedy largest-area opening (gather4) instead. */
+static float* g_dpC;    /* [nbin][5] */
+static int8_t* g_dpS;   /* [nbin][5]: 0 = n is a wide node, j > 0 = left gets j slots */
+static int dp_on = -1;
+
+static void dp_prepare(const onode* bin, uint32_t nbin) {
+  g_dpC = (float*)malloc((size_t)nbin * 5 * sizeof(float));
+  g_dpS = (int8_t*)malloc((size_t)nbin * 5);
+  int* st = (int*)malloc((size_t)nbin * 2 * sizeof(int) + 8);
+  int top = 0;
+  st[top++] = 0;
+  int* order = (int*)malloc((size_t)nbin * sizeof(int) + 4);
+  int no = 0;
+  while (top) {  /* pre-order, reversed below = children before parents */
+    const int v = st[--top];
+    order[no++] = v;
+    if (bin[v].c0 >= 0) st[top++] = bin[v].c0;
+    if (bin[v].c1 >= 0) st[top++] = bin[v].c1;
+  }
+  for (int q = no - 1; q >= 0; --q) {
+    const int v = order[q];
+    const onode* b = &bin[v];
+    float bb[6];
+    for (int a = 0; a < 3; ++a) {
+      bb[a] = fminf(b->lo0[a], b->lo1[a]);
+      bb[3 + a] = fmaxf(b->hi0[a], b->hi1[a]);
+    }
+    float cl[5], cr[5];
+    for (int i = 1; i <= 4; ++i) {
+      cl[i] = b->c0 >= 0 ? g_dpC[b->c0 * 5 + i] : 0.0f;
+      cr[i] = b->c1 >= 0 ? g_dpC[b->c1 * 5 + i] : 0.0f;
+    }
+    float D[5];
+    int8_t J[5];
+    for (int i = 2; i <= 4; ++i) {
+      D[i] = INFINITY; J[i] = 1;
+      for (int j = 1; j < i; ++j) {
+        const float c = cl[j] + cr[i - j];
+        if (c < D[i]) { D[i] = c; J[i] = (int8_t)j; }
+      }
+    }
+    const float self = half_area(bb) + D[4];
+    g_dpC[v * 5 + 1] = self; g_dpS[v * 5 + 1] = 0;
+    for (int i = 2; i <= 4; ++i) {
+      if (D[i] < self) { g_dpC[v * 5 + i] = D[i]; g_dpS[v * 5 + i] = J[i]; }
+      else { g_dpC[v * 5 + i] = self; g_dpS[v * 5 + i] = 0; }
+    }
+  }
+  free(order); free(st);
+}
+
+/* slot roots of the subtree of binary ref c (leaf or internal) with k slots, left first */
+static void dp_expand(const onode* bin, int c, const float* cbox, int k, int* ref, float (*box)[6], int* cnt) {
+  if (c < 0 || g_dpS[c * 5 + k] == 0) {
+    ref[*cnt] = c;
+    memcpy(box[*cnt], cbox, 24);
+    ++*cnt;
+    return;
+  }
+  const onode* b = &bin[c];
+  const int j = g_dpS[c * 5 + k];
+  float l[6] = {b->lo0[0], b->lo0[1], b->lo0[2], b->hi0[0], b->hi0[1], b->hi0[2]};
+  float r[6] = {b->lo1[0], b->lo1[1], b->lo1[2], b->hi1[0], b->hi1[1], b->hi1[2]};
+  dp_expand(bin, b->c0, l, j, ref, box, cnt);
+  dp_expand(bin, b->c1, r, k - j, ref, box, cnt);
+}
+
+static int gather4_dp(const onode* bin, int root, int ref[4], float box[4][6]) {
+  const onode* b = &bin[root];
+  /* root is a wide node: distribute its 4 slots as D(root, 4) chose */
+  float cl[5], cr[5];
+  for (int i = 1; i <= 4; ++i) {
+    cl[i] = b->c0 >= 0 ? g_dpC[b->c0 * 5 + i] : 0.0f;
+    cr[i] = b->c1 >= 0 ? g_dpC[b->c1 * 5 + i] : 0.0f;
+  }
+  int bj = 1;
+  float bc = INFINITY;
+  for (int jj = 1; jj < 4; ++jj) {
+    const float c = cl[jj] + cr[4 - jj];
+    if (c < bc) { bc = c; bj = jj; }
+  }
+  float l[6] = {b->lo0[0], b->lo0[1], b->lo0[2], b->hi0[0], b->hi0[1], b->hi0[2]};
+  float r[6] = {b->lo1[0], b->lo1[1], b->lo1[2], b->hi1[0], b->hi1[1], b->hi1[2]};
+  int cnt = 0;
+  dp_expand(bin, b->c0, l, bj, ref, box, &cnt);
+  dp_expand(bin, b->c1, r, 4 - bj, ref, box, &cnt);
+  return cnt;
+}
+
+/* collapse the binary tree into 4-wide nodes (SAH DP, or greedy largest-area opening), BFS order
+ * (k_collapse) */
 static uint32_t collapse(const onode* bin, uint32_t nbin, o4node* out, uint32_t* count, uint32_t* max_stack) {
+  if (dp_on < 0) dp_on = getenv("ORACLE_GREEDY_COLLAPSE") == NULL;
+  if (dp_on) dp_prepare(bin, nbin);
   int* q = (int*)malloc((size_t)nbin * sizeof(int) + sizeof(int));
   int* ps = (int*)calloc((size_t)nbin + 1, sizeof(int)); /* siblings left on the stack above a node */
   int best = 0;
@@ -316,7 +413,7 @@ static uint32_t collapse(const onode* bin, uint32_t nbin, o4node* out, uint32_t*
     for (; head < level_end; ++head) {
       int ref[4];
       float box[4][6];
-      const int cnt = gather4(bin, q[head], ref, box);
+      const int cnt = dp_on ? gather4_dp(bin, q[head], ref, box) : gather4(bin, q[head], ref, box);
       o4node nd;
       memset(&nd, 0, sizeof(nd));
       uint32_t valid = 0;
@@ -348,6 +445,7 @@ static uint32_t collapse(const onode* bin, uint32_t nbin, o4node* out, uint32_t*
   *max_stack = (uint32_t)best;
   free(ps);
   free(q);
+  if (dp_on) { free(g_dpC); free(g_dpS); }
   return depth;
 }
 

@@ -19,6 +19,10 @@
 
 #include "rt_internal.hpp"
 
+#ifndef RT_SAH_COLLAPSE
+#define RT_SAH_COLLAPSE 1  // SAH-optimal binary -> BVH4 collapse (DP); 0: greedy largest-area opening
+#endif
+
 namespace rt {
 namespace {
 
@@ -232,9 +236,54 @@ __device__ __forceinline__ void load_box(int c, const float* __restrict__ nbox,
 
 // 5. bottom-up refit. The second arrival at a node computes its box. Hand-off follows the
 // agent-scope release -> counter -> acquire protocol (node boxes may be cached on other XCDs).
+__device__ __forceinline__ float half_area6(const float* b) {
+  const float dx = b[3] - b[0], dy = b[4] - b[1], dz = b[5] - b[2];
+  return (dx * dy + dy * dz) + dz * dx;
+}
+
+// SAH-optimal collapse DP at binary node `node` with box bb and children c0, c1 (>= 0: internal,
+// DP already final; < 0: a triangle / instance leaf, cost 0). The cost of a collapse is the sum of
+// its wide nodes' half areas: a wide node's visit tests all four slots, and every triangle is tested
+// under the same conditions whatever the collapse. C(n, i) = least cost of n's subtree as at most i
+// slot roots: D(n, i) = min_j C(c0, j) + C(c1, i - j), C(n, 1) = A(n) + D(n, 4) (n is a wide node),
+// C(n, i) = min(C(n, 1), D(n, i)). dpc[n] = C(n, 1..4); dps[n] byte i-1 = 0 when n is a wide node
+// for i slots, else j (the slots of c0). Strict < keeps the lowest j; oracle dp_prepare is the same
+// arithmetic in the same order.
+__device__ __forceinline__ void sah_dp(int node, const float* bb, int c0, int c1, float4* __restrict__ dpc,
+                                       uint32_t* __restrict__ dps) {
+  const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  const float4 l = c0 >= 0 ? dpc[c0] : zero, r = c1 >= 0 ? dpc[c1] : zero;
+  const float cl[5] = {0.0f, l.x, l.y, l.z, l.w}, cr[5] = {0.0f, r.x, r.y, r.z, r.w};
+  float D[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  uint32_t J[5] = {0, 0, 0, 0, 0};
+  for (int i = 2; i <= 4; ++i) {
+    D[i] = INFINITY;
+    J[i] = 1;
+    for (int j = 1; j < i; ++j) {
+      const float c = cl[j] + cr[i - j];
+      if (c < D[i]) {
+        D[i] = c;
+        J[i] = (uint32_t)j;
+      }
+    }
+  }
+  const float self = half_area6(bb) + D[4];
+  float C[5];
+  uint32_t S = 0;
+  C[1] = self;
+  for (int i = 2; i <= 4; ++i) {
+    const bool split = D[i] < self;
+    C[i] = split ? D[i] : self;
+    S |= (split ? J[i] : 0u) << (8 * (i - 1));
+  }
+  dpc[node] = make_float4(C[1], C[2], C[3], C[4]);
+  dps[node] = S;
+}
+
 __global__ void k_refit(int n, const int* __restrict__ parent_leaf, const int* __restrict__ parent_int,
                         const int* __restrict__ child, const float* __restrict__ primbox,
-                        const uint32_t* __restrict__ sorted, float* nbox, uint32_t* flags) {
+                        const uint32_t* __restrict__ sorted, float* nbox, uint32_t* flags,
+                        float4* __restrict__ dpc, uint32_t* __restrict__ dps) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   int node = parent_leaf[i];
@@ -249,10 +298,13 @@ __global__ void k_refit(int n, const int* __restrict__ parent_leaf, const int* _
     load_box(child[2 * node], nbox, primbox, sorted, a);
     load_box(child[2 * node + 1], nbox, primbox, sorted, b);
     float* o = nbox + (size_t)node * 6;
+    float bb[6];
     for (int k = 0; k < 3; ++k) {
-      o[k] = fminf(a[k], b[k]);
-      o[3 + k] = fmaxf(a[3 + k], b[3 + k]);
+      bb[k] = fminf(a[k], b[k]);
+      bb[3 + k] = fmaxf(a[3 + k], b[3 + k]);
     }
+    for (int k = 0; k < 6; ++k) o[k] = bb[k];
+    if (dpc) sah_dp(node, bb, child[2 * node], child[2 * node + 1], dpc, dps);
     node = parent_int[node];
   }
 }
@@ -295,7 +347,8 @@ __global__ void k_single(const float* __restrict__ primbox, bool leaf_ref_is_pri
   nodes[0] = nd;
 }
 
-// 7. collapse the binary tree into 4-wide nodes in BFS order (children chosen by gather4). One
+// 7. collapse the binary tree into 4-wide nodes in BFS order (children chosen by gather4_dp from
+// the SAH DP of k_refit; gather4, the greedy largest-area opening, with RT_SAH_COLLAPSE=0). One
 // workgroup walks the levels; each level's new node indices come from a block-wide exclusive
 // scan of per-node internal-child counts (deterministic, no atomics), so the oracle's sequential
 // BFS yields the same array. Unused slots get kEmptyChild and the box lo = hi = +inf, which
@@ -350,7 +403,74 @@ __device__ __forceinline__ int gather4(const BinNode* __restrict__ bin, int root
   return cnt;
 }
 
-__global__ __launch_bounds__(1024) void k_collapse(const BinNode* __restrict__ bin, Bvh4Node* __restrict__ out,
+// Children of the 4-wide node rooted at binary node `root` under the collapse DP: the root's four
+// slots split between its children as D(root, 4) chose, each child expanded while its choice for
+// its slot count is a split (left first; mirrors oracle gather4_dp / dp_expand).
+__device__ __forceinline__ int gather4_dp(const BinNode* __restrict__ bin, const float4* __restrict__ dpc,
+                                          const uint32_t* __restrict__ dps, int root, int ref[4], float box[4][6]) {
+  const BinNode& b = bin[root];
+  const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  const float4 l = b.c0 >= 0 ? dpc[b.c0] : zero, r = b.c1 >= 0 ? dpc[b.c1] : zero;
+  const float cl[4] = {l.x, l.y, l.z, l.w}, cr[4] = {r.x, r.y, r.z, r.w};
+  int bj = 1;
+  float bc = INFINITY;
+  for (int j = 1; j < 4; ++j) {
+    const float c = cl[j - 1] + cr[4 - j - 1];
+    if (c < bc) {
+      bc = c;
+      bj = j;
+    }
+  }
+  // explicit stack of (ref, slots, box); right pushed before left so slots come out left first
+  int sref[4], sk[4];
+  float sbox[4][6];
+  int top = 0;
+  sref[top] = b.c1;
+  sk[top] = 4 - bj;
+  for (int a = 0; a < 3; ++a) {
+    sbox[top][a] = b.lo1[a];
+    sbox[top][3 + a] = b.hi1[a];
+  }
+  ++top;
+  sref[top] = b.c0;
+  sk[top] = bj;
+  for (int a = 0; a < 3; ++a) {
+    sbox[top][a] = b.lo0[a];
+    sbox[top][3 + a] = b.hi0[a];
+  }
+  ++top;
+  int cnt = 0;
+  while (top > 0) {
+    --top;
+    const int c = sref[top], k = sk[top];
+    const uint32_t j = c >= 0 ? (dps[c] >> (8 * (k - 1))) & 0xffu : 0u;
+    if (j == 0) {
+      ref[cnt] = c;
+      for (int a = 0; a < 6; ++a) box[cnt][a] = sbox[top][a];
+      ++cnt;
+      continue;
+    }
+    const BinNode& g = bin[c];
+    sref[top] = g.c1;
+    sk[top] = k - (int)j;
+    for (int a = 0; a < 3; ++a) {
+      sbox[top][a] = g.lo1[a];
+      sbox[top][3 + a] = g.hi1[a];
+    }
+    ++top;
+    sref[top] = g.c0;
+    sk[top] = (int)j;
+    for (int a = 0; a < 3; ++a) {
+      sbox[top][a] = g.lo0[a];
+      sbox[top][3 + a] = g.hi0[a];
+    }
+    ++top;
+  }
+  return cnt;
+}
+
+__global__ __launch_bounds__(1024) void k_collapse(const BinNode* __restrict__ bin, const float4* __restrict__ dpc,
+                                                   const uint32_t* __restrict__ dps, Bvh4Node* __restrict__ out,
                                                    int* la, int* lb, int* ps, uint32_t* __restrict__ info) {
   __shared__ int scan[1024];
   __shared__ int s_maxstack;
@@ -374,7 +494,7 @@ __global__ __launch_bounds__(1024) void k_collapse(const BinNode* __restrict__ b
       int ref[4];
       float box[4][6];
       int cnt = 0;
-      if (valid) cnt = gather4(bin, cur[i], ref, box);
+      if (valid) cnt = dpc ? gather4_dp(bin, dpc, dps, cur[i], ref, box) : gather4(bin, cur[i], ref, box);
       int m = 0;
       for (int j = 0; j < cnt; ++j) m += ref[j] >= 0;
       scan[tid] = m;
@@ -523,7 +643,7 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
   RT_TRY(hipEventRecord(e0, s));
   const uint32_t nblocks = (n + kRsTile - 1) / kRsTile;
   const uint32_t nbin = n > 1 ? n - 1 : 1;
-  DevBuf stats, keys0, keys1, vals1, hist, child, pint, pleaf, nbox, flags, info, bin, la, lb, ps;
+  DevBuf stats, keys0, keys1, vals1, hist, child, pint, pleaf, nbox, flags, info, bin, la, lb, ps, dpc, dps;
   RT_TRY(hipMalloc(&stats.p, 12 * sizeof(float)));
   RT_TRY(hipMalloc(&keys0.p, (size_t)n * 4));
   RT_TRY(hipMalloc(&keys1.p, (size_t)n * 4));
@@ -565,13 +685,19 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
     RT_TRY(hipMalloc(&flags.p, (size_t)(n - 1) * 4));
     RT_TRY(hipMemsetAsync(flags.p, 0, (size_t)(n - 1) * 4, s));
     k_karras<<<grid1(n - 1, 256), 256, 0, s>>>(ka, (int)n, (int*)child.p, (int*)pint.p, (int*)pleaf.p);
+    if (RT_SAH_COLLAPSE) {
+      RT_TRY(hipMalloc(&dpc.p, (size_t)(n - 1) * sizeof(float4)));
+      RT_TRY(hipMalloc(&dps.p, (size_t)(n - 1) * 4));
+    }
     k_refit<<<grid1(n, 256), 256, 0, s>>>((int)n, (int*)pleaf.p, (int*)pint.p, (int*)child.p, d_primbox,
-                                          d_sorted, (float*)nbox.p, (uint32_t*)flags.p);
+                                          d_sorted, (float*)nbox.p, (uint32_t*)flags.p, (float4*)dpc.p,
+                                          (uint32_t*)dps.p);
     k_pack<<<grid1(n - 1, 256), 256, 0, s>>>((int)n, (int*)child.p, (float*)nbox.p, d_primbox, d_sorted,
                                              leaf_ref_is_prim, d_bin);
     RT_TRY(hipGetLastError());
   }
-  k_collapse<<<1, 1024, 0, s>>>(d_bin, d_nodes, (int*)la.p, (int*)lb.p, (int*)ps.p, (uint32_t*)info.p);
+  k_collapse<<<1, 1024, 0, s>>>(d_bin, (const float4*)dpc.p, (const uint32_t*)dps.p, d_nodes, (int*)la.p,
+                                (int*)lb.p, (int*)ps.p, (uint32_t*)info.p);
   RT_TRY(hipGetLastError());
   RT_TRY(hipEventRecord(e1, s));
   float hb[12];
