@@ -486,26 +486,22 @@ __device__ __forceinline__ int packet_tlas_node(const RT_CONST char* pool, int r
   // scalar-cache round trip instead of starting a second one after the slab tests
   asm volatile("" ::"s"(ch[0]), "s"(ch[1]), "s"(ch[2]), "s"(ch[3]));
   if (ent == 0) return 0;
-  // uniform keys: the lead ray's key, all-ones where the child is not descended into
-  uint32_t key[4];
+  // nearest entered child by the lead ray's key, lowest slot on ties: per lane in VALU (keys
+  // masked to the entered set), one readlane
+  const uint32_t nent = ~ent;
+  uint32_t idx = 0;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    uint32_t vk = vkey[0][k];
+  for (int r = 0; r < R; ++r) {
+    uint32_t kk[4];
 #pragma unroll
-    for (int r = 1; r < R; ++r) vk = pl.lead_r == (uint32_t)r ? vkey[r][k] : vk;
-    const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)vk, (int)pl.lead_l);
-    key[k] = ((ent >> k) & 1u) ? kl : 0xffffffffu;
+    for (int k = 0; k < 4; ++k) kk[k] = vkey[r][k] | bit_mask_v(nent, k);
+    const uint32_t m = min(min(kk[0], kk[1]), min(kk[2], kk[3]));
+    const uint32_t ir = kk[0] == m ? 0u : kk[1] == m ? 1u : kk[2] == m ? 2u : 3u;
+    idx = (r == 0 || pl.lead_r == (uint32_t)r) ? ir : idx;
   }
-  uint32_t kb = key[0];
-  int rb = cref[0];
-  uint32_t ib = 0;
-#pragma unroll
-  for (int k = 1; k < 4; ++k) {
-    const bool s = key[k] < kb;
-    kb = s ? key[k] : kb;
-    rb = s ? cref[k] : rb;
-    ib = s ? (uint32_t)k : ib;
-  }
+  const uint32_t ib = (uint32_t)__builtin_amdgcn_readlane((int)idx, (int)pl.lead_l);
+  const i4v c4 = {ch[0], ch[1], ch[2], ch[3]};
+  const int rb = c4[ib];
   // pushed set P (entered, not the nearest) as a 4-bit mask; descending slot order puts child k
   // at sp + popcount(P >> (k + 1)), so the four writes are independent of each other
   const uint32_t P = ent & ~(1u << ib);
