@@ -935,10 +935,10 @@ static int opk_node(const o4node* nd, const opkray* ry, float tmin, ohit* h, int
   uint32_t key[4];
   for (int k = 0; k < 4; ++k) key[k] = ((ent >> k) & 1u) ? vkey[*lead][k] : 0xffffffffu;
   /* nearest first (lowest slot on ties), the other entered children pushed in descending slot order;
-   * any-hit BLAS nodes skip the distance order: the lowest entered slot goes first */
+   * any-hit nodes skip the distance order: the lowest entered slot goes first */
   uint32_t kb = key[0];
   int rb = nd->child[0], ib = 0;
-  if (leaves && any) {
+  if (any) {
     ib = __builtin_ctz(ent);
     rb = nd->child[ib];
   } else {

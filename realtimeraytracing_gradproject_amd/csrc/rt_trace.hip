@@ -471,7 +471,7 @@ __device__ __forceinline__ uint32_t packet_slabs(const f4v (&pl6)[6], const Pack
 // descending slot order, so the lowest slot pops next. Pushes that do not happen write the spare
 // lane kPacketStack - 1; the bookkeeping is plain integer SALU work. Returns 1 with *next set,
 // 0 when nothing is left to descend into.
-template <bool STATS, int R>
+template <bool ANY_HIT, bool STATS, int R>
 __device__ __forceinline__ int packet_tlas_node(const RT_CONST char* pool, int ref, const PacketRay<R>& ry,
                                                 float tmin, PacketLive<R>& pl, const HitRec* hit, WaveStack& stk,
                                                 int& sp, int cap, int& next, Counters& cnt) {
@@ -487,19 +487,24 @@ __device__ __forceinline__ int packet_tlas_node(const RT_CONST char* pool, int r
   asm volatile("" ::"s"(ch[0]), "s"(ch[1]), "s"(ch[2]), "s"(ch[3]));
   if (ent == 0) return 0;
   // nearest entered child by the lead ray's key, lowest slot on ties: per lane in VALU (keys
-  // masked to the entered set), one readlane
-  const uint32_t nent = ~ent;
-  uint32_t idx = 0;
+  // masked to the entered set), one readlane. Any-hit walks take the lowest entered slot.
+  uint32_t ib;
+  if (ANY_HIT) {
+    ib = (uint32_t)__builtin_ctz(ent);
+  } else {
+    const uint32_t nent = ~ent;
+    uint32_t idx = 0;
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    uint32_t kk[4];
+    for (int r = 0; r < R; ++r) {
+      uint32_t kk[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) kk[k] = vkey[r][k] | bit_mask_v(nent, k);
-    const uint32_t m = min(min(kk[0], kk[1]), min(kk[2], kk[3]));
-    const uint32_t ir = kk[0] == m ? 0u : kk[1] == m ? 1u : kk[2] == m ? 2u : 3u;
-    idx = (r == 0 || pl.lead_r == (uint32_t)r) ? ir : idx;
+      for (int k = 0; k < 4; ++k) kk[k] = vkey[r][k] | bit_mask_v(nent, k);
+      const uint32_t m = min(min(kk[0], kk[1]), min(kk[2], kk[3]));
+      const uint32_t ir = kk[0] == m ? 0u : kk[1] == m ? 1u : kk[2] == m ? 2u : 3u;
+      idx = (r == 0 || pl.lead_r == (uint32_t)r) ? ir : idx;
+    }
+    ib = (uint32_t)__builtin_amdgcn_readlane((int)idx, (int)pl.lead_l);
   }
-  const uint32_t ib = (uint32_t)__builtin_amdgcn_readlane((int)idx, (int)pl.lead_l);
   const i4v c4 = {ch[0], ch[1], ch[2], ch[3]};
   const int rb = c4[ib];
   // pushed set P (entered, not the nearest) as a 4-bit mask; descending slot order puts child k
@@ -664,7 +669,7 @@ __device__ __forceinline__ void packet_walk(const SceneView& sc, const V3* o, co
   while (true) {
     int next;
     if (ref >= 0) {
-      if (packet_tlas_node<STATS, R>(pool, ref, w, tmin, pl, hit, stk, sp, cap, next, cnt)) {
+      if (packet_tlas_node<ANY_HIT, STATS, R>(pool, ref, w, tmin, pl, hit, stk, sp, cap, next, cnt)) {
         ref = next;
         continue;
       }
