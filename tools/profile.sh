@@ -12,9 +12,9 @@ BENCH="$R/bench.py --config $CFG --no-cpu-baseline --extra="
 mkdir -p "$R/gpurun_out"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_kt" -o run --output-format csv \
-  -- python3 $BENCH --steps 100 --warmup 5 > "$R/gpurun_out/prof_kt.log" 2>&1 || exit $?
+  -- python3 $BENCH --steps 200 --warmup 100 > "$R/gpurun_out/prof_kt.log" 2>&1 || exit $?
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_trace_frame -d "$R/gpurun_out/prof_fetch" \
-  -o run --output-format csv -- python3 $BENCH --steps 20 --warmup 2 > "$R/gpurun_out/prof_fetch.log" 2>&1 || exit $?
+  -o run --output-format csv -- python3 $BENCH --steps 20 --warmup 100 > "$R/gpurun_out/prof_fetch.log" 2>&1 || exit $?
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_trace_frame -d "$R/gpurun_out/prof_write" \
-  -o run --output-format csv -- python3 $BENCH --steps 20 --warmup 2 > "$R/gpurun_out/prof_write.log" 2>&1 || exit $?
+  -o run --output-format csv -- python3 $BENCH --steps 20 --warmup 100 > "$R/gpurun_out/prof_write.log" 2>&1 || exit $?
 echo "profiles: run python3 tools/pmc_summary.py --tag $TAG --config $CFG locally after the merge"
