@@ -637,23 +637,40 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
                       bool leaf_ref_is_prim, uint32_t* node_count, uint32_t* depth, uint32_t* max_stack,
                       float bounds[6], float* build_ms, hipStream_t s) {
   if (n == 0) return hipErrorInvalidValue;
+  const uint32_t nblocks = (n + kRsTile - 1) / kRsTile;
+  const uint32_t nbin = n > 1 ? n - 1 : 1;
+  // all temporaries in ONE allocation (hipMalloc costs ~0.1 ms each; a hot-reload rebuild pays it)
+  struct Part {
+    size_t off, bytes;
+  };
+  size_t total = 0;
+  auto part = [&](size_t bytes) {
+    Part q{total, bytes};
+    total += (bytes + 255) & ~(size_t)255;
+    return q;
+  };
+  const Part p_stats = part(12 * sizeof(float)), p_keys0 = part((size_t)n * 4), p_keys1 = part((size_t)n * 4),
+             p_vals1 = part((size_t)n * 4), p_hist = part((size_t)256 * nblocks * 4), p_info = part(12),
+             p_ps = part((size_t)nbin * 4), p_bin = part((size_t)nbin * sizeof(BinNode)), p_la = part((size_t)nbin * 4),
+             p_lb = part((size_t)nbin * 4), p_child = part((size_t)nbin * 8), p_pint = part((size_t)nbin * 4),
+             p_pleaf = part((size_t)n * 4), p_nbox = part((size_t)nbin * 24), p_flags = part((size_t)nbin * 4),
+             p_dpc = part(RT_SAH_COLLAPSE ? (size_t)nbin * sizeof(float4) : 0),
+             p_dps = part(RT_SAH_COLLAPSE ? (size_t)nbin * 4 : 0);
+  DevBuf arena;
+  RT_TRY(hipMalloc(&arena.p, total));
+  char* A = (char*)arena.p;
+  struct View {
+    void* p;
+  };
+  auto at = [&](const Part& q) { return View{q.bytes ? (void*)(A + q.off) : nullptr}; };
+  View stats = at(p_stats), keys0 = at(p_keys0), keys1 = at(p_keys1), vals1 = at(p_vals1), hist = at(p_hist),
+       info = at(p_info), ps = at(p_ps), bin = at(p_bin), la = at(p_la), lb = at(p_lb), child = at(p_child),
+       pint = at(p_pint), pleaf = at(p_pleaf), nbox = at(p_nbox), flags = at(p_flags), dpc = at(p_dpc),
+       dps = at(p_dps);
   hipEvent_t e0, e1;
   RT_TRY(hipEventCreate(&e0));
   RT_TRY(hipEventCreate(&e1));
   RT_TRY(hipEventRecord(e0, s));
-  const uint32_t nblocks = (n + kRsTile - 1) / kRsTile;
-  const uint32_t nbin = n > 1 ? n - 1 : 1;
-  DevBuf stats, keys0, keys1, vals1, hist, child, pint, pleaf, nbox, flags, info, bin, la, lb, ps, dpc, dps;
-  RT_TRY(hipMalloc(&stats.p, 12 * sizeof(float)));
-  RT_TRY(hipMalloc(&keys0.p, (size_t)n * 4));
-  RT_TRY(hipMalloc(&keys1.p, (size_t)n * 4));
-  RT_TRY(hipMalloc(&vals1.p, (size_t)n * 4));
-  RT_TRY(hipMalloc(&hist.p, (size_t)256 * nblocks * 4));
-  RT_TRY(hipMalloc(&info.p, 12));
-  RT_TRY(hipMalloc(&ps.p, (size_t)nbin * 4));
-  RT_TRY(hipMalloc(&bin.p, (size_t)nbin * sizeof(BinNode)));
-  RT_TRY(hipMalloc(&la.p, (size_t)nbin * 4));
-  RT_TRY(hipMalloc(&lb.p, (size_t)nbin * 4));
   float* cb = (float*)stats.p;
   k_bounds<<<1, 1024, 0, s>>>(d_primbox, n, cb);
   RT_TRY(hipGetLastError());
@@ -678,17 +695,8 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
     k_single<<<1, 1, 0, s>>>(d_primbox, leaf_ref_is_prim, d_bin);
     RT_TRY(hipGetLastError());
   } else {
-    RT_TRY(hipMalloc(&child.p, (size_t)(n - 1) * 8));
-    RT_TRY(hipMalloc(&pint.p, (size_t)(n - 1) * 4));
-    RT_TRY(hipMalloc(&pleaf.p, (size_t)n * 4));
-    RT_TRY(hipMalloc(&nbox.p, (size_t)(n - 1) * 24));
-    RT_TRY(hipMalloc(&flags.p, (size_t)(n - 1) * 4));
     RT_TRY(hipMemsetAsync(flags.p, 0, (size_t)(n - 1) * 4, s));
     k_karras<<<grid1(n - 1, 256), 256, 0, s>>>(ka, (int)n, (int*)child.p, (int*)pint.p, (int*)pleaf.p);
-    if (RT_SAH_COLLAPSE) {
-      RT_TRY(hipMalloc(&dpc.p, (size_t)(n - 1) * sizeof(float4)));
-      RT_TRY(hipMalloc(&dps.p, (size_t)(n - 1) * 4));
-    }
     k_refit<<<grid1(n, 256), 256, 0, s>>>((int)n, (int*)pleaf.p, (int*)pint.p, (int*)child.p, d_primbox,
                                           d_sorted, (float*)nbox.p, (uint32_t*)flags.p, (float4*)dpc.p,
                                           (uint32_t*)dps.p);
