@@ -469,8 +469,27 @@ __device__ __forceinline__ int gather4_dp(const BinNode* __restrict__ bin, const
   return cnt;
 }
 
-__global__ __launch_bounds__(1024) void k_collapse(const BinNode* __restrict__ bin, const float4* __restrict__ dpc,
-                                                   const uint32_t* __restrict__ dps, Bvh4Node* __restrict__ out,
+// The DP expansion of every binary node, in parallel (only wide-node roots are read): k_collapse
+// then takes one record per node instead of walking dependent loads level by level.
+struct alignas(128) Exp4 {
+  int ref[4];
+  float box[4][6];
+  int cnt, pad[3];
+};
+
+__global__ void k_dp_expand(int nbin, const BinNode* __restrict__ bin, const float4* __restrict__ dpc,
+                            const uint32_t* __restrict__ dps, Exp4* __restrict__ exp) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nbin) return;
+  Exp4 e;
+  e.cnt = gather4_dp(bin, dpc, dps, i, e.ref, e.box);
+  for (int j = e.cnt; j < 4; ++j) e.ref[j] = kEmptyChild;
+  e.pad[0] = e.pad[1] = e.pad[2] = 0;
+  exp[i] = e;
+}
+
+__global__ __launch_bounds__(1024) void k_collapse(const BinNode* __restrict__ bin, const Exp4* __restrict__ exp,
+                                                   Bvh4Node* __restrict__ out,
                                                    int* la, int* lb, int* ps, uint32_t* __restrict__ info) {
   __shared__ int scan[1024];
   __shared__ int s_maxstack;
@@ -494,7 +513,18 @@ __global__ __launch_bounds__(1024) void k_collapse(const BinNode* __restrict__ b
       int ref[4];
       float box[4][6];
       int cnt = 0;
-      if (valid) cnt = dpc ? gather4_dp(bin, dpc, dps, cur[i], ref, box) : gather4(bin, cur[i], ref, box);
+      if (valid) {
+        if (exp) {
+          const Exp4& e = exp[cur[i]];
+          cnt = e.cnt;
+          for (int j = 0; j < 4; ++j) {
+            ref[j] = e.ref[j];
+            for (int a = 0; a < 6; ++a) box[j][a] = e.box[j][a];
+          }
+        } else {
+          cnt = gather4(bin, cur[i], ref, box);
+        }
+      }
       int m = 0;
       for (int j = 0; j < cnt; ++j) m += ref[j] >= 0;
       scan[tid] = m;
@@ -655,7 +685,8 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
              p_lb = part((size_t)nbin * 4), p_child = part((size_t)nbin * 8), p_pint = part((size_t)nbin * 4),
              p_pleaf = part((size_t)n * 4), p_nbox = part((size_t)nbin * 24), p_flags = part((size_t)nbin * 4),
              p_dpc = part(RT_SAH_COLLAPSE ? (size_t)nbin * sizeof(float4) : 0),
-             p_dps = part(RT_SAH_COLLAPSE ? (size_t)nbin * 4 : 0);
+             p_dps = part(RT_SAH_COLLAPSE ? (size_t)nbin * 4 : 0),
+             p_exp = part(RT_SAH_COLLAPSE ? (size_t)nbin * sizeof(Exp4) : 0);
   DevBuf arena;
   RT_TRY(hipMalloc(&arena.p, total));
   char* A = (char*)arena.p;
@@ -666,7 +697,7 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
   View stats = at(p_stats), keys0 = at(p_keys0), keys1 = at(p_keys1), vals1 = at(p_vals1), hist = at(p_hist),
        info = at(p_info), ps = at(p_ps), bin = at(p_bin), la = at(p_la), lb = at(p_lb), child = at(p_child),
        pint = at(p_pint), pleaf = at(p_pleaf), nbox = at(p_nbox), flags = at(p_flags), dpc = at(p_dpc),
-       dps = at(p_dps);
+       dps = at(p_dps), expd = at(p_exp);
   hipEvent_t e0, e1;
   RT_TRY(hipEventCreate(&e0));
   RT_TRY(hipEventCreate(&e1));
@@ -704,8 +735,13 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
                                              leaf_ref_is_prim, d_bin);
     RT_TRY(hipGetLastError());
   }
-  k_collapse<<<1, 1024, 0, s>>>(d_bin, (const float4*)dpc.p, (const uint32_t*)dps.p, d_nodes, (int*)la.p,
-                                (int*)lb.p, (int*)ps.p, (uint32_t*)info.p);
+  if (RT_SAH_COLLAPSE) {
+    k_dp_expand<<<grid1(nbin, 256), 256, 0, s>>>((int)nbin, d_bin, (const float4*)dpc.p, (const uint32_t*)dps.p,
+                                                 (Exp4*)expd.p);
+    RT_TRY(hipGetLastError());
+  }
+  k_collapse<<<1, 1024, 0, s>>>(d_bin, (const Exp4*)expd.p, d_nodes, (int*)la.p, (int*)lb.p, (int*)ps.p,
+                                (uint32_t*)info.p);
   RT_TRY(hipGetLastError());
   RT_TRY(hipEventRecord(e1, s));
   float hb[12];
