@@ -10,9 +10,9 @@ import pytest
 import realtimeraytracing_gradproject_amd as rt
 from realtimeraytracing_gradproject_amd import scenes
 import oracle
+from oracle import np_reference
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-from oracle import np_reference
 
 GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "frames_small.npz"))
 SIZES = {"REF": (96, 54), "C1": (64, 64), "C2": (96, 54), "C2F": (96, 54), "C3": (96, 54), "C4": (96, 54),
