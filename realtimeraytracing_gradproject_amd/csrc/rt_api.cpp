@@ -461,6 +461,12 @@ rt_status rt_tlas_export(rt_ctx_t c, void* nodes, size_t nodes_bytes) {
 rt_status rt_set_camera(rt_ctx_t c, const float cb[64]) {
   if (!c || !cb) return fail(c, RT_E_INVALID, "rt_set_camera: null argument");
   std::memcpy(c->fp.cb, cb, 64 * sizeof(float));
+  {
+    // RayGen's origin, uniform over the frame: the device's own hlsl_mul4 (RT_HD, no contraction)
+    // evaluated once here gives the bits the kernel would compute
+    const float zero_one[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+    rt::hlsl_mul4(c->fp.cb + 32, zero_one, c->fp.cam_origin);
+  }
   c->have_camera = true;
   return RT_OK;
 }
@@ -648,6 +654,8 @@ rt_status rt_dispatch_rays(rt_ctx_t c, uint32_t W, uint32_t H, const uint32_t* r
   }
   c->fp.width = W;
   c->fp.height = H;
+  c->fp.fwidth = (float)W;  // exact: W, H < 2^24
+  c->fp.fheight = (float)H;
   c->fp.nrows = nrows;
   rt::SceneView sv = scene_view(c);
   if (sv.stack_cap > rt::kMaxTraversalStack)

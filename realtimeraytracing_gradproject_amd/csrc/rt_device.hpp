@@ -131,6 +131,11 @@ struct FrameParams {
   uint32_t spp_side;  // k for k x k stratified samples
   uint32_t width, height;
   uint32_t nrows;
+  // frame constants the host evaluates once with the device's own arithmetic (uniform values the
+  // kernel would otherwise compute per lane into VGPRs): the RayGen origin
+  // mul(viewInverse, (0, 0, 0, 1)) and the dimensions as floats
+  float cam_origin[4];
+  float fwidth, fheight;
 };
 
 // The trace kernels read one node pool and one triangle pool per scene: [TLAS | BLAS 0 | BLAS 1 ..]

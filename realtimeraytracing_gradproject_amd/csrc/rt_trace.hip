@@ -859,7 +859,7 @@ __device__ bool shadow_ray(const SceneView& sc, V3 P, V3 dir, const LaneStack& s
 }
 
 __device__ __forceinline__ V3 miss_color(const FrameParams& fp, uint32_t py) {
-  const float ramp = (float)py / (float)fp.height;  // Miss.hlsl:8 (DispatchRaysIndex: the pixel row at every depth)
+  const float ramp = (float)py / fp.fheight;  // Miss.hlsl:8 (DispatchRaysIndex: the pixel row at every depth)
   return v3(0.0f, 0.2f, 0.7f - 0.3f * ramp);
 }
 
@@ -930,16 +930,14 @@ __device__ V3 shade_ref(const SceneView& sc, const FrameParams& fp, uint32_t py,
 template <int MODE, bool STATS>
 __device__ V3 shade_sample(const SceneView& sc, const FrameParams& fp, uint32_t px, uint32_t py,
                            float ox, float oy, const LaneStack& stk, Counters& cnt) {
-  const float dx = (((float)px + ox) / (float)fp.width) * 2.0f - 1.0f;
-  const float dy = (((float)py + oy) / (float)fp.height) * 2.0f - 1.0f;
-  float org4[4], dc[4], dw[4];
-  const float zero_one[4] = {0.0f, 0.0f, 0.0f, 1.0f};
-  hlsl_mul4(fp.cb + 32, zero_one, org4);
+  const float dx = (((float)px + ox) / fp.fwidth) * 2.0f - 1.0f;
+  const float dy = (((float)py + oy) / fp.fheight) * 2.0f - 1.0f;
+  float dc[4], dw[4];
   const float ndc[4] = {dx, -dy, 1.0f, 1.0f};
   hlsl_mul4(fp.cb + 48, ndc, dc);
   const float dcam[4] = {dc[0], dc[1], dc[2], 0.0f};
   hlsl_mul4(fp.cb + 32, dcam, dw);
-  const V3 O = v3(org4[0], org4[1], org4[2]);
+  const V3 O = v3(fp.cam_origin[0], fp.cam_origin[1], fp.cam_origin[2]);  // mul(viewInverse, (0,0,0,1))
   const V3 D = normalize(v3(dw[0], dw[1], dw[2]));  // CastDefaultRay
   HitRec hit;
   if (STATS) ++cnt.primary;
@@ -978,16 +976,14 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
   bool found[R], occl[R], need[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const float dx = (((float)px[r] + ox) / (float)fp.width) * 2.0f - 1.0f;
-    const float dy = (((float)py[r] + oy) / (float)fp.height) * 2.0f - 1.0f;
-    float org4[4], dc[4], dw[4];
-    const float zero_one[4] = {0.0f, 0.0f, 0.0f, 1.0f};
-    hlsl_mul4(fp.cb + 32, zero_one, org4);
+    const float dx = (((float)px[r] + ox) / fp.fwidth) * 2.0f - 1.0f;
+    const float dy = (((float)py[r] + oy) / fp.fheight) * 2.0f - 1.0f;
+    float dc[4], dw[4];
     const float ndc[4] = {dx, -dy, 1.0f, 1.0f};
     hlsl_mul4(fp.cb + 48, ndc, dc);
     const float dcam[4] = {dc[0], dc[1], dc[2], 0.0f};
     hlsl_mul4(fp.cb + 32, dcam, dw);
-    O[r] = v3(org4[0], org4[1], org4[2]);
+    O[r] = v3(fp.cam_origin[0], fp.cam_origin[1], fp.cam_origin[2]);  // mul(viewInverse, (0,0,0,1))
     D[r] = normalize(v3(dw[0], dw[1], dw[2]));  // CastDefaultRay
     if (STATS && inimg[r]) ++cnt.primary;
   }
