@@ -1163,11 +1163,12 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void k_trace_frame(SceneView 
 // threads, 16 x 8R pixels; smaller workgroups shorten the tail of the launch). Every lane runs
 // the sample loop (rays outside the image or the row list join the packets dead) and stores only
 // in-image pixels.
-// Occupancy: LAMBERT_SHADOW (the perf configs) runs at 6 waves per SIMD (80 VGPRs, 13 spilled
-// outside the traversal loops); 5, 7 and 8 waves measured slower. REF and PRIMARY keep the
-// allocator's choice (REF would spill hundreds of bytes; PRIMARY measured neutral).
+// Occupancy: LAMBERT_SHADOW (the perf configs) runs at 7 waves per SIMD (72 VGPRs: the one-sample
+// kernel needs 67, the 4-spp one spills a few outside the traversal loops); 6 and 8 measured
+// slower overall. REF and PRIMARY keep the allocator's choice (REF would spill hundreds of
+// bytes; PRIMARY measured neutral).
 #ifndef RT_LS_WAVES
-#define RT_LS_WAVES 6
+#define RT_LS_WAVES 7
 #endif
 #ifndef RT_PACKET_WX
 #define RT_PACKET_WX 2  // waves of a packet workgroup along x (8-pixel tiles)
@@ -1176,7 +1177,9 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void k_trace_frame(SceneView 
 #define RT_PACKET_WY 1  // ... and along y (8R-row tiles); 2 x 1 measured best (C4/C5 -6 % vs 2 x 2)
 #endif
 constexpr int kPacketBlock = 64 * RT_PACKET_WX * RT_PACKET_WY;
-template <int MODE, bool STATS, int R>
+// SPP1: one sample per pixel (spp_side == 1, every perf config but C5): no accumulator lives
+// across the traces.
+template <int MODE, bool STATS, int R, bool SPP1>
 __global__ __launch_bounds__(kPacketBlock) __attribute__((amdgpu_waves_per_eu((MODE == 1 && !STATS) ? RT_LS_WAVES : 1)))
 void k_trace_frame_packet(SceneView sc, FrameParams fp,
                                                                const uint32_t* __restrict__ rows,
@@ -1198,15 +1201,19 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp,
     acc[r] = v3(0.0f, 0.0f, 0.0f);
   }
   Counters cnt;
-  const uint32_t k = fp.spp_side;
-  for (uint32_t sy = 0; sy < k; ++sy)
-    for (uint32_t sx = 0; sx < k; ++sx) {
-      const float ox = ((float)sx + 0.5f) / (float)k;
-      const float oy = ((float)sy + 0.5f) / (float)k;
-      shade_sample_packet<MODE, STATS, R>(sc, fp, px, py, ox, oy, inimg, col, cnt);
+  const uint32_t k = SPP1 ? 1u : fp.spp_side;
+  if (SPP1) {
+    shade_sample_packet<MODE, STATS, R>(sc, fp, px, py, 0.5f, 0.5f, inimg, acc, cnt);  // (0 + 0.5) / 1
+  } else {
+    for (uint32_t sy = 0; sy < k; ++sy)
+      for (uint32_t sx = 0; sx < k; ++sx) {
+        const float ox = ((float)sx + 0.5f) / (float)k;
+        const float oy = ((float)sy + 0.5f) / (float)k;
+        shade_sample_packet<MODE, STATS, R>(sc, fp, px, py, ox, oy, inimg, col, cnt);
 #pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] = add(acc[r], col[r]);
-    }
+        for (int r = 0; r < R; ++r) acc[r] = add(acc[r], col[r]);
+      }
+  }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     V3 a = acc[r];
@@ -1265,8 +1272,12 @@ hipError_t launch_mode(const SceneView& sc, const FrameParams& fp, const uint32_
     constexpr int R = RT_PACKET_RAYS;
     constexpr uint32_t tw = 8 * RT_PACKET_WX, th = 8 * R * RT_PACKET_WY;
     dim3 gp((fp.width + tw - 1) / tw, (fp.nrows + th - 1) / th);
-    hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R>), gp, dim3(kPacketBlock), 0, s, sc, fp, rows,
-                       (uint32_t*)rgba8, (float4*)rgba32f, stats);
+    if (fp.spp_side == 1)
+      hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R, true>), gp, dim3(kPacketBlock), 0, s, sc, fp, rows,
+                         (uint32_t*)rgba8, (float4*)rgba32f, stats);
+    else
+      hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R, false>), gp, dim3(kPacketBlock), 0, s, sc, fp, rows,
+                         (uint32_t*)rgba8, (float4*)rgba32f, stats);
   } else {
     size_t lds = (size_t)sc.lds_cap * kBlock * sizeof(int);
     hipLaunchKernelGGL((k_trace_frame<MODE, STATS>), grid, dim3(kBlock), lds, s, sc, fp, rows,
