@@ -56,7 +56,7 @@ def parse():
     p.add_argument("--assemble", action="store_true",
                    help="N>1: split one frame into strips and gather it to rank 0 (strong scaling)")
     p.add_argument("--save-image", default="", help="write the rank-0 frame as .npy")
-    p.add_argument("--extra", default="C2F,C3,C4,C5",
+    p.add_argument("--extra", default="C2F,C3,C4,C5,REF",
                    help="comma list of further configs timed on one GPU (N=1 only; '' to skip)")
     return p.parse_args()
 
