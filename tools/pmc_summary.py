@@ -18,6 +18,15 @@ import statistics
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+
+def is_frame_kernel(name: str) -> bool:
+    """The timed frame kernel: k_trace_frame*<MODE, STATS=false, ...> (the STATS=true launch is the
+    untimed counter pass)."""
+    if "k_trace_frame" not in name or "<" not in name:
+        return False
+    args = [a.strip() for a in name.split("<", 1)[1].split(">", 1)[0].split(",")]
+    return len(args) > 1 and args[1] == "false"
+
 def find(pattern):
     hits = sorted(glob.glob(os.path.join(ROOT, "gpurun_out", pattern), recursive=True))
     return hits[0] if hits else None
@@ -27,8 +36,7 @@ def counter_per_launch(path, name):
     vals = []
     with open(path) as f:
         for row in csv.DictReader(f):
-            if row.get("Counter_Name") == name and "k_trace_frame" in row.get("Kernel_Name", "") \
-                    and "true" not in row.get("Kernel_Name", ""):
+            if row.get("Counter_Name") == name and is_frame_kernel(row.get("Kernel_Name", "")):
                 vals.append(float(row["Counter_Value"]))
     return statistics.median(vals) if vals else None, len(vals)
 
