@@ -344,13 +344,6 @@ __device__ __forceinline__ uint32_t nonzero_mask4(const uint64_t (&m)[4]) {
   return r;
 }
 
-// bit if the uniform 64-bit mask m is nonzero, else 0: s_cmp_lg_u64 + s_cselect_b32 (the
-// compiler otherwise round-trips the boolean through a VGPR and readfirstlane)
-__device__ __forceinline__ uint32_t nonzero_bit(uint64_t m, uint32_t bit) {
-  uint32_t r;
-  asm("s_cmp_lg_u64 %1, 0\n\ts_cselect_b32 %0, %2, 0" : "=s"(r) : "s"(m), "s"(bit) : "scc");
-  return r;
-}
 
 // Live rays of the packet: one ballot mask per ray slot r, and the lead ray (lowest r, then
 // lowest lane).
@@ -523,117 +516,96 @@ __device__ __forceinline__ int packet_tlas_node(const RT_CONST char* pool, int r
   return 1;
 }
 
-// BLAS node of the packet walk. Entered triangle children are tested right here, in slot order.
-// Of the entered internal children the nearest (the lead ray's entry distance, lowest slot on
-// ties; chosen per lane in VALU, one readlane) is descended into; the rest become ONE stack entry
-// (first_inner << 8 | inner_mask << 4 | pending slots) that pops its slots lowest first — exactly
-// the order in which per-child pushes in descending slot order would pop them, so the walk (and
-// every counter) is that of the per-child stack, with a fraction of the scalar bookkeeping.
-// Internal child k's ref is first_inner + popcount(inner_mask below k) (BFS allocation).
-// Returns 1 with *next set, 0 when nothing is left to descend into, 2 when an any-hit packet has
-// no live ray left.
-template <bool ANY_HIT, bool STATS, int R, bool OCT>
-__device__ __forceinline__ int packet_blas_node(const RT_CONST char* pool, const RT_CONST TriRec* tpool, int ref,
-                                                const PacketRay<R>& ry, float tmin, uint32_t cur, float face,
-                                                PacketLive<R>& pl, HitRec* hit, WaveStack& stk, int& sp, int cap,
-                                                int& next, const NodeOct& oc, Counters& cnt) {
-  const RT_CONST char* nb = pool + ((uint32_t)ref << 7);
-  const i8v ch = *(const RT_CONST i8v*)(nb + 96);  // child[4], count, first_inner, inner_mask, pad
-  uint64_t hm[R][4];
-  uint32_t vkey[R][4];
-  f4v planes[6];
-  if (OCT) {
-    planes[0] = cld4(nb + oc.nx);
-    planes[1] = cld4(nb + oc.fx);
-    planes[2] = cld4(nb + oc.ny);
-    planes[3] = cld4(nb + oc.fy);
-    planes[4] = cld4(nb + oc.nz);
-    planes[5] = cld4(nb + oc.fz);
-  } else {
-#pragma unroll
-    for (int q = 0; q < 6; ++q) planes[q] = cld4(nb + 16 * q);
-  }
-  uint32_t ent = packet_slabs<STATS, R, OCT>(planes, ry, tmin, pl, hit, (uint32_t)ch[4], hm, vkey, cnt);
-  asm volatile("" ::"s"(ch[0]), "s"(ch[1]), "s"(ch[2]), "s"(ch[3]), "s"(ch[5]), "s"(ch[6]), "s"(ch[7]));
-  if (ent == 0) return 0;
-  const uint32_t imask = (uint32_t)ch[6];
-  uint32_t tl = ent & ~imask;
-  ent &= imask;
-  const bool tested = tl != 0;
-  while (tl) {
-    const uint32_t k = (uint32_t)__builtin_ctz(tl);
-    tl &= tl - 1u;
-    const i4v c4 = {ch[0], ch[1], ch[2], ch[3]};
-    packet_tri<ANY_HIT, STATS, R>(tpool, c4[k], ry, tmin, cur, face, pl, hit, cnt);
-  }
-  if (ANY_HIT && tested) {  // rays can only have left the packet in a triangle test
-    if (!pl.update()) return 2;
-    // children only finished rays wanted are dropped
-    uint32_t still = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      uint64_t any = 0;
-#pragma unroll
-      for (int r = 0; r < R; ++r) any |= hm[r][k] & pl.mask[r];
-      still |= nonzero_bit(any, 1u << k);
-    }
-    ent &= still;
-  }
-  if (ent == 0) return 0;
-  if (ANY_HIT) {
-    // occlusion rays skip the nearest-first choice (no keys, no readlane): the lowest entered slot
-    // goes first. Measured -2..-7 % on C2-C5; unoccluded rays (most of C2's, which leave through
-    // the teapot's open top) visit the same nodes in any order.
-    const uint32_t ib = (uint32_t)__builtin_ctz(ent);
-    const uint32_t first = (uint32_t)ch[5];
-    next = (int)(first + (uint32_t)__builtin_popcount(imask & ((1u << ib) - 1u)));
-    stk.v = push_entry(stk.v, sp, (uint32_t)ch[7], ent, 1u << ib);
-    return 1;
-  }
-  // per lane: the slot of its smallest key over the entered internal children (all-ones keys
-  // elsewhere), lowest slot on ties; the lead lane's answer is the packet's
-  const uint32_t nent = ~ent;
-  uint32_t idx = 0;
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    uint32_t kk[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) kk[k] = vkey[r][k] | bit_mask_v(nent, k);
-    const uint32_t m = min(min(kk[0], kk[1]), min(kk[2], kk[3]));
-    const uint32_t ir = kk[0] == m ? 0u : kk[1] == m ? 1u : kk[2] == m ? 2u : 3u;
-    idx = (r == 0 || pl.lead_r == (uint32_t)r) ? ir : idx;
-  }
-  const uint32_t ib = (uint32_t)__builtin_amdgcn_readlane((int)idx, (int)pl.lead_l);
-  const uint32_t first = (uint32_t)ch[5];
-  next = (int)(first + (uint32_t)__builtin_popcount(imask & ((1u << ib) - 1u)));
-  if (STATS && (ent & ~(1u << ib)) && sp + 1 > cap)  // never: cap bounds the entries (one per BLAS level)
-#pragma unroll
-    for (int r = 0; r < R; ++r) cnt.overflow += pl.live[r] ? 1u : 0u;
-  stk.v = push_entry(stk.v, sp, (uint32_t)ch[7], ent, 1u << ib);
-  return 1;
-}
-
-// One BLAS walk of the packet (instance cur, object rays b) on the stack above `base`. Returns
-// false when an any-hit packet has no live ray left.
+// BLAS walk of the packet (instance cur, object rays ry) on the stack above `base`; returns false
+// when an any-hit packet has no live ray left. One loop iteration per node, straight-line uniform
+// control flow (no status codes between a node function and the loop). At a node: entered
+// triangle children are tested right here, in slot order; of the entered internal children the
+// nearest (the lead ray's entry distance, lowest slot on ties; chosen per lane in VALU, one
+// readlane; any-hit walks take the lowest entered slot) is descended into, and the rest become ONE
+// stack entry (first_inner << 8 | inner_mask << 4 | pending slots) that pops its slots lowest
+// first — exactly the order in which per-child pushes in descending slot order would pop them, so
+// the walk (and every counter) is that of the per-child stack with a fraction of the scalar
+// bookkeeping. Internal child k's ref is first_inner + popcount(inner_mask below k).
 template <bool ANY_HIT, bool STATS, int R, bool OCT>
 __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, const RT_CONST TriRec* tpool, int bref,
-                                                 const PacketRay<R>& b, float tmin, uint32_t cur, float face,
+                                                 const PacketRay<R>& ry, float tmin, uint32_t cur, float face,
                                                  PacketLive<R>& pl, HitRec* hit, WaveStack& stk, int& sp, int cap,
                                                  const NodeOct& oc, Counters& cnt) {
   const int base = sp;
   while (true) {
-    // only internal nodes reach here: triangle children are tested inside packet_blas_node
-    int next;
-    const int st = packet_blas_node<ANY_HIT, STATS, R, OCT>(pool, tpool, bref, b, tmin, cur, face, pl, hit, stk, sp,
-                                                            cap, next, oc, cnt);
-    if (st == 1) {
-      bref = next;
-      continue;
+    const RT_CONST char* nb = pool + ((uint32_t)bref << 7);
+    const i8v ch = *(const RT_CONST i8v*)(nb + 96);  // child[4], count, first_inner, inner_mask, entry_base
+    uint64_t hm[R][4];
+    uint32_t vkey[R][4];
+    f4v planes[6];
+    if (OCT) {
+      planes[0] = cld4(nb + oc.nx);
+      planes[1] = cld4(nb + oc.fx);
+      planes[2] = cld4(nb + oc.ny);
+      planes[3] = cld4(nb + oc.fy);
+      planes[4] = cld4(nb + oc.nz);
+      planes[5] = cld4(nb + oc.fz);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 6; ++q) planes[q] = cld4(nb + 16 * q);
     }
-    if (ANY_HIT && st == 2) return false;
-    if (sp == base) return true;
-    // top entry: its lowest pending slot is next; the entry stays while slots remain
-    bref = pop_entry(stk.v, sp);
+    uint32_t ent = packet_slabs<STATS, R, OCT>(planes, ry, tmin, pl, hit, (uint32_t)ch[4], hm, vkey, cnt);
+    asm volatile("" ::"s"(ch[0]), "s"(ch[1]), "s"(ch[2]), "s"(ch[3]), "s"(ch[5]), "s"(ch[6]), "s"(ch[7]));
+    const uint32_t imask = (uint32_t)ch[6];
+    uint32_t tl = ent & ~imask;
+    ent &= imask;
+    if (tl) {
+      do {
+        const uint32_t k = (uint32_t)__builtin_ctz(tl);
+        tl &= tl - 1u;
+        const i4v c4 = {ch[0], ch[1], ch[2], ch[3]};
+        packet_tri<ANY_HIT, STATS, R>(tpool, c4[k], ry, tmin, cur, face, pl, hit, cnt);
+      } while (tl);
+      if (ANY_HIT) {  // rays can only have left the packet in a triangle test
+        if (!pl.update()) return false;
+        // children only finished rays wanted are dropped
+        uint64_t any[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          any[k] = 0;
+#pragma unroll
+          for (int r = 0; r < R; ++r) any[k] |= hm[r][k] & pl.mask[r];
+        }
+        ent &= nonzero_mask4(any);
+      }
+    }
+    if (ent) {
+      uint32_t ib;
+      if (ANY_HIT) {
+        // occlusion rays skip the nearest-first choice (no keys, no readlane): for an occlusion ray
+        // the order only decides how soon it stops
+        ib = (uint32_t)__builtin_ctz(ent);
+      } else {
+        // per lane: the slot of its smallest key over the entered internal children (all-ones
+        // keys elsewhere), lowest slot on ties; the lead lane's answer is the packet's
+        const uint32_t nent = ~ent;
+        uint32_t idx = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          uint32_t kk[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) kk[k] = vkey[r][k] | bit_mask_v(nent, k);
+          const uint32_t m = min(min(kk[0], kk[1]), min(kk[2], kk[3]));
+          const uint32_t ir = kk[0] == m ? 0u : kk[1] == m ? 1u : kk[2] == m ? 2u : 3u;
+          idx = (r == 0 || pl.lead_r == (uint32_t)r) ? ir : idx;
+        }
+        ib = (uint32_t)__builtin_amdgcn_readlane((int)idx, (int)pl.lead_l);
+      }
+      if (STATS && (ent & ~(1u << ib)) && sp + 1 > cap)  // never: cap bounds the entries (one per level)
+#pragma unroll
+        for (int r = 0; r < R; ++r) cnt.overflow += pl.live[r] ? 1u : 0u;
+      stk.v = push_entry(stk.v, sp, (uint32_t)ch[7], ent, 1u << ib);
+      bref = (int)((uint32_t)ch[5] + (uint32_t)__builtin_popcount(imask & ((1u << ib) - 1u)));
+    } else {
+      if (sp == base) return true;
+      // top entry: its lowest pending slot is next; the entry stays while slots remain
+      bref = pop_entry(stk.v, sp);
+    }
   }
 }
 
