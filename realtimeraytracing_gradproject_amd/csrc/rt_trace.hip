@@ -49,6 +49,7 @@ __device__ __forceinline__ V3 ld3(const float* p) { return v3(p[0], p[1], p[2]);
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef int i4v __attribute__((ext_vector_type(4)));
 typedef int i8v __attribute__((ext_vector_type(8)));
+typedef float f8v __attribute__((ext_vector_type(8)));
 #ifndef RT_PACKET_OCT
 #define RT_PACKET_OCT 1  // uniform-octant BLAS walks load near/far planes directly (no min/max pairs)
 #endif
@@ -382,8 +383,10 @@ __device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref
                                            float tmin, uint32_t cur, float face, PacketLive<R>& pl, HitRec* hit,
                                            Counters& cnt) {
   // 32-bit byte offsets (pools are < 2 GiB): the scalar load takes them as its SGPR offset
-  const RT_CONST f4v* tq = (const RT_CONST f4v*)((const RT_CONST char*)tpool + (uint32_t)(~ref) * 48u);
-  const f4v ta = tq[0], tb = tq[1], tc = tq[2];
+  const RT_CONST char* tq = (const RT_CONST char*)tpool + (uint32_t)(~ref) * 48u;
+  const f8v tab = *(const RT_CONST f8v*)tq;  // one s_load_dwordx8 + one x4 for the 48-B record
+  const f4v tc = *(const RT_CONST f4v*)(tq + 32);
+  const f4v ta = {tab[0], tab[1], tab[2], tab[3]}, tb = {tab[4], tab[5], tab[6], tab[7]};
   const uint32_t prim = __float_as_uint(ta.w);
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -392,8 +395,9 @@ __device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref
     const bool ok = moller_trumbore_flat(ry.o[r], ry.d[r], v3(ta.x, ta.y, ta.z), v3(tb.x, tb.y, tb.z),
                                          v3(tc.x, tc.y, tc.z), face, t, u, v);
     HitRec& h = hit[r];
-    const bool better = t < h.t || (t == h.t && (cur < h.inst || (cur == h.inst && prim < h.prim)));
-    const bool take = pl.live[r] && ok && t >= tmin && better;
+    // bitwise & / | (no short-circuit): no exec-mask branches around the compares (-2 %)
+    const bool better = (t < h.t) | ((t == h.t) & ((cur < h.inst) | ((cur == h.inst) & (prim < h.prim))));
+    const bool take = pl.live[r] & ok & (t >= tmin) & better;
     // an any-hit ray that accepts leaves the packet with t = -inf: every later slab test rejects it
     h.t = take ? (ANY_HIT ? -__builtin_inff() : t) : h.t;
     h.u = take ? u : h.u;
