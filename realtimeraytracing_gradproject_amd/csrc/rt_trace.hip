@@ -466,10 +466,10 @@ __device__ __forceinline__ uint32_t packet_slabs(const f4v (&pl6)[6], const Pack
 // TLAS node of the packet walk (children: TLAS nodes and instance leaves). The entered children go
 // nearest first by the lead ray's entry distance (lowest slot on ties); the others are pushed in
 // descending slot order, so the lowest slot pops next. Pushes that do not happen write the spare
-// lane kPacketStack - 1; the bookkeeping is plain integer SALU work. Returns 1 with *next set,
-// 0 when nothing is left to descend into.
+// lane kPacketStack - 1; the bookkeeping is plain integer SALU work. Returns true with *next set,
+// false when nothing is left to descend into.
 template <bool ANY_HIT, bool STATS, int R>
-__device__ __forceinline__ int packet_tlas_node(const RT_CONST char* pool, int ref, const PacketRay<R>& ry,
+__device__ __forceinline__ bool packet_tlas_node(const RT_CONST char* pool, int ref, const PacketRay<R>& ry,
                                                 float tmin, PacketLive<R>& pl, const HitRec* hit, WaveStack& stk,
                                                 int& sp, int cap, int& next, Counters& cnt) {
   const RT_CONST char* nb = pool + ((uint32_t)ref << 7);
@@ -482,7 +482,7 @@ __device__ __forceinline__ int packet_tlas_node(const RT_CONST char* pool, int r
   // pin the child-ref load before the early exit: issued with the plane loads, it shares their
   // scalar-cache round trip instead of starting a second one after the slab tests
   asm volatile("" ::"s"(ch[0]), "s"(ch[1]), "s"(ch[2]), "s"(ch[3]));
-  if (ent == 0) return 0;
+  if (ent == 0) return false;
   // nearest entered child by the lead ray's key, lowest slot on ties: per lane in VALU (keys
   // masked to the entered set), one readlane. Any-hit walks take the lowest entered slot.
   uint32_t ib;
@@ -517,7 +517,7 @@ __device__ __forceinline__ int packet_tlas_node(const RT_CONST char* pool, int r
   }
   sp = __builtin_amdgcn_readfirstlane(sp + __builtin_popcount(P));  // uniform by construction: an SGPR
   next = rb;
-  return 1;
+  return true;
 }
 
 // BLAS walk of the packet (instance cur, object rays ry) on the stack above `base`; returns false
@@ -643,12 +643,11 @@ __device__ __forceinline__ void packet_walk(const SceneView& sc, const V3* o, co
   // TLAS walk; each instance leaf runs a nested BLAS walk on the stack above the TLAS entries
   // (the world rays are invariant here, the object rays inside: no ray state moves around).
   while (true) {
-    int next;
+    bool descend = false;
     if (ref >= 0) {
-      if (packet_tlas_node<ANY_HIT, STATS, R>(pool, ref, w, tmin, pl, hit, stk, sp, cap, next, cnt)) {
-        ref = next;
-        continue;
-      }
+      int next;
+      descend = packet_tlas_node<ANY_HIT, STATS, R>(pool, ref, w, tmin, pl, hit, stk, sp, cap, next, cnt);
+      ref = descend ? next : ref;
     } else {
       const uint32_t cur = (uint32_t)(~ref);
       const RT_CONST InstanceRec& ir = ipool[cur];
@@ -685,8 +684,10 @@ __device__ __forceinline__ void packet_walk(const SceneView& sc, const V3* o, co
                                                                            cur, face, pl, hit, stk, sp, cap, oc, cnt);
       if (ANY_HIT && !more) return;
     }
-    if (sp == 0) return;
-    ref = stk.get(--sp);
+    if (!descend) {
+      if (sp == 0) return;
+      ref = stk.get(--sp);
+    }
   }
 }
 
