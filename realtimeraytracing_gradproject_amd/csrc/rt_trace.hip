@@ -348,18 +348,21 @@ __device__ __forceinline__ uint32_t nonzero_mask4(const uint64_t (&m)[4]) {
 
 // Live rays of the packet: one ballot mask per ray slot r, and the lead ray (lowest r, then
 // lowest lane).
+// A ray is live while its t is not -inf: rays that are not alive start at -inf, and an any-hit ray
+// that accepts a hit goes to -inf (no per-lane flag to maintain).
+__device__ __forceinline__ bool ray_live(const HitRec& h) { return __float_as_uint(h.t) != 0xff800000u; }
+
 template <int R>
 struct PacketLive {
-  bool live[R];
   uint64_t mask[R];
   uint32_t lead_r, lead_l;
-  __device__ __forceinline__ bool update() {  // false when no ray is live
+  __device__ __forceinline__ bool update(const HitRec* hit) {  // false when no ray is live
     bool any = false;
     lead_r = 0;
     lead_l = 0;
 #pragma unroll
     for (int r = R - 1; r >= 0; --r) {
-      mask[r] = wave_ballot(live[r]);
+      mask[r] = wave_ballot(ray_live(hit[r]));
       if (mask[r]) {
         any = true;
         lead_r = (uint32_t)r;
@@ -390,21 +393,23 @@ __device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref
   const uint32_t prim = __float_as_uint(ta.w);
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    if (STATS && pl.live[r]) ++cnt.tri;
+    if (STATS && ray_live(hit[r])) ++cnt.tri;
     float t, u, v;
     const bool ok = moller_trumbore_flat(ry.o[r], ry.d[r], v3(ta.x, ta.y, ta.z), v3(tb.x, tb.y, tb.z),
                                          v3(tc.x, tc.y, tc.z), face, t, u, v);
     HitRec& h = hit[r];
     // bitwise & / | (no short-circuit): no exec-mask branches around the compares (-2 %)
-    const bool better = (t < h.t) | ((t == h.t) & ((cur < h.inst) | ((cur == h.inst) & (prim < h.prim))));
-    const bool take = pl.live[r] & ok & (t >= tmin) & better;
+    // a ray that is not live has t = -inf and takes nothing; a live any-hit ray still holds
+    // {tmax, ~0, ~0}, for which the (t, instance, primitive) order reduces to t <= tmax
+    const bool better = ANY_HIT ? (t <= h.t)
+                                : (t < h.t) | ((t == h.t) & ((cur < h.inst) | ((cur == h.inst) & (prim < h.prim))));
+    const bool take = ok & (t >= tmin) & better;
     // an any-hit ray that accepts leaves the packet with t = -inf: every later slab test rejects it
     h.t = take ? (ANY_HIT ? -__builtin_inff() : t) : h.t;
     h.u = take ? u : h.u;
     h.v = take ? v : h.v;
     h.inst = take ? cur : h.inst;
     h.prim = take ? prim : h.prim;
-    if (ANY_HIT) pl.live[r] = pl.live[r] && !take;
   }
 }
 
@@ -451,7 +456,7 @@ __device__ __forceinline__ uint32_t packet_slabs(const f4v (&pl6)[6], const Pack
       hm[r][k] = wave_ballot(h);  // dead rays carry tbest = -inf: their h is false
       vkey[r][k] = h ? (__float_as_uint(n) & 0x7fffffffu) : 0x7f800000u;
     }
-    if (STATS && pl.live[r]) cnt.aabb += count;
+    if (STATS && ray_live(hit[r])) cnt.aabb += count;
   }
   uint64_t any[4];
 #pragma unroll
@@ -509,7 +514,7 @@ __device__ __forceinline__ bool packet_tlas_node(const RT_CONST char* pool, int 
   const uint32_t P = ent & ~(1u << ib);
   if (STATS && sp + __builtin_popcount(P) > cap)  // never: cap is the exact worst case
 #pragma unroll
-    for (int r = 0; r < R; ++r) cnt.overflow += pl.live[r] ? 1u : 0u;
+    for (int r = 0; r < R; ++r) cnt.overflow += ray_live(hit[r]) ? 1u : 0u;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int pos = sp + __builtin_popcount(P >> (k + 1));
@@ -566,7 +571,7 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
         packet_tri<ANY_HIT, STATS, R>(tpool, c4[k], ry, tmin, cur, face, pl, hit, cnt);
       } while (tl);
       if (ANY_HIT) {  // rays can only have left the packet in a triangle test
-        if (!pl.update()) return false;
+        if (!pl.update(hit)) return false;
         // children only finished rays wanted are dropped
         uint64_t any[4];
 #pragma unroll
@@ -602,7 +607,7 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
       }
       if (STATS && (ent & ~(1u << ib)) && sp + 1 > cap)  // never: cap bounds the entries (one per level)
 #pragma unroll
-        for (int r = 0; r < R; ++r) cnt.overflow += pl.live[r] ? 1u : 0u;
+        for (int r = 0; r < R; ++r) cnt.overflow += ray_live(hit[r]) ? 1u : 0u;
       stk.v = push_entry(stk.v, sp, (uint32_t)ch[7], ent, 1u << ib);
       bref = (int)((uint32_t)ch[5] + (uint32_t)__builtin_popcount(imask & ((1u << ib) - 1u)));
     } else {
@@ -629,13 +634,12 @@ __device__ __forceinline__ void packet_walk(const SceneView& sc, const V3* o, co
     hit[r].inst = 0xffffffffu;
     hit[r].prim = 0xffffffffu;
     hit[r].u = hit[r].v = 0.0f;
-    pl.live[r] = alive[r];
     w.o[r] = o[r];
     w.d[r] = d[r];
     w.invd[r] = v3(safe_inv(d[r].x), safe_inv(d[r].y), safe_inv(d[r].z));
     w.noinv[r] = neg(mul(o[r], w.invd[r]));
   }
-  if (!pl.update()) return;
+  if (!pl.update(hit)) return;
   WaveStack stk;
   const int cap = sc.packet_cap;  // < kPacketStack (checked at launch): lane 63 stays spare
   int sp = 0;
@@ -657,7 +661,7 @@ __device__ __forceinline__ void packet_walk(const SceneView& sc, const V3* o, co
       PacketRay<R> b;
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        if (STATS && pl.live[r]) ++cnt.inst;
+        if (STATS && ray_live(hit[r])) ++cnt.inst;
         b.o[r] = xform_point(m, o[r]);
         b.d[r] = xform_dir(m, d[r]);
         b.invd[r] = v3(safe_inv(b.d[r].x), safe_inv(b.d[r].y), safe_inv(b.d[r].z));
