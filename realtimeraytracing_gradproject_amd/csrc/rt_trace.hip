@@ -584,14 +584,17 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
       }
     }
     if (ent) {
-      uint32_t ib;
+      uint32_t ib, nref;
       if (ANY_HIT) {
         // occlusion rays skip the nearest-first choice (no keys, no readlane): for an occlusion ray
         // the order only decides how soon it stops
         ib = (uint32_t)__builtin_ctz(ent);
+        nref = (uint32_t)ch[5] + (uint32_t)__builtin_popcount(imask & ((1u << ib) - 1u));
       } else {
         // per lane: the slot of its smallest key over the entered internal children (all-ones
-        // keys elsewhere), lowest slot on ties; the lead lane's answer is the packet's
+        // keys elsewhere), lowest slot on ties, and that child's ref (first_inner + internal
+        // children below it: v_bfm / v_and / v_bcnt in VALU), packed as ref << 2 | slot; the lead
+        // lane's answer, one readlane, is the packet's
         const uint32_t nent = ~ent;
         uint32_t idx = 0;
 #pragma unroll
@@ -601,15 +604,18 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
           for (int k = 0; k < 4; ++k) kk[k] = vkey[r][k] | bit_mask_v(nent, k);
           const uint32_t m = min(min(kk[0], kk[1]), min(kk[2], kk[3]));
           const uint32_t ir = kk[0] == m ? 0u : kk[1] == m ? 1u : kk[2] == m ? 2u : 3u;
-          idx = (r == 0 || pl.lead_r == (uint32_t)r) ? ir : idx;
+          const uint32_t pr = (((uint32_t)ch[5] + (uint32_t)__builtin_popcount(imask & ((1u << ir) - 1u))) << 2) | ir;
+          idx = (r == 0 || pl.lead_r == (uint32_t)r) ? pr : idx;
         }
-        ib = (uint32_t)__builtin_amdgcn_readlane((int)idx, (int)pl.lead_l);
+        const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)idx, (int)pl.lead_l);
+        ib = pk & 3u;
+        nref = pk >> 2;
       }
       if (STATS && (ent & ~(1u << ib)) && sp + 1 > cap)  // never: cap bounds the entries (one per level)
 #pragma unroll
         for (int r = 0; r < R; ++r) cnt.overflow += ray_live(hit[r]) ? 1u : 0u;
       stk.v = push_entry(stk.v, sp, (uint32_t)ch[7], ent, 1u << ib);
-      bref = (int)((uint32_t)ch[5] + (uint32_t)__builtin_popcount(imask & ((1u << ib) - 1u)));
+      bref = (int)nref;
     } else {
       if (sp == base) return true;
       // top entry: its lowest pending slot is next; the entry stays while slots remain
