@@ -150,10 +150,80 @@ def config(name: str) -> SceneSpec:
         if name == "REFLO":
             s.camera = ((9.0, 6.0, 11.0), (-1.5, 0.5, 0.0), (0.0, 1.0, 0.0))
         return s
+    if name == "DEGEN":
+        return degenerate_scene()
     raise KeyError(name)
 
 
-CONFIGS = ("REF", "C1", "C2", "C2F", "C3", "C4", "C5", "REFL", "REFLO")
+CONFIGS = ("REF", "C1", "C2", "C2F", "C3", "C4", "C5", "REFL", "REFLO", "DEGEN")
+
+
+def _rot_scale(axis, angle_deg: float, scale, t) -> np.ndarray:
+    """3x4 row-major object-to-world: rotation about `axis`, then per-axis scale, then translation."""
+    a = np.asarray(axis, np.float64)
+    a = a / np.linalg.norm(a)
+    c, s = np.cos(np.radians(angle_deg)), np.sin(np.radians(angle_deg))
+    K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+    R = np.eye(3) + s * K + (1 - c) * (K @ K)
+    M = np.diag(np.asarray(scale, np.float64)) @ R
+    x = np.zeros((3, 4))
+    x[:, :3] = M
+    x[:, 3] = t
+    return x.astype(np.float32).ravel()
+
+
+def degenerate_soup(ntri: int = 1500, seed: int = 77) -> np.ndarray:
+    """Non-indexed triangle soup with the inputs an LBVH build and Moller-Trumbore must survive:
+    ordinary triangles, collinear (zero-area) ones, single points, exact duplicates, slivers
+    spanning the whole box and axis-aligned (zero-thickness) ones. Normals (0,1,0)."""
+    rng = np.random.default_rng(seed)
+    p = np.empty((ntri, 3, 3), np.float32)
+    kind = rng.integers(0, 6, size=ntri)
+    for k in range(ntri):
+        c = rng.uniform(-3.0, 3.0, size=3)
+        v = c + rng.normal(scale=0.35, size=(3, 3))
+        if kind[k] == 1:    # collinear
+            v[2] = v[0] + rng.uniform(-2.0, 2.0) * (v[1] - v[0])
+        elif kind[k] == 2:  # a point
+            v[:] = v[0]
+        elif kind[k] == 3 and k > 0:  # duplicate of the previous triangle
+            v = p[k - 1].astype(np.float64)
+        elif kind[k] == 4:  # sliver across the box
+            v[1] = -v[0] + rng.normal(scale=1e-3, size=3)
+            v[2] = v[1] + rng.normal(scale=1e-4, size=3)
+        elif kind[k] == 5:  # zero thickness in y
+            v[:, 1] = v[0, 1]
+        p[k] = v
+    out = np.zeros((ntri * 3, 6), np.float32)
+    out[:, :3] = p.reshape(-1, 3)
+    out[:, 4] = 1.0
+    return out
+
+
+def point_cloud_mesh(ntri: int = 16) -> np.ndarray:
+    """Every vertex at one point: a BLAS whose bounds have zero extent on all three axes."""
+    out = np.zeros((ntri * 3, 6), np.float32)
+    out[:, :3] = (0.25, 0.5, -0.75)
+    out[:, 4] = 1.0
+    return out
+
+
+def degenerate_scene() -> SceneSpec:
+    """DEGEN: the degenerate soup under identity, rotated + non-uniformly scaled, and mirrored
+    instances, the teapot rotated, a zero-extent BLAS and the ground plane (test scene, not a
+    BASELINE config)."""
+    teapot = _model("teapot")
+    meshes = [(degenerate_soup(), None), teapot, (point_cloud_mesh(), None), (plane_vertices(), None)]
+    inst = [
+        (0, IDENTITY, 0, RT_HITGROUP_MODEL),
+        (0, _rot_scale((1, 2, 0.5), 33.0, (1.5, 0.6, 1.0), (6.0, 1.0, -2.0)), 1, RT_HITGROUP_MODEL),
+        (0, _rot_scale((0, 1, 0), -70.0, (-1.0, 1.0, 1.0), (-6.0, 2.0, 1.0)), 2, RT_HITGROUP_MODEL),  # mirrored
+        (1, _rot_scale((0.3, 1, -0.2), 125.0, (1.2, 1.2, 1.2), (0.0, 0.5, 6.0)), 3, RT_HITGROUP_MODEL),
+        (2, IDENTITY, 4, RT_HITGROUP_MODEL),
+        (3, IDENTITY, 5, RT_HITGROUP_PLANE),
+    ]
+    return SceneSpec("DEGEN", meshes, inst, REFERENCE_LIGHTS[:2], REFERENCE_MATERIAL,
+                     ((14.0, 9.0, 16.0), (0.0, 1.0, 1.0), (0.0, 1.0, 0.0)), 320, 180, RT_SHADE_LAMBERT_SHADOW)
 
 
 def upload(ctx, spec: SceneSpec) -> List[int]:

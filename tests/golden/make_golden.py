@@ -32,8 +32,8 @@ import oracle  # noqa: E402
 from oracle import np_reference  # noqa: E402
 
 SIZES = {"REF": (96, 54), "C1": (64, 64), "C2": (96, 54), "C2F": (96, 54), "C3": (96, 54), "C4": (96, 54),
-         "C5": (48, 27), "REFL": (96, 54), "REFLO": (96, 54)}
-NUMPY_CHECK = {"REF", "C1", "C2", "C2F", "C3", "C4"}  # C5 (257 instances x 4 spp) is too slow in numpy
+         "C5": (48, 27), "REFL": (96, 54), "REFLO": (96, 54), "DEGEN": (96, 54)}
+NUMPY_CHECK = {"REF", "C1", "C2", "C2F", "C3", "C4", "DEGEN"}  # C5 (257 instances x 4 spp) is too slow in numpy
 NUMPY_TOL = 1e-4
 
 

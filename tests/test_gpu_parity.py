@@ -95,6 +95,18 @@ def test_blas_edge_sizes(ntri):
     c.close()
 
 
+@pytest.mark.parametrize("mesh", ["soup", "point"])
+def test_blas_degenerate_geometry(mesh):
+    # zero-area, point, duplicate, sliver and flat triangles; a BLAS with zero extent on every axis
+    v = scenes.degenerate_soup() if mesh == "soup" else scenes.point_cloud_mesh()
+    c = fresh_ctx()
+    gn, gt = c.blas_export(c.blas_build(v))
+    o = oracle.Scene()
+    on, ot = o.export_blas(o.add_blas(v))
+    assert np.array_equal(gn, on) and np.array_equal(gt, ot)
+    c.close()
+
+
 def test_blas_duplicate_centroids():
     # many triangles with identical Morton codes: Karras tie-break on leaf position
     v = np.zeros((300 * 3, 6), np.float32)
@@ -111,7 +123,7 @@ def test_blas_duplicate_centroids():
     c.close()
 
 
-@pytest.mark.parametrize("name", ["REF", "C4"])
+@pytest.mark.parametrize("name", ["REF", "C4", "DEGEN"])
 def test_tlas_bitwise_equal_to_oracle(name):
     spec = scenes.config(name)
     c, o = load_both(spec)
@@ -126,7 +138,7 @@ def test_tlas_bitwise_equal_to_oracle(name):
 # ------------------------------------------------------------------------------------------
 
 SMALL = {"REF": (160, 90), "C1": (128, 128), "C2": (192, 108), "C3": (192, 108), "C4": (192, 108),
-         "C5": (96, 54), "REFL": (160, 90), "REFLO": (160, 90)}
+         "C5": (96, 54), "REFL": (160, 90), "REFLO": (160, 90), "DEGEN": (320, 180)}
 
 
 SCHEDULES = {"packet": rt.RT_SCHED_PACKET, "lane": rt.RT_SCHED_LANE}
@@ -144,7 +156,7 @@ def test_frame_parity_small(name, sched):
 
 
 @pytest.mark.parametrize("sched", list(SCHEDULES))
-@pytest.mark.parametrize("name", ["REF", "C2", "C2F", "C4", "C5", "REFL", "REFLO"])
+@pytest.mark.parametrize("name", ["REF", "C2", "C2F", "C4", "C5", "REFL", "REFLO", "DEGEN"])
 def test_counters_match_oracle(name, sched):
     """Traversal counters equal the oracle's emulation of the same schedule: same visit order."""
     spec = scenes.config(name).with_size(*SMALL.get(name, (192, 108)))
@@ -262,6 +274,34 @@ def test_trace_rays_equals_bruteforce(any_hit, cull):
         bb, _, _ = o.trace_rays(rays[:20000], any_hit=True, brute_force=True)
         assert np.array_equal(g[:20000, 3], bb[:, 3]), "occlusion flag differs from brute force"
     assert g[:, 3].sum() > n // 10  # the sample actually hits geometry
+    c.close()
+
+
+@pytest.mark.parametrize("any_hit,cull", [(False, None), (True, None), (False, "back"), (False, "front")])
+def test_trace_rays_degenerate_and_transformed(any_hit, cull):
+    """DEGEN: degenerate triangles under rotated, scaled and mirrored instances (the mirrored one
+    swaps the culled face), plus a zero-extent BLAS: GPU == oracle BVH == brute force."""
+    spec = scenes.config("DEGEN")
+    c, o = load_both(spec)
+    n = 60000
+    rays = random_rays(n, 0xDE6E, center=(0.0, 1.0, 1.0), radius=14.0)
+    d_rays = torch.from_numpy(rays).cuda()
+    d_hits = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+    d_uv = torch.zeros((n, 2), dtype=torch.float32, device="cuda")
+    c.trace_rays(d_rays, n, any_hit, d_hits, d_uv, cull_back=cull == "back", cull_front=cull == "front")
+    torch.cuda.synchronize()
+    g = d_hits.cpu().numpy().view(np.uint32)
+    guv = d_uv.cpu().numpy()
+    kw = dict(any_hit=any_hit, cull_back=cull == "back", cull_front=cull == "front")
+    ob, ouv, _ = o.trace_rays(rays, **kw)
+    assert np.array_equal(g, ob) and np.array_equal(guv, ouv)
+    sub = slice(0, 8000)
+    bb, buv, _ = o.trace_rays(rays[sub], brute_force=True, **kw)
+    if any_hit:
+        assert np.array_equal(g[sub, 3], bb[:, 3])
+    else:
+        assert np.array_equal(g[sub], bb) and np.array_equal(guv[sub], buv)
+    assert len(np.unique(g[g[:, 3] == 1, 1])) >= 4  # rays reach most instances
     c.close()
 
 
@@ -391,7 +431,7 @@ def test_assemble_kernel_equals_host_twin():
 
 
 GOLDEN_SIZES = {"REF": (96, 54), "C1": (64, 64), "C2": (96, 54), "C2F": (96, 54), "C3": (96, 54), "C4": (96, 54),
-                "C5": (48, 27), "REFL": (96, 54), "REFLO": (96, 54)}
+                "C5": (48, 27), "REFL": (96, 54), "REFLO": (96, 54), "DEGEN": (96, 54)}
 
 
 @pytest.mark.parametrize("name", list(GOLDEN_SIZES))

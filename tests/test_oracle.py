@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "frames_small.npz"))
 SIZES = {"REF": (96, 54), "C1": (64, 64), "C2": (96, 54), "C2F": (96, 54), "C3": (96, 54), "C4": (96, 54),
-         "C5": (48, 27), "REFL": (96, 54), "REFLO": (96, 54)}
+         "C5": (48, 27), "REFL": (96, 54), "REFLO": (96, 54), "DEGEN": (96, 54)}
 
 
 EMPTY = np.int32(-2**31 + 1)
@@ -119,7 +119,7 @@ def test_sah_collapse_beats_greedy(model):
     assert n_dp < n_gr
 
 
-@pytest.mark.parametrize("name", ["REF", "C1", "C2F", "C3", "C4"])
+@pytest.mark.parametrize("name", ["REF", "C1", "C2F", "C3", "C4", "DEGEN"])
 def test_bvh_image_equals_bruteforce(name):
     spec = scenes.config(name).with_size(48, 27)
     o = oracle.Scene(spec)
@@ -152,6 +152,21 @@ def test_trace_rays_bvh_equals_bruteforce(any_hit):
     assert h1[:, 3].sum() > 300
 
 
+@pytest.mark.parametrize("any_hit,cull", [(False, None), (True, None), (False, "back"), (False, "front")])
+def test_trace_rays_degenerate_and_transformed(any_hit, cull):
+    """Degenerate triangles under rotated / scaled / mirrored instances: BVH == brute force."""
+    o = oracle.Scene(scenes.config("DEGEN"))
+    rays = random_rays(3000, 11)
+    kw = dict(any_hit=any_hit, cull_back=cull == "back", cull_front=cull == "front")
+    h1, uv1, _ = o.trace_rays(rays, **kw)
+    h2, uv2, _ = o.trace_rays(rays, brute_force=True, **kw)
+    if any_hit:
+        assert np.array_equal(h1[:, 3], h2[:, 3])
+    else:
+        assert np.array_equal(h1, h2) and np.array_equal(uv1, uv2)
+    assert h1[:, 3].sum() > 300
+
+
 def test_tie_break_duplicate_instances():
     """Instances 1 and 2 of the reference scene coincide (D3D12HelloTriangle.cpp:785-786): the
     lower instance index wins."""
@@ -175,7 +190,7 @@ def test_oracle_matches_golden_frames(name):
         assert np.array_equal(st, GOLD[f"{name}_{key}"])
 
 
-@pytest.mark.parametrize("name", ["REF", "C1", "C2F", "C3"])
+@pytest.mark.parametrize("name", ["REF", "C1", "C2F", "C3", "DEGEN"])
 def test_oracle_vs_independent_numpy(name):
     spec = scenes.config(name).with_size(40, 24)
     img, _ = np_reference.Scene(spec).render(spec.camera_buffer())
