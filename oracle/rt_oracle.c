@@ -394,6 +394,13 @@ static int gather4_dp(const onode* bin, int root, int ref[4], float box[4][6]) {
   int cnt = 0;
   dp_expand(bin, b->c0, l, bj, ref, box, &cnt);
   dp_expand(bin, b->c1, r, 4 - bj, ref, box, &cnt);
+  /* slots by ascending half area, stable (k_dp_expand) */
+  for (int a = 1; a < cnt; ++a)
+    for (int q = a; q > 0 && half_area(box[q]) < half_area(box[q - 1]); --q) {
+      int tr = ref[q]; ref[q] = ref[q - 1]; ref[q - 1] = tr;
+      float tb[6];
+      memcpy(tb, box[q], 24); memcpy(box[q], box[q - 1], 24); memcpy(box[q - 1], tb, 24);
+    }
   return cnt;
 }
 

@@ -483,6 +483,19 @@ __global__ void k_dp_expand(int nbin, const BinNode* __restrict__ bin, const flo
   if (i >= nbin) return;
   Exp4 e;
   e.cnt = gather4_dp(bin, dpc, dps, i, e.ref, e.box);
+  // slots by ascending half area (stable): nearest-first ties (rays starting inside several child
+  // boxes) and the any-hit lowest-slot order then visit the tighter box first
+  for (int a = 1; a < e.cnt; ++a)
+    for (int b = a; b > 0 && half_area6(e.box[b]) < half_area6(e.box[b - 1]); --b) {
+      const int tr = e.ref[b];
+      e.ref[b] = e.ref[b - 1];
+      e.ref[b - 1] = tr;
+      for (int q = 0; q < 6; ++q) {
+        const float t = e.box[b][q];
+        e.box[b][q] = e.box[b - 1][q];
+        e.box[b - 1][q] = t;
+      }
+    }
   for (int j = e.cnt; j < 4; ++j) e.ref[j] = kEmptyChild;
   e.pad[0] = e.pad[1] = e.pad[2] = 0;
   exp[i] = e;

@@ -85,6 +85,22 @@ def test_node_meta_for_packet_stack(model):
         assert u[k, 31] == ((int(u[k, 29]) << 8) | (mask << 4))
 
 
+@pytest.mark.parametrize("model", ["teapot", "rabbit"])
+def test_slots_in_ascending_area(model):
+    """Each node's slots hold its children by ascending half area (stable): the nearest-first walk
+    breaks key ties (rays starting inside several boxes) and any-hit walks go lowest slot first,
+    both then enter the tighter box first."""
+    v, i = scenes.load_model(model)
+    o = oracle.Scene()
+    nodes, _ = o.export_blas(o.add_blas(v, i))
+    lo, hi, ch, count = unpack4(nodes)
+    d = (hi - lo).astype(np.float32)
+    area = (d[..., 0] * d[..., 1] + d[..., 1] * d[..., 2]) + d[..., 2] * d[..., 0]
+    for k in range(len(nodes)):
+        a = area[k, :count[k]]
+        assert (a[1:] >= a[:-1]).all()
+
+
 def _wide_area(model: str, greedy: bool) -> float:
     """Sum of the wide nodes' half areas (the collapse's SAH cost) from a fresh process: the oracle
     reads ORACLE_GREEDY_COLLAPSE once."""
