@@ -232,6 +232,7 @@ typedef struct {
   float w2o[12], o2w[12], nrm[9];
   uint32_t instance_id, hit_group, blas;
   float face; /* +1, or -1 when the transform mirrors (front-face sense flipped for culling) */
+  int translate; /* upper 3x3 exactly the identity: the object ray is (o + t, d) (InstanceRec::translate) */
 } oinst;
 
 struct oracle_scene {
@@ -675,6 +676,11 @@ static vec3 xdir(const float* m, vec3 d) {
   return mk((m[0] * d.x + m[1] * d.y) + m[2] * d.z, (m[4] * d.x + m[5] * d.y) + m[6] * d.z,
             (m[8] * d.x + m[9] * d.y) + m[10] * d.z);
 }
+/* world -> object ray of an instance (inst_point / inst_dir in rt_device.hpp) */
+static vec3 ipoint(const oinst* ir, vec3 p) {
+  return ir->translate ? mk(p.x + ir->w2o[3], p.y + ir->w2o[7], p.z + ir->w2o[11]) : xpoint(ir->w2o, p);
+}
+static vec3 idir(const oinst* ir, vec3 d) { return ir->translate ? d : xdir(ir->w2o, d); }
 static vec3 m3mul(const float* m, vec3 d) {
   return mk((m[0] * d.x + m[1] * d.y) + m[2] * d.z, (m[3] * d.x + m[4] * d.y) + m[5] * d.z,
             (m[6] * d.x + m[7] * d.y) + m[8] * d.z);
@@ -697,6 +703,8 @@ int oracle_set_instances(oracle_scene* s, const oracle_instance* in, uint32_t n)
     const double det = L[0] * (L[4] * L[8] - L[5] * L[7]) + L[1] * (L[5] * L[6] - L[3] * L[8]) +
                        L[2] * (L[3] * L[7] - L[4] * L[6]);
     r->face = det < 0.0 ? -1.0f : 1.0f;
+    r->translate = M[0] == 1.0f && M[1] == 0.0f && M[2] == 0.0f && M[4] == 0.0f && M[5] == 1.0f && M[6] == 0.0f &&
+                   M[8] == 0.0f && M[9] == 0.0f && M[10] == 1.0f;
     double t[3] = {M[3], M[7], M[11]};
     for (int a = 0; a < 3; ++a) {
       r->w2o[a * 4 + 0] = (float)Li[a * 3 + 0];
@@ -838,8 +846,8 @@ static int otrace(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax,
       st->v[4]++;
       if (sp < cap) {
         stack[sp++] = SENT;
-        ro = xpoint(ir->w2o, o);
-        rd = xdir(ir->w2o, d);
+        ro = ipoint(ir, o);
+        rd = idir(ir, d);
         rinvd = mk(sinv(rd.x), sinv(rd.y), sinv(rd.z));
         rno = vneg(vmul(ro, rinvd));
         nodes = s->blas[ir->blas].nodes;
@@ -998,8 +1006,8 @@ static void opacket(const oracle_scene* s, const vec3* o, const vec3* d, float t
       const oblas* bl = &s->blas[ir->blas];
       for (int l = 0; l < OPK; ++l) {
         if (live[l]) st->v[4]++;
-        b.o[l] = xpoint(ir->w2o, o[l]);
-        b.d[l] = xdir(ir->w2o, d[l]);
+        b.o[l] = ipoint(ir, o[l]);
+        b.d[l] = idir(ir, d[l]);
         b.invd[l] = mk(sinv(b.d[l].x), sinv(b.d[l].y), sinv(b.d[l].z));
         b.no[l] = vneg(vmul(b.o[l], b.invd[l]));
       }
@@ -1028,7 +1036,7 @@ static int obrute(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax,
   for (uint32_t i = 0; i < s->ninst; ++i) {
     const oinst* ir = &s->inst[i];
     const oblas* b = &s->blas[ir->blas];
-    vec3 ro = xpoint(ir->w2o, o), rd = xdir(ir->w2o, d);
+    vec3 ro = ipoint(ir, o), rd = idir(ir, d);
     for (uint32_t k = 0; k < b->ntri; ++k) {
       const otri* tr = &b->tris[k];
       float t, u, v;

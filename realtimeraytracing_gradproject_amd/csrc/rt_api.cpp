@@ -120,6 +120,8 @@ bool fill_instance_xform(const float* o2w, rt::InstanceRec& r) {
   const double det = L[0] * (L[4] * L[8] - L[5] * L[7]) + L[1] * (L[5] * L[6] - L[3] * L[8]) +
                      L[2] * (L[3] * L[7] - L[4] * L[6]);
   r.flip = det < 0.0 ? 1u : 0u;
+  r.translate = (o2w[0] == 1.0f && o2w[1] == 0.0f && o2w[2] == 0.0f && o2w[4] == 0.0f && o2w[5] == 1.0f &&
+               o2w[6] == 0.0f && o2w[8] == 0.0f && o2w[9] == 0.0f && o2w[10] == 1.0f) ? 1u : 0u;
   double t[3] = {o2w[3], o2w[7], o2w[11]};
   for (int i = 0; i < 3; ++i) {
     r.w2o[i * 4 + 0] = (float)Li[i * 3 + 0];

@@ -96,7 +96,8 @@ struct alignas(16) InstanceRec {
   const TriRec* tris;
   uint32_t pool_root;     // the BLAS root's index in the scene pool (see SceneView)
   uint32_t flip;          // instance transform has a negative determinant (front-face sense flipped)
-  uint32_t pad_[2];
+  uint32_t translate;     // upper 3x3 exactly the identity: the object ray is (o + t, d)
+  uint32_t pad_;
   const float* vtx;       // 6 floats per vertex: pos.xyz, normal.xyz (stride 24 B)
   const uint32_t* idx;    // triangle list, or nullptr for non-indexed geometry
 };
@@ -194,6 +195,13 @@ RT_HD V3 xform_dir(const float* m, V3 d) {
   return v3((m[0] * d.x + m[1] * d.y) + m[2] * d.z, (m[4] * d.x + m[5] * d.y) + m[6] * d.z,
             (m[8] * d.x + m[9] * d.y) + m[10] * d.z);
 }
+// World -> object ray of an instance. A pure translation moves the origin only: the general
+// product costs 33 operations (and turns a -0 direction component into +0; safe_inv maps both
+// zeros to +1e20, so the inverse direction is the world ray's).
+RT_HD V3 inst_point(const float* m, uint32_t translate, V3 p) {
+  return translate ? v3(p.x + m[3], p.y + m[7], p.z + m[11]) : xform_point(m, p);
+}
+RT_HD V3 inst_dir(const float* m, uint32_t translate, V3 d) { return translate ? d : xform_dir(m, d); }
 RT_HD V3 mat3_mul(const float* m, V3 d) {
   return v3((m[0] * d.x + m[1] * d.y) + m[2] * d.z, (m[3] * d.x + m[4] * d.y) + m[5] * d.z,
             (m[6] * d.x + m[7] * d.y) + m[8] * d.z);

@@ -199,9 +199,10 @@ __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, H
         ++sp;
         float m[12];
         for (int k = 0; k < 12; ++k) m[k] = ir->w2o[k];
-        ro = xform_point(m, o);
-        rd = xform_dir(m, d);
-        rinvd = v3(safe_inv(rd.x), safe_inv(rd.y), safe_inv(rd.z));
+        const uint32_t tr = ir->translate;
+        ro = inst_point(m, tr, o);
+        rd = inst_dir(m, tr, d);
+        rinvd = tr ? winvd : v3(safe_inv(rd.x), safe_inv(rd.y), safe_inv(rd.z));
         rnoinv = neg(mul(ro, rinvd));
         oct = octant(rinvd);
         if (CULL) face = (ir->flip ? -1.0f : 1.0f) * sc.cull_sense;
@@ -668,9 +669,15 @@ __device__ __forceinline__ void packet_walk(const SceneView& sc, const V3* o, co
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         if (STATS && ray_live(hit[r])) ++cnt.inst;
-        b.o[r] = xform_point(m, o[r]);
-        b.d[r] = xform_dir(m, d[r]);
-        b.invd[r] = v3(safe_inv(b.d[r].x), safe_inv(b.d[r].y), safe_inv(b.d[r].z));
+        if (ir.translate) {  // uniform: origin moved, direction and its inverse are the world ray's
+          b.o[r] = inst_point(m, 1u, o[r]);
+          b.d[r] = d[r];
+          b.invd[r] = w.invd[r];
+        } else {
+          b.o[r] = xform_point(m, o[r]);
+          b.d[r] = xform_dir(m, d[r]);
+          b.invd[r] = v3(safe_inv(b.d[r].x), safe_inv(b.d[r].y), safe_inv(b.d[r].z));
+        }
         b.noinv[r] = neg(mul(b.o[r], b.invd[r]));
       }
       const float face = CULL ? (ir.flip ? -1.0f : 1.0f) * sc.cull_sense : 0.0f;
