@@ -291,7 +291,7 @@ def main():
                        "schedule": a.schedule},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "k_trace_frame", "kernel_ms": round(kernel_ms, 4),
+                         "kernel": "k_trace_frame" if a.schedule == "lane" else "k_trace_frame_packet", "kernel_ms": round(kernel_ms, 4),
                          "bytes_per_launch": int(bytes_launch),
                          "aabb_tests": int(st["aabb_tests"]), "tri_tests": int(st["tri_tests"]),
                          # the BVH (~1 MB) is L2-resident: algorithmic bytes are served by L2/L1, so
