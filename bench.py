@@ -6,21 +6,33 @@ A step is one frame: RayGen -> TLAS/BLAS traversal -> shading + shadow rays -> R
 reference's DispatchRays, D3D12HelloTriangle.cpp:558-592). The scene is static: the LBVH build
 runs once before the timed region and is reported separately (build_ms).
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): every pixel is an
-independent unit, so the job shards with no data-path collective. Default ("frames"): a step is a
-batch of N frames of the configured view, one per rank, each left in its rank's HBM (per-GPU work
-fixed: scaling "weak"). --assemble instead splits ONE frame into interleaved 8-row strips (strip s
--> rank s mod N), gathers them to rank 0 over RCCL and un-interleaves them there
-(rt_assemble_strips): scaling "strong", the presentation path of a single-view frame.
+Multi-GPU (north star "frames are tiled across GPUs with an RCCL gather"): with
+N > 1 a step is ONE frame split into interleaved 8-row strips (strip s -> rank s mod N), each rank
+renders its strips into a compact buffer, one RCCL gather brings them to rank 0 and
+rt_assemble_strips un-interleaves them there: total work fixed, "scaling": "strong". The gather
+and assembly of frame k run on a second stream, overlapped with the render of frame k+1 (two
+buffer slots; a slot is re-rendered only after its gather finished). `bench.py --gpus N` without
+torchrun re-launches itself under torch.distributed.run (N processes, one per GPU) before anything
+touches the GPU. The multi-GPU configs C4 (rabbit x64, 2 lights) and C5 (rabbit x256, 4 lights,
+4K, 4 spp) are timed the same way at the same N and reported under "extra".
 
 value = rays traced in one step (all ranks, counted by the device counters in an untimed pass)
 x steps / max-over-ranks wall time of the timed region.
+
+Untimed before the W warmup frames: the counter pass and a clock settle (--settle-ms of frames:
+the GPU needs ~20 ms of load to reach its steady clock; with 5 warmup frames alone the same build
+read 0.20 ms instead of 0.15 ms per frame).
 """
 from __future__ import annotations
 
 import argparse
+import contextlib
+import hashlib
+import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -32,56 +44,349 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-import realtimeraytracing_gradproject_amd as rt  # noqa: E402
-from realtimeraytracing_gradproject_amd import distributed as D, scenes  # noqa: E402
-
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 L2_PEAK_GBS = 34500.0  # aggregate L2 bandwidth, 8 XCDs (MI355X_MICROARCH.md, L2 section)
-BYTES_PER_AABB_TEST = 24  # one child box (6 floats) per slab test
-BYTES_PER_TRI_TEST = 36   # v0, e1, e2 (9 floats) per Moller-Trumbore test
-BYTES_PER_PIXEL = 4       # RGBA8 write
-STRIP_ROWS = D.STRIP_ROWS
+# Bytes FETCHED per record visit (the roofline numerator; rt_api.h RT_STAT_*_FETCHES): the packet
+# schedule loads each record once per wave into SGPRs, the per-lane schedule once per lane.
+BYTES_PER_NODE_FETCH = 128  # one BVH4 node = one 128-B line (6 plane rows + child record)
+BYTES_PER_TRI_FETCH = 48    # v0 / e1 / e2 rows of a TriRec
+BYTES_PER_INST_FETCH = 64   # world-to-object 3x4 + translate flag + pool root of an InstanceRec
+BYTES_PER_SHADE = 108       # per primary ray (upper bound: misses fetch nothing): 60 B of the
+                            # instance's shading fields + 12 B indices + 36 B of 3 normals / positions
+BYTES_PER_PIXEL = 4         # RGBA8 write
+STRIP_ROWS = 8
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
-    p.add_argument("--warmup", type=int, default=100,
-                   help="untimed frames first: the GPU needs ~20 ms of load to reach steady clocks")
-    p.add_argument("--config", default="C2", choices=[c for c in scenes.CONFIGS])
+    p.add_argument("--warmup", type=int, default=100)
+    p.add_argument("--settle-ms", type=float, default=300.0,
+                   help="untimed frames before the warmup until this much GPU time has passed (clock ramp)")
+    p.add_argument("--config", default="C2")
+    p.add_argument("--size", default="", help="WxH override (tests)")
     p.add_argument("--schedule", default="packet", choices=["packet", "lane"])
+    p.add_argument("--mode", default="auto", choices=["auto", "strips", "frames"],
+                   help="N>1: strips = one frame tiled over ranks + RCCL gather (default); frames = N "
+                        "independent replicas (no collective)")
+    p.add_argument("--no-pipeline", action="store_true", help="strips: gather after each frame, no overlap")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum wall time of the CPU baseline sample")
-    p.add_argument("--assemble", action="store_true",
-                   help="N>1: split one frame into strips and gather it to rank 0 (strong scaling)")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="minimum wall time of the CPU baseline sample")
     p.add_argument("--save-image", default="", help="write the rank-0 frame as .npy")
-    p.add_argument("--extra", default="C2F,C3,C4,C5,REF",
-                   help="comma list of further configs timed on one GPU (N=1 only; '' to skip)")
-    return p.parse_args()
+    p.add_argument("--extra", default=None,
+                   help="comma list of further configs ('' to skip); default N=1: C1,C2F,C3,C4,C5,REF (+ REF "
+                        "raster); N>1: C4,C5 tiled over the same ranks")
+    return p.parse_args(argv)
 
 
-def load_traffic(config: str):
-    """HBM bytes per trace launch from the committed rocprofv3 PMC pass (profiles/), if present."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+# ---------------------------------------------------------------------------------------------
+# launcher: one process per GPU
+# ---------------------------------------------------------------------------------------------
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn(a, argv) -> int:
+    """`bench.py --gpus N` outside torchrun: run N ranks under torch.distributed.run as a CHILD
+    process (nothing here has touched the GPU) and return its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+# ---------------------------------------------------------------------------------------------
+# backends: the HIP library (product) or a test renderer (tests/, CPU + gloo)
+# ---------------------------------------------------------------------------------------------
+
+class _NullStream:
+    cuda_stream = None
+
+    def wait_event(self, e):
+        pass
+
+
+class _NullEvent:
+    def record(self, stream=None):
+        pass
+
+    def elapsed_time(self, other):
+        return 0.0
+
+
+class HipBackend:
+    """rt_* through the C-ABI on this rank's GPU; collectives over RCCL."""
+    dist_backend = "nccl"
+
+    def __init__(self, local: int):
+        import realtimeraytracing_gradproject_amd as rt
+        self.rt = rt
+        torch.cuda.set_device(local)
+        self.local = local
+        self.device = torch.device("cuda", local)
+        self.ctx = None
+
+    def init_pg(self):
+        dist.init_process_group("nccl", device_id=self.device)
+
+    def load(self, spec, schedule: str):
+        from realtimeraytracing_gradproject_amd import scenes
+        if self.ctx is not None:
+            self.ctx.close()
+        self.ctx = self.rt.Context(self.local)
+        scenes.upload(self.ctx, spec)
+        self.ctx.set_schedule(self.rt.RT_SCHED_LANE if schedule == "lane" else self.rt.RT_SCHED_PACKET)
+        self.spec = spec
+        return ([round(self.ctx.blas_info(b).build_ms, 3) for b in range(len(spec.meshes))],
+                round(self.ctx.tlas_info().build_ms, 3))
+
+    def zeros(self, shape):
+        return torch.zeros(shape, dtype=torch.uint8, device=self.device)
+
+    def stream(self):
+        return torch.cuda.Stream(device=self.device)
+
+    def event(self, timing=False):
+        return torch.cuda.Event(enable_timing=timing)
+
+    def use_stream(self, s):
+        return torch.cuda.stream(s)
+
+    def synchronize(self):
+        torch.cuda.synchronize(self.device)
+
+    def dispatch(self, buf, rows, stream):
+        self.ctx.dispatch(self.spec.width, self.spec.height, buf, None, rows=rows, stream=stream.cuda_stream)
+
+    def counted(self, buf, rows, stream) -> dict:
+        self.ctx.set_stats(True)
+        self.ctx.stats_reset()
+        self.dispatch(buf, rows, stream)
+        self.synchronize()
+        st = self.ctx.stats()
+        self.ctx.set_stats(False)
+        return st
+
+    def assemble(self, world, gathered, frame, stream):
+        self.ctx.assemble_strips(self.spec.width, self.spec.height, world, STRIP_ROWS, gathered, frame,
+                                 stream=stream.cuda_stream)
+
+    def raster(self, spec, steps, warmup):
+        return measure_raster(self, spec, steps, warmup)
+
+    def close(self):
+        if self.ctx is not None:
+            self.ctx.close()
+            self.ctx = None
+
+
+def make_backend(local: int):
+    """RT_BENCH_TEST_BACKEND=module:factory (tests only) swaps in a CPU renderer with gloo so the
+    launcher, partition, gather, assembly and timing code below runs without a GPU."""
+    hook = os.environ.get("RT_BENCH_TEST_BACKEND", "")
+    if hook:
+        mod, _, fn = hook.partition(":")
+        return getattr(importlib.import_module(mod), fn)(local)
+    return HipBackend(local)
+
+
+# ---------------------------------------------------------------------------------------------
+# the measured loop
+# ---------------------------------------------------------------------------------------------
+
+def strip_plan(H: int, world: int, rank: int):
+    from realtimeraytracing_gradproject_amd import distributed as D
+    return D.rank_rows(H, world, rank), D.padded_rows(H, world)
+
+
+def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_ms: float, strips: bool,
+               pipeline: bool, schedule: str, save_image: str = ""):
+    """Builds the scene, counts one step's rays (untimed), settles, warms up, then times exactly
+    `steps` steps between barrier + synchronize on both sides. Returns a dict (rank 0 meaningful)."""
+    from realtimeraytracing_gradproject_amd import distributed as D
+    distributed = world > 1
+    W, H = spec.width, spec.height
+    build = be.load(spec, schedule)
+    if strips:
+        rows, rows_per_rank = strip_plan(H, world, rank)
+    else:
+        rows, rows_per_rank = None, H
+    nslot = 2 if (strips and pipeline) else 1
+    render = be.stream()
+    comm = be.stream() if strips else render
+    local = [be.zeros((rows_per_rank, W, 4)) for _ in range(nslot)]
+    gathered = [be.zeros((world, rows_per_rank, W, 4)) if rank == 0 else None for _ in range(nslot)] if strips else None
+    frame = [be.zeros((H, W, 4)) if rank == 0 else None for _ in range(nslot)] if strips else None
+    rendered = [be.event() for _ in range(nslot)]
+    freed = [be.event() for _ in range(nslot)]
+
+    def step(k: int):
+        s = k % nslot
+        if strips:
+            render.wait_event(freed[s])  # slot s free: the gather of frame k - nslot is done
+        be.dispatch(local[s], rows, render)
+        if strips:
+            rendered[s].record(render)
+            comm.wait_event(rendered[s])
+            with be.use_stream(comm):
+                D.gather_strips(local[s], world, rank, gathered[s])
+                if rank == 0:
+                    be.assemble(world, gathered[s], frame[s], comm)
+            freed[s].record(comm)
+
+    # untimed counter pass: rays, tests and record fetches of this rank's share of one step
+    st = be.counted(local[0], rows, render)
+    counts = torch.tensor([st["primary_rays"] + st["shadow_rays"], st["primary_rays"], st["shadow_rays"]],
+                          dtype=torch.float64, device=be.device)
+    if distributed:
+        dist.all_reduce(counts)
+    rays_step = int(counts[0].item()) if strips else int(counts[0].item())  # frames mode: N frames' rays
+
+    # clock settle + warmup (untimed)
+    k = 0
+    if settle_ms > 0:
+        t0 = time.perf_counter()
+        while (time.perf_counter() - t0) * 1e3 < settle_ms:
+            for _ in range(4):
+                step(k)
+                k += 1
+            be.synchronize()
+    for _ in range(warmup):
+        step(k)
+        k += 1
+    be.synchronize()
+    if distributed:
+        dist.barrier()
+    be.synchronize()
+
+    # timed region. One HIP event pair on the render stream brackets it (per-launch events would
+    # put a timestamp between back-to-back frames); in strips mode the pair brackets renders only
+    e0, e1 = be.event(True), be.event(True)
+    t0 = time.perf_counter()
+    e0.record(render)
+    for _ in range(steps):
+        step(k)
+        k += 1
+    e1.record(render)
+    be.synchronize()
+    if distributed:
+        dist.barrier()
+    be.synchronize()
+    elapsed = time.perf_counter() - t0
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=be.device)
+    if distributed:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    tmax = float(tmax.item())
+    render_ms = e0.elapsed_time(e1) / steps
+
+    if strips:
+        # the roofline's kernel time: this rank's render alone, back to back (untimed for value)
+        be.synchronize()
+        f0, f1 = be.event(True), be.event(True)
+        f0.record(render)
+        for _ in range(max(5, min(steps, 50))):
+            be.dispatch(local[0], rows, render)
+        f1.record(render)
+        be.synchronize()
+        kernel_ms = f0.elapsed_time(f1) / max(5, min(steps, 50))
+    else:
+        kernel_ms = render_ms
+
+    if save_image and rank == 0:
+        last = (k - 1) % nslot
+        img = frame[last] if strips else local[0][:H]
+        np.save(save_image, img.cpu().numpy())
+    return {"rays_step": rays_step, "primary": int(counts[1].item()), "shadow": int(counts[2].item()),
+            "tmax": tmax, "kernel_ms": kernel_ms, "stats": st, "build": build, "rows_local": len(rows) if strips else H}
+
+
+# ---------------------------------------------------------------------------------------------
+# roofline
+# ---------------------------------------------------------------------------------------------
+
+def lib_sha() -> str:
+    p = os.path.join(ROOT, "realtimeraytracing_gradproject_amd", "lib", "librtamd.so")
     try:
-        with open(path) as f:
-            d = json.load(f)
-        e = d.get(config)
-        return float(e["bytes_per_launch"]) if e else None
-    except Exception:
+        with open(p, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        return ""
+
+
+def load_profile(config: str):
+    """Per-launch HBM traffic and SQ issue counts of the trace kernel from the committed rocprofv3
+    passes (profiles/roofline_inputs.json, written by tools/roofline.py summarize)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "roofline_inputs.json")) as f:
+            return json.load(f).get(config)
+    except (OSError, ValueError):
         return None
 
 
-def cpu_baseline(spec, seconds: float):
-    """The oracle (scalar C, pthreads over interleaved rows) on the same frame, on this host."""
-    import oracle
+def fetched_bytes(st: dict, pixels: int) -> int:
+    return (BYTES_PER_NODE_FETCH * st["node_fetches"] + BYTES_PER_TRI_FETCH * st["tri_fetches"]
+            + BYTES_PER_INST_FETCH * st["instance_fetches"] + BYTES_PER_SHADE * st["primary_rays"]
+            + BYTES_PER_PIXEL * pixels)
 
-    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    threads = max(1, min(16, ncpu or 1))
+
+def roofline(config: str, st: dict, pixels: int, kernel_ms: float, schedule: str) -> dict:
+    """Fetched bytes per launch (per-wave record fetches, counted by the STATS pass) against the L2
+    roof, the measured HBM traffic against the HBM roof, and the SALU / VALU issue fractions from the
+    committed SQ counters; `bound` names the pipe closest to its roof."""
+    b = fetched_bytes(st, pixels)
+    achieved = b / (kernel_ms * 1e-3) / 1e9
+    prof = load_profile(config) or {}
+    traffic = prof.get("hbm_bytes_per_launch")
+    issue = prof.get("issue")
+    fracs = {"l2": achieved / L2_PEAK_GBS}
+    if traffic:
+        fracs["hbm"] = traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+    if issue:
+        fracs["salu"] = issue["salu_frac"]
+        fracs["valu"] = issue["valu_frac"]
+    bound = max(fracs, key=fracs.get)
+    out = {"bound": bound, "achieved": round(achieved, 1), "peak": L2_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / L2_PEAK_GBS, 4), "traffic": traffic,
+           "kernel": "k_trace_frame" if schedule == "lane" else "k_trace_frame_packet",
+           "kernel_ms": round(kernel_ms, 4), "bytes_per_launch": int(b),
+           "model": (f"{BYTES_PER_NODE_FETCH} B/node fetch + {BYTES_PER_TRI_FETCH} B/triangle fetch + "
+                     f"{BYTES_PER_INST_FETCH} B/instance fetch (per wave in packets) + {BYTES_PER_SHADE} B/primary "
+                     f"ray shading + {BYTES_PER_PIXEL} B/pixel"),
+           "node_fetches": int(st["node_fetches"]), "tri_fetches": int(st["tri_fetches"]),
+           "instance_fetches": int(st["instance_fetches"]),
+           "aabb_tests": int(st["aabb_tests"]), "tri_tests": int(st["tri_tests"]),
+           "fracs": {k: round(v, 4) for k, v in fracs.items()}}
+    if traffic:
+        out["hbm"] = {"achieved": round(traffic / (kernel_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                      "frac": round(fracs["hbm"], 4), "source": prof.get("source")}
+    if issue:
+        out["issue"] = dict(issue)
+        out["issue"]["profile_lib_sha"] = prof.get("lib_sha")
+        out["issue"]["stale"] = bool(prof.get("lib_sha")) and prof.get("lib_sha") != lib_sha()
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# CPU baseline (rank 0, N = 1): the oracle's scalar per-ray traversal of the same BVH
+# ---------------------------------------------------------------------------------------------
+
+def cpu_baseline(spec, seconds: float):
+    """oracle/rt_oracle.c (scalar C, per-ray traversal over the identical trees, pthreads over
+    interleaved rows) on the same frame, on every CPU this process may run on; plus one thread, and
+    C1 (BASELINE configs[0]: teapot 512^2 primary only, the reference's CPU plumbing case)."""
+    import oracle
+    from realtimeraytracing_gradproject_amd import scenes
+
+    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = max(1, min(256, ncpu))  # oracle_render caps its pool at 256 threads
     o = oracle.Scene(spec)
-    rays = 0
-    frames = 0
+    rays = frames = 0
     t0 = time.perf_counter()
     while True:
         _, _, st = o.render_spec(spec, nthreads=threads, want_float=False, schedule=1)  # per-ray: the CPU form
@@ -90,62 +395,53 @@ def cpu_baseline(spec, seconds: float):
         dt = time.perf_counter() - t0
         if dt >= seconds:
             break
-    # also one thread, and the host CPU model
     t1 = time.perf_counter()
     _, _, st1 = o.render_spec(spec, nthreads=1, want_float=False, schedule=1)
     dt1 = time.perf_counter() - t1
+    c1 = scenes.config("C1")
+    o1 = oracle.Scene(c1)
+    t2 = time.perf_counter()
+    n1 = 0
+    r1 = 0
+    while True:
+        _, _, s1 = o1.render_spec(c1, nthreads=threads, want_float=False, schedule=1)
+        r1 += int(s1[0] + s1[1])
+        n1 += 1
+        if time.perf_counter() - t2 >= 2.0:
+            break
+    d2 = time.perf_counter() - t2
+    t3 = time.perf_counter()
+    _, _, s1b = o1.render_spec(c1, nthreads=1, want_float=False, schedule=1)
+    d3 = time.perf_counter() - t3
     model = None
     try:
         with open("/proc/cpuinfo") as f:
             model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), None)
     except OSError:
         pass
-    return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{frames} full {spec.name} frame(s) {spec.width}x{spec.height} by oracle/rt_oracle.c "
-                      f"({threads} threads, {dt:.1f} s wall)",
-            "single_thread": round(int(st1[0] + st1[1]) / dt1 / 1e6, 3), "host_cpus": ncpu, "cpu_model": model}
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{frames} full {spec.name} frame(s) {spec.width}x{spec.height} by oracle/rt_oracle.c per-ray "
+                      f"traversal ({threads} threads, {dt:.1f} s wall)",
+            "single_thread": round(int(st1[0] + st1[1]) / dt1 / 1e6, 3), "host_cpus": ncpu,
+            "os_cpu_count": os.cpu_count(), "cgroup_cpu_quota": quota, "cpu_model": model,
+            "C1": {"value": round(r1 / d2 / 1e6, 3), "unit": "Mrays/s", "cores": threads,
+                   "single_thread": round(int(s1b[0] + s1b[1]) / d3 / 1e6, 3),
+                   "sample": f"{n1} C1 frame(s) 512x512 primary only"}}
 
 
-def measure_config(name: str, steps: int, warmup: int, schedule: int) -> dict:
-    """Single-GPU frame rate of another BASELINE config (reported under "extra", not the headline)."""
-    spec = scenes.config(name)
+def measure_raster(be, spec, steps: int, warmup: int) -> dict:
+    """Raster fallback (rt_raster_draw: the reference's scrapped raster pipeline) on one GPU."""
+    from realtimeraytracing_gradproject_amd import scenes
     W, H = spec.width, spec.height
-    with rt.Context(torch.cuda.current_device()) as ctx:
-        scenes.upload(ctx, spec)
-        ctx.set_schedule(schedule)
-        stream = torch.cuda.Stream()
-        out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
-        ctx.set_stats(True)
-        ctx.stats_reset()
-        ctx.dispatch(W, H, out, None, stream=stream.cuda_stream)
-        torch.cuda.synchronize()
-        st = ctx.stats()
-        ctx.set_stats(False)
-        for _ in range(warmup):
-            ctx.dispatch(W, H, out, None, stream=stream.cuda_stream)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        t0 = time.perf_counter()
-        e0.record(stream)
-        for _ in range(steps):
-            ctx.dispatch(W, H, out, None, stream=stream.cuda_stream)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        wall = time.perf_counter() - t0
-        ms = e0.elapsed_time(e1) / steps
-    rays = st["primary_rays"] + st["shadow_rays"]
-    return {"config": name, "Mrays_s": round(rays * steps / wall / 1e6, 1), "frame_ms": round(wall / steps * 1e3, 4),
-            "kernel_ms": round(ms, 4), "rays_per_frame": int(rays), "resolution": f"{W}x{H}", "spp": spec.spp,
-            "aabb_tests_per_ray": round(st["aabb_tests"] / max(rays, 1), 2),
-            "tri_tests_per_ray": round(st["tri_tests"] / max(rays, 1), 2)}
-
-
-def measure_raster(name: str, steps: int, warmup: int) -> dict:
-    """Raster fallback (rt_raster_draw: the reference's scrapped raster pipeline, model + plane with
-    instance 0's transform) on one GPU, reported under "extra"."""
-    spec = scenes.config(name)
-    W, H = spec.width, spec.height
-    with rt.Context(torch.cuda.current_device()) as ctx:
+    rt = be.rt
+    with rt.Context(be.local) as ctx:
         ids = scenes.upload(ctx, spec)
         stream = torch.cuda.Stream()
         out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
@@ -163,112 +459,73 @@ def measure_raster(name: str, steps: int, warmup: int) -> dict:
         wall = time.perf_counter() - t0
         ms = e0.elapsed_time(e1) / steps
     tris = sum(((v.shape[0] if i is None else len(i)) // 3) for v, i in spec.meshes)
-    return {"config": f"{name} raster", "frame_ms": round(wall / steps * 1e3, 4), "gpu_ms": round(ms, 4),
+    return {"config": f"{spec.name} raster", "frame_ms": round(wall / steps * 1e3, 4), "gpu_ms": round(ms, 4),
             "triangles": int(tris), "resolution": f"{W}x{H}"}
 
 
-def main():
-    a = parse()
+def workload(spec) -> str:
+    return (f"{spec.name}: {spec.model}.obj x{len(spec.instances) - 1} + plane, {len(spec.lights)} light(s), "
+            f"{spec.width}x{spec.height}, {spec.spp} spp, shade {['ref', 'lambert_shadow', 'primary'][spec.mode]}")
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn(a, argv)
+    if world > 1 and a.gpus != world:
+        a.gpus = world
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        a.gpus = world if world > 1 else a.gpus
     distributed = world > 1
-    strips = distributed and a.assemble  # one frame split over ranks + RCCL gather
-    torch.cuda.set_device(local)
+    strips = distributed and a.mode in ("auto", "strips")
+
+    from realtimeraytracing_gradproject_amd import scenes
+    be = make_backend(local)
     if distributed:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        be.init_pg()
 
-    spec = scenes.config(a.config)
-    W, H = spec.width, spec.height
-    ctx = rt.Context(local)
-    scenes.upload(ctx, spec)
-    ctx.set_schedule(rt.RT_SCHED_LANE if a.schedule == "lane" else rt.RT_SCHED_PACKET)
-    binfo = [ctx.blas_info(b) for b in range(len(spec.meshes))]
-    tinfo = ctx.tlas_info()
+    def spec_of(name):
+        s = scenes.config(name)
+        if a.size:
+            w, h = (int(v) for v in a.size.lower().split("x"))
+            s = s.with_size(w, h)
+        return s
 
-    rows = D.rank_rows(H, world, rank) if strips else None
-    nrows = H if rows is None else len(rows)
-    rows_per_rank = D.padded_rows(H, world) if strips else H
-    stream = torch.cuda.Stream()
-    sp = stream.cuda_stream
-    local8 = torch.zeros((rows_per_rank, W, 4), dtype=torch.uint8, device="cuda")
-    gathered = torch.zeros((world, rows_per_rank, W, 4), dtype=torch.uint8, device="cuda") if strips and rank == 0 else None
-    frame = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") if strips and rank == 0 else None
+    spec = spec_of(a.config)
+    r = run_config(be, spec, world, rank, a.steps, a.warmup, a.settle_ms, strips, not a.no_pipeline, a.schedule,
+                   a.save_image)
 
-    def step():
-        ctx.dispatch(W, H, local8, None, rows=rows, stream=sp)
-        if strips:
-            with torch.cuda.stream(stream):
-                D.gather_strips(local8, world, rank, gathered)
-                if rank == 0:
-                    ctx.assemble_strips(W, H, world, STRIP_ROWS, gathered, frame, stream=sp)
-
-    # untimed counter pass: rays, box and triangle tests of this rank's share of the frame
-    ctx.set_stats(True)
-    ctx.stats_reset()
-    ctx.dispatch(W, H, local8, None, rows=rows, stream=sp)
-    torch.cuda.synchronize()
-    st = ctx.stats()
-    ctx.set_stats(False)
-    rays_local = st["primary_rays"] + st["shadow_rays"]
-    counts = torch.tensor([rays_local, st["primary_rays"], st["shadow_rays"]], dtype=torch.float64, device="cuda")
-    if distributed:
-        dist.all_reduce(counts)
-    rays_step = int(counts[0].item())  # frames mode: N frames; strips mode: one frame
-
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-
-    # one HIP event pair on the launch stream brackets the timed region: per-launch events would
-    # put a timestamp (and its wait-for-idle) between back-to-back frames
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    e0.record(stream)
-    for k in range(a.steps):
-        ctx.dispatch(W, H, local8, None, rows=rows, stream=sp)
-        if strips:
-            with torch.cuda.stream(stream):
-                D.gather_strips(local8, world, rank, gathered)
-                if rank == 0:
-                    ctx.assemble_strips(W, H, world, STRIP_ROWS, gathered, frame, stream=sp)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    # average launch duration over the timed region (strips mode: frame + gather + assembly)
-    kernel_ms = e0.elapsed_time(e1) / a.steps
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if distributed:
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    tmax = float(tmax.item())
-
-    if a.save_image and rank == 0:
-        img = (frame if strips else local8[:H]).cpu().numpy()
-        np.save(a.save_image, img)
+    extra = []
+    names = a.extra if a.extra is not None else ("C4,C5" if distributed else "C1,C2F,C3,C4,C5,REF")
+    for name in [n for n in names.split(",") if n]:
+        es = spec_of(name)
+        # few frames: C5 is ~8 ms per frame on one GPU
+        n_steps = max(3, a.steps // (20 if es.spp > 1 else 4))
+        x = run_config(be, es, world, rank, n_steps, 2, 0.0, strips, not a.no_pipeline, a.schedule)
+        if rank == 0:
+            st = x["stats"]
+            rays = max(x["rays_step"], 1)
+            extra.append({"config": name, "Mrays_s": round(x["rays_step"] * n_steps / x["tmax"] / 1e6, 1),
+                          "frame_ms": round(x["tmax"] / n_steps * 1e3, 4), "kernel_ms": round(x["kernel_ms"], 4),
+                          "rays_per_step": x["rays_step"], "resolution": f"{es.width}x{es.height}", "spp": es.spp,
+                          "n_gpus": world, "parallelism": f"strips{world}+gather" if strips else f"frames{world}",
+                          "aabb_tests_per_ray_rank0": round(st["aabb_tests"] / rays, 2) if not distributed else None,
+                          "node_fetches": int(st["node_fetches"]), "tri_fetches": int(st["tri_fetches"])})
+    if not distributed and (a.extra is None) and isinstance(be, HipBackend):
+        extra.append(be.raster(scenes.config("REF"), max(5, a.steps // 4), 2))
 
     if rank == 0:
-        value = rays_step * a.steps / tmax / 1e6
-        bytes_launch = (BYTES_PER_AABB_TEST * st["aabb_tests"] + BYTES_PER_TRI_TEST * st["tri_tests"]
-                        + BYTES_PER_PIXEL * W * nrows)
-        achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
-        traffic = load_traffic(a.config) if not strips else None
+        W, H = spec.width, spec.height
+        value = r["rays_step"] * a.steps / r["tmax"] / 1e6
+        st = r["stats"]
         cpu = None
         if not distributed and not a.no_cpu_baseline:
             cpu = cpu_baseline(spec, a.cpu_seconds)
-        extra = []
-        if not distributed and a.extra:
-            sched = rt.RT_SCHED_LANE if a.schedule == "lane" else rt.RT_SCHED_PACKET
-            for name in a.extra.split(","):
-                extra.append(measure_config(name, max(5, a.steps // 2), 2, sched))
-            extra.append(measure_raster("REF", max(5, a.steps // 2), 2))
+        rf = roofline(spec.name, st, W * r["rows_local"], r["kernel_ms"], a.schedule)
+        if distributed:
+            rf["note"] = "rank 0's strip render alone, timed back to back after the timed region"
         out = {
             "metric": "Mrays/sec (primary+shadow) at 1080p",
             "value": round(value, 2),
@@ -276,36 +533,30 @@ def main():
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": round(tmax / a.steps * 1e3, 4),
+            "ms_per_step": round(r["tmax"] / a.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "strong" if strips else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic camera/lights of BASELINE config; meshes teapot.obj/rabbit.obj from the reference",
-            "config": {"workload": f"{spec.name}: {spec.model}.obj x{len(spec.instances) - 1} + plane, "
-                                   f"{len(spec.lights)} light(s), {W}x{H}, {spec.spp} spp, shade "
-                                   f"{['ref', 'lambert_shadow', 'primary'][spec.mode]}",
-                       "rays_per_step": rays_step,
-                       "rays_per_frame": rays_step if strips else int(rays_local),
-                       "primary_rays": int(counts[1].item()), "shadow_rays": int(counts[2].item()), "parallelism": (f"strips{world}+gather" if strips else f"frames{world}"),
-                       "schedule": a.schedule},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "k_trace_frame" if a.schedule == "lane" else "k_trace_frame_packet", "kernel_ms": round(kernel_ms, 4),
-                         "bytes_per_launch": int(bytes_launch),
-                         "aabb_tests": int(st["aabb_tests"]), "tri_tests": int(st["tri_tests"]),
-                         # the BVH (~1 MB) is L2-resident: algorithmic bytes are served by L2/L1, so
-                         # frac vs HBM can exceed 1; the L2 roof (MI355X_MICROARCH.md) is the cache bound
-                         "l2_peak": L2_PEAK_GBS, "l2_frac": round(achieved / L2_PEAK_GBS, 4)},
+            "config": {"workload": workload(spec), "rays_per_step": r["rays_step"],
+                       "primary_rays": r["primary"], "shadow_rays": r["shadow"],
+                       "parallelism": (f"strips{world}+gather" + ("" if a.no_pipeline else " (pipelined)")) if strips
+                       else f"frames{world}",
+                       "rccl_world_size": world if distributed else None, "schedule": a.schedule,
+                       "settle_ms": a.settle_ms},
+            "roofline": rf,
             "cpu_baseline": cpu,
-            "build_ms": {"blas": [round(b.build_ms, 3) for b in binfo], "tlas": round(tinfo.build_ms, 3)},
+            "build_ms": {"blas": r["build"][0], "tlas": r["build"][1]},
             "extra": extra,
         }
         print(json.dumps(out), flush=True)
-    ctx.close()
+    be.close()
     if distributed:
+        dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -109,7 +109,13 @@ enum {
   RT_STAT_PIXELS = 6,
   RT_STAT_DISPATCHES = 7,
   RT_STAT_REFLECTION_RAYS = 8, /* RT_SHADE_REF with reflectivity != 0 (Hit.hlsl:176-203) */
-  RT_STAT_COUNT = 9
+  /* Fetches, the roofline's byte counts: in the packet schedule once per WAVE per visit (the node,
+   * triangle or instance record is loaded once into SGPRs for the whole packet), in the per-lane
+   * schedule once per lane per visit. */
+  RT_STAT_NODE_FETCHES = 9,     /* 128-B BVH4 node records */
+  RT_STAT_TRI_FETCHES = 10,     /* 48-B triangle records */
+  RT_STAT_INSTANCE_FETCHES = 11, /* instance-record loads on a TLAS -> BLAS hand-off */
+  RT_STAT_COUNT = 12
 };
 
 /* ------------------------------------------------------------------------------------------ */

@@ -237,7 +237,7 @@ class Scene:
         nrows = H if rows is None else len(rows)
         rgba8 = np.zeros((nrows, W, 4), np.uint8)
         rgba32 = np.zeros((nrows, W, 4), np.float32) if want_float else None
-        stats = np.zeros(9, np.uint64)
+        stats = np.zeros(12, np.uint64)
         rp = None
         if rows is not None:
             r = np.ascontiguousarray(rows, dtype=np.uint32)
@@ -258,7 +258,7 @@ class Scene:
         n = r.shape[0]
         hits = np.zeros((n, 4), np.uint32)
         uv = np.zeros((n, 2), np.float32)
-        stats = np.zeros(9, np.uint64)
+        stats = np.zeros(12, np.uint64)
         flags = (0x04 if any_hit else 0) | (0x10 if cull_back else 0) | (0x20 if cull_front else 0)  # D3D12_RAY_FLAG
         if lib.oracle_trace_rays(self._h, r.ctypes.data_as(_P), n, flags, hits.ctypes.data_as(_P),
                               uv.ctypes.data_as(_P), 1 if brute_force else 0, stats.ctypes.data_as(_P)):

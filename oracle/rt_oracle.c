@@ -758,7 +758,9 @@ int oracle_export_tlas(const oracle_scene* s, void* nodes) {
 /* ---------------------------------------------------------------------------------------- */
 /* traversal: DXR TraceRay semantics (closest hit / any hit), Common.hlsl:44-82               */
 /* ---------------------------------------------------------------------------------------- */
-typedef struct { uint64_t v[9]; } ostats;
+/* v[0..8] = RT_STAT_* 0..8; v[9..11] record fetches (RT_STAT_NODE/TRI/INSTANCE_FETCHES): per ray in
+ * otrace, once per emulated wave in opacket */
+typedef struct { uint64_t v[12]; } ostats;
 typedef struct { float t, u, v; uint32_t inst, prim; } ohit;
 
 static inline float sinv(float d) { return fabsf(d) > 1e-20f ? 1.0f / d : (d < 0.0f ? -1e20f : 1e20f); }
@@ -831,6 +833,7 @@ static int otrace(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax,
       float tn[4];
       int32_t r[4] = {nd->child[0], nd->child[1], nd->child[2], nd->child[3]};
       oslab4(nd, rinvd, rno, tmin, h->t, tn);
+      st->v[9]++;
       for (int k = 0; k < 4; ++k) st->v[2] += r[k] != O_EMPTY;
       osort4(tn, r);
       if (tn[0] != INFINITY) {
@@ -844,6 +847,7 @@ static int otrace(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax,
       cur = (uint32_t)(~ref);
       const oinst* ir = &s->inst[cur];
       st->v[4]++;
+      st->v[11]++;
       if (sp < cap) {
         stack[sp++] = SENT;
         ro = ipoint(ir, o);
@@ -861,6 +865,7 @@ static int otrace(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax,
       const otri* tr = tris + (~ref);
       float t, u, v;
       st->v[3]++;
+      st->v[10]++;
       if (omt(ro, rd, tr, cull ? (float)cull * s->inst[cur].face : 0.0f, &t, &u, &v) && t >= tmin && better(t, cur, tr->prim, h)) {
         h->t = t; h->u = u; h->v = v; h->inst = cur; h->prim = tr->prim;
         found = 1;
@@ -903,6 +908,7 @@ static int opk_node(const o4node* nd, const opkray* ry, float tmin, ohit* h, int
                     int cap, int* next, ostats* st) {
   uint64_t hm[4] = {0, 0, 0, 0};
   uint32_t vkey[OPK][4];
+  st->v[9]++; /* one node fetch per wave */
   for (int l = 0; l < OPK; ++l) {
     for (int k = 0; k < 4; ++k) {
       float tlx = fmaf(nd->lox[k], ry->invd[l].x, ry->no[l].x), thx = fmaf(nd->hix[k], ry->invd[l].x, ry->no[l].x);
@@ -927,6 +933,7 @@ static int opk_node(const o4node* nd, const opkray* ry, float tmin, ohit* h, int
     for (int k = 0; k < 4; ++k) {
       if (!((tl >> k) & 1u)) continue;
       const otri* tr = leaves + (~nd->child[k]);
+      st->v[10]++; /* one triangle fetch per wave */
       for (int l = 0; l < OPK; ++l) {
         if (!live[l]) continue;
         float t, u, v;
@@ -1004,6 +1011,7 @@ static void opacket(const oracle_scene* s, const vec3* o, const vec3* d, float t
       const uint32_t cur = (uint32_t)(~ref);
       const oinst* ir = &s->inst[cur];
       const oblas* bl = &s->blas[ir->blas];
+      st->v[11]++; /* one instance-record fetch per wave */
       for (int l = 0; l < OPK; ++l) {
         if (live[l]) st->v[4]++;
         b.o[l] = ipoint(ir, o[l]);
@@ -1564,7 +1572,8 @@ int oracle_render(const oracle_scene* s, const float cb[64], const oracle_light*
     for (int t = 0; t < nthreads; ++t)
       for (int q = 0; q < 6; ++q) stats[q] += jobs[t].st.v[q];
   if (stats)
-    for (int t = 0; t < nthreads; ++t) stats[8] += jobs[t].st.v[8];
+    for (int t = 0; t < nthreads; ++t)
+      for (int q = 8; q < 12; ++q) stats[q] += jobs[t].st.v[q];
   if (stats) { stats[6] += (uint64_t)W * nrows; stats[7] += 1; }
   return 0;
 }
@@ -1591,6 +1600,9 @@ int oracle_trace_rays(const oracle_scene* s, const float* rays, uint32_t n, uint
     hits[i * 4 + 3] = f ? 1u : 0u;
     if (uv) { uv[i * 2] = f ? h.u : 0.0f; uv[i * 2 + 1] = f ? h.v : 0.0f; }
   }
-  if (stats) for (int q = 0; q < 6; ++q) stats[q] += st.v[q];
+  if (stats) {
+    for (int q = 0; q < 6; ++q) stats[q] += st.v[q];
+    for (int q = 9; q < 12; ++q) stats[q] += st.v[q];
+  }
   return 0;
 }

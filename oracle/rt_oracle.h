@@ -57,7 +57,7 @@ int oracle_tlas_info(const oracle_scene* s, uint32_t out[4]);
 int oracle_export_blas(const oracle_scene* s, int blas, void* nodes, void* tris);
 int oracle_export_tlas(const oracle_scene* s, void* nodes);
 
-/* render W x H (rows NULL = all). stats[9] accumulates (same slots as RT_STAT_*), may be NULL.
+/* render W x H (rows NULL = all). stats[12] accumulates (same slots as RT_STAT_*), may be NULL.
  * brute_force != 0: closest hit by testing every triangle of every instance (no BVH).
  * schedule: RT_SCHED_PACKET (0: 8 x 8 wave packets, as the device) or RT_SCHED_LANE (1: one
  * independent traversal per pixel). The image is the same; the traversal counters follow it. */

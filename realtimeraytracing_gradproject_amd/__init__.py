@@ -32,7 +32,8 @@ RT_SCHED_PACKET, RT_SCHED_LANE = 0, 1
 RT_RAY_FLAG_ACCEPT_FIRST_HIT_AND_END_SEARCH, RT_RAY_FLAG_CULL_BACK_FACING_TRIANGLES = 0x04, 0x10
 RT_RAY_FLAG_CULL_FRONT_FACING_TRIANGLES = 0x20
 STAT_NAMES = ("primary_rays", "shadow_rays", "aabb_tests", "tri_tests", "instance_entries",
-              "stack_overflows", "pixels", "dispatches", "reflection_rays")
+              "stack_overflows", "pixels", "dispatches", "reflection_rays", "node_fetches", "tri_fetches",
+              "instance_fetches")
 
 
 class RtError(RuntimeError):

@@ -90,6 +90,26 @@ rt_status hip_fail(rt_ctx* c, hipError_t e, const char* what) {
     if (e_ != hipSuccess) return hip_fail(ctx, e_, what); \
   } while (0)
 
+// Waits for every launch that may still read the context's device buffers. Dispatches run on
+// caller streams (rt_dispatch_rays / rt_trace_rays / rt_raster_draw take any hipStream_t), so a
+// sync of the context's own stream is not enough before an in-place overwrite or a free: the
+// reference waits on its fence the same way before it rebuilds (D3D12HelloTriangle.cpp:1482-1568).
+// Only the rare mutating calls pay this (builds, rebuilds, a changed row list, buffer growth).
+hipError_t quiesce(rt_ctx* c) {
+  (void)hipSetDevice(c->device);
+  return hipDeviceSynchronize();
+}
+
+// Runs f on scope exit: frees a build's device scratch on every return path.
+template <class F>
+struct ScopeExit {
+  F f;
+  explicit ScopeExit(F fn) : f(fn) {}
+  ~ScopeExit() { f(); }
+  ScopeExit(const ScopeExit&) = delete;
+  ScopeExit& operator=(const ScopeExit&) = delete;
+};
+
 // inverse of a 3x3 (row-major) in double, rounded to float; returns false if singular.
 bool inverse3(const double m[9], double inv[9]) {
   double c00 = m[4] * m[8] - m[5] * m[7];
@@ -179,6 +199,12 @@ rt_status upload_blas(rt_ctx* c, DeviceBlas& b, const void* vtx, uint32_t vcount
   rt::TriRec* unsorted = nullptr;
   float* primbox = nullptr;
   uint32_t* sorted = nullptr;
+  auto free_fn = [&] {  // every return below (the caller releases b on failure)
+    if (unsorted) (void)hipFree(unsorted);
+    if (primbox) (void)hipFree(primbox);
+    if (sorted) (void)hipFree(sorted);
+  };
+  ScopeExit<decltype(free_fn)> scratch(free_fn);
   HIPCHK(c, hipMalloc(&b.nodes, (size_t)nn * sizeof(rt::Bvh4Node)), "hipMalloc(nodes)");
   HIPCHK(c, hipMalloc(&b.tris, (size_t)ntri * sizeof(rt::TriRec)), "hipMalloc(tris)");
   HIPCHK(c, hipMalloc(&unsorted, (size_t)ntri * sizeof(rt::TriRec)), "hipMalloc(scratch)");
@@ -191,9 +217,6 @@ rt_status upload_blas(rt_ctx* c, DeviceBlas& b, const void* vtx, uint32_t vcount
     e = rt::lbvh_build(primbox, ntri, b.nodes, sorted, false, &nnodes4, &b.depth, &b.max_stack, b.bounds, &ms, s);
   if (e == hipSuccess) e = rt::blas_reorder(unsorted, sorted, ntri, b.tris, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
-  (void)hipFree(unsorted);
-  (void)hipFree(primbox);
-  (void)hipFree(sorted);
   if (e != hipSuccess) return hip_fail(c, e, "BLAS build");
   b.ntri = ntri;
   b.nnodes = nnodes4;
@@ -203,6 +226,7 @@ rt_status upload_blas(rt_ctx* c, DeviceBlas& b, const void* vtx, uint32_t vcount
 }
 
 hipStream_t pick_stream(rt_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
+
 
 }  // namespace
 
@@ -287,8 +311,8 @@ rt_status rt_blas_build(rt_ctx_t c, const void* vtx, uint32_t vcount, uint32_t s
 rt_status rt_blas_rebuild(rt_ctx_t c, rt_blas_t id, const void* vtx, uint32_t vcount, uint32_t stride,
                           const uint32_t* idx, uint32_t icount) {
   if (!c || id >= c->blas.size()) return fail(c, RT_E_INVALID, "rt_blas_rebuild: unknown BLAS");
-  (void)hipSetDevice(c->device);
-  (void)hipStreamSynchronize(c->stream);
+  // frames in flight on any stream shade from this BLAS's vertex / index arrays
+  HIPCHK(c, quiesce(c), "rt_blas_rebuild: wait for in-flight work");
   DeviceBlas b;
   rt_status st = upload_blas(c, b, vtx, vcount, stride, idx, icount);
   if (st != RT_OK) {
@@ -375,8 +399,13 @@ rt_status rt_tlas_build(rt_ctx_t c, const rt_instance* in, uint32_t n, int updat
     for (int k = 0; k < 6; ++k) bb[i * 6 + k] = b.bounds[k];
   }
   hipStream_t s = c->stream;
-  (void)hipStreamSynchronize(s);
+  // every buffer below is overwritten in place or freed: no frame on any stream may still read it
+  HIPCHK(c, quiesce(c), "rt_tlas_build: wait for in-flight work");
+  // until this build completes, the scene must not be traced (a failure below leaves it stale;
+  // rt_dispatch_rays / rt_trace_rays refuse a stale scene instead of walking half-built pools)
+  c->tlas_stale = true;
   if (!update_only || !c->inst) {
+    c->ninst = 0;  // an update needs a completed build of the same instance count
     if (c->tlas_nodes) (void)hipFree(c->tlas_nodes);
     if (c->inst) (void)hipFree(c->inst);
     if (c->tlas_sorted) (void)hipFree(c->tlas_sorted);
@@ -390,6 +419,11 @@ rt_status rt_tlas_build(rt_ctx_t c, const rt_instance* in, uint32_t n, int updat
   }
   float* d_bb = nullptr;
   float* d_box = nullptr;
+  auto free_fn = [&] {
+    if (d_bb) (void)hipFree(d_bb);
+    if (d_box) (void)hipFree(d_box);
+  };
+  ScopeExit<decltype(free_fn)> scratch(free_fn);
   HIPCHK(c, hipMalloc(&d_bb, bb.size() * 4), "hipMalloc(scratch)");
   HIPCHK(c, hipMalloc(&d_box, bb.size() * 4), "hipMalloc(scratch)");
   hipError_t e = hipMemcpyAsync(c->inst, recs.data(), recs.size() * sizeof(rt::InstanceRec), hipMemcpyHostToDevice, s);
@@ -402,8 +436,6 @@ rt_status rt_tlas_build(rt_ctx_t c, const rt_instance* in, uint32_t n, int updat
     e = rt::lbvh_build(d_box, n, c->tlas_nodes, c->tlas_sorted, true, &c->tlas_nodes_n, &c->tlas_depth, &c->tlas_max_stack,
                        c->tlas_bounds, &ms, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
-  (void)hipFree(d_bb);
-  (void)hipFree(d_box);
   if (e != hipSuccess) return hip_fail(c, e, "TLAS build");
   // scene pools (rebased copies; the per-BLAS arrays stay for export and rebuilds)
   if (pool_n > c->pool_nodes_cap) {
@@ -531,7 +563,7 @@ static rt_status ensure_overflow(rt_ctx* c, rt::SceneView& sv, size_t lanes, hip
   if (sv.stack_cap <= sv.lds_cap) return RT_OK;
   const size_t need = lanes * (size_t)(sv.stack_cap - sv.lds_cap);
   if (need > c->ovf_cap) {
-    (void)hipStreamSynchronize(s);
+    HIPCHK(c, quiesce(c), "overflow stack: wait for in-flight work");
     if (c->d_ovf) (void)hipFree(c->d_ovf);
     c->d_ovf = nullptr;
     c->ovf_cap = 0;
@@ -589,7 +621,7 @@ rt_status rt_raster_draw(rt_ctx_t c, const rt_blas_t* draws, uint32_t ndraws, co
   };
   rt_status st = RT_OK;
   if (c->raster_tile_cap < ntiles || c->raster_prim_cap < total) {
-    (void)hipStreamSynchronize(s);
+    HIPCHK(c, quiesce(c), "rt_raster_draw: wait for in-flight work");
     if (c->raster_tile_cap < ntiles) {
       if ((st = regrow((void**)&c->raster.tcount, ntiles * 4, "hipMalloc(raster tile counts)")) != RT_OK) return st;
       if ((st = regrow((void**)&c->raster.toffs, (ntiles + 1) * 4, "hipMalloc(raster tile offsets)")) != RT_OK) return st;
@@ -615,6 +647,7 @@ rt_status rt_raster_draw(rt_ctx_t c, const rt_blas_t* draws, uint32_t ndraws, co
   HIPCHK(c, hipMemcpyAsync(&nbins, c->raster.toffs + ntiles, 4, hipMemcpyDeviceToHost, s), "raster bin count");
   HIPCHK(c, hipStreamSynchronize(s), "raster bin count");
   if (c->raster_bin_cap < nbins) {
+    HIPCHK(c, quiesce(c), "rt_raster_draw: wait for in-flight work");
     const size_t cap = (size_t)nbins + nbins / 2;
     if ((st = regrow((void**)&c->raster.bins, cap * 4, "hipMalloc(raster bins)")) != RT_OK) return st;
     c->raster_bin_cap = cap;
@@ -628,7 +661,8 @@ rt_status rt_dispatch_rays(rt_ctx_t c, uint32_t W, uint32_t H, const uint32_t* r
                            void* rgba8, float* rgba32f, void* stream) {
   if (!c) return RT_E_INVALID;
   if (!c->inst) return fail(c, RT_E_INVALID, "rt_dispatch_rays: no TLAS built");
-  if (c->tlas_stale) return fail(c, RT_E_INVALID, "rt_dispatch_rays: BLAS rebuilt since the last rt_tlas_build");
+  if (c->tlas_stale)
+    return fail(c, RT_E_INVALID, "rt_dispatch_rays: scene stale (BLAS rebuilt, or the last rt_tlas_build failed)");
   if (!c->have_camera || !c->have_shading) return fail(c, RT_E_INVALID, "rt_dispatch_rays: camera/shading not set");
   if (W == 0 || H == 0 || !rgba8) return fail(c, RT_E_INVALID, "rt_dispatch_rays: bad size or output");
   if (!rows) nrows = H;
@@ -641,8 +675,9 @@ rt_status rt_dispatch_rays(rt_ctx_t c, uint32_t W, uint32_t H, const uint32_t* r
       if (rows[r] >= H) return fail(c, RT_E_INVALID, "rt_dispatch_rays: row index out of range");
     bool same = c->rows_host.size() == nrows && std::memcmp(c->rows_host.data(), rows, (size_t)nrows * 4) == 0;
     if (!same) {
+      // the cached list may still be read by a frame in flight on another stream
+      HIPCHK(c, quiesce(c), "rt_dispatch_rays: wait for in-flight work");
       if (c->rows_cap < nrows) {
-        (void)hipStreamSynchronize(s);
         if (c->d_rows) (void)hipFree(c->d_rows);
         c->d_rows = nullptr;
         HIPCHK(c, hipMalloc(&c->d_rows, (size_t)nrows * 4), "hipMalloc(rows)");
@@ -687,7 +722,8 @@ rt_status rt_trace_rays(rt_ctx_t c, const float* rays, uint32_t n, uint32_t ray_
   const bool cull_front = (ray_flags & RT_RAY_FLAG_CULL_FRONT_FACING_TRIANGLES) != 0;
   if (cull_back && cull_front) return fail(c, RT_E_INVALID, "rt_trace_rays: both cull flags set");
   if (!c->inst) return fail(c, RT_E_INVALID, "rt_trace_rays: no TLAS built");
-  if (c->tlas_stale) return fail(c, RT_E_INVALID, "rt_trace_rays: BLAS rebuilt since the last rt_tlas_build");
+  if (c->tlas_stale)
+    return fail(c, RT_E_INVALID, "rt_trace_rays: scene stale (BLAS rebuilt, or the last rt_tlas_build failed)");
   (void)hipSetDevice(c->device);
   rt::SceneView sv = scene_view(c);
   sv.cull_sense = cull_front ? -1.0f : 1.0f;
@@ -736,7 +772,7 @@ rt_status rt_stats(rt_ctx_t c, uint64_t out[RT_STAT_COUNT]) {
   for (int k = 0; k < 6; ++k) out[k] = h[k];
   out[RT_STAT_PIXELS] = c->pixels;
   out[RT_STAT_DISPATCHES] = c->dispatches;
-  out[RT_STAT_REFLECTION_RAYS] = h[RT_STAT_REFLECTION_RAYS];
+  for (int k = RT_STAT_REFLECTION_RAYS; k < RT_STAT_COUNT; ++k) out[k] = h[k];
   return RT_OK;
 }
 

@@ -32,6 +32,9 @@ constexpr float kPi = 3.14159265359f;  // Common.hlsl:1
 
 struct Counters {
   uint32_t primary = 0, shadow = 0, aabb = 0, tri = 0, inst = 0, overflow = 0, refl = 0;
+  // record fetches (RT_STAT_*_FETCHES): per lane in the per-lane schedule; in the packet schedule
+  // wave-uniform (every lane holds the wave's count, flushed once per wave)
+  uint32_t nfetch = 0, tfetch = 0, ifetch = 0;
 };
 
 struct HitRec {
@@ -148,6 +151,7 @@ __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, H
       int32_t r[4] = {ch.x, ch.y, ch.z, ch.w};
       float tn[4];
       slab4_octant(nx, fx, ny, fy, nz, fz, r, rinvd, rnoinv, tmin, hit.t, tn);
+      if (STATS) ++cnt.nfetch;
       if (STATS)
         cnt.aabb += (uint32_t)(r[0] != kEmptyChild) + (uint32_t)(r[1] != kEmptyChild) +
                     (uint32_t)(r[2] != kEmptyChild) + (uint32_t)(r[3] != kEmptyChild);
@@ -194,6 +198,7 @@ __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, H
       cur = (uint32_t)(~ref);
       const RT_GLOBAL InstanceRec* ir = gp(sc.inst) + cur;
       if (STATS) ++cnt.inst;
+      if (STATS) ++cnt.ifetch;
       if (sp < cap) {
         stk.put(sp, kStackSentinel);
         ++sp;
@@ -215,6 +220,7 @@ __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, H
       const uint32_t toff = (uint32_t)(~ref) * (uint32_t)sizeof(TriRec);
       const f4v a = ldf4(pt, toff), b = ldf4(pt, toff + 16u), c = ldf4(pt, toff + 32u);
       if (STATS) ++cnt.tri;
+      if (STATS) ++cnt.tfetch;
       float t, u, v;
       if (moller_trumbore(ro, rd, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), v3(c.x, c.y, c.z), face, t, u, v) &&
           t >= tmin) {
@@ -392,6 +398,7 @@ __device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref
   const f4v tc = *(const RT_CONST f4v*)(tq + 32);
   const f4v ta = {tab[0], tab[1], tab[2], tab[3]}, tb = {tab[4], tab[5], tab[6], tab[7]};
   const uint32_t prim = __float_as_uint(ta.w);
+  if (STATS) ++cnt.tfetch;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     if (STATS && ray_live(hit[r])) ++cnt.tri;
@@ -481,6 +488,7 @@ __device__ __forceinline__ bool packet_tlas_node(const RT_CONST char* pool, int 
   const RT_CONST char* nb = pool + ((uint32_t)ref << 7);
   const i8v ch = *(const RT_CONST i8v*)(nb + 96);  // child[4], count, first_inner, inner_mask, pad
   const int cref[4] = {ch[0], ch[1], ch[2], ch[3]};
+  if (STATS) ++cnt.nfetch;
   uint64_t hm[R][4];
   uint32_t vkey[R][4];
   const f4v planes[6] = {cld4(nb), cld4(nb + 16), cld4(nb + 32), cld4(nb + 48), cld4(nb + 64), cld4(nb + 80)};
@@ -545,6 +553,7 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
   while (true) {
     const RT_CONST char* nb = pool + ((uint32_t)bref << 7);
     const i8v ch = *(const RT_CONST i8v*)(nb + 96);  // child[4], count, first_inner, inner_mask, entry_base
+    if (STATS) ++cnt.nfetch;
     uint64_t hm[R][4];
     uint32_t vkey[R][4];
     f4v planes[6];
@@ -665,6 +674,7 @@ __device__ __forceinline__ void packet_walk(const SceneView& sc, const V3* o, co
       const RT_CONST f4v* mq = (const RT_CONST f4v*)ir.w2o;
       const f4v m0 = mq[0], m1 = mq[1], m2 = mq[2];
       const float m[12] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w, m2.x, m2.y, m2.z, m2.w};
+      if (STATS) ++cnt.ifetch;
       PacketRay<R> b;
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -1103,12 +1113,15 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
     }
 }
 
+// WAVE_FETCH: the fetch counters are wave-uniform (packet schedule) and count once per wave.
+template <bool WAVE_FETCH>
 __device__ __forceinline__ void flush_stats(const Counters& c, unsigned long long* stats) {
-  uint32_t v[7] = {c.primary, c.shadow, c.aabb, c.tri, c.inst, c.overflow, c.refl};
-  const int slot[7] = {0, 1, 2, 3, 4, 5, 8};
-  for (int k = 0; k < 7; ++k) {
+  uint32_t v[10] = {c.primary, c.shadow, c.aabb, c.tri, c.inst, c.overflow, c.refl, c.nfetch, c.tfetch, c.ifetch};
+  const int slot[10] = {0, 1, 2, 3, 4, 5, 8, 9, 10, 11};
+  for (int k = 0; k < 10; ++k) {
     unsigned long long x = v[k];
-    for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, 64);
+    if (!WAVE_FETCH || k < 7)
+      for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, 64);
     if ((threadIdx.x & 63) == 0 && x) atomicAdd(stats + slot[k], x);
   }
 }
@@ -1149,7 +1162,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void k_trace_frame(SceneView 
     rgba8[o] = unorm8(acc.x) | (unorm8(acc.y) << 8) | (unorm8(acc.z) << 16) | (255u << 24);
     if (rgba32f) rgba32f[o] = make_float4(acc.x, acc.y, acc.z, 1.0f);
   }
-  if (STATS) flush_stats(cnt, stats);
+  if (STATS) flush_stats<false>(cnt, stats);
 }
 
 // Wave-packet frame kernel. A wave covers an 8 x 8R tile (ray r of lane l: column l % 8, row
@@ -1221,7 +1234,7 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp,
       if (rgba32f) rgba32f[o] = make_float4(a.x, a.y, a.z, 1.0f);
     }
   }
-  if (STATS) flush_stats(cnt, stats);
+  if (STATS) flush_stats<true>(cnt, stats);
 }
 
 template <bool ANY_HIT, bool STATS, bool CULL>
@@ -1242,7 +1255,7 @@ __global__ __launch_bounds__(kBlock) void k_trace_rays(SceneView sc, const float
                          f ? h.prim : 0xffffffffu, f ? 1u : 0u);
     if (uv) uv[i] = make_float2(f ? h.u : 0.0f, f ? h.v : 0.0f);
   }
-  if (STATS) flush_stats(cnt, stats);
+  if (STATS) flush_stats<false>(cnt, stats);
 }
 
 __global__ void k_assemble(uint32_t W, uint32_t H, uint32_t nranks, uint32_t strip_rows,

@@ -169,6 +169,8 @@ def test_counters_match_oracle(name, sched):
     keys = ["primary_rays", "shadow_rays", "aabb_tests", "tri_tests", "instance_entries", "stack_overflows"]
     assert [s[k] for k in keys] == [int(x) for x in ost[:6]]
     assert s["reflection_rays"] == int(ost[8])
+    # record fetches (the roofline's byte counts): per wave in packets, per lane per ray
+    assert [s[k] for k in ["node_fetches", "tri_fetches", "instance_fetches"]] == [int(x) for x in ost[9:12]]
     assert s["stack_overflows"] == 0
     c.close()
 
@@ -331,6 +333,55 @@ def test_blas_rebuild_and_tlas_update():
     assert_images_equal(g8, g32, o8, o32, "after TLAS update")
     with pytest.raises(rt.RtError):
         c.tlas_build(inst[:3], update_only=True)  # count change is not an update
+    c.close()
+
+
+def test_tlas_update_waits_for_frame_in_flight():
+    """rt_tlas_build(update_only) overwrites the instance records and scene pools in
+    place. A frame dispatched on a caller (torch) stream just before must still render the OLD
+    scene: the build waits for in-flight work on every stream (quiesce), as the reference waits on
+    its fence before rebuilding (D3D12HelloTriangle.cpp:1482-1568)."""
+    spec = scenes.config("C4")  # 1080p, 65 instances: ~0.4 ms in flight
+    c = fresh_ctx()
+    scenes.upload(c, spec)
+    ref8, _ = gpu_render(c, spec)
+    moved = [(m, scenes.translation(float(x[3]) + 0.7, float(x[7]), float(x[11]) - 0.4) if hg == rt.RT_HITGROUP_MODEL
+              else x, iid, hg) for (m, x, iid, hg) in spec.instances]
+    s = torch.cuda.Stream()
+    outs = []
+    for _ in range(3):
+        out = torch.empty((spec.height, spec.width, 4), dtype=torch.uint8, device="cuda")
+        c.dispatch(spec.width, spec.height, out, None, stream=s.cuda_stream)
+        outs.append(out)
+    c.tlas_build(moved, update_only=True)  # no synchronisation by the caller in between
+    after = torch.empty((spec.height, spec.width, 4), dtype=torch.uint8, device="cuda")
+    c.dispatch(spec.width, spec.height, after, None, stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    for k, out in enumerate(outs):
+        assert np.array_equal(out.cpu().numpy(), ref8), f"frame {k} in flight saw the update"
+    spec2 = scenes.SceneSpec(**{**spec.__dict__})
+    spec2.instances = moved
+    c2 = fresh_ctx()
+    scenes.upload(c2, spec2)
+    want8, _ = gpu_render(c2, spec2)
+    assert np.array_equal(after.cpu().numpy(), want8)
+    assert not np.array_equal(want8, ref8)
+    c.close()
+    c2.close()
+
+
+def test_rejected_tlas_build_keeps_scene():
+    """A TLAS build rejected by validation touches nothing: the previous scene still renders. (A
+    build that fails after validation marks the scene stale until a build succeeds: rt_api.cpp.)"""
+    spec = scenes.config("C2").with_size(96, 54)
+    c, o = load_both(spec)
+    bad = list(spec.instances)
+    bad[0] = (0, np.zeros(12, np.float32), 0, rt.RT_HITGROUP_MODEL)  # singular transform
+    with pytest.raises(rt.RtError):
+        c.tlas_build(bad)
+    good8, good32 = gpu_render(c, spec)  # validation failed before anything was touched
+    o8, o32, _ = o.render_spec(spec, nthreads=4)
+    assert_images_equal(good8, good32, o8, o32, "after rejected build")
     c.close()
 
 
