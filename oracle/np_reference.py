@@ -3,7 +3,10 @@
 Used to cross-check the C oracle (oracle/rt_oracle.c) where the reference itself cannot run
 (HLSL/DXR). It shares no code with either the oracle or the product: brute-force ray/triangle tests
 over every triangle of every instance (no BVH), shading formulas transcribed from the HLSL:
-  RayGen.hlsl:28-43, Common.hlsl:44-82, Hit.hlsl:67-241, Miss.hlsl:3-10, ShadowRay.hlsl:10-20.
+  RayGen.hlsl:28-43, Common.hlsl:44-82, Hit.hlsl:67-241, Miss.hlsl:3-10, ShadowRay.hlsl:10-20,
+including the ReflectRay chains of InstanceID 0 / 1 (Hit.hlsl:176-203, CastReflectionRay
+Common.hlsl:58-69) evaluated as HLSL nests them: color_k = lerp(s_k, color_{k+1}, r), innermost
+first, and the spp average (2x2 stratified samples).
 Evaluation is float64, so agreement with the float32 oracle is to a tolerance, and pixels whose
 primary ray grazes an edge can legitimately flip between triangles or between hit and miss.
 """
@@ -12,6 +15,7 @@ from __future__ import annotations
 import numpy as np
 
 PI = 3.14159265359
+MAX_REFLECT = 18  # reflection rays per camera ray: 20 TraceRay levels (D3D12HelloTriangle.cpp:954), SURVEY A.6-1
 
 
 def _norm(v):
@@ -43,58 +47,99 @@ class Scene:
             M = np.asarray(x, np.float64).reshape(3, 4)
             L, t = M[:, :3], M[:, 3]
             Li = np.linalg.inv(L)
-            self.inst.append(dict(v=v, tri=tri, w2o_L=Li, w2o_t=-Li @ t, nrm=Li.T, hg=hg))
+            # a mirroring transform flips the front face (DXR: clockwise seen from the ray origin)
+            self.inst.append(dict(v=v, tri=tri, w2o_L=Li, w2o_t=-Li @ t, nrm=Li.T, hg=hg, iid=iid,
+                                  face=-1.0 if np.linalg.det(L) < 0 else 1.0))
 
-    def intersect(self, O, D, tmin, tmax, any_hit=False):
+    CHUNK = 32  # triangles per culling box (consecutive primitive indices)
+
+    def _chunks(self, I):
+        """Per-instance culling boxes over runs of CHUNK consecutive triangles (a speed-up only: no
+        hierarchy, no shared code with the BVH builders); the last run is padded with det = 0
+        triangles that never hit."""
+        if "cp0" not in I:
+            C = self.CHUNK
+            p0 = I["v"][I["tri"][:, 0], :3]
+            e1 = I["v"][I["tri"][:, 1], :3] - p0
+            e2 = I["v"][I["tri"][:, 2], :3] - p0
+            n = p0.shape[0]
+            m = -(-n // C) * C
+            pad = lambda a: np.concatenate([a, np.zeros((m - n, 3))]) if m > n else a
+            I["cp0"], I["ce1"], I["ce2"] = pad(p0).reshape(-1, C, 3), pad(e1).reshape(-1, C, 3), pad(e2).reshape(-1, C, 3)
+            pts = np.stack([p0, p0 + e1, p0 + e2], 1)
+            pts = np.concatenate([pts, np.repeat(pts[-1:], m - n, 0)]) if m > n else pts
+            pts = pts.reshape(-1, C * 3, 3)
+            I["clo"], I["chi"] = pts.min(1) - 1e-4, pts.max(1) + 1e-4
+            I["ntri"] = n
+        return I
+
+    def intersect(self, O, D, tmin, tmax, any_hit=False, cull_back=False):
+        """Closest hit over every triangle of every instance: the lexicographic minimum of
+        (t, instance, primitive), as DXR's closest hit with the pinned tie rule."""
         n = O.shape[0]
         best_t = np.full(n, tmax, np.float64) if np.ndim(tmax) == 0 else tmax.astype(np.float64).copy()
         best_i = np.full(n, -1, np.int64)
         best_p = np.full(n, -1, np.int64)
         bu = np.zeros(n)
         bv = np.zeros(n)
+        C = self.CHUNK
         for k, I in enumerate(self.inst):
+            I = self._chunks(I)
             o_all = O @ I["w2o_L"].T + I["w2o_t"]
             d_all = D @ I["w2o_L"].T
-            p0 = I["v"][I["tri"][:, 0], :3]
-            e1 = I["v"][I["tri"][:, 1], :3] - p0
-            e2 = I["v"][I["tri"][:, 2], :3] - p0
-            # only rays whose segment meets the (slightly padded) object-space box: a pure speed-up
-            lo = np.min(I["v"][I["tri"].ravel(), :3], 0) - 1e-4
-            hi = np.max(I["v"][I["tri"].ravel(), :3], 0) + 1e-4
             with np.errstate(divide="ignore", invalid="ignore"):
-                ta, tb = (lo - o_all) / d_all, (hi - o_all) / d_all
-            tn = np.nanmax(np.minimum(ta, tb), axis=1)
-            tf = np.nanmin(np.maximum(ta, tb), axis=1)
-            rsel = np.where((tn <= tf) & (tf >= tmin) & (tn <= best_t))[0]
-            o, d = o_all[rsel], d_all[rsel]
-            for s in range(0, rsel.size, 256):
-                oo, dd = o[s:s + 256, None, :], d[s:s + 256, None, :]
-                pv = np.cross(dd, e2[None])
-                det = np.sum(e1[None] * pv, -1)
+                inv_d = 1.0 / d_all
+            # (ray, run) pairs whose segment meets the run's box
+            rows = []
+            for s0 in range(0, n, 2048):
+                o, iv = o_all[s0:s0 + 2048, None, :], inv_d[s0:s0 + 2048, None, :]
+                with np.errstate(divide="ignore", invalid="ignore"):
+                    ta, tb = (I["clo"][None] - o) * iv, (I["chi"][None] - o) * iv
+                tn = np.nanmax(np.minimum(ta, tb), axis=2)
+                tf = np.nanmin(np.maximum(ta, tb), axis=2)
+                r, c = np.nonzero((tn <= tf) & (tf >= tmin) & (tn <= best_t[s0:s0 + 2048, None]))
+                rows.append((r + s0, c))
+            ri = np.concatenate([a for a, _ in rows])
+            ci = np.concatenate([b for _, b in rows])
+            for q0 in range(0, ri.size, 4096):
+                rr, cc = ri[q0:q0 + 4096], ci[q0:q0 + 4096]
+                oo, dd = o_all[rr][:, None, :], d_all[rr][:, None, :]
+                p0, e1, e2 = I["cp0"][cc], I["ce1"][cc], I["ce2"][cc]
+                pv = np.cross(dd, e2)
+                det = np.sum(e1 * pv, -1)
                 with np.errstate(divide="ignore", invalid="ignore"):
                     inv = 1.0 / det
-                    sv = oo - p0[None]
+                    sv = oo - p0
                     u = np.sum(sv * pv, -1) * inv
-                    q = np.cross(sv, e1[None])
-                    v = np.sum(dd * q, -1) * inv
-                    t = np.sum(e2[None] * q, -1) * inv
+                    qv = np.cross(sv, e1)
+                    v = np.sum(dd * qv, -1) * inv
+                    t = np.sum(e2 * qv, -1) * inv
                 ok = (det != 0) & (u >= 0) & (u <= 1) & (v >= 0) & (u + v <= 1) & (t >= tmin)
+                if cull_back:  # RAY_FLAG_CULL_BACK_FACING_TRIANGLES: keep front faces only
+                    ok &= det * I["face"] > 0
                 t = np.where(ok, t, np.inf)
-                j = np.argmin(t, axis=1)  # lowest primitive index on ties
-                tj = t[np.arange(t.shape[0]), j]
-                sl = rsel[s:s + t.shape[0]]
-                better = tj < best_t[sl]
-                best_t[sl] = np.where(better, tj, best_t[sl])
-                best_i[sl] = np.where(better, k, best_i[sl])
-                best_p[sl] = np.where(better, j, best_p[sl])
-                bu[sl] = np.where(better, u[np.arange(t.shape[0]), j], bu[sl])
-                bv[sl] = np.where(better, v[np.arange(t.shape[0]), j], bv[sl])
+                j = np.argmin(t, axis=1)  # lowest primitive of the run on ties
+                a = np.arange(rr.size)
+                tj, pj = t[a, j], cc * C + j
+                # per ray: smallest t, then lowest primitive (runs are in primitive order)
+                order = np.lexsort((pj, tj, rr))
+                rr, tj, pj, uj, vj = rr[order], tj[order], pj[order], u[a, j][order], v[a, j][order]
+                first = np.ones(rr.size, bool)
+                first[1:] = rr[1:] != rr[:-1]
+                rr, tj, pj, uj, vj = rr[first], tj[first], pj[first], uj[first], vj[first]
+                # strictly smaller t, or the same t in this instance at a lower primitive (earlier
+                # instances keep ties: lower instance index)
+                better = (tj < best_t[rr]) | ((tj == best_t[rr]) & (best_i[rr] == k) & (pj < best_p[rr]))
+                better &= np.isfinite(tj)
+                rr = rr[better]
+                best_t[rr], best_i[rr], best_p[rr] = tj[better], k, pj[better]
+                bu[rr], bv[rr] = uj[better], vj[better]
         return best_t, best_i, best_p, bu, bv
 
     def _vertex_ids(self, k, prims):
         return self.inst[k]["tri"][prims]
 
-    def shade(self, O, D, t, inst, prim, u, v, py, mode):
+    def shade(self, O, D, t, inst, prim, u, v, py, mode, depth=0):
         spec = self.spec
         lights = [(np.array(c, float), np.array(p, float), float(i)) for (c, p, i) in spec.lights]
         mat = np.array(spec.material, float)
@@ -127,7 +172,19 @@ class Scene:
                 c = np.maximum(0, np.sum(n * ld, -1)) * np.where(shadowed, 0.3, 1.0)
                 out[sel] = c[:, None]
             elif mode == 0:
-                out[sel] = self._direct(P, n, mat[:3], lights) + self._pbr(n, O[sel], P, lights, mat)
+                s = self._direct(P, n, mat[:3], lights) + self._pbr(n, O[sel], P, lights, mat)
+                r = mat[5]
+                if r != 0.0 and I["iid"] in (0, 1) and depth < MAX_REFLECT:
+                    # ReflectRay: normalize(reflect(normalize(WorldRayDirection()), n)), normalised
+                    # again by CastReflectionRay; origin offset 0.001, TMin 0.001, TMax 1000, back
+                    # faces culled; the payload colour is the nested lerp
+                    dn = _norm(D[sel])
+                    rd = _norm(_norm(dn - 2.0 * n * np.sum(dn * n, -1, keepdims=True)))
+                    ro = P + 0.001 * rd
+                    tt, ii, pp, uu2, vv2 = self.intersect(ro, rd, 0.001, 1000.0, cull_back=True)
+                    c_next = self.shade(ro, rd, tt, ii, pp, uu2, vv2, py[sel], mode, depth + 1)
+                    s = s + r * (c_next - s)
+                out[sel] = s
             else:
                 c = np.zeros(sel.size)
                 for (lc, lp, li) in lights:

@@ -1250,17 +1250,26 @@ static vec3 oplane(const octx* c, vec3 P, const ohit* h, ostats* st) {
   return mk(v, v, v);
 }
 
+/* HLSL lerp(x, y, s) = x + s (y - x), per channel */
+static vec3 olerp(vec3 x, vec3 y, float s) {
+  return mk(x.x + s * (y.x - x.x), x.y + s * (y.y - x.y), x.z + s * (y.z - x.z));
+}
+
+/* payload colour of a reflection chain as the recursion returns it (Hit.hlsl:194-203): level k
+ * sets lerp(s_k, <colour of level k+1>, r) after its nested TraceRay returned, innermost first */
+static vec3 ounwind(const vec3* sk, int n, vec3 col, float r) {
+  for (int k = n - 1; k >= 0; --k) col = olerp(sk[k], col, r);
+  return col;
+}
+
 /* RT_SHADE_REF for one camera ray: ClosestHit (Hit.hlsl:183-204) / PlaneClosestHit / Miss, with
  * the reflection rays of InstanceID 0 and 1 (ReflectRay :176-181, CastReflectionRay
  * Common.hlsl:58-69: origin offset 0.001, TMin 0.001, TMax 1000, back faces culled) when the
- * material's reflectivity r != 0. The nested lerp(s_k, c_{k+1}, r) chain is evaluated front to
- * back: acc += (w (1 - r)) s_k, w *= r, ending with acc + w c_N (mathematically the same sum;
- * this float order is the pinned one). r == 0 traces no reflection. */
+ * material's reflectivity r != 0; the nested lerps unwound innermost first (ounwind).
+ * r == 0 traces no reflection. */
 static vec3 oshade_ref(const octx* c, uint32_t py, vec3 O, vec3 D, int f, ohit h, ostats* st) {
   const float refl = c->mat[5];
-  vec3 acc = mk(0, 0, 0), ro = O, rd = D;
-  float w = 1.0f;
-  int chain = 0;
+  vec3 sk[O_MAX_REFLECT], ro = O, rd = D;
   for (int depth = 0;; ++depth) {
     vec3 term;
     if (!f) {
@@ -1274,9 +1283,7 @@ static vec3 oshade_ref(const octx* c, uint32_t py, vec3 O, vec3 D, int f, ohit h
         vec3 n = o_interp_normal(c->s, h.inst, h.prim, h.u, h.v);
         vec3 s = vadd(odirect(P, n, ld3(c->mat), c->L, c->nl), opbr(n, ro, P, c->L, c->nl, c->mat));
         if (refl != 0.0f && (ir->instance_id == 0u || ir->instance_id == 1u) && depth < O_MAX_REFLECT) {
-          acc = vadd(acc, vscale(s, w * (1.0f - refl)));
-          w = w * refl;
-          chain = 1;
+          sk[depth] = s;
           vec3 dir = vnorm(vnorm(vreflect(vnorm(rd), n)));
           ro = vadd(P, vscale(dir, 0.001f));
           rd = dir;
@@ -1288,7 +1295,7 @@ static vec3 oshade_ref(const octx* c, uint32_t py, vec3 O, vec3 D, int f, ohit h
         term = s;
       }
     }
-    return chain ? vadd(acc, vscale(term, w)) : term;
+    return ounwind(sk, depth, term, refl);
   }
 }
 
@@ -1347,13 +1354,13 @@ static uint32_t unorm8(float x) {
 
 /* One camera sample for the 64 lanes of a wave tile, traces as wave packets
  * (shade_sample_packet in rt_trace.hip): lanes without a ray of a kind join that packet dead. */
-static void osample_packet(const octx* c, const uint32_t* px, const uint32_t* py, const int* inimg, float ox,
-                           float oy, vec3* color, ostats* st) {
+static void osample_packet(const octx* c, const uint32_t* px, const uint32_t* py, const int* inimg, const float* ox,
+                           const float* oy, vec3* color, ostats* st) {
   vec3 O[OPK], D[OPK], P[OPK], sd[OPK];
   ohit h[OPK], hs[OPK];
   int found[OPK], occl[OPK], need[OPK];
   for (int l = 0; l < OPK; ++l) {
-    oraygen(c, px[l], py[l], ox, oy, &O[l], &D[l]);
+    oraygen(c, px[l], py[l], ox[l], oy[l], &O[l], &D[l]);
     if (inimg[l]) st->v[0]++;
   }
   opacket(c->s, O, D, 0.0f, 100000.0f, 0, 0, inimg, h, found, st);
@@ -1365,11 +1372,11 @@ static void osample_packet(const octx* c, const uint32_t* px, const uint32_t* py
     /* oshade_ref, level by level for the whole tile: each level's shadow rays and next
      * reflection rays are one packet each */
     const float refl = c->mat[5];
-    vec3 acc[OPK], ro[OPK], rd[OPK], ldir[OPK], nf[OPK];
-    float w[OPK];
-    int chain[OPK], act[OPK], nxt[OPK];
+    vec3 ro[OPK], rd[OPK], ldir[OPK], nf[OPK];
+    static _Thread_local vec3 sk[OPK][O_MAX_REFLECT];
+    int act[OPK], nxt[OPK];
     for (int l = 0; l < OPK; ++l) {
-      acc[l] = mk(0, 0, 0); ro[l] = O[l]; rd[l] = D[l]; w[l] = 1.0f; chain[l] = 0; act[l] = inimg[l];
+      ro[l] = O[l]; rd[l] = D[l]; act[l] = inimg[l];
     }
     for (int depth = 0;; ++depth) {
       int any_next = 0;
@@ -1395,9 +1402,7 @@ static void osample_packet(const octx* c, const uint32_t* px, const uint32_t* py
           vec3 n = o_interp_normal(c->s, h[l].inst, h[l].prim, h[l].u, h[l].v);
           vec3 s = vadd(odirect(P[l], n, ld3(c->mat), c->L, c->nl), opbr(n, ro[l], P[l], c->L, c->nl, c->mat));
           if (refl != 0.0f && (ir->instance_id == 0u || ir->instance_id == 1u) && depth < O_MAX_REFLECT) {
-            acc[l] = vadd(acc[l], vscale(s, w[l] * (1.0f - refl)));
-            w[l] = w[l] * refl;
-            chain[l] = 1;
+            sk[l][depth] = s;
             vec3 dir = vnorm(vnorm(vreflect(vnorm(rd[l]), n)));
             ro[l] = vadd(P[l], vscale(dir, 0.001f));
             rd[l] = dir;
@@ -1408,7 +1413,7 @@ static void osample_packet(const octx* c, const uint32_t* px, const uint32_t* py
           }
           term = s;
         }
-        color[l] = chain[l] ? vadd(acc[l], vscale(term, w[l])) : term;
+        color[l] = ounwind(sk[l], depth, term, refl);
         act[l] = 0;
       }
       opacket(c->s, P, sd, 0.01f, 100000.0f, 1, 0, need, hs, occl, st);
@@ -1420,7 +1425,7 @@ static void osample_packet(const octx* c, const uint32_t* px, const uint32_t* py
         float li = fmax2(0.0f, vdot(nf[l], ldir[l]));
         float v = (1.0f * li) * factor;
         vec3 term = mk(v, v, v);
-        color[l] = chain[l] ? vadd(acc[l], vscale(term, w[l])) : term;
+        color[l] = ounwind(sk[l], depth, term, refl);
         act[l] = 0;
       }
       if (!any_next) return;
@@ -1479,37 +1484,56 @@ static void store_px(const ojob* j, size_t o, vec3 acc) {
   }
 }
 
-/* wave tiles of 8 x 8 (pixel column, row-list entry), lane = 8 * (row % 8) + column % 8 */
+/* Wave tiles as the device deals them (rt_trace.hip k_trace_frame_packet): spp 1 (and the sample
+ * loop for spp 9): 8 x 8 pixels (pixel column, row-list entry), lane = 8 * (row % 8) + column % 8;
+ * spp 4 / 16: the k x k samples of a pixel in consecutive lanes, (8 / k) x (8 / k) pixels per wave,
+ * lane = k^2 * (8/k * (row % (8/k)) + column % (8/k)) + sample, sample = k * sy + sx; the pixel's
+ * samples are summed in sample order as the loop adds them. */
 static void* render_tiles(void* arg) {
   ojob* j = (ojob*)arg;
   const octx* c = j->c;
-  const uint32_t tw = (c->W + 7) / 8, th = (j->nrows + 7) / 8;
+  const int lanes_k = (c->k == 2 || c->k == 4) ? c->k : 1; /* samples held by lanes */
+  const uint32_t ns = (uint32_t)(lanes_k * lanes_k), tp = 8u / (uint32_t)lanes_k;
+  const uint32_t tw = (c->W + tp - 1) / tp, th = (j->nrows + tp - 1) / tp;
   for (uint32_t t = j->tid; t < tw * th; t += j->nthreads) {
     const uint32_t tx = t % tw, ty = t / tw;
-    uint32_t px[OPK], py[OPK];
+    uint32_t px[OPK], py[OPK], orow[OPK];
     int inimg[OPK];
+    float ox[OPK], oy[OPK];
     vec3 acc[OPK], col[OPK];
     for (int l = 0; l < OPK; ++l) {
-      px[l] = tx * 8 + (uint32_t)(l & 7);
-      const uint32_t orow = ty * 8 + (uint32_t)(l >> 3);
-      inimg[l] = px[l] < c->W && orow < j->nrows;
-      py[l] = inimg[l] ? (j->rows ? j->rows[orow] : orow) : 0;
+      const uint32_t s = (uint32_t)l % ns, p = (uint32_t)l / ns;
+      px[l] = tx * tp + p % tp;
+      orow[l] = ty * tp + p / tp;
+      inimg[l] = px[l] < c->W && orow[l] < j->nrows;
+      py[l] = inimg[l] ? (j->rows ? j->rows[orow[l]] : orow[l]) : 0;
+      ox[l] = ((float)(s % (uint32_t)lanes_k) + 0.5f) / (float)lanes_k;
+      oy[l] = ((float)(s / (uint32_t)lanes_k) + 0.5f) / (float)lanes_k;
       acc[l] = mk(0, 0, 0);
     }
-    for (int sy = 0; sy < c->k; ++sy)
-      for (int sx = 0; sx < c->k; ++sx) {
-        float ox = ((float)sx + 0.5f) / (float)c->k, oy = ((float)sy + 0.5f) / (float)c->k;
-        osample_packet(c, px, py, inimg, ox, oy, col, &j->st);
-        for (int l = 0; l < OPK; ++l) acc[l] = vadd(acc[l], col[l]);
-      }
-    for (int l = 0; l < OPK; ++l) {
+    if (lanes_k > 1) {
+      osample_packet(c, px, py, inimg, ox, oy, col, &j->st);
+      for (int l = 0; l < OPK; l += (int)ns)
+        for (uint32_t q = 0; q < ns; ++q) acc[l] = vadd(acc[l], col[l + (int)q]);
+    } else {
+      for (int sy = 0; sy < c->k; ++sy)
+        for (int sx = 0; sx < c->k; ++sx) {
+          for (int l = 0; l < OPK; ++l) {
+            ox[l] = ((float)sx + 0.5f) / (float)c->k;
+            oy[l] = ((float)sy + 0.5f) / (float)c->k;
+          }
+          osample_packet(c, px, py, inimg, ox, oy, col, &j->st);
+          for (int l = 0; l < OPK; ++l) acc[l] = vadd(acc[l], col[l]);
+        }
+    }
+    for (int l = 0; l < OPK; l += (int)ns) {
       if (!inimg[l]) continue;
       vec3 a = acc[l];
       if (c->k > 1) {
-        float ns = (float)(c->k * c->k);
-        a = mk(a.x / ns, a.y / ns, a.z / ns);
+        float n = (float)(c->k * c->k);
+        a = mk(a.x / n, a.y / n, a.z / n);
       }
-      store_px(j, (size_t)(ty * 8 + (uint32_t)(l >> 3)) * c->W + px[l], a);
+      store_px(j, (size_t)orow[l] * c->W + px[l], a);
     }
   }
   return NULL;

@@ -880,19 +880,33 @@ __device__ __forceinline__ bool reflective(const FrameParams& fp, const HitInsta
          depth < kMaxReflectDepth;
 }
 
+// HLSL lerp(x, y, s) = x + s * (y - x).
+__device__ __forceinline__ V3 lerp3(V3 x, V3 y, float s) {
+  return v3(x.x + s * (y.x - x.x), x.y + s * (y.y - x.y), x.z + s * (y.z - x.z));
+}
+
+// The payload colour of a reflection chain as the HLSL recursion returns it: each ClosestHit
+// level k sets lerp(s_k, <colour of level k + 1>, r) after its nested TraceRay returned
+// (Hit.hlsl:194-203), so the innermost lerp is evaluated first. sk[0..n) holds the levels'
+// own surface colours (finalSurfaceColor), c the colour the innermost ray came back with.
+__device__ __forceinline__ V3 unwind_chain(const V3* sk, int n, V3 c, float r) {
+  for (int k = n - 1; k >= 0; --k) c = lerp3(sk[k], c, r);
+  return c;
+}
+
 // RT_SHADE_REF for one camera ray, one lane: ClosestHit (Hit.hlsl:183-204) / PlaneClosestHit
 // (:207-241) / Miss, with the reflection rays of InstanceID 0 and 1 when the material's
-// reflectivity r != 0 (back faces culled). The nested lerp(s_k, c_{k+1}, r) chain is evaluated
-// front to back: acc += (w (1 - r)) s_k, w *= r, ending with acc + w c_N (the pinned order,
-// mirrored by oracle/rt_oracle.c oshade_ref). r == 0 traces no reflection.
+// reflectivity r != 0 (back faces culled). Each level's surface colour is kept (per-lane
+// scratch, touched only by reflective hits) and the nested lerps are unwound innermost first,
+// as the recursion evaluates them (oracle/rt_oracle.c oshade_ref mirrors it). r == 0 traces no
+// reflection.
 template <bool STATS>
 __device__ V3 shade_ref(const SceneView& sc, const FrameParams& fp, uint32_t py, V3 O, V3 D, bool f, HitRec hit,
                         const LaneStack& stk, Counters& cnt) {
   const float refl = fp.material.reflectivity;
   const V3 albedo = v3(fp.material.albedo[0], fp.material.albedo[1], fp.material.albedo[2]);
-  V3 acc = v3(0.0f, 0.0f, 0.0f), ro = O, rd = D;
-  float w = 1.0f;
-  bool chain = false;
+  V3 sk[kMaxReflectDepth];
+  V3 ro = O, rd = D;
   for (int depth = 0;; ++depth) {
     V3 term;
     if (!f) {
@@ -915,9 +929,7 @@ __device__ V3 shade_ref(const SceneView& sc, const FrameParams& fp, uint32_t py,
         const V3 n = interpolated_world_normal(ir, hit.prim, hit.u, hit.v);
         const V3 s = add(direct_lighting(fp, P, n, albedo), pbr_shading(fp, n, ro, P));
         if (reflective(fp, ir, depth)) {
-          acc = add(acc, muls(s, w * (1.0f - refl)));
-          w = w * refl;
-          chain = true;
+          sk[depth] = s;
           reflection_ray(P, n, rd, ro, rd);
           if (STATS) ++cnt.refl;
           f = trace<false, STATS, true>(sc, ro, rd, 0.001f, 1000.0f, hit, stk, cnt);
@@ -926,7 +938,7 @@ __device__ V3 shade_ref(const SceneView& sc, const FrameParams& fp, uint32_t py,
         term = s;
       }
     }
-    return chain ? add(acc, muls(term, w)) : term;
+    return unwind_chain(sk, depth, term, refl);
   }
 }
 
@@ -993,25 +1005,21 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
   }
   trace_packet<false, STATS, R>(sc, O, D, 0.0f, 100000.0f, inimg, found, hit, cnt);
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    color[r] = miss_color(fp, py[r]);
-    P[r] = add(O[r], muls(D[r], hit[r].t));  // GetWorldHitPoint, Common.hlsl:24-27
-  }
+  for (int r = 0; r < R; ++r) P[r] = add(O[r], muls(D[r], hit[r].t));  // GetWorldHitPoint, Common.hlsl:24-27
   if (MODE == 0) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) color[r] = miss_color(fp, py[r]);
     // shade_ref level by level for the whole packet: each level's shadow rays and next
     // reflection rays are one packet each (mirrored by oracle osample_packet)
     const float refl = fp.material.reflectivity;
     const V3 albedo = v3(fp.material.albedo[0], fp.material.albedo[1], fp.material.albedo[2]);
-    V3 acc[R], ro[R], rd[R], ldir[R], nf[R];
-    float w[R];
-    bool chain[R], act[R], nxt[R];
+    V3 ro[R], rd[R], ldir[R], nf[R];
+    V3 sk[R][kMaxReflectDepth];  // surface colours of the reflective levels (unwound innermost first)
+    bool act[R], nxt[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      acc[r] = v3(0.0f, 0.0f, 0.0f);
       ro[r] = O[r];
       rd[r] = D[r];
-      w[r] = 1.0f;
-      chain[r] = false;
       act[r] = inimg[r];
     }
     for (int depth = 0;; ++depth) {
@@ -1039,9 +1047,7 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
           const V3 n = interpolated_world_normal(ir, hit[r].prim, hit[r].u, hit[r].v);
           const V3 s = add(direct_lighting(fp, P[r], n, albedo), pbr_shading(fp, n, ro[r], P[r]));
           if (reflective(fp, ir, depth)) {
-            acc[r] = add(acc[r], muls(s, w[r] * (1.0f - refl)));
-            w[r] = w[r] * refl;
-            chain[r] = true;
+            sk[r][depth] = s;
             reflection_ray(P[r], n, rd[r], ro[r], rd[r]);
             nxt[r] = true;
             if (STATS) ++cnt.refl;
@@ -1049,7 +1055,8 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
           }
           term = s;
         }
-        color[r] = chain[r] ? add(acc[r], muls(term, w[r])) : term;
+        // a lane ending its chain at this level holds exactly `depth` reflective levels
+        color[r] = unwind_chain(sk[r], depth, term, refl);
         act[r] = false;
       }
       trace_packet<true, STATS, R>(sc, P, sd, 0.01f, 100000.0f, need, occl, sh, cnt);
@@ -1062,7 +1069,7 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
         const float li = maxf(0.0f, dot(nf[r], ldir[r]));
         const float c = (1.0f * li) * factor;
         const V3 term = v3(c, c, c);
-        color[r] = chain[r] ? add(acc[r], muls(term, w[r])) : term;
+        color[r] = unwind_chain(sk[r], depth, term, refl);
         act[r] = false;
       }
       // uniform exit: no ray of the packet reflects further
@@ -1105,12 +1112,12 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
     for (int r = 0; r < R; ++r)
       if (need[r]) c[r] = c[r] + nl[r] * (occl[r] ? 0.3f : 1.0f);
   }
+  // the miss colour is formed here, not kept live across the shadow walks
 #pragma unroll
-  for (int r = 0; r < R; ++r)
-    if (found[r]) {
-      const float v = c[r] / (float)fp.nlights;
-      color[r] = v3(v, v, v);
-    }
+  for (int r = 0; r < R; ++r) {
+    const float v = c[r] / (float)fp.nlights;
+    color[r] = found[r] ? v3(v, v, v) : miss_color(fp, py[r]);
+  }
 }
 
 // WAVE_FETCH: the fetch counters are wave-uniform (packet schedule) and count once per wave.
@@ -1165,52 +1172,85 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void k_trace_frame(SceneView 
   if (STATS) flush_stats<false>(cnt, stats);
 }
 
-// Wave-packet frame kernel. A wave covers an 8 x 8R tile (ray r of lane l: column l % 8, row
-// entry 8r + l / 8 of the tile), a workgroup RT_PACKET_WX x RT_PACKET_WY tiles (2 x 1: 128
-// threads, 16 x 8R pixels; smaller workgroups shorten the tail of the launch). Every lane runs
-// the sample loop (rays outside the image or the row list join the packets dead) and stores only
-// in-image pixels.
-// Occupancy: LAMBERT_SHADOW (the perf configs) runs at 7 waves per SIMD (72 VGPRs: the one-sample
-// kernel needs 67, the 4-spp one spills a few outside the traversal loops); 6 and 8 measured
-// slower overall. REF and PRIMARY keep the allocator's choice (REF would spill hundreds of
-// bytes; PRIMARY measured neutral).
+// Wave-packet frame kernel. KS = 1: a wave covers an 8 x 8R pixel tile (ray r of lane l: column
+// l % 8, row entry 8r + l / 8 of the tile), one camera sample per pixel. KS = 2 / 4 (spp 4 / 16,
+// R = 1): the KS x KS samples of a pixel sit in consecutive lanes and a wave covers an
+// (8 / KS) x (8 / KS) pixel tile: every lane traces ONE sample (no accumulator lives across the
+// traces, so the multi-sample kernel has the one-sample kernel's registers), the packet's
+// footprint on screen shrinks with the sample count (more coherent packets), and the pixel's
+// samples are summed across lanes in sample order at the end — the same float additions, in the
+// same order, as the sample loop. KS = 0: the sample loop (spp 9, or R > 1). A workgroup is
+// RT_PACKET_WX x RT_PACKET_WY waves (2 x 1: 128 threads; smaller workgroups shorten the tail of
+// the launch). Rays outside the image or the row list join the packets dead; only in-image
+// pixels are stored.
+// Occupancy: LAMBERT_SHADOW (the perf configs) runs at 7 waves per SIMD (72 VGPRs, no spills);
+// 6 and 8 measured slower overall. REF and PRIMARY keep the allocator's choice (REF would spill
+// hundreds of bytes; PRIMARY measured neutral).
 #ifndef RT_LS_WAVES
 #define RT_LS_WAVES 7
 #endif
+#ifndef RT_SPP_WAVES
+#define RT_SPP_WAVES 5  // the sample-loop kernel (KS = 0) needs ~95 VGPRs: 5 waves spill nothing
+#endif
+#ifndef RT_KS_WAVES
+#define RT_KS_WAVES RT_LS_WAVES  // the sample-lane kernels (KS = 2, 4)
+#endif
 #ifndef RT_PACKET_WX
-#define RT_PACKET_WX 2  // waves of a packet workgroup along x (8-pixel tiles)
+#define RT_PACKET_WX 2  // waves of a packet workgroup along x
 #endif
 #ifndef RT_PACKET_WY
-#define RT_PACKET_WY 1  // ... and along y (8R-row tiles); 2 x 1 measured best (C4/C5 -6 % vs 2 x 2)
+#define RT_PACKET_WY 1  // ... and along y; 2 x 1 measured best (C4/C5 -6 % vs 2 x 2)
+#endif
+#ifndef RT_SAMPLE_LANES
+#define RT_SAMPLE_LANES 1  // 0: every multi-sample frame uses the sample loop (A/B knob)
 #endif
 constexpr int kPacketBlock = 64 * RT_PACKET_WX * RT_PACKET_WY;
-// SPP1: one sample per pixel (spp_side == 1, every perf config but C5): no accumulator lives
-// across the traces.
-template <int MODE, bool STATS, int R, bool SPP1>
-__global__ __launch_bounds__(kPacketBlock) __attribute__((amdgpu_waves_per_eu((MODE == 1 && !STATS) ? RT_LS_WAVES : 1)))
-void k_trace_frame_packet(SceneView sc, FrameParams fp,
-                                                               const uint32_t* __restrict__ rows,
-                                                               uint32_t* __restrict__ rgba8,
-                                                               float4* __restrict__ rgba32f,
-                                                               unsigned long long* __restrict__ stats) {
+
+template <int MODE, bool STATS, int R, int KS>
+__global__ __launch_bounds__(kPacketBlock) __attribute__((amdgpu_waves_per_eu(
+    (MODE == 1 && !STATS) ? (KS == 0 ? RT_SPP_WAVES : (KS == 1 ? RT_LS_WAVES : RT_KS_WAVES)) : 1)))
+void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restrict__ rows,
+                          uint32_t* __restrict__ rgba8, float4* __restrict__ rgba32f,
+                          unsigned long long* __restrict__ stats) {
+  static_assert(KS <= 1 || R == 1, "sample lanes need one ray per lane");
+  constexpr uint32_t NS = KS > 1 ? KS * KS : 1;  // samples of a pixel held by consecutive lanes
+  constexpr uint32_t TP = KS > 1 ? 8 / KS : 8;    // tile side in pixels
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-  const uint32_t x = blockIdx.x * (8u * RT_PACKET_WX) + (w % RT_PACKET_WX) * 8u + (lane & 7u);
-  uint32_t px[R], py[R], orow[R];
+  const uint32_t sample = lane % NS, pix = lane / NS;
+  const uint32_t x = blockIdx.x * (TP * RT_PACKET_WX) + (w % RT_PACKET_WX) * TP + (pix % TP);
+  uint32_t px[R], py[R], out[R];  // out: the pixel's output index, ~0 when this lane stores nothing
   bool inimg[R];
   V3 acc[R], col[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     px[r] = x;
-    orow[r] = blockIdx.y * (8u * R * RT_PACKET_WY) + (w / RT_PACKET_WX) * (8u * R) + 8u * r + (lane >> 3);
-    inimg[r] = x < fp.width && orow[r] < fp.nrows;
+    const uint32_t orow = blockIdx.y * (TP * R * RT_PACKET_WY) + (w / RT_PACKET_WX) * (TP * R) + TP * r + pix / TP;
+    inimg[r] = x < fp.width && orow < fp.nrows;
     py[r] = 0;
-    if (inimg[r]) py[r] = rows ? rows[orow[r]] : orow[r];
+    if (inimg[r]) py[r] = rows ? rows[orow] : orow;
+    out[r] = (inimg[r] && sample == 0) ? orow * fp.width + x : 0xffffffffu;  // < 2^32 pixels (rt_api.cpp)
     acc[r] = v3(0.0f, 0.0f, 0.0f);
   }
   Counters cnt;
-  const uint32_t k = SPP1 ? 1u : fp.spp_side;
-  if (SPP1) {
+  const uint32_t k = KS == 1 ? 1u : (KS > 1 ? (uint32_t)KS : fp.spp_side);
+  if (KS == 1) {
     shade_sample_packet<MODE, STATS, R>(sc, fp, px, py, 0.5f, 0.5f, inimg, acc, cnt);  // (0 + 0.5) / 1
+  } else if (KS > 1) {
+    // this lane's sample (sx, sy) of the k x k grid, the sample loop's offsets
+    const float ox = ((float)(sample % KS) + 0.5f) / (float)KS;
+    const float oy = ((float)(sample / KS) + 0.5f) / (float)KS;
+    shade_sample_packet<MODE, STATS, R>(sc, fp, px, py, ox, oy, inimg, col, cnt);
+    // sum in sample order: ((0 + c0) + c1) + ... exactly as the loop adds them (0 + c0 == c0).
+    // The lane id is re-read here (v_mbcnt) rather than kept live across the traces.
+    uint32_t lid;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lid));
+    const int base = (int)(lid & ~(NS - 1u));
+    V3 sum = v3(__shfl(col[0].x, base, 64), __shfl(col[0].y, base, 64), __shfl(col[0].z, base, 64));
+#pragma unroll
+    for (int q = 1; q < (int)NS; ++q)
+      sum = add(sum, v3(__shfl(col[0].x, base + q, 64), __shfl(col[0].y, base + q, 64),
+                        __shfl(col[0].z, base + q, 64)));
+    acc[0] = sum;
   } else {
     for (uint32_t sy = 0; sy < k; ++sy)
       for (uint32_t sx = 0; sx < k; ++sx) {
@@ -1228,8 +1268,8 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp,
       const float ns = (float)(k * k);
       a = v3(a.x / ns, a.y / ns, a.z / ns);
     }
-    if (inimg[r]) {
-      const size_t o = (size_t)orow[r] * fp.width + px[r];
+    if (out[r] != 0xffffffffu) {
+      const uint32_t o = out[r];
       rgba8[o] = unorm8(a.x) | (unorm8(a.y) << 8) | (unorm8(a.z) << 16) | (255u << 24);
       if (rgba32f) rgba32f[o] = make_float4(a.x, a.y, a.z, 1.0f);
     }
@@ -1277,14 +1317,20 @@ hipError_t launch_mode(const SceneView& sc, const FrameParams& fp, const uint32_
   dim3 grid((fp.width + 15) / 16, (fp.nrows + 15) / 16);
   if (schedule == RT_SCHED_PACKET && sc.packet_cap < kPacketStack) {
     constexpr int R = RT_PACKET_RAYS;
-    constexpr uint32_t tw = 8 * RT_PACKET_WX, th = 8 * R * RT_PACKET_WY;
+    // KS: 1 one sample per pixel; 2 / 4 the k x k samples of a pixel in consecutive lanes; 0 the loop
+    const int ks = fp.spp_side == 1 ? 1 : ((RT_SAMPLE_LANES && R == 1 && (fp.spp_side == 2 || fp.spp_side == 4))
+                                               ? (int)fp.spp_side : 0);
+    const uint32_t tp = ks > 1 ? 8u / (uint32_t)ks : 8u;
+    const uint32_t tw = tp * RT_PACKET_WX, th = tp * R * RT_PACKET_WY;
     dim3 gp((fp.width + tw - 1) / tw, (fp.nrows + th - 1) / th);
-    if (fp.spp_side == 1)
-      hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R, true>), gp, dim3(kPacketBlock), 0, s, sc, fp, rows,
-                         (uint32_t*)rgba8, (float4*)rgba32f, stats);
-    else
-      hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R, false>), gp, dim3(kPacketBlock), 0, s, sc, fp, rows,
-                         (uint32_t*)rgba8, (float4*)rgba32f, stats);
+#define RT_LAUNCH_PACKET(KS)                                                                                   \
+  hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R, (R == 1 ? KS : 0)>), gp, dim3(kPacketBlock), 0, s, sc, fp, \
+                     rows, (uint32_t*)rgba8, (float4*)rgba32f, stats)
+    if (ks == 1) RT_LAUNCH_PACKET(1);
+    else if (ks == 2) RT_LAUNCH_PACKET(2);
+    else if (ks == 4) RT_LAUNCH_PACKET(4);
+    else RT_LAUNCH_PACKET(0);
+#undef RT_LAUNCH_PACKET
   } else {
     size_t lds = (size_t)sc.lds_cap * kBlock * sizeof(int);
     hipLaunchKernelGGL((k_trace_frame<MODE, STATS>), grid, dim3(kBlock), lds, s, sc, fp, rows,

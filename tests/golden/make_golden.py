@@ -6,7 +6,8 @@ manipulator.json  camera-manipulator trajectories (mouseMove / motion / wheel / 
                   from oracle/ref_glm_manip.cpp over the reference's vendored glm (oracle/_ref/).
 frames_small.npz  oracle frames (RGBA8 + float32) of every config at small sizes; each is first
                   cross-checked against the independent float64 numpy restatement
-                  (oracle/np_reference.py) and the script refuses to write on disagreement.
+                  (oracle/np_reference.py: brute force, reflection chains, spp averaging) and
+                  the script refuses to write on any disagreement.
                   Traversal counters for both schedules: <cfg>_stats (wave packets, the device
                   default) and <cfg>_stats_lane (one traversal per pixel); the two schedules
                   must render the identical image.
@@ -33,8 +34,13 @@ from oracle import np_reference  # noqa: E402
 
 SIZES = {"REF": (96, 54), "C1": (64, 64), "C2": (96, 54), "C2F": (96, 54), "C3": (96, 54), "C4": (96, 54),
          "C5": (48, 27), "REFL": (96, 54), "REFLO": (96, 54), "DEGEN": (96, 54)}
-NUMPY_CHECK = {"REF", "C1", "C2", "C2F", "C3", "C4", "DEGEN"}  # C5 (257 instances x 4 spp) is too slow in numpy
+NUMPY_CHECK = {"REF", "C1", "C2", "C2F", "C3", "C4", "C5", "REFL", "REFLO", "DEGEN"}
 NUMPY_TOL = 1e-4
+# C5 looks at small rabbit triangles (~0.05 units) from ~70 units away: float32 Moller-Trumbore
+# barycentrics there are good to ~7e-4 (measured: one sample, |dv| 6.6e-4, whose vertex normals
+# differ by ~0.9 across the triangle), so a shaded value can move by up to ~1e-3 of the float64
+# restatement with the same triangle hit. The north-star bound (L-inf < 1e-3) is the tolerance.
+NUMPY_TOL_BY_CFG = {"C5": 1e-3}
 
 
 def _harness(name: str, fixture: str):
@@ -64,7 +70,7 @@ def frames():
             img, _ = np_reference.Scene(spec).render(spec.camera_buffer())
             d = float(np.abs(img - o32[..., :3]).max())
             print(f"{name}: numpy float64 vs oracle L-inf {d:.3g}")
-            if d > NUMPY_TOL:
+            if d > NUMPY_TOL_BY_CFG.get(name, NUMPY_TOL):
                 raise SystemExit(f"{name}: oracle disagrees with the numpy restatement ({d})")
         data[f"{name}_rgba8"] = o8
         data[f"{name}_rgba32f"] = o32

@@ -200,14 +200,17 @@ def test_rows_subset_matches_full_frame():
     c.close()
 
 
-def test_full_size_c2_sampled_rows():
-    """Full BASELINE size (1920x1080): GPU frame vs oracle on a deterministic row sample."""
-    spec = scenes.config("C2")
+@pytest.mark.parametrize("name,step", [("C2", 41), ("C3", 41), ("C4", 37), ("C5", 79), ("REF", 29), ("REFL", 53)])
+def test_full_size_sampled_rows(name, step):
+    """Full BASELINE sizes (C2-C4 1920x1080, C5 3840x2160 at 4 spp, the reference scene 1280x720):
+    the whole GPU frame, compared with the oracle on a deterministic row sample (every step-th row,
+    plus the last), bit for bit."""
+    spec = scenes.config(name)
     c, o = load_both(spec)
     g8, g32 = gpu_render(c, spec)
-    rows = np.arange(0, spec.height, 41, dtype=np.uint32)
-    o8, o32, _ = o.render_spec(spec, rows=rows, nthreads=8)
-    assert_images_equal(g8[rows], g32[rows], o8, o32, "C2 1080p sampled rows")
+    rows = np.unique(np.append(np.arange(0, spec.height, step), spec.height - 1)).astype(np.uint32)
+    o8, o32, _ = o.render_spec(spec, rows=rows, nthreads=16)
+    assert_images_equal(g8[rows], g32[rows], o8, o32, f"{name} {spec.width}x{spec.height} sampled rows")
     # size-independent property: alpha channel is opaque everywhere
     assert (g8[..., 3] == 255).all()
     c.close()

@@ -206,7 +206,7 @@ def test_oracle_matches_golden_frames(name):
         assert np.array_equal(st, GOLD[f"{name}_{key}"])
 
 
-@pytest.mark.parametrize("name", ["REF", "C1", "C2F", "C3", "DEGEN"])
+@pytest.mark.parametrize("name", ["REF", "C1", "C2F", "C3", "DEGEN", "REFLO"])
 def test_oracle_vs_independent_numpy(name):
     spec = scenes.config(name).with_size(40, 24)
     img, _ = np_reference.Scene(spec).render(spec.camera_buffer())
