@@ -980,6 +980,69 @@ __device__ V3 shade_sample(const SceneView& sc, const FrameParams& fp, uint32_t 
   return v3(c, c, c);
 }
 
+#ifndef RT_SHADOW_COMPACT
+#define RT_SHADOW_COMPACT 0  // workgroup shadow-ray compaction (measured: not a win)
+#endif
+
+// Workgroup ray compaction of one light's shadow rays (north star: "wavefront ballot/prefix-sum for
+// ray compaction"): each wave ballots its lanes that need the ray, the waves' counts go through
+// LDS, and when all of them fit one 64-ray packet (and more than one wave has some) the rays are
+// compacted — slot = the wave's prefix + mbcnt of the ballot — and wave 0 traces them as ONE packet,
+// the occlusion bits coming back through LDS; otherwise every wave traces its own packet. The
+// whole workgroup must call it (uniform per light: two barriers). Same results as the per-wave
+// packets (a ray's occlusion does not depend on its packet). Kept as RT_SHADOW_COMPACT: with the
+// screen-tile waves the shadow packets are already ~94-99 % full (C2-C4), so it rarely fires.
+template <bool STATS>
+__device__ bool shadow_compact(const SceneView& sc, V3 P, V3 d, bool need, uint32_t parity, Counters& cnt) {
+  __shared__ float s_ray[6][64];
+  __shared__ uint32_t s_cnt[2][4];
+  __shared__ uint32_t s_occ[2];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint64_t m = wave_ballot(need);
+  if (lane == 0) s_cnt[parity][w] = (uint32_t)__builtin_popcountll(m);
+  __syncthreads();
+  uint32_t total = 0, base = 0, busy = 0;
+  for (uint32_t k = 0; k < nw; ++k) {
+    const uint32_t c = s_cnt[parity][k];
+    base += k < w ? c : 0u;
+    total += c;
+    busy += c ? 1u : 0u;
+  }
+  const bool merge = total <= 64u && busy >= 2u;  // uniform over the workgroup
+  const uint32_t slot = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  V3 q = P, e = d;
+  bool alive = need;
+  if (merge) {
+    if (need) {
+      s_ray[0][slot] = P.x;
+      s_ray[1][slot] = P.y;
+      s_ray[2][slot] = P.z;
+      s_ray[3][slot] = d.x;
+      s_ray[4][slot] = d.y;
+      s_ray[5][slot] = d.z;
+    }
+    __syncthreads();
+    alive = w == 0 && lane < total;
+    if (alive) {
+      q = v3(s_ray[0][lane], s_ray[1][lane], s_ray[2][lane]);
+      e = v3(s_ray[3][lane], s_ray[4][lane], s_ray[5][lane]);
+    }
+  }
+  // one packet per wave, or the merged packet in wave 0 (the other waves' packets are all dead and
+  // return at once); a single inlined walk keeps the kernel's registers
+  HitRec h;
+  bool f;
+  trace_packet<true, STATS, 1>(sc, &q, &e, 0.01f, 100000.0f, &alive, &f, &h, cnt);
+  if (!merge) return f;
+  const uint64_t om = wave_ballot(f);
+  if (w == 0 && lane == 0) {
+    s_occ[0] = (uint32_t)om;
+    s_occ[1] = (uint32_t)(om >> 32);
+  }
+  __syncthreads();
+  return need && ((s_occ[slot >> 5] >> (slot & 31u)) & 1u) != 0u;
+}
+
 // shade_sample for the wave-packet traversal: identical arithmetic per ray, with every trace
 // hoisted to wave-uniform control flow (rays without a trace of that kind join the packet dead).
 // Each lane shades R camera samples (R pixels) at once.
@@ -1107,7 +1170,12 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
       occl[r] = false;
       if (MODE == 1 && STATS && need[r]) ++cnt.shadow;
     }
-    if (MODE == 1) trace_packet<true, STATS, R>(sc, P, sd, 0.01f, 100000.0f, need, occl, sh, cnt);
+    if (MODE == 1) {
+      if (RT_SHADOW_COMPACT && R == 1)
+        occl[0] = shadow_compact<STATS>(sc, P[0], sd[0], need[0], l & 1u, cnt);
+      else
+        trace_packet<true, STATS, R>(sc, P, sd, 0.01f, 100000.0f, need, occl, sh, cnt);
+    }
 #pragma unroll
     for (int r = 0; r < R; ++r)
       if (need[r]) c[r] = c[r] + nl[r] * (occl[r] ? 0.3f : 1.0f);
