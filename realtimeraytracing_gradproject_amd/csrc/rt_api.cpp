@@ -214,8 +214,8 @@ rt_status upload_blas(rt_ctx* c, DeviceBlas& b, const void* vtx, uint32_t vcount
   float ms = 0.0f;
   uint32_t nnodes4 = 0;
   if (e == hipSuccess)
-    e = rt::lbvh_build(primbox, ntri, b.nodes, sorted, false, &nnodes4, &b.depth, &b.max_stack, b.bounds, &ms, s);
-  if (e == hipSuccess) e = rt::blas_reorder(unsorted, sorted, ntri, b.tris, s);
+    e = rt::lbvh_build(primbox, ntri, b.nodes, sorted, false, &nnodes4, &b.depth, &b.max_stack, b.bounds, &ms, s,
+                       unsorted, b.tris);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return hip_fail(c, e, "BLAS build");
   b.ntri = ntri;

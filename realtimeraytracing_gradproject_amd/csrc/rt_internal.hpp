@@ -14,10 +14,12 @@ namespace rt {
 // used, the number of levels and the worst-case traversal stack of the tree are returned, with
 // the root box, in host memory. d_sorted
 // receives the leaf-order -> primitive permutation. Leaf refs are ~leaf_slot (BLAS, primitives
-// reordered afterwards) or ~primitive (TLAS). Synchronous.
+// reordered afterwards) or ~primitive (TLAS). With d_tri_in the BLAS triangles are gathered into
+// leaf order (d_tri_out) as part of the build. Synchronous.
 hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uint32_t* d_sorted,
                       bool leaf_ref_is_prim, uint32_t* node_count, uint32_t* depth, uint32_t* max_stack,
-                      float bounds[6], float* build_ms, hipStream_t stream);
+                      float bounds[6], float* build_ms, hipStream_t stream, const TriRec* d_tri_in = nullptr,
+                      TriRec* d_tri_out = nullptr);
 
 // Triangle setup: prim boxes + unsorted MT records from a {pos, normal} vertex array.
 hipError_t blas_prepare(const float* d_vtx, const uint32_t* d_idx, uint32_t ntri, TriRec* d_tris,

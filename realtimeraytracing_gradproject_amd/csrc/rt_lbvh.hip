@@ -11,14 +11,30 @@
 //                           exclusive scan, stable scatter with wave64 ballot match + popcount
 //                           ranks (keys tie-break on primitive index: stable)
 //   4. Karras hierarchy     Karras 2012 over key64 = morton << 32 | leaf position
-//   5. bottom-up refit      one thread per leaf, agent-scope release/acquire arrival counters
+//   5. bottom-up refit      one thread per leaf, agent-scope release/acquire arrival counters,
+//                           with the SAH collapse DP at each node
 //   6. pack                 64-B child-pair nodes (both child boxes per node)
+//   7. DP expansion + collapse into 4-wide BFS nodes, triangle gather into leaf order
+// Builds of n <= kFusedMax primitives (every BLAS and TLAS of the BASELINE configs) run all of
+// it in one 1024-thread workgroup instead (k_build_small): one launch, LDS-resident sort.
 #include <hip/hip_runtime.h>
 
 #include <vector>
 
 #include "rt_internal.hpp"
 
+#ifndef RT_FUSED_BUILD
+#define RT_FUSED_BUILD 1  // n <= kFusedMax: the whole build in one workgroup (k_build_small)
+#endif
+#ifndef RT_FUSED_MAX_N
+#define RT_FUSED_MAX_N 3072  // largest n built by k_build_small (measured crossover; capacity kFusedMax)
+#endif
+#ifndef RT_REFIT_WT
+#define RT_REFIT_WT 1  // multi-kernel refit: write-through hand-off instead of agent release/acquire fences
+#endif
+#ifndef RT_BUILD_TIMING
+#define RT_BUILD_TIMING 0  // 1: k_build_small prints per-phase shader-clock counts (diagnostics)
+#endif
 #ifndef RT_SAH_COLLAPSE
 #define RT_SAH_COLLAPSE 1  // SAH-optimal binary -> BVH4 collapse (DP); 0: greedy largest-area opening
 #endif
@@ -249,10 +265,7 @@ __device__ __forceinline__ float half_area6(const float* b) {
 // C(n, i) = min(C(n, 1), D(n, i)). dpc[n] = C(n, 1..4); dps[n] byte i-1 = 0 when n is a wide node
 // for i slots, else j (the slots of c0). Strict < keeps the lowest j; oracle dp_prepare is the same
 // arithmetic in the same order.
-__device__ __forceinline__ void sah_dp(int node, const float* bb, int c0, int c1, float4* __restrict__ dpc,
-                                       uint32_t* __restrict__ dps) {
-  const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  const float4 l = c0 >= 0 ? dpc[c0] : zero, r = c1 >= 0 ? dpc[c1] : zero;
+__device__ __forceinline__ void sah_dp_vals(const float* bb, float4 l, float4 r, float4& out_c, uint32_t& out_s) {
   const float cl[5] = {0.0f, l.x, l.y, l.z, l.w}, cr[5] = {0.0f, r.x, r.y, r.z, r.w};
   float D[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
   uint32_t J[5] = {0, 0, 0, 0, 0};
@@ -276,8 +289,29 @@ __device__ __forceinline__ void sah_dp(int node, const float* bb, int c0, int c1
     C[i] = split ? D[i] : self;
     S |= (split ? J[i] : 0u) << (8 * (i - 1));
   }
-  dpc[node] = make_float4(C[1], C[2], C[3], C[4]);
-  dps[node] = S;
+  out_c = make_float4(C[1], C[2], C[3], C[4]);
+  out_s = S;
+}
+
+__device__ __forceinline__ void sah_dp(int node, const float* bb, int c0, int c1, float4* __restrict__ dpc,
+                                       uint32_t* __restrict__ dps) {
+  const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  const float4 l = c0 >= 0 ? dpc[c0] : zero, r = c1 >= 0 ? dpc[c1] : zero;
+  float4 c;
+  uint32_t sj;
+  sah_dp_vals(bb, l, r, c, sj);
+  dpc[node] = c;
+  dps[node] = sj;
+}
+
+// Write-through hand-off (MI355X_MICROARCH.md, handoff-flag: sc1 payload -> vmcnt(0) -> flag):
+// agent-scope relaxed stores / loads are the sc1 forms, coherent across the XCDs' L2s without the
+// L2 write-back an agent-scope release fence issues at every level of the climb.
+__device__ __forceinline__ float ld_wt(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ void k_refit(int n, const int* __restrict__ parent_leaf, const int* __restrict__ parent_int,
@@ -287,6 +321,51 @@ __global__ void k_refit(int n, const int* __restrict__ parent_leaf, const int* _
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   int node = parent_leaf[i];
+#if RT_REFIT_WT
+  // the node records of the climb (box, DP costs, DP choices) move by write-through stores and
+  // coherent loads; a climbing thread's stores are complete (vmcnt(0)) before its arrival counts
+  while (node >= 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(&flags[node], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == 0) return;
+    const int c[2] = {child[2 * node], child[2 * node + 1]};
+    float cb[2][6];
+    float4 cd[2];
+    for (int k = 0; k < 2; ++k) {
+      cd[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      if (c[k] >= 0) {
+        const float* p = nbox + (size_t)c[k] * 6;
+        for (int q = 0; q < 6; ++q) cb[k][q] = ld_wt(p + q);
+        if (dpc) {
+          const float* d = (const float*)(dpc + c[k]);
+          cd[k] = make_float4(ld_wt(d), ld_wt(d + 1), ld_wt(d + 2), ld_wt(d + 3));
+        }
+      } else {
+        const float* p = primbox + (size_t)sorted[~c[k]] * 6;
+        for (int q = 0; q < 6; ++q) cb[k][q] = p[q];
+      }
+    }
+    float bb[6];
+    for (int k = 0; k < 3; ++k) {
+      bb[k] = fminf(cb[0][k], cb[1][k]);
+      bb[3 + k] = fmaxf(cb[0][3 + k], cb[1][3 + k]);
+    }
+    float* o = nbox + (size_t)node * 6;
+    for (int k = 0; k < 6; ++k) st_wt(o + k, bb[k]);
+    if (dpc) {
+      float4 dc;
+      uint32_t sj;
+      sah_dp_vals(bb, cd[0], cd[1], dc, sj);
+      float* d = (float*)(dpc + node);
+      st_wt(d, dc.x);
+      st_wt(d + 1, dc.y);
+      st_wt(d + 2, dc.z);
+      st_wt(d + 3, dc.w);
+      dps[node] = sj;  // read only by later kernels
+    }
+    node = parent_int[node];
+  }
+#else
   while (node >= 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -307,6 +386,7 @@ __global__ void k_refit(int n, const int* __restrict__ parent_leaf, const int* _
     if (dpc) sah_dp(node, bb, child[2 * node], child[2 * node + 1], dpc, dps);
     node = parent_int[node];
   }
+#endif
 }
 
 // 6. pack child-pair nodes.
@@ -501,10 +581,39 @@ __global__ void k_dp_expand(int nbin, const BinNode* __restrict__ bin, const flo
   exp[i] = e;
 }
 
+constexpr int kFusedThreads = 1024;
+constexpr int kFusedWaves = kFusedThreads / 64;
+constexpr uint32_t kFusedMax = 8192;  // keys + values, double-buffered in LDS: 128 KiB
+static_assert(RT_FUSED_MAX_N <= kFusedMax, "the one-workgroup build holds at most kFusedMax keys");
+
+// Exclusive prefix sum of one value per thread over the workgroup, in thread order; *total gets
+// the sum. Two barriers (a wave scan by shuffles, then the 16 wave totals through LDS).
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, uint32_t* total) {
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off, 64);
+    x += lane >= (uint32_t)off ? y : 0u;
+  }
+  if (lane == 63u) s_w[w] = x;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < kFusedWaves; ++k) {
+    const uint32_t c = s_w[k];
+    pre += (uint32_t)k < w ? c : 0u;
+    tot += c;
+  }
+  __syncthreads();  // s_w is reused by the next call
+  *total = tot;
+  return pre + x - v;
+}
+
 __global__ __launch_bounds__(1024) void k_collapse(const BinNode* __restrict__ bin, const Exp4* __restrict__ exp,
                                                    Bvh4Node* __restrict__ out,
                                                    int* la, int* lb, int* ps, uint32_t* __restrict__ info) {
-  __shared__ int scan[1024];
+  __shared__ uint32_t s_w[kFusedWaves];
   __shared__ int s_maxstack;
   const int tid = threadIdx.x;
   int* cur = la;
@@ -538,18 +647,11 @@ __global__ __launch_bounds__(1024) void k_collapse(const BinNode* __restrict__ b
           cnt = gather4(bin, cur[i], ref, box);
         }
       }
-      int m = 0;
+      uint32_t m = 0;
       for (int j = 0; j < cnt; ++j) m += ref[j] >= 0;
-      scan[tid] = m;
-      __syncthreads();
-      for (int off = 1; off < 1024; off <<= 1) {
-        const int add = tid >= off ? scan[tid - off] : 0;
-        __syncthreads();
-        scan[tid] += add;
-        __syncthreads();
-      }
-      const int excl = scan[tid] - m;
-      const int chunk_total = scan[1023];
+      uint32_t tot;
+      const int excl = (int)block_excl_scan(m, s_w, &tot);
+      const int chunk_total = (int)tot;
       if (valid) {
         Bvh4Node nd;
         int o = excl;
@@ -605,6 +707,488 @@ __global__ __launch_bounds__(1024) void k_collapse(const BinNode* __restrict__ b
     info[1] = (uint32_t)depth;
     info[2] = (uint32_t)s_maxstack;
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// Fused small-N build: every stage above in ONE 1024-thread workgroup (n <= kFusedMax), the
+// per-stage launches and the device-scope hand-offs replaced by workgroup barriers and LDS.
+// Same arithmetic in the same order as the multi-kernel path, so the tree is bitwise the same:
+//   bounds      the k_bounds reduction (exact min / max)
+//   morton      keys and values straight into LDS
+//   radix sort  4 x 8-bit LSD passes LDS -> LDS; each wave owns a contiguous chunk, ranks its
+//               64 keys per round with 8 ballots; one block scan of the (digit, wave) counts per
+//               pass orders digits, then waves, then rounds, then lanes: stable, like k_rs_*
+//   Karras      from the sorted keys in LDS
+//   refit + DP  the leaf-to-root climb with the arrival counters in LDS (workgroup-scope
+//               atomics: no L2 write-back per level as the agent-scope hand-off of k_refit needs)
+//   pack, DP expansion, collapse (level lists and stack sums in LDS, wave-scan prefix sums)
+//   + the triangle gather into leaf order (BLAS).
+// Teapot (6320 triangles): ~20 launches -> 1.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int delta_lds(const uint32_t* keys, int n, int i, int j) {
+  if (j < 0 || j >= n) return -1;
+  const uint64_t a = ((uint64_t)keys[i] << 32) | (uint32_t)i;
+  const uint64_t b = ((uint64_t)keys[j] << 32) | (uint32_t)j;
+  return __clzll(a ^ b);
+}
+
+// gather4_dp without a local stack (registers only: the one-workgroup build cannot hide scratch
+// latency). A slot is (ref, parent binary node, side); its box is read from the parent afterwards.
+// The expansion is the same recursion in the same left-to-right order: the DP hands a child k of
+// the root's four slots, and a child given k > 1 slots is split as dps chose (0: kept whole).
+struct Slots4 {
+  int ref[4], par[4], side[4];
+  int cnt;
+};
+__device__ __forceinline__ void put_slot(Slots4& s, int ref, int par, int side) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (s.cnt == q) {
+      s.ref[q] = ref;
+      s.par[q] = par;
+      s.side[q] = side;
+    }
+  ++s.cnt;
+}
+template <int K>
+__device__ __forceinline__ void expand_slots(const BinNode* __restrict__ bin, const uint32_t* __restrict__ dps, int c,
+                                             int par, int side, Slots4& s) {
+  if (K == 1 || c < 0) {
+    put_slot(s, c, par, side);
+    return;
+  }
+  const uint32_t j = (dps[c] >> (8 * (K - 1))) & 0xffu;
+  if (j == 0) {
+    put_slot(s, c, par, side);
+    return;
+  }
+  const int2 g = *reinterpret_cast<const int2*>(&bin[c].c0);
+  if (K == 2) {
+    expand_slots<1>(bin, dps, g.x, c, 0, s);
+    expand_slots<1>(bin, dps, g.y, c, 1, s);
+  } else if (j == 1) {
+    expand_slots<1>(bin, dps, g.x, c, 0, s);
+    expand_slots<(K > 2 ? K - 1 : 1)>(bin, dps, g.y, c, 1, s);
+  } else {
+    expand_slots<(K > 2 ? K - 1 : 1)>(bin, dps, g.x, c, 0, s);
+    expand_slots<1>(bin, dps, g.y, c, 1, s);
+  }
+}
+
+// The wide node rooted at binary node `root` (gather4_dp + the k_dp_expand slot order), in registers.
+__device__ __forceinline__ int wide_slots_dp(const BinNode* __restrict__ bin, const float4* __restrict__ dpc,
+                                             const uint32_t* __restrict__ dps, int root, int ref[4], float box[4][6]) {
+  const int2 rc = *reinterpret_cast<const int2*>(&bin[root].c0);
+  const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  const float4 l = rc.x >= 0 ? dpc[rc.x] : zero, r = rc.y >= 0 ? dpc[rc.y] : zero;
+  const float cl[4] = {l.x, l.y, l.z, l.w}, cr[4] = {r.x, r.y, r.z, r.w};
+  int bj = 1;
+  float bc = INFINITY;
+#pragma unroll
+  for (int j = 1; j < 4; ++j) {
+    const float c = cl[j - 1] + cr[4 - j - 1];
+    if (c < bc) {
+      bc = c;
+      bj = j;
+    }
+  }
+  Slots4 s;
+  s.cnt = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) s.ref[q] = s.par[q] = s.side[q] = 0;
+  if (bj == 1) {
+    expand_slots<1>(bin, dps, rc.x, root, 0, s);
+    expand_slots<3>(bin, dps, rc.y, root, 1, s);
+  } else if (bj == 2) {
+    expand_slots<2>(bin, dps, rc.x, root, 0, s);
+    expand_slots<2>(bin, dps, rc.y, root, 1, s);
+  } else {
+    expand_slots<3>(bin, dps, rc.x, root, 0, s);
+    expand_slots<1>(bin, dps, rc.y, root, 1, s);
+  }
+  float a[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    ref[q] = s.ref[q];
+    const BinNode& pb = bin[s.par[q]];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      box[q][k] = q < s.cnt ? (s.side[q] ? pb.lo1[k] : pb.lo0[k]) : 0.0f;
+      box[q][3 + k] = q < s.cnt ? (s.side[q] ? pb.hi1[k] : pb.hi0[k]) : 0.0f;
+    }
+    a[q] = half_area6(box[q]);
+  }
+  // ascending half area, stable (k_dp_expand's insertion sort with every comparison unrolled: once
+  // an element stops, the comparisons below it find the prefix sorted and swap nothing)
+#pragma unroll
+  for (int x = 1; x < 4; ++x)
+#pragma unroll
+    for (int y = x; y > 0; --y)
+      if (x < s.cnt && a[y] < a[y - 1]) {
+        const float ta = a[y];
+        a[y] = a[y - 1];
+        a[y - 1] = ta;
+        const int tr = ref[y];
+        ref[y] = ref[y - 1];
+        ref[y - 1] = tr;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          const float t = box[y][q];
+          box[y][q] = box[y - 1][q];
+          box[y - 1][q] = t;
+        }
+      }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (j >= s.cnt) ref[j] = kEmptyChild;
+  return s.cnt;
+}
+
+__global__ __launch_bounds__(kFusedThreads) void k_build_small(
+    const float* __restrict__ primbox, uint32_t n, bool leaf_ref_is_prim, uint32_t* __restrict__ sorted,
+    float* __restrict__ cb_out, int* __restrict__ child, int* __restrict__ pint, int* __restrict__ pleaf,
+    float* nbox, float4* dpc, uint32_t* dps, BinNode* bin, Exp4* expd, Bvh4Node* __restrict__ out,
+    uint32_t* __restrict__ info, const TriRec* __restrict__ tri_in, TriRec* __restrict__ tri_out) {
+  // LDS: sort buffers (keys A | values A | keys B | values B) + (digit, wave) counts; later
+  // phases reuse the same words: arrival flags (refit), level lists and stack sums (collapse)
+  __shared__ uint32_t s_mem[4 * kFusedMax + 256 * kFusedWaves];
+  __shared__ float s_red[12][kFusedWaves];
+  __shared__ float s_cb[12];
+  __shared__ uint32_t s_w[kFusedWaves];
+  __shared__ int s_maxstack;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+#if RT_BUILD_TIMING
+  uint64_t bt[9];
+  bt[0] = __builtin_amdgcn_s_memtime();
+#define RT_BT(k) bt[k] = __builtin_amdgcn_s_memtime()
+#else
+#define RT_BT(k) (void)0
+#endif
+  uint32_t* keyA = s_mem;
+  uint32_t* valA = s_mem + kFusedMax;
+  uint32_t* keyB = s_mem + 2 * kFusedMax;
+  uint32_t* valB = s_mem + 3 * kFusedMax;
+  uint32_t* cnt = s_mem + 4 * kFusedMax;  // [digit][wave]
+
+  // 1. bounds (k_bounds)
+  {
+    float v[12];
+    for (int k = 0; k < 3; ++k) {
+      v[k] = INFINITY;
+      v[3 + k] = -INFINITY;
+      v[6 + k] = INFINITY;
+      v[9 + k] = -INFINITY;
+    }
+    for (uint32_t i = tid; i < n; i += kFusedThreads) {
+      const float* b = primbox + (size_t)i * 6;
+      for (int k = 0; k < 3; ++k) {
+        const float c = (b[k] + b[3 + k]) * 0.5f;
+        v[k] = fminf(v[k], c);
+        v[3 + k] = fmaxf(v[3 + k], c);
+        v[6 + k] = fminf(v[6 + k], b[k]);
+        v[9 + k] = fmaxf(v[9 + k], b[3 + k]);
+      }
+    }
+    for (int off = 32; off >= 1; off >>= 1)
+      for (int k = 0; k < 12; ++k) {
+        const float o = __shfl_xor(v[k], off, 64);
+        v[k] = (k % 6) < 3 ? fminf(v[k], o) : fmaxf(v[k], o);
+      }
+    if (lane == 0)
+      for (int k = 0; k < 12; ++k) s_red[k][w] = v[k];
+    __syncthreads();
+    if (tid < 12) {
+      const int k = (int)tid;
+      float r = s_red[k][0];
+      for (int j = 1; j < kFusedWaves; ++j) r = (k % 6) < 3 ? fminf(r, s_red[k][j]) : fmaxf(r, s_red[k][j]);
+      s_cb[k] = r;
+      cb_out[k] = r;
+    }
+    __syncthreads();
+  }
+  RT_BT(1);
+  // 2. Morton codes (k_morton)
+  for (uint32_t i = tid; i < n; i += kFusedThreads) {
+    const float* b = primbox + (size_t)i * 6;
+    uint32_t q[3];
+    for (int k = 0; k < 3; ++k) {
+      const float ext = s_cb[3 + k] - s_cb[k];
+      const float inv = ext > 0.0f ? 1.0f / ext : 0.0f;
+      const float c = (b[k] + b[3 + k]) * 0.5f;
+      q[k] = quantize10(c, s_cb[k], inv);
+    }
+    keyA[i] = (expand_bits10(q[0]) << 2) | (expand_bits10(q[1]) << 1) | expand_bits10(q[2]);
+    valA[i] = i;
+  }
+  // 3. radix sort, 4 passes: A -> B -> A -> B -> A
+  {
+    const uint32_t chunk = (((n + kFusedWaves - 1) / kFusedWaves) + 63u) & ~63u;  // keys per wave
+    const uint32_t c0 = w * chunk, c1 = min(c0 + chunk, n);
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64u - lane));
+    uint32_t *kin = keyA, *vin = valA, *kout = keyB, *vout = valB;
+    for (int pass = 0; pass < 4; ++pass) {
+      const int shift = pass * 8;
+      for (uint32_t k = tid; k < 256u * kFusedWaves; k += kFusedThreads) cnt[k] = 0;
+      __syncthreads();
+      // counts of each digit in this wave's chunk (one writer per (digit, wave): the rank-0 lane)
+      for (uint32_t b = c0; b < c1; b += 64) {
+        const uint32_t i = b + lane;
+        const bool valid = i < c1;
+        const uint32_t digit = valid ? (kin[i] >> shift) & 255u : 0u;
+        uint64_t peers = __ballot(valid);
+        for (int q = 0; q < 8; ++q) {
+          const bool bit = (digit >> q) & 1u;
+          const uint64_t m = __ballot(valid && bit);
+          peers &= bit ? m : ~m;
+        }
+        if (valid && (peers & lt) == 0) cnt[digit * kFusedWaves + w] += (uint32_t)__popcll(peers);
+      }
+      __syncthreads();
+      // exclusive scan over (digit, wave): 4 consecutive entries per thread
+      {
+        uint32_t e[4], s = 0;
+        for (int q = 0; q < 4; ++q) {
+          e[q] = cnt[tid * 4 + q];
+          s += e[q];
+        }
+        uint32_t tot;
+        uint32_t run = block_excl_scan(s, s_w, &tot);
+        for (int q = 0; q < 4; ++q) {
+          cnt[tid * 4 + q] = run;
+          run += e[q];
+        }
+      }
+      __syncthreads();
+      // stable scatter: the wave's rounds in order, lanes in order within a round
+      for (uint32_t b = c0; b < c1; b += 64) {
+        const uint32_t i = b + lane;
+        const bool valid = i < c1;
+        const uint32_t key = valid ? kin[i] : 0u, val = valid ? vin[i] : 0u;
+        const uint32_t digit = (key >> shift) & 255u;
+        uint64_t peers = __ballot(valid);
+        for (int q = 0; q < 8; ++q) {
+          const bool bit = (digit >> q) & 1u;
+          const uint64_t m = __ballot(valid && bit);
+          peers &= bit ? m : ~m;
+        }
+        const uint32_t rank = (uint32_t)__popcll(peers & lt);
+        const uint32_t base = valid ? cnt[digit * kFusedWaves + w] : 0u;  // every lane reads before the update
+        if (valid) {
+          kout[base + rank] = key;
+          vout[base + rank] = val;
+        }
+        if (valid && rank == 0) cnt[digit * kFusedWaves + w] = base + (uint32_t)__popcll(peers);
+      }
+      __syncthreads();
+      uint32_t* t = kin;
+      kin = kout;
+      kout = t;
+      t = vin;
+      vin = vout;
+      vout = t;
+    }
+  }
+  RT_BT(2);
+  // sorted permutation (values A) out; Karras from keys A
+  for (uint32_t i = tid; i < n; i += kFusedThreads) sorted[i] = valA[i];
+  __syncthreads();  // values A and buffers B take the hierarchy: parents of internal nodes, children
+  int* s_pint = (int*)s_mem + kFusedMax;
+  int* s_child = (int*)s_mem + 2 * kFusedMax;
+  if (n == 1) {
+    if (tid == 0) {  // k_single
+      BinNode nd;
+      for (int k = 0; k < 3; ++k) {
+        nd.lo0[k] = nd.lo1[k] = primbox[k];
+        nd.hi0[k] = nd.hi1[k] = primbox[3 + k];
+      }
+      nd.c0 = ~0;
+      nd.c1 = kEmptyChild;
+      nd.pad0 = nd.pad1 = 0;
+      bin[0] = nd;
+    }
+  } else {
+    // 4. Karras (k_karras)
+    for (int i = (int)tid; i < (int)n - 1; i += kFusedThreads) {
+      const int nn = (int)n;
+      const int d = (delta_lds(keyA, nn, i, i + 1) - delta_lds(keyA, nn, i, i - 1)) >= 0 ? 1 : -1;
+      const int dmin = delta_lds(keyA, nn, i, i - d);
+      int lmax = 2;
+      while (delta_lds(keyA, nn, i, i + lmax * d) > dmin) lmax <<= 1;
+      int l = 0;
+      for (int t = lmax >> 1; t >= 1; t >>= 1)
+        if (delta_lds(keyA, nn, i, i + (l + t) * d) > dmin) l += t;
+      const int j = i + l * d;
+      const int dnode = delta_lds(keyA, nn, i, j);
+      int s = 0, t = l;
+      while (true) {
+        t = (t + 1) >> 1;
+        if (delta_lds(keyA, nn, i, i + (s + t) * d) > dnode) s += t;
+        if (t <= 1) break;
+      }
+      const int gamma = i + s * d + (d < 0 ? d : 0);
+      const int lo = i < j ? i : j, hi = i < j ? j : i;
+      const int left = (lo == gamma) ? ~gamma : gamma;
+      const int right = (hi == gamma + 1) ? ~(gamma + 1) : gamma + 1;
+      s_child[2 * i] = left;
+      s_child[2 * i + 1] = right;
+      if (left >= 0) s_pint[left] = i; else pleaf[~left] = i;
+      if (right >= 0) s_pint[right] = i; else pleaf[~right] = i;
+      if (i == 0) s_pint[0] = -1;
+    }
+  RT_BT(3);
+    __syncthreads();  // keys no longer needed: the arrival flags take their words
+    uint32_t* flags = s_mem;
+    for (uint32_t i = tid; i < n - 1; i += kFusedThreads) flags[i] = 0;
+    __syncthreads();
+    // 5. refit + collapse DP (k_refit): the second arrival at a node computes it. Hand-off inside
+    // the workgroup: the child's box / DP stores complete (vmcnt(0)), then the LDS counter.
+    for (uint32_t i = tid; i < n; i += kFusedThreads) {
+      int node = pleaf[i];
+      while (node >= 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t old = __hip_atomic_fetch_add(&flags[node], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (old == 0) break;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        float a[6], b[6];
+        const int ca = s_child[2 * node], cbb = s_child[2 * node + 1];
+        load_box(ca, nbox, primbox, sorted, a);
+        load_box(cbb, nbox, primbox, sorted, b);
+        float bb[6];
+        for (int k = 0; k < 3; ++k) {
+          bb[k] = fminf(a[k], b[k]);
+          bb[3 + k] = fmaxf(a[3 + k], b[3 + k]);
+        }
+        float* o = nbox + (size_t)node * 6;
+        for (int k = 0; k < 6; ++k) o[k] = bb[k];
+        if (dpc) sah_dp(node, bb, ca, cbb, dpc, dps);
+        node = s_pint[node];
+      }
+    }
+    __syncthreads();
+  RT_BT(4);
+    // 6. pack (k_pack)
+    for (int i = (int)tid; i < (int)n - 1; i += kFusedThreads) {
+      BinNode nd;
+      int c[2] = {s_child[2 * i], s_child[2 * i + 1]};
+      float b[2][6];
+      for (int k = 0; k < 2; ++k) load_box(c[k], nbox, primbox, sorted, b[k]);
+      for (int k = 0; k < 3; ++k) {
+        nd.lo0[k] = b[0][k];
+        nd.hi0[k] = b[0][3 + k];
+        nd.lo1[k] = b[1][k];
+        nd.hi1[k] = b[1][3 + k];
+      }
+      for (int k = 0; k < 2; ++k)
+        if (c[k] < 0 && leaf_ref_is_prim) c[k] = ~(int)sorted[~c[k]];
+      nd.c0 = c[0];
+      nd.c1 = c[1];
+      nd.pad0 = nd.pad1 = 0;
+      bin[i] = nd;
+    }
+  }
+  __syncthreads();
+  RT_BT(5);
+  RT_BT(6);
+  // 8. collapse into BFS-ordered 4-wide nodes (k_collapse); level lists and stack sums in LDS
+  {
+    int* cur = (int*)s_mem;
+    int* nxt = (int*)s_mem + kFusedMax;
+    int* ps = (int*)s_mem + 2 * kFusedMax;
+    if (tid == 0) {
+      cur[0] = 0;
+      ps[0] = 0;
+      s_maxstack = 0;
+    }
+    __syncthreads();
+    int lmax = 0, cur_n = 1, base = 0, depth = 0;
+    while (cur_n > 0) {
+      ++depth;
+      int next_total = 0;
+      for (int cs = 0; cs < cur_n; cs += kFusedThreads) {
+        const int i = cs + (int)tid;
+        const bool valid = i < cur_n;
+        int ref[4];
+        float box[4][6];
+        int cnt4 = 0;
+        if (valid) {
+          if (dpc)  // the DP expansion of this wide node's root, in registers (no k_dp_expand pass)
+            cnt4 = wide_slots_dp(bin, dpc, dps, cur[i], ref, box);
+          else
+            cnt4 = gather4(bin, cur[i], ref, box);
+        }
+        uint32_t m = 0;
+        for (int j = 0; j < cnt4; ++j) m += ref[j] >= 0;
+        uint32_t chunk_total;
+        const int excl = (int)block_excl_scan(m, s_w, &chunk_total);
+        if (valid) {
+          Bvh4Node nd;
+          int o = excl;
+          const int below = ps[base + i] + cnt4 - 1;
+          lmax = below > lmax ? below : lmax;
+          uint32_t nvalid = 0, inner = 0;
+          nd.first_inner = 0;
+          for (int j = 0; j < 4; ++j) {
+            const float inf = __builtin_inff();
+            float b6[6] = {inf, inf, inf, inf, inf, inf};
+            int32_t r = kEmptyChild;
+            if (j < cnt4 && ref[j] != kEmptyChild) {
+              ++nvalid;
+              for (int a = 0; a < 6; ++a) b6[a] = box[j][a];
+              if (ref[j] >= 0) {
+                const int pos = next_total + o;
+                nxt[pos] = ref[j];
+                r = base + cur_n + pos;
+                ps[r] = below;
+                if (o == excl) nd.first_inner = r;
+                inner |= 1u << j;
+                ++o;
+              } else {
+                r = ref[j];
+              }
+            }
+            nd.lox[j] = b6[0];
+            nd.loy[j] = b6[1];
+            nd.loz[j] = b6[2];
+            nd.hix[j] = b6[3];
+            nd.hiy[j] = b6[4];
+            nd.hiz[j] = b6[5];
+            nd.child[j] = r;
+          }
+          nd.count = nvalid;
+          nd.inner_mask = inner;
+          nd.entry_base = ((uint32_t)nd.first_inner << 8) | (inner << 4);
+          out[base + i] = nd;
+        }
+        next_total += (int)chunk_total;
+      }
+      __syncthreads();  // the next level reads nxt / ps
+      int* t = cur;
+      cur = nxt;
+      nxt = t;
+      base += cur_n;
+      cur_n = next_total;
+    }
+    atomicMax(&s_maxstack, lmax);
+    __syncthreads();
+    if (tid == 0) {
+      info[0] = (uint32_t)base;
+      info[1] = (uint32_t)depth;
+      info[2] = (uint32_t)s_maxstack;
+    }
+  }
+  RT_BT(7);
+  // 9. triangles into leaf order (k_tri_reorder)
+  if (tri_in)
+    for (uint32_t i = tid; i < n; i += kFusedThreads) tri_out[i] = tri_in[sorted[i]];
+#if RT_BUILD_TIMING
+  RT_BT(8);
+  if (tid == 0)
+    printf("k_build_small n=%u cycles: bounds %lu morton+sort %lu karras %lu refit %lu pack %lu dpexp %lu collapse %lu reorder %lu\n",
+           n, bt[1] - bt[0], bt[2] - bt[1], bt[3] - bt[2], bt[4] - bt[3], bt[5] - bt[4], bt[6] - bt[5], bt[7] - bt[6],
+           bt[8] - bt[7]);
+#endif
+#undef RT_BT
 }
 
 __global__ void k_tri_setup(const float* __restrict__ vtx, const uint32_t* __restrict__ idx,
@@ -678,7 +1262,7 @@ struct DevBuf {
 
 hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uint32_t* d_sorted,
                       bool leaf_ref_is_prim, uint32_t* node_count, uint32_t* depth, uint32_t* max_stack,
-                      float bounds[6], float* build_ms, hipStream_t s) {
+                      float bounds[6], float* build_ms, hipStream_t s, const TriRec* d_tri_in, TriRec* d_tri_out) {
   if (n == 0) return hipErrorInvalidValue;
   const uint32_t nblocks = (n + kRsTile - 1) / kRsTile;
   const uint32_t nbin = n > 1 ? n - 1 : 1;
@@ -716,6 +1300,13 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
   RT_TRY(hipEventCreate(&e1));
   RT_TRY(hipEventRecord(e0, s));
   float* cb = (float*)stats.p;
+  if (RT_FUSED_BUILD && n <= (uint32_t)RT_FUSED_MAX_N) {
+    k_build_small<<<1, kFusedThreads, 0, s>>>(d_primbox, n, leaf_ref_is_prim, d_sorted, cb, (int*)child.p,
+                                              (int*)pint.p, (int*)pleaf.p, (float*)nbox.p, (float4*)dpc.p,
+                                              (uint32_t*)dps.p, (BinNode*)bin.p, (Exp4*)expd.p, d_nodes,
+                                              (uint32_t*)info.p, d_tri_in, d_tri_out);
+    RT_TRY(hipGetLastError());
+  } else {
   k_bounds<<<1, 1024, 0, s>>>(d_primbox, n, cb);
   RT_TRY(hipGetLastError());
   uint32_t* ka = (uint32_t*)keys0.p;
@@ -756,6 +1347,11 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
   k_collapse<<<1, 1024, 0, s>>>(d_bin, (const Exp4*)expd.p, d_nodes, (int*)la.p, (int*)lb.p, (int*)ps.p,
                                 (uint32_t*)info.p);
   RT_TRY(hipGetLastError());
+  if (d_tri_in) {
+    k_tri_reorder<<<grid1(n, 256), 256, 0, s>>>(d_tri_in, d_sorted, n, d_tri_out);
+    RT_TRY(hipGetLastError());
+  }
+  }
   RT_TRY(hipEventRecord(e1, s));
   float hb[12];
   uint32_t hinfo[3];

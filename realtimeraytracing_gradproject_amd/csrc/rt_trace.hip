@@ -1258,10 +1258,13 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void k_trace_frame(SceneView 
 #define RT_LS_WAVES 7
 #endif
 #ifndef RT_SPP_WAVES
-#define RT_SPP_WAVES 5  // the sample-loop kernel (KS = 0) needs ~95 VGPRs: 5 waves spill nothing
+#define RT_SPP_WAVES 4  // the sample-loop kernel (KS = 0, e.g. spp 9) needs 97 VGPRs: 4 waves spill nothing
 #endif
 #ifndef RT_KS_WAVES
 #define RT_KS_WAVES RT_LS_WAVES  // the sample-lane kernels (KS = 2, 4)
+#endif
+#ifndef RT_REF_WAVES
+#define RT_REF_WAVES 1  // REF (MODE 0) one-sample kernel: 1 = the allocator's choice
 #endif
 #ifndef RT_PACKET_WX
 #define RT_PACKET_WX 2  // waves of a packet workgroup along x
@@ -1276,14 +1279,16 @@ constexpr int kPacketBlock = 64 * RT_PACKET_WX * RT_PACKET_WY;
 
 template <int MODE, bool STATS, int R, int KS>
 __global__ __launch_bounds__(kPacketBlock) __attribute__((amdgpu_waves_per_eu(
-    (MODE == 1 && !STATS) ? (KS == 0 ? RT_SPP_WAVES : (KS == 1 ? RT_LS_WAVES : RT_KS_WAVES)) : 1)))
+    (MODE == 1 && !STATS) ? (KS == 0 ? RT_SPP_WAVES : (KS == 1 ? RT_LS_WAVES : RT_KS_WAVES))
+                          : ((MODE == 0 && !STATS && KS == 1) ? RT_REF_WAVES : 1))))
 void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restrict__ rows,
                           uint32_t* __restrict__ rgba8, float4* __restrict__ rgba32f,
                           unsigned long long* __restrict__ stats) {
   static_assert(KS <= 1 || R == 1, "sample lanes need one ray per lane");
   constexpr uint32_t NS = KS > 1 ? KS * KS : 1;  // samples of a pixel held by consecutive lanes
   constexpr uint32_t TP = KS > 1 ? 8 / KS : 8;    // tile side in pixels
-  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  // the wave index is uniform: an SGPR, so the pixel of a lane can be re-derived from its lane id
+  const uint32_t lane = threadIdx.x & 63u, w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t sample = lane % NS, pix = lane / NS;
   const uint32_t x = blockIdx.x * (TP * RT_PACKET_WX) + (w % RT_PACKET_WX) * TP + (pix % TP);
   uint32_t px[R], py[R], out[R];  // out: the pixel's output index, ~0 when this lane stores nothing
@@ -1319,6 +1324,10 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
       sum = add(sum, v3(__shfl(col[0].x, base + q, 64), __shfl(col[0].y, base + q, 64),
                         __shfl(col[0].z, base + q, 64)));
     acc[0] = sum;
+    // the store index too (not kept live across the traces: the 7-wave budget has no VGPR to spare)
+    const uint32_t xp = lid / NS, xx = blockIdx.x * (TP * RT_PACKET_WX) + (w % RT_PACKET_WX) * TP + (xp % TP);
+    const uint32_t orow = blockIdx.y * (TP * RT_PACKET_WY) + (w / RT_PACKET_WX) * TP + xp / TP;
+    out[0] = (xx < fp.width && orow < fp.nrows && (lid % NS) == 0u) ? orow * fp.width + xx : 0xffffffffu;
   } else {
     for (uint32_t sy = 0; sy < k; ++sy)
       for (uint32_t sx = 0; sx < k; ++sx) {

@@ -78,7 +78,8 @@ def test_blas_bitwise_equal_to_oracle(model):
     c.close()
 
 
-@pytest.mark.parametrize("ntri", [1, 2, 3, 7, 1000, 1025, 5000])
+# <= 8192: the one-workgroup build (k_build_small); 8193 and 20000: the multi-kernel build
+@pytest.mark.parametrize("ntri", [1, 2, 3, 7, 63, 64, 65, 1000, 1025, 5000, 8191, 8192, 8193, 20000])
 def test_blas_edge_sizes(ntri):
     rng = np.random.default_rng(1234 + ntri)
     v = np.zeros((ntri * 3, 6), np.float32)
@@ -107,11 +108,13 @@ def test_blas_degenerate_geometry(mesh):
     c.close()
 
 
-def test_blas_duplicate_centroids():
-    # many triangles with identical Morton codes: Karras tie-break on leaf position
-    v = np.zeros((300 * 3, 6), np.float32)
+@pytest.mark.parametrize("count", [300, 3000, 9000])
+def test_blas_duplicate_centroids(count):
+    # many triangles with identical Morton codes: Karras tie-break on leaf position; the sort must
+    # stay stable across waves (3000) and across the fused / multi-kernel builds (9000)
+    v = np.zeros((count * 3, 6), np.float32)
     base = np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0]], np.float32)
-    for k in range(300):
+    for k in range(count):
         v[k * 3:(k + 1) * 3, :3] = base
     c = fresh_ctx()
     b = c.blas_build(v)
@@ -127,6 +130,30 @@ def test_blas_duplicate_centroids():
 def test_tlas_bitwise_equal_to_oracle(name):
     spec = scenes.config(name)
     c, o = load_both(spec)
+    assert np.array_equal(c.tlas_export(), o.export_tlas())
+    info = c.tlas_info()
+    assert (info.prim_count, info.node_count, info.depth, info.max_stack) == tuple(o.tlas_info())
+    c.close()
+
+
+@pytest.mark.parametrize("ninst", [1, 3, 1024, 8192, 9000])
+def test_tlas_instance_counts(ninst):
+    # TLAS over ninst instances of one small mesh at seeded translations / rotations (coincident
+    # boxes included): fused (<= 8192) and multi-kernel (9000) builds against the oracle
+    rng = np.random.default_rng(ninst)
+    v = np.array([[0, 0, 0, 0, 1, 0], [1, 0, 0, 0, 1, 0], [0, 1, 0, 0, 1, 0],
+                  [0, 0, 1, 0, 1, 0], [1, 1, 1, 0, 1, 0], [0, 1, 1, 0, 1, 0]], np.float32)
+    inst = []
+    for k in range(ninst):
+        t = rng.integers(-40, 40, size=3).astype(np.float64) * 0.5
+        x = scenes._rot_scale((0.0, 1.0, 0.0), float(k % 90) if k % 3 == 1 else 0.0, (1.0, 1.0, 1.0), t)
+        inst.append((0, x, k, 0))
+    c = fresh_ctx()
+    b = c.blas_build(v)
+    c.tlas_build([(b, x, iid, hg) for (_, x, iid, hg) in inst])
+    o = oracle.Scene()
+    ob = o.add_blas(v)
+    o.set_instances([(ob, x, iid, hg) for (_, x, iid, hg) in inst])
     assert np.array_equal(c.tlas_export(), o.export_tlas())
     info = c.tlas_info()
     assert (info.prim_count, info.node_count, info.depth, info.max_stack) == tuple(o.tlas_info())
