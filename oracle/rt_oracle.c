@@ -408,6 +408,9 @@ static int gather4_dp(const onode* bin, int root, int ref[4], float box[4][6]) {
 /* collapse the binary tree into 4-wide nodes (SAH DP, or greedy largest-area opening), BFS order
  * (k_collapse) */
 static uint32_t collapse(const onode* bin, uint32_t nbin, o4node* out, uint32_t* count, uint32_t* max_stack) {
+#ifdef OSTUDY_BIN_HOOK /* design studies only (tools/wide_study.c): a copy of the binary tree */
+  OSTUDY_BIN_HOOK(bin, nbin);
+#endif
   if (dp_on < 0) dp_on = getenv("ORACLE_GREEDY_COLLAPSE") == NULL;
   if (dp_on) dp_prepare(bin, nbin);
   int* q = (int*)malloc((size_t)nbin * sizeof(int) + sizeof(int));
@@ -961,7 +964,11 @@ static int opk_node(const o4node* nd, const opkray* ry, float tmin, ohit* h, int
   uint32_t kb = key[0];
   int rb = nd->child[0], ib = 0;
   if (any) {
+#ifdef OANY_CHOOSE /* design studies only (tools/anyhit_study.c): another any-hit child order */
+    ib = OANY_CHOOSE(ent, vkey, *lead, hm, live, nd, tmin);
+#else
     ib = __builtin_ctz(ent);
+#endif
     rb = nd->child[ib];
   } else {
     for (int k = 1; k < 4; ++k)

@@ -53,6 +53,9 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 typedef int i4v __attribute__((ext_vector_type(4)));
 typedef int i8v __attribute__((ext_vector_type(8)));
 typedef float f8v __attribute__((ext_vector_type(8)));
+#ifndef RT_ANY_MT_BITS
+#define RT_ANY_MT_BITS 0  // any-hit triangle tests with the bitwise acceptance (A/B knob)
+#endif
 #ifndef RT_PACKET_OCT
 #define RT_PACKET_OCT 1  // uniform-octant BLAS walks load near/far planes directly (no min/max pairs)
 #endif
@@ -403,8 +406,11 @@ __device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref
   for (int r = 0; r < R; ++r) {
     if (STATS && ray_live(hit[r])) ++cnt.tri;
     float t, u, v;
-    const bool ok = moller_trumbore_flat(ry.o[r], ry.d[r], v3(ta.x, ta.y, ta.z), v3(tb.x, tb.y, tb.z),
-                                         v3(tc.x, tc.y, tc.z), face, t, u, v);
+    const bool ok = (ANY_HIT && RT_ANY_MT_BITS)
+                        ? moller_trumbore_bits(ry.o[r], ry.d[r], v3(ta.x, ta.y, ta.z), v3(tb.x, tb.y, tb.z),
+                                               v3(tc.x, tc.y, tc.z), face, t, u, v)
+                        : moller_trumbore_flat(ry.o[r], ry.d[r], v3(ta.x, ta.y, ta.z), v3(tb.x, tb.y, tb.z),
+                                               v3(tc.x, tc.y, tc.z), face, t, u, v);
     HitRec& h = hit[r];
     // bitwise & / | (no short-circuit): no exec-mask branches around the compares (-2 %)
     // a ray that is not live has t = -inf and takes nothing; a live any-hit ray still holds
@@ -558,12 +564,14 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
     uint32_t vkey[R][4];
     f4v planes[6];
     if (OCT) {
-      planes[0] = cld4(nb + oc.nx);
-      planes[1] = cld4(nb + oc.fx);
-      planes[2] = cld4(nb + oc.ny);
-      planes[3] = cld4(nb + oc.fy);
-      planes[4] = cld4(nb + oc.nz);
-      planes[5] = cld4(nb + oc.fz);
+      // one 32-bit offset per row: the scalar load takes it as its SGPR offset (no 64-bit adds)
+      const uint32_t noff = (uint32_t)bref << 7;
+      planes[0] = cld4(pool + (noff + oc.nx));
+      planes[1] = cld4(pool + (noff + oc.fx));
+      planes[2] = cld4(pool + (noff + oc.ny));
+      planes[3] = cld4(pool + (noff + oc.fy));
+      planes[4] = cld4(pool + (noff + oc.nz));
+      planes[5] = cld4(pool + (noff + oc.fz));
     } else {
 #pragma unroll
       for (int q = 0; q < 6; ++q) planes[q] = cld4(nb + 16 * q);
@@ -1046,10 +1054,23 @@ __device__ bool shadow_compact(const SceneView& sc, V3 P, V3 d, bool need, uint3
 // shade_sample for the wave-packet traversal: identical arithmetic per ray, with every trace
 // hoisted to wave-uniform control flow (rays without a trace of that kind join the packet dead).
 // Each lane shades R camera samples (R pixels) at once.
+#ifndef RT_KO_SHADE
+#define RT_KO_SHADE 0  // knock-out studies (tools/ab.py --no-check): never in a shipped build
+#endif
+#ifndef RT_KO_SHADOW
+#define RT_KO_SHADOW 0
+#endif
+#ifndef RT_PHASE_TIMING
+#define RT_PHASE_TIMING 0  // 1: sampled waves printf s_memtime per phase (diagnostics only)
+#endif
 template <int MODE, bool STATS, int R>
 __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, const uint32_t* px,
                                     const uint32_t* py, float ox, float oy, const bool* inimg, V3* color,
                                     Counters& cnt) {
+#if RT_PHASE_TIMING
+  uint64_t ph[6];
+  ph[0] = __builtin_amdgcn_s_memtime();
+#endif
   V3 O[R], D[R], P[R], sd[R];
   HitRec hit[R], sh[R];
   bool found[R], occl[R], need[R];
@@ -1146,6 +1167,9 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
     }
   }
   // RT_SHADE_LAMBERT_SHADOW (MODE 1) and RT_SHADE_PRIMARY (MODE 2)
+#if RT_PHASE_TIMING
+  ph[1] = __builtin_amdgcn_s_memtime();
+#endif
   V3 n[R];
   float c[R];
 #pragma unroll
@@ -1153,11 +1177,24 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
     n[r] = v3(0.0f, 0.0f, 0.0f);
     c[r] = 0.0f;
     if (found[r]) {
+#if RT_KO_SHADE  // knock-out study only (wrong image): no hit-instance / vertex fetches
+      n[r] = neg(D[r]);
+#else
       const HitInstance ir = load_hit_instance(sc, hit[r].inst);
       n[r] = ir.hit_group == 2u ? face_world_normal(ir, hit[r].prim)
                                 : neg(interpolated_world_normal(ir, hit[r].prim, hit[r].u, hit[r].v));
+#endif
     }
   }
+#if RT_PHASE_TIMING
+  {
+    float z = 0.0f;
+#pragma unroll
+    for (int r = 0; r < R; ++r) z += n[r].x;
+    asm volatile("" ::"v"(z));  // the normals are complete here
+    ph[2] = __builtin_amdgcn_s_memtime();
+  }
+#endif
   for (uint32_t l = 0; l < fp.nlights; ++l) {
     const LightRec& Lr = fp.lights[l];
     float nl[R];
@@ -1170,7 +1207,7 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
       occl[r] = false;
       if (MODE == 1 && STATS && need[r]) ++cnt.shadow;
     }
-    if (MODE == 1) {
+    if (MODE == 1 && !RT_KO_SHADOW) {
       if (RT_SHADOW_COMPACT && R == 1)
         occl[0] = shadow_compact<STATS>(sc, P[0], sd[0], need[0], l & 1u, cnt);
       else
@@ -1186,6 +1223,11 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
     const float v = c[r] / (float)fp.nlights;
     color[r] = found[r] ? v3(v, v, v) : miss_color(fp, py[r]);
   }
+#if RT_PHASE_TIMING
+  ph[3] = __builtin_amdgcn_s_memtime();
+  if ((threadIdx.x & 63u) == 0 && (blockIdx.x * 7u + blockIdx.y * 13u) % 61u == 0u)
+    printf("PH %lu %lu %lu\n", ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2]);
+#endif
 }
 
 // WAVE_FETCH: the fetch counters are wave-uniform (packet schedule) and count once per wave.
