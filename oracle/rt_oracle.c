@@ -376,6 +376,16 @@ static void dp_expand(const onode* bin, int c, const float* cbox, int k, int* re
   dp_expand(bin, b->c1, r, k - j, ref, box, cnt);
 }
 
+/* BLAS: internal children first, stable (inner_first in rt_lbvh.hip); no visit order changes */
+static void oinner_first(int cnt, int* ref, float (*box)[6]) {
+  for (int x = 1; x < cnt; ++x)
+    for (int y = x; y > 0 && ref[y] >= 0 && ref[y - 1] < 0; --y) {
+      int tr = ref[y]; ref[y] = ref[y - 1]; ref[y - 1] = tr;
+      float tb[6];
+      memcpy(tb, box[y], 24); memcpy(box[y], box[y - 1], 24); memcpy(box[y - 1], tb, 24);
+    }
+}
+
 static int gather4_dp(const onode* bin, int root, int ref[4], float box[4][6]) {
   const onode* b = &bin[root];
   /* root is a wide node: distribute its 4 slots as D(root, 4) chose */
@@ -407,7 +417,8 @@ static int gather4_dp(const onode* bin, int root, int ref[4], float box[4][6]) {
 
 /* collapse the binary tree into 4-wide nodes (SAH DP, or greedy largest-area opening), BFS order
  * (k_collapse) */
-static uint32_t collapse(const onode* bin, uint32_t nbin, o4node* out, uint32_t* count, uint32_t* max_stack) {
+static uint32_t collapse(const onode* bin, uint32_t nbin, o4node* out, uint32_t* count, uint32_t* max_stack,
+                         int blas) {
 #ifdef OSTUDY_BIN_HOOK /* design studies only (tools/wide_study.c): a copy of the binary tree */
   OSTUDY_BIN_HOOK(bin, nbin);
 #endif
@@ -425,6 +436,7 @@ static uint32_t collapse(const onode* bin, uint32_t nbin, o4node* out, uint32_t*
       int ref[4];
       float box[4][6];
       const int cnt = dp_on ? gather4_dp(bin, q[head], ref, box) : gather4(bin, q[head], ref, box);
+      if (blas) oinner_first(cnt, ref, box);
       o4node nd;
       memset(&nd, 0, sizeof(nd));
       uint32_t valid = 0;
@@ -592,7 +604,7 @@ static uint32_t lbvh(const float* primbox, uint32_t n, o4node** out4, uint32_t* 
   free(keys); free(k2); free(v2);
   (void)depth;
   *out4 = (o4node*)malloc((size_t)nbin * sizeof(o4node));
-  uint32_t levels = collapse(nodes, nbin, *out4, count4, max_stack);
+  uint32_t levels = collapse(nodes, nbin, *out4, count4, max_stack, !leaf_ref_is_prim);
   free(nodes);
   return levels;
 }

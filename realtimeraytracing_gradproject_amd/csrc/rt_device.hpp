@@ -63,8 +63,8 @@ struct alignas(128) Bvh4Node {
   int32_t child[4];
   uint32_t count;       // valid children
   int32_t first_inner;  // ref of the first internal child (0 when none): the internal children's
-                        // refs are consecutive in slot order (BFS allocation), so internal slot k
-                        // is first_inner + popcount(inner_mask & ((1 << k) - 1))
+                        // refs are consecutive in slot order (BFS allocation); BLAS nodes hold them
+                        // in the lowest slots, so there slot k is first_inner + k
   uint32_t inner_mask;  // bit k: child[k] is an internal node (>= 0)
   uint32_t entry_base;  // first_inner << 8 | inner_mask << 4: the packet walk's stack entry for this
                         // node, OR-ed with the pending slots

@@ -549,6 +549,29 @@ __device__ __forceinline__ int gather4_dp(const BinNode* __restrict__ bin, const
   return cnt;
 }
 
+// BLAS nodes keep their internal children in the lowest slots (stable: ascending half area within
+// the internal and within the leaf children). The walk tests a node's entered triangles in place and
+// then orders only its internal children, so this changes no visit order and no counter; with it, an
+// internal child's ref is first_inner + slot (the packet stack pops without a popcount).
+template <int M>
+__device__ __forceinline__ void inner_first(int (&ref)[M], float (&box)[M][6]) {
+#pragma unroll
+  for (int x = 1; x < M; ++x)
+#pragma unroll
+    for (int y = x; y > 0; --y)
+      if (ref[y] >= 0 && ref[y - 1] < 0) {
+        const int tr = ref[y];
+        ref[y] = ref[y - 1];
+        ref[y - 1] = tr;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          const float t = box[y][q];
+          box[y][q] = box[y - 1][q];
+          box[y - 1][q] = t;
+        }
+      }
+}
+
 // The DP expansion of every binary node, in parallel (only wide-node roots are read): k_collapse
 // then takes one record per node instead of walking dependent loads level by level.
 struct alignas(128) Exp4 {
@@ -558,7 +581,7 @@ struct alignas(128) Exp4 {
 };
 
 __global__ void k_dp_expand(int nbin, const BinNode* __restrict__ bin, const float4* __restrict__ dpc,
-                            const uint32_t* __restrict__ dps, Exp4* __restrict__ exp) {
+                            const uint32_t* __restrict__ dps, Exp4* __restrict__ exp, bool blas) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nbin) return;
   Exp4 e;
@@ -577,6 +600,7 @@ __global__ void k_dp_expand(int nbin, const BinNode* __restrict__ bin, const flo
       }
     }
   for (int j = e.cnt; j < 4; ++j) e.ref[j] = kEmptyChild;
+  if (blas) inner_first(e.ref, e.box);
   e.pad[0] = e.pad[1] = e.pad[2] = 0;
   exp[i] = e;
 }
@@ -612,7 +636,8 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, u
 
 __global__ __launch_bounds__(1024) void k_collapse(const BinNode* __restrict__ bin, const Exp4* __restrict__ exp,
                                                    Bvh4Node* __restrict__ out,
-                                                   int* la, int* lb, int* ps, uint32_t* __restrict__ info) {
+                                                   int* la, int* lb, int* ps, uint32_t* __restrict__ info,
+                                                   bool blas) {
   __shared__ uint32_t s_w[kFusedWaves];
   __shared__ int s_maxstack;
   const int tid = threadIdx.x;
@@ -645,6 +670,8 @@ __global__ __launch_bounds__(1024) void k_collapse(const BinNode* __restrict__ b
           }
         } else {
           cnt = gather4(bin, cur[i], ref, box);
+          for (int j = cnt; j < 4; ++j) ref[j] = kEmptyChild;
+          if (blas) inner_first(ref, box);
         }
       }
       uint32_t m = 0;
@@ -777,7 +804,8 @@ __device__ __forceinline__ void expand_slots(const BinNode* __restrict__ bin, co
 
 // The wide node rooted at binary node `root` (gather4_dp + the k_dp_expand slot order), in registers.
 __device__ __forceinline__ int wide_slots_dp(const BinNode* __restrict__ bin, const float4* __restrict__ dpc,
-                                             const uint32_t* __restrict__ dps, int root, int ref[4], float box[4][6]) {
+                                             const uint32_t* __restrict__ dps, int root, int (&ref)[4],
+                                             float (&box)[4][6], bool blas) {
   const int2 rc = *reinterpret_cast<const int2*>(&bin[root].c0);
   const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   const float4 l = rc.x >= 0 ? dpc[rc.x] : zero, r = rc.y >= 0 ? dpc[rc.y] : zero;
@@ -841,6 +869,7 @@ __device__ __forceinline__ int wide_slots_dp(const BinNode* __restrict__ bin, co
 #pragma unroll
   for (int j = 0; j < 4; ++j)
     if (j >= s.cnt) ref[j] = kEmptyChild;
+  if (blas) inner_first(ref, box);
   return s.cnt;
 }
 
@@ -1113,9 +1142,12 @@ __global__ __launch_bounds__(kFusedThreads) void k_build_small(
         int cnt4 = 0;
         if (valid) {
           if (dpc)  // the DP expansion of this wide node's root, in registers (no k_dp_expand pass)
-            cnt4 = wide_slots_dp(bin, dpc, dps, cur[i], ref, box);
-          else
+            cnt4 = wide_slots_dp(bin, dpc, dps, cur[i], ref, box, !leaf_ref_is_prim);
+          else {
             cnt4 = gather4(bin, cur[i], ref, box);
+            for (int j = cnt4; j < 4; ++j) ref[j] = kEmptyChild;
+            if (!leaf_ref_is_prim) inner_first(ref, box);
+          }
         }
         uint32_t m = 0;
         for (int j = 0; j < cnt4; ++j) m += ref[j] >= 0;
@@ -1341,11 +1373,11 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
   }
   if (RT_SAH_COLLAPSE) {
     k_dp_expand<<<grid1(nbin, 256), 256, 0, s>>>((int)nbin, d_bin, (const float4*)dpc.p, (const uint32_t*)dps.p,
-                                                 (Exp4*)expd.p);
+                                                 (Exp4*)expd.p, !leaf_ref_is_prim);
     RT_TRY(hipGetLastError());
   }
   k_collapse<<<1, 1024, 0, s>>>(d_bin, (const Exp4*)expd.p, d_nodes, (int*)la.p, (int*)lb.p, (int*)ps.p,
-                                (uint32_t*)info.p);
+                                (uint32_t*)info.p, !leaf_ref_is_prim);
   RT_TRY(hipGetLastError());
   if (d_tri_in) {
     k_tri_reorder<<<grid1(n, 256), 256, 0, s>>>(d_tri_in, d_sorted, n, d_tri_out);

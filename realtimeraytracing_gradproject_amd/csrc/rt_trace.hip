@@ -53,6 +53,12 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 typedef int i4v __attribute__((ext_vector_type(4)));
 typedef int i8v __attribute__((ext_vector_type(8)));
 typedef float f8v __attribute__((ext_vector_type(8)));
+#ifndef RT_PUSH_P_VALU
+#define RT_PUSH_P_VALU 0  // closest-hit BLAS push: the pending set formed per lane in VALU (A/B knob)
+#endif
+#ifndef RT_TRI_UNROLL
+#define RT_TRI_UNROLL 1  // triangle children tested per slot, unrolled (0: a ctz loop with a ref-select chain)
+#endif
 #ifndef RT_ANY_MT_BITS
 #define RT_ANY_MT_BITS 0  // any-hit triangle tests with the bitwise acceptance (A/B knob)
 #endif
@@ -310,19 +316,32 @@ __device__ __forceinline__ int push_entry(int stk, int& sp, uint32_t entry_base,
   return amdgcn_writelane((int)e, (int)lane, stk);
 }
 
-// Pops the packet walk's top BLAS entry (sp > base): returns its lowest pending child
-// (first_inner + the internal children below that slot) and keeps the entry, minus that slot,
-// while slots remain. e & (e - 1) clears the lowest pending bit (the pending bits are the low
-// four and never all zero).
+// The same push with P = pk & 15 already formed per lane in VALU (the lead lane's pk, read with the
+// child's ref): SCC comes from that one s_and.
+__device__ __forceinline__ int push_entry_p(int stk, int& sp, uint32_t entry_base, uint32_t pk) {
+  uint32_t p, e, lane;
+  asm volatile(
+      "s_and_b32 %0, %4, 15\n\t"
+      "s_cselect_b32 %3, %1, 63\n\t"
+      "s_addc_u32 %1, %1, 0\n\t"
+      "s_or_b32 %2, %5, %0"
+      : "=&s"(p), "+s"(sp), "=&s"(e), "=&s"(lane)
+      : "s"(pk), "s"(entry_base)
+      : "scc");
+  return amdgcn_writelane((int)e, (int)lane, stk);
+}
+
+// Pops the packet walk's top BLAS entry (sp > base): returns its lowest pending child and keeps
+// the entry, minus that slot, while slots remain. BLAS nodes hold their internal children in the
+// lowest slots (inner_first in rt_lbvh.hip), so the child in slot k is first_inner + k (the lowest
+// set bit of e is the lowest pending slot: the pending bits are the low four, never all zero).
+// e & (e - 1) clears it.
 __device__ __forceinline__ int pop_entry(int& stk, int& sp) {
   const int top = sp - 1;
   const uint32_t e = (uint32_t)__builtin_amdgcn_readlane(stk, top);
   uint32_t ref, rest, lane, t0, t1;
   asm volatile(
       "s_ff1_i32_b32 %3, %6\n\t"
-      "s_bfm_b32 %3, %3, 4\n\t"
-      "s_and_b32 %3, %6, %3\n\t"
-      "s_bcnt1_i32_b32 %3, %3\n\t"
       "s_lshr_b32 %0, %6, 8\n\t"
       "s_add_u32 %0, %0, %3\n\t"
       "s_add_u32 %4, %6, -1\n\t"
@@ -582,12 +601,19 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
     uint32_t tl = ent & ~imask;
     ent &= imask;
     if (tl) {
+#if RT_TRI_UNROLL
+      // one test per slot with the slot's ref in a fixed SGPR (no ref-select chain, no loop)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (tl & (1u << k)) packet_tri<ANY_HIT, STATS, R>(tpool, ch[k], ry, tmin, cur, face, pl, hit, cnt);
+#else
       do {
         const uint32_t k = (uint32_t)__builtin_ctz(tl);
         tl &= tl - 1u;
         const i4v c4 = {ch[0], ch[1], ch[2], ch[3]};
         packet_tri<ANY_HIT, STATS, R>(tpool, c4[k], ry, tmin, cur, face, pl, hit, cnt);
       } while (tl);
+#endif
       if (ANY_HIT) {  // rays can only have left the packet in a triangle test
         if (!pl.update(hit)) return false;
         // children only finished rays wanted are dropped
@@ -607,7 +633,7 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
         // occlusion rays skip the nearest-first choice (no keys, no readlane): for an occlusion ray
         // the order only decides how soon it stops
         ib = (uint32_t)__builtin_ctz(ent);
-        nref = (uint32_t)ch[5] + (uint32_t)__builtin_popcount(imask & ((1u << ib) - 1u));
+        nref = (uint32_t)ch[5] + ib;  // internal children in the lowest slots
       } else {
         // per lane: the slot of its smallest key over the entered internal children (all-ones
         // keys elsewhere), lowest slot on ties, and that child's ref (first_inner + internal
@@ -622,12 +648,26 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
           for (int k = 0; k < 4; ++k) kk[k] = vkey[r][k] | bit_mask_v(nent, k);
           const uint32_t m = min(min(kk[0], kk[1]), min(kk[2], kk[3]));
           const uint32_t ir = kk[0] == m ? 0u : kk[1] == m ? 1u : kk[2] == m ? 2u : 3u;
-          const uint32_t pr = (((uint32_t)ch[5] + (uint32_t)__builtin_popcount(imask & ((1u << ir) - 1u))) << 2) | ir;
+#if RT_PUSH_P_VALU
+          // ref << 4 | the entered internal children other than ir (VALU: the scalar unit only unpacks)
+          const uint32_t pr = (((uint32_t)ch[5] + ir) << 4) | (ent & ~(1u << ir));
+#else
+          const uint32_t pr = (((uint32_t)ch[5] + ir) << 2) | ir;
+#endif
           idx = (r == 0 || pl.lead_r == (uint32_t)r) ? pr : idx;
         }
         const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)idx, (int)pl.lead_l);
+#if RT_PUSH_P_VALU
+        if (STATS && (pk & 15u) && sp + 1 > cap)  // never: cap bounds the entries (one per level)
+#pragma unroll
+          for (int r = 0; r < R; ++r) cnt.overflow += ray_live(hit[r]) ? 1u : 0u;
+        stk.v = push_entry_p(stk.v, sp, (uint32_t)ch[7], pk);
+        bref = (int)(pk >> 4);
+        continue;
+#else
         ib = pk & 3u;
         nref = pk >> 2;
+#endif
       }
       if (STATS && (ent & ~(1u << ib)) && sp + 1 > cap)  // never: cap bounds the entries (one per level)
 #pragma unroll

@@ -87,18 +87,25 @@ def test_node_meta_for_packet_stack(model):
 
 @pytest.mark.parametrize("model", ["teapot", "rabbit"])
 def test_slots_in_ascending_area(model):
-    """Each node's slots hold its children by ascending half area (stable): the nearest-first walk
-    breaks key ties (rays starting inside several boxes) and any-hit walks go lowest slot first,
-    both then enter the tighter box first."""
+    """BLAS nodes hold their internal children first, then their triangles, each group by ascending
+    half area (stable): the nearest-first walk breaks key ties (rays starting inside several boxes)
+    and any-hit walks go lowest slot first, both then enter the tighter box first; triangles are
+    tested in place, so only the internal children's order matters, and internal child k is
+    first_inner + k."""
     v, i = scenes.load_model(model)
     o = oracle.Scene()
     nodes, _ = o.export_blas(o.add_blas(v, i))
     lo, hi, ch, count = unpack4(nodes)
     d = (hi - lo).astype(np.float32)
     area = (d[..., 0] * d[..., 1] + d[..., 1] * d[..., 2]) + d[..., 2] * d[..., 0]
+    first_inner = nodes.view(np.int32)[:, 29]
     for k in range(len(nodes)):
-        a = area[k, :count[k]]
-        assert (a[1:] >= a[:-1]).all()
+        inner = ch[k, :count[k]] >= 0
+        ni = int(inner.sum())
+        assert inner[:ni].all() and not inner[ni:].any()
+        for grp in (area[k, :ni], area[k, ni:count[k]]):
+            assert (grp[1:] >= grp[:-1]).all()
+        assert np.array_equal(ch[k, :ni], first_inner[k] + np.arange(ni))
 
 
 def _wide_area(model: str, greedy: bool) -> float:
