@@ -53,6 +53,9 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 typedef int i4v __attribute__((ext_vector_type(4)));
 typedef int i8v __attribute__((ext_vector_type(8)));
 typedef float f8v __attribute__((ext_vector_type(8)));
+#ifndef RT_KEY_BFI
+#define RT_KEY_BFI 1  // nearest-child keys masked by v_bfi against the entered set (no s_not)
+#endif
 #ifndef RT_PUSH_P_VALU
 #define RT_PUSH_P_VALU 0  // closest-hit BLAS push: the pending set formed per lane in VALU (A/B knob)
 #endif
@@ -299,6 +302,17 @@ __device__ __forceinline__ uint32_t bit_mask_v(uint32_t m, int k) {
   return r;
 }
 
+// key where bit k of the uniform entered set m is set, else all ones (v_bfe_i32 + v_bfi_b32 on the
+// SGPR m: no scalar instruction to invert m first)
+__device__ __forceinline__ uint32_t key_if_entered(uint32_t key, uint32_t m, int k) {
+  uint32_t r, t;
+  asm("v_bfe_i32 %0, %2, %3, 1\n\t"
+      "v_bfi_b32 %1, %0, %4, -1"
+      : "=&v"(t), "=v"(r)
+      : "s"(m), "i"(k), "v"(key));
+  return r;
+}
+
 // Pushes entry_base | P with P = ent & ~nearest when P != 0: the write goes to lane sp, or to the
 // spare lane kPacketStack - 1 when nothing is pending, and sp advances by SCC (= P != 0): four
 // scalar instructions and one v_writelane (its lane select goes through m0, placed by the
@@ -528,13 +542,12 @@ __device__ __forceinline__ bool packet_tlas_node(const RT_CONST char* pool, int 
   if (ANY_HIT) {
     ib = (uint32_t)__builtin_ctz(ent);
   } else {
-    const uint32_t nent = ~ent;
     uint32_t idx = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       uint32_t kk[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) kk[k] = vkey[r][k] | bit_mask_v(nent, k);
+      for (int k = 0; k < 4; ++k) kk[k] = RT_KEY_BFI ? key_if_entered(vkey[r][k], ent, k) : vkey[r][k] | bit_mask_v(~ent, k);
       const uint32_t m = min(min(kk[0], kk[1]), min(kk[2], kk[3]));
       const uint32_t ir = kk[0] == m ? 0u : kk[1] == m ? 1u : kk[2] == m ? 2u : 3u;
       idx = (r == 0 || pl.lead_r == (uint32_t)r) ? ir : idx;
@@ -639,13 +652,13 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
         // keys elsewhere), lowest slot on ties, and that child's ref (first_inner + internal
         // children below it: v_bfm / v_and / v_bcnt in VALU), packed as ref << 2 | slot; the lead
         // lane's answer, one readlane, is the packet's
-        const uint32_t nent = ~ent;
         uint32_t idx = 0;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           uint32_t kk[4];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) kk[k] = vkey[r][k] | bit_mask_v(nent, k);
+          for (int k = 0; k < 4; ++k)
+            kk[k] = RT_KEY_BFI ? key_if_entered(vkey[r][k], ent, k) : vkey[r][k] | bit_mask_v(~ent, k);
           const uint32_t m = min(min(kk[0], kk[1]), min(kk[2], kk[3]));
           const uint32_t ir = kk[0] == m ? 0u : kk[1] == m ? 1u : kk[2] == m ? 2u : 3u;
 #if RT_PUSH_P_VALU
@@ -1100,6 +1113,9 @@ __device__ bool shadow_compact(const SceneView& sc, V3 P, V3 d, bool need, uint3
 #ifndef RT_KO_SHADOW
 #define RT_KO_SHADOW 0
 #endif
+#ifndef RT_WAVE_TIMES
+#define RT_WAVE_TIMES 0  // 1: every wave stores its start / end clock (diagnostics; tools/wave_times.py)
+#endif
 #ifndef RT_PHASE_TIMING
 #define RT_PHASE_TIMING 0  // 1: sampled waves printf s_memtime per phase (diagnostics only)
 #endif
@@ -1367,6 +1383,9 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
                           uint32_t* __restrict__ rgba8, float4* __restrict__ rgba32f,
                           unsigned long long* __restrict__ stats) {
   static_assert(KS <= 1 || R == 1, "sample lanes need one ray per lane");
+#if RT_WAVE_TIMES
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
   constexpr uint32_t NS = KS > 1 ? KS * KS : 1;  // samples of a pixel held by consecutive lanes
   constexpr uint32_t TP = KS > 1 ? 8 / KS : 8;    // tile side in pixels
   // the wave index is uniform: an SGPR, so the pixel of a lane can be re-derived from its lane id
@@ -1430,10 +1449,23 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
     if (out[r] != 0xffffffffu) {
       const uint32_t o = out[r];
       rgba8[o] = unorm8(a.x) | (unorm8(a.y) << 8) | (unorm8(a.z) << 16) | (255u << 24);
-      if (rgba32f) rgba32f[o] = make_float4(a.x, a.y, a.z, 1.0f);
+      if (rgba32f && !RT_WAVE_TIMES) rgba32f[o] = make_float4(a.x, a.y, a.z, 1.0f);
     }
   }
   if (STATS) flush_stats<true>(cnt, stats);
+#if RT_WAVE_TIMES
+  // diagnostics only: (start, end) of this wave on the 100 MHz clock + its XCC / CU ids, into the
+  // caller's float4 buffer (slot = wave index; the float image is not written in this variant)
+  if (rgba32f && (threadIdx.x & 63u) == 0) {
+    const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+    uint32_t xcc, hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    const uint32_t wid = (blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    uint4* o = reinterpret_cast<uint4*>(rgba32f) + wid;
+    *o = make_uint4((uint32_t)t_start, (uint32_t)t_end, xcc, hw);
+  }
+#endif
 }
 
 template <bool ANY_HIT, bool STATS, bool CULL>

@@ -1,0 +1,63 @@
+"""Per-wave start / end clocks of one frame (library built with -DRT_WAVE_TIMES=1): occupancy over
+time, the launch's ramp and tail, per-XCD finish times.
+  python tools/wave_times.py --lib <variant .so> --config C2"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import realtimeraytracing_gradproject_amd as rt  # noqa: E402
+from realtimeraytracing_gradproject_amd import scenes  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--lib", required=True)
+ap.add_argument("--config", default="C2")
+ap.add_argument("--frames", type=int, default=30)
+a = ap.parse_args()
+spec = scenes.config(a.config)
+c = rt.Context(0, library=rt._load(a.lib))
+scenes.upload(c, spec)
+W, H = spec.width, spec.height
+out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+tb = torch.zeros((H * W * 4,), dtype=torch.float32, device="cuda")
+s = torch.cuda.current_stream().cuda_stream
+for _ in range(a.frames):
+    c.dispatch(W, H, out, tb.view(H, W, 4), stream=s)
+torch.cuda.synchronize()
+tb.zero_()
+c.dispatch(W, H, out, tb.view(H, W, 4), stream=s)
+torch.cuda.synchronize()
+u = tb.view(torch.int32).cpu().numpy().astype(np.uint32).reshape(-1, 4)
+nw = (W // 8) * (H // 8) if spec.spp == 1 else None
+live = u[:, 1] != 0
+u = u[live]
+t0 = u[:, 0].astype(np.int64)
+t1 = u[:, 1].astype(np.int64)
+base = t0.min()
+t0 -= base
+t1 -= base
+T = t1.max()
+print(f"{a.config}: {len(u)} waves, frame {T * 10 / 1000:.1f} us (100 MHz clock)")
+dur = (t1 - t0) * 10 / 1000
+print(f"wave duration us: mean {dur.mean():.2f} p50 {np.median(dur):.2f} p90 {np.percentile(dur, 90):.2f} "
+      f"max {dur.max():.2f}")
+# occupancy over time in 20 bins
+edges = np.linspace(0, T, 21)
+occ = []
+for k in range(20):
+    lo, hi = edges[k], edges[k + 1]
+    ov = np.clip(np.minimum(t1, hi) - np.maximum(t0, lo), 0, None).sum() / (hi - lo)
+    occ.append(ov)
+print("resident waves per 5% of the frame:", " ".join(f"{o:.0f}" for o in occ))
+print(f"mean resident {np.mean(occ):.0f}; last wave start at {t0.max() * 10 / 1000:.1f} us")
+xcc = u[:, 2] & 0xf
+for x in range(8):
+    m = xcc == x
+    if m.any():
+        print(f"XCC {x}: waves {m.sum()} last end {t1[m].max() * 10 / 1000:.1f} us mean dur {dur[m].mean():.2f} us")
+c.close()
