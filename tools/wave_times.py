@@ -33,7 +33,6 @@ tb.zero_()
 c.dispatch(W, H, out, tb.view(H, W, 4), stream=s)
 torch.cuda.synchronize()
 u = tb.view(torch.int32).cpu().numpy().astype(np.uint32).reshape(-1, 4)
-nw = (W // 8) * (H // 8) if spec.spp == 1 else None
 live = u[:, 1] != 0
 u = u[live]
 t0 = u[:, 0].astype(np.int64)
@@ -60,4 +59,5 @@ for x in range(8):
     m = xcc == x
     if m.any():
         print(f"XCC {x}: waves {m.sum()} last end {t1[m].max() * 10 / 1000:.1f} us mean dur {dur[m].mean():.2f} us")
+np.savez(os.path.join(ROOT, "gpurun_out", f"wt_{a.config}.npz"), t0=t0, t1=t1, ids=np.nonzero(live)[0], xcc=xcc)
 c.close()
