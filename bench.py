@@ -111,12 +111,19 @@ class HipBackend:
     def __init__(self, local: int):
         import realtimeraytracing_gradproject_amd as rt
         self.rt = rt
+        # RT_BENCH_ONE_DEVICE=1 (rehearsal only): every rank on device 0, to exercise the RCCL path on a
+        # one-GPU box; never used for a reported number
+        if os.environ.get("RT_BENCH_ONE_DEVICE") == "1":
+            local = 0
         torch.cuda.set_device(local)
         self.local = local
         self.device = torch.device("cuda", local)
         self.ctx = None
 
     def init_pg(self):
+        if os.environ.get("RT_BENCH_ONE_DEVICE") == "1":  # rehearsal: RCCL refuses two ranks on one GPU
+            dist.init_process_group("gloo")
+            return
         dist.init_process_group("nccl", device_id=self.device)
 
     def load(self, spec, schedule: str):

@@ -1,0 +1,41 @@
+"""bench.py's multi-rank path on the GPU: `bench.py --gpus 2` spawns two ranks that tile one frame
+into strips, render them with the HIP kernel on their own streams, gather them (pipelined: the
+gather of frame k beside the render of frame k + 1) and un-interleave them with rt_assemble_strips.
+A one-GPU box cannot host two RCCL ranks (RCCL refuses two ranks on one device), so this rehearsal
+puts both ranks on device 0 and moves the strips with gloo (RT_BENCH_ONE_DEVICE=1); everything
+else is the code path of the 8-GPU run. The assembled frame must equal the oracle's bit for bit."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("config,size", [("C2F", "320x184"), ("C4", "256x136")])
+def test_bench_two_ranks_strips_on_gpu(tmp_path, config, size):
+    sys.path.insert(0, ROOT)
+    import oracle
+    from realtimeraytracing_gradproject_amd import scenes
+    img = tmp_path / "frame.npy"
+    env = dict(os.environ, RT_BENCH_ONE_DEVICE="1", OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", config, "--size", size,
+           "--steps", "4", "--warmup", "1", "--settle-ms", "0", "--extra=", "--no-cpu-baseline",
+           "--save-image", str(img)]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["rccl_world_size"] == 2
+    w, h = (int(v) for v in size.split("x"))
+    spec = scenes.config(config).with_size(w, h)
+    o8, _, st = oracle.Scene(spec).render_spec(spec, nthreads=8, want_float=False)
+    assert out["config"]["rays_per_step"] == int(st[0] + st[1])
+    assert np.array_equal(np.load(img), o8)
