@@ -53,6 +53,12 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 typedef int i4v __attribute__((ext_vector_type(4)));
 typedef int i8v __attribute__((ext_vector_type(8)));
 typedef float f8v __attribute__((ext_vector_type(8)));
+#ifndef RT_REF0_WAVES
+#define RT_REF0_WAVES 7  // the reflectivity-0 REF kernel (MODE 3, one sample)
+#endif
+#ifndef RT_REF_NOREFL
+#define RT_REF_NOREFL 1  // RT_SHADE_REF with reflectivity 0: the kernel specialised without reflection rays
+#endif
 #ifndef RT_KEY_BFI
 #define RT_KEY_BFI 1  // nearest-child keys masked by v_bfi against the entered set (no s_not)
 #endif
@@ -1019,7 +1025,7 @@ __device__ V3 shade_sample(const SceneView& sc, const FrameParams& fp, uint32_t 
   HitRec hit;
   if (STATS) ++cnt.primary;
   const bool f = trace<false, STATS>(sc, O, D, 0.0f, 100000.0f, hit, stk, cnt);
-  if (MODE == 0) return shade_ref<STATS>(sc, fp, py, O, D, f, hit, stk, cnt);
+  if (MODE == 0 || MODE == 3) return shade_ref<STATS>(sc, fp, py, O, D, f, hit, stk, cnt);
   if (!f) return miss_color(fp, py);
   const HitInstance ir = load_hit_instance(sc, hit.inst);
   const V3 P = add(O, muls(D, hit.t));  // GetWorldHitPoint, Common.hlsl:24-27
@@ -1146,7 +1152,7 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
   trace_packet<false, STATS, R>(sc, O, D, 0.0f, 100000.0f, inimg, found, hit, cnt);
 #pragma unroll
   for (int r = 0; r < R; ++r) P[r] = add(O[r], muls(D[r], hit[r].t));  // GetWorldHitPoint, Common.hlsl:24-27
-  if (MODE == 0) {
+  if (MODE == 0 || MODE == 3) {  // MODE 3: RT_SHADE_REF with reflectivity 0 (no reflection rays)
 #pragma unroll
     for (int r = 0; r < R; ++r) color[r] = miss_color(fp, py[r]);
     // shade_ref level by level for the whole packet: each level's shadow rays and next
@@ -1186,7 +1192,7 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
           }
           const V3 n = interpolated_world_normal(ir, hit[r].prim, hit[r].u, hit[r].v);
           const V3 s = add(direct_lighting(fp, P[r], n, albedo), pbr_shading(fp, n, ro[r], P[r]));
-          if (reflective(fp, ir, depth)) {
+          if (MODE == 0 && reflective(fp, ir, depth)) {
             sk[r][depth] = s;
             reflection_ray(P[r], n, rd[r], ro[r], rd[r]);
             nxt[r] = true;
@@ -1378,7 +1384,8 @@ constexpr int kPacketBlock = 64 * RT_PACKET_WX * RT_PACKET_WY;
 template <int MODE, bool STATS, int R, int KS>
 __global__ __launch_bounds__(kPacketBlock) __attribute__((amdgpu_waves_per_eu(
     (MODE == 1 && !STATS) ? (KS == 0 ? RT_SPP_WAVES : (KS == 1 ? RT_LS_WAVES : RT_KS_WAVES))
-                          : ((MODE == 0 && !STATS && KS == 1) ? RT_REF_WAVES : 1))))
+    : (MODE == 3 && !STATS) ? (KS == 0 ? RT_SPP_WAVES : (KS == 1 ? RT_REF0_WAVES : RT_KS_WAVES))
+                            : ((MODE == 0 && !STATS && KS == 1) ? RT_REF_WAVES : 1))))
 void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restrict__ rows,
                           uint32_t* __restrict__ rgba8, float4* __restrict__ rgba32f,
                           unsigned long long* __restrict__ stats) {
@@ -1537,6 +1544,11 @@ hipError_t launch_trace_frame(const SceneView& sc, const FrameParams& fp, const 
                               int schedule, hipStream_t s) {
   switch (fp.shade_mode) {
     case 0:
+      // the reference scene's parity config pins reflectivity to 0: a kernel without
+      // the reflection-chain state (registers, the per-lane sk[] stack) then runs at a higher occupancy
+      if (fp.material.reflectivity == 0.0f && RT_REF_NOREFL)
+        return stats ? launch_mode<3, true>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, s)
+                     : launch_mode<3, false>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, s);
       return stats ? launch_mode<0, true>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, s)
                    : launch_mode<0, false>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, s);
     case 1:
