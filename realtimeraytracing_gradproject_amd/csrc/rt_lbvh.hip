@@ -875,8 +875,8 @@ __device__ __forceinline__ int wide_slots_dp(const BinNode* __restrict__ bin, co
 
 __global__ __launch_bounds__(kFusedThreads) void k_build_small(
     const float* __restrict__ primbox, uint32_t n, bool leaf_ref_is_prim, uint32_t* __restrict__ sorted,
-    float* __restrict__ cb_out, int* __restrict__ child, int* __restrict__ pint, int* __restrict__ pleaf,
-    float* nbox, float4* dpc, uint32_t* dps, BinNode* bin, Exp4* expd, Bvh4Node* __restrict__ out,
+    float* __restrict__ cb_out, int* __restrict__ pleaf, float* nbox, float4* dpc, uint32_t* dps, BinNode* bin,
+    Bvh4Node* __restrict__ out,
     uint32_t* __restrict__ info, const TriRec* __restrict__ tri_in, TriRec* __restrict__ tri_out) {
   // LDS: sort buffers (keys A | values A | keys B | values B) + (digit, wave) counts; later
   // phases reuse the same words: arrival flags (refit), level lists and stack sums (collapse)
@@ -897,7 +897,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_build_small(
   uint32_t* valA = s_mem + kFusedMax;
   uint32_t* keyB = s_mem + 2 * kFusedMax;
   uint32_t* valB = s_mem + 3 * kFusedMax;
-  uint32_t* cnt = s_mem + 4 * kFusedMax;  // [digit][wave]
+  uint32_t* cnt = s_mem + 4 * kFusedMax;  // [wave][digit]: a wave's lanes hit distinct banks
 
   // 1. bounds (k_bounds)
   {
@@ -970,20 +970,22 @@ __global__ __launch_bounds__(kFusedThreads) void k_build_small(
           const uint64_t m = __ballot(valid && bit);
           peers &= bit ? m : ~m;
         }
-        if (valid && (peers & lt) == 0) cnt[digit * kFusedWaves + w] += (uint32_t)__popcll(peers);
+        if (valid && (peers & lt) == 0) cnt[w * 256u + digit] += (uint32_t)__popcll(peers);
       }
       __syncthreads();
       // exclusive scan over (digit, wave): 4 consecutive entries per thread
       {
         uint32_t e[4], s = 0;
         for (int q = 0; q < 4; ++q) {
-          e[q] = cnt[tid * 4 + q];
+          const uint32_t si = tid * 4 + q;  // scan order: digit-major, wave-minor
+          e[q] = cnt[(si % kFusedWaves) * 256u + si / kFusedWaves];
           s += e[q];
         }
         uint32_t tot;
         uint32_t run = block_excl_scan(s, s_w, &tot);
         for (int q = 0; q < 4; ++q) {
-          cnt[tid * 4 + q] = run;
+          const uint32_t si = tid * 4 + q;
+          cnt[(si % kFusedWaves) * 256u + si / kFusedWaves] = run;
           run += e[q];
         }
       }
@@ -1001,12 +1003,12 @@ __global__ __launch_bounds__(kFusedThreads) void k_build_small(
           peers &= bit ? m : ~m;
         }
         const uint32_t rank = (uint32_t)__popcll(peers & lt);
-        const uint32_t base = valid ? cnt[digit * kFusedWaves + w] : 0u;  // every lane reads before the update
+        const uint32_t base = valid ? cnt[w * 256u + digit] : 0u;  // every lane reads before the update
         if (valid) {
           kout[base + rank] = key;
           vout[base + rank] = val;
         }
-        if (valid && rank == 0) cnt[digit * kFusedWaves + w] = base + (uint32_t)__popcll(peers);
+        if (valid && rank == 0) cnt[w * 256u + digit] = base + (uint32_t)__popcll(peers);
       }
       __syncthreads();
       uint32_t* t = kin;
@@ -1333,10 +1335,9 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
   RT_TRY(hipEventRecord(e0, s));
   float* cb = (float*)stats.p;
   if (RT_FUSED_BUILD && n <= (uint32_t)RT_FUSED_MAX_N) {
-    k_build_small<<<1, kFusedThreads, 0, s>>>(d_primbox, n, leaf_ref_is_prim, d_sorted, cb, (int*)child.p,
-                                              (int*)pint.p, (int*)pleaf.p, (float*)nbox.p, (float4*)dpc.p,
-                                              (uint32_t*)dps.p, (BinNode*)bin.p, (Exp4*)expd.p, d_nodes,
-                                              (uint32_t*)info.p, d_tri_in, d_tri_out);
+    k_build_small<<<1, kFusedThreads, 0, s>>>(d_primbox, n, leaf_ref_is_prim, d_sorted, cb, (int*)pleaf.p,
+                                              (float*)nbox.p, (float4*)dpc.p, (uint32_t*)dps.p, (BinNode*)bin.p,
+                                              d_nodes, (uint32_t*)info.p, d_tri_in, d_tri_out);
     RT_TRY(hipGetLastError());
   } else {
   k_bounds<<<1, 1024, 0, s>>>(d_primbox, n, cb);
