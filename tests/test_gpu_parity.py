@@ -356,6 +356,48 @@ def test_trace_rays_equals_bruteforce(any_hit, cull):
     c.close()
 
 
+@pytest.mark.parametrize("any_hit", [False, True])
+def test_large_soup_multi_kernel_build_and_trace(any_hit):
+    """60 K-triangle soup (the multi-kernel LBVH build, deep trees) under a rotated + scaled instance and
+    a translated copy: tree bitwise equal to the oracle's, 50 K rays' hits equal the oracle's BVH
+    walk (itself == brute force on smaller scenes) and, for 2 K of them, the oracle's brute force."""
+    rng = np.random.default_rng(60000)
+    ntri = 60000
+    c0 = rng.uniform(-4, 4, size=(ntri, 1, 3))
+    v = np.zeros((ntri * 3, 6), np.float32)
+    v[:, :3] = (c0 + rng.normal(scale=0.08, size=(ntri, 3, 3))).reshape(-1, 3).astype(np.float32)
+    v[:, 4] = 1.0
+    inst = [(0, scenes._rot_scale((1.0, 2.0, 0.5), 33.0, (1.0, 0.7, 1.3), (0.0, 0.5, 0.0)), 0, 0),
+            (0, scenes._rot_scale((0.0, 1.0, 0.0), 0.0, (1.0, 1.0, 1.0), (9.0, 0.0, -3.0)), 1, 0)]
+    c = fresh_ctx()
+    b = c.blas_build(v)
+    c.tlas_build([(b, x, iid, hg) for (_, x, iid, hg) in inst])
+    o = oracle.Scene()
+    ob = o.add_blas(v)
+    o.set_instances([(ob, x, iid, hg) for (_, x, iid, hg) in inst])
+    gn, gt = c.blas_export(b)
+    on, ot = o.export_blas(ob)
+    assert np.array_equal(gn, on) and np.array_equal(gt, ot)
+    n = 50000
+    rays = random_rays(n, 0x5EED + 7)
+    d_rays = torch.from_numpy(rays).cuda()
+    d_hits = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+    d_uv = torch.zeros((n, 2), dtype=torch.float32, device="cuda")
+    c.trace_rays(d_rays, n, any_hit, d_hits, d_uv)
+    torch.cuda.synchronize()
+    g = d_hits.cpu().numpy().view(np.uint32)
+    oh, ouv, _ = o.trace_rays(rays, any_hit=any_hit)
+    assert np.array_equal(g, oh)
+    if not any_hit:
+        assert np.array_equal(d_uv.cpu().numpy(), ouv)
+    bb, _, _ = o.trace_rays(rays[:2000], any_hit=any_hit, brute_force=True)
+    assert np.array_equal(g[:2000, 3], bb[:, 3])
+    if not any_hit:
+        assert np.array_equal(g[:2000], bb)
+    assert g[:, 3].sum() > n // 20
+    c.close()
+
+
 @pytest.mark.parametrize("any_hit,cull", [(False, None), (True, None), (False, "back"), (False, "front")])
 def test_trace_rays_degenerate_and_transformed(any_hit, cull):
     """DEGEN: degenerate triangles under rotated, scaled and mirrored instances (the mirrored one
