@@ -933,7 +933,11 @@ static int opk_node(const o4node* nd, const opkray* ry, float tmin, ohit* h, int
       float f = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), h[l].t));
       int hit = n <= f * 1.0000004f; /* empty slots hold +inf boxes: never accepted */
       if (hit && live[l]) hm[k] |= 1ull << l;
+#ifdef OCLOSEST_KEY /* design studies only (tools/key_study.c): another nearest-first key */
+      vkey[l][k] = hit ? OCLOSEST_KEY(n, f) : 0x7f800000u;
+#else
       vkey[l][k] = hit ? (f2bits(n) & 0x7fffffffu) : 0x7f800000u;
+#endif
     }
     if (live[l]) st->v[2] += nd->count;
   }
@@ -1002,6 +1006,9 @@ static void opacket(const oracle_scene* s, const vec3* o, const vec3* d, float t
                     int cull, const int* alive, ohit* h, int* found, ostats* st) {
   int live[OPK];
   opkray w, b;
+#ifdef OSTUDY_PACKET_HOOK /* design studies only (tools/refl_study.c): packet occupancy */
+  OSTUDY_PACKET_HOOK(any, cull, alive);
+#endif
   for (int l = 0; l < OPK; ++l) {
     live[l] = alive[l];
     found[l] = 0;

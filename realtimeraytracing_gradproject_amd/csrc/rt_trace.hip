@@ -53,6 +53,9 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 typedef int i4v __attribute__((ext_vector_type(4)));
 typedef int i8v __attribute__((ext_vector_type(8)));
 typedef float f8v __attribute__((ext_vector_type(8)));
+#ifndef RT_SINGLE_SKIP
+#define RT_SINGLE_SKIP 1  // closest-hit BLAS nodes with one entered internal child skip the keys
+#endif
 #ifndef RT_REF0_WAVES
 #define RT_REF0_WAVES 7  // the reflectivity-0 REF kernel (MODE 3, one sample)
 #endif
@@ -648,9 +651,10 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
     }
     if (ent) {
       uint32_t ib, nref;
-      if (ANY_HIT) {
+      if (ANY_HIT || (RT_SINGLE_SKIP && (ent & (ent - 1u)) == 0u)) {
         // occlusion rays skip the nearest-first choice (no keys, no readlane): for an occlusion ray
-        // the order only decides how soon it stops
+        // the order only decides how soon it stops; a closest-hit node with ONE entered internal
+        // child has no choice to make (RT_SINGLE_SKIP)
         ib = (uint32_t)__builtin_ctz(ent);
         nref = (uint32_t)ch[5] + ib;  // internal children in the lowest slots
       } else {
