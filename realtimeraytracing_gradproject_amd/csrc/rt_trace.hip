@@ -56,6 +56,9 @@ typedef float f8v __attribute__((ext_vector_type(8)));
 #ifndef RT_SINGLE_SKIP
 #define RT_SINGLE_SKIP 1  // closest-hit BLAS nodes with one entered internal child skip the keys
 #endif
+#ifndef RT_TLAS_SINGLE_SKIP
+#define RT_TLAS_SINGLE_SKIP 1  // the same for TLAS nodes
+#endif
 #ifndef RT_REF0_WAVES
 #define RT_REF0_WAVES 7  // the reflectivity-0 REF kernel (MODE 3, one sample)
 #endif
@@ -548,7 +551,7 @@ __device__ __forceinline__ bool packet_tlas_node(const RT_CONST char* pool, int 
   // nearest entered child by the lead ray's key, lowest slot on ties: per lane in VALU (keys
   // masked to the entered set), one readlane. Any-hit walks take the lowest entered slot.
   uint32_t ib;
-  if (ANY_HIT) {
+  if (ANY_HIT || (RT_TLAS_SINGLE_SKIP && (ent & (ent - 1u)) == 0u)) {  // no choice with one entered child
     ib = (uint32_t)__builtin_ctz(ent);
   } else {
     uint32_t idx = 0;
