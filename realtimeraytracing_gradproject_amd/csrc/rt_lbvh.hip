@@ -19,6 +19,8 @@
 // it in one 1024-thread workgroup instead (k_build_small): one launch, LDS-resident sort.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "rt_internal.hpp"
@@ -28,6 +30,12 @@
 #endif
 #ifndef RT_FUSED_MAX_N
 #define RT_FUSED_MAX_N 3072  // largest n built by k_build_small (measured crossover; capacity kFusedMax)
+#endif
+#ifndef RT_MID_BUILD
+#define RT_MID_BUILD 1  // RT_MID_MIN_N <= n <= kMidMax: the five-launch build (k_mid_*)
+#endif
+#ifndef RT_MID_MIN_N
+#define RT_MID_MIN_N 2  // smallest n built by k_mid_* (measured crossover against k_build_small)
 #endif
 #ifndef RT_REFIT_WT
 #define RT_REFIT_WT 1  // multi-kernel refit: write-through hand-off instead of agent release/acquire fences
@@ -1225,6 +1233,446 @@ __global__ __launch_bounds__(kFusedThreads) void k_build_small(
 #undef RT_BT
 }
 
+// ------------------------------------------------------------------------------------------
+// Four-launch build for RT_MID_MIN_N <= n <= kMidMax (the teapot / rabbit BLASes, every TLAS of
+// the configs) instead of ~20 launches, none of them a long single-workgroup pipeline:
+//   k_mid_rank       bounds + Morton codes + sort by RANK, one launch: every workgroup reduces the
+//                    bounds of all n boxes itself (exact min / max: any order gives the same
+//                    floats), holds all n keys in LDS, and ranks 64 of them with 16 waves splitting
+//                    the j range: the stable order of key64 = morton << 32 | index is
+//                    rank(i) = #{j : key64_j < key64_i}. The scatter by rank also writes the
+//                    triangles in leaf order.
+//   k_mid_tree       hierarchy + refit + SAH DP + pack in ONE bottom-up pass (Apetrei 2014,
+//                    agglomerative LBVH): a node [l, r] is the left child of the split at r when
+//                    delta(r) > delta(l - 1), else the right child of the split at l - 1, so a leaf's
+//                    thread climbs without parent pointers. The binary radix tree over distinct keys
+//                    is unique, so this is Karras' tree (internal nodes numbered by split position
+//                    instead; the collapse output does not depend on the numbering). A workgroup
+//                    owns a block of S leaves and completes every node whose range stays inside it,
+//                    hand-offs through LDS. Whether a parent stays inside is decided from its split
+//                    s alone (its range is the keys sharing delta(s) prefix bits with key s: inside
+//                    iff lcp(s, B - 1) < delta(s) and lcp(s, B + S) < delta(s)), so both arrivals
+//                    agree; a child whose parent leaves the block goes to the frontier list.
+//   k_mid_expand     the DP expansion (wide_slots_dp) of every node built so far, in parallel
+//   k_mid_collapse   one workgroup: the top of the tree climbed from the frontier with LDS hand-
+//                    offs (the nodes that cross block boundaries: at most (blocks - 1) x 64, the
+//                    key64 bit length bounding the depth), their expansions, then the BFS numbering
+//                    level by level over 16-bit child lists in LDS, every 4-wide node written in
+//                    parallel.
+// The device-scope arrival protocol of k_refit (a write-through payload, a wait for its
+// acknowledgement and an agent-scope atomic per level: ~3 memory round trips) is not used: the
+// block-crossing chains from the block boundaries to the root were the critical path with it.
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t kMidMax = 8192;
+constexpr int kMidBlock = 1024;       // leaves per k_mid_tree workgroup
+constexpr int kMidTopSlots = 1024;    // top-climb payload slots: >= 2 x (kMidMax / kMidBlock - 1) x 64
+constexpr uint16_t kMidLeaf = 0xfffeu, kMidEmpty = 0xffffu;
+constexpr uint32_t kDpsUnbuilt = 0xffffffffu;  // dps of a node k_mid_tree left to the collapse
+static_assert(kMidTopSlots >= 2 * (kMidMax / kMidBlock - 1) * 64, "top-climb slots");
+
+struct MidSlot {  // a child's hand-off record: box, DP costs, ref, range
+  float b[6];
+  float d[4];
+  int32_t ref, l, r, pad;
+};
+
+__device__ __forceinline__ int lcp64(uint64_t a, uint64_t b) { return __clzll(a ^ b); }
+
+// Builds the parent at split s from its two children (a = this thread's node, o = the sibling's
+// record; `left`: a is the left child): BinNode, DP (k_refit / k_pack arithmetic, left child first),
+// and the parent's box / DP / range back into a.
+__device__ __forceinline__ void mid_join(int s, bool left, MidSlot& a, const MidSlot& o, BinNode* __restrict__ bin,
+                                         float4* __restrict__ dpc, uint32_t* __restrict__ dps) {
+  const MidSlot& L = left ? a : o;
+  const MidSlot& R = left ? o : a;
+  BinNode nd;
+  float bb[6];
+  for (int k = 0; k < 3; ++k) {
+    nd.lo0[k] = L.b[k];
+    nd.hi0[k] = L.b[3 + k];
+    nd.lo1[k] = R.b[k];
+    nd.hi1[k] = R.b[3 + k];
+    bb[k] = fminf(L.b[k], R.b[k]);
+    bb[3 + k] = fmaxf(L.b[3 + k], R.b[3 + k]);
+  }
+  nd.c0 = L.ref;
+  nd.c1 = R.ref;
+  nd.pad0 = nd.pad1 = 0;
+  float4 dc;
+  uint32_t sj;
+  sah_dp_vals(bb, make_float4(L.d[0], L.d[1], L.d[2], L.d[3]), make_float4(R.d[0], R.d[1], R.d[2], R.d[3]), dc, sj);
+  const int nl = L.l, nr = R.r;
+  bin[s] = nd;
+  dpc[s] = dc;
+  dps[s] = sj;
+  for (int k = 0; k < 6; ++k) a.b[k] = bb[k];
+  a.d[0] = dc.x;
+  a.d[1] = dc.y;
+  a.d[2] = dc.z;
+  a.d[3] = dc.w;
+  a.ref = s;
+  a.l = nl;
+  a.r = nr;
+}
+
+__global__ __launch_bounds__(1024) void k_mid_rank(const float* __restrict__ primbox, uint32_t n,
+                                                   float* __restrict__ cb_out, uint32_t* __restrict__ keys_sorted,
+                                                   uint32_t* __restrict__ sorted, uint32_t* __restrict__ dps,
+                                                   uint32_t* __restrict__ info, const TriRec* __restrict__ tri_in,
+                                                   TriRec* __restrict__ tri_out) {
+  __shared__ uint64_t s_key[kMidMax];
+  __shared__ uint32_t s_part[16][64];
+  __shared__ float s_red[12][16];
+  __shared__ float s_cb[12];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  constexpr int kPer = kMidMax / 1024;
+  float bx[kPer][6];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const uint32_t i = tid + 1024u * q;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) bx[q][k] = i < n ? primbox[(size_t)i * 6 + k] : 0.0f;
+  }
+  {  // bounds (k_bounds' values: exact min / max)
+    float v[12];
+    for (int k = 0; k < 3; ++k) {
+      v[k] = INFINITY;
+      v[3 + k] = -INFINITY;
+      v[6 + k] = INFINITY;
+      v[9 + k] = -INFINITY;
+    }
+#pragma unroll
+    for (int q = 0; q < kPer; ++q)
+      if (tid + 1024u * q < n)
+        for (int k = 0; k < 3; ++k) {
+          const float c = (bx[q][k] + bx[q][3 + k]) * 0.5f;
+          v[k] = fminf(v[k], c);
+          v[3 + k] = fmaxf(v[3 + k], c);
+          v[6 + k] = fminf(v[6 + k], bx[q][k]);
+          v[9 + k] = fmaxf(v[9 + k], bx[q][3 + k]);
+        }
+    for (int off = 32; off >= 1; off >>= 1)
+      for (int k = 0; k < 12; ++k) {
+        const float o = __shfl_xor(v[k], off, 64);
+        v[k] = (k % 6) < 3 ? fminf(v[k], o) : fmaxf(v[k], o);
+      }
+    if (lane == 0)
+      for (int k = 0; k < 12; ++k) s_red[k][w] = v[k];
+    __syncthreads();
+    if (tid < 12) {
+      const int k = (int)tid;
+      float r = s_red[k][0];
+      for (int j = 1; j < 16; ++j) r = (k % 6) < 3 ? fminf(r, s_red[k][j]) : fmaxf(r, s_red[k][j]);
+      s_cb[k] = r;
+      if (blockIdx.x == 0) cb_out[k] = r;
+    }
+    if (blockIdx.x == 0 && tid == 12) info[4] = 0u;  // k_mid_tree's frontier count
+    __syncthreads();
+  }
+  float lo[3], inv[3];
+  for (int k = 0; k < 3; ++k) {  // k_morton's quantisation, operation for operation
+    const float ext = s_cb[3 + k] - s_cb[k];
+    inv[k] = ext > 0.0f ? 1.0f / ext : 0.0f;
+    lo[k] = s_cb[k];
+  }
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const uint32_t i = tid + 1024u * q;
+    if (i < n) {
+      uint32_t c[3];
+      for (int k = 0; k < 3; ++k) c[k] = quantize10((bx[q][k] + bx[q][3 + k]) * 0.5f, lo[k], inv[k]);
+      const uint32_t code = (expand_bits10(c[0]) << 2) | (expand_bits10(c[1]) << 1) | expand_bits10(c[2]);
+      s_key[i] = ((uint64_t)code << 32) | i;
+    }
+  }
+  __syncthreads();
+  const uint32_t i = blockIdx.x * 64u + lane;
+  const uint64_t ki = i < n ? s_key[i] : ~0ull;
+  const uint32_t chunk = (((n + 15u) / 16u) + 7u) & ~7u, j0 = min(w * chunk, n), j1 = min(j0 + chunk, n);
+  uint32_t c = 0;
+  uint32_t j = j0;
+  for (; j + 8 <= j1; j += 8) {
+    uint64_t kk[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) kk[u] = s_key[j + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) c += kk[u] < ki ? 1u : 0u;
+  }
+  for (; j < j1; ++j) c += s_key[j] < ki ? 1u : 0u;
+  s_part[w][lane] = c;
+  __syncthreads();
+  if (i >= n) return;
+  if (w == 0) {
+    uint32_t rank = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) rank += s_part[q][lane];
+    keys_sorted[rank] = (uint32_t)(ki >> 32);
+    sorted[rank] = i;
+    if (tri_out) tri_out[rank] = tri_in[i];
+  } else if (w == 1 && i + 1 < n) {
+    dps[i] = kDpsUnbuilt;  // overwritten by whichever kernel builds split i
+  }
+}
+
+__global__ __launch_bounds__(kMidBlock) void k_mid_tree(uint32_t n, const uint32_t* __restrict__ keys_sorted,
+                                                        const uint32_t* __restrict__ sorted,
+                                                        const float* __restrict__ primbox, bool leaf_ref_is_prim,
+                                                        BinNode* __restrict__ bin, float4* __restrict__ dpc,
+                                                        uint32_t* __restrict__ dps, MidSlot* __restrict__ frontier,
+                                                        uint32_t* __restrict__ info) {
+  __shared__ uint64_t s_k[kMidBlock + 2];  // keys B - 1 .. B + S
+  __shared__ uint32_t s_flag[kMidBlock];
+  __shared__ MidSlot s_slot[kMidBlock];   // by position: the left child of split s at s, the right at s + 1
+  const uint32_t S = kMidBlock, B = blockIdx.x * S, tid = threadIdx.x;
+  for (uint32_t k = tid; k < S + 2; k += S) {
+    const int64_t p = (int64_t)B - 1 + (int64_t)k;
+    s_k[k] = (p >= 0 && p < (int64_t)n) ? (((uint64_t)keys_sorted[p] << 32) | (uint64_t)p) : 0ull;
+  }
+  s_flag[tid] = 0u;
+  __syncthreads();
+  const uint32_t i = B + tid;
+  if (i >= n) return;
+  MidSlot a;
+  {
+    const uint32_t prim = sorted[i];
+    const float* p = primbox + (size_t)prim * 6;
+    for (int k = 0; k < 6; ++k) a.b[k] = p[k];
+    for (int k = 0; k < 4; ++k) a.d[k] = 0.0f;
+    a.ref = leaf_ref_is_prim ? ~(int)prim : ~(int)i;
+    a.l = a.r = (int)i;
+    a.pad = 0;
+  }
+  const int ib = (int)B;
+  while (!(a.l == 0 && a.r == (int)n - 1)) {
+    const uint64_t kl = s_k[a.l - ib + 1], kr = s_k[a.r - ib + 1];
+    const int dl = a.l > 0 ? lcp64(s_k[a.l - ib], kl) : -1;
+    const int dr = a.r < (int)n - 1 ? lcp64(kr, s_k[a.r - ib + 2]) : -1;
+    const bool left = dr > dl;  // this node is the left child of the split at r
+    const int s = left ? a.r : a.l - 1;
+    const int q = left ? dr : dl;
+    bool inside = s >= ib && s + 1 < ib + (int)S;
+    if (inside) {
+      const uint64_t ks = left ? kr : s_k[s - ib + 1];
+      inside = (B == 0 || lcp64(ks, s_k[0]) < q) && (B + S >= n || lcp64(ks, s_k[S + 1]) < q);
+    }
+    if (!inside) {  // the parent crosses the block: the collapse workgroup climbs on from here
+      const uint32_t f = __hip_atomic_fetch_add(&info[4], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      frontier[f] = a;
+      return;
+    }
+    const int pos = (left ? s : s + 1) - ib;
+    s_slot[pos] = a;
+    const uint32_t old = __hip_atomic_fetch_add(&s_flag[s - ib], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (old == 0) return;
+    const MidSlot o = s_slot[(left ? s + 1 : s) - ib];
+    mid_join(s, left, a, o, bin, dpc, dps);
+  }
+  info[3] = (uint32_t)a.ref;  // the whole tree inside one block: the root's binary index
+}
+
+__global__ void k_mid_expand(int nbin, const BinNode* __restrict__ bin, const float4* __restrict__ dpc,
+                             const uint32_t* __restrict__ dps, Exp4* __restrict__ exp, uint2* __restrict__ e16,
+                             bool blas) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nbin || dps[i] == kDpsUnbuilt) return;  // top nodes: expanded by k_mid_collapse
+  Exp4 e;
+  e.cnt = wide_slots_dp(bin, dpc, dps, i, e.ref, e.box, blas);
+  e.pad[0] = e.pad[1] = e.pad[2] = 0;
+  exp[i] = e;
+  uint32_t h[4];
+  for (int j = 0; j < 4; ++j) h[j] = j >= e.cnt ? kMidEmpty : e.ref[j] >= 0 ? (uint32_t)e.ref[j] : kMidLeaf;
+  e16[i] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+}
+
+__global__ __launch_bounds__(1024) void k_mid_collapse(uint32_t n, const uint32_t* __restrict__ keys_sorted,
+                                                       const MidSlot* __restrict__ frontier, BinNode* bin,
+                                                       float4* dpc, uint32_t* dps, Exp4* exp,
+                                                       const uint2* __restrict__ e16, uint16_t* __restrict__ order_out,
+                                                       uint16_t* __restrict__ bfs_out, uint32_t* __restrict__ info,
+                                                       bool blas) {
+  // phase A (top climb): keys | arrival words | payload slots; afterwards the same bytes hold the
+  // 16-bit child lists, the BFS order / index maps and the stack sums
+  constexpr size_t kA = kMidMax * 8 + kMidMax * 4 + kMidTopSlots * sizeof(MidSlot);
+  constexpr size_t kD = kMidMax * 8 + 3 * kMidMax * 2;
+  __shared__ __attribute__((aligned(16))) unsigned char s_raw[kA > kD ? kA : kD];
+  __shared__ uint16_t s_top[kMidTopSlots];
+  __shared__ uint32_t s_ntop, s_nslot, s_root;
+  __shared__ uint32_t s_w[kFusedWaves];
+  __shared__ int s_maxstack;
+  const int tid = (int)threadIdx.x;
+  const int nbin = (int)n - 1;
+#if RT_BUILD_TIMING
+  uint64_t bt[4];
+  bt[0] = __builtin_amdgcn_s_memtime();
+#define RT_BT(k) bt[k] = __builtin_amdgcn_s_memtime()
+#else
+#define RT_BT(k) (void)0
+#endif
+  const uint32_t nf = info[4];
+  if (nf > 0) {
+    uint64_t* s_k = (uint64_t*)s_raw;
+    uint32_t* s_arr = (uint32_t*)(s_raw + kMidMax * 8);
+    MidSlot* s_pay = (MidSlot*)(s_raw + kMidMax * 8 + kMidMax * 4);
+    for (int k = tid; k < (int)n; k += 1024) s_k[k] = ((uint64_t)keys_sorted[k] << 32) | (uint64_t)k;
+    for (int k = tid; k < nbin; k += 1024) s_arr[k] = 0u;
+    if (tid == 0) s_ntop = s_nslot = 0u;
+    __syncthreads();
+    for (uint32_t f = (uint32_t)tid; f < nf; f += 1024u) {
+      MidSlot a = frontier[f];
+      while (!(a.l == 0 && a.r == (int)n - 1)) {
+        const int dl = a.l > 0 ? lcp64(s_k[a.l - 1], s_k[a.l]) : -1;
+        const int dr = a.r < (int)n - 1 ? lcp64(s_k[a.r], s_k[a.r + 1]) : -1;
+        const bool left = dr > dl;
+        const int s = left ? a.r : a.l - 1;
+        // each arrival parks its record in a fresh slot and swaps the slot (+1) into the split's
+        // word: the second arrival gets the first's slot back
+        const uint32_t mine = __hip_atomic_fetch_add(&s_nslot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        s_pay[mine] = a;
+        const uint32_t other =
+            __hip_atomic_exchange(&s_arr[s], mine + 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (other == 0u) break;
+        const MidSlot o = s_pay[other - 1u];
+        mid_join(s, left, a, o, bin, dpc, dps);
+        s_top[__hip_atomic_fetch_add(&s_ntop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)] = (uint16_t)s;
+        if (a.l == 0 && a.r == (int)n - 1) s_root = (uint32_t)s;
+      }
+    }
+    __threadfence_block();
+    __syncthreads();
+  } else if (tid == 0) {
+    s_ntop = 0u;
+    s_root = info[3];
+  }
+  __syncthreads();
+  RT_BT(1);
+  uint2* s_e = (uint2*)s_raw;                                  // per binary node: its wide node's slot refs
+  uint16_t* s_order = (uint16_t*)(s_raw + kMidMax * 8);        // BFS index -> binary node
+  uint16_t* s_bfs = s_order + kMidMax;                         // binary node -> BFS index
+  uint16_t* s_ps = s_bfs + kMidMax;                            // BFS index -> stack entries below
+  for (int k = tid; k < nbin; k += 1024) s_e[k] = e16[k];
+  const int ntop = (int)s_ntop;
+  __syncthreads();
+  // phase B: expansions of the top nodes (their descendants are all built now)
+  for (int k = tid; k < ntop; k += 1024) {
+    const int sn = (int)s_top[k];
+    Exp4 e;
+    e.cnt = wide_slots_dp(bin, dpc, dps, sn, e.ref, e.box, blas);
+    e.pad[0] = e.pad[1] = e.pad[2] = 0;
+    exp[sn] = e;
+    uint32_t h[4];
+    for (int j = 0; j < 4; ++j) h[j] = j >= e.cnt ? kMidEmpty : e.ref[j] >= 0 ? (uint32_t)e.ref[j] : kMidLeaf;
+    s_e[sn] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+  }
+  const int root = min((int)s_root, nbin - 1);  // (a root outside the tree would be a bug)
+  __threadfence_block();
+  __syncthreads();
+  RT_BT(2);
+  if (tid == 0) {
+    s_order[0] = (uint16_t)root;
+    s_bfs[root] = 0;
+    s_ps[0] = 0;
+    s_maxstack = 0;
+  }
+  __syncthreads();
+  // phase C: BFS numbering, level by level
+  int lmax = 0, cur_n = 1, base = 0, depth = 0;
+  while (cur_n > 0) {
+    ++depth;
+    int next_total = 0;
+    for (int cs = 0; cs < cur_n; cs += 1024) {
+      const int i = cs + tid;
+      const bool valid = i < cur_n;
+      uint32_t h[4] = {kMidEmpty, kMidEmpty, kMidEmpty, kMidEmpty};
+      if (valid) {
+        const uint2 e = s_e[s_order[base + i]];
+        h[0] = e.x & 0xffffu;
+        h[1] = e.x >> 16;
+        h[2] = e.y & 0xffffu;
+        h[3] = e.y >> 16;
+      }
+      uint32_t m = 0, cnt = 0;
+      for (int j = 0; j < 4; ++j) {
+        m += h[j] < kMidLeaf ? 1u : 0u;
+        cnt += h[j] != kMidEmpty ? 1u : 0u;
+      }
+      uint32_t chunk_total;
+      const int excl = (int)block_excl_scan(m, s_w, &chunk_total);
+      if (valid) {
+        const int below = (int)s_ps[base + i] + (int)cnt - 1;
+        lmax = below > lmax ? below : lmax;
+        int o = base + cur_n + next_total + excl;
+        for (int j = 0; j < 4; ++j)
+          if (h[j] < kMidLeaf) {
+            s_order[o] = (uint16_t)h[j];
+            s_bfs[h[j]] = (uint16_t)o;
+            s_ps[o] = (uint16_t)below;
+            ++o;
+          }
+      }
+      next_total += (int)chunk_total;
+    }
+    __syncthreads();
+    base += cur_n;
+    cur_n = next_total;
+  }
+  RT_BT(3);
+  // the node writes run in k_mid_write (many workgroups): BFS order and index maps to HBM
+  for (int k = tid; k < base; k += 1024) order_out[k] = s_order[k];
+  for (int k = tid; k < nbin; k += 1024) bfs_out[k] = s_bfs[k];
+  atomicMax(&s_maxstack, lmax);
+  __syncthreads();
+  if (tid == 0) {
+    info[0] = (uint32_t)base;
+    info[1] = (uint32_t)depth;
+    info[2] = (uint32_t)s_maxstack;
+#if RT_BUILD_TIMING
+    printf("k_mid_collapse n=%u frontier %u top %d levels %d cycles: top-climb %lu expand %lu bfs %lu\n", n, nf, ntop,
+           depth, bt[1] - bt[0], bt[2] - bt[1], bt[3] - bt[2]);
+#endif
+  }
+#undef RT_BT
+}
+
+// Every 4-wide node in parallel (BFS index k): its wide root's expansion with the slot refs mapped to
+// BFS indices.
+__global__ void k_mid_write(const Exp4* __restrict__ exp, const uint16_t* __restrict__ order,
+                            const uint16_t* __restrict__ bfs, const uint32_t* __restrict__ info,
+                            Bvh4Node* __restrict__ out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= (int)info[0]) return;
+  const Exp4& e = exp[order[k]];
+  Bvh4Node nd;
+  uint32_t nvalid = 0, inner = 0;
+  nd.first_inner = 0;
+  for (int j = 0; j < 4; ++j) {
+    const float inf = __builtin_inff();
+    float b6[6] = {inf, inf, inf, inf, inf, inf};
+    int32_t r = kEmptyChild;
+    if (j < e.cnt && e.ref[j] != kEmptyChild) {
+      ++nvalid;
+      for (int q = 0; q < 6; ++q) b6[q] = e.box[j][q];
+      if (e.ref[j] >= 0) {
+        r = (int32_t)bfs[e.ref[j]];
+        if (!inner) nd.first_inner = r;
+        inner |= 1u << j;
+      } else {
+        r = e.ref[j];
+      }
+    }
+    nd.lox[j] = b6[0];
+    nd.loy[j] = b6[1];
+    nd.loz[j] = b6[2];
+    nd.hix[j] = b6[3];
+    nd.hiy[j] = b6[4];
+    nd.hiz[j] = b6[5];
+    nd.child[j] = r;
+  }
+  nd.count = nvalid;
+  nd.inner_mask = inner;
+  nd.entry_base = ((uint32_t)nd.first_inner << 8) | (inner << 4);
+  out[k] = nd;
+}
+
 __global__ void k_tri_setup(const float* __restrict__ vtx, const uint32_t* __restrict__ idx,
                             uint32_t ntri, TriRec* __restrict__ tris, float* __restrict__ box) {
   uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1279,6 +1727,24 @@ __global__ void k_inst_boxes(const InstanceRec* __restrict__ inst, const float* 
 
 inline unsigned grid1(uint32_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
+enum { kPathSmall = 0, kPathMid = 1, kPathMulti = 2 };
+
+// Which schedule builds n primitives (measured crossovers). RT_BUILD_PATH=small|mid|multi
+// in the environment forces one where it can hold n (A/B timing only; every schedule builds the
+// bitwise-identical tree).
+int build_path(uint32_t n) {
+  const char* f = getenv("RT_BUILD_PATH");
+  const bool small_ok = RT_FUSED_BUILD && n <= kFusedMax, mid_ok = RT_SAH_COLLAPSE && n >= 2 && n <= kMidMax;
+  if (f) {
+    if (!strcmp(f, "small") && small_ok) return kPathSmall;
+    if (!strcmp(f, "mid") && mid_ok) return kPathMid;
+    if (!strcmp(f, "multi")) return kPathMulti;
+  }
+  if (RT_MID_BUILD && mid_ok && n >= (uint32_t)RT_MID_MIN_N) return kPathMid;
+  if (small_ok && n <= (uint32_t)RT_FUSED_MAX_N) return kPathSmall;
+  return kPathMulti;
+}
+
 struct DevBuf {
   void* p = nullptr;
   ~DevBuf() {
@@ -1311,13 +1777,15 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
     return q;
   };
   const Part p_stats = part(12 * sizeof(float)), p_keys0 = part((size_t)n * 4), p_keys1 = part((size_t)n * 4),
-             p_vals1 = part((size_t)n * 4), p_hist = part((size_t)256 * nblocks * 4), p_info = part(12),
+             p_vals1 = part((size_t)n * 4), p_hist = part((size_t)256 * nblocks * 4), p_info = part(32),
              p_ps = part((size_t)nbin * 4), p_bin = part((size_t)nbin * sizeof(BinNode)), p_la = part((size_t)nbin * 4),
              p_lb = part((size_t)nbin * 4), p_child = part((size_t)nbin * 8), p_pint = part((size_t)nbin * 4),
              p_pleaf = part((size_t)n * 4), p_nbox = part((size_t)nbin * 24), p_flags = part((size_t)nbin * 4),
              p_dpc = part(RT_SAH_COLLAPSE ? (size_t)nbin * sizeof(float4) : 0),
              p_dps = part(RT_SAH_COLLAPSE ? (size_t)nbin * 4 : 0),
-             p_exp = part(RT_SAH_COLLAPSE ? (size_t)nbin * sizeof(Exp4) : 0);
+             p_exp = part(RT_SAH_COLLAPSE ? (size_t)nbin * sizeof(Exp4) : 0),
+             p_gslot = part((size_t)n * sizeof(MidSlot)), p_e16 = part((size_t)nbin * sizeof(uint2)),
+             p_order = part((size_t)nbin * 2), p_bfs = part((size_t)nbin * 2);
   DevBuf arena;
   RT_TRY(hipMalloc(&arena.p, total));
   char* A = (char*)arena.p;
@@ -1328,13 +1796,30 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
   View stats = at(p_stats), keys0 = at(p_keys0), keys1 = at(p_keys1), vals1 = at(p_vals1), hist = at(p_hist),
        info = at(p_info), ps = at(p_ps), bin = at(p_bin), la = at(p_la), lb = at(p_lb), child = at(p_child),
        pint = at(p_pint), pleaf = at(p_pleaf), nbox = at(p_nbox), flags = at(p_flags), dpc = at(p_dpc),
-       dps = at(p_dps), expd = at(p_exp);
+       dps = at(p_dps), expd = at(p_exp), gslot = at(p_gslot), e16 = at(p_e16), order = at(p_order),
+       bfsmap = at(p_bfs);
   hipEvent_t e0, e1;
   RT_TRY(hipEventCreate(&e0));
   RT_TRY(hipEventCreate(&e1));
   RT_TRY(hipEventRecord(e0, s));
   float* cb = (float*)stats.p;
-  if (RT_FUSED_BUILD && n <= (uint32_t)RT_FUSED_MAX_N) {
+  const int path = build_path(n);
+  if (path == kPathMid) {
+    k_mid_rank<<<grid1(n, 64), 1024, 0, s>>>(d_primbox, n, cb, (uint32_t*)keys0.p, d_sorted, (uint32_t*)dps.p,
+                                              (uint32_t*)info.p, d_tri_in, d_tri_out);
+    k_mid_tree<<<grid1(n, kMidBlock), kMidBlock, 0, s>>>(n, (const uint32_t*)keys0.p, d_sorted, d_primbox,
+                                                          leaf_ref_is_prim, (BinNode*)bin.p, (float4*)dpc.p,
+                                                          (uint32_t*)dps.p, (MidSlot*)gslot.p, (uint32_t*)info.p);
+    k_mid_expand<<<grid1(nbin, 256), 256, 0, s>>>((int)nbin, (const BinNode*)bin.p, (const float4*)dpc.p,
+                                                  (const uint32_t*)dps.p, (Exp4*)expd.p, (uint2*)e16.p,
+                                                  !leaf_ref_is_prim);
+    k_mid_collapse<<<1, 1024, 0, s>>>(n, (const uint32_t*)keys0.p, (const MidSlot*)gslot.p, (BinNode*)bin.p,
+                                      (float4*)dpc.p, (uint32_t*)dps.p, (Exp4*)expd.p, (const uint2*)e16.p,
+                                      (uint16_t*)order.p, (uint16_t*)bfsmap.p, (uint32_t*)info.p, !leaf_ref_is_prim);
+    k_mid_write<<<grid1(nbin, 256), 256, 0, s>>>((const Exp4*)expd.p, (const uint16_t*)order.p,
+                                                 (const uint16_t*)bfsmap.p, (const uint32_t*)info.p, d_nodes);
+    RT_TRY(hipGetLastError());
+  } else if (path == kPathSmall) {
     k_build_small<<<1, kFusedThreads, 0, s>>>(d_primbox, n, leaf_ref_is_prim, d_sorted, cb, (int*)pleaf.p,
                                               (float*)nbox.p, (float4*)dpc.p, (uint32_t*)dps.p, (BinNode*)bin.p,
                                               d_nodes, (uint32_t*)info.p, d_tri_in, d_tri_out);

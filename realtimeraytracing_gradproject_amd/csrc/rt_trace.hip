@@ -1129,6 +1129,12 @@ __device__ bool shadow_compact(const SceneView& sc, V3 P, V3 d, bool need, uint3
 #ifndef RT_WAVE_TIMES
 #define RT_WAVE_TIMES 0  // 1: every wave stores its start / end clock (diagnostics; tools/wave_times.py)
 #endif
+#ifndef RT_PRIO
+#define RT_PRIO 0  // 1: s_setprio(1) for every shadow phase; 2: by the primary walk's duration (A/B)
+#endif
+#ifndef RT_PRIO_T
+#define RT_PRIO_T 20000  // RT_PRIO 2: shader clocks of primary walk for priority 1 (2x: priority 2)
+#endif
 #ifndef RT_PHASE_TIMING
 #define RT_PHASE_TIMING 0  // 1: sampled waves printf s_memtime per phase (diagnostics only)
 #endif
@@ -1139,6 +1145,9 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
 #if RT_PHASE_TIMING
   uint64_t ph[6];
   ph[0] = __builtin_amdgcn_s_memtime();
+#endif
+#if RT_PRIO
+  const uint64_t t_start = __builtin_amdgcn_s_memtime();
 #endif
   V3 O[R], D[R], P[R], sd[R];
   HitRec hit[R], sh[R];
@@ -1262,6 +1271,17 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
     for (int r = 0; r < R; ++r) z += n[r].x;
     asm volatile("" ::"v"(z));  // the normals are complete here
     ph[2] = __builtin_amdgcn_s_memtime();
+  }
+#endif
+#if RT_PRIO
+  // wave priority for the shadow walks (A/B study): waves whose primary walk was long are the
+  // launch's long waves; give them the SIMD's issue slots first
+  if (RT_PRIO == 1) {
+    __builtin_amdgcn_s_setprio(1);
+  } else {
+    const uint64_t el = __builtin_amdgcn_s_memtime() - t_start;
+    if (el > 2u * (uint64_t)RT_PRIO_T) __builtin_amdgcn_s_setprio(2);
+    else if (el > (uint64_t)RT_PRIO_T) __builtin_amdgcn_s_setprio(1);
   }
 #endif
   for (uint32_t l = 0; l < fp.nlights; ++l) {

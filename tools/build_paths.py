@@ -1,0 +1,55 @@
+"""Build time of the three LBVH schedules (one-workgroup `small`, five-launch `mid`, `multi`-kernel)
+on random triangle soups and the reference meshes, in one process (RT_BUILD_PATH selects the schedule
+per build), with the trees of the schedules checked bitwise equal:
+  python tools/build_paths.py --sizes 2,64,1024,3072,4968,6320,8192 --reps 15"""
+import argparse
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+import realtimeraytracing_gradproject_amd as rt  # noqa: E402
+from realtimeraytracing_gradproject_amd import scenes  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--sizes", default="2,64,256,1024,2048,3072,4096,8192")
+ap.add_argument("--reps", type=int, default=15)
+ap.add_argument("--paths", default="small,mid,multi")
+ap.add_argument("--lib", default=rt.LIB_PATH)
+a = ap.parse_args()
+
+cases = []
+for n in [int(x) for x in a.sizes.split(",") if x]:
+    rng = np.random.default_rng(n)
+    v = np.zeros((n * 3, 6), np.float32)
+    c0 = rng.uniform(-5, 5, size=(n, 1, 3))
+    v[:, :3] = (c0 + rng.uniform(-0.2, 0.2, size=(n, 3, 3))).reshape(-1, 3).astype(np.float32)
+    cases.append((f"soup {n}", v, None))
+for m in ("teapot", "rabbit"):
+    v, i = scenes.load_model(m)
+    cases.append((m, v, i))
+
+c = rt.Context(0, library=rt._load(a.lib))
+for name, v, i in cases:
+    row, ref = [f"{name:12s}"], None
+    for p in a.paths.split(","):
+        os.environ["RT_BUILD_PATH"] = p
+        b = c.blas_build(v, i)
+        ms = []
+        for _ in range(a.reps):
+            c.blas_rebuild(b, v, i)
+            ms.append(c.blas_info(b).build_ms)
+        nodes, tris = c.blas_export(b)
+        same = ""
+        if ref is None:
+            ref = (nodes, tris)
+        elif not (np.array_equal(ref[0], nodes) and np.array_equal(ref[1], tris)):
+            same = " TREE DIFFERS"
+        row.append(f"{p} {statistics.median(ms):.4f}{same}")
+    print("  ".join(row), flush=True)
+os.environ.pop("RT_BUILD_PATH", None)
+c.close()

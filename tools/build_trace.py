@@ -13,10 +13,10 @@ START = ("k_tri_setup", "k_inst_boxes")
 
 
 def short(name):
-    n = name.split("(")[0]
+    n = name
     for p in ("rt::(anonymous namespace)::", "void "):
         n = n.replace(p, "")
-    return n
+    return n.split("(")[0]
 
 
 def main(paths):
@@ -30,6 +30,8 @@ def main(paths):
     builds, cur = [], None
     for s, e, n in rows:
         if n.startswith(START) or cur is None:
+            if "fillBuffer" in n:
+                continue
             cur = []
             builds.append(cur)
         if "k_trace" in n or "k_raster" in n:
