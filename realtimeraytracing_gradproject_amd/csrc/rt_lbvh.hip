@@ -1263,6 +1263,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_build_small(
 // acknowledgement and an agent-scope atomic per level: ~3 memory round trips) is not used: the
 // block-crossing chains from the block boundaries to the root were the critical path with it.
 // ------------------------------------------------------------------------------------------
+#define RT_KCONST __attribute__((address_space(4)))
 constexpr uint32_t kMidMax = 8192;
 constexpr int kMidBlock = 1024;       // leaves per k_mid_tree workgroup
 constexpr int kMidTopSlots = 1024;    // top-climb payload slots: >= 2 x (kMidMax / kMidBlock - 1) x 64
@@ -1316,11 +1317,11 @@ __device__ __forceinline__ void mid_join(int s, bool left, MidSlot& a, const Mid
 }
 
 __global__ __launch_bounds__(1024) void k_mid_rank(const float* __restrict__ primbox, uint32_t n,
-                                                   float* __restrict__ cb_out, uint32_t* __restrict__ keys_sorted,
-                                                   uint32_t* __restrict__ sorted, uint32_t* __restrict__ dps,
-                                                   uint32_t* __restrict__ info, const TriRec* __restrict__ tri_in,
-                                                   TriRec* __restrict__ tri_out) {
-  __shared__ uint64_t s_key[kMidMax];
+                                                   float* __restrict__ cb_out, uint64_t* keys64,
+                                                   uint32_t* __restrict__ keys_sorted, uint32_t* __restrict__ sorted,
+                                                   float* __restrict__ sbox,
+                                                   uint32_t* __restrict__ dps, uint32_t* __restrict__ info,
+                                                   const TriRec* __restrict__ tri_in, TriRec* __restrict__ tri_out) {
   __shared__ uint32_t s_part[16][64];
   __shared__ float s_red[12][16];
   __shared__ float s_cb[12];
@@ -1328,10 +1329,10 @@ __global__ __launch_bounds__(1024) void k_mid_rank(const float* __restrict__ pri
   constexpr int kPer = kMidMax / 1024;
   float bx[kPer][6];
 #pragma unroll
-  for (int q = 0; q < kPer; ++q) {
-    const uint32_t i = tid + 1024u * q;
+  for (int q = 0; q < kPer; ++q) {  // past n: copies of the last box (the min / max do not change)
+    const uint32_t i = min(tid + 1024u * q, n - 1u);
 #pragma unroll
-    for (int k = 0; k < 6; ++k) bx[q][k] = i < n ? primbox[(size_t)i * 6 + k] : 0.0f;
+    for (int k = 0; k < 6; ++k) bx[q][k] = primbox[(size_t)i * 6 + k];
   }
   {  // bounds (k_bounds' values: exact min / max)
     float v[12];
@@ -1343,8 +1344,7 @@ __global__ __launch_bounds__(1024) void k_mid_rank(const float* __restrict__ pri
     }
 #pragma unroll
     for (int q = 0; q < kPer; ++q)
-      if (tid + 1024u * q < n)
-        for (int k = 0; k < 3; ++k) {
+      for (int k = 0; k < 3; ++k) {
           const float c = (bx[q][k] + bx[q][3 + k]) * 0.5f;
           v[k] = fminf(v[k], c);
           v[3 + k] = fmaxf(v[3 + k], c);
@@ -1375,6 +1375,11 @@ __global__ __launch_bounds__(1024) void k_mid_rank(const float* __restrict__ pri
     inv[k] = ext > 0.0f ? 1.0f / ext : 0.0f;
     lo[k] = s_cb[k];
   }
+  // every workgroup computes every key; all of them store the same values to keys64 (a benign
+  // race of identical data), read back through the scalar cache: the j keys are wave-uniform, so
+  // they travel as SGPR operands instead of through the LDS / L1 return path to 64 lanes
+  uint64_t ki = ~0ull;
+  const uint32_t iq = blockIdx.x * 64u + lane;  // this lane's key
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {
     const uint32_t i = tid + 1024u * q;
@@ -1382,25 +1387,33 @@ __global__ __launch_bounds__(1024) void k_mid_rank(const float* __restrict__ pri
       uint32_t c[3];
       for (int k = 0; k < 3; ++k) c[k] = quantize10((bx[q][k] + bx[q][3 + k]) * 0.5f, lo[k], inv[k]);
       const uint32_t code = (expand_bits10(c[0]) << 2) | (expand_bits10(c[1]) << 1) | expand_bits10(c[2]);
-      s_key[i] = ((uint64_t)code << 32) | i;
+      keys64[i] = ((uint64_t)code << 32) | i;
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const uint32_t i = blockIdx.x * 64u + lane;
-  const uint64_t ki = i < n ? s_key[i] : ~0ull;
-  const uint32_t chunk = (((n + 15u) / 16u) + 7u) & ~7u, j0 = min(w * chunk, n), j1 = min(j0 + chunk, n);
+  const RT_KCONST uint64_t* kc = (const RT_KCONST uint64_t*)keys64;
+  asm volatile("" : "+s"(kc));  // the scalar loads stay behind the barrier
+  if (iq < n) ki = kc[iq];
+  const uint32_t wu = (uint32_t)__builtin_amdgcn_readfirstlane((int)w);  // wave-uniform: scalar j loop
+  const uint32_t chunk = (((n + 15u) / 16u) + 31u) & ~31u, j0 = min(wu * chunk, n), j1 = min(j0 + chunk, n);
   uint32_t c = 0;
   uint32_t j = j0;
-  for (; j + 8 <= j1; j += 8) {
-    uint64_t kk[8];
+  typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+  for (; j + 32 <= j1; j += 32) {  // 8 keys per s_load_dwordx16, four loads in flight (the keys
+                                   // were just written: scalar-cache misses, L2 latency each)
+    u32x16 kv[4];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) kk[u] = s_key[j + u];
+    for (int h = 0; h < 4; ++h) kv[h] = *(const RT_KCONST u32x16*)(kc + j + 8 * h);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) c += kk[u] < ki ? 1u : 0u;
+    for (int h = 0; h < 4; ++h)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) c += (((uint64_t)kv[h][2 * u + 1] << 32) | kv[h][2 * u]) < ki ? 1u : 0u;
   }
-  for (; j < j1; ++j) c += s_key[j] < ki ? 1u : 0u;
+  for (; j < j1; ++j) c += kc[j] < ki ? 1u : 0u;
   s_part[w][lane] = c;
   __syncthreads();
+  const uint32_t i = iq;
   if (i >= n) return;
   if (w == 0) {
     uint32_t rank = 0;
@@ -1408,6 +1421,7 @@ __global__ __launch_bounds__(1024) void k_mid_rank(const float* __restrict__ pri
     for (int q = 0; q < 16; ++q) rank += s_part[q][lane];
     keys_sorted[rank] = (uint32_t)(ki >> 32);
     sorted[rank] = i;
+    for (int k = 0; k < 6; ++k) sbox[(size_t)rank * 6 + k] = primbox[(size_t)i * 6 + k];
     if (tri_out) tri_out[rank] = tri_in[i];
   } else if (w == 1 && i + 1 < n) {
     dps[i] = kDpsUnbuilt;  // overwritten by whichever kernel builds split i
@@ -1416,7 +1430,7 @@ __global__ __launch_bounds__(1024) void k_mid_rank(const float* __restrict__ pri
 
 __global__ __launch_bounds__(kMidBlock) void k_mid_tree(uint32_t n, const uint32_t* __restrict__ keys_sorted,
                                                         const uint32_t* __restrict__ sorted,
-                                                        const float* __restrict__ primbox, bool leaf_ref_is_prim,
+                                                        const float* __restrict__ sbox, bool leaf_ref_is_prim,
                                                         BinNode* __restrict__ bin, float4* __restrict__ dpc,
                                                         uint32_t* __restrict__ dps, MidSlot* __restrict__ frontier,
                                                         uint32_t* __restrict__ info) {
@@ -1435,7 +1449,7 @@ __global__ __launch_bounds__(kMidBlock) void k_mid_tree(uint32_t n, const uint32
   MidSlot a;
   {
     const uint32_t prim = sorted[i];
-    const float* p = primbox + (size_t)prim * 6;
+    const float* p = sbox + (size_t)i * 6;  // the leaf boxes in leaf order (k_mid_rank)
     for (int k = 0; k < 6; ++k) a.b[k] = p[k];
     for (int k = 0; k < 4; ++k) a.d[k] = 0.0f;
     a.ref = leaf_ref_is_prim ? ~(int)prim : ~(int)i;
@@ -1443,18 +1457,18 @@ __global__ __launch_bounds__(kMidBlock) void k_mid_tree(uint32_t n, const uint32
     a.pad = 0;
   }
   const int ib = (int)B;
+  const uint64_t kb0 = s_k[0], kb1 = s_k[S + 1];  // keys B - 1 and B + S
   while (!(a.l == 0 && a.r == (int)n - 1)) {
-    const uint64_t kl = s_k[a.l - ib + 1], kr = s_k[a.r - ib + 1];
-    const int dl = a.l > 0 ? lcp64(s_k[a.l - ib], kl) : -1;
-    const int dr = a.r < (int)n - 1 ? lcp64(kr, s_k[a.r - ib + 2]) : -1;
+    // the four keys around the node in one LDS round trip (past the ends: unused zeros)
+    const uint64_t klm = s_k[a.l - ib], kl = s_k[a.l - ib + 1], kr = s_k[a.r - ib + 1], krp = s_k[a.r - ib + 2];
+    const int dl = a.l > 0 ? lcp64(klm, kl) : -1;
+    const int dr = a.r < (int)n - 1 ? lcp64(kr, krp) : -1;
     const bool left = dr > dl;  // this node is the left child of the split at r
     const int s = left ? a.r : a.l - 1;
     const int q = left ? dr : dl;
-    bool inside = s >= ib && s + 1 < ib + (int)S;
-    if (inside) {
-      const uint64_t ks = left ? kr : s_k[s - ib + 1];
-      inside = (B == 0 || lcp64(ks, s_k[0]) < q) && (B + S >= n || lcp64(ks, s_k[S + 1]) < q);
-    }
+    const uint64_t ks = left ? kr : klm;  // key s
+    const bool inside = s >= ib && s + 1 < ib + (int)S && (B == 0 || lcp64(ks, kb0) < q) &&
+                        (B + S >= n || lcp64(ks, kb1) < q);
     if (!inside) {  // the parent crosses the block: the collapse workgroup climbs on from here
       const uint32_t f = __hip_atomic_fetch_add(&info[4], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       frontier[f] = a;
@@ -1462,7 +1476,13 @@ __global__ __launch_bounds__(kMidBlock) void k_mid_tree(uint32_t n, const uint32
     }
     const int pos = (left ? s : s + 1) - ib;
     s_slot[pos] = a;
-    const uint32_t old = __hip_atomic_fetch_add(&s_flag[s - ib], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    // LDS executes one wave's operations in order and the sibling's record is read only after its
+    // arrival was observed: a relaxed LDS atomic between compiler barriers orders the hand-off. An
+    // acquire / release atomic would also wait for this thread's outstanding HBM stores (bin, DP)
+    // at every level.
+    asm volatile("" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(&s_flag[s - ib], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
     if (old == 0) return;
     const MidSlot o = s_slot[(left ? s + 1 : s) - ib];
     mid_join(s, left, a, o, bin, dpc, dps);
@@ -1497,7 +1517,7 @@ __global__ __launch_bounds__(1024) void k_mid_collapse(uint32_t n, const uint32_
   __shared__ __attribute__((aligned(16))) unsigned char s_raw[kA > kD ? kA : kD];
   __shared__ uint16_t s_top[kMidTopSlots];
   __shared__ uint32_t s_ntop, s_nslot, s_root;
-  __shared__ uint32_t s_w[kFusedWaves];
+  __shared__ uint32_t s_w[2 * kFusedWaves];
   __shared__ int s_maxstack;
   const int tid = (int)threadIdx.x;
   const int nbin = (int)n - 1;
@@ -1509,32 +1529,47 @@ __global__ __launch_bounds__(1024) void k_mid_collapse(uint32_t n, const uint32_
 #define RT_BT(k) (void)0
 #endif
   const uint32_t nf = info[4];
+  // the child lists of every node k_mid_expand built, loaded now (into registers: the LDS they go to
+  // holds the top climb's keys and slots first), in flight during the top climb
+  constexpr int kPer = kMidMax / 1024;
+  uint2 ev[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) ev[q] = e16[min(tid + 1024 * q, nbin - 1)];
   if (nf > 0) {
     uint64_t* s_k = (uint64_t*)s_raw;
     uint32_t* s_arr = (uint32_t*)(s_raw + kMidMax * 8);
     MidSlot* s_pay = (MidSlot*)(s_raw + kMidMax * 8 + kMidMax * 4);
+    MidSlot a0;
+    if ((uint32_t)tid < nf) a0 = frontier[tid];
     for (int k = tid; k < (int)n; k += 1024) s_k[k] = ((uint64_t)keys_sorted[k] << 32) | (uint64_t)k;
     for (int k = tid; k < nbin; k += 1024) s_arr[k] = 0u;
     if (tid == 0) s_ntop = s_nslot = 0u;
     __syncthreads();
     for (uint32_t f = (uint32_t)tid; f < nf; f += 1024u) {
-      MidSlot a = frontier[f];
+      MidSlot a = f == (uint32_t)tid ? a0 : frontier[f];
       while (!(a.l == 0 && a.r == (int)n - 1)) {
-        const int dl = a.l > 0 ? lcp64(s_k[a.l - 1], s_k[a.l]) : -1;
-        const int dr = a.r < (int)n - 1 ? lcp64(s_k[a.r], s_k[a.r + 1]) : -1;
+        const uint64_t klm = s_k[max(a.l - 1, 0)], kl = s_k[a.l], kr = s_k[a.r], krp = s_k[min(a.r + 1, (int)n - 1)];
+        const int dl = a.l > 0 ? lcp64(klm, kl) : -1;
+        const int dr = a.r < (int)n - 1 ? lcp64(kr, krp) : -1;
         const bool left = dr > dl;
         const int s = left ? a.r : a.l - 1;
         // each arrival parks its record in a fresh slot and swaps the slot (+1) into the split's
         // word: the second arrival gets the first's slot back
         const uint32_t mine = __hip_atomic_fetch_add(&s_nslot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         s_pay[mine] = a;
+        asm volatile("" ::: "memory");  // LDS order suffices (see k_mid_tree): no wait for HBM stores
         const uint32_t other =
-            __hip_atomic_exchange(&s_arr[s], mine + 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_exchange(&s_arr[s], mine + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        asm volatile("" ::: "memory");
         if (other == 0u) break;
         const MidSlot o = s_pay[other - 1u];
         mid_join(s, left, a, o, bin, dpc, dps);
         s_top[__hip_atomic_fetch_add(&s_ntop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)] = (uint16_t)s;
         if (a.l == 0 && a.r == (int)n - 1) s_root = (uint32_t)s;
+#if RT_BUILD_TIMING
+        if (a.l == 0 && a.r == (int)n - 1)
+          printf("  top climb: root thread %d done at %lu (start %lu)\n", tid, __builtin_amdgcn_s_memtime() - bt[0], 0ul);
+#endif
       }
     }
     __threadfence_block();
@@ -1549,7 +1584,9 @@ __global__ __launch_bounds__(1024) void k_mid_collapse(uint32_t n, const uint32_
   uint16_t* s_order = (uint16_t*)(s_raw + kMidMax * 8);        // BFS index -> binary node
   uint16_t* s_bfs = s_order + kMidMax;                         // binary node -> BFS index
   uint16_t* s_ps = s_bfs + kMidMax;                            // BFS index -> stack entries below
-  for (int k = tid; k < nbin; k += 1024) s_e[k] = e16[k];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q)
+    if (tid + 1024 * q < nbin) s_e[tid + 1024 * q] = ev[q];
   const int ntop = (int)s_ntop;
   __syncthreads();
   // phase B: expansions of the top nodes (their descendants are all built now)
@@ -1574,46 +1611,65 @@ __global__ __launch_bounds__(1024) void k_mid_collapse(uint32_t n, const uint32_
     s_maxstack = 0;
   }
   __syncthreads();
-  // phase C: BFS numbering, level by level
+  // phase C: BFS numbering, level by level, two barriers per level. A thread takes `per` consecutive
+  // nodes of the level; the exclusive sum of their internal-child counts (<= 32: six bits) is
+  // formed from one ballot per bit (popcount of the lower lanes), the waves' totals through LDS.
   int lmax = 0, cur_n = 1, base = 0, depth = 0;
+#if RT_BUILD_TIMING
+  uint64_t lvt[16];
+  lvt[0] = __builtin_amdgcn_s_memtime();
+#endif
+  const uint32_t lane = (uint32_t)tid & 63u, wv = (uint32_t)tid >> 6;
+  const uint64_t lower = lane == 0 ? 0ull : (~0ull >> (64u - lane));
   while (cur_n > 0) {
-    ++depth;
-    int next_total = 0;
-    for (int cs = 0; cs < cur_n; cs += 1024) {
-      const int i = cs + tid;
-      const bool valid = i < cur_n;
-      uint32_t h[4] = {kMidEmpty, kMidEmpty, kMidEmpty, kMidEmpty};
-      if (valid) {
-        const uint2 e = s_e[s_order[base + i]];
-        h[0] = e.x & 0xffffu;
-        h[1] = e.x >> 16;
-        h[2] = e.y & 0xffffu;
-        h[3] = e.y >> 16;
-      }
-      uint32_t m = 0, cnt = 0;
-      for (int j = 0; j < 4; ++j) {
-        m += h[j] < kMidLeaf ? 1u : 0u;
-        cnt += h[j] != kMidEmpty ? 1u : 0u;
-      }
-      uint32_t chunk_total;
-      const int excl = (int)block_excl_scan(m, s_w, &chunk_total);
-      if (valid) {
-        const int below = (int)s_ps[base + i] + (int)cnt - 1;
-        lmax = below > lmax ? below : lmax;
-        int o = base + cur_n + next_total + excl;
-        for (int j = 0; j < 4; ++j)
-          if (h[j] < kMidLeaf) {
-            s_order[o] = (uint16_t)h[j];
-            s_bfs[h[j]] = (uint16_t)o;
-            s_ps[o] = (uint16_t)below;
-            ++o;
-          }
-      }
-      next_total += (int)chunk_total;
+    const int per = (cur_n + 1023) / 1024;  // <= 8
+    const int i0 = min(tid * per, cur_n), i1 = min(i0 + per, cur_n);
+    uint32_t msum = 0;
+    for (int i = i0; i < i1; ++i) {
+      const uint2 e = s_e[s_order[base + i]];
+      msum += ((e.x & 0xffffu) < kMidLeaf ? 1u : 0u) + ((e.x >> 16) < kMidLeaf ? 1u : 0u) +
+              ((e.y & 0xffffu) < kMidLeaf ? 1u : 0u) + ((e.y >> 16) < kMidLeaf ? 1u : 0u);
     }
+    uint32_t pre = 0, wtot = 0;
+#pragma unroll
+    for (int bit = 0; bit < 6; ++bit) {
+      const uint64_t bal = __ballot((msum >> bit) & 1u);
+      pre += (uint32_t)__popcll(bal & lower) << bit;
+      wtot += (uint32_t)__popcll(bal) << bit;
+    }
+    uint32_t* s_wl = s_w + (depth & 1) * kFusedWaves;  // double-buffered: no barrier before the write
+    if (lane == 0) s_wl[wv] = wtot;
     __syncthreads();
+    uint32_t woff = 0, total = 0;
+#pragma unroll
+    for (int k = 0; k < kFusedWaves; ++k) {
+      const uint32_t c = s_wl[k];
+      woff += (uint32_t)k < wv ? c : 0u;
+      total += c;
+    }
+    int o = base + cur_n + (int)(woff + pre);
+    for (int i = i0; i < i1; ++i) {
+      const uint2 e = s_e[s_order[base + i]];
+      const uint32_t h[4] = {e.x & 0xffffu, e.x >> 16, e.y & 0xffffu, e.y >> 16};
+      uint32_t cnt = 0;
+      for (int j = 0; j < 4; ++j) cnt += h[j] != kMidEmpty ? 1u : 0u;
+      const int below = (int)s_ps[base + i] + (int)cnt - 1;
+      lmax = below > lmax ? below : lmax;
+      for (int j = 0; j < 4; ++j)
+        if (h[j] < kMidLeaf) {
+          s_order[o] = (uint16_t)h[j];
+          s_bfs[h[j]] = (uint16_t)o;
+          s_ps[o] = (uint16_t)below;
+          ++o;
+        }
+    }
+    ++depth;
+    __syncthreads();
+#if RT_BUILD_TIMING
+    if (depth < 16) lvt[depth] = __builtin_amdgcn_s_memtime();
+#endif
     base += cur_n;
-    cur_n = next_total;
+    cur_n = (int)total;
   }
   RT_BT(3);
   // the node writes run in k_mid_write (many workgroups): BFS order and index maps to HBM
@@ -1628,6 +1684,7 @@ __global__ __launch_bounds__(1024) void k_mid_collapse(uint32_t n, const uint32_
 #if RT_BUILD_TIMING
     printf("k_mid_collapse n=%u frontier %u top %d levels %d cycles: top-climb %lu expand %lu bfs %lu\n", n, nf, ntop,
            depth, bt[1] - bt[0], bt[2] - bt[1], bt[3] - bt[2]);
+    for (int k = 1; k < depth && k < 16; ++k) printf("  bfs level %d: %lu\n", k, lvt[k] - lvt[k - 1]);
 #endif
   }
 #undef RT_BT
@@ -1785,7 +1842,8 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
              p_dps = part(RT_SAH_COLLAPSE ? (size_t)nbin * 4 : 0),
              p_exp = part(RT_SAH_COLLAPSE ? (size_t)nbin * sizeof(Exp4) : 0),
              p_gslot = part((size_t)n * sizeof(MidSlot)), p_e16 = part((size_t)nbin * sizeof(uint2)),
-             p_order = part((size_t)nbin * 2), p_bfs = part((size_t)nbin * 2);
+             p_order = part((size_t)nbin * 2), p_bfs = part((size_t)nbin * 2),
+             p_k64 = part((size_t)n * 8), p_sbox = part((size_t)n * 24);
   DevBuf arena;
   RT_TRY(hipMalloc(&arena.p, total));
   char* A = (char*)arena.p;
@@ -1797,7 +1855,7 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
        info = at(p_info), ps = at(p_ps), bin = at(p_bin), la = at(p_la), lb = at(p_lb), child = at(p_child),
        pint = at(p_pint), pleaf = at(p_pleaf), nbox = at(p_nbox), flags = at(p_flags), dpc = at(p_dpc),
        dps = at(p_dps), expd = at(p_exp), gslot = at(p_gslot), e16 = at(p_e16), order = at(p_order),
-       bfsmap = at(p_bfs);
+       bfsmap = at(p_bfs), k64 = at(p_k64), sbox = at(p_sbox);
   hipEvent_t e0, e1;
   RT_TRY(hipEventCreate(&e0));
   RT_TRY(hipEventCreate(&e1));
@@ -1805,9 +1863,11 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
   float* cb = (float*)stats.p;
   const int path = build_path(n);
   if (path == kPathMid) {
-    k_mid_rank<<<grid1(n, 64), 1024, 0, s>>>(d_primbox, n, cb, (uint32_t*)keys0.p, d_sorted, (uint32_t*)dps.p,
-                                              (uint32_t*)info.p, d_tri_in, d_tri_out);
-    k_mid_tree<<<grid1(n, kMidBlock), kMidBlock, 0, s>>>(n, (const uint32_t*)keys0.p, d_sorted, d_primbox,
+    k_mid_rank<<<grid1(n, 64), 1024, 0, s>>>(d_primbox, n, cb, (uint64_t*)k64.p, (uint32_t*)keys0.p, d_sorted,
+                                              (float*)sbox.p, (uint32_t*)dps.p, (uint32_t*)info.p, d_tri_in,
+                                              d_tri_out);
+    k_mid_tree<<<grid1(n, kMidBlock), kMidBlock, 0, s>>>(n, (const uint32_t*)keys0.p, d_sorted,
+                                                          (const float*)sbox.p,
                                                           leaf_ref_is_prim, (BinNode*)bin.p, (float4*)dpc.p,
                                                           (uint32_t*)dps.p, (MidSlot*)gslot.p, (uint32_t*)info.p);
     k_mid_expand<<<grid1(nbin, 256), 256, 0, s>>>((int)nbin, (const BinNode*)bin.p, (const float4*)dpc.p,
