@@ -78,8 +78,10 @@ def test_blas_bitwise_equal_to_oracle(model):
     c.close()
 
 
-# <= 8192: the one-workgroup build (k_build_small); 8193 and 20000: the multi-kernel build
-@pytest.mark.parametrize("ntri", [1, 2, 3, 7, 63, 64, 65, 1000, 1025, 5000, 8191, 8192, 8193, 20000])
+# 1: the one-workgroup build (k_build_small); 2 .. 8192: the four-launch build (k_mid_*, block
+# boundaries at 1024-leaf multiples); 8193 and 20000: the multi-kernel build
+@pytest.mark.parametrize("ntri", [1, 2, 3, 7, 63, 64, 65, 1000, 1023, 1024, 1025, 2049, 5000, 8191, 8192, 8193,
+                                  20000])
 def test_blas_edge_sizes(ntri):
     rng = np.random.default_rng(1234 + ntri)
     v = np.zeros((ntri * 3, 6), np.float32)
@@ -94,6 +96,34 @@ def test_blas_edge_sizes(ntri):
     assert np.array_equal(gn, on)
     assert np.array_equal(gt, ot)
     c.close()
+
+
+@pytest.mark.parametrize("ntri", [2, 100, 1025, 3000, 8192])
+def test_build_schedules_bitwise_equal(ntri, monkeypatch):
+    # every schedule that can hold n (RT_BUILD_PATH: one workgroup, four launches, multi-kernel)
+    # builds the oracle's tree, BLAS and TLAS alike
+    rng = np.random.default_rng(77 + ntri)
+    v = np.zeros((ntri * 3, 6), np.float32)
+    c0 = rng.uniform(-5, 5, size=(ntri, 1, 3))
+    v[:, :3] = (c0 + rng.uniform(-0.3, 0.3, size=(ntri, 3, 3))).reshape(-1, 3).astype(np.float32)
+    o = oracle.Scene()
+    ob = o.add_blas(v)
+    on, ot = o.export_blas(ob)
+    ninst = min(ntri, 600)
+    inst = [(0, scenes._rot_scale((0.0, 1.0, 0.0), float(k % 7) * 10.0, (1.0, 1.0, 1.0),
+                                  tuple(rng.integers(-30, 30, size=3).astype(np.float64))), k, 0)
+            for k in range(ninst)]
+    o.set_instances([(ob, x, iid, hg) for (_, x, iid, hg) in inst])
+    otl = o.export_tlas()
+    for path in ("small", "mid", "multi"):
+        monkeypatch.setenv("RT_BUILD_PATH", path)
+        c = fresh_ctx()
+        b = c.blas_build(v)
+        gn, gt = c.blas_export(b)
+        assert np.array_equal(gn, on) and np.array_equal(gt, ot), f"{path}: BLAS differs"
+        c.tlas_build([(b, x, iid, hg) for (_, x, iid, hg) in inst])
+        assert np.array_equal(c.tlas_export(), otl), f"{path}: TLAS differs"
+        c.close()
 
 
 @pytest.mark.parametrize("mesh", ["soup", "point"])
