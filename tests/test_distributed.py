@@ -124,8 +124,9 @@ def test_gloo_frames_mode_weak():
         assert tmax == float(world)
 
 
-def test_bench_spawn_path_gloo_world2(tmp_path):
-    """bench.py's own N>1 path end to end on CPU: `bench.py --gpus 2` (no WORLD_SIZE) re-launches
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_spawn_path_gloo(tmp_path, world):
+    """bench.py's own N>1 path end to end on CPU: `bench.py --gpus N` (no WORLD_SIZE) re-launches
     itself under torch.distributed.run, the ranks tile one frame into strips, gather and assemble
     it (pipelined, two slots), all-reduce the counters and max-reduce the clock; rank 0 prints the
     JSON line. The test backend swaps the HIP renderer for the oracle (gloo, CPU tensors)."""
@@ -139,7 +140,8 @@ def test_bench_spawn_path_gloo_world2(tmp_path):
     env = dict(os.environ, RT_BENCH_TEST_BACKEND="tests.bench_cpu_backend:CpuBackend",
                PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""), OMP_NUM_THREADS="1")
     env.pop("WORLD_SIZE", None)
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "C2F", "--size", "64x44",
+    # 64 x 44: 6 strips of 8 rows, so at N = 8 two ranks render nothing (ragged partition)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--config", "C2F", "--size", "64x44",
            "--steps", "3", "--warmup", "1", "--settle-ms", "0", "--extra", "C4", "--no-cpu-baseline",
            "--save-image", str(img)]
     p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
@@ -147,12 +149,12 @@ def test_bench_spawn_path_gloo_world2(tmp_path):
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 2 and out["scaling"] == "strong"
-    assert out["config"]["rccl_world_size"] == 2
-    assert out["config"]["parallelism"].startswith("strips2+gather")
+    assert out["n_gpus"] == world and out["scaling"] == "strong"
+    assert out["config"]["rccl_world_size"] == world
+    assert out["config"]["parallelism"].startswith(f"strips{world}+gather")
     spec = scenes.config("C2F").with_size(64, 44)
     o8, _, st = oracle.Scene(spec).render_spec(spec, nthreads=2, want_float=False)
     assert out["config"]["rays_per_step"] == int(st[0] + st[1])  # one frame's rays over both ranks
     assert np.array_equal(np.load(img), o8)  # assembled from both ranks' strips, bit for bit
-    assert [e["config"] for e in out["extra"]] == ["C4"] and out["extra"][0]["n_gpus"] == 2
+    assert [e["config"] for e in out["extra"]] == ["C4"] and out["extra"][0]["n_gpus"] == world
     assert out["roofline"]["frac"] <= 1.0
