@@ -2,6 +2,9 @@
 
 camera_glm.json   glm::lookAt / glm::rotate from the reference's vendored glm, via the harness
                   oracle/ref_glm_camera.cpp built into oracle/_ref/ (`make ref`).
+obj_ingest.json   OBJFileManager::LoadObjFile output for teapot.obj / rabbit.obj (counts, sha256 of
+                  positions and indices) from oracle/ref_obj_ingest.cpp: the reference's own
+                  OBJ_Loader.h / OBJ_Loader.cpp compiled from /root/reference (`make ref`).
 manipulator.json  camera-manipulator trajectories (mouseMove / motion / wheel / roll in every mode)
                   from oracle/ref_glm_manip.cpp over the reference's vendored glm (oracle/_ref/).
 frames_small.npz  oracle frames (RGBA8 + float32) of every config at small sizes; each is first
@@ -57,6 +60,32 @@ def camera():
     _harness("glm_manip", "manipulator.json")
 
 
+def obj_ingest():
+    """obj_ingest.json: LoadObjFile's output for the reference's models, from oracle/ref_obj_ingest.cpp
+    (the reference's own OBJ_Loader types + its LoadObjFile code path, compiled from /root/reference):
+    counts, sha256 of the float32 positions and the u32 indices, the first and last vertex / face."""
+    import hashlib
+    import tempfile
+    subprocess.run(["make", "-C", ROOT, "ref"], check=True)
+    exe = os.path.join(ROOT, "oracle", "_ref", "obj_ingest")
+    out = {}
+    for m in ("teapot", "rabbit"):
+        with tempfile.TemporaryDirectory() as td:
+            b = os.path.join(td, "o.bin")
+            subprocess.run([exe, f"/root/reference/models/{m}.obj", b], check=True)
+            raw = open(b, "rb").read()
+        nv, ni = (int(x) for x in np.frombuffer(raw[:8], np.uint32))
+        pos = np.frombuffer(raw[8:8 + 12 * nv], np.float32).reshape(-1, 3)
+        idx = np.frombuffer(raw[8 + 12 * nv:], np.uint32)
+        out[m] = {"vertices": nv, "indices": ni,
+                  "positions_sha256": hashlib.sha256(pos.tobytes()).hexdigest(),
+                  "indices_sha256": hashlib.sha256(idx.tobytes()).hexdigest(),
+                  "first_vertex": pos[0].tolist(), "last_vertex": pos[-1].tolist(),
+                  "first_face": idx[:3].tolist(), "last_face": idx[-3:].tolist()}
+    with open(os.path.join(HERE, "obj_ingest.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 def frames():
     data = {}
     for name, (w, h) in SIZES.items():
@@ -82,4 +111,5 @@ def frames():
 if __name__ == "__main__":
     if "--frames-only" not in sys.argv:
         camera()
+        obj_ingest()
     frames()

@@ -1,9 +1,11 @@
 """Mesh ingest (OBJFileManager::LoadObjFile, OBJ_FileManager.cpp:10-71), vertex normals
 (ComputeVertexNormals, D3D12HelloTriangle.cpp:1430-1462) and the ground plane (:1237-1271).
 
-Golden vectors: counts, first vertex and first face of teapot.obj / rabbit.obj as produced by the
-reference's own LoadObjFile compiled at survey time. The product (C++ in
-librtamd.so) and the oracle (C) are also compared with each other on every byte.
+Golden vectors: counts, first vertex and first face of teapot.obj / rabbit.obj, and
+tests/golden/obj_ingest.json: the WHOLE LoadObjFile output of both models (sha256 of every position
+and index) from oracle/ref_obj_ingest.cpp — the reference's own OBJ_Loader.h / OBJ_Loader.cpp compiled
+from /root/reference, driving LoadObjFile's code path (tests/golden/make_golden.py). The product (C++
+in librtamd.so) and the oracle (C) are also compared with each other on every byte.
 """
 import gzip
 import hashlib
@@ -46,6 +48,21 @@ def test_ingest_matches_reference_goldens(name):
     assert (m.indices < m.vertex_count).all()
     # default Vertex normal (0,1,0) until ComputeVertexNormals (D3D12HelloTriangle.h:55)
     assert (m.vertices[:, 3:] == np.array([0, 1, 0], np.float32)).all()
+
+
+@pytest.mark.parametrize("name", ["teapot", "rabbit"])
+def test_ingest_matches_reference_loader_fixture(name):
+    import json
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "obj_ingest.json")) as f:
+        g = json.load(f)[name]
+    m = rt.Mesh.asset(name)
+    pos = np.ascontiguousarray(m.vertices[:, :3], dtype=np.float32)
+    idx = np.ascontiguousarray(m.indices, dtype=np.uint32)
+    assert (m.vertex_count, m.index_count) == (g["vertices"], g["indices"])
+    assert hashlib.sha256(pos.tobytes()).hexdigest() == g["positions_sha256"]
+    assert hashlib.sha256(idx.tobytes()).hexdigest() == g["indices_sha256"]
+    assert pos[0].tolist() == g["first_vertex"] and pos[-1].tolist() == g["last_vertex"]
+    assert idx[:3].tolist() == g["first_face"] and idx[-3:].tolist() == g["last_face"]
 
 
 @pytest.mark.parametrize("name", ["teapot", "rabbit"])
