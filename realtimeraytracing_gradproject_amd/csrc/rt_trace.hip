@@ -60,7 +60,8 @@ typedef float f8v __attribute__((ext_vector_type(8)));
 #define RT_TLAS_SINGLE_SKIP 1  // the same for TLAS nodes
 #endif
 #ifndef RT_REF0_WAVES
-#define RT_REF0_WAVES 7  // the reflectivity-0 REF kernel (MODE 3, one sample)
+#define RT_REF0_WAVES 6  // the reflectivity-0 REF kernel (MODE 3, one sample): 73 VGPRs, no spills (7 waves: 2
+                         // spilled VGPRs, the same frame time)
 #endif
 #ifndef RT_REF_NOREFL
 #define RT_REF_NOREFL 1  // RT_SHADE_REF with reflectivity 0: the kernel specialised without reflection rays
