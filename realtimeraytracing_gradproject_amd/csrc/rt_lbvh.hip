@@ -31,6 +31,12 @@
 #ifndef RT_FUSED_MAX_N
 #define RT_FUSED_MAX_N 3072  // largest n built by k_build_small (measured crossover; capacity kFusedMax)
 #endif
+#ifndef RT_TINY_BUILD
+#define RT_TINY_BUILD 1  // 2 <= n <= RT_TINY_MAX_N: the one-launch LDS build (k_build_tiny)
+#endif
+#ifndef RT_TINY_MAX_N
+#define RT_TINY_MAX_N 512  // largest n built by k_build_tiny (capacity kTinyMax)
+#endif
 #ifndef RT_MID_BUILD
 #define RT_MID_BUILD 1  // RT_MID_MIN_N <= n <= kMidMax: the five-launch build (k_mid_*)
 #endif
@@ -1730,6 +1736,237 @@ __global__ void k_mid_write(const Exp4* __restrict__ exp, const uint16_t* __rest
   out[k] = nd;
 }
 
+// ------------------------------------------------------------------------------------------
+// One-launch build for 2 <= n <= kTinyMax (the TLASes and the plane BLAS of the configs): the
+// k_mid_* stages in ONE 512-thread workgroup with every intermediate in LDS — rank sort, the
+// Apetrei climb (the whole tree is one block: every hand-off in LDS), the binary nodes, their DP and
+// expansions, the BFS numbering — and only the finished 4-wide nodes (and the triangle gather)
+// written to HBM. Same arithmetic in the same order as k_mid_*: the identical tree.
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t kTinyMax = 512;
+constexpr int kTinyWaves = kTinyMax / 64;
+
+// The 4-wide node for a wide root's expansion (ref / box / cnt), slot refs mapped to BFS indices.
+__device__ __forceinline__ void write_wide_node(const int (&ref)[4], const float (&box)[4][6], int cnt,
+                                                const uint16_t* bfs, Bvh4Node* __restrict__ out) {
+  Bvh4Node nd;
+  uint32_t nvalid = 0, inner = 0;
+  nd.first_inner = 0;
+  for (int j = 0; j < 4; ++j) {
+    const float inf = __builtin_inff();
+    float b6[6] = {inf, inf, inf, inf, inf, inf};
+    int32_t r = kEmptyChild;
+    if (j < cnt && ref[j] != kEmptyChild) {
+      ++nvalid;
+      for (int q = 0; q < 6; ++q) b6[q] = box[j][q];
+      if (ref[j] >= 0) {
+        r = (int32_t)bfs[ref[j]];
+        if (!inner) nd.first_inner = r;
+        inner |= 1u << j;
+      } else {
+        r = ref[j];
+      }
+    }
+    nd.lox[j] = b6[0];
+    nd.loy[j] = b6[1];
+    nd.loz[j] = b6[2];
+    nd.hix[j] = b6[3];
+    nd.hiy[j] = b6[4];
+    nd.hiz[j] = b6[5];
+    nd.child[j] = r;
+  }
+  nd.count = nvalid;
+  nd.inner_mask = inner;
+  nd.entry_base = ((uint32_t)nd.first_inner << 8) | (inner << 4);
+  *out = nd;
+}
+
+__global__ __launch_bounds__(kTinyMax) void k_build_tiny(const float* __restrict__ primbox, uint32_t n,
+                                                         bool leaf_ref_is_prim, uint32_t* __restrict__ sorted,
+                                                         float* __restrict__ cb_out, Bvh4Node* __restrict__ out,
+                                                         uint32_t* __restrict__ info, const TriRec* __restrict__ tri_in,
+                                                         TriRec* __restrict__ tri_out) {
+  __shared__ uint64_t s_key[kTinyMax];   // key64 by primitive, then (s_skey) by leaf position
+  __shared__ uint64_t s_skey[kTinyMax];
+  __shared__ float s_lbox[kTinyMax][6];  // leaf boxes in leaf order
+  __shared__ uint32_t s_lprim[kTinyMax];
+  __shared__ uint32_t s_flag[kTinyMax];
+  __shared__ MidSlot s_slot[kTinyMax];   // by position, as in k_mid_tree
+  __shared__ BinNode s_bin[kTinyMax];
+  __shared__ float4 s_dpc[kTinyMax];
+  __shared__ uint32_t s_dps[kTinyMax];
+  __shared__ uint2 s_e[kTinyMax];
+  __shared__ uint16_t s_order[kTinyMax], s_bfs[kTinyMax], s_ps[kTinyMax];
+  __shared__ float s_red[12][kTinyWaves];
+  __shared__ float s_cb[12];
+  __shared__ uint32_t s_w[2 * kTinyWaves];
+  __shared__ int s_root, s_maxstack;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  const int nbin = (int)n - 1;
+  // 1. bounds (k_bounds' values) and keys
+  float bx[6];
+  {
+    const uint32_t i = min(tid, n - 1u);  // past n: copies of the last box
+    for (int k = 0; k < 6; ++k) bx[k] = primbox[(size_t)i * 6 + k];
+    float v[12];
+    for (int k = 0; k < 3; ++k) {
+      const float c = (bx[k] + bx[3 + k]) * 0.5f;
+      v[k] = c;
+      v[3 + k] = c;
+      v[6 + k] = bx[k];
+      v[9 + k] = bx[3 + k];
+    }
+    for (int off = 32; off >= 1; off >>= 1)
+      for (int k = 0; k < 12; ++k) {
+        const float o = __shfl_xor(v[k], off, 64);
+        v[k] = (k % 6) < 3 ? fminf(v[k], o) : fmaxf(v[k], o);
+      }
+    if (lane == 0)
+      for (int k = 0; k < 12; ++k) s_red[k][w] = v[k];
+    if (tid == 0) s_maxstack = 0;
+    __syncthreads();
+    if (tid < 12) {
+      const int k = (int)tid;
+      float r = s_red[k][0];
+      for (int j = 1; j < kTinyWaves; ++j) r = (k % 6) < 3 ? fminf(r, s_red[k][j]) : fmaxf(r, s_red[k][j]);
+      s_cb[k] = r;
+      cb_out[k] = r;
+    }
+    __syncthreads();
+  }
+  if (tid < n) {
+    uint32_t q[3];
+    for (int k = 0; k < 3; ++k) {  // k_morton's quantisation, operation for operation
+      const float ext = s_cb[3 + k] - s_cb[k];
+      const float inv = ext > 0.0f ? 1.0f / ext : 0.0f;
+      q[k] = quantize10((bx[k] + bx[3 + k]) * 0.5f, s_cb[k], inv);
+    }
+    const uint32_t code = (expand_bits10(q[0]) << 2) | (expand_bits10(q[1]) << 1) | expand_bits10(q[2]);
+    s_key[tid] = ((uint64_t)code << 32) | tid;
+  }
+  s_flag[tid] = 0u;
+  __syncthreads();
+  // 2. rank sort (stable: key64 carries the index) and the scatter into leaf order
+  if (tid < n) {
+    const uint64_t ki = s_key[tid];
+    uint32_t rank = 0;
+    for (uint32_t j = 0; j < n; ++j) rank += s_key[j] < ki ? 1u : 0u;
+    s_skey[rank] = ((ki >> 32) << 32) | rank;  // key64 of the sorted array: code << 32 | position
+    for (int k = 0; k < 6; ++k) s_lbox[rank][k] = bx[k];
+    s_lprim[rank] = tid;
+    sorted[rank] = tid;
+    if (tri_out) tri_out[rank] = tri_in[tid];
+  }
+  __syncthreads();
+  // 3. the Apetrei climb, one block: every hand-off in LDS
+  if (tid < n) {
+    MidSlot a;
+    for (int k = 0; k < 6; ++k) a.b[k] = s_lbox[tid][k];
+    for (int k = 0; k < 4; ++k) a.d[k] = 0.0f;
+    a.ref = leaf_ref_is_prim ? ~(int)s_lprim[tid] : ~(int)tid;
+    a.l = a.r = (int)tid;
+    a.pad = 0;
+    while (!(a.l == 0 && a.r == nbin)) {
+      const uint64_t klm = s_skey[max(a.l - 1, 0)], kl = s_skey[a.l], kr = s_skey[a.r], krp = s_skey[min(a.r + 1, nbin)];
+      const int dl = a.l > 0 ? lcp64(klm, kl) : -1;
+      const int dr = a.r < nbin ? lcp64(kr, krp) : -1;
+      const bool left = dr > dl;
+      const int s = left ? a.r : a.l - 1;
+      s_slot[left ? s : s + 1] = a;
+      asm volatile("" ::: "memory");  // LDS order suffices (k_mid_tree)
+      const uint32_t old = __hip_atomic_fetch_add(&s_flag[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      asm volatile("" ::: "memory");
+      if (old == 0) break;
+      const MidSlot o = s_slot[left ? s + 1 : s];
+      mid_join(s, left, a, o, s_bin, s_dpc, s_dps);
+    }
+    if (a.l == 0 && a.r == nbin) s_root = a.ref;
+  }
+  __syncthreads();
+  // 4. expansions (child lists for the numbering; recomputed for the node writes)
+  const bool blas = !leaf_ref_is_prim;
+  for (int sn = (int)tid; sn < nbin; sn += kTinyMax) {
+    int ref[4];
+    float box[4][6];
+    const int cnt = wide_slots_dp(s_bin, s_dpc, s_dps, sn, ref, box, blas);
+    uint32_t h[4];
+    for (int j = 0; j < 4; ++j) h[j] = j >= cnt ? kMidEmpty : ref[j] >= 0 ? (uint32_t)ref[j] : kMidLeaf;
+    s_e[sn] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+  }
+  if (tid == 0) {
+    s_order[0] = (uint16_t)s_root;
+    s_bfs[s_root] = 0;
+    s_ps[0] = 0;
+  }
+  __syncthreads();
+  // 5. BFS numbering (k_mid_collapse phase C, one node per thread: a level holds < kTinyMax nodes)
+  const uint64_t lower = lane == 0 ? 0ull : (~0ull >> (64u - lane));
+  int lmax = 0, cur_n = 1, base = 0, depth = 0;
+  while (cur_n > 0) {
+    const bool valid = (int)tid < cur_n;
+    uint32_t h[4] = {kMidEmpty, kMidEmpty, kMidEmpty, kMidEmpty};
+    if (valid) {
+      const uint2 e = s_e[s_order[base + tid]];
+      h[0] = e.x & 0xffffu;
+      h[1] = e.x >> 16;
+      h[2] = e.y & 0xffffu;
+      h[3] = e.y >> 16;
+    }
+    uint32_t m = 0, cnt = 0;
+    for (int j = 0; j < 4; ++j) {
+      m += h[j] < kMidLeaf ? 1u : 0u;
+      cnt += h[j] != kMidEmpty ? 1u : 0u;
+    }
+    uint32_t pre = 0, wtot = 0;
+#pragma unroll
+    for (int bit = 0; bit < 3; ++bit) {
+      const uint64_t bal = __ballot((m >> bit) & 1u);
+      pre += (uint32_t)__popcll(bal & lower) << bit;
+      wtot += (uint32_t)__popcll(bal) << bit;
+    }
+    uint32_t* s_wl = s_w + (depth & 1) * kTinyWaves;
+    if (lane == 0) s_wl[w] = wtot;
+    __syncthreads();
+    uint32_t woff = 0, total = 0;
+#pragma unroll
+    for (int k = 0; k < kTinyWaves; ++k) {
+      const uint32_t c = s_wl[k];
+      woff += (uint32_t)k < w ? c : 0u;
+      total += c;
+    }
+    if (valid) {
+      const int below = (int)s_ps[base + tid] + (int)cnt - 1;
+      lmax = below > lmax ? below : lmax;
+      int o = base + cur_n + (int)(woff + pre);
+      for (int j = 0; j < 4; ++j)
+        if (h[j] < kMidLeaf) {
+          s_order[o] = (uint16_t)h[j];
+          s_bfs[h[j]] = (uint16_t)o;
+          s_ps[o] = (uint16_t)below;
+          ++o;
+        }
+    }
+    ++depth;
+    __syncthreads();
+    base += cur_n;
+    cur_n = (int)total;
+  }
+  // 6. the 4-wide nodes
+  for (int k = (int)tid; k < base; k += kTinyMax) {
+    int ref[4];
+    float box[4][6];
+    const int cnt = wide_slots_dp(s_bin, s_dpc, s_dps, (int)s_order[k], ref, box, blas);
+    write_wide_node(ref, box, cnt, s_bfs, out + k);
+  }
+  atomicMax(&s_maxstack, lmax);
+  __syncthreads();
+  if (tid == 0) {
+    info[0] = (uint32_t)base;
+    info[1] = (uint32_t)depth;
+    info[2] = (uint32_t)s_maxstack;
+  }
+}
+
 __global__ void k_tri_setup(const float* __restrict__ vtx, const uint32_t* __restrict__ idx,
                             uint32_t ntri, TriRec* __restrict__ tris, float* __restrict__ box) {
   uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1784,7 +2021,7 @@ __global__ void k_inst_boxes(const InstanceRec* __restrict__ inst, const float* 
 
 inline unsigned grid1(uint32_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
-enum { kPathSmall = 0, kPathMid = 1, kPathMulti = 2 };
+enum { kPathSmall = 0, kPathMid = 1, kPathMulti = 2, kPathTiny = 3 };
 
 // Which schedule builds n primitives (measured crossovers). RT_BUILD_PATH=small|mid|multi
 // in the environment forces one where it can hold n (A/B timing only; every schedule builds the
@@ -1792,11 +2029,14 @@ enum { kPathSmall = 0, kPathMid = 1, kPathMulti = 2 };
 int build_path(uint32_t n) {
   const char* f = getenv("RT_BUILD_PATH");
   const bool small_ok = RT_FUSED_BUILD && n <= kFusedMax, mid_ok = RT_SAH_COLLAPSE && n >= 2 && n <= kMidMax;
+  const bool tiny_ok = RT_SAH_COLLAPSE && n >= 2 && n <= kTinyMax;
   if (f) {
+    if (!strcmp(f, "tiny") && tiny_ok) return kPathTiny;
     if (!strcmp(f, "small") && small_ok) return kPathSmall;
     if (!strcmp(f, "mid") && mid_ok) return kPathMid;
     if (!strcmp(f, "multi")) return kPathMulti;
   }
+  if (RT_TINY_BUILD && tiny_ok && n <= (uint32_t)RT_TINY_MAX_N) return kPathTiny;
   if (RT_MID_BUILD && mid_ok && n >= (uint32_t)RT_MID_MIN_N) return kPathMid;
   if (small_ok && n <= (uint32_t)RT_FUSED_MAX_N) return kPathSmall;
   return kPathMulti;
@@ -1862,7 +2102,11 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
   RT_TRY(hipEventRecord(e0, s));
   float* cb = (float*)stats.p;
   const int path = build_path(n);
-  if (path == kPathMid) {
+  if (path == kPathTiny) {
+    k_build_tiny<<<1, kTinyMax, 0, s>>>(d_primbox, n, leaf_ref_is_prim, d_sorted, cb, d_nodes, (uint32_t*)info.p,
+                                        d_tri_in, d_tri_out);
+    RT_TRY(hipGetLastError());
+  } else if (path == kPathMid) {
     k_mid_rank<<<grid1(n, 64), 1024, 0, s>>>(d_primbox, n, cb, (uint64_t*)k64.p, (uint32_t*)keys0.p, d_sorted,
                                               (float*)sbox.p, (uint32_t*)dps.p, (uint32_t*)info.p, d_tri_in,
                                               d_tri_out);

@@ -100,7 +100,8 @@ def test_blas_edge_sizes(ntri):
 
 @pytest.mark.parametrize("ntri", [2, 100, 1025, 3000, 8192])
 def test_build_schedules_bitwise_equal(ntri, monkeypatch):
-    # every schedule that can hold n (RT_BUILD_PATH: one workgroup, four launches, multi-kernel)
+    # every schedule that can hold n (RT_BUILD_PATH: one-launch LDS build for n <= 512, one workgroup,
+    # four launches, multi-kernel; a schedule that cannot hold n falls back to the default)
     # builds the oracle's tree, BLAS and TLAS alike
     rng = np.random.default_rng(77 + ntri)
     v = np.zeros((ntri * 3, 6), np.float32)
@@ -115,7 +116,7 @@ def test_build_schedules_bitwise_equal(ntri, monkeypatch):
             for k in range(ninst)]
     o.set_instances([(ob, x, iid, hg) for (_, x, iid, hg) in inst])
     otl = o.export_tlas()
-    for path in ("small", "mid", "multi"):
+    for path in ("tiny", "small", "mid", "multi"):
         monkeypatch.setenv("RT_BUILD_PATH", path)
         c = fresh_ctx()
         b = c.blas_build(v)

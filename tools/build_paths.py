@@ -18,7 +18,7 @@ from realtimeraytracing_gradproject_amd import scenes  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--sizes", default="2,64,256,1024,2048,3072,4096,8192")
 ap.add_argument("--reps", type=int, default=15)
-ap.add_argument("--paths", default="small,mid,multi")
+ap.add_argument("--paths", default="tiny,small,mid,multi")
 ap.add_argument("--lib", default=rt.LIB_PATH)
 a = ap.parse_args()
 
