@@ -78,6 +78,9 @@ typedef float f8v __attribute__((ext_vector_type(8)));
 #ifndef RT_ANY_MT_BITS
 #define RT_ANY_MT_BITS 0  // any-hit triangle tests with the bitwise acceptance (A/B knob)
 #endif
+#ifndef RT_OCT_BASES
+#define RT_OCT_BASES 2  // uniform-octant row loads: 1 one SGPR base per row, 2 node base + row soffset (A/B)
+#endif
 #ifndef RT_PACKET_OCT
 #define RT_PACKET_OCT 1  // uniform-octant BLAS walks load near/far planes directly (no min/max pairs)
 #endif
@@ -601,6 +604,12 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
                                                  PacketLive<R>& pl, HitRec* hit, WaveStack& stk, int& sp, int cap,
                                                  const NodeOct& oc, Counters& cnt) {
   const int base = sp;
+#if RT_OCT_BASES == 1
+  // one base per plane row, the octant's row offset folded in once per BLAS entry: each row load is
+  // then base + the node's 32-bit offset (SGPR soffset), no per-node s_or for the row offsets
+  const RT_CONST char *bnx = pool + oc.nx, *bfx = pool + oc.fx, *bny = pool + oc.ny, *bfy = pool + oc.fy,
+                      *bnz = pool + oc.nz, *bfz = pool + oc.fz;
+#endif
   while (true) {
     const RT_CONST char* nb = pool + ((uint32_t)bref << 7);
     const i8v ch = *(const RT_CONST i8v*)(nb + 96);  // child[4], count, first_inner, inner_mask, entry_base
@@ -611,12 +620,38 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
     if (OCT) {
       // one 32-bit offset per row: the scalar load takes it as its SGPR offset (no 64-bit adds)
       const uint32_t noff = (uint32_t)bref << 7;
+#if RT_OCT_BASES == 1
+      planes[0] = cld4(bnx + noff);
+      planes[1] = cld4(bfx + noff);
+      planes[2] = cld4(bny + noff);
+      planes[3] = cld4(bfy + noff);
+      planes[4] = cld4(bnz + noff);
+      planes[5] = cld4(bfz + noff);
+#elif RT_OCT_BASES == 2
+      // each row at the pool base + its octant offset (SGPR soffset) + the node offset as the
+      // instruction's... the node offset goes into the base once (two SALU); six s_load_dwordx4 with
+      // the row offsets as soffset (the compiler would add 64-bit addresses per row itself)
+      const RT_CONST char* nbo = pool + noff;
+      asm volatile(
+          "s_load_dwordx4 %0, %6, %7\n\t"
+          "s_load_dwordx4 %1, %6, %8\n\t"
+          "s_load_dwordx4 %2, %6, %9\n\t"
+          "s_load_dwordx4 %3, %6, %10\n\t"
+          "s_load_dwordx4 %4, %6, %11\n\t"
+          "s_load_dwordx4 %5, %6, %12\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&s"(planes[0]), "=&s"(planes[1]), "=&s"(planes[2]), "=&s"(planes[3]), "=&s"(planes[4]),
+            "=&s"(planes[5])
+          : "s"(nbo), "s"(oc.nx), "s"(oc.fx), "s"(oc.ny), "s"(oc.fy), "s"(oc.nz), "s"(oc.fz)
+          : "memory");
+#else
       planes[0] = cld4(pool + (noff + oc.nx));
       planes[1] = cld4(pool + (noff + oc.fx));
       planes[2] = cld4(pool + (noff + oc.ny));
       planes[3] = cld4(pool + (noff + oc.fy));
       planes[4] = cld4(pool + (noff + oc.nz));
       planes[5] = cld4(pool + (noff + oc.fz));
+#endif
     } else {
 #pragma unroll
       for (int q = 0; q < 6; ++q) planes[q] = cld4(nb + 16 * q);
