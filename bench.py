@@ -227,6 +227,7 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
     frame = [be.zeros((H, W, 4)) if rank == 0 else None for _ in range(nslot)] if strips else None
     rendered = [be.event() for _ in range(nslot)]
     freed = [be.event() for _ in range(nslot)]
+    parts = [D.gather_parts(gathered[s], world, rank) for s in range(nslot)] if strips else None
 
     def step(k: int):
         s = k % nslot
@@ -237,7 +238,7 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
             rendered[s].record(render)
             comm.wait_event(rendered[s])
             with be.use_stream(comm):
-                D.gather_strips(local[s], world, rank, gathered[s])
+                D.gather_strips(local[s], world, rank, gathered[s], parts=parts[s])
                 if rank == 0:
                     be.assemble(world, gathered[s], frame[s], comm)
             freed[s].record(comm)

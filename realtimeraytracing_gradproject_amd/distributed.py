@@ -25,12 +25,20 @@ def padded_rows(height: int, world: int, strip: int = STRIP_ROWS) -> int:
     return strip_rows_per_rank(height, world, strip)
 
 
-def gather_strips(local, world: int, rank: int, gathered: Optional[object] = None, dst: int = 0):
+def gather_parts(gathered, world: int, rank: int, dst: int = 0) -> Optional[List]:
+    """The per-rank views of `gathered` dist.gather fills on dst (None elsewhere); built once per
+    buffer, not per frame (each view costs a Python call on the frame loop's critical path)."""
+    return [gathered[r] for r in range(world)] if rank == dst else None
+
+
+def gather_strips(local, world: int, rank: int, gathered: Optional[object] = None, dst: int = 0,
+                  parts: Optional[List] = None):
     """dist.gather of the per-rank compact buffers into `gathered` (world x rows x W x 4) on dst."""
     import torch.distributed as dist
 
-    parts: Optional[List] = [gathered[r] for r in range(world)] if rank == dst else None
-    dist.gather(local, parts, dst=dst)
+    if parts is None and rank == dst:
+        parts = gather_parts(gathered, world, rank, dst)
+    dist.gather(local, parts if rank == dst else None, dst=dst)
     return gathered if rank == dst else None
 
 
