@@ -1415,7 +1415,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void k_trace_frame(SceneView 
 // footprint on screen shrinks with the sample count (more coherent packets), and the pixel's
 // samples are summed across lanes in sample order at the end — the same float additions, in the
 // same order, as the sample loop. KS = 0: the sample loop (spp 9, or R > 1). A workgroup is
-// RT_PACKET_WX x RT_PACKET_WY waves (2 x 1: 128 threads; smaller workgroups shorten the tail of
+// RT_PACKET_WX x RT_PACKET_WY waves (2 x 1: 128 threads; multi-sample kernels 1 x 1; smaller workgroups shorten the tail of
 // the launch). Rays outside the image or the row list join the packets dead; only in-image
 // pixels are stored.
 // Occupancy: LAMBERT_SHADOW (the perf configs) runs at 7 waves per SIMD (72 VGPRs, no spills);
@@ -1442,10 +1442,16 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void k_trace_frame(SceneView 
 #ifndef RT_SAMPLE_LANES
 #define RT_SAMPLE_LANES 1  // 0: every multi-sample frame uses the sample loop (A/B knob)
 #endif
-constexpr int kPacketBlock = 64 * RT_PACKET_WX * RT_PACKET_WY;
+#ifndef RT_PACKET_WX_MS
+#define RT_PACKET_WX_MS 1  // multi-sample kernels (KS = 2, 4): one-wave workgroups (C5 -2.8 % vs 2 x 1)
+#endif
+// waves along x / y of a packet workgroup for the sample layout KS
+__host__ __device__ constexpr int packet_wx(int ks) { return ks > 1 ? RT_PACKET_WX_MS : RT_PACKET_WX; }
+__host__ __device__ constexpr int packet_wy(int ks) { return ks > 1 ? 1 : RT_PACKET_WY; }
+__host__ __device__ constexpr int packet_block(int ks) { return 64 * packet_wx(ks) * packet_wy(ks); }
 
 template <int MODE, bool STATS, int R, int KS>
-__global__ __launch_bounds__(kPacketBlock) __attribute__((amdgpu_waves_per_eu(
+__global__ __launch_bounds__(packet_block(KS)) __attribute__((amdgpu_waves_per_eu(
     (MODE == 1 && !STATS) ? (KS == 0 ? RT_SPP_WAVES : (KS == 1 ? RT_LS_WAVES : RT_KS_WAVES))
     : (MODE == 3 && !STATS) ? (KS == 0 ? RT_SPP_WAVES : (KS == 1 ? RT_REF0_WAVES : RT_KS_WAVES))
                             : ((MODE == 0 && !STATS && KS == 1) ? RT_REF_WAVES : 1))))
@@ -1458,17 +1464,18 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
 #endif
   constexpr uint32_t NS = KS > 1 ? KS * KS : 1;  // samples of a pixel held by consecutive lanes
   constexpr uint32_t TP = KS > 1 ? 8 / KS : 8;    // tile side in pixels
+  constexpr uint32_t WX = packet_wx(KS), WY = packet_wy(KS);
   // the wave index is uniform: an SGPR, so the pixel of a lane can be re-derived from its lane id
   const uint32_t lane = threadIdx.x & 63u, w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t sample = lane % NS, pix = lane / NS;
-  const uint32_t x = blockIdx.x * (TP * RT_PACKET_WX) + (w % RT_PACKET_WX) * TP + (pix % TP);
+  const uint32_t x = blockIdx.x * (TP * WX) + (w % WX) * TP + (pix % TP);
   uint32_t px[R], py[R], out[R];  // out: the pixel's output index, ~0 when this lane stores nothing
   bool inimg[R];
   V3 acc[R], col[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     px[r] = x;
-    const uint32_t orow = blockIdx.y * (TP * R * RT_PACKET_WY) + (w / RT_PACKET_WX) * (TP * R) + TP * r + pix / TP;
+    const uint32_t orow = blockIdx.y * (TP * R * WY) + (w / WX) * (TP * R) + TP * r + pix / TP;
     inimg[r] = x < fp.width && orow < fp.nrows;
     py[r] = 0;
     if (inimg[r]) py[r] = rows ? rows[orow] : orow;
@@ -1496,8 +1503,8 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
                         __shfl(col[0].z, base + q, 64)));
     acc[0] = sum;
     // the store index too (not kept live across the traces: the 7-wave budget has no VGPR to spare)
-    const uint32_t xp = lid / NS, xx = blockIdx.x * (TP * RT_PACKET_WX) + (w % RT_PACKET_WX) * TP + (xp % TP);
-    const uint32_t orow = blockIdx.y * (TP * RT_PACKET_WY) + (w / RT_PACKET_WX) * TP + xp / TP;
+    const uint32_t xp = lid / NS, xx = blockIdx.x * (TP * WX) + (w % WX) * TP + (xp % TP);
+    const uint32_t orow = blockIdx.y * (TP * WY) + (w / WX) * TP + xp / TP;
     out[0] = (xx < fp.width && orow < fp.nrows && (lid % NS) == 0u) ? orow * fp.width + xx : 0xffffffffu;
   } else {
     for (uint32_t sy = 0; sy < k; ++sy)
@@ -1582,10 +1589,10 @@ hipError_t launch_mode(const SceneView& sc, const FrameParams& fp, const uint32_
     const int ks = fp.spp_side == 1 ? 1 : ((RT_SAMPLE_LANES && R == 1 && (fp.spp_side == 2 || fp.spp_side == 4))
                                                ? (int)fp.spp_side : 0);
     const uint32_t tp = ks > 1 ? 8u / (uint32_t)ks : 8u;
-    const uint32_t tw = tp * RT_PACKET_WX, th = tp * R * RT_PACKET_WY;
+    const uint32_t tw = tp * (uint32_t)packet_wx(ks), th = tp * R * (uint32_t)packet_wy(ks);
     dim3 gp((fp.width + tw - 1) / tw, (fp.nrows + th - 1) / th);
 #define RT_LAUNCH_PACKET(KS)                                                                                   \
-  hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R, (R == 1 ? KS : 0)>), gp, dim3(kPacketBlock), 0, s, sc, fp, \
+  hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R, (R == 1 ? KS : 0)>), gp, dim3(packet_block(R == 1 ? KS : 0)), 0, s, sc, fp, \
                      rows, (uint32_t*)rgba8, (float4*)rgba32f, stats)
     if (ks == 1) RT_LAUNCH_PACKET(1);
     else if (ks == 2) RT_LAUNCH_PACKET(2);
