@@ -78,10 +78,11 @@ def test_blas_bitwise_equal_to_oracle(model):
     c.close()
 
 
-# 1: the one-workgroup build (k_build_small); 2 .. 8192: the four-launch build (k_mid_*, block
-# boundaries at 1024-leaf multiples); 8193 and 20000: the multi-kernel build
-@pytest.mark.parametrize("ntri", [1, 2, 3, 7, 63, 64, 65, 1000, 1023, 1024, 1025, 2049, 5000, 8191, 8192, 8193,
-                                  20000])
+# 1: the one-workgroup build (k_build_small); 2 .. 512: the one-launch LDS build (k_build_tiny);
+# 513 .. 8192: the four-launch build (k_mid_*, block boundaries at 1024-leaf multiples); 8193 and
+# 20000: the multi-kernel build
+@pytest.mark.parametrize("ntri", [1, 2, 3, 7, 63, 64, 65, 512, 513, 1000, 1023, 1024, 1025, 2049, 5000, 8191, 8192,
+                                  8193, 20000])
 def test_blas_edge_sizes(ntri):
     rng = np.random.default_rng(1234 + ntri)
     v = np.zeros((ntri * 3, 6), np.float32)
@@ -139,10 +140,10 @@ def test_blas_degenerate_geometry(mesh):
     c.close()
 
 
-@pytest.mark.parametrize("count", [300, 3000, 9000])
+@pytest.mark.parametrize("count", [300, 512, 513, 1025, 3000, 8192, 9000])
 def test_blas_duplicate_centroids(count):
     # many triangles with identical Morton codes: Karras tie-break on leaf position; the sort must
-    # stay stable across waves (3000) and across the fused / multi-kernel builds (9000)
+    # stay stable across waves and across every build schedule (tiny <= 512 < mid <= 8192 < multi)
     v = np.zeros((count * 3, 6), np.float32)
     base = np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0]], np.float32)
     for k in range(count):
@@ -170,7 +171,8 @@ def test_tlas_bitwise_equal_to_oracle(name):
 @pytest.mark.parametrize("ninst", [1, 3, 1024, 8192, 9000])
 def test_tlas_instance_counts(ninst):
     # TLAS over ninst instances of one small mesh at seeded translations / rotations (coincident
-    # boxes included): fused (<= 8192) and multi-kernel (9000) builds against the oracle
+    # boxes included): tiny (<= 512), four-launch (<= 8192) and multi-kernel (9000) builds against
+    # the oracle
     rng = np.random.default_rng(ninst)
     v = np.array([[0, 0, 0, 0, 1, 0], [1, 0, 0, 0, 1, 0], [0, 1, 0, 0, 1, 0],
                   [0, 0, 1, 0, 1, 0], [1, 1, 1, 0, 1, 0], [0, 1, 1, 0, 1, 0]], np.float32)
