@@ -4,7 +4,14 @@
 //   BottomLevelASGenerator::Generate  nv_helpers_dx12/BottomLevelASGenerator.cpp:177-245 (build :234)
 //   TopLevelASGenerator::Generate     nv_helpers_dx12/TopLevelASGenerator.cpp:148-249 (build :239)
 //
-// Pipeline (all deterministic, so oracle/rt_oracle.c rebuilds the bit-identical tree):
+// Four schedules of the same tree (all deterministic, so oracle/rt_oracle.c rebuilds the bit-identical
+// tree; build_path() picks one, RT_BUILD_PATH forces one for A/B):
+//   2 <= n <= 512     k_build_tiny: one 512-thread workgroup, everything in LDS (rank sort, Apetrei
+//                     climb, DP, expansion, BFS numbering), one launch
+//   513 .. 8192       k_mid_*: rank sort, Apetrei climb with in-block LDS hand-offs, expansion, a
+//                     one-workgroup top climb + BFS numbering, parallel node writes: four launches + one
+//   n = 1             k_build_small: the multi-kernel stages in one 1024-thread workgroup
+//   larger n          the multi-kernel pipeline:
 //   1. centroid bounds      one 1024-thread workgroup, LDS min/max reduction (exact)
 //   2. Morton codes         30-bit (10 bits/axis) of box centroids
 //   3. LSD radix sort       4 passes x 8 bits; per pass: block digit histogram (LDS atomics),
@@ -15,8 +22,6 @@
 //                           with the SAH collapse DP at each node
 //   6. pack                 64-B child-pair nodes (both child boxes per node)
 //   7. DP expansion + collapse into 4-wide BFS nodes, triangle gather into leaf order
-// Builds of n <= kFusedMax primitives (every BLAS and TLAS of the BASELINE configs) run all of
-// it in one 1024-thread workgroup instead (k_build_small): one launch, LDS-resident sort.
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
