@@ -2101,9 +2101,16 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
        pint = at(p_pint), pleaf = at(p_pleaf), nbox = at(p_nbox), flags = at(p_flags), dpc = at(p_dpc),
        dps = at(p_dps), expd = at(p_exp), gslot = at(p_gslot), e16 = at(p_e16), order = at(p_order),
        bfsmap = at(p_bfs), k64 = at(p_k64), sbox = at(p_sbox);
-  hipEvent_t e0, e1;
-  RT_TRY(hipEventCreate(&e0));
-  RT_TRY(hipEventCreate(&e1));
+  struct Events {  // destroyed on every return path
+    hipEvent_t a = nullptr, b = nullptr;
+    ~Events() {
+      if (a) (void)hipEventDestroy(a);
+      if (b) (void)hipEventDestroy(b);
+    }
+  } ev;
+  RT_TRY(hipEventCreate(&ev.a));
+  RT_TRY(hipEventCreate(&ev.b));
+  hipEvent_t e0 = ev.a, e1 = ev.b;
   RT_TRY(hipEventRecord(e0, s));
   float* cb = (float*)stats.p;
   const int path = build_path(n);
@@ -2192,8 +2199,6 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
   float ms = 0.0f;
   RT_TRY(hipEventElapsedTime(&ms, e0, e1));
   if (build_ms) *build_ms = ms;
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
   return hipSuccess;
 }
 
