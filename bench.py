@@ -160,6 +160,21 @@ class HipBackend:
     def use_stream(self, s):
         return torch.cuda.stream(s)
 
+    def sync_event(self):
+        """Render/gather hand-off of the strips loop: rt_event_* (no timestamp, no system-scope
+        fence: ~3 us less per record than a torch.cuda.Event on the frame's critical path)."""
+        ev = self.rt.PipelineEvent()
+        ev.recorded = False
+        return ev
+
+    def record(self, ev, stream):
+        ev.record(stream.cuda_stream)
+        ev.recorded = True
+
+    def wait(self, stream, ev):
+        if ev.recorded:
+            ev.wait_on(stream.cuda_stream)
+
     def synchronize(self):
         torch.cuda.synchronize(self.device)
 
@@ -225,23 +240,23 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
     local = [be.zeros((rows_per_rank, W, 4)) for _ in range(nslot)]
     gathered = [be.zeros((world, rows_per_rank, W, 4)) if rank == 0 else None for _ in range(nslot)] if strips else None
     frame = [be.zeros((H, W, 4)) if rank == 0 else None for _ in range(nslot)] if strips else None
-    rendered = [be.event() for _ in range(nslot)]
-    freed = [be.event() for _ in range(nslot)]
+    rendered = [be.sync_event() for _ in range(nslot)]
+    freed = [be.sync_event() for _ in range(nslot)]
     parts = [D.gather_parts(gathered[s], world, rank) for s in range(nslot)] if strips else None
 
     def step(k: int):
         s = k % nslot
         if strips:
-            render.wait_event(freed[s])  # slot s free: the gather of frame k - nslot is done
+            be.wait(render, freed[s])  # slot s free: the gather of frame k - nslot is done
         be.dispatch(local[s], rows, render)
         if strips:
-            rendered[s].record(render)
-            comm.wait_event(rendered[s])
+            be.record(rendered[s], render)
+            be.wait(comm, rendered[s])
             with be.use_stream(comm):
                 D.gather_strips(local[s], world, rank, gathered[s], parts=parts[s])
                 if rank == 0:
                     be.assemble(world, gathered[s], frame[s], comm)
-            freed[s].record(comm)
+            be.record(freed[s], comm)
 
     # untimed counter pass: rays, tests and record fetches of this rank's share of one step
     st = be.counted(local[0], rows, render)

@@ -236,6 +236,16 @@ rt_status rt_assemble_strips(rt_ctx_t ctx, uint32_t W, uint32_t H, uint32_t nran
  * strip_rows rows. Writes up to cap rows to rows_out; returns the row count (0 on bad args). */
 uint32_t rt_strip_rows(uint32_t H, uint32_t nranks, uint32_t rank, uint32_t strip_rows,
                        uint32_t* rows_out, uint32_t cap);
+/* Frame-pipeline events for the strips loop (render of frame k + 1 beside the gather + assembly of
+ * frame k on a second stream). No reference counterpart (the reference renders on one GPU): plain
+ * hipEvent_t handles without timestamps and without the system-scope fence hipEventRecord performs
+ * by default (both streams are on one device; the consumer is a kernel, not the host), which takes
+ * ~3 us off every record on the frame's critical path. rt_stream_wait_event(stream, ev) makes
+ * later work on `stream` wait for the last record of `ev`. */
+rt_status rt_event_create(void** ev_out);
+rt_status rt_event_destroy(void* ev);
+rt_status rt_event_record(void* ev, void* hip_stream);
+rt_status rt_stream_wait_event(void* hip_stream, void* ev);
 
 /* Copies the counters (RT_STAT_*) to out[RT_STAT_COUNT]; synchronises the context. */
 rt_status rt_stats(rt_ctx_t ctx, uint64_t out[RT_STAT_COUNT]);

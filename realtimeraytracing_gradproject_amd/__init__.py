@@ -103,6 +103,10 @@ SIGNATURES = [
     ("rt_raster_draw", _I, [_P, _UP, _U32, _FP, _U32, _U32, _P, _P, _P]),
     ("rt_assemble_strips", _I, [_P, _U32, _U32, _U32, _U32, _P, _P, _P]),
     ("rt_strip_rows", _U32, [_U32, _U32, _U32, _U32, _P, _U32]),
+    ("rt_event_create", _I, [ctypes.POINTER(_P)]),
+    ("rt_event_destroy", _I, [_P]),
+    ("rt_event_record", _I, [_P, _P]),
+    ("rt_stream_wait_event", _I, [_P, _P]),
     ("rt_stats", _I, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     ("rt_stats_reset", _I, [_P]),
     ("rt_mesh_load_obj", _I, [ctypes.c_char_p, ctypes.POINTER(_P)]),
@@ -325,6 +329,41 @@ def strip_rows(height: int, nranks: int, rank: int, strip_rows_: int = 8) -> np.
     out = np.zeros(n, np.uint32)
     lib.rt_strip_rows(height, nranks, rank, strip_rows_, out.ctypes.data_as(_P), n)
     return out
+
+
+class PipelineEvent:
+    """rt_event_*: a device-side sync point between the strips loop's render and gather streams
+    (no timestamp, no system-scope fence on record). record(stream) / wait_on(stream) take raw
+    hipStream_t handles (torch: stream.cuda_stream)."""
+
+    def __init__(self):
+        h = _P()
+        st = lib.rt_event_create(ctypes.byref(h))
+        if st != RT_OK:
+            raise RtError(st, "rt_event_create")
+        self._h = h
+
+    def record(self, stream: Optional[int]):
+        st = lib.rt_event_record(self._h, stream)
+        if st != RT_OK:
+            raise RtError(st, "rt_event_record")
+
+    def wait_on(self, stream: Optional[int]):
+        """Later work on `stream` waits for this event's last record."""
+        st = lib.rt_stream_wait_event(stream, self._h)
+        if st != RT_OK:
+            raise RtError(st, "rt_stream_wait_event")
+
+    def close(self):
+        if self._h:
+            lib.rt_event_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001  (interpreter shutdown)
+            pass
 
 
 def strip_rows_per_rank(height: int, nranks: int, strip_rows_: int = 8) -> int:

@@ -763,6 +763,30 @@ uint32_t rt_strip_rows(uint32_t H, uint32_t nranks, uint32_t rank, uint32_t stri
   return n;
 }
 
+rt_status rt_event_create(void** ev_out) {
+  if (!ev_out) return RT_E_INVALID;
+  *ev_out = nullptr;
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) return RT_E_HIP;
+  *ev_out = e;
+  return RT_OK;
+}
+
+rt_status rt_event_destroy(void* ev) {
+  if (!ev) return RT_E_INVALID;
+  return hipEventDestroy((hipEvent_t)ev) == hipSuccess ? RT_OK : RT_E_HIP;
+}
+
+rt_status rt_event_record(void* ev, void* stream) {
+  if (!ev) return RT_E_INVALID;
+  return hipEventRecord((hipEvent_t)ev, (hipStream_t)stream) == hipSuccess ? RT_OK : RT_E_HIP;
+}
+
+rt_status rt_stream_wait_event(void* stream, void* ev) {
+  if (!ev) return RT_E_INVALID;
+  return hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)ev, 0) == hipSuccess ? RT_OK : RT_E_HIP;
+}
+
 rt_status rt_stats(rt_ctx_t c, uint64_t out[RT_STAT_COUNT]) {
   if (!c || !out) return RT_E_INVALID;
   (void)hipSetDevice(c->device);

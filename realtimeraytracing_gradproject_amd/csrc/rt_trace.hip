@@ -1579,6 +1579,27 @@ __global__ void k_assemble(uint32_t W, uint32_t H, uint32_t nranks, uint32_t str
   out[(size_t)y * W + x] = in[((size_t)rank * rows_per_rank + lrow) * W + x];
 }
 
+// 16 B per thread (W % 4 == 0, 16-B aligned buffers): kAsmRows output rows per workgroup, so the
+// copy is few short waves that interleave with a concurrent frame's trace waves instead of
+// flooding the dispatcher (one 4-B thread per pixel is 8 K workgroups per 1080p frame)
+constexpr uint32_t kAsmRows = 8;
+__global__ __launch_bounds__(256) void k_assemble16(uint32_t W4, uint32_t H, uint32_t nranks, uint32_t strip_rows,
+                                                    const uint4* __restrict__ in, uint4* __restrict__ out,
+                                                    uint32_t rows_per_rank) {
+  const uint32_t x = blockIdx.x * 256u + threadIdx.x;
+  if (x >= W4) return;
+  const uint32_t y0 = blockIdx.y * kAsmRows;
+#pragma unroll
+  for (uint32_t i = 0; i < kAsmRows; ++i) {
+    const uint32_t y = y0 + i;
+    if (y >= H) break;
+    const uint32_t s = y / strip_rows, within = y % strip_rows;
+    const uint32_t rank = s % nranks, local_strip = s / nranks;
+    const uint32_t lrow = local_strip * strip_rows + within;
+    out[(size_t)y * W4 + x] = in[((size_t)rank * rows_per_rank + lrow) * W4 + x];
+  }
+}
+
 template <int MODE, bool STATS>
 hipError_t launch_mode(const SceneView& sc, const FrameParams& fp, const uint32_t* rows, void* rgba8,
                        float* rgba32f, unsigned long long* stats, int schedule, hipStream_t s) {
@@ -1658,6 +1679,13 @@ hipError_t launch_assemble_strips(uint32_t W, uint32_t H, uint32_t nranks, uint3
   const uint32_t nstrips = (H + strip_rows - 1) / strip_rows;
   const uint32_t strips_per_rank = (nstrips + nranks - 1) / nranks;
   const uint32_t rows_per_rank = strips_per_rank * strip_rows;
+  if (W % 4 == 0 && ((uintptr_t)gathered | (uintptr_t)out) % 16 == 0) {
+    const uint32_t W4 = W / 4;
+    dim3 grid((W4 + 255) / 256, (H + kAsmRows - 1) / kAsmRows);
+    hipLaunchKernelGGL(k_assemble16, grid, dim3(256), 0, s, W4, H, nranks, strip_rows, (const uint4*)gathered,
+                       (uint4*)out, rows_per_rank);
+    return hipGetLastError();
+  }
   dim3 grid((W + 255) / 256, H);
   hipLaunchKernelGGL(k_assemble, grid, dim3(256), 0, s, W, H, nranks, strip_rows, (const uint32_t*)gathered,
                      (uint32_t*)out, rows_per_rank);

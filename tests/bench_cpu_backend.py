@@ -66,6 +66,15 @@ class CpuBackend:
     def use_stream(self, s):
         return contextlib.nullcontext()
 
+    def sync_event(self):
+        return _WallEvent()
+
+    def record(self, ev, stream):
+        ev.record(stream)
+
+    def wait(self, stream, ev):
+        pass
+
     def synchronize(self):
         pass
 

@@ -620,12 +620,14 @@ def test_cpp_host_app_drag_frames(tmp_path, buttons, dx, dy):
     assert not np.array_equal(views[0], views[-1])  # the drag moved the camera
 
 
-def test_assemble_kernel_equals_host_twin():
+@pytest.mark.parametrize("H,W,world", [(99, 33, 4), (99, 36, 3), (7, 4, 2), (1080, 1920, 8), (1083, 1924, 5)])
+def test_assemble_kernel_equals_host_twin(H, W, world):
+    """4-B path (W % 4 != 0) and the 16-B row-batched path (ragged last row batch, rows < kAsmRows)."""
     from realtimeraytracing_gradproject_amd import distributed as D
-    H, W, world = 99, 33, 4
     pad = D.padded_rows(H, world)
     g = torch.randint(0, 255, (world, pad, W, 4), dtype=torch.uint8, device="cuda")
     out = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # the call below runs on the context's own stream, not torch's
     c = fresh_ctx()
     c.assemble_strips(W, H, world, D.STRIP_ROWS, g, out)
     torch.cuda.synchronize()
