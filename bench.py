@@ -19,9 +19,10 @@ touches the GPU. The multi-GPU configs C4 (rabbit x64, 2 lights) and C5 (rabbit 
 value = rays traced in one step (all ranks, counted by the device counters in an untimed pass)
 x steps / max-over-ranks wall time of the timed region.
 
-Untimed before the W warmup frames: the counter pass and a clock settle (--settle-ms of frames:
-the GPU needs ~20 ms of load to reach its steady clock; with 5 warmup frames alone the same build
-read 0.20 ms instead of 0.15 ms per frame).
+Untimed before the W warmup frames: a clock settle (--settle-ms of frames: the GPU needs ~20 ms of
+load to reach its steady clock; with 5 warmup frames alone the same build read 0.20 ms instead of
+0.15 ms per frame; the ranks agree on its length, as every strips step is a collective), the
+tile-rows autotune (pick_tile_rows) and the counter pass.
 """
 from __future__ import annotations
 
@@ -160,6 +161,9 @@ class HipBackend:
     def use_stream(self, s):
         return torch.cuda.stream(s)
 
+    def set_tile_rows(self, rows: int):
+        self.ctx.set_tile_rows(rows)
+
     def sync_event(self):
         """Render/gather hand-off of the strips loop: rt_event_* (no timestamp, no system-scope
         fence: ~3 us less per record than a torch.cuda.Event on the frame's critical path)."""
@@ -222,6 +226,30 @@ def strip_plan(H: int, world: int, rank: int):
     return D.rank_rows(H, world, rank), D.padded_rows(H, world)
 
 
+def pick_tile_rows(be, buf, rows, stream, frames: int = 8, rounds: int = 3):
+    """Untimed autotune of rt_set_tile_rows: this rank's render alone at 8 x 8 and 8 x 4 pixel tiles per
+    wave, alternating, best of `rounds`; keeps the faster (the image is the same). 8 x 4 wins only when
+    so few waves run that the slowest tile sets the frame time (one rank's strips of a frame tiled over
+    many GPUs); a backend without the setting keeps 8. Returns (rows, {rows: ms per frame})."""
+    if not hasattr(be, "set_tile_rows"):
+        return 8, None
+    best = {8: float("inf"), 4: float("inf")}
+    for _ in range(rounds):
+        for tr in (8, 4):
+            be.set_tile_rows(tr)
+            be.dispatch(buf, rows, stream)
+            e0, e1 = be.event(True), be.event(True)
+            e0.record(stream)
+            for _ in range(frames):
+                be.dispatch(buf, rows, stream)
+            e1.record(stream)
+            be.synchronize()
+            best[tr] = min(best[tr], e0.elapsed_time(e1) / frames)
+    pick = 4 if best[4] < best[8] else 8
+    be.set_tile_rows(pick)
+    return pick, {k: round(v, 4) for k, v in best.items()}
+
+
 def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_ms: float, strips: bool,
                pipeline: bool, schedule: str, save_image: str = ""):
     """Builds the scene, counts one step's rays (untimed), settles, warms up, then times exactly
@@ -258,6 +286,25 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
                     be.assemble(world, gathered[s], frame[s], comm)
             be.record(freed[s], comm)
 
+    # clock settle (untimed). Every rank must run the same number of steps (each strips step is a
+    # collective), so the ranks agree after every 4 steps whether any of them still needs time.
+    k = 0
+    if settle_ms > 0:
+        t0 = time.perf_counter()
+        while True:
+            for _ in range(4):
+                step(k)
+                k += 1
+            be.synchronize()
+            more = torch.tensor([1.0 if (time.perf_counter() - t0) * 1e3 < settle_ms else 0.0],
+                                dtype=torch.float64, device=be.device)
+            if distributed:
+                dist.all_reduce(more, op=dist.ReduceOp.MAX)
+            if more.item() == 0.0:
+                break
+
+    tile_rows, tile_ms = pick_tile_rows(be, local[0], rows, render)
+
     # untimed counter pass: rays, tests and record fetches of this rank's share of one step
     st = be.counted(local[0], rows, render)
     counts = torch.tensor([st["primary_rays"] + st["shadow_rays"], st["primary_rays"], st["shadow_rays"]],
@@ -266,15 +313,7 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
         dist.all_reduce(counts)
     rays_step = int(counts[0].item())  # strips: one frame over all ranks; frames mode: N frames
 
-    # clock settle + warmup (untimed)
-    k = 0
-    if settle_ms > 0:
-        t0 = time.perf_counter()
-        while (time.perf_counter() - t0) * 1e3 < settle_ms:
-            for _ in range(4):
-                step(k)
-                k += 1
-            be.synchronize()
+    # warmup (untimed)
     for _ in range(warmup):
         step(k)
         k += 1
@@ -321,7 +360,8 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
         img = frame[last] if strips else local[0][:H]
         np.save(save_image, img.cpu().numpy())
     return {"rays_step": rays_step, "primary": int(counts[1].item()), "shadow": int(counts[2].item()),
-            "tmax": tmax, "kernel_ms": kernel_ms, "stats": st, "build": build, "rows_local": len(rows) if strips else H}
+            "tmax": tmax, "kernel_ms": kernel_ms, "stats": st, "build": build, "rows_local": len(rows) if strips else H,
+            "tile_rows": tile_rows, "tile_ms": tile_ms}
 
 
 # ---------------------------------------------------------------------------------------------
@@ -539,6 +579,7 @@ def main(argv=None) -> int:
                           "frame_ms": round(x["tmax"] / n_steps * 1e3, 4), "kernel_ms": round(x["kernel_ms"], 4),
                           "rays_per_step": x["rays_step"], "resolution": f"{es.width}x{es.height}", "spp": es.spp,
                           "n_gpus": world, "parallelism": f"strips{world}+gather" if strips else f"frames{world}",
+                          "tile_rows": x["tile_rows"],
                           "aabb_tests_per_ray_rank0": round(st["aabb_tests"] / rays, 2) if not distributed else None,
                           "node_fetches": int(st["node_fetches"]), "tri_fetches": int(st["tri_fetches"])})
     if not distributed and (a.extra is None) and isinstance(be, HipBackend):
@@ -572,6 +613,7 @@ def main(argv=None) -> int:
                        "parallelism": (f"strips{world}+gather" + ("" if a.no_pipeline else " (pipelined)")) if strips
                        else f"frames{world}",
                        "rccl_world_size": world if distributed else None, "schedule": a.schedule,
+                       "tile_rows": r["tile_rows"], "tile_ms_rank0": r["tile_ms"],
                        "settle_ms": a.settle_ms},
             "roofline": rf,
             "cpu_baseline": cpu,

@@ -97,6 +97,7 @@ SIGNATURES = [
     ("rt_set_camera", _I, [_P, _FP]),
     ("rt_set_shading", _I, [_P, ctypes.POINTER(rt_light), _U32, ctypes.POINTER(rt_material), _I, _I]),
     ("rt_set_schedule", _I, [_P, _I]),
+    ("rt_set_tile_rows", _I, [_P, _I]),
     ("rt_set_stats", _I, [_P, _I]),
     ("rt_dispatch_rays", _I, [_P, _U32, _U32, _P, _U32, _P, _P, _P]),
     ("rt_trace_rays", _I, [_P, _P, _U32, _U32, _P, _P, _P]),
@@ -494,6 +495,10 @@ class Context:
 
     def set_schedule(self, schedule: int):
         self._check(self._lib.rt_set_schedule(self._h, schedule), "rt_set_schedule")
+
+    def set_tile_rows(self, rows: int):
+        """rt_set_tile_rows: 8 (8 x 8 pixel tiles per wave, default) or 4 (8 x 4)."""
+        self._check(self._lib.rt_set_tile_rows(self._h, rows), "rt_set_tile_rows")
 
     def set_stats(self, on: bool):
         self._check(self._lib.rt_set_stats(self._h, 1 if on else 0), "rt_set_stats")

@@ -52,6 +52,7 @@ struct rt_ctx {
   rt::FrameParams fp{};
   bool have_camera = false, have_shading = false;
   int schedule = RT_SCHED_PACKET;
+  uint32_t tile_rows = 8;  // rt_set_tile_rows
   bool stats_on = false;
   unsigned long long* d_stats = nullptr;
   uint64_t dispatches = 0, pixels = 0;
@@ -530,6 +531,13 @@ rt_status rt_set_schedule(rt_ctx_t c, int schedule) {
   return RT_OK;
 }
 
+rt_status rt_set_tile_rows(rt_ctx_t c, int rows) {
+  if (!c) return RT_E_INVALID;
+  if (rows != 4 && rows != 8) return fail(c, RT_E_INVALID, "rt_set_tile_rows: rows must be 4 or 8");
+  c->tile_rows = (uint32_t)rows;
+  return RT_OK;
+}
+
 rt_status rt_set_stats(rt_ctx_t c, int enable) {
   if (!c) return RT_E_INVALID;
   c->stats_on = enable != 0;
@@ -694,6 +702,7 @@ rt_status rt_dispatch_rays(rt_ctx_t c, uint32_t W, uint32_t H, const uint32_t* r
   c->fp.fwidth = (float)W;  // exact: W, H < 2^24
   c->fp.fheight = (float)H;
   c->fp.nrows = nrows;
+  c->fp.tile_rows = c->tile_rows;
   rt::SceneView sv = scene_view(c);
   if (sv.stack_cap > rt::kMaxTraversalStack)
     return fail(c, RT_E_UNSUPPORTED, "rt_dispatch_rays: BVH too deep for the traversal stack");

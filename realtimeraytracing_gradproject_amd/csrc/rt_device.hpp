@@ -137,6 +137,7 @@ struct FrameParams {
   // mul(viewInverse, (0, 0, 0, 1)) and the dimensions as floats
   float cam_origin[4];
   float fwidth, fheight;
+  uint32_t tile_rows;  // packet schedule, one-sample frames: rows of a wave's 8-wide tile (8 or 4)
 };
 
 // The trace kernels read one node pool and one triangle pool per scene: [TLAS | BLAS 0 | BLAS 1 ..]

@@ -1465,6 +1465,8 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
   constexpr uint32_t NS = KS > 1 ? KS * KS : 1;  // samples of a pixel held by consecutive lanes
   constexpr uint32_t TP = KS > 1 ? 8 / KS : 8;    // tile side in pixels
   constexpr uint32_t WX = packet_wx(KS), WY = packet_wy(KS);
+  // tile rows of a wave: TP, or 4 for 8 x 8 tiles at rt_set_tile_rows(4) (lanes past them idle)
+  const uint32_t TR = (KS <= 1 && fp.tile_rows == 4u) ? 4u : TP;
   // the wave index is uniform: an SGPR, so the pixel of a lane can be re-derived from its lane id
   const uint32_t lane = threadIdx.x & 63u, w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t sample = lane % NS, pix = lane / NS;
@@ -1475,8 +1477,8 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     px[r] = x;
-    const uint32_t orow = blockIdx.y * (TP * R * WY) + (w / WX) * (TP * R) + TP * r + pix / TP;
-    inimg[r] = x < fp.width && orow < fp.nrows;
+    const uint32_t orow = blockIdx.y * (TR * R * WY) + (w / WX) * (TR * R) + TR * r + pix / TP;
+    inimg[r] = x < fp.width && orow < fp.nrows && pix / TP < TR;
     py[r] = 0;
     if (inimg[r]) py[r] = rows ? rows[orow] : orow;
     out[r] = (inimg[r] && sample == 0) ? orow * fp.width + x : 0xffffffffu;  // < 2^32 pixels (rt_api.cpp)
@@ -1610,7 +1612,8 @@ hipError_t launch_mode(const SceneView& sc, const FrameParams& fp, const uint32_
     const int ks = fp.spp_side == 1 ? 1 : ((RT_SAMPLE_LANES && R == 1 && (fp.spp_side == 2 || fp.spp_side == 4))
                                                ? (int)fp.spp_side : 0);
     const uint32_t tp = ks > 1 ? 8u / (uint32_t)ks : 8u;
-    const uint32_t tw = tp * (uint32_t)packet_wx(ks), th = tp * R * (uint32_t)packet_wy(ks);
+    const uint32_t tr = (ks <= 1 && fp.tile_rows == 4u) ? 4u : tp;  // as the kernel's TR (KS <= 1: 8 x 8 tiles)
+    const uint32_t tw = tp * (uint32_t)packet_wx(ks), th = tr * R * (uint32_t)packet_wy(ks);
     dim3 gp((fp.width + tw - 1) / tw, (fp.nrows + th - 1) / th);
 #define RT_LAUNCH_PACKET(KS)                                                                                   \
   hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R, (R == 1 ? KS : 0)>), gp, dim3(packet_block(R == 1 ? KS : 0)), 0, s, sc, fp, \

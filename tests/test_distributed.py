@@ -142,7 +142,8 @@ def test_bench_spawn_path_gloo(tmp_path, world):
     env.pop("WORLD_SIZE", None)
     # 64 x 44: 6 strips of 8 rows, so at N = 8 two ranks render nothing (ragged partition)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--config", "C2F", "--size", "64x44",
-           "--steps", "3", "--warmup", "1", "--settle-ms", "0", "--extra", "C4", "--no-cpu-baseline",
+           # a clock settle on: ranks with unequal strip shares must still agree on its step count
+           "--steps", "3", "--warmup", "1", "--settle-ms", "30", "--extra", "C4", "--no-cpu-baseline",
            "--save-image", str(img)]
     p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]

@@ -307,6 +307,28 @@ def test_rows_subset_matches_full_frame():
     c.close()
 
 
+@pytest.mark.parametrize("name,size", [("C2", (150, 93)), ("C4", (200, 101)), ("REF", (96, 54)), ("REFL", (64, 37)),
+                                       ("C5", (48, 27)), ("C2", (7, 3))])
+def test_tile_rows_4_matches_oracle(name, size):
+    """rt_set_tile_rows(4) (8 x 4 pixel tiles per wave, half the lanes idle) renders the oracle's image, whole
+    frames with ragged heights and a strip row list; multi-sample frames (C5) ignore the setting."""
+    spec = scenes.config(name).with_size(*size)
+    c, o = load_both(spec)
+    c.set_tile_rows(4)
+    g8, g32 = gpu_render(c, spec)
+    o8, o32, _ = o.render_spec(spec, nthreads=8)
+    assert_images_equal(g8, g32, o8, o32, f"{name} tile rows 4")
+    rows = rt.strip_rows(spec.height, 3, 1) if spec.height > 8 else np.array([2, 0], np.uint32)
+    r8, r32 = gpu_render(c, spec, rows=rows)
+    assert np.array_equal(r8, o8[rows]) and np.array_equal(r32, o32[rows])
+    c.set_tile_rows(8)
+    f8, _ = gpu_render(c, spec)
+    assert np.array_equal(f8, g8)
+    with pytest.raises(rt.RtError):
+        c.set_tile_rows(2)
+    c.close()
+
+
 @pytest.mark.parametrize("name,step", [("C2", 41), ("C3", 41), ("C4", 37), ("C5", 79), ("REF", 29), ("REFL", 53)])
 def test_full_size_sampled_rows(name, step):
     """Full BASELINE sizes (C2-C4 1920x1080, C5 3840x2160 at 4 spp, the reference scene 1280x720):

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--schedule", type=int, default=0)
     ap.add_argument("--mode", type=int, default=-1, help="override the shade mode (2 = primary rays only)")
+    ap.add_argument("--share", type=int, default=1, help="render rank 0's strips of a frame tiled over N ranks")
     ap.add_argument("--no-check", action="store_true", help="time variants whose frames differ (knock-out studies)")
     a = ap.parse_args()
     libs, scheds = {}, {}
@@ -43,6 +44,8 @@ def main():
         if a.mode >= 0:
             spec.mode = a.mode
         W, H = spec.width, spec.height
+        rows = rt.strip_rows(H, a.share, 0) if a.share > 1 else None
+        NR = len(rows) if rows is not None else H
         stream = torch.cuda.Stream()
         ctxs, outs = {}, {}
         for name, lib in libs.items():
@@ -50,9 +53,9 @@ def main():
             scenes.upload(c, spec)
             c.set_schedule(scheds[name])
             ctxs[name] = c
-            outs[name] = (torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda"),
-                          torch.zeros((H, W, 4), dtype=torch.float32, device="cuda"))
-            c.dispatch(W, H, outs[name][0], outs[name][1], stream=stream.cuda_stream)
+            outs[name] = (torch.zeros((NR, W, 4), dtype=torch.uint8, device="cuda"),
+                          torch.zeros((NR, W, 4), dtype=torch.float32, device="cuda"))
+            c.dispatch(W, H, outs[name][0], outs[name][1], rows=rows, stream=stream.cuda_stream)
         torch.cuda.synchronize()
         first = next(iter(libs))
         for name in libs:
@@ -67,7 +70,7 @@ def main():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
                 for _ in range(a.steps):
-                    c.dispatch(W, H, outs[name][0], None, stream=stream.cuda_stream)
+                    c.dispatch(W, H, outs[name][0], None, rows=rows, stream=stream.cuda_stream)
                 e1.record(stream)
                 torch.cuda.synchronize()
                 times[name].append(e0.elapsed_time(e1) / a.steps)
