@@ -81,6 +81,9 @@ typedef float f8v __attribute__((ext_vector_type(8)));
 #ifndef RT_OCT_BASES
 #define RT_OCT_BASES 2  // uniform-octant row loads: 1 one SGPR base per row, 2 node base + row soffset (A/B)
 #endif
+#ifndef RT_TBEST_ASM
+#define RT_TBEST_ASM 1  // slab tests: the min with the ray's t as v_min asm (no per-node canonicalise: C2 -2 % median, C4/C5 -0.3..0.6 %)
+#endif
 #ifndef RT_PACKET_OCT
 #define RT_PACKET_OCT 1  // uniform-octant BLAS walks load near/far planes directly (no min/max pairs)
 #endif
@@ -508,12 +511,21 @@ __device__ __forceinline__ uint32_t packet_slabs(const f4v (&pl6)[6], const Pack
       const float tly = __builtin_fmaf(loy[k], iv.y, no.y), thy = __builtin_fmaf(hiy[k], iv.y, no.y);
       const float tlz = __builtin_fmaf(loz[k], iv.z, no.z), thz = __builtin_fmaf(hiz[k], iv.z, no.z);
       float n, f;
+      const float fzz = OCT ? thz : fmaxf(tlz, thz);
+      float fz;
+#if RT_TBEST_ASM
+      // min with the loop-carried t: fminf would re-canonicalise t (a v_max t, t) at every node
+      // visit; t is always a quiet value (arithmetic results and +-inf), so v_min gives its bits
+      asm("v_min_f32 %0, %1, %2" : "=v"(fz) : "v"(fzz), "v"(tbest));
+#else
+      fz = fminf(fzz, tbest);
+#endif
       if (OCT) {  // lo* hold the near planes, hi* the far planes
         n = fmaxf(fmaxf(tlx, tly), fmaxf(tlz, tmin));
-        f = fminf(fminf(thx, thy), fminf(thz, tbest));
+        f = fminf(fminf(thx, thy), fz);
       } else {
         n = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), tmin));
-        f = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tbest));
+        f = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fz);
       }
       const bool h = n <= f * 1.0000004f;  // only the lead's key is read
       hm[r][k] = wave_ballot(h);  // dead rays carry tbest = -inf: their h is false
