@@ -2,7 +2,9 @@
 // No exception crosses the boundary; every failure returns an rt_status and sets rt_last_error.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -71,6 +73,8 @@ struct rt_ctx {
   // raster fallback scratch (grown on demand)
   rt::RasterScratch raster;
   size_t raster_tile_cap = 0, raster_prim_cap = 0, raster_bin_cap = 0;
+  uint32_t* raster_total_host = nullptr;  // pinned: the last draw's bin-entry total, copied back async
+  rt::RasterDraws raster_draws_host;      // what raster.draws holds on the device (valid when n > 0)
 };
 
 namespace {
@@ -289,6 +293,7 @@ rt_status rt_destroy(rt_ctx_t c) {
   for (void* p : {(void*)c->raster.clip, (void*)c->raster.slots, (void*)c->raster.tiles, (void*)c->raster.tcount,
                   (void*)c->raster.toffs, (void*)c->raster.bins, (void*)c->raster.bsum, (void*)c->raster.draws})
     if (p) (void)hipFree(p);
+  if (c->raster_total_host) (void)hipHostFree(c->raster_total_host);
   (void)hipStreamDestroy(c->stream);
   delete c;
   return RT_OK;
@@ -648,20 +653,49 @@ rt_status rt_raster_draw(rt_ctx_t c, const rt_blas_t* draws, uint32_t ndraws, co
       c->raster_prim_cap = n;
     }
   }
+  if (!c->raster_total_host) {
+    HIPCHK(c, hipHostMalloc((void**)&c->raster_total_host, 4, hipHostMallocDefault), "hipHostMalloc(raster total)");
+    *c->raster_total_host = 0;
+  }
+  // the draw list on the device changes only with the draws (or a BLAS rebuild): uploaded then,
+  // not per draw, so nothing of a draw reads host memory after the call returns
+  if (std::memcmp(&c->raster_draws_host, &dr, sizeof(dr)) != 0) {
+    HIPCHK(c, quiesce(c), "rt_raster_draw: wait for in-flight work");
+    HIPCHK(c, hipMemcpy(c->raster.draws, &dr, sizeof(dr), hipMemcpyHostToDevice), "upload raster draws");
+    c->raster_draws_host = dr;
+  }
+  // bins are sized from a bin-entry total already known on the host: the first draw reads its own
+  // (one synchronisation), later draws the last total copied back asynchronously. A draw with more
+  // entries than that capacity still renders the same image (k_raster_tile walks every slot) and
+  // the next draw grows the bins.
+  const uint32_t last_total = *(volatile uint32_t*)c->raster_total_host;
   hipError_t e = rt::launch_raster_bin(dr, rv, c->raster, s);
   if (e != hipSuccess) return hip_fail(c, e, "raster bin launch");
-  // the bin total sizes the bin array: one 4-byte read-back per draw
-  uint32_t nbins = 0;
-  HIPCHK(c, hipMemcpyAsync(&nbins, c->raster.toffs + ntiles, 4, hipMemcpyDeviceToHost, s), "raster bin count");
-  HIPCHK(c, hipStreamSynchronize(s), "raster bin count");
-  if (c->raster_bin_cap < nbins) {
-    HIPCHK(c, quiesce(c), "rt_raster_draw: wait for in-flight work");
-    const size_t cap = (size_t)nbins + nbins / 2;
-    if ((st = regrow((void**)&c->raster.bins, cap * 4, "hipMalloc(raster bins)")) != RT_OK) return st;
-    c->raster_bin_cap = cap;
+  size_t want = 0;
+  if (c->raster_bin_cap == 0) {
+    uint32_t nbins = 0;
+    HIPCHK(c, hipMemcpyAsync(&nbins, c->raster.toffs + ntiles, 4, hipMemcpyDeviceToHost, s), "raster bin count");
+    HIPCHK(c, hipStreamSynchronize(s), "raster bin count");
+    want = (size_t)nbins + nbins / 2 + 64;
+  } else if (last_total > c->raster_bin_cap) {
+    want = (size_t)last_total + last_total / 2;
   }
-  e = rt::launch_raster_draw(dr, rv, c->raster, rgba8, depth32f, s);
+  // test hook: RT_RASTER_BIN_CAP caps the capacity (forces the slot-walk path)
+  if (const char* ev = std::getenv("RT_RASTER_BIN_CAP")) {
+    const size_t lim = (size_t)std::strtoull(ev, nullptr, 10);
+    if (want == 0 && c->raster_bin_cap > lim) want = lim;
+    if (want > lim) want = lim;
+  }
+  if (want != 0 && want != c->raster_bin_cap) {
+    HIPCHK(c, quiesce(c), "rt_raster_draw: wait for in-flight work");
+    if ((st = regrow((void**)&c->raster.bins, (want ? want : 1) * 4, "hipMalloc(raster bins)")) != RT_OK) return st;
+    c->raster_bin_cap = want;
+  }
+  const uint32_t cap = (uint32_t)std::min<size_t>(c->raster_bin_cap, 0xffffffffu);
+  e = rt::launch_raster_draw(dr, rv, c->raster, cap, rgba8, depth32f, s);
   if (e != hipSuccess) return hip_fail(c, e, "raster launch");
+  HIPCHK(c, hipMemcpyAsync(c->raster_total_host, c->raster.toffs + ntiles, 4, hipMemcpyDeviceToHost, s),
+         "raster bin total");
   return RT_OK;
 }
 

@@ -86,11 +86,12 @@ struct RasterScratch {
   RasterDraws* draws = nullptr; // device copy of the draw list
 };
 
-// Phase 1: vertex stage, clipping, setup and bin counting; toffs[ntiles] = number of bin entries
-// (the caller reads it to size `bins`). Phase 2: bin fill + per-tile raster and shading.
+// Phase 1: vertex stage, clipping, setup and bin counting; toffs[ntiles] = number of bin entries.
+// Phase 2: bin fill + per-tile raster and shading. `bins` holds bin_cap entries: a draw with more
+// entries leaves the bins unfilled and every tile walks the whole slot list (same image, slower).
 hipError_t launch_raster_bin(const RasterDraws& dr, const RasterView& rv, const RasterScratch& s,
                              hipStream_t stream);
-hipError_t launch_raster_draw(const RasterDraws& dr, const RasterView& rv, const RasterScratch& s, void* rgba8,
-                              float* depth, hipStream_t stream);
+hipError_t launch_raster_draw(const RasterDraws& dr, const RasterView& rv, const RasterScratch& s, uint32_t bin_cap,
+                              void* rgba8, float* depth, hipStream_t stream);
 
 }  // namespace rt

@@ -7,8 +7,9 @@
 //                       16.8 fixed-point snap, back-face cull (clockwise front), then up to 7 fan
 //                       triangles into fixed slots 7t..7t+6 with their 8x8-pixel tile counts.
 //   2. k_raster_bin<0> one wave per slot: count the 8x8 screen tiles each triangle overlaps;
-//      k_raster_scan   exclusive scan of the per-tile counts -> bin offsets (the host reads the
-//                      total once to size the bins);
+//      k_raster_scan   exclusive scan of the per-tile counts -> bin offsets (the host sizes the
+//                      bins from the first draw's total, later draws from the last total it read
+//                      back asynchronously: no synchronisation inside a draw);
 //      k_raster_bin<1> the same walk, appending the slot to each overlapped tile's bin.
 //   3. k_raster_tile   one wave per screen tile, the tile's depth buffer in registers: for every
 //                      binned triangle, edge functions with the top-left rule and screen-linear
@@ -266,7 +267,8 @@ template <int PASS>
 __global__ __launch_bounds__(256) void k_raster_bin(const RasterSlot* __restrict__ slots,
                                                     const uint32_t* __restrict__ slot_tiles, uint32_t nslots,
                                                     uint32_t tiles_x, uint32_t* __restrict__ tcount,
-                                                    const uint32_t* __restrict__ toffs, uint32_t* __restrict__ bins) {
+                                                    const uint32_t* __restrict__ toffs, uint32_t* __restrict__ bins,
+                                                    uint32_t bin_cap) {
   const uint32_t s = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   if (s >= nslots) return;
   const uint32_t n = slot_tiles[s];
@@ -279,8 +281,56 @@ __global__ __launch_bounds__(256) void k_raster_bin(const RasterSlot* __restrict
     if (PASS == 0) {
       atomicAdd(&tcount[tile], 1u);
     } else {
-      bins[toffs[tile] + atomicAdd(&tcount[tile], 1u)] = s;
+      // bins hold bin_cap entries: a draw with more (sized from an earlier draw's total) leaves
+      // them unwritten, and k_raster_tile walks the slot list instead
+      const uint32_t pos = toffs[tile] + atomicAdd(&tcount[tile], 1u);
+      if (pos < bin_cap) bins[pos] = s;
     }
+  }
+}
+
+// Per-pixel LESS test of one screen-space triangle (16.8 vertices X/Y, depths Z) against the
+// pixel centre (px, py): edge functions with the top-left rule, screen-linear depth; keeps the
+// minimum of (depth bits << 32 | primitive) in best.
+__device__ __forceinline__ void raster_pixel(const int32_t (&X)[3], const int32_t (&Y)[3], const float (&Z)[3],
+                                             uint32_t prim, int64_t px, int64_t py, unsigned long long& best) {
+  int64_t e[3];
+  bool in = true;
+  for (int i = 0; i < 3; ++i) {  // E_i: edge from vertex i+1 to i+2 (opposite vertex i)
+    const int a = (i + 1) % 3, c = (i + 2) % 3;
+    const int64_t dx = (int64_t)X[c] - X[a], dy = (int64_t)Y[c] - Y[a];
+    e[i] = dx * (py - Y[a]) - dy * (px - X[a]);
+    const bool top_left = dy < 0 || (dy == 0 && dx > 0);
+    in = in && (e[i] > 0 || (e[i] == 0 && top_left));
+  }
+  if (!in) return;
+  // depth, linear in screen space: z0 + (E1 (z1 - z0) + E2 (z2 - z0)) / area, in double
+  const double area = (double)(e[0] + e[1] + e[2]);
+  const double dz = ((double)e[1] * ((double)Z[1] - (double)Z[0]) +
+                     (double)e[2] * ((double)Z[2] - (double)Z[0])) / area;
+  float z = (float)((double)Z[0] + dz);
+  z = z < 0.0f ? 0.0f : z;  // viewport depth range [0, 1]
+  if (!(z < 1.0f)) return;  // LESS against the 1.0 clear
+  const unsigned long long key =
+      ((unsigned long long)__builtin_bit_cast(uint32_t, z + 0.0f) << 32) | (unsigned long long)prim;
+  best = key < best ? key : best;
+}
+
+// The triangles held by the lanes set in `live` (one slot record per lane), broadcast lane by lane.
+__device__ __forceinline__ void raster_batch(uint64_t live, const int32_t (&lx)[3], const int32_t (&ly)[3],
+                                             const float (&lz)[3], uint32_t lp, int64_t px, int64_t py,
+                                             unsigned long long& best) {
+  while (live) {
+    const int j = __builtin_ctzll(live);
+    live &= live - 1;
+    int32_t X[3], Y[3];
+    float Z[3];
+    for (int k = 0; k < 3; ++k) {
+      X[k] = __builtin_amdgcn_readlane(lx[k], j);
+      Y[k] = __builtin_amdgcn_readlane(ly[k], j);
+      Z[k] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int32_t, lz[k]), j));
+    }
+    raster_pixel(X, Y, Z, (uint32_t)__builtin_amdgcn_readlane((int)lp, j), px, py, best);
   }
 }
 
@@ -291,60 +341,61 @@ __global__ __launch_bounds__(256) void k_raster_bin(const RasterSlot* __restrict
 __global__ __launch_bounds__(256) void k_raster_tile(const RasterDraws* __restrict__ drp, const float4* __restrict__ clip,
                                                      const RasterSlot* __restrict__ slots,
                                                      const uint32_t* __restrict__ toffs,
-                                                     const uint32_t* __restrict__ bins, uint32_t tiles_x,
-                                                     uint32_t ntiles, uint32_t width, uint32_t height,
-                                                     uint32_t* __restrict__ rgba8, float* __restrict__ depth) {
+                                                     const uint32_t* __restrict__ bins, uint32_t bin_cap,
+                                                     const uint32_t* __restrict__ slot_tiles, uint32_t nslots,
+                                                     uint32_t tiles_x, uint32_t ntiles, uint32_t width,
+                                                     uint32_t height, uint32_t* __restrict__ rgba8,
+                                                     float* __restrict__ depth) {
   const uint32_t tile = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   if (tile >= ntiles) return;
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t x = (tile % tiles_x) * 8u + (lane & 7u), y = (tile / tiles_x) * 8u + (lane >> 3);
+  const uint32_t tx = tile % tiles_x, ty = tile / tiles_x;
+  const uint32_t x = tx * 8u + (lane & 7u), y = ty * 8u + (lane >> 3);
   const int64_t px = (int64_t)x * 256 + 128, py = (int64_t)y * 256 + 128;
   unsigned long long best = kRasterClear;
-  const uint32_t b0 = toffs[tile], b1 = toffs[tile + 1];
-  // the bin is fetched 64 entries at a time, one slot record per lane, then broadcast lane by lane
-  for (uint32_t base = b0; base < b1; base += 64u) {
-    const uint32_t cnt = min(64u, b1 - base);
-    int32_t lx[3] = {0, 0, 0}, ly[3] = {0, 0, 0};
-    float lz[3] = {0.0f, 0.0f, 0.0f};
-    uint32_t lp = 0;
-    if (lane < cnt) {
-      const RasterSlot& q = slots[bins[base + lane]];
-      for (int k = 0; k < 3; ++k) {
-        lx[k] = q.x[k];
-        ly[k] = q.y[k];
-        lz[k] = q.z[k];
+  if (toffs[ntiles] <= bin_cap) {
+    const uint32_t b0 = toffs[tile], b1 = toffs[tile + 1];
+    // the bin is fetched 64 entries at a time, one slot record per lane, then broadcast lane by lane
+    for (uint32_t base = b0; base < b1; base += 64u) {
+      const uint32_t cnt = min(64u, b1 - base);
+      int32_t lx[3] = {0, 0, 0}, ly[3] = {0, 0, 0};
+      float lz[3] = {0.0f, 0.0f, 0.0f};
+      uint32_t lp = 0;
+      if (lane < cnt) {
+        const RasterSlot& q = slots[bins[base + lane]];
+        for (int k = 0; k < 3; ++k) {
+          lx[k] = q.x[k];
+          ly[k] = q.y[k];
+          lz[k] = q.z[k];
+        }
+        lp = q.prim;
       }
-      lp = q.prim;
+      raster_batch(cnt == 64u ? ~0ull : ((1ull << cnt) - 1ull), lx, ly, lz, lp, px, py, best);
     }
-    for (uint32_t j = 0; j < cnt; ++j) {
-      int32_t X[3], Y[3];
-      float Z[3];
-      for (int k = 0; k < 3; ++k) {
-        X[k] = __builtin_amdgcn_readlane(lx[k], j);
-        Y[k] = __builtin_amdgcn_readlane(ly[k], j);
-        Z[k] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int32_t, lz[k]), j));
+  } else {
+    // the bins overflowed (more entries than the capacity sized from an earlier draw): the same
+    // (slot, tile) pairs k_raster_bin would have binned, found by walking every slot
+    for (uint32_t base = 0; base < nslots; base += 64u) {
+      const uint32_t s = base + lane;
+      int32_t lx[3] = {0, 0, 0}, ly[3] = {0, 0, 0};
+      float lz[3] = {0.0f, 0.0f, 0.0f};
+      uint32_t lp = 0;
+      bool mine = false;
+      if (s < nslots) {
+        const uint32_t n = slot_tiles[s];
+        if (n != 0) {
+          const RasterSlot q = slots[s];
+          const uint32_t dx = tx - q.tx0, dy = ty - q.ty0;  // unsigned: left / above the box wrap
+          mine = dx < q.tw && (uint64_t)dy * q.tw + dx < n && tile_overlaps(q, tx, ty);
+          for (int k = 0; k < 3; ++k) {
+            lx[k] = q.x[k];
+            ly[k] = q.y[k];
+            lz[k] = q.z[k];
+          }
+          lp = q.prim;
+        }
       }
-      const uint32_t prim = __builtin_amdgcn_readlane(lp, j);
-      int64_t e[3];
-      bool in = true;
-      for (int i = 0; i < 3; ++i) {  // E_i: edge from vertex i+1 to i+2 (opposite vertex i)
-        const int a = (i + 1) % 3, c = (i + 2) % 3;
-        const int64_t dx = (int64_t)X[c] - X[a], dy = (int64_t)Y[c] - Y[a];
-        e[i] = dx * (py - Y[a]) - dy * (px - X[a]);
-        const bool top_left = dy < 0 || (dy == 0 && dx > 0);
-        in = in && (e[i] > 0 || (e[i] == 0 && top_left));
-      }
-      if (!in) continue;
-      // depth, linear in screen space: z0 + (E1 (z1 - z0) + E2 (z2 - z0)) / area, in double
-      const double area = (double)(e[0] + e[1] + e[2]);
-      const double dz = ((double)e[1] * ((double)Z[1] - (double)Z[0]) +
-                         (double)e[2] * ((double)Z[2] - (double)Z[0])) / area;
-      float z = (float)((double)Z[0] + dz);
-      z = z < 0.0f ? 0.0f : z;  // viewport depth range [0, 1]
-      if (!(z < 1.0f)) continue;  // LESS against the 1.0 clear
-      const unsigned long long key =
-          ((unsigned long long)__builtin_bit_cast(uint32_t, z + 0.0f) << 32) | (unsigned long long)prim;
-      best = key < best ? key : best;
+      raster_batch(__builtin_amdgcn_ballot_w64(mine), lx, ly, lz, lp, px, py, best);
     }
   }
   if (x >= width || y >= height) return;
@@ -392,12 +443,10 @@ hipError_t launch_raster_bin(const RasterDraws& dr, const RasterView& rv, const 
   const uint32_t tx = (rv.width + 7) / 8, ty = (rv.height + 7) / 8, ntiles = tx * ty;
   hipError_t e = hipMemsetAsync(s.tcount, 0, (size_t)ntiles * 4, stream);
   if (e != hipSuccess) return e;
-  e = hipMemcpyAsync(s.draws, &dr, sizeof(RasterDraws), hipMemcpyHostToDevice, stream);
-  if (e != hipSuccess) return e;
   if (dr.total) {
     k_raster_setup<<<(dr.total + kSetupBlock - 1) / kSetupBlock, kSetupBlock, 0, stream>>>(s.draws, dr.total, rv,
                                                                                           s.clip, s.slots, s.tiles);
-    k_raster_bin<0><<<(nslots + 3) / 4, 256, 0, stream>>>(s.slots, s.tiles, nslots, tx, s.tcount, nullptr, nullptr);
+    k_raster_bin<0><<<(nslots + 3) / 4, 256, 0, stream>>>(s.slots, s.tiles, nslots, tx, s.tcount, nullptr, nullptr, 0u);
   }
   const uint32_t nb = (ntiles + kScanBlock - 1) / kScanBlock;
   k_scan_blocks<<<nb, 1024, 0, stream>>>(s.tcount, ntiles, s.toffs, s.bsum);
@@ -406,17 +455,18 @@ hipError_t launch_raster_bin(const RasterDraws& dr, const RasterView& rv, const 
   return hipGetLastError();
 }
 
-hipError_t launch_raster_draw(const RasterDraws& dr, const RasterView& rv, const RasterScratch& s, void* rgba8,
-                              float* depth, hipStream_t stream) {
+hipError_t launch_raster_draw(const RasterDraws& dr, const RasterView& rv, const RasterScratch& s, uint32_t bin_cap,
+                              void* rgba8, float* depth, hipStream_t stream) {
   const uint32_t nslots = dr.total * 7u;
   const uint32_t tx = (rv.width + 7) / 8, ty = (rv.height + 7) / 8, ntiles = tx * ty;
   if (dr.total) {
     hipError_t e = hipMemsetAsync(s.tcount, 0, (size_t)ntiles * 4, stream);
     if (e != hipSuccess) return e;
-    k_raster_bin<1><<<(nslots + 3) / 4, 256, 0, stream>>>(s.slots, s.tiles, nslots, tx, s.tcount, s.toffs, s.bins);
+    k_raster_bin<1><<<(nslots + 3) / 4, 256, 0, stream>>>(s.slots, s.tiles, nslots, tx, s.tcount, s.toffs, s.bins,
+                                                          bin_cap);
   }
-  k_raster_tile<<<(ntiles + 3) / 4, 256, 0, stream>>>(s.draws, s.clip, s.slots, s.toffs, s.bins, tx, ntiles, rv.width,
-                                                      rv.height, (uint32_t*)rgba8, depth);
+  k_raster_tile<<<(ntiles + 3) / 4, 256, 0, stream>>>(s.draws, s.clip, s.slots, s.toffs, s.bins, bin_cap, s.tiles,
+                                                      nslots, tx, ntiles, rv.width, rv.height, (uint32_t*)rgba8, depth);
   return hipGetLastError();
 }
 

@@ -97,3 +97,48 @@ def test_raster_argument_errors():
     with pytest.raises(rt.RtError):
         ctx.raster_draw([0], 4, 4, out)  # no BLAS, no camera
     ctx.close()
+
+
+def test_raster_bins_overflow_walks_slots(monkeypatch):
+    """A draw whose bin entries exceed the capacity (sized from an earlier draw: draws do not
+    synchronise) renders the same image through the slot walk; the capacity then grows."""
+    spec = scenes.config("REF")
+    W, H = spec.width, spec.height
+    x0 = spec.instances[0][1]
+    o8, od, _ = oracle.raster(list(spec.meshes), spec.camera_buffer(), W, H, x0)
+    ctx = rt.Context(0)
+    ids = scenes.upload(ctx, spec)
+    monkeypatch.setenv("RT_RASTER_BIN_CAP", "1")
+    img, depth = gpu_raster(ctx, ids, W, H, x0)  # capacity 1: every tile walks the slots
+    assert np.array_equal(img, o8)
+    assert np.array_equal(depth.view(np.uint32), od.view(np.uint32))
+    monkeypatch.delenv("RT_RASTER_BIN_CAP")
+    for _ in range(2):  # the first grows from the read-back total, the second uses the bins
+        img, depth = gpu_raster(ctx, ids, W, H, x0)
+        assert np.array_equal(img, o8)
+        assert np.array_equal(depth.view(np.uint32), od.view(np.uint32))
+    ctx.close()
+
+
+def test_raster_draws_stream_ordered():
+    """Back-to-back draws on one caller stream with no host synchronisation in between: three small
+    frames, then two 4x larger ones (the first of them overflows the bins sized from the small
+    frames' total and walks the slots, the second grows them); every output equals the oracle."""
+    spec = scenes.config("REF")
+    x0 = spec.instances[0][1]
+    ctx = rt.Context(0)
+    ids = scenes.upload(ctx, spec.with_size(320, 184))
+    stream = torch.cuda.Stream()
+    outs = []
+    for (W, H) in [(320, 184)] * 3 + [(1280, 736)] * 2:
+        ctx.set_camera(spec.with_size(W, H).camera_buffer())
+        img = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
+        ctx.raster_draw(ids, W, H, img, None, object_to_world=x0, stream=stream.cuda_stream)
+        outs.append((W, H, img))
+    torch.cuda.synchronize()
+    ref = {}
+    for W, H, img in outs:
+        if (W, H) not in ref:
+            ref[(W, H)] = oracle.raster(list(spec.meshes), spec.with_size(W, H).camera_buffer(), W, H, x0)[0]
+        assert np.array_equal(img.cpu().numpy(), ref[(W, H)]), (W, H)
+    ctx.close()
