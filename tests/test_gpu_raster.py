@@ -113,7 +113,7 @@ def test_raster_bins_overflow_walks_slots(monkeypatch):
     assert np.array_equal(img, o8)
     assert np.array_equal(depth.view(np.uint32), od.view(np.uint32))
     monkeypatch.delenv("RT_RASTER_BIN_CAP")
-    for _ in range(2):  # the first grows from the read-back total, the second uses the bins
+    for _ in range(2):  # the capacity grows from the total read back after the capped draw
         img, depth = gpu_raster(ctx, ids, W, H, x0)
         assert np.array_equal(img, o8)
         assert np.array_equal(depth.view(np.uint32), od.view(np.uint32))
