@@ -16,13 +16,20 @@ torchrun re-launches itself under torch.distributed.run (N processes, one per GP
 touches the GPU. The multi-GPU configs C4 (rabbit x64, 2 lights) and C5 (rabbit x256, 4 lights,
 4K, 4 spp) are timed the same way at the same N and reported under "extra".
 
+Frames in flight: consecutive frames are issued round robin over S render streams, each frame into
+its own buffer slot, so the waves of frame k + 1 fill the wave slots the tail of frame k leaves
+idle (a frame lasts as long as its slowest 8 x 8 tile; a reference-style renderer keeps two back
+buffers for the same reason). Every frame is rendered in full; S (1..3) is picked by an untimed
+autotune (pick_in_flight) and reported as config.frames_in_flight beside the one-stream frame time
+(config.frame_ms_one_stream, the roofline's per-launch time). --in-flight 1 gives the serial loop.
+
 value = rays traced in one step (all ranks, counted by the device counters in an untimed pass)
 x steps / max-over-ranks wall time of the timed region.
 
 Untimed before the W warmup frames: a clock settle (--settle-ms of frames: the GPU needs ~20 ms of
 load to reach its steady clock; with 5 warmup frames alone the same build read 0.20 ms instead of
-0.15 ms per frame; the ranks agree on its length, as every strips step is a collective), the
-tile-rows autotune (pick_tile_rows) and the counter pass.
+0.15 ms per frame; the ranks agree on its length), the tile-rows and frames-in-flight autotunes
+and the counter pass.
 """
 from __future__ import annotations
 
@@ -71,6 +78,8 @@ def parse(argv=None):
                    help="N>1: strips = one frame tiled over ranks + RCCL gather (default); frames = N "
                         "independent replicas (no collective)")
     p.add_argument("--no-pipeline", action="store_true", help="strips: gather after each frame, no overlap")
+    p.add_argument("--in-flight", type=int, default=0,
+                   help="frames in flight (render streams, one buffer each); 0 = untimed autotune over 1..3")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="minimum wall time of the CPU baseline sample")
     p.add_argument("--save-image", default="", help="write the rank-0 frame as .npy")
@@ -108,6 +117,7 @@ def spawn(a, argv) -> int:
 class HipBackend:
     """rt_* through the C-ABI on this rank's GPU; collectives over RCCL."""
     dist_backend = "nccl"
+    multi_stream = True  # streams run concurrently: frames in flight are worth measuring
 
     def __init__(self, local: int):
         import realtimeraytracing_gradproject_amd as rt
@@ -250,10 +260,36 @@ def pick_tile_rows(be, buf, rows, stream, frames: int = 8, rounds: int = 3):
     return pick, {k: round(v, 4) for k, v in best.items()}
 
 
+def pick_in_flight(be, W, NR, rows, frames: int = 16, rounds: int = 3, choices=(1, 2, 3)):
+    """Untimed autotune of the frames in flight: `frames` renders of this rank's share issued round
+    robin over S streams into S buffers, S in `choices`, interleaved, best of `rounds` (host wall
+    clock around the synchronised loop). With S > 1 the waves of frame k + 1 fill the wave slots
+    the tail of frame k leaves idle (a frame ends with its slowest 8 x 8 tile; measured in
+    tools/overlap_probe.py). Which streams share a hardware queue is the HIP runtime's choice, so
+    the count is measured, not assumed. A backend without streams of its own keeps 1. Returns
+    (S, {S: ms per frame})."""
+    if not getattr(be, "multi_stream", False):
+        return 1, None
+    streams = {n: [be.stream() for _ in range(n)] for n in choices}
+    bufs = {n: [be.zeros((NR, W, 4)) for _ in range(n)] for n in choices}
+    best = {n: float("inf") for n in choices}
+    for _ in range(rounds):
+        for n in choices:
+            be.synchronize()
+            t0 = time.perf_counter()
+            for k in range(frames):
+                be.dispatch(bufs[n][k % n], rows, streams[n][k % n])
+            be.synchronize()
+            best[n] = min(best[n], (time.perf_counter() - t0) * 1e3 / frames)
+    pick = min(choices, key=lambda n: (best[n], n))
+    return pick, {n: round(v, 4) for n, v in best.items()}
+
+
 def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_ms: float, strips: bool,
-               pipeline: bool, schedule: str, save_image: str = ""):
+               pipeline: bool, schedule: str, save_image: str = "", in_flight: int = 0):
     """Builds the scene, counts one step's rays (untimed), settles, warms up, then times exactly
-    `steps` steps between barrier + synchronize on both sides. Returns a dict (rank 0 meaningful)."""
+    `steps` steps between barrier + synchronize on both sides. Returns a dict (rank 0 meaningful).
+    in_flight: frames in flight (render streams, each with its own buffer slot); 0 = autotune."""
     from realtimeraytracing_gradproject_amd import distributed as D
     distributed = world > 1
     W, H = spec.width, spec.height
@@ -262,9 +298,35 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
         rows, rows_per_rank = strip_plan(H, world, rank)
     else:
         rows, rows_per_rank = None, H
-    nslot = 2 if (strips and pipeline) else 1
-    render = be.stream()
-    comm = be.stream() if strips else render
+    NR = rows_per_rank
+    comm = be.stream() if strips else None
+    # clock settle (untimed) on a plain single-stream loop before any autotune
+    if settle_ms > 0:
+        probe_s, probe_b = be.stream(), be.zeros((NR, W, 4))
+        t0 = time.perf_counter()
+        while True:
+            for _ in range(4):
+                be.dispatch(probe_b, rows, probe_s)
+            be.synchronize()
+            more = torch.tensor([1.0 if (time.perf_counter() - t0) * 1e3 < settle_ms else 0.0],
+                                dtype=torch.float64, device=be.device)
+            if distributed:
+                dist.all_reduce(more, op=dist.ReduceOp.MAX)
+            if more.item() == 0.0:
+                break
+        del probe_b
+
+    tile_rows, tile_ms = pick_tile_rows(be, be.zeros((NR, W, 4)), rows, be.stream())
+    if in_flight > 0:
+        nstream, flight_ms = in_flight, None
+    else:
+        nstream, flight_ms = pick_in_flight(be, W, NR, rows)
+        if distributed:  # the ranks agree (not required for correctness: the collectives stay in frame order)
+            t = torch.tensor([float(nstream)], dtype=torch.float64, device=be.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            nstream = int(t.item())
+    nslot = max(nstream, 2 if (strips and pipeline) else 1)
+    render = [be.stream() for _ in range(nstream)]
     local = [be.zeros((rows_per_rank, W, 4)) for _ in range(nslot)]
     gathered = [be.zeros((world, rows_per_rank, W, 4)) if rank == 0 else None for _ in range(nslot)] if strips else None
     frame = [be.zeros((H, W, 4)) if rank == 0 else None for _ in range(nslot)] if strips else None
@@ -274,11 +336,12 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
 
     def step(k: int):
         s = k % nslot
+        rs = render[s % nstream]  # a slot always renders on the same stream: its reuse is stream-ordered
         if strips:
-            be.wait(render, freed[s])  # slot s free: the gather of frame k - nslot is done
-        be.dispatch(local[s], rows, render)
+            be.wait(rs, freed[s])  # slot s free: the gather of frame k - nslot is done
+        be.dispatch(local[s], rows, rs)
         if strips:
-            be.record(rendered[s], render)
+            be.record(rendered[s], rs)
             be.wait(comm, rendered[s])
             with be.use_stream(comm):
                 D.gather_strips(local[s], world, rank, gathered[s], parts=parts[s])
@@ -286,27 +349,9 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
                     be.assemble(world, gathered[s], frame[s], comm)
             be.record(freed[s], comm)
 
-    # clock settle (untimed). Every rank must run the same number of steps (each strips step is a
-    # collective), so the ranks agree after every 4 steps whether any of them still needs time.
     k = 0
-    if settle_ms > 0:
-        t0 = time.perf_counter()
-        while True:
-            for _ in range(4):
-                step(k)
-                k += 1
-            be.synchronize()
-            more = torch.tensor([1.0 if (time.perf_counter() - t0) * 1e3 < settle_ms else 0.0],
-                                dtype=torch.float64, device=be.device)
-            if distributed:
-                dist.all_reduce(more, op=dist.ReduceOp.MAX)
-            if more.item() == 0.0:
-                break
-
-    tile_rows, tile_ms = pick_tile_rows(be, local[0], rows, render)
-
     # untimed counter pass: rays, tests and record fetches of this rank's share of one step
-    st = be.counted(local[0], rows, render)
+    st = be.counted(local[0], rows, render[0])
     counts = torch.tensor([st["primary_rays"] + st["shadow_rays"], st["primary_rays"], st["shadow_rays"]],
                           dtype=torch.float64, device=be.device)
     if distributed:
@@ -322,15 +367,17 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
         dist.barrier()
     be.synchronize()
 
-    # timed region. One HIP event pair on the render stream brackets it (per-launch events would
-    # put a timestamp between back-to-back frames); in strips mode the pair brackets renders only
+    # timed region (wall clock, synchronised on both sides). With one render stream and no strips a
+    # HIP event pair on it also gives the per-launch kernel time (per-launch events would put a
+    # timestamp between back-to-back frames)
+    single = nstream == 1 and not strips
     e0, e1 = be.event(True), be.event(True)
     t0 = time.perf_counter()
-    e0.record(render)
+    e0.record(render[0])
     for _ in range(steps):
         step(k)
         k += 1
-    e1.record(render)
+    e1.record(render[0])
     be.synchronize()
     if distributed:
         dist.barrier()
@@ -342,14 +389,15 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
     tmax = float(tmax.item())
     render_ms = e0.elapsed_time(e1) / steps
 
-    if strips:
-        # the roofline's kernel time: this rank's render alone, back to back (untimed for value)
+    if not single:
+        # the roofline's kernel time: this rank's render alone, back to back on one stream (untimed
+        # for value)
         be.synchronize()
         f0, f1 = be.event(True), be.event(True)
-        f0.record(render)
+        f0.record(render[0])
         for _ in range(max(5, min(steps, 50))):
-            be.dispatch(local[0], rows, render)
-        f1.record(render)
+            be.dispatch(local[0], rows, render[0])
+        f1.record(render[0])
         be.synchronize()
         kernel_ms = f0.elapsed_time(f1) / max(5, min(steps, 50))
     else:
@@ -357,11 +405,11 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
 
     if save_image and rank == 0:
         last = (k - 1) % nslot
-        img = frame[last] if strips else local[0][:H]
+        img = frame[last] if strips else local[last][:H]
         np.save(save_image, img.cpu().numpy())
     return {"rays_step": rays_step, "primary": int(counts[1].item()), "shadow": int(counts[2].item()),
             "tmax": tmax, "kernel_ms": kernel_ms, "stats": st, "build": build, "rows_local": len(rows) if strips else H,
-            "tile_rows": tile_rows, "tile_ms": tile_ms}
+            "tile_rows": tile_rows, "tile_ms": tile_ms, "in_flight": nstream, "in_flight_ms": flight_ms}
 
 
 # ---------------------------------------------------------------------------------------------
@@ -563,7 +611,7 @@ def main(argv=None) -> int:
 
     spec = spec_of(a.config)
     r = run_config(be, spec, world, rank, a.steps, a.warmup, a.settle_ms, strips, not a.no_pipeline, a.schedule,
-                   a.save_image)
+                   a.save_image, a.in_flight)
 
     extra = []
     names = a.extra if a.extra is not None else ("C4,C5" if distributed else "C1,C2F,C3,C4,C5,REF")
@@ -571,7 +619,8 @@ def main(argv=None) -> int:
         es = spec_of(name)
         # few frames: C5 is ~8 ms per frame on one GPU
         n_steps = max(3, a.steps // (20 if es.spp > 1 else 4))
-        x = run_config(be, es, world, rank, n_steps, 2, 0.0, strips, not a.no_pipeline, a.schedule)
+        x = run_config(be, es, world, rank, n_steps, 2, 0.0, strips, not a.no_pipeline, a.schedule,
+                       in_flight=a.in_flight)
         if rank == 0:
             st = x["stats"]
             rays = max(x["rays_step"], 1)
@@ -579,7 +628,7 @@ def main(argv=None) -> int:
                           "frame_ms": round(x["tmax"] / n_steps * 1e3, 4), "kernel_ms": round(x["kernel_ms"], 4),
                           "rays_per_step": x["rays_step"], "resolution": f"{es.width}x{es.height}", "spp": es.spp,
                           "n_gpus": world, "parallelism": f"strips{world}+gather" if strips else f"frames{world}",
-                          "tile_rows": x["tile_rows"],
+                          "tile_rows": x["tile_rows"], "frames_in_flight": x["in_flight"],
                           "aabb_tests_per_ray_rank0": round(st["aabb_tests"] / rays, 2) if not distributed else None,
                           "node_fetches": int(st["node_fetches"]), "tri_fetches": int(st["tri_fetches"])})
     if not distributed and (a.extra is None) and isinstance(be, HipBackend):
@@ -614,6 +663,8 @@ def main(argv=None) -> int:
                        else f"frames{world}",
                        "rccl_world_size": world if distributed else None, "schedule": a.schedule,
                        "tile_rows": r["tile_rows"], "tile_ms_rank0": r["tile_ms"],
+                       "frames_in_flight": r["in_flight"], "in_flight_ms_rank0": r["in_flight_ms"],
+                       "frame_ms_one_stream": round(r["kernel_ms"], 4),
                        "settle_ms": a.settle_ms},
             "roofline": rf,
             "cpu_baseline": cpu,

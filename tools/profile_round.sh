@@ -1,6 +1,7 @@
 #!/bin/bash
 # rocprofv3 passes of a round (run on the GPU box from the repo root), per config:
-#   kt    kernel trace + stats over bench.py            -> gpurun_out/prof_<tag>_<cfg>_kt/
+#   kt    kernel trace + stats over bench.py, one frame in flight (per-launch durations not
+#         stretched by a concurrent frame)              -> gpurun_out/prof_<tag>_<cfg>_kt/
 #   pmc1  FETCH_SIZE                                   -> gpurun_out/prof_<tag>_<cfg>_pmc1/
 #   pmc2  WRITE_SIZE (TCC slots: not with FETCH_SIZE)  -> gpurun_out/prof_<tag>_<cfg>_pmc2/
 #   pmc3  wave / issue-stall SQ counters               -> gpurun_out/prof_<tag>_<cfg>_pmc3/
@@ -17,7 +18,7 @@ sha256sum "$R/realtimeraytracing_gradproject_amd/lib/librtamd.so" > "$O/prof_${T
 cd /tmp && export TMPDIR=/tmp
 for CFG in $CFGS; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_${TAG}_${CFG}_kt" -o run --output-format csv \
-    -- python3 "$R/bench.py" --config "$CFG" --no-cpu-baseline --extra= --steps 100 --warmup 20 \
+    -- python3 "$R/bench.py" --config "$CFG" --no-cpu-baseline --extra= --steps 100 --warmup 20 --in-flight 1 \
     > "$O/prof_${TAG}_${CFG}_kt.log" 2>&1 || { echo "kt $CFG failed rc=$?"; exit 1; }
   i=0
   for set in "FETCH_SIZE" "WRITE_SIZE" \
