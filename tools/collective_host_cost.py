@@ -46,8 +46,17 @@ def main():
         def ag():
             dist.all_gather_into_tensor(flat, lflat)
 
+        pg = dist.distributed_c10d._get_default_group()
+        gopts = dist.GatherOptions()
+        gopts.rootRank = 0
+        outs, ins = [parts], [local]
+
+        def gd():  # the ProcessGroup call dist.gather makes, without its Python-side checks
+            pg.gather(outs, ins, gopts).wait()
+
         res = {}
-        for name, fn in (("gather", g), ("all_gather_into_tensor", ag), ("gather", g), ("all_gather_into_tensor", ag)):
+        for name, fn in (("gather", g), ("all_gather_into_tensor", ag), ("pg_gather", gd), ("gather", g),
+                         ("all_gather_into_tensor", ag), ("pg_gather", gd)):
             with torch.cuda.stream(comm):
                 for _ in range(100):
                     fn()
