@@ -1,6 +1,6 @@
 """Host issue cost of bench.py's strips loop on ONE GPU: bench.run_config itself, strips forced, in a
-world-1 RCCL group (the gather is a local copy), with renders and gathers issued from one host
-thread or from two. A frame of 1920 x (1080 / N) stands in for rank 0's share of a 1080p frame
+world-1 RCCL group (the gather is a local copy). (A two-thread issue variant of the loop — renders
+on one host thread, gathers on another — was measured with this probe and dropped: DESIGN §7.) A frame of 1920 x (1080 / N) stands in for rank 0's share of a 1080p frame
 tiled over N ranks (the same rows per rank, so the same render and issue work per step).
   python tools/strips_issue_probe.py --shares 1,8
 """
@@ -34,11 +34,10 @@ def main():
     for n in [int(x) for x in a.shares.split(",")]:
         base = scenes.config(a.config)
         spec = base.with_size(base.width, (base.height + n - 1) // n)
-        res = {"one_thread": [], "two_threads": []}
+        res = {"step_ms": []}
         for _ in range(a.rounds):
-            for name, thr in (("one_thread", False), ("two_threads", True)):
-                r = bench.run_config(be, spec, 1, 0, a.steps, 50, 50.0, True, True, "packet", issue_threads=thr)
-                res[name].append(r["tmax"] / a.steps * 1e3)
+            r = bench.run_config(be, spec, 1, 0, a.steps, 50, 50.0, True, True, "packet")
+            res["step_ms"].append(r["tmax"] / a.steps * 1e3)
         out[f"share{n}"] = {k: round(sorted(v)[len(v) // 2], 4) for k, v in res.items()}
         out[f"share{n}"]["render_one_stream_ms"] = round(r["kernel_ms"], 4)
         out[f"share{n}"]["in_flight"] = r["in_flight"]
