@@ -19,8 +19,8 @@ touches the GPU. The multi-GPU configs C4 (rabbit x64, 2 lights) and C5 (rabbit 
 Frames in flight: consecutive frames are issued round robin over S render streams, each frame into
 its own buffer slot, so the waves of frame k + 1 fill the wave slots the tail of frame k leaves
 idle (a frame lasts as long as its slowest 8 x 8 tile; a reference-style renderer keeps two back
-buffers for the same reason). Every frame is rendered in full; S (1..3) is picked by an untimed
-autotune (pick_in_flight) and reported as config.frames_in_flight beside the one-stream frame time
+buffers for the same reason). Every frame is rendered in full; S (1..4) is picked by an untimed
+autotune (pick_in_flight, per rank) and reported as config.frames_in_flight beside the one-stream frame time
 (config.frame_ms_one_stream, the roofline's per-launch time). --in-flight 1 gives the serial loop.
 
 value = rays traced in one step (all ranks, counted by the device counters in an untimed pass)
@@ -79,7 +79,7 @@ def parse(argv=None):
                         "independent replicas (no collective)")
     p.add_argument("--no-pipeline", action="store_true", help="strips: gather after each frame, no overlap")
     p.add_argument("--in-flight", type=int, default=0,
-                   help="frames in flight (render streams, one buffer each); 0 = untimed autotune over 1..3")
+                   help="frames in flight (render streams, one buffer each); 0 = untimed autotune over 1..4")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="minimum wall time of the CPU baseline sample")
     p.add_argument("--save-image", default="", help="write the rank-0 frame as .npy")
@@ -260,29 +260,30 @@ def pick_tile_rows(be, buf, rows, stream, frames: int = 8, rounds: int = 3):
     return pick, {k: round(v, 4) for k, v in best.items()}
 
 
-def pick_in_flight(be, W, NR, rows, frames: int = 16, rounds: int = 3, choices=(1, 2, 3)):
+def pick_in_flight(be, W, NR, rows, frames: int = 16, rounds: int = 3, choices=(1, 2, 3, 4)):
     """Untimed autotune of the frames in flight: `frames` renders of this rank's share issued round
-    robin over S streams into S buffers, S in `choices`, interleaved, best of `rounds` (host wall
-    clock around the synchronised loop). With S > 1 the waves of frame k + 1 fill the wave slots
-    the tail of frame k leaves idle (a frame ends with its slowest 8 x 8 tile; measured in
-    tools/overlap_probe.py). Which streams share a hardware queue is the HIP runtime's choice, so
-    the count is measured, not assumed. A backend without streams of its own keeps 1. Returns
-    (S, {S: ms per frame})."""
+    robin over the first S streams of one stream pool into S buffers, S in `choices`, interleaved,
+    best of `rounds` (host wall clock around the synchronised loop). With S > 1 the waves of frame
+    k + 1 fill the wave slots the tail of frame k leaves idle (a frame ends with its slowest 8 x 8
+    tile; tools/overlap_probe.py). Which streams share a hardware queue is the HIP runtime's choice
+    (two streams can land on one queue and then run one after the other), so the count is
+    measured, not assumed, and the caller renders on the very streams that were measured. A backend
+    without streams of its own keeps 1. Returns (S, {S: ms per frame}, the S streams)."""
     if not getattr(be, "multi_stream", False):
-        return 1, None
-    streams = {n: [be.stream() for _ in range(n)] for n in choices}
-    bufs = {n: [be.zeros((NR, W, 4)) for _ in range(n)] for n in choices}
+        return 1, None, None
+    pool = [be.stream() for _ in range(max(choices))]
+    bufs = [be.zeros((NR, W, 4)) for _ in range(max(choices))]
     best = {n: float("inf") for n in choices}
     for _ in range(rounds):
         for n in choices:
             be.synchronize()
             t0 = time.perf_counter()
             for k in range(frames):
-                be.dispatch(bufs[n][k % n], rows, streams[n][k % n])
+                be.dispatch(bufs[k % n], rows, pool[k % n])
             be.synchronize()
             best[n] = min(best[n], (time.perf_counter() - t0) * 1e3 / frames)
     pick = min(choices, key=lambda n: (best[n], n))
-    return pick, {n: round(v, 4) for n, v in best.items()}
+    return pick, {n: round(v, 4) for n, v in best.items()}, pool[:pick]
 
 
 def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_ms: float, strips: bool,
@@ -317,16 +318,13 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
         del probe_b
 
     tile_rows, tile_ms = pick_tile_rows(be, be.zeros((NR, W, 4)), rows, be.stream())
+    measured = None
     if in_flight > 0:
         nstream, flight_ms = in_flight, None
     else:
-        nstream, flight_ms = pick_in_flight(be, W, NR, rows)
-        if distributed:  # the ranks agree (not required for correctness: the collectives stay in frame order)
-            t = torch.tensor([float(nstream)], dtype=torch.float64, device=be.device)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            nstream = int(t.item())
+        nstream, flight_ms, measured = pick_in_flight(be, W, NR, rows)
+    render = measured if measured else [be.stream() for _ in range(nstream)]
     nslot = max(nstream, 2 if (strips and pipeline) else 1)
-    render = [be.stream() for _ in range(nstream)]
     local = [be.zeros((rows_per_rank, W, 4)) for _ in range(nslot)]
     gathered = [be.zeros((world, rows_per_rank, W, 4)) if rank == 0 else None for _ in range(nslot)] if strips else None
     frame = [be.zeros((H, W, 4)) if rank == 0 else None for _ in range(nslot)] if strips else None
