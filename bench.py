@@ -333,6 +333,8 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
     parts = [D.gather_parts(gathered[s], world, rank) for s in range(nslot)] if strips else None
 
     def step(k: int):
+        """One frame. In strips mode the caller holds `comm` as the current stream (the gather runs
+        on it; everything else names its stream explicitly), so no stream context is entered per step."""
         s = k % nslot
         rs = render[s % nstream]  # a slot always renders on the same stream: its reuse is stream-ordered
         if strips:
@@ -341,11 +343,13 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
         if strips:
             be.record(rendered[s], rs)
             be.wait(comm, rendered[s])
-            with be.use_stream(comm):
-                D.gather_strips(local[s], world, rank, gathered[s], parts=parts[s])
-                if rank == 0:
-                    be.assemble(world, gathered[s], frame[s], comm)
+            D.gather_strips(local[s], world, rank, gathered[s], parts=parts[s])
+            if rank == 0:
+                be.assemble(world, gathered[s], frame[s], comm)
             be.record(freed[s], comm)
+
+    import contextlib
+    on_comm = (lambda: be.use_stream(comm)) if strips else contextlib.nullcontext
 
     k = 0
     # untimed counter pass: rays, tests and record fetches of this rank's share of one step
@@ -357,9 +361,10 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
     rays_step = int(counts[0].item())  # strips: one frame over all ranks; frames mode: N frames
 
     # warmup (untimed)
-    for _ in range(warmup):
-        step(k)
-        k += 1
+    with on_comm():
+        for _ in range(warmup):
+            step(k)
+            k += 1
     be.synchronize()
     if distributed:
         dist.barrier()
@@ -372,9 +377,10 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
     e0, e1 = be.event(True), be.event(True)
     t0 = time.perf_counter()
     e0.record(render[0])
-    for _ in range(steps):
-        step(k)
-        k += 1
+    with on_comm():
+        for _ in range(steps):
+            step(k)
+            k += 1
     e1.record(render[0])
     be.synchronize()
     if distributed:
