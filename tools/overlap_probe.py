@@ -25,10 +25,11 @@ def main():
     ap.add_argument("--streams", default="2,3")
     ap.add_argument("--frames", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--lib", default="", help="a library variant (tools/build_variant.sh) instead of the shipped one")
     a = ap.parse_args()
     spec = scenes.config(a.config)
     W, H = spec.width, spec.height
-    ctx = rt.Context(0)
+    ctx = rt.Context(0, library=rt._load(a.lib)) if a.lib else rt.Context(0)
     scenes.upload(ctx, spec)
     out = {}
     for n in [int(x) for x in a.shares.split(",")]:
