@@ -229,7 +229,9 @@ rt_status rt_trace_rays(rt_ctx_t ctx, const float* rays_dev, uint32_t n, uint32_
  * next vertex's position.x; 0 for the last vertex). rgba8: W x H RGBA8 (cleared to
  * {0.03, 0.35, 0.43, 1}); depth32f: optional W x H floats. Device pointers, on `stream`.
  * Asynchronous, except the first draw of a context (one 4-byte read-back sizes the tile bins) and
- * draws that must grow buffers or upload a changed draw list (they wait for in-flight work). */
+ * draws that must grow buffers or upload a changed draw list (they wait for in-flight work).
+ * Test hook: the environment variable RT_RASTER_BIN_CAP caps the tile-bin capacity (a draw that
+ * overflows it renders the same image through the slower slot walk). */
 rt_status rt_raster_draw(rt_ctx_t ctx, const rt_blas_t* draws, uint32_t ndraws, const float* object_to_world,
                          uint32_t W, uint32_t H, void* rgba8, float* depth32f, void* stream);
 
