@@ -17,13 +17,19 @@ CXXFLAGS  := -O2 -std=c++17 -fPIC -ffp-contract=off -Wall
 # Oracle: scalar C, explicit fmaf in the slab test (matches __builtin_fmaf on the GPU).
 OCFLAGS   := -O2 -std=c11 -fPIC -ffp-contract=off -mfma -Wall -Wno-unused-function
 
+# CPU baseline: the same restatement at -O3, scalar (no SIMD intrinsics; -mfma for the
+# slab test's explicit fmaf; no errno, so sqrtf stays one instruction), counters compiled out, plain-compare
+# min/max in the slab test (rt_oracle.c OMINF). Same frames as the checker. Bench-only, like the checker.
+BCFLAGS   := -O3 -std=c11 -fPIC -ffp-contract=off -fno-math-errno -mfma -DORACLE_NO_COUNTERS
+
 LIB       := $(LIBDIR)/librtamd.so
 APP       := $(LIBDIR)/rt_app
 ORACLE    := oracle/liboracle.so
+BASELINE  := oracle/libbaseline.so
 
 HDRS      := include/rt_api.h $(SRC)/rt_device.hpp $(SRC)/rt_internal.hpp
 
-all: $(LIB) $(APP) $(ORACLE)
+all: $(LIB) $(APP) $(ORACLE) $(BASELINE)
 
 $(BUILD)/%.o: $(SRC)/%.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -49,7 +55,10 @@ $(APP): $(SRC)/host/rt_app.cpp $(wildcard $(SRC)/host/*.hpp) $(LIB) | $(LIBDIR)
 	    -L$(LIBDIR) -lrtamd -L$(ROCM)/lib -lamdhip64 -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(ROCM)/lib
 
 $(ORACLE): oracle/rt_oracle.c oracle/rt_raster_oracle.c oracle/rt_oracle.h
-	gcc $(OCFLAGS) -shared -o $@ oracle/rt_oracle.c oracle/rt_raster_oracle.c -lm -lpthread
+	gcc $(OCFLAGS) -DORACLE_FLAGS='"$(OCFLAGS)"' -shared -o $@ oracle/rt_oracle.c oracle/rt_raster_oracle.c -lm -lpthread
+
+$(BASELINE): oracle/rt_oracle.c oracle/rt_raster_oracle.c oracle/rt_oracle.h
+	gcc $(BCFLAGS) -DORACLE_FLAGS='"$(BCFLAGS)"' -shared -o $@ oracle/rt_oracle.c oracle/rt_raster_oracle.c -lm -lpthread
 
 ref:
 	$(MAKE) -C oracle -f Makefile.ref
@@ -58,6 +67,6 @@ $(BUILD) $(LIBDIR):
 	mkdir -p $@
 
 clean:
-	rm -rf $(BUILD) $(LIB) $(APP) $(ORACLE)
+	rm -rf $(BUILD) $(LIB) $(APP) $(ORACLE) $(BASELINE)
 
 .PHONY: all clean ref

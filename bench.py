@@ -496,26 +496,28 @@ def _cgroup_cpus():
         return None
 
 
-def _cpu_rate(o, spec, threads: int, seconds: float):
-    """Frames of the oracle's per-ray traversal until `seconds` passed: (Mrays/s, frames, wall)."""
-    rays = frames = 0
-    t0 = time.perf_counter()
-    while True:
-        _, _, st = o.render_spec(spec, nthreads=threads, want_float=False, schedule=1)  # per-ray: the CPU form
-        rays += int(st[0] + st[1])
-        frames += 1
-        dt = time.perf_counter() - t0
-        if dt >= seconds:
-            return rays / dt / 1e6, frames, dt
+def _frame_median(o, spec, threads: int, frames: int = 5):
+    """BASELINE.md section 3 timing: one warm-up frame, then the median wall time of `frames` frames of the
+    per-ray traversal (the CPU form: one traversal per ray, LANE order) at `threads` threads."""
+    o.render_spec(spec, nthreads=threads, want_float=False, schedule=1)
+    ts = []
+    for _ in range(frames):
+        t0 = time.perf_counter()
+        o.render_spec(spec, nthreads=threads, want_float=False, schedule=1)
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), float(sum(ts))
 
 
-def cpu_baseline(spec, seconds: float):
-    """oracle/rt_oracle.c (scalar C, per-ray traversal over the identical trees, pthreads over
-    interleaved rows) on the same frame on this host: with one thread per CPU the process may run on
-    (os.sched_getaffinity), and — when a cgroup CPU quota caps the process below that (the GPU box
-    gives one GPU's job 16 CPUs' worth of time on a 256-CPU host) — with one thread per CPU of the
-    quota too; `value` is the better of the two. Plus one thread, and C1 (BASELINE configs[0]:
-    teapot 512^2 primary only, the reference's CPU plumbing case)."""
+def cpu_baseline(spec, seconds: float = 0.0):
+    """BASELINE.md section 3's CPU baseline: oracle/libbaseline.so — the oracle's scalar C restatement
+    (per-ray traversal of the identical trees, identical shading, pthreads over interleaved rows) built at
+    -O3 with the counters compiled out (frames identical to the checker's) — on the same frame on this
+    host. Threads: one per CPU the process may run on (os.sched_getaffinity) and, when a cgroup CPU quota
+    caps the process below that (the GPU box gives one GPU's job 16 CPUs' worth of time on a 256-CPU host),
+    one per CPU of the quota; `value` is the better. Plus one thread, the checker build (liboracle.so: -O2,
+    counters on) for comparison, and C1 (BASELINE configs[0]: teapot 512^2 primary only). Rays per frame come
+    from the checker's counters (deterministic). Each figure: one warm-up frame, median of 5 frames.
+    `seconds` is unused (kept for the CLI)."""
     import math
     import oracle
     from realtimeraytracing_gradproject_amd import scenes
@@ -525,21 +527,28 @@ def cpu_baseline(spec, seconds: float):
     counts = [min(256, ncpu)]  # oracle_render caps its pool at 256 threads
     if quota and math.ceil(quota) < counts[0]:
         counts.append(max(1, math.ceil(quota)))
-    o = oracle.Scene(spec)
+    blib = oracle.baseline_lib()
+    t_all = time.perf_counter()
+
+    def rays_of(sp):
+        _, _, st = oracle.Scene(sp).render_spec(sp, nthreads=counts[-1], want_float=False, schedule=1)
+        return int(st[0] + st[1])
+
+    rays = rays_of(spec)
+    o = oracle.Scene(spec, library=blib)
     runs = []
     for th in counts:
-        v, frames, dt = _cpu_rate(o, spec, th, seconds / len(counts))
-        runs.append({"threads": th, "value": round(v, 3), "frames": frames, "wall_s": round(dt, 2)})
+        med, wall = _frame_median(o, spec, th)
+        runs.append({"threads": th, "value": round(rays / med / 1e6, 3), "frame_s": round(med, 4),
+                     "wall_s": round(wall, 2)})
     best = max(runs, key=lambda r: r["value"])
-    t1 = time.perf_counter()
-    _, _, st1 = o.render_spec(spec, nthreads=1, want_float=False, schedule=1)
-    dt1 = time.perf_counter() - t1
+    med1, _ = _frame_median(o, spec, 1)
+    chk, _ = _frame_median(oracle.Scene(spec), spec, best["threads"], frames=3)
     c1 = scenes.config("C1")
-    o1 = oracle.Scene(c1)
-    v1, n1, _ = _cpu_rate(o1, c1, best["threads"], 2.0)
-    t3 = time.perf_counter()
-    _, _, s1b = o1.render_spec(c1, nthreads=1, want_float=False, schedule=1)
-    d3 = time.perf_counter() - t3
+    r1 = rays_of(c1)
+    o1 = oracle.Scene(c1, library=blib)
+    m1, _ = _frame_median(o1, c1, best["threads"])
+    m1s, _ = _frame_median(o1, c1, 1)
     model = None
     try:
         with open("/proc/cpuinfo") as f:
@@ -547,13 +556,17 @@ def cpu_baseline(spec, seconds: float):
     except OSError:
         pass
     return {"value": best["value"], "unit": "Mrays/s", "cores": best["threads"], "kind": "port",
-            "sample": f"{best['frames']} full {spec.name} frame(s) {spec.width}x{spec.height} by oracle/rt_oracle.c "
-                      f"per-ray traversal ({best['threads']} threads, {best['wall_s']} s wall)",
-            "runs": runs, "single_thread": round(int(st1[0] + st1[1]) / dt1 / 1e6, 3), "host_cpus": ncpu,
-            "os_cpu_count": os.cpu_count(), "cgroup_cpu_quota": quota, "cpu_model": model,
-            "C1": {"value": round(v1, 3), "unit": "Mrays/s", "cores": best["threads"],
-                   "single_thread": round(int(s1b[0] + s1b[1]) / d3 / 1e6, 3),
-                   "sample": f"{n1} C1 frame(s) 512x512 primary only"}}
+            "build": blib.oracle_build_info().decode(),
+            "sample": f"{spec.name} {spec.width}x{spec.height} full frames ({rays} rays each): oracle/libbaseline.so "
+                      f"per-ray traversal, {best['threads']} threads, 1 warm-up + median of 5 frames",
+            "runs": runs, "single_thread": round(rays / med1 / 1e6, 3),
+            "checker": {"value": round(rays / chk / 1e6, 3), "threads": best["threads"],
+                        "build": "oracle/liboracle.so (-O2, counters on: the parity checker)"},
+            "host_cpus": ncpu, "os_cpu_count": os.cpu_count(), "cgroup_cpu_quota": quota, "cpu_model": model,
+            "wall_s": round(time.perf_counter() - t_all, 1),
+            "C1": {"value": round(r1 / m1 / 1e6, 3), "unit": "Mrays/s", "cores": best["threads"],
+                   "single_thread": round(r1 / m1s / 1e6, 3),
+                   "sample": f"C1 512x512 primary only ({r1} rays), 1 warm-up + median of 5 frames"}}
 
 
 def measure_raster(be, spec, steps: int, warmup: int) -> dict:

@@ -196,7 +196,10 @@ rt_status rt_set_stats(rt_ctx_t ctx, int enable);
  * rows, in order); the output is compact: row r of the output is global row rows[r].
  * rgba8_dev: device buffer of nrows*W*4 bytes, R8G8B8A8_UNORM (D3D12HelloTriangle.cpp:971).
  * rgba32f_dev: optional device buffer of nrows*W*4 floats (the pre-quantisation float4), or NULL.
- * hip_stream: hipStream_t or NULL (context stream). Asynchronous. */
+ * hip_stream: hipStream_t or NULL (context stream). Asynchronous, and frames may be in flight on several
+ * streams at once (the reference keeps two frames in its swap chain): the per-launch device scratch — the row
+ * list's device copy and, for trees deeper than the 32-entry LDS stack, the HBM overflow stack — comes from a
+ * small ring of slots, each ordered on the device after the other streams' last uses of it (no host wait). */
 rt_status rt_dispatch_rays(rt_ctx_t ctx, uint32_t W, uint32_t H, const uint32_t* rows,
                            uint32_t nrows, void* rgba8_dev, float* rgba32f_dev, void* hip_stream);
 
@@ -213,7 +216,8 @@ enum {
  * ray_flags: RT_RAY_FLAG_* (other bits, or both cull flags: RT_E_INVALID). Front faces are clockwise seen from the
  * ray origin (DXR's default), flipped by an instance transform with a negative determinant.
  * hits_dev: n x 4 x 32-bit: (t as float, instance_id, primitive index, hit flag) with u,v written
- * to uv_dev (n x 2 floats) when uv_dev != NULL. A miss has hit flag 0 and t = tmax. Asynchronous. */
+ * to uv_dev (n x 2 floats) when uv_dev != NULL. A miss has hit flag 0 and t = tmax. Asynchronous; may run
+ * concurrently with frames and other batches on other streams (per-launch overflow stack, as rt_dispatch_rays). */
 rt_status rt_trace_rays(rt_ctx_t ctx, const float* rays_dev, uint32_t n, uint32_t ray_flags,
                         uint32_t* hits_dev, float* uv_dev, void* hip_stream);
 
@@ -229,7 +233,8 @@ rt_status rt_trace_rays(rt_ctx_t ctx, const float* rays_dev, uint32_t n, uint32_
  * next vertex's position.x; 0 for the last vertex). rgba8: W x H RGBA8 (cleared to
  * {0.03, 0.35, 0.43, 1}); depth32f: optional W x H floats. Device pointers, on `stream`.
  * Asynchronous, except the first draw of a context (one 4-byte read-back sizes the tile bins) and
- * draws that must grow buffers or upload a changed draw list (they wait for in-flight work).
+ * draws that must grow buffers or upload a changed draw list (they wait for in-flight work). The raster
+ * scratch is per context: a draw issued on another stream than the previous draw waits for it on the device.
  * Test hook: the environment variable RT_RASTER_BIN_CAP caps the tile-bin capacity (a draw that
  * overflows it renders the same image through the slower slot walk). */
 rt_status rt_raster_draw(rt_ctx_t ctx, const rt_blas_t* draws, uint32_t ndraws, const float* object_to_world,

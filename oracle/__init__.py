@@ -51,14 +51,18 @@ _SIGS = [
     ("oracle_pbr", None, [_FP, _FP, _FP, ctypes.POINTER(oracle_light), _U32, _FP, _FP]),
     ("oracle_direct", None, [_FP, _FP, ctypes.POINTER(oracle_light), _U32, _FP, _FP]),
     ("oracle_pow", ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
+    ("oracle_max_stack_reached", _I, [_I]),
 ]
 
 
-def _load():
-    if not os.path.exists(LIB_PATH):
-        raise ImportError(f"{LIB_PATH} missing: run `make oracle/liboracle.so`")
-    lib = ctypes.CDLL(LIB_PATH)
-    for n, r, a in _SIGS:
+BASELINE_PATH = os.path.join(_HERE, "libbaseline.so")
+
+
+def _load(path=LIB_PATH, sigs=None):
+    if not os.path.exists(path):
+        raise ImportError(f"{path} missing: run `make {os.path.relpath(path, os.path.dirname(_HERE))}`")
+    lib = ctypes.CDLL(path)
+    for n, r, a in (sigs if sigs is not None else _SIGS):
         f = getattr(lib, n)
         f.restype = r
         f.argtypes = a
@@ -66,6 +70,16 @@ def _load():
 
 
 lib = _load()
+_baseline = None
+
+
+def baseline_lib():
+    """oracle/libbaseline.so: the same C restatement built as BASELINE.md section 3's CPU baseline
+    (-O3, counters compiled out; identical frames). Loaded on first use (bench.py's cpu_baseline leg)."""
+    global _baseline
+    if _baseline is None:
+        _baseline = _load(BASELINE_PATH, _SIGS + [("oracle_build_info", ctypes.c_char_p, [])])
+    return _baseline
 
 
 def _f(a):
@@ -163,6 +177,11 @@ def raster(draws, cb, W: int, H: int, object_to_world=None):
     return rgba8, depth, prim
 
 
+def max_stack_reached(reset: bool = True) -> int:
+    """Deepest per-ray (LANE-order) traversal stack the oracle reached since the last reset."""
+    return int(lib.oracle_max_stack_reached(1 if reset else 0))
+
+
 def pow_(x: float, y: float) -> float:
     return float(lib.oracle_pow(x, y))
 
@@ -170,24 +189,25 @@ def pow_(x: float, y: float) -> float:
 class Scene:
     """Oracle twin of a product scene (same LBVH, same traversal order)."""
 
-    def __init__(self, spec=None):
-        self._h = lib.oracle_scene_create()
+    def __init__(self, spec=None, library=None):
+        self._lib = library if library is not None else lib
+        self._h = self._lib.oracle_scene_create()
         self.blas_ids = []
         if spec is not None:
             self.load(spec)
 
     def __del__(self):
-        if getattr(self, "_h", None) and lib is not None:
-            lib.oracle_scene_destroy(self._h)
+        if getattr(self, "_h", None) and getattr(self, "_lib", None) is not None:
+            self._lib.oracle_scene_destroy(self._h)
             self._h = None
 
     def add_blas(self, verts, idx=None) -> int:
         v, vp = _f(verts)
         if idx is None:
-            r = lib.oracle_add_blas(self._h, vp, v.shape[0], None, 0)
+            r = self._lib.oracle_add_blas(self._h, vp, v.shape[0], None, 0)
         else:
             i = np.ascontiguousarray(idx, dtype=np.uint32)
-            r = lib.oracle_add_blas(self._h, vp, v.shape[0], i.ctypes.data_as(_P), i.size)
+            r = self._lib.oracle_add_blas(self._h, vp, v.shape[0], i.ctypes.data_as(_P), i.size)
         if r < 0:
             raise RuntimeError("oracle_add_blas failed")
         return r
@@ -199,7 +219,7 @@ class Scene:
             arr[k].xform[:] = [float(v) for v in np.asarray(x, np.float32).ravel()]
             arr[k].instance_id = iid
             arr[k].hit_group = hg
-        if lib.oracle_set_instances(self._h, arr, len(instances)):
+        if self._lib.oracle_set_instances(self._h, arr, len(instances)):
             raise RuntimeError("oracle_set_instances failed")
 
     def load(self, spec):
@@ -209,25 +229,25 @@ class Scene:
 
     def blas_info(self, b):
         out = np.zeros(4, np.uint32)
-        lib.oracle_blas_info(self._h, b, out.ctypes.data_as(_P))
+        self._lib.oracle_blas_info(self._h, b, out.ctypes.data_as(_P))
         return out
 
     def tlas_info(self):
         out = np.zeros(4, np.uint32)
-        lib.oracle_tlas_info(self._h, out.ctypes.data_as(_P))
+        self._lib.oracle_tlas_info(self._h, out.ctypes.data_as(_P))
         return out
 
     def export_blas(self, b):
         prims, nn, _, _ = self.blas_info(b)
         nodes = np.zeros(nn * 32, np.uint32)  # 128-B 4-wide nodes
         tris = np.zeros(prims * 12, np.uint32)
-        lib.oracle_export_blas(self._h, b, nodes.ctypes.data_as(_P), tris.ctypes.data_as(_P))
+        self._lib.oracle_export_blas(self._h, b, nodes.ctypes.data_as(_P), tris.ctypes.data_as(_P))
         return nodes.reshape(-1, 32), tris.reshape(-1, 12)
 
     def export_tlas(self):
         _, nn, _, _ = self.tlas_info()
         nodes = np.zeros(nn * 32, np.uint32)
-        lib.oracle_export_tlas(self._h, nodes.ctypes.data_as(_P))
+        self._lib.oracle_export_tlas(self._h, nodes.ctypes.data_as(_P))
         return nodes.reshape(-1, 32)
 
     def render(self, cb, lights, material, mode, spp, W, H, rows: Optional[np.ndarray] = None, nthreads=1,
@@ -242,7 +262,7 @@ class Scene:
         if rows is not None:
             r = np.ascontiguousarray(rows, dtype=np.uint32)
             rp = r.ctypes.data_as(_P)
-        st = lib.oracle_render(self._h, cp, _lights(lights), len(lights), mp, mode, spp, W, H, rp, nrows,
+        st = self._lib.oracle_render(self._h, cp, _lights(lights), len(lights), mp, mode, spp, W, H, rp, nrows,
                                rgba8.ctypes.data_as(_P), rgba32.ctypes.data_as(_P) if want_float else None,
                                nthreads, stats.ctypes.data_as(_P), 1 if brute_force else 0, schedule)
         if st:
@@ -260,7 +280,7 @@ class Scene:
         uv = np.zeros((n, 2), np.float32)
         stats = np.zeros(12, np.uint64)
         flags = (0x04 if any_hit else 0) | (0x10 if cull_back else 0) | (0x20 if cull_front else 0)  # D3D12_RAY_FLAG
-        if lib.oracle_trace_rays(self._h, r.ctypes.data_as(_P), n, flags, hits.ctypes.data_as(_P),
+        if self._lib.oracle_trace_rays(self._h, r.ctypes.data_as(_P), n, flags, hits.ctypes.data_as(_P),
                               uv.ctypes.data_as(_P), 1 if brute_force else 0, stats.ctypes.data_as(_P)):
             raise RuntimeError("oracle_trace_rays failed")
         return hits, uv, stats

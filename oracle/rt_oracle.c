@@ -776,18 +776,37 @@ int oracle_export_tlas(const oracle_scene* s, void* nodes) {
 /* v[0..8] = RT_STAT_* 0..8; v[9..11] record fetches (RT_STAT_NODE/TRI/INSTANCE_FETCHES): per ray in
  * otrace, once per emulated wave in opacket */
 typedef struct { uint64_t v[12]; } ostats;
+/* Counters: the checker build counts every test and fetch (compared with the device's). The CPU
+ * baseline build (-DORACLE_NO_COUNTERS -O3, oracle/libbaseline.so: BASELINE.md section 3's scalar
+ * traversal without counters) compiles them out; its frames are identical. */
+#ifdef ORACLE_NO_COUNTERS
+#define OST(i, n) ((void)0)
+#else
+#define OST(i, n) (st->v[i] += (n))
+#endif
 typedef struct { float t, u, v; uint32_t inst, prim; } ohit;
 
 static inline float sinv(float d) { return fabsf(d) > 1e-20f ? 1.0f / d : (d < 0.0f ? -1e20f : 1e20f); }
 
 /* slab tests of the 4 children of a node against [tmin, tbest]; +inf = missed or empty */
+/* The slab operands are never NaN (finite origins, safe_inv never 0 or inf, +-inf planes of empty slots
+ * times a finite inverse), and the sign of a zero min/max never changes a comparison or a key (keys drop the
+ * sign bit), so the CPU baseline build may use plain compares (minss / maxss) instead of the libm calls
+ * gcc emits for fminf / fmaxf without -ffast-math. Same frames (tests/test_oracle.py). */
+#ifdef ORACLE_NO_COUNTERS
+#define OMINF(a, b) ((a) < (b) ? (a) : (b))
+#define OMAXF(a, b) ((a) > (b) ? (a) : (b))
+#else
+#define OMINF(a, b) fminf(a, b)
+#define OMAXF(a, b) fmaxf(a, b)
+#endif
 static inline void oslab4(const o4node* nd, vec3 invd, vec3 noinv, float tmin, float tbest, float tn[4]) {
   for (int k = 0; k < 4; ++k) {
     float tlx = fmaf(nd->lox[k], invd.x, noinv.x), thx = fmaf(nd->hix[k], invd.x, noinv.x);
     float tly = fmaf(nd->loy[k], invd.y, noinv.y), thy = fmaf(nd->hiy[k], invd.y, noinv.y);
     float tlz = fmaf(nd->loz[k], invd.z, noinv.z), thz = fmaf(nd->hiz[k], invd.z, noinv.z);
-    float n = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), tmin));
-    float f = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tbest));
+    float n = OMAXF(OMAXF(OMINF(tlx, thx), OMINF(tly, thy)), OMAXF(OMINF(tlz, thz), tmin));
+    float f = OMINF(OMINF(OMAXF(tlx, thx), OMAXF(tly, thy)), OMINF(OMAXF(tlz, thz), tbest));
     tn[k] = (nd->child[k] != O_EMPTY && n <= f * 1.0000004f) ? n : INFINITY;
   }
 }
@@ -825,7 +844,22 @@ static inline int better(float t, uint32_t inst, uint32_t prim, const ohit* h) {
 
 #define SENT INT32_MIN
 
-#define OPUSH(X) do { if (sp < cap) stack[sp++] = (X); else st->v[5]++; } while (0)
+/* deepest per-ray stack reached by otrace since the last reset (diagnostics for tests: a scene meant to
+ * exercise the device's HBM overflow stack must really reach past its 32 LDS entries; racy across
+ * render threads, read it after single-threaded renders) */
+static int g_max_sp = 0;
+#ifndef ORACLE_FLAGS
+#define ORACLE_FLAGS "unknown"
+#endif
+/* compiler and flags of this build (bench.py's cpu_baseline reports them) */
+const char* oracle_build_info(void) { return "gcc " __VERSION__ " " ORACLE_FLAGS; }
+int oracle_max_stack_reached(int reset) { int m = g_max_sp; if (reset) g_max_sp = 0; return m; }
+#ifdef ORACLE_NO_COUNTERS
+#define OSP_TRACK() ((void)0)
+#else
+#define OSP_TRACK() do { if (sp > g_max_sp) g_max_sp = sp; } while (0)
+#endif
+#define OPUSH(X) do { if (sp < cap) { stack[sp++] = (X); OSP_TRACK(); } else OST(5, 1); } while (0)
 
 static int otrace(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax, int any, int cull, ohit* h,
                   ostats* st) {
@@ -848,8 +882,8 @@ static int otrace(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax,
       float tn[4];
       int32_t r[4] = {nd->child[0], nd->child[1], nd->child[2], nd->child[3]};
       oslab4(nd, rinvd, rno, tmin, h->t, tn);
-      st->v[9]++;
-      for (int k = 0; k < 4; ++k) st->v[2] += r[k] != O_EMPTY;
+      OST(9, 1);
+      for (int k = 0; k < 4; ++k) OST(2, r[k] != O_EMPTY);
       osort4(tn, r);
       if (tn[0] != INFINITY) {
         if (tn[3] != INFINITY) OPUSH(r[3]);
@@ -861,10 +895,11 @@ static int otrace(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax,
     } else if (!in_blas) {
       cur = (uint32_t)(~ref);
       const oinst* ir = &s->inst[cur];
-      st->v[4]++;
-      st->v[11]++;
+      OST(4, 1);
+      OST(11, 1);
       if (sp < cap) {
         stack[sp++] = SENT;
+        OSP_TRACK();
         ro = ipoint(ir, o);
         rd = idir(ir, d);
         rinvd = mk(sinv(rd.x), sinv(rd.y), sinv(rd.z));
@@ -875,12 +910,12 @@ static int otrace(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax,
         ref = 0;
         continue;
       }
-      st->v[5]++;
+      OST(5, 1);
     } else {
       const otri* tr = tris + (~ref);
       float t, u, v;
-      st->v[3]++;
-      st->v[10]++;
+      OST(3, 1);
+      OST(10, 1);
       if (omt(ro, rd, tr, cull ? (float)cull * s->inst[cur].face : 0.0f, &t, &u, &v) && t >= tmin && better(t, cur, tr->prim, h)) {
         h->t = t; h->u = u; h->v = v; h->inst = cur; h->prim = tr->prim;
         found = 1;
@@ -923,7 +958,7 @@ static int opk_node(const o4node* nd, const opkray* ry, float tmin, ohit* h, int
                     int cap, int* next, ostats* st) {
   uint64_t hm[4] = {0, 0, 0, 0};
   uint32_t vkey[OPK][4];
-  st->v[9]++; /* one node fetch per wave */
+  OST(9, 1); /* one node fetch per wave */
   for (int l = 0; l < OPK; ++l) {
     for (int k = 0; k < 4; ++k) {
       float tlx = fmaf(nd->lox[k], ry->invd[l].x, ry->no[l].x), thx = fmaf(nd->hix[k], ry->invd[l].x, ry->no[l].x);
@@ -939,7 +974,7 @@ static int opk_node(const o4node* nd, const opkray* ry, float tmin, ohit* h, int
       vkey[l][k] = hit ? (f2bits(n) & 0x7fffffffu) : 0x7f800000u;
 #endif
     }
-    if (live[l]) st->v[2] += nd->count;
+    if (live[l]) OST(2, nd->count);
   }
   uint32_t ent = 0;
   for (int k = 0; k < 4; ++k) if (hm[k]) ent |= 1u << k;
@@ -952,11 +987,11 @@ static int opk_node(const o4node* nd, const opkray* ry, float tmin, ohit* h, int
     for (int k = 0; k < 4; ++k) {
       if (!((tl >> k) & 1u)) continue;
       const otri* tr = leaves + (~nd->child[k]);
-      st->v[10]++; /* one triangle fetch per wave */
+      OST(10, 1); /* one triangle fetch per wave */
       for (int l = 0; l < OPK; ++l) {
         if (!live[l]) continue;
         float t, u, v;
-        st->v[3]++;
+        OST(3, 1);
         if (omt(ry->o[l], ry->d[l], tr, face, &t, &u, &v) && t >= tmin && better(t, cur, tr->prim, &h[l])) {
           h[l].t = t; h[l].u = u; h[l].v = v; h[l].inst = cur; h[l].prim = tr->prim;
           found[l] = 1;
@@ -992,7 +1027,7 @@ static int opk_node(const o4node* nd, const opkray* ry, float tmin, ohit* h, int
   }
   const uint32_t P = ent & ~(1u << ib);
   if (*sp + __builtin_popcount(P) > cap) /* never: cap is the exact worst case; counted per live lane */
-    for (int l = 0; l < OPK; ++l) st->v[5] += live[l] ? 1u : 0u;
+    for (int l = 0; l < OPK; ++l) OST(5, live[l] ? 1u : 0u);
   for (int k = 3; k >= 0; --k) {
     if (!((P >> k) & 1u)) continue;
     if (*sp < OSTACK) stack[*sp] = nd->child[k];
@@ -1037,9 +1072,9 @@ static void opacket(const oracle_scene* s, const vec3* o, const vec3* d, float t
       const uint32_t cur = (uint32_t)(~ref);
       const oinst* ir = &s->inst[cur];
       const oblas* bl = &s->blas[ir->blas];
-      st->v[11]++; /* one instance-record fetch per wave */
+      OST(11, 1); /* one instance-record fetch per wave */
       for (int l = 0; l < OPK; ++l) {
-        if (live[l]) st->v[4]++;
+        if (live[l]) OST(4, 1);
         b.o[l] = ipoint(ir, o[l]);
         b.d[l] = idir(ir, d[l]);
         b.invd[l] = mk(sinv(b.d[l].x), sinv(b.d[l].y), sinv(b.d[l].z));
@@ -1074,7 +1109,7 @@ static int obrute(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax,
     for (uint32_t k = 0; k < b->ntri; ++k) {
       const otri* tr = &b->tris[k];
       float t, u, v;
-      st->v[3]++;
+      OST(3, 1);
       if (omt(ro, rd, tr, cull ? (float)cull * ir->face : 0.0f, &t, &u, &v) && t >= tmin && better(t, i, tr->prim, h)) {
         h->t = t; h->u = u; h->v = v; h->inst = i; h->prim = tr->prim;
         found = 1;
@@ -1245,7 +1280,7 @@ typedef struct {
 
 static int trace_any(const octx* c, vec3 P, vec3 dir, ostats* st) {
   ohit h;
-  st->v[1]++;
+  OST(1, 1);
   vec3 d = vnorm(dir); /* CastShadowRay normalises (Common.hlsl:73) */
   return c->brute ? obrute(c->s, P, d, 0.01f, 100000.0f, 1, 0, &h, st)
                   : otrace(c->s, P, d, 0.01f, 100000.0f, 1, 0, &h, st);
@@ -1313,7 +1348,7 @@ static vec3 oshade_ref(const octx* c, uint32_t py, vec3 O, vec3 D, int f, ohit h
           vec3 dir = vnorm(vnorm(vreflect(vnorm(rd), n)));
           ro = vadd(P, vscale(dir, 0.001f));
           rd = dir;
-          st->v[8]++;
+          OST(8, 1);
           f = c->brute ? obrute(c->s, ro, rd, 0.001f, 1000.0f, 0, 1, &h, st)
                        : otrace(c->s, ro, rd, 0.001f, 1000.0f, 0, 1, &h, st);
           continue;
@@ -1349,7 +1384,7 @@ static vec3 osample(const octx* c, uint32_t px, uint32_t py, float ox, float oy,
   vec3 O, D;
   oraygen(c, px, py, ox, oy, &O, &D);
   ohit h;
-  st->v[0]++;
+  OST(0, 1);
   int f = c->brute ? obrute(c->s, O, D, 0.0f, 100000.0f, 0, 0, &h, st)
                    : otrace(c->s, O, D, 0.0f, 100000.0f, 0, 0, &h, st);
   if (c->mode == 0) return oshade_ref(c, py, O, D, f, h, st);
@@ -1387,7 +1422,7 @@ static void osample_packet(const octx* c, const uint32_t* px, const uint32_t* py
   int found[OPK], occl[OPK], need[OPK];
   for (int l = 0; l < OPK; ++l) {
     oraygen(c, px[l], py[l], ox[l], oy[l], &O[l], &D[l]);
-    if (inimg[l]) st->v[0]++;
+    if (inimg[l]) OST(0, 1);
   }
   opacket(c->s, O, D, 0.0f, 100000.0f, 0, 0, inimg, h, found, st);
   for (int l = 0; l < OPK; ++l) {
@@ -1422,7 +1457,7 @@ static void osample_packet(const octx* c, const uint32_t* px, const uint32_t* py
             nf[l] = o_face_normal(c->s, h[l].inst, h[l].prim);
             need[l] = 1;
             sd[l] = vnorm(ldir[l]);
-            st->v[1]++;
+            OST(1, 1);
             continue;
           }
           vec3 n = o_interp_normal(c->s, h[l].inst, h[l].prim, h[l].u, h[l].v);
@@ -1434,7 +1469,7 @@ static void osample_packet(const octx* c, const uint32_t* px, const uint32_t* py
             rd[l] = dir;
             nxt[l] = 1;
             any_next = 1;
-            st->v[8]++;
+            OST(8, 1);
             continue;
           }
           term = s;
@@ -1475,7 +1510,7 @@ static void osample_packet(const octx* c, const uint32_t* px, const uint32_t* py
       need[l] = found[l] && nl[l] > 0.0f;
       occl[l] = 0;
       sd[l] = need[l] ? vnorm(Ld[l]) : mk(0, 0, 1);
-      if (c->mode == 1 && need[l]) st->v[1]++;
+      if (c->mode == 1 && need[l]) OST(1, 1);
     }
     if (c->mode == 1) opacket(c->s, P, sd, 0.01f, 100000.0f, 1, 0, need, hs, occl, st);
     for (int l = 0; l < OPK; ++l)

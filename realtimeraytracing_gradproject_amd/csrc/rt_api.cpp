@@ -35,6 +35,102 @@ struct DeviceBlas {
   }
 };
 
+// Device scratch that launches on different streams may need at the same time (the HBM
+// overflow stack of the per-lane traversal, the row list of a strip dispatch). The calls are
+// stream-ordered and asynchronous (rt_api.h), so one buffer per context would be written by two
+// frames in flight at once. Each buffer is a slot of a small ring; a slot remembers, per stream,
+// an event recorded after that stream's last launch that used it. A launch on stream s:
+//   - takes a slot no other stream is still using (its events have completed), or that only s
+//     used (stream order protects it), else a new slot (up to kMaxSlots);
+//   - with every slot busy, reuses the least recently used one after making s WAIT (on the
+//     device, hipStreamWaitEvent) for the other streams' last uses of it.
+// The host never waits except to grow a slot (rare: its old buffer is freed).
+struct StreamUse {
+  hipStream_t stream;
+  hipEvent_t ev;
+};
+
+struct ScratchSlot {
+  void* buf = nullptr;
+  size_t cap = 0;               // bytes
+  uint64_t tick = 0;            // last acquisition (LRU)
+  std::vector<StreamUse> uses;  // one entry per stream that used the slot
+  // row-list slots: the list held (content key), its pinned upload staging and the upload's event
+  std::vector<uint32_t> key;
+  uint32_t* staging = nullptr;
+  size_t staging_cap = 0;
+  hipEvent_t upload_ev = nullptr;
+  hipStream_t upload_stream = nullptr;
+  bool uploaded = false;  // an upload may still be pending (upload_ev not yet seen complete)
+};
+
+struct ScratchRing {
+  static constexpr size_t kMaxSlots = 8;
+  std::vector<ScratchSlot> slots;
+  uint64_t clock = 0;
+};
+
+hipEvent_t new_sync_event() {
+  hipEvent_t e = nullptr;
+  // no timestamp, no system-scope release: the consumers are device-side waits and host queries of completion
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) return nullptr;
+  return e;
+}
+
+// true when no stream other than s may still be using the slot
+bool slot_free_for(const ScratchSlot& sl, hipStream_t s) {
+  for (const StreamUse& u : sl.uses)
+    if (u.stream != s && hipEventQuery(u.ev) != hipSuccess) return false;
+  return true;
+}
+
+// stream s waits (on the device) for every other stream's last use of the slot
+hipError_t slot_order_after_others(const ScratchSlot& sl, hipStream_t s) {
+  for (const StreamUse& u : sl.uses)
+    if (u.stream != s) {
+      hipError_t e = hipStreamWaitEvent(s, u.ev, 0);
+      if (e != hipSuccess) return e;
+    }
+  return hipSuccess;
+}
+
+// the host waits for every use of the slot (before its buffer is freed)
+hipError_t slot_drain(const ScratchSlot& sl) {
+  for (const StreamUse& u : sl.uses) {
+    hipError_t e = hipEventSynchronize(u.ev);
+    if (e != hipSuccess) return e;
+  }
+  if (sl.upload_ev && sl.uploaded) return hipEventSynchronize(sl.upload_ev);
+  return hipSuccess;
+}
+
+// records that a launch just enqueued on s used the slot
+hipError_t slot_mark_use(ScratchSlot& sl, hipStream_t s) {
+  for (StreamUse& u : sl.uses)
+    if (u.stream == s) return hipEventRecord(u.ev, s);
+  // forget streams whose last use completed long ago (streams come and go: torch, callers)
+  if (sl.uses.size() >= 8) {
+    std::vector<StreamUse> keep;
+    for (const StreamUse& u : sl.uses) {
+      if (hipEventQuery(u.ev) == hipSuccess) (void)hipEventDestroy(u.ev);
+      else keep.push_back(u);
+    }
+    sl.uses.swap(keep);
+  }
+  hipEvent_t ev = new_sync_event();
+  if (!ev) return hipErrorOutOfMemory;
+  sl.uses.push_back({s, ev});
+  return hipEventRecord(ev, s);
+}
+
+void slot_release(ScratchSlot& sl) {
+  if (sl.buf) (void)hipFree(sl.buf);
+  if (sl.staging) (void)hipHostFree(sl.staging);
+  for (const StreamUse& u : sl.uses) (void)hipEventDestroy(u.ev);
+  if (sl.upload_ev) (void)hipEventDestroy(sl.upload_ev);
+  sl = ScratchSlot();
+}
+
 }  // namespace
 
 struct rt_ctx {
@@ -58,13 +154,11 @@ struct rt_ctx {
   bool stats_on = false;
   unsigned long long* d_stats = nullptr;
   uint64_t dispatches = 0, pixels = 0;
-  // cached row list
-  uint32_t* d_rows = nullptr;
-  size_t rows_cap = 0;
-  std::vector<uint32_t> rows_host;
-  // traversal-stack overflow area in HBM for lanes whose path outgrows the LDS part
-  int* d_ovf = nullptr;
-  size_t ovf_cap = 0;
+  // row lists of strip dispatches (one slot per distinct list in use, keyed by content)
+  ScratchRing rows;
+  // traversal-stack overflow areas in HBM for lanes whose path outgrows the LDS part: one slot per
+  // launch that may run concurrently with another (frames in flight, rt_trace_rays batches)
+  ScratchRing ovf;
   // scene pools read by the trace kernels (rebuilt by every rt_tlas_build)
   rt::Bvh4Node* pool_nodes = nullptr;
   rt::TriRec* pool_tris = nullptr;
@@ -75,6 +169,11 @@ struct rt_ctx {
   size_t raster_tile_cap = 0, raster_prim_cap = 0, raster_bin_cap = 0;
   uint32_t* raster_total_host = nullptr;  // pinned: the last draw's bin-entry total, copied back async
   rt::RasterDraws raster_draws_host;      // what raster.draws holds on the device (valid when n > 0)
+  // every draw uses the one raster scratch: a draw on another stream waits (on the device) for the
+  // previous draw, recorded here
+  hipEvent_t raster_ev = nullptr;
+  hipStream_t raster_stream = nullptr;
+  bool raster_pending = false;
 };
 
 namespace {
@@ -280,14 +379,15 @@ rt_status rt_create(int hip_device, rt_ctx_t* out) {
 rt_status rt_destroy(rt_ctx_t c) {
   if (!c) return RT_E_INVALID;
   (void)hipSetDevice(c->device);
-  (void)hipStreamSynchronize(c->stream);
+  (void)quiesce(c);  // launches on caller streams may still read the context's buffers
   for (auto& b : c->blas) b.release();
   if (c->tlas_nodes) (void)hipFree(c->tlas_nodes);
   if (c->inst) (void)hipFree(c->inst);
   if (c->tlas_sorted) (void)hipFree(c->tlas_sorted);
   if (c->d_stats) (void)hipFree(c->d_stats);
-  if (c->d_rows) (void)hipFree(c->d_rows);
-  if (c->d_ovf) (void)hipFree(c->d_ovf);
+  for (auto& sl : c->rows.slots) slot_release(sl);
+  for (auto& sl : c->ovf.slots) slot_release(sl);
+  if (c->raster_ev) (void)hipEventDestroy(c->raster_ev);
   if (c->pool_nodes) (void)hipFree(c->pool_nodes);
   if (c->pool_tris) (void)hipFree(c->pool_tris);
   for (void* p : {(void*)c->raster.clip, (void*)c->raster.slots, (void*)c->raster.tiles, (void*)c->raster.tcount,
@@ -571,20 +671,101 @@ static rt::SceneView scene_view(rt_ctx* c) {
   return sv;
 }
 
-// Sizes the HBM overflow stack for `lanes` lanes when the trees are deeper than the LDS part.
-static rt_status ensure_overflow(rt_ctx* c, rt::SceneView& sv, size_t lanes, hipStream_t s) {
-  if (sv.stack_cap <= sv.lds_cap) return RT_OK;
-  const size_t need = lanes * (size_t)(sv.stack_cap - sv.lds_cap);
-  if (need > c->ovf_cap) {
-    HIPCHK(c, quiesce(c), "overflow stack: wait for in-flight work");
-    if (c->d_ovf) (void)hipFree(c->d_ovf);
-    c->d_ovf = nullptr;
-    c->ovf_cap = 0;
-    HIPCHK(c, hipMalloc(&c->d_ovf, need * sizeof(int)), "hipMalloc(stack overflow area)");
-    c->ovf_cap = need;
+// Picks the ring slot a launch on s uses (see ScratchRing). `match` (row lists): a slot holding
+// the same content is shared as is — launches only read it.
+static ScratchSlot* ring_acquire(ScratchRing& ring, hipStream_t s, const std::vector<uint32_t>* match, bool* hit,
+                                 hipError_t* err) {
+  *hit = false;
+  *err = hipSuccess;
+  ScratchSlot* pick = nullptr;
+  if (match) {
+    for (ScratchSlot& sl : ring.slots)
+      if (sl.key == *match) {
+        *hit = true;
+        sl.tick = ++ring.clock;
+        return &sl;
+      }
   }
-  sv.ovf = c->d_ovf;
+  for (ScratchSlot& sl : ring.slots)  // idle for s: only s used it, or every other use completed
+    if (slot_free_for(sl, s) && (!pick || sl.tick < pick->tick)) pick = &sl;
+  if (!pick && ring.slots.size() < ScratchRing::kMaxSlots) {
+    ring.slots.emplace_back();
+    pick = &ring.slots.back();
+  }
+  if (!pick) {  // every slot busy on other streams: the least recently used one, ordered on the device
+    for (ScratchSlot& sl : ring.slots)
+      if (!pick || sl.tick < pick->tick) pick = &sl;
+    *err = slot_order_after_others(*pick, s);
+  }
+  pick->tick = ++ring.clock;
+  return pick;
+}
+
+// grows a slot's device buffer (the host waits for the slot's own uses, not the whole device)
+static hipError_t slot_reserve(ScratchSlot& sl, size_t bytes) {
+  if (sl.cap >= bytes) return hipSuccess;
+  hipError_t e = slot_drain(sl);
+  if (e != hipSuccess) return e;
+  if (sl.buf) (void)hipFree(sl.buf);
+  sl.buf = nullptr;
+  sl.cap = 0;
+  e = hipMalloc(&sl.buf, bytes);
+  if (e == hipSuccess) sl.cap = bytes;
+  return e;
+}
+
+// The HBM overflow stack for `lanes` lanes when the trees are deeper than the LDS part: a slot of
+// its own per concurrent launch. Returns the slot to mark after the launch (nullptr: none needed).
+static rt_status ensure_overflow(rt_ctx* c, rt::SceneView& sv, size_t lanes, hipStream_t s, ScratchSlot** used) {
+  *used = nullptr;
+  if (sv.stack_cap <= sv.lds_cap) return RT_OK;
+  const size_t need = lanes * (size_t)(sv.stack_cap - sv.lds_cap) * sizeof(int);
+  bool hit;
+  hipError_t e;
+  ScratchSlot* sl = ring_acquire(c->ovf, s, nullptr, &hit, &e);
+  if (e != hipSuccess) return hip_fail(c, e, "overflow stack: order after in-flight launches");
+  HIPCHK(c, slot_reserve(*sl, need), "hipMalloc(stack overflow area)");
+  sv.ovf = (int*)sl->buf;
   sv.ovf_lanes = (uint32_t)lanes;
+  *used = sl;
+  return RT_OK;
+}
+
+// Device copy of a strip dispatch's row list, shared by every launch that renders the same rows.
+static rt_status ensure_rows(rt_ctx* c, const uint32_t* rows, uint32_t nrows, hipStream_t s, ScratchSlot** used,
+                             const uint32_t** d_rows) {
+  std::vector<uint32_t> key(rows, rows + nrows);
+  bool hit;
+  hipError_t e;
+  ScratchSlot* sl = ring_acquire(c->rows, s, &key, &hit, &e);
+  if (e != hipSuccess) return hip_fail(c, e, "rows: order after in-flight launches");
+  if (!hit) {
+    const size_t bytes = (size_t)nrows * 4;
+    HIPCHK(c, slot_reserve(*sl, bytes), "hipMalloc(rows)");
+    // this slot held another list: every launch that read it (any stream) precedes the upload
+    HIPCHK(c, slot_order_after_others(*sl, s), "rows: order after in-flight launches");
+    if (sl->upload_ev && sl->uploaded) HIPCHK(c, hipEventSynchronize(sl->upload_ev), "rows staging");
+    if (sl->staging_cap < bytes) {
+      if (sl->staging) (void)hipHostFree(sl->staging);
+      sl->staging = nullptr;
+      sl->staging_cap = 0;
+      HIPCHK(c, hipHostMalloc((void**)&sl->staging, bytes, hipHostMallocDefault), "hipHostMalloc(rows staging)");
+      sl->staging_cap = bytes;
+    }
+    if (!sl->upload_ev && !(sl->upload_ev = new_sync_event())) return fail(c, RT_E_HIP, "rows: event");
+    std::memcpy(sl->staging, rows, bytes);
+    sl->key.swap(key);
+    HIPCHK(c, hipMemcpyAsync(sl->buf, sl->staging, bytes, hipMemcpyHostToDevice, s), "upload rows");
+    HIPCHK(c, hipEventRecord(sl->upload_ev, s), "upload rows");
+    sl->uploaded = true;
+    sl->upload_stream = s;
+  } else if (sl->uploaded && sl->upload_stream != s) {
+    // the same list, uploaded on another stream: this launch must not read it before the copy lands
+    if (hipEventQuery(sl->upload_ev) == hipSuccess) sl->uploaded = false;  // landed: no wait from now on
+    else HIPCHK(c, hipStreamWaitEvent(s, sl->upload_ev, 0), "rows: order after upload");
+  }
+  *used = sl;
+  *d_rows = (const uint32_t*)sl->buf;
   return RT_OK;
 }
 
@@ -669,6 +850,11 @@ rt_status rt_raster_draw(rt_ctx_t c, const rt_blas_t* draws, uint32_t ndraws, co
   // entries than that capacity still renders the same image (k_raster_tile walks every slot) and
   // the next draw grows the bins.
   const uint32_t last_total = *(volatile uint32_t*)c->raster_total_host;
+  // one raster scratch per context: a draw on another stream than the previous draw's runs after it
+  if (c->raster_pending && c->raster_stream != s) {
+    if (hipEventQuery(c->raster_ev) == hipSuccess) c->raster_pending = false;
+    else HIPCHK(c, hipStreamWaitEvent(s, c->raster_ev, 0), "rt_raster_draw: order after the previous draw");
+  }
   hipError_t e = rt::launch_raster_bin(dr, rv, c->raster, s);
   if (e != hipSuccess) return hip_fail(c, e, "raster bin launch");
   size_t want = 0;
@@ -696,6 +882,10 @@ rt_status rt_raster_draw(rt_ctx_t c, const rt_blas_t* draws, uint32_t ndraws, co
   if (e != hipSuccess) return hip_fail(c, e, "raster launch");
   HIPCHK(c, hipMemcpyAsync(c->raster_total_host, c->raster.toffs + ntiles, 4, hipMemcpyDeviceToHost, s),
          "raster bin total");
+  if (!c->raster_ev && !(c->raster_ev = new_sync_event())) return fail(c, RT_E_HIP, "rt_raster_draw: event");
+  HIPCHK(c, hipEventRecord(c->raster_ev, s), "rt_raster_draw: record");
+  c->raster_stream = s;
+  c->raster_pending = true;
   return RT_OK;
 }
 
@@ -712,25 +902,9 @@ rt_status rt_dispatch_rays(rt_ctx_t c, uint32_t W, uint32_t H, const uint32_t* r
   (void)hipSetDevice(c->device);
   hipStream_t s = pick_stream(c, stream);
   const uint32_t* d_rows = nullptr;
-  if (rows) {
+  if (rows)
     for (uint32_t r = 0; r < nrows; ++r)
       if (rows[r] >= H) return fail(c, RT_E_INVALID, "rt_dispatch_rays: row index out of range");
-    bool same = c->rows_host.size() == nrows && std::memcmp(c->rows_host.data(), rows, (size_t)nrows * 4) == 0;
-    if (!same) {
-      // the cached list may still be read by a frame in flight on another stream
-      HIPCHK(c, quiesce(c), "rt_dispatch_rays: wait for in-flight work");
-      if (c->rows_cap < nrows) {
-        if (c->d_rows) (void)hipFree(c->d_rows);
-        c->d_rows = nullptr;
-        HIPCHK(c, hipMalloc(&c->d_rows, (size_t)nrows * 4), "hipMalloc(rows)");
-        c->rows_cap = nrows;
-      }
-      HIPCHK(c, hipMemcpyAsync(c->d_rows, rows, (size_t)nrows * 4, hipMemcpyHostToDevice, s), "upload rows");
-      HIPCHK(c, hipStreamSynchronize(s), "upload rows");
-      c->rows_host.assign(rows, rows + nrows);
-    }
-    d_rows = c->d_rows;
-  }
   c->fp.width = W;
   c->fp.height = H;
   c->fp.fwidth = (float)W;  // exact: W, H < 2^24
@@ -740,14 +914,19 @@ rt_status rt_dispatch_rays(rt_ctx_t c, uint32_t W, uint32_t H, const uint32_t* r
   rt::SceneView sv = scene_view(c);
   if (sv.stack_cap > rt::kMaxTraversalStack)
     return fail(c, RT_E_UNSUPPORTED, "rt_dispatch_rays: BVH too deep for the traversal stack");
+  ScratchSlot* ovf_slot = nullptr;
+  ScratchSlot* rows_slot = nullptr;
   {
     const size_t lanes = (size_t)((W + 15) / 16) * ((nrows + 15) / 16) * 256;
-    rt_status st = ensure_overflow(c, sv, lanes, s);
+    rt_status st = ensure_overflow(c, sv, lanes, s, &ovf_slot);
+    if (st == RT_OK && rows) st = ensure_rows(c, rows, nrows, s, &rows_slot, &d_rows);
     if (st != RT_OK) return st;
   }
   hipError_t e = rt::launch_trace_frame(sv, c->fp, d_rows, rgba8, rgba32f, c->d_stats, c->stats_on,
                                         c->schedule, s);
   if (e != hipSuccess) return hip_fail(c, e, "trace launch");
+  if (ovf_slot) HIPCHK(c, slot_mark_use(*ovf_slot, s), "overflow stack: record use");
+  if (rows_slot) HIPCHK(c, slot_mark_use(*rows_slot, s), "rows: record use");
   if (c->stats_on) {
     c->dispatches += 1;
     c->pixels += (uint64_t)W * nrows;
@@ -772,14 +951,17 @@ rt_status rt_trace_rays(rt_ctx_t c, const float* rays, uint32_t n, uint32_t ray_
   sv.cull_sense = cull_front ? -1.0f : 1.0f;
   if (sv.stack_cap > rt::kMaxTraversalStack)
     return fail(c, RT_E_UNSUPPORTED, "rt_trace_rays: BVH too deep for the traversal stack");
+  if (n == 0) return RT_OK;
+  hipStream_t s = pick_stream(c, stream);
+  ScratchSlot* ovf_slot = nullptr;
   {
-    rt_status st = ensure_overflow(c, sv, (size_t)((n + 255) / 256) * 256, pick_stream(c, stream));
+    rt_status st = ensure_overflow(c, sv, (size_t)((n + 255) / 256) * 256, s, &ovf_slot);
     if (st != RT_OK) return st;
   }
   hipError_t e = rt::launch_trace_rays(sv, rays, n, (ray_flags & RT_RAY_FLAG_ACCEPT_FIRST_HIT_AND_END_SEARCH) != 0,
-                                       cull_back || cull_front, hits, uv, c->d_stats,
-                                       c->stats_on, pick_stream(c, stream));
+                                       cull_back || cull_front, hits, uv, c->d_stats, c->stats_on, s);
   if (e != hipSuccess) return hip_fail(c, e, "trace_rays launch");
+  if (ovf_slot) HIPCHK(c, slot_mark_use(*ovf_slot, s), "overflow stack: record use");
   return RT_OK;
 }
 

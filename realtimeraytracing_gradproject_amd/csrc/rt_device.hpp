@@ -342,9 +342,6 @@ RT_HD bool moller_trumbore(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, float& t
 #endif
 }
 
-// Moller-Trumbore without early exits: every lane runs the same instructions (the wave-packet
-// path, where a divergent early exit costs exec-mask SALU work on the busiest pipe). Accepts
-// exactly what moller_trumbore accepts, with the same u, v, t.
 // Bitwise acceptance (no short-circuit, so no exec-mask branch around the u / v / t products):
 // the same predicate, every term evaluated.
 RT_HD bool moller_trumbore_bits(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, float& t, float& u, float& v) {
@@ -359,6 +356,9 @@ RT_HD bool moller_trumbore_bits(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, flo
   return (det != 0.0f) & !(det * face < 0.0f) & (u >= 0.0f) & (u <= 1.0f) & (v >= 0.0f) & (u + v <= 1.0f);
 }
 
+// Moller-Trumbore without early exits: every lane runs the same instructions (the wave-packet
+// path, where a divergent early exit costs exec-mask SALU work on the busiest pipe). Accepts
+// exactly what moller_trumbore accepts, with the same u, v, t.
 RT_HD bool moller_trumbore_flat(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, float& t, float& u, float& v) {
   const V3 p = cross(d, e2);
   const float det = dot(e1, p);

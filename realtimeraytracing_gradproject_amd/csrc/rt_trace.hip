@@ -609,7 +609,8 @@ __device__ __forceinline__ bool packet_tlas_node(const RT_CONST char* pool, int 
 // stack entry (first_inner << 8 | inner_mask << 4 | pending slots) that pops its slots lowest
 // first — exactly the order in which per-child pushes in descending slot order would pop them, so
 // the walk (and every counter) is that of the per-child stack with a fraction of the scalar
-// bookkeeping. Internal child k's ref is first_inner + popcount(inner_mask below k).
+// bookkeeping. BLAS nodes hold their internal children in the lowest slots, so the internal child in
+// slot k is first_inner + k.
 template <bool ANY_HIT, bool STATS, int R, bool OCT>
 __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, const RT_CONST TriRec* tpool, int bref,
                                                  const PacketRay<R>& ry, float tmin, uint32_t cur, float face,
@@ -710,9 +711,9 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
         nref = (uint32_t)ch[5] + ib;  // internal children in the lowest slots
       } else {
         // per lane: the slot of its smallest key over the entered internal children (all-ones
-        // keys elsewhere), lowest slot on ties, and that child's ref (first_inner + internal
-        // children below it: v_bfm / v_and / v_bcnt in VALU), packed as ref << 2 | slot; the lead
-        // lane's answer, one readlane, is the packet's
+        // keys elsewhere), lowest slot on ties, and that child's ref (first_inner + slot: internal
+        // children sit in the lowest slots), packed as ref << 2 | slot; the lead lane's answer, one
+        // readlane, is the packet's
         uint32_t idx = 0;
 #pragma unroll
         for (int r = 0; r < R; ++r) {

@@ -152,6 +152,8 @@ def config(name: str) -> SceneSpec:
         return s
     if name == "DEGEN":
         return degenerate_scene()
+    if name == "DEEP":
+        return deep_scene()
     raise KeyError(name)
 
 
@@ -224,6 +226,41 @@ def degenerate_scene() -> SceneSpec:
     ]
     return SceneSpec("DEGEN", meshes, inst, REFERENCE_LIGHTS[:2], REFERENCE_MATERIAL,
                      ((14.0, 9.0, 16.0), (0.0, 1.0, 1.0), (0.0, 1.0, 0.0)), 320, 180, RT_SHADE_LAMBERT_SHADOW)
+
+
+def deep_chain_mesh(reps: int = 8, half: float = 60.0, seed: int = 5) -> np.ndarray:
+    """A BLAS whose 4-wide tree is deeper than the trace kernels' 32-entry LDS stack, with paths that
+    really use that depth: triangle box centres on a Morton chain (one axis coordinate 2^j / 1024 of
+    the centre bounds, j = 9..0, per axis: the binary LBVH is a 30-level chain) and every triangle
+    large (2 x `half` across, facing +z), so a ray crossing the scene enters nearly every box of a
+    node and the per-lane walk pushes its siblings level after level. Test scene, not a config."""
+    rng = np.random.default_rng(seed)
+    cents = [np.full(3, 0.5), np.full(3, 1023.5)]  # the anchors fix the centre bounds
+    for j in range(9, -1, -1):
+        for ax in range(3):
+            c = np.full(3, 0.5)
+            c[ax] = 2 ** j + 0.5
+            cents.append(c)
+    tris = []
+    for c in cents:
+        for _ in range(reps):
+            p = c / 1024.0 * 40.0 + rng.normal(scale=0.05, size=3)
+            tris.append([p + (-half, -half, 0.0), p + (half, -half, 0.0), p + (0.0, half, 0.0)])
+    out = np.zeros((len(tris) * 3, 6), np.float32)
+    out[:, :3] = np.asarray(tris).reshape(-1, 3)
+    out[:, 4] = 1.0
+    return out
+
+
+def deep_scene() -> SceneSpec:
+    """DEEP: three instances of deep_chain_mesh (per-lane stack bound > 32: the HBM overflow stack is
+    used) and the plane, LAMBERT_SHADOW, small frame (test scene for concurrent launches)."""
+    m = (deep_chain_mesh(), None)
+    inst = [(0, IDENTITY, 0, RT_HITGROUP_MODEL), (0, translation(3.0, 1.0, -5.0), 1, RT_HITGROUP_MODEL),
+            (0, _rot_scale((0, 1, 0), 20.0, (1.0, 1.0, 1.0), (-4.0, 0.0, -9.0)), 2, RT_HITGROUP_MODEL),
+            (1, IDENTITY, 3, RT_HITGROUP_PLANE)]
+    return SceneSpec("DEEP", [m, (plane_vertices(), None)], inst, REFERENCE_LIGHTS[:2], REFERENCE_MATERIAL,
+                     ((20.0, 22.0, 70.0), (20.0, 18.0, 0.0), (0.0, 1.0, 0.0)), 96, 64, RT_SHADE_LAMBERT_SHADOW)
 
 
 def upload(ctx, spec: SceneSpec) -> List[int]:

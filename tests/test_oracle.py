@@ -361,3 +361,29 @@ def test_reflection_chain_kat():
     assert st[8] == 1
     expect = (1.0 - r) * s32[0, 0, :3].astype(np.float64) + r * miss
     assert np.abs(o32[0, 0, :3] - expect).max() < 1e-6
+
+
+@pytest.mark.parametrize("name,size", [("C2", (192, 108)), ("C4", (160, 90)), ("REFL", (96, 54)), ("DEGEN", (160, 90)),
+                                       ("C5", (64, 36))])
+def test_cpu_baseline_build_renders_the_checker_frames(name, size):
+    """oracle/libbaseline.so (-O3, counters compiled out, plain-compare slab min/max) is the
+    bench's CPU baseline; it must render exactly the checker's frames (per-ray schedule, as the bench times it)."""
+    spec = scenes.config(name).with_size(*size)
+    base = oracle.baseline_lib()
+    assert b"-O3" in base.oracle_build_info() and b"ORACLE_NO_COUNTERS" in base.oracle_build_info()
+    c8, c32, cst = oracle.Scene(spec).render_spec(spec, nthreads=4, schedule=1)
+    b8, b32, bst = oracle.Scene(spec, library=base).render_spec(spec, nthreads=4, schedule=1)
+    assert np.array_equal(c8, b8) and np.array_equal(c32.view(np.uint32), b32.view(np.uint32))
+    assert cst[0] > 0 and not bst[[0, 1, 2, 3, 4, 5, 8, 9, 10, 11]].any()  # the baseline counts no tests
+
+
+def test_deep_scene_reaches_past_the_lds_stack():
+    """DEEP (scenes.deep_scene): the per-lane traversal's stack goes past the device's 32 LDS entries, so the
+    -m gpu concurrency test really exercises the HBM overflow stack."""
+    spec = scenes.config("DEEP")
+    o = oracle.Scene(spec)
+    tlas, blas = o.tlas_info(), o.blas_info(0)
+    assert int(tlas[3]) + 1 + int(blas[3]) > 32
+    oracle.max_stack_reached()
+    o.render_spec(spec, nthreads=1, schedule=1)
+    assert oracle.max_stack_reached() > 32
