@@ -52,6 +52,7 @@ _SIGS = [
     ("oracle_direct", None, [_FP, _FP, ctypes.POINTER(oracle_light), _U32, _FP, _FP]),
     ("oracle_pow", ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
     ("oracle_max_stack_reached", _I, [_I]),
+    ("oracle_camera_rays", None, [_FP, _U32, _U32, _P, _P, _U32, ctypes.c_float, ctypes.c_float, _P]),
 ]
 
 
@@ -175,6 +176,18 @@ def raster(draws, cb, W: int, H: int, object_to_world=None):
     if r:
         raise RuntimeError(f"oracle_raster failed ({r})")
     return rgba8, depth, prim
+
+
+def camera_rays(cb, W: int, H: int, px, py, ox: float = 0.5, oy: float = 0.5) -> np.ndarray:
+    """RayGen's float32 camera rays (the frame's exact bits) for pixels (px, py): (n, 8) float32 rows
+    (o.xyz, tmin 0, d.xyz, tmax 1e5), the trace_rays layout."""
+    c, cp = _f(cb)
+    x = np.ascontiguousarray(px, dtype=np.uint32)
+    y = np.ascontiguousarray(py, dtype=np.uint32)
+    out = np.zeros((x.size, 8), np.float32)
+    lib.oracle_camera_rays(cp, W, H, x.ctypes.data_as(_P), y.ctypes.data_as(_P), x.size, ox, oy,
+                           out.ctypes.data_as(_P))
+    return out
 
 
 def max_stack_reached(reset: bool = True) -> int:

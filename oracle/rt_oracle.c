@@ -1663,6 +1663,26 @@ int oracle_render(const oracle_scene* s, const float cb[64], const oracle_light*
   return 0;
 }
 
+/* RayGen's camera rays (oraygen: the exact float32 bits the frame traces) for n pixels (px[i], py[i]) at the
+ * sample offset (ox, oy), in oracle_trace_rays' layout: 8 floats per ray (o.xyz, tmin 0, d.xyz, tmax 1e5,
+ * CastDefaultRay, Common.hlsl:44-56). Test infrastructure: the full-size float64 cross-check compares the
+ * float32 primary hits of these rays with its own. */
+void oracle_camera_rays(const float cb[64], uint32_t W, uint32_t H, const uint32_t* px, const uint32_t* py, uint32_t n,
+                        float ox, float oy, float* rays) {
+  octx c;
+  memset(&c, 0, sizeof(c));
+  c.cb = cb;
+  c.W = W;
+  c.H = H;
+  for (uint32_t i = 0; i < n; ++i) {
+    vec3 O, D;
+    oraygen(&c, px[i], py[i], ox, oy, &O, &D);
+    float* r = rays + (size_t)i * 8;
+    r[0] = O.x; r[1] = O.y; r[2] = O.z; r[3] = 0.0f;
+    r[4] = D.x; r[5] = D.y; r[6] = D.z; r[7] = 100000.0f;
+  }
+}
+
 int oracle_trace_rays(const oracle_scene* s, const float* rays, uint32_t n, uint32_t flags, uint32_t* hits,
                       float* uv, int brute, uint64_t* stats) {
   if (!s || !s->tlas) return -1;

@@ -67,6 +67,8 @@ int oracle_render(const oracle_scene* s, const float cb[64], const oracle_light*
                   int brute_force, int schedule);
 /* batch trace: rays n x 8 floats, ray_flags = D3D12_RAY_FLAG bits (0x04 first hit ends, 0x10 cull back
  * faces), hits n x 4 u32 (t bits, instance, prim, flag), uv n x 2 (may be NULL) */
+void oracle_camera_rays(const float cb[64], uint32_t W, uint32_t H, const uint32_t* px, const uint32_t* py, uint32_t n,
+                        float ox, float oy, float* rays);
 int oracle_trace_rays(const oracle_scene* s, const float* rays, uint32_t n, uint32_t ray_flags, uint32_t* hits,
                       float* uv, int brute_force, uint64_t* stats);
 

@@ -108,7 +108,95 @@ def frames():
     np.savez_compressed(os.path.join(HERE, "frames_small.npz"), **data)
 
 
+# Full BASELINE sizes against the float64 restatement: evenly spaced rows of the full frame
+FULLSIZE_ROWS = {"C2": 64, "C2F": 64, "C3": 64, "REF": 64, "C4": 32}
+FULLSIZE_BOUND = 1e-3  # the north-star per-channel bound
+
+
+def _classify(h32, inst64, prim64):
+    """Primary-hit identity of the float32 walk (oracle BVH, RayGen's exact rays) against the float64 brute
+    force: agree, edge (same instance, another triangle: a shared edge), leak (float32 misses, or hits another
+    instance, where float64 hits: a ray through a seam or silhouette float32 Moller-Trumbore is not watertight
+    on), extra (float32 hits where float64 misses or hits another instance farther away)."""
+    f32 = h32[:, 3] == 1
+    i32 = np.where(f32, h32[:, 1].astype(np.int64), -1)
+    p32 = np.where(f32, h32[:, 2].astype(np.int64), -1)
+    t32 = np.where(f32, h32[:, 0].view(np.float32).astype(np.float64), np.inf)
+    cls = np.full(h32.shape[0], "agree", dtype=object)
+    same_i = i32 == inst64
+    cls[same_i & (p32 != prim64)] = "edge"
+    diff = ~same_i
+    cls[diff & (inst64 >= 0) & ((i32 < 0) | (t32 > 0))] = "leak"
+    cls[diff & (i32 >= 0) & (inst64 < 0)] = "extra"
+    return cls, t32
+
+
+def fullsize(names=None):
+    """tests/golden/fullsize_numpy.json: for C2, C3, C4 (1920x1080) and REF (1280x720), evenly spaced rows of
+    the FULL frame rendered by the float32 oracle (the GPU's frame bit for bit: the -m gpu full-frame tests)
+    and by the independent float64 numpy restatement: per-config L-inf, every pixel above the 1e-3 bound
+    with its cause, and the primary-hit identity of both (watertightness of float32 Moller-Trumbore along the
+    teapot's 1,036 seam edges: pixels where one precision hits the model and the other passes through)."""
+    import hashlib
+    import time
+    path = os.path.join(HERE, "fullsize_numpy.json")
+    out = {}
+    if os.path.exists(path):
+        with open(path) as f:
+            out = json.load(f)
+    for name in (names or FULLSIZE_ROWS):
+        t0 = time.time()
+        spec = scenes.config(name)
+        W, H = spec.width, spec.height
+        rows = np.unique(np.linspace(0, H - 1, FULLSIZE_ROWS[name]).round().astype(np.uint32))
+        sc = oracle.Scene(spec)
+        o8, o32, _ = sc.render_spec(spec, rows=rows, nthreads=8, schedule=1)
+        cb = spec.camera_buffer()
+        py, px = (a.ravel() for a in np.meshgrid(rows, np.arange(W, dtype=np.uint32), indexing="ij"))
+        npr = np_reference.Scene(spec)
+        O, D = np_reference.camera_rays(cb, W, H, px.astype(np.float64), py.astype(np.float64))
+        t64, i64, p64, u64, v64 = npr.intersect(O, D, 0.0, 100000.0)
+        img = npr.shade(O, D, t64, i64, p64, u64, v64, py.astype(np.float64), spec.mode)
+        h32, _, _ = sc.trace_rays(oracle.camera_rays(cb, W, H, px, py))
+        cls, t32 = _classify(h32, i64, p64)
+        d = np.abs(o32[..., :3].reshape(-1, 3).astype(np.float64) - img).max(axis=1)
+        big = np.argsort(-d)[: int((d > FULLSIZE_BOUND).sum())]
+        inst_names = {k: ("plane" if hg == 2 else f"model{iid}") for k, (_, _, iid, hg) in enumerate(spec.instances)}
+
+        def who(i):
+            return "miss" if i < 0 else inst_names[int(i)]
+        over = []
+        for j in big[:60]:
+            c = cls[j]
+            if c == "agree":
+                c = "shading"  # same primary hit: a shadow ray decided differently, or shading rounding
+            over.append({"x": int(px[j]), "y": int(py[j]), "linf": round(float(d[j]), 6), "cause": c,
+                         "hit32": who(int(h32[j, 1]) if h32[j, 3] else -1), "hit64": who(int(i64[j]))})
+        counts = {c: int((cls == c).sum()) for c in ("agree", "edge", "leak", "extra")}
+        out[name] = {
+            "size": [W, H], "rows": rows.tolist(), "pixels": int(px.size),
+            "linf": round(float(d.max()), 7),
+            "linf_agreeing_hits": round(float(d[cls == "agree"].max()), 7),
+            "pixels_over_bound": int((d > FULLSIZE_BOUND).sum()),
+            "over_bound_by_cause": {c: int(((d > FULLSIZE_BOUND) & (cls == c)).sum())
+                                    for c in ("agree", "edge", "leak", "extra")},
+            "primary_hit_identity": counts,
+            "leak_pixels": [{"x": int(px[j]), "y": int(py[j]), "hit32": who(int(h32[j, 1]) if h32[j, 3] else -1),
+                             "hit64": who(int(i64[j])), "t64": round(float(t64[j]), 5)}
+                            for j in np.nonzero(cls == "leak")[0][:40]],
+            "over_bound": over,
+            "oracle_rows_rgba8_sha256": hashlib.sha256(o8.tobytes()).hexdigest(),
+            "seconds": round(time.time() - t0, 1),
+        }
+        print(name, json.dumps({k: v for k, v in out[name].items() if k not in ("rows", "over_bound", "leak_pixels")}))
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+
+
 if __name__ == "__main__":
+    if "--fullsize" in sys.argv:
+        fullsize([a for a in sys.argv[1:] if not a.startswith("--")] or None)
+        sys.exit(0)
     if "--frames-only" not in sys.argv:
         camera()
         obj_ingest()

@@ -387,3 +387,24 @@ def test_deep_scene_reaches_past_the_lds_stack():
     oracle.max_stack_reached()
     o.render_spec(spec, nthreads=1, schedule=1)
     assert oracle.max_stack_reached() > 32
+
+
+def test_fullsize_float64_crosscheck_fixture():
+    """tests/golden/fullsize_numpy.json (make_golden.py --fullsize): evenly spaced rows of FULL-size frames of C2,
+    C2F, C3, C4 and REF rendered by the oracle and by the independent float64 numpy restatement. Every pixel
+    within the north-star 1e-3 bound, and float32 and float64 agree on every primary hit (no leak through the
+    teapot's seams at these cameras). The oracle still renders those rows to the recorded bytes (no drift)."""
+    import hashlib
+    import json
+    with open(os.path.join(os.path.dirname(__file__), "golden", "fullsize_numpy.json")) as f:
+        fx = json.load(f)
+    assert {"C2", "C2F", "C3", "C4", "REF"} <= set(fx)
+    for name, r in fx.items():
+        assert r["linf"] < 1e-3 and r["pixels_over_bound"] == 0, name
+        assert r["primary_hit_identity"]["leak"] == 0 and r["primary_hit_identity"]["extra"] == 0, name
+        assert len(r["rows"]) >= (64 if name != "C4" else 32)
+    for name in ("C2", "REF"):  # drift check on the two cheapest
+        spec = scenes.config(name)
+        rows = np.asarray(fx[name]["rows"], np.uint32)
+        o8, _, _ = oracle.Scene(spec).render_spec(spec, rows=rows, nthreads=8, schedule=1)
+        assert hashlib.sha256(o8.tobytes()).hexdigest() == fx[name]["oracle_rows_rgba8_sha256"], name
