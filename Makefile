@@ -44,11 +44,14 @@ $(BUILD)/rt_trace.o: $(SRC)/rt_trace.hip $(HDRS) | $(BUILD)
 $(BUILD)/rt_api.o: $(SRC)/rt_api.cpp $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(BUILD)/rt_comm.o: $(SRC)/rt_comm.cpp $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(BUILD)/rt_host.o: $(SRC)/rt_host.cpp include/rt_api.h | $(BUILD)
 	g++ $(CXXFLAGS) -c $< -o $@
 
-$(LIB): $(BUILD)/rt_api.o $(BUILD)/rt_host.o $(BUILD)/rt_lbvh.o $(BUILD)/rt_trace.o $(BUILD)/rt_raster.o | $(LIBDIR)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-rpath,$(ROCM)/lib
+$(LIB): $(BUILD)/rt_api.o $(BUILD)/rt_comm.o $(BUILD)/rt_host.o $(BUILD)/rt_lbvh.o $(BUILD)/rt_trace.o $(BUILD)/rt_raster.o | $(LIBDIR)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -ldl -Wl,-rpath,$(ROCM)/lib
 
 $(APP): $(SRC)/host/rt_app.cpp $(wildcard $(SRC)/host/*.hpp) $(LIB) | $(LIBDIR)
 	g++ $(CXXFLAGS) -I$(ROCM)/include -D__HIP_PLATFORM_AMD__ -o $@ $(SRC)/host/rt_app.cpp \

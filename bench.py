@@ -211,6 +211,22 @@ class HipBackend:
     def raster(self, spec, steps, warmup):
         return measure_raster(self, spec, steps, warmup)
 
+    @property
+    def native_strips(self) -> bool:
+        """Strips mode through the C-ABI's own frame loop (rt_render_strips: render -> ncclGather -> assembly
+        issued from C++); the gloo rehearsal on one device keeps the torch.distributed loop."""
+        return os.environ.get("RT_BENCH_ONE_DEVICE") != "1" and os.environ.get("RT_BENCH_TORCH_STRIPS") != "1"
+
+    def comm_open(self, world: int, rank: int):
+        """rt_comm over this rank's context: rank 0's ncclUniqueId is broadcast over the torch process group."""
+        uid = self.rt.comm_unique_id() if rank == 0 else bytes(self.rt.RT_COMM_ID_BYTES)
+        t = torch.tensor(list(uid), dtype=torch.uint8, device=self.device)
+        dist.broadcast(t, 0)
+        return self.rt.Comm(self.ctx, world, rank, bytes(t.cpu().tolist()))
+
+    def render_strips(self, comm, frame, stream):
+        comm.render_strips(self.spec.width, self.spec.height, frame, stream.cuda_stream, STRIP_ROWS)
+
     def close(self):
         if self.ctx is not None:
             self.ctx.close()
@@ -324,13 +340,22 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
     else:
         nstream, flight_ms, measured = pick_in_flight(be, W, NR, rows)
     render = measured if measured else [be.stream() for _ in range(nstream)]
+    native = strips and getattr(be, "native_strips", False)
     nslot = max(nstream, 2 if (strips and pipeline) else 1)
     local = [be.zeros((rows_per_rank, W, 4)) for _ in range(nslot)]
-    gathered = [be.zeros((world, rows_per_rank, W, 4)) if rank == 0 else None for _ in range(nslot)] if strips else None
+    gathered = ([be.zeros((world, rows_per_rank, W, 4)) if rank == 0 else None for _ in range(nslot)]
+                if strips and not native else None)
     frame = [be.zeros((H, W, 4)) if rank == 0 else None for _ in range(nslot)] if strips else None
+    rcomm = be.comm_open(world, rank) if native else None
     rendered = [be.sync_event() for _ in range(nslot)]
     freed = [be.sync_event() for _ in range(nslot)]
-    parts = [D.gather_parts(gathered[s], world, rank) for s in range(nslot)] if strips else None
+    parts = [D.gather_parts(gathered[s], world, rank) for s in range(nslot)] if strips and not native else None
+
+    def step_native(k: int):
+        """One frame through rt_render_strips: render on this slot's stream, ncclGather + assembly on the
+        communicator's stream, the slot pipeline and its events inside the library (one C call)."""
+        s = k % nslot
+        be.render_strips(rcomm, frame[s] if rank == 0 else None, render[s % nstream])
 
     def step(k: int):
         """One frame. In strips mode the caller holds `comm` as the current stream (the gather runs
@@ -349,7 +374,9 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
             be.record(freed[s], comm)
 
     import contextlib
-    on_comm = (lambda: be.use_stream(comm)) if strips else contextlib.nullcontext
+    on_comm = (lambda: be.use_stream(comm)) if strips and not native else contextlib.nullcontext
+    if native:
+        step = step_native  # noqa: F811
 
     k = 0
     # untimed counter pass: rays, tests and record fetches of this rank's share of one step
@@ -411,9 +438,13 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
         last = (k - 1) % nslot
         img = frame[last] if strips else local[last][:H]
         np.save(save_image, img.cpu().numpy())
+    if rcomm is not None:
+        rcomm.close()
     return {"rays_step": rays_step, "primary": int(counts[1].item()), "shadow": int(counts[2].item()),
             "tmax": tmax, "kernel_ms": kernel_ms, "stats": st, "build": build, "rows_local": len(rows) if strips else H,
-            "tile_rows": tile_rows, "tile_ms": tile_ms, "in_flight": nstream, "in_flight_ms": flight_ms}
+            "tile_rows": tile_rows, "tile_ms": tile_ms, "in_flight": nstream, "in_flight_ms": flight_ms,
+            "strips_loop": ("rt_render_strips (C-ABI: render -> ncclGather -> assembly)" if native else
+                            "torch.distributed gather" if strips else None)}
 
 
 # ---------------------------------------------------------------------------------------------
@@ -612,11 +643,17 @@ def main(argv=None) -> int:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
-    strips = distributed and a.mode in ("auto", "strips")
+    # --mode strips at N = 1: the tiled-frame loop over a world-1 communicator (rehearsal of the N > 1 path)
+    strips = (distributed and a.mode in ("auto", "strips")) or a.mode == "strips"
 
     from realtimeraytracing_gradproject_amd import scenes
     be = make_backend(local)
-    if distributed:
+    if distributed or strips:
+        if not distributed:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         be.init_pg()
 
     def spec_of(name):
@@ -678,9 +715,11 @@ def main(argv=None) -> int:
                        "primary_rays": r["primary"], "shadow_rays": r["shadow"],
                        "parallelism": (f"strips{world}+gather" + ("" if a.no_pipeline else " (pipelined)")) if strips
                        else f"frames{world}",
-                       "rccl_world_size": world if distributed else None, "schedule": a.schedule,
+                       "rccl_world_size": world if (distributed or strips) else None, "strips_loop": r["strips_loop"],
+                       "schedule": a.schedule,
                        "tile_rows": r["tile_rows"], "tile_ms_rank0": r["tile_ms"],
                        "frames_in_flight": r["in_flight"], "in_flight_ms_rank0": r["in_flight_ms"],
+                       # SURVEY 8(d)'s frame latency: one frame alone, enqueue -> complete (one stream, back to back)
                        "frame_ms_one_stream": round(r["kernel_ms"], 4),
                        "settle_ms": a.settle_ms},
             "roofline": rf,
@@ -690,7 +729,7 @@ def main(argv=None) -> int:
         }
         print(json.dumps(out), flush=True)
     be.close()
-    if distributed:
+    if distributed or strips:
         dist.barrier()
         dist.destroy_process_group()
     return 0

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RT_API_VERSION 2
+#define RT_API_VERSION 3
 
 typedef struct rt_ctx* rt_ctx_t;
 typedef struct rt_mesh* rt_mesh_t;
@@ -37,7 +37,7 @@ typedef enum {
   RT_E_INVALID = -1,     /* bad argument / misuse (reference: std::logic_error) */
   RT_E_OOM = -2,         /* device or host allocation failed */
   RT_E_HIP = -3,         /* a HIP runtime call failed (reference: FAILED(hr)) */
-  RT_E_RCCL = -4,        /* reserved: collective failure */
+  RT_E_RCCL = -4,        /* a collective (RCCL) call failed: rt_comm_*, rt_render_strips */
   RT_E_UNSUPPORTED = -5, /* no gfx950 device / feature not built */
   RT_E_IO = -6           /* file could not be opened (reference: LoadObjFile returns false) */
 } rt_status;
@@ -260,6 +260,35 @@ rt_status rt_event_create(void** ev_out);
 rt_status rt_event_destroy(void* ev);
 rt_status rt_event_record(void* ev, void* hip_stream);
 rt_status rt_stream_wait_event(void* hip_stream, void* ev);
+
+/* ---- Multi-GPU frame loop ---------------------------------------------------------
+ * One frame (the reference's DispatchRays W x H, D3D12HelloTriangle.cpp:584-592) tiled over N ranks, one
+ * process and one rt_ctx per GPU, each holding the full scene: rank r renders the interleaved strips
+ * s % N == r (strip_rows rows each) into a compact buffer, one ncclGather (rccl.h:745) brings every rank's
+ * buffer to rank 0, and rt_assemble_strips un-interleaves them there. No reference counterpart (the reference
+ * renders on one GPU). RCCL is loaded at run time (librccl.so.1; RT_E_UNSUPPORTED when absent). */
+typedef struct rt_comm* rt_comm_t;
+#define RT_COMM_ID_BYTES 128 /* == sizeof(ncclUniqueId) */
+/* ncclGetUniqueId: rank 0 creates the id; the caller hands the 128 bytes to every rank (MPI, a file, a
+ * torch.distributed broadcast). */
+rt_status rt_comm_get_unique_id(void* id_out);
+/* ncclCommInitRank on the context's device. Collective: returns once all nranks ranks have joined. */
+rt_status rt_comm_init(rt_ctx_t ctx, uint32_t nranks, uint32_t rank, const void* id, rt_comm_t* out);
+rt_status rt_comm_destroy(rt_comm_t comm);
+const char* rt_comm_last_error(rt_comm_t comm);
+/* hipStream_t of the communicator: the gathers and rank 0's assembly run on it. */
+void* rt_comm_stream(rt_comm_t comm);
+rt_status rt_comm_synchronize(rt_comm_t comm);
+/* One tiled frame, collective over the ranks (every rank calls it, in the same frame order): this rank's
+ * strips are rendered on render_stream (NULL = the context's stream) into one of the communicator's pipeline
+ * slots; the communicator's stream waits for that render (a device-side event), gathers the slots of all ranks
+ * into rank 0 and, on rank 0, assembles the W x H RGBA8 frame into frame_out (device buffer; ignored on other
+ * ranks). A slot is re-rendered only after its gather and assembly finished (device-side events; no host
+ * waits), so consecutive calls overlap frame k's gather with frame k + 1's render, and renders issued on
+ * different streams overlap each other (frames in flight). Asynchronous: frame_out is complete once the work
+ * issued so far on rt_comm_stream(comm) has finished. */
+rt_status rt_render_strips(rt_comm_t comm, uint32_t W, uint32_t H, uint32_t strip_rows, void* frame_out,
+                           void* render_stream);
 
 /* Copies the counters (RT_STAT_*) to out[RT_STAT_COUNT]; synchronises the context. */
 rt_status rt_stats(rt_ctx_t ctx, uint64_t out[RT_STAT_COUNT]);

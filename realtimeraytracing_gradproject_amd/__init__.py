@@ -108,6 +108,13 @@ SIGNATURES = [
     ("rt_event_destroy", _I, [_P]),
     ("rt_event_record", _I, [_P, _P]),
     ("rt_stream_wait_event", _I, [_P, _P]),
+    ("rt_comm_get_unique_id", _I, [_P]),
+    ("rt_comm_init", _I, [_P, _U32, _U32, _P, ctypes.POINTER(_P)]),
+    ("rt_comm_destroy", _I, [_P]),
+    ("rt_comm_last_error", ctypes.c_char_p, [_P]),
+    ("rt_comm_stream", _P, [_P]),
+    ("rt_comm_synchronize", _I, [_P]),
+    ("rt_render_strips", _I, [_P, _U32, _U32, _U32, _P, _P]),
     ("rt_stats", _I, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     ("rt_stats_reset", _I, [_P]),
     ("rt_mesh_load_obj", _I, [ctypes.c_char_p, ctypes.POINTER(_P)]),
@@ -358,6 +365,64 @@ class PipelineEvent:
     def close(self):
         if self._h:
             lib.rt_event_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001  (interpreter shutdown)
+            pass
+
+
+RT_COMM_ID_BYTES = 128
+
+
+def comm_unique_id() -> bytes:
+    """rt_comm_get_unique_id (ncclGetUniqueId): created on rank 0, handed to every rank by the caller."""
+    buf = ctypes.create_string_buffer(RT_COMM_ID_BYTES)
+    st = lib.rt_comm_get_unique_id(buf)
+    if st != RT_OK:
+        raise RtError(st, "rt_comm_get_unique_id")
+    return buf.raw
+
+
+class Comm:
+    """rt_comm_*: the native multi-GPU frame loop (strips -> ncclGather -> assembly on rank 0) of one context.
+    Collective: every rank constructs it with the same 128-byte id and calls render_strips in the same order."""
+
+    def __init__(self, ctx: "Context", nranks: int, rank: int, uid: bytes):
+        if len(uid) != RT_COMM_ID_BYTES:
+            raise ValueError("the communicator id is 128 bytes")
+        self._lib = ctx._lib
+        self.ctx, self.nranks, self.rank = ctx, nranks, rank
+        h = _P()
+        self._idbuf = ctypes.create_string_buffer(uid, RT_COMM_ID_BYTES)
+        st = self._lib.rt_comm_init(ctx._h, nranks, rank, self._idbuf, ctypes.byref(h))
+        if st != RT_OK:
+            raise RtError(st, f"rt_comm_init(nranks={nranks}, rank={rank})")
+        self._h = h
+
+    def _check(self, st: int, what: str):
+        if st != RT_OK:
+            raise RtError(st, f"{what}: {self._lib.rt_comm_last_error(self._h).decode()}")
+
+    def render_strips(self, width: int, height: int, frame_out=None, stream: Optional[int] = None,
+                      strip_rows_: int = 8):
+        """One tiled frame (rt_render_strips): frame_out is rank 0's H x W x 4 device buffer."""
+        self._check(self._lib.rt_render_strips(self._h, width, height, strip_rows_, _ptr(frame_out), stream),
+                    "rt_render_strips")
+
+    @property
+    def stream(self) -> int:
+        """hipStream_t of the gathers and the assembly."""
+        return self._lib.rt_comm_stream(self._h)
+
+    def synchronize(self):
+        self._check(self._lib.rt_comm_synchronize(self._h), "rt_comm_synchronize")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.rt_comm_destroy(self._h)
             self._h = None
 
     def __del__(self):

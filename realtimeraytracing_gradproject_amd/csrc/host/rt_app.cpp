@@ -8,6 +8,12 @@
 //          [--lights N] [--mode ref|lambert_shadow|primary] [--spp S] [--frames F]
 //          [--eye x y z --center x y z] [--out frame.ppm] [--raw frame.rgba]
 //          [--drag BUTTONS DX DY] [--out-pattern frame_%03d.ppm]
+//          [--ranks N --rank R --comm-id FILE]
+//
+// --ranks tiles every frame over N processes (one per GPU, device = R % visible GPUs) through the C-ABI's
+// frame loop: rt_render_strips renders rank R's interleaved strips, ncclGathers them into rank 0 and assembles
+// the frame there. Rank 0 writes the communicator id (ncclGetUniqueId) to FILE, the other ranks
+// read it; --ranks 1 runs the same loop over a world-1 communicator. Only rank 0 writes frames.
 //
 // --drag replays a mouse drag through the manipulator, as the reference's window messages do
 // (OnButtonDown / OnMouseMove, D3D12HelloTriangle.cpp:1206-1234): button down at the window
@@ -18,6 +24,8 @@
 
 #include <chrono>
 #include <cstdio>
+#include <fstream>
+#include <thread>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -37,6 +45,8 @@ struct Options {
   std::string model = "teapot.obj", scene = "ref", mode = "ref", out, raw, drag, out_pattern;
   int drag_dx = 0, drag_dy = 0;
   int width = 1280, height = 720, lights = 6, spp = 1, frames = 1;
+  int ranks = 0, rank = 0;  // --ranks N: frames tiled over N processes (0: one GPU, no communicator)
+  std::string comm_id;
   float eye[3] = {1.5f, 1.5f, 1.5f}, center[3] = {0, 0, 0}, up[3] = {0, 1, 0};
 };
 
@@ -55,11 +65,35 @@ class RayTracingApp {
   void OnInit() {
     CameraManip().setWindowSize(m_opt.width, m_opt.height);
     CameraManip().setLookat(m_opt.eye, m_opt.center, m_opt.up);
-    ThrowIfFailed(rt_create(0, &m_ctx), nullptr, "rt_create");
+    int ndev = 1;
+    hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+    ThrowIfFailed(rt_create(m_opt.ranks > 0 ? m_opt.rank % ndev : 0, &m_ctx), nullptr, "rt_create");
     LoadAssets();
     CreateAccelerationStructures();
     hip_check(hipMalloc(&m_output, (size_t)m_opt.width * m_opt.height * 4), "hipMalloc(output)");
     hip_check(hipStreamCreate(&m_stream), "hipStreamCreate");
+    if (m_opt.ranks > 0) CreateCommunicator();
+  }
+
+  // The multi-GPU frame loop: rank 0's ncclUniqueId travels through a file (no MPI in this app).
+  void CreateCommunicator() {
+    unsigned char id[RT_COMM_ID_BYTES];
+    if (m_opt.rank == 0) {
+      ThrowIfFailed(rt_comm_get_unique_id(id), nullptr, "rt_comm_get_unique_id");
+      if (m_opt.ranks > 1) {
+        const std::string tmp = m_opt.comm_id + ".tmp";
+        std::ofstream(tmp, std::ios::binary).write((const char*)id, sizeof(id));
+        if (std::rename(tmp.c_str(), m_opt.comm_id.c_str()) != 0) throw std::runtime_error("cannot write " + m_opt.comm_id);
+      }
+    } else {
+      for (int tries = 0;; ++tries) {
+        std::ifstream f(m_opt.comm_id, std::ios::binary);
+        if (f && f.read((char*)id, sizeof(id)) && f.gcount() == (std::streamsize)sizeof(id)) break;
+        if (tries > 3000) throw std::runtime_error("no communicator id in " + m_opt.comm_id);
+        std::this_thread::sleep_for(std::chrono::milliseconds(10));
+      }
+    }
+    ThrowIfFailed(rt_comm_init(m_ctx, (uint32_t)m_opt.ranks, (uint32_t)m_opt.rank, id, &m_comm), m_ctx, "rt_comm_init");
   }
 
   // D3D12HelloTriangle::OnButtonDown (:1206-1212): the reference negates the window coordinates
@@ -87,9 +121,21 @@ class RayTracingApp {
     hip_check(hipEventCreate(&a), "event");
     hip_check(hipEventCreate(&b), "event");
     hip_check(hipEventRecord(a, m_stream), "event");
-    ThrowIfFailed(rt_dispatch_rays(m_ctx, (uint32_t)m_opt.width, (uint32_t)m_opt.height, nullptr, 0, m_output, nullptr,
-                                   m_stream),
-                  m_ctx, "rt_dispatch_rays");
+    if (m_comm) {
+      // the frame tiled over the ranks: strips rendered here, gathered and assembled on rank 0
+      const rt_status st = rt_render_strips(m_comm, (uint32_t)m_opt.width, (uint32_t)m_opt.height, 8, m_output, m_stream);
+      if (st != RT_OK) throw std::runtime_error(std::string("rt_render_strips: ") + rt_comm_last_error(m_comm));
+      // the frame is complete when the communicator's stream is: the timing stream waits for it
+      hipEvent_t done;
+      hip_check(hipEventCreateWithFlags(&done, hipEventDisableTiming), "event");
+      hip_check(hipEventRecord(done, (hipStream_t)rt_comm_stream(m_comm)), "event");
+      hip_check(hipStreamWaitEvent(m_stream, done, 0), "event");
+      (void)hipEventDestroy(done);
+    } else {
+      ThrowIfFailed(rt_dispatch_rays(m_ctx, (uint32_t)m_opt.width, (uint32_t)m_opt.height, nullptr, 0, m_output,
+                                     nullptr, m_stream),
+                    m_ctx, "rt_dispatch_rays");
+    }
     hip_check(hipEventRecord(b, m_stream), "event");
     hip_check(hipStreamSynchronize(m_stream), "WaitForPreviousFrame");
     float ms = 0;
@@ -118,7 +164,11 @@ class RayTracingApp {
     }
   }
 
+  bool IsRoot() const { return m_opt.ranks == 0 || m_opt.rank == 0; }
+
   void OnDestroy() {
+    if (m_comm) rt_comm_destroy(m_comm);
+    m_comm = nullptr;
     if (m_output) (void)hipFree(m_output);
     if (m_stream) (void)hipStreamDestroy(m_stream);
     if (m_ctx) rt_destroy(m_ctx);
@@ -174,6 +224,7 @@ class RayTracingApp {
 
   Options m_opt;
   rt_ctx_t m_ctx = nullptr;
+  rt_comm_t m_comm = nullptr;
   void* m_output = nullptr;
   hipStream_t m_stream = nullptr;
   std::vector<float> m_vertices, m_plane;
@@ -230,6 +281,9 @@ Options parse(int argc, char** argv) {
       o.drag_dx = std::atoi(next());
       o.drag_dy = std::atoi(next());
     } else if (a == "--out-pattern") o.out_pattern = next();
+    else if (a == "--ranks") o.ranks = std::atoi(next());
+    else if (a == "--rank") o.rank = std::atoi(next());
+    else if (a == "--comm-id") o.comm_id = next();
     else {
       std::fprintf(stderr, "unknown option %s\n", a.c_str());
       std::exit(2);
@@ -242,6 +296,10 @@ Options parse(int argc, char** argv) {
 
 int main(int argc, char** argv) {
   Options o = parse(argc, argv);
+  if (o.ranks < 0 || (o.ranks > 0 && (o.rank < 0 || o.rank >= o.ranks)) || (o.ranks > 1 && o.comm_id.empty())) {
+    std::fprintf(stderr, "--ranks N needs 0 <= --rank < N and, for N > 1, --comm-id FILE\n");
+    return 2;
+  }
   RayTracingApp app(o);
   try {
     app.OnInit();
@@ -260,13 +318,13 @@ int main(int argc, char** argv) {
       float ms = app.OnRender();
       sum += ms;
       best = ms < best ? ms : best;
-      if (!o.out_pattern.empty()) {
+      if (!o.out_pattern.empty() && app.IsRoot()) {
         char name[1024];
         std::snprintf(name, sizeof(name), o.out_pattern.c_str(), f);
         app.Save(name, "");
       }
     }
-    app.Save(o.out, o.raw);
+    if (app.IsRoot()) app.Save(o.out, o.raw);
     std::printf("{\"frames\": %d, \"ms_mean\": %.4f, \"ms_best\": %.4f, \"width\": %d, \"height\": %d}\n", o.frames,
                 sum / o.frames, best, o.width, o.height);
     app.OnDestroy();

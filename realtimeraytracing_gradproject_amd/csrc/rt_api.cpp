@@ -176,6 +176,11 @@ struct rt_ctx {
   bool raster_pending = false;
 };
 
+namespace rt {
+int ctx_device(rt_ctx* c) { return c ? c->device : 0; }
+void* ctx_stream(rt_ctx* c) { return c ? (void*)c->stream : nullptr; }
+}  // namespace rt
+
 namespace {
 
 rt_status fail(rt_ctx* c, rt_status st, const std::string& msg) {
@@ -668,6 +673,7 @@ static rt::SceneView scene_view(rt_ctx* c) {
   sv.ovf = nullptr;
   sv.ovf_lanes = 0;
   sv.cull_sense = 1.0f;
+  sv.hybrid = maxb <= (uint32_t)rt::kHybridStack ? 1 : 0;
   return sv;
 }
 

@@ -1,0 +1,240 @@
+// rt_comm.cpp — the multi-GPU frame loop behind the C-ABI: one frame tiled over the
+// ranks in interleaved strips, ONE ncclGather of every rank's compact strip buffer into rank 0
+// (rccl.h:745), then the un-interleave kernel (rt_assemble_strips) on rank 0. One process per GPU,
+// each with its own rt_ctx and the full scene; nothing but finished strips crosses xGMI.
+//
+// The frame being tiled is the reference's DispatchRays W x H (D3D12HelloTriangle.cpp:584-592),
+// issued once per OnRender (:436-471). The whole step is issued from C++ (render on the caller's
+// stream, gather + assembly on the communicator's stream, device-side events between them), so a
+// step costs one call of host issue instead of a Python loop of collectives.
+//
+// RCCL is bound at run time (dlopen of librccl.so.1): a process that already loaded RCCL (torch)
+// shares that copy, and a context that never creates a communicator never loads it.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <dlfcn.h>
+
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_api.h"
+#include "rt_internal.hpp"
+
+namespace {
+
+struct RcclApi {
+  bool ok = false;
+  std::string err;
+  ncclResult_t (*getUniqueId)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*commInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*commDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*gather)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  const char* (*getErrorString)(ncclResult_t) = nullptr;
+};
+
+RcclApi& rccl() {
+  static RcclApi api;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+      const char* e = dlerror();
+      api.err = std::string("dlopen(librccl.so.1): ") + (e ? e : "not found");
+      return;
+    }
+    auto sym = [&](const char* n) { return dlsym(h, n); };
+    api.getUniqueId = (decltype(api.getUniqueId))sym("ncclGetUniqueId");
+    api.commInitRank = (decltype(api.commInitRank))sym("ncclCommInitRank");
+    api.commDestroy = (decltype(api.commDestroy))sym("ncclCommDestroy");
+    api.gather = (decltype(api.gather))sym("ncclGather");
+    api.getErrorString = (decltype(api.getErrorString))sym("ncclGetErrorString");
+    api.ok = api.getUniqueId && api.commInitRank && api.commDestroy && api.gather && api.getErrorString;
+    if (!api.ok) api.err = "librccl.so.1 lacks ncclGather / ncclCommInitRank";
+  });
+  return api;
+}
+
+struct Slot {
+  void* local = nullptr;     // this rank's strips, compact: rows_per_rank x W RGBA8
+  void* gathered = nullptr;  // rank 0: nranks x rows_per_rank x W RGBA8
+  hipEvent_t rendered = nullptr, freed = nullptr;
+  bool used = false;
+};
+
+constexpr uint32_t kSlots = 4;  // frames in the render -> gather pipeline (frames in flight <= 4, bench.py)
+
+hipEvent_t pipeline_event() {
+  hipEvent_t e = nullptr;
+  // device-side hand-offs only: no timestamp, no system-scope release (rt_event_create's flags)
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) return nullptr;
+  return e;
+}
+
+}  // namespace
+
+struct rt_comm {
+  rt_ctx_t ctx = nullptr;
+  int device = 0;
+  uint32_t nranks = 1, rank = 0;
+  ncclComm_t comm = nullptr;
+  hipStream_t stream = nullptr;  // gathers + assembly
+  std::string err;
+  // frame geometry of the slots (re-planned when it changes)
+  uint32_t W = 0, H = 0, strip = 0, rows_per_rank = 0;
+  std::vector<uint32_t> rows;  // this rank's global rows, output order
+  Slot slots[kSlots];
+  uint64_t next = 0;
+};
+
+namespace {
+
+rt_status cfail(rt_comm* c, rt_status st, const std::string& m) {
+  if (c) c->err = m;
+  return st;
+}
+
+rt_status nccl_fail(rt_comm* c, ncclResult_t r, const char* what) {
+  return cfail(c, RT_E_RCCL, std::string(what) + ": " + rccl().getErrorString(r));
+}
+
+void release_slots(rt_comm* c) {
+  for (Slot& s : c->slots) {
+    if (s.local) (void)hipFree(s.local);
+    if (s.gathered) (void)hipFree(s.gathered);
+    if (s.rendered) (void)hipEventDestroy(s.rendered);
+    if (s.freed) (void)hipEventDestroy(s.freed);
+    s = Slot();
+  }
+}
+
+// (re)plans the strips of a W x H frame and sizes the pipeline slots; waits for the slots' last uses
+rt_status plan(rt_comm* c, uint32_t W, uint32_t H, uint32_t strip) {
+  if (c->W == W && c->H == H && c->strip == strip) return RT_OK;
+  if (c->stream && hipStreamSynchronize(c->stream) != hipSuccess) return cfail(c, RT_E_HIP, "rt_render_strips: drain");
+  for (Slot& s : c->slots)
+    if (s.used && s.freed && hipEventSynchronize(s.freed) != hipSuccess)
+      return cfail(c, RT_E_HIP, "rt_render_strips: drain");
+  release_slots(c);
+  c->W = c->H = c->strip = 0;
+  const uint32_t n = rt_strip_rows(H, c->nranks, c->rank, strip, nullptr, 0);
+  c->rows.assign(n, 0u);
+  if (n) rt_strip_rows(H, c->nranks, c->rank, strip, c->rows.data(), n);
+  const uint32_t nstrips = (H + strip - 1) / strip;
+  c->rows_per_rank = ((nstrips + c->nranks - 1) / c->nranks) * strip;
+  const size_t local_bytes = (size_t)c->rows_per_rank * W * 4;
+  for (Slot& s : c->slots) {
+    if (hipMalloc(&s.local, local_bytes) != hipSuccess) return cfail(c, RT_E_OOM, "rt_render_strips: hipMalloc(local)");
+    if (c->rank == 0 && hipMalloc(&s.gathered, local_bytes * c->nranks) != hipSuccess)
+      return cfail(c, RT_E_OOM, "rt_render_strips: hipMalloc(gathered)");
+    if (!(s.rendered = pipeline_event()) || !(s.freed = pipeline_event()))
+      return cfail(c, RT_E_HIP, "rt_render_strips: events");
+  }
+  c->W = W;
+  c->H = H;
+  c->strip = strip;
+  return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+rt_status rt_comm_get_unique_id(void* id_out) {
+  if (!id_out) return RT_E_INVALID;
+  RcclApi& api = rccl();
+  if (!api.ok) return RT_E_UNSUPPORTED;
+  ncclUniqueId id;
+  if (api.getUniqueId(&id) != ncclSuccess) return RT_E_RCCL;
+  static_assert(sizeof(ncclUniqueId) == RT_COMM_ID_BYTES, "ncclUniqueId size");
+  std::memcpy(id_out, &id, sizeof(id));
+  return RT_OK;
+}
+
+rt_status rt_comm_init(rt_ctx_t ctx, uint32_t nranks, uint32_t rank, const void* id, rt_comm_t* out) {
+  if (!out) return RT_E_INVALID;
+  *out = nullptr;
+  if (!ctx || !id || nranks == 0 || rank >= nranks) return RT_E_INVALID;
+  RcclApi& api = rccl();
+  if (!api.ok) return RT_E_UNSUPPORTED;
+  rt_comm* c = new (std::nothrow) rt_comm();
+  if (!c) return RT_E_OOM;
+  c->ctx = ctx;
+  c->device = rt::ctx_device(ctx);
+  c->nranks = nranks;
+  c->rank = rank;
+  if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return RT_E_HIP;
+  }
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  // collective: returns when every rank has joined
+  if (api.commInitRank(&c->comm, (int)nranks, uid, (int)rank) != ncclSuccess) {
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return RT_E_RCCL;
+  }
+  *out = c;
+  return RT_OK;
+}
+
+rt_status rt_comm_destroy(rt_comm_t c) {
+  if (!c) return RT_E_INVALID;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  for (Slot& s : c->slots)
+    if (s.used && s.freed) (void)hipEventSynchronize(s.freed);
+  if (c->comm) (void)rccl().commDestroy(c->comm);
+  release_slots(c);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+  return RT_OK;
+}
+
+const char* rt_comm_last_error(rt_comm_t c) { return c ? c->err.c_str() : "null communicator"; }
+
+void* rt_comm_stream(rt_comm_t c) { return c ? (void*)c->stream : nullptr; }
+
+rt_status rt_comm_synchronize(rt_comm_t c) {
+  if (!c) return RT_E_INVALID;
+  (void)hipSetDevice(c->device);
+  return hipStreamSynchronize(c->stream) == hipSuccess ? RT_OK : cfail(c, RT_E_HIP, "rt_comm_synchronize");
+}
+
+rt_status rt_render_strips(rt_comm_t c, uint32_t W, uint32_t H, uint32_t strip_rows, void* frame_out,
+                           void* render_stream) {
+  if (!c) return RT_E_INVALID;
+  if (W == 0 || H == 0 || strip_rows == 0) return cfail(c, RT_E_INVALID, "rt_render_strips: bad size");
+  if (c->rank == 0 && !frame_out) return cfail(c, RT_E_INVALID, "rt_render_strips: rank 0 needs frame_out");
+  (void)hipSetDevice(c->device);
+  rt_status st = plan(c, W, H, strip_rows);
+  if (st != RT_OK) return st;
+  hipStream_t rs = render_stream ? (hipStream_t)render_stream : (hipStream_t)rt::ctx_stream(c->ctx);
+  Slot& s = c->slots[c->next % kSlots];
+  ++c->next;
+  // the slot's previous frame must have left it (its gather read `local`, its assembly `gathered`)
+  if (s.used && hipStreamWaitEvent(rs, s.freed, 0) != hipSuccess)
+    return cfail(c, RT_E_HIP, "rt_render_strips: order after the slot's last gather");
+  if (!c->rows.empty()) {
+    st = rt_dispatch_rays(c->ctx, W, H, c->rows.data(), (uint32_t)c->rows.size(), s.local, nullptr, rs);
+    if (st != RT_OK) return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));
+  }
+  if (hipEventRecord(s.rendered, rs) != hipSuccess || hipStreamWaitEvent(c->stream, s.rendered, 0) != hipSuccess)
+    return cfail(c, RT_E_HIP, "rt_render_strips: render -> gather hand-off");
+  const size_t count = (size_t)c->rows_per_rank * W * 4;
+  ncclResult_t r = rccl().gather(s.local, c->rank == 0 ? s.gathered : nullptr, count, ncclUint8, 0, c->comm, c->stream);
+  if (r != ncclSuccess) return nccl_fail(c, r, "rt_render_strips: ncclGather");
+  if (c->rank == 0) {
+    st = rt_assemble_strips(c->ctx, W, H, c->nranks, strip_rows, s.gathered, frame_out, c->stream);
+    if (st != RT_OK) return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));
+  }
+  if (hipEventRecord(s.freed, c->stream) != hipSuccess) return cfail(c, RT_E_HIP, "rt_render_strips: record");
+  s.used = true;
+  return RT_OK;
+}
+
+}  // extern "C"

@@ -106,6 +106,9 @@ constexpr int kMaxLights = 16;
 constexpr int32_t kStackSentinel = INT32_MIN;  // TLAS -> BLAS transition marker
 constexpr int kMaxTraversalStack = 256;        // entries per lane (LDS part + HBM overflow)
 constexpr int kLdsStackEntries = 32;           // LDS part: 32 KB per 256-lane workgroup
+// Packet walks hand a BLAS subtree to per-lane walks when few lanes want it (rt_trace.hip, lane_subtree):
+// their stacks live in LDS, kHybridStack entries per lane, so only scenes whose BLAS bound fits take it.
+constexpr int kHybridStack = 32;
 // Reflection bounces per camera sample in RT_SHADE_REF: the reference pipeline allows 20 nested
 // TraceRay levels (D3D12HelloTriangle.cpp:954) = camera ray + 18 reflections + the plane's
 // shadow ray. A reflective hit at the limit shades as non-reflective (pinned; DXR would fail).
@@ -156,6 +159,8 @@ struct SceneView {
   int* ovf;            // HBM overflow area, [entry - lds_cap][global lane], or null
   uint32_t ovf_lanes;  // lanes of the launch (overflow row pitch)
   float cull_sense;    // culling traces: +1 culls back faces, -1 front faces (DXR ray flags 0x10 / 0x20)
+  int hybrid;          // every BLAS's worst-case stack fits kHybridStack: packet walks may hand subtrees to
+                       // per-lane walks (lane_subtree)
 };
 
 // ------------------------------------------------------------------------------------------

@@ -3,9 +3,14 @@
 
 #include <hip/hip_runtime.h>
 
+#include "../../include/rt_api.h"
 #include "rt_device.hpp"
 
 namespace rt {
+
+// --- context accessors for the other host translation units (rt_comm.cpp) ---------------------
+int ctx_device(rt_ctx* c);
+void* ctx_stream(rt_ctx* c);
 
 // --- LBVH build (rt_lbvh.hip) ---------------------------------------------------------------
 

@@ -35,6 +35,9 @@ struct Counters {
   // record fetches (RT_STAT_*_FETCHES): per lane in the per-lane schedule; in the packet schedule
   // wave-uniform (every lane holds the wave's count, flushed once per wave)
   uint32_t nfetch = 0, tfetch = 0, ifetch = 0;
+  // record fetches of per-lane subtree walks inside the packet schedule (lane_subtree): per lane, summed
+  // over the wave at the flush and added to the node / triangle fetch slots
+  uint32_t lnfetch = 0, ltfetch = 0;
 };
 
 struct HitRec {
@@ -600,6 +603,120 @@ __device__ __forceinline__ bool packet_tlas_node(const RT_CONST char* pool, int 
   return true;
 }
 
+#ifndef RT_HYBRID_T
+#define RT_HYBRID_T 0  // packet BLAS nodes wanted by at most this many lanes go to per-lane walks (0: never)
+#endif
+#ifndef RT_HYBRID_ROOT
+#define RT_HYBRID_ROOT 0  // 1: the hand-off is considered at a BLAS's root node only (one check per instance)
+#endif
+constexpr int kHybridLanes = RT_HYBRID_T > 0 ? RT_HYBRID_T : 1;  // LDS stack columns per wave
+constexpr int kMaxPacketWaves = 2;                                // waves of a packet workgroup (packet_block)
+#if RT_HYBRID_T
+// the per-lane subtree stacks of a packet workgroup: one LDS array for every instantiation of the walk
+// (a __shared__ inside the template would be allocated once per instantiation)
+__shared__ int g_hyb[kMaxPacketWaves][kHybridStack * kHybridLanes];
+#endif
+
+// Per-lane subtree walk inside the packet schedule (north star: wavefront ballot / prefix-sum ray
+// compaction). A packet visits the union of its lanes' paths; when a BLAS node is wanted by few lanes
+// (the ballot of lanes accepting any of its children), those lanes finish that node's subtree on their
+// own: each lane takes a column of a small LDS stack by its prefix rank among them (mbcnt of the ballot:
+// conflict-free, [entry][rank]), pushes its own accepted children nearest first and walks on with vector
+// loads of the pool (the per-lane schedule's node visit: octant near / far rows, sort4, Moller-Trumbore).
+// The wave then resumes the packet walk from its own stack. Results are the packet walk's: a lane visits
+// every node and triangle of the subtree its own slab tests accept. tn: this lane's entry distances of the
+// node's children (+inf: not accepted); refs: the node's child refs (pool node index, or ~triangle slot).
+template <bool ANY_HIT, bool STATS>
+__device__ __forceinline__ void lane_subtree(const RT_GLOBAL char* pn, const RT_GLOBAL char* pt, const int32_t* refs,
+                                             const float* tn0, V3 ro, V3 rd, V3 rinvd, V3 rnoinv, float tmin,
+                                             uint32_t cur, float face, HitRec& h, int* col, Counters& cnt) {
+  float tn[4] = {tn0[0], tn0[1], tn0[2], tn0[3]};
+  int32_t r[4] = {refs[0], refs[1], refs[2], refs[3]};
+  sort4(tn, r);
+  int sp = 0;
+#pragma unroll
+  for (int k = 3; k >= 1; --k)
+    if (tn[k] != __builtin_inff()) col[(sp++) * kHybridLanes] = r[k];
+  int ref = r[0];
+  const Octant oct = octant(rinvd);
+  while (true) {
+    if (ref >= 0) {
+      // slab tests axis by axis (two rows live at a time, not the node's 28 floats: the walk runs inside
+      // the packet kernel's register budget). max / min are exact, so the regrouping gives
+      // slab4_octant's entry / exit distances up to the sign of a zero, which no comparison sees.
+      const uint32_t off = (uint32_t)ref << 7;
+      f4v tn4, tf4;
+      {
+        const f4v a = ldf4(pn, off + oct.x), b = ldf4(pn, off + (oct.x ^ 16u));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          tn4[k] = __builtin_fmaf(a[k], rinvd.x, rnoinv.x);
+          tf4[k] = __builtin_fmaf(b[k], rinvd.x, rnoinv.x);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      {
+        const f4v a = ldf4(pn, off + oct.y), b = ldf4(pn, off + (oct.y ^ 16u));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          tn4[k] = fmaxf(tn4[k], __builtin_fmaf(a[k], rinvd.y, rnoinv.y));
+          tf4[k] = fminf(tf4[k], __builtin_fmaf(b[k], rinvd.y, rnoinv.y));
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const i4v ch = ldi4(pn, off + 96u);
+      float t4[4];
+      {
+        const f4v a = ldf4(pn, off + oct.z), b = ldf4(pn, off + (oct.z ^ 16u));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float n = fmaxf(tn4[k], fmaxf(__builtin_fmaf(a[k], rinvd.z, rnoinv.z), tmin));
+          const float f = fminf(tf4[k], fminf(__builtin_fmaf(b[k], rinvd.z, rnoinv.z), h.t));
+          t4[k] = n <= f * 1.0000004f ? n : __builtin_inff();
+        }
+      }
+      int32_t c[4] = {ch.x, ch.y, ch.z, ch.w};
+      if (STATS) {
+        ++cnt.lnfetch;
+        cnt.aabb += (uint32_t)(c[0] != kEmptyChild) + (uint32_t)(c[1] != kEmptyChild) +
+                    (uint32_t)(c[2] != kEmptyChild) + (uint32_t)(c[3] != kEmptyChild);
+      }
+      sort4(t4, c);
+      if (t4[0] != __builtin_inff()) {
+#pragma unroll
+        for (int k = 3; k >= 1; --k)
+          if (t4[k] != __builtin_inff()) col[(sp++) * kHybridLanes] = c[k];
+        ref = c[0];
+        continue;
+      }
+    } else {
+      const uint32_t toff = (uint32_t)(~ref) * (uint32_t)sizeof(TriRec);
+      const f4v a = ldf4(pt, toff), b = ldf4(pt, toff + 16u), c = ldf4(pt, toff + 32u);
+      if (STATS) {
+        ++cnt.tri;
+        ++cnt.ltfetch;
+      }
+      float t, u, v;
+      if (moller_trumbore(ro, rd, v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), v3(c.x, c.y, c.z), face, t, u, v) &&
+          t >= tmin) {
+        const uint32_t prim = __float_as_uint(a.w);
+        const bool better = ANY_HIT ? (t <= h.t)
+                                    : (t < h.t || (t == h.t && (cur < h.inst || (cur == h.inst && prim < h.prim))));
+        if (better) {
+          h.t = ANY_HIT ? -__builtin_inff() : t;  // an any-hit ray leaves with t = -inf, as in the packet
+          h.u = u;
+          h.v = v;
+          h.inst = cur;
+          h.prim = prim;
+          if (ANY_HIT) return;
+        }
+      }
+    }
+    if (sp == 0) return;
+    ref = col[(--sp) * kHybridLanes];
+  }
+}
+
 // BLAS walk of the packet (instance cur, object rays ry) on the stack above `base`; returns false
 // when an any-hit packet has no live ray left. One loop iteration per node, straight-line uniform
 // control flow (no status codes between a node function and the loop). At a node: entered
@@ -615,8 +732,15 @@ template <bool ANY_HIT, bool STATS, int R, bool OCT>
 __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, const RT_CONST TriRec* tpool, int bref,
                                                  const PacketRay<R>& ry, float tmin, uint32_t cur, float face,
                                                  PacketLive<R>& pl, HitRec* hit, WaveStack& stk, int& sp, int cap,
-                                                 const NodeOct& oc, Counters& cnt) {
+                                                 const NodeOct& oc, int hybrid, Counters& cnt) {
   const int base = sp;
+#if RT_HYBRID_T
+  // the same pools for per-lane (vector) loads in lane_subtree
+  const RT_GLOBAL char* gpool = (const RT_GLOBAL char*)pool;
+  const RT_GLOBAL char* gtpool = (const RT_GLOBAL char*)tpool;
+#else
+  (void)hybrid;
+#endif
 #if RT_OCT_BASES == 1
   // one base per plane row, the octant's row offset folded in once per BLAS entry: each row load is
   // then base + the node's 32-bit offset (SGPR soffset), no per-node s_or for the row offsets
@@ -671,6 +795,28 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
     }
     uint32_t ent = packet_slabs<STATS, R, OCT>(planes, ry, tmin, pl, hit, (uint32_t)ch[4], hm, vkey, cnt);
     asm volatile("" ::"s"(ch[0]), "s"(ch[1]), "s"(ch[2]), "s"(ch[3]), "s"(ch[5]), "s"(ch[6]), "s"(ch[7]));
+#if RT_HYBRID_T
+    // few lanes want this node: they walk its subtree on their own (lane_subtree), then the packet pops
+    if (R == 1 && hybrid && (ent & (uint32_t)ch[6]) != 0u && (!RT_HYBRID_ROOT || sp == base)) {
+      const uint64_t act = (hm[0][0] | hm[0][1]) | (hm[0][2] | hm[0][3]);
+      if (__builtin_popcountll(act) <= RT_HYBRID_T) {
+        const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+        const uint32_t rank =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+        if ((act >> (threadIdx.x & 63u)) & 1ull) {
+          const float tn[4] = {__uint_as_float(vkey[0][0]), __uint_as_float(vkey[0][1]), __uint_as_float(vkey[0][2]),
+                               __uint_as_float(vkey[0][3])};
+          const int32_t refs[4] = {ch[0], ch[1], ch[2], ch[3]};
+          lane_subtree<ANY_HIT, STATS>(gpool, gtpool, refs, tn, ry.o[0], ry.d[0], ry.invd[0], ry.noinv[0], tmin, cur,
+                                       face, hit[0], &g_hyb[w][rank], cnt);
+        }
+        if (ANY_HIT && !pl.update(hit)) return false;
+        if (sp == base) return true;
+        bref = pop_entry(stk.v, sp);
+        continue;
+      }
+    }
+#endif
     const uint32_t imask = (uint32_t)ch[6];
     uint32_t tl = ent & ~imask;
     ent &= imask;
@@ -829,9 +975,10 @@ __device__ __forceinline__ void packet_walk(const SceneView& sc, const V3* o, co
       }
 #endif
       const bool more = uni ? packet_blas_walk<ANY_HIT, STATS, R, true>(pool, tpool, (int)ir.pool_root, b, tmin, cur,
-                                                                          face, pl, hit, stk, sp, cap, oc, cnt)
+                                                                          face, pl, hit, stk, sp, cap, oc, sc.hybrid, cnt)
                             : packet_blas_walk<ANY_HIT, STATS, R, false>(pool, tpool, (int)ir.pool_root, b, tmin,
-                                                                           cur, face, pl, hit, stk, sp, cap, oc, cnt);
+                                                                           cur, face, pl, hit, stk, sp, cap, oc, sc.hybrid,
+                                                                           cnt);
       if (ANY_HIT && !more) return;
     }
     if (!descend) {
@@ -1371,11 +1518,12 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
 // WAVE_FETCH: the fetch counters are wave-uniform (packet schedule) and count once per wave.
 template <bool WAVE_FETCH>
 __device__ __forceinline__ void flush_stats(const Counters& c, unsigned long long* stats) {
-  uint32_t v[10] = {c.primary, c.shadow, c.aabb, c.tri, c.inst, c.overflow, c.refl, c.nfetch, c.tfetch, c.ifetch};
-  const int slot[10] = {0, 1, 2, 3, 4, 5, 8, 9, 10, 11};
-  for (int k = 0; k < 10; ++k) {
+  uint32_t v[12] = {c.primary, c.shadow, c.aabb, c.tri, c.inst, c.overflow, c.refl, c.nfetch, c.tfetch, c.ifetch,
+                    c.lnfetch, c.ltfetch};
+  const int slot[12] = {0, 1, 2, 3, 4, 5, 8, 9, 10, 11, 9, 10};
+  for (int k = 0; k < 12; ++k) {
     unsigned long long x = v[k];
-    if (!WAVE_FETCH || k < 7)
+    if (!WAVE_FETCH || k < 7 || k >= 10)
       for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, 64);
     if ((threadIdx.x & 63) == 0 && x) atomicAdd(stats + slot[k], x);
   }
@@ -1462,6 +1610,8 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void k_trace_frame(SceneView 
 __host__ __device__ constexpr int packet_wx(int ks) { return ks > 1 ? RT_PACKET_WX_MS : RT_PACKET_WX; }
 __host__ __device__ constexpr int packet_wy(int ks) { return ks > 1 ? 1 : RT_PACKET_WY; }
 __host__ __device__ constexpr int packet_block(int ks) { return 64 * packet_wx(ks) * packet_wy(ks); }
+static_assert(packet_block(1) <= 64 * kMaxPacketWaves && packet_block(2) <= 64 * kMaxPacketWaves,
+              "lane_subtree's LDS stacks: one per wave of a packet workgroup");
 
 template <int MODE, bool STATS, int R, int KS>
 __global__ __launch_bounds__(packet_block(KS)) __attribute__((amdgpu_waves_per_eu(

@@ -659,8 +659,11 @@ def test_invalid_arguments_raise():
 # the C++ host mirror (nv_helpers_hip.hpp) end to end: rt_app == oracle
 # ------------------------------------------------------------------------------------------
 
-@pytest.mark.parametrize("scene,cfg,mode,lights", [("ref", "REF", "ref", 6), ("grid8", "C4", "lambert_shadow", 2)])
-def test_cpp_host_app_matches_oracle(tmp_path, scene, cfg, mode, lights):
+@pytest.mark.parametrize("scene,cfg,mode,lights,ranks", [("ref", "REF", "ref", 6, 0), ("grid8", "C4", "lambert_shadow", 2, 0),
+                                                         ("ref", "REF", "ref", 6, 1), ("grid8", "C4", "lambert_shadow", 2, 1)])
+def test_cpp_host_app_matches_oracle(tmp_path, scene, cfg, mode, lights, ranks):
+    """rt_app (the reference application over nv_helpers_hip.hpp) == oracle; with --ranks 1 every frame goes
+    through the C-ABI's tiled-frame loop (rt_render_strips over a world-1 RCCL communicator)."""
     import gzip
     import os
     import subprocess
@@ -672,6 +675,8 @@ def test_cpp_host_app_matches_oracle(tmp_path, scene, cfg, mode, lights):
     cmd = [os.path.join(os.path.dirname(rt.LIB_PATH), "rt_app"), "--model", str(model), "--scene", scene,
            "--mode", mode, "--lights", str(lights), "--width", "160", "--height", "90", "--frames", "2",
            "--raw", str(raw), "--eye", *map(str, eye), "--center", *map(str, center)]
+    if ranks:
+        cmd += ["--ranks", str(ranks), "--rank", "0"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     img = np.frombuffer(raw.read_bytes(), np.uint8).reshape(90, 160, 4)
