@@ -157,7 +157,15 @@ class HipBackend:
             self.ctx.tlas_build([(m, x, iid, hg) for (m, x, iid, hg) in spec.instances])
             tlas_w.append(self.ctx.tlas_info().build_ms)
         med = lambda xs: round(sorted(xs)[len(xs) // 2], 4)  # noqa: E731
-        return first + ([med(x) for x in blas_w], med(tlas_w))
+        # per-frame TLAS update (TopLevelASGenerator.cpp:202-222 from OnUpdate, D3D12HelloTriangle.cpp:421-433):
+        # the host wall time of rt_tlas_build(update_only) (double-buffered, no device-wide sync) and its kernels
+        upd_wall, upd_dev = [], []
+        inst = [(m, x, iid, hg) for (m, x, iid, hg) in spec.instances]
+        for _ in range(10):
+            self.ctx.tlas_build(inst, update_only=True)
+            upd_wall.append(self.ctx.tlas_build_wall_ms())
+            upd_dev.append(self.ctx.tlas_info().build_ms)
+        return first + ([med(x) for x in blas_w], med(tlas_w), med(upd_wall), med(upd_dev))
 
     def zeros(self, shape):
         return torch.zeros(shape, dtype=torch.uint8, device=self.device)
@@ -724,7 +732,8 @@ def main(argv=None) -> int:
                        "settle_ms": a.settle_ms},
             "roofline": rf,
             "cpu_baseline": cpu,
-            "build_ms": dict(zip(("blas", "tlas", "blas_warm", "tlas_warm"), r["build"])),
+            "build_ms": dict(zip(("blas", "tlas", "blas_warm", "tlas_warm", "tlas_update_wall", "tlas_update_kernel"),
+                                 r["build"])),
             "extra": extra,
         }
         print(json.dumps(out), flush=True)

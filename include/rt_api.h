@@ -159,9 +159,15 @@ rt_status rt_blas_export(rt_ctx_t ctx, rt_blas_t blas, void* nodes, size_t nodes
  * UpdateInstancePropertiesBuffer (D3D12HelloTriangle.cpp:1181-1204): the per-instance normal
  * matrix transpose(inverse(upper3x3)) is derived here. update_only != 0 refits the existing TLAS
  * (same instance count and BLAS ids; new transforms), as TopLevelASGenerator.cpp:202-222.
- * Synchronous. */
+ * Double-buffered: launches already issued keep reading the previous version while this one is built into
+ * the other (a per-frame update with frames in flight); the build waits on the device for the launches of
+ * the version it overwrites, launches issued after it wait for it on the device, and the host returns once
+ * this build's own kernels finished (the tree's size and stack bound come back). Only a changed layout (a
+ * BLAS built or rebuilt since, or more instances than ever before) waits for all in-flight work. */
 rt_status rt_tlas_build(rt_ctx_t ctx, const rt_instance* instances, uint32_t n, int update_only);
 rt_status rt_tlas_info(rt_ctx_t ctx, rt_bvh_info* out);
+/* Host wall time of the last rt_tlas_build call (ms), beside rt_bvh_info.build_ms (its kernels' device time). */
+double rt_tlas_build_wall_ms(rt_ctx_t ctx);
 /* nodes: node_count x 128 B 4-wide nodes; leaf refs are ~instance_index. */
 rt_status rt_tlas_export(rt_ctx_t ctx, void* nodes, size_t nodes_bytes);
 

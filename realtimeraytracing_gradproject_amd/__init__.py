@@ -93,6 +93,7 @@ SIGNATURES = [
     ("rt_blas_export", _I, [_P, _U32, _P, ctypes.c_size_t, _P, ctypes.c_size_t]),
     ("rt_tlas_build", _I, [_P, ctypes.POINTER(rt_instance), _U32, _I]),
     ("rt_tlas_info", _I, [_P, ctypes.POINTER(rt_bvh_info)]),
+    ("rt_tlas_build_wall_ms", ctypes.c_double, [_P]),
     ("rt_tlas_export", _I, [_P, _P, ctypes.c_size_t]),
     ("rt_set_camera", _I, [_P, _FP]),
     ("rt_set_shading", _I, [_P, ctypes.POINTER(rt_light), _U32, ctypes.POINTER(rt_material), _I, _I]),
@@ -534,6 +535,10 @@ class Context:
         info = rt_bvh_info()
         self._check(self._lib.rt_tlas_info(self._h, ctypes.byref(info)), "rt_tlas_info")
         return info
+
+    def tlas_build_wall_ms(self) -> float:
+        """Host wall time of the last tlas_build (ms)."""
+        return float(self._lib.rt_tlas_build_wall_ms(self._h))
 
     def tlas_export(self) -> np.ndarray:
         info = self.tlas_info()

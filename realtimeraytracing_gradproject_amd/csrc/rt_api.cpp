@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -131,6 +132,35 @@ void slot_release(ScratchSlot& sl) {
   sl = ScratchSlot();
 }
 
+// One TLAS version: device instance records, the raw TLAS (export), its slot in the scene pool, pinned
+// upload staging, and the uses of the version by launches (a ScratchSlot's per-stream events).
+struct TlasVersion {
+  rt::Bvh4Node* nodes = nullptr;  // as built (child refs local to the TLAS), for rt_tlas_export
+  rt::InstanceRec* inst = nullptr;
+  uint32_t* sorted = nullptr;
+  uint32_t cap = 0;               // instances the arrays hold
+  uint32_t ninst = 0, nodes_n = 0, depth = 0, max_stack = 0;
+  float bounds[6] = {0, 0, 0, 0, 0, 0};
+  double ms = 0.0;
+  uint32_t pool_base = 0;         // this version's TLAS root in the scene pool
+  bool valid = false;             // built against the current pool layout
+  std::vector<rt_instance> host;  // the instances as given
+  rt::InstanceRec* staging = nullptr;  // pinned upload staging (records, then BLAS boxes)
+  size_t staging_bytes = 0;
+  ScratchSlot use;                // launches that read this version
+  hipEvent_t ready = nullptr;     // recorded on the context stream when the version's pool slot is written
+  bool ready_pending = false;     // launches on other streams still wait for `ready`
+  void release() {
+    if (nodes) (void)hipFree(nodes);
+    if (inst) (void)hipFree(inst);
+    if (sorted) (void)hipFree(sorted);
+    if (staging) (void)hipHostFree(staging);
+    if (ready) (void)hipEventDestroy(ready);
+    slot_release(use);
+    *this = TlasVersion();
+  }
+};
+
 }  // namespace
 
 struct rt_ctx {
@@ -138,14 +168,21 @@ struct rt_ctx {
   hipStream_t stream = nullptr;
   std::string err;
   std::vector<DeviceBlas> blas;
-  // TLAS
-  rt::Bvh4Node* tlas_nodes = nullptr;
-  rt::InstanceRec* inst = nullptr;
-  uint32_t* tlas_sorted = nullptr;
-  uint32_t ninst = 0, tlas_nodes_n = 0, tlas_depth = 0, tlas_max_stack = 0;
-  float tlas_bounds[6] = {0, 0, 0, 0, 0, 0};
-  double tlas_ms = 0.0;
-  std::vector<rt_instance> inst_host;
+  // TLAS: two versions (double buffering, as the reference's per-frame update of the instance buffer
+  // behind its fences, D3D12HelloTriangle.cpp:421-433 / TopLevelASGenerator.cpp:202-222). Frames in flight
+  // read version `cur` while an update writes the other one; a version is rewritten only after the launches
+  // that read it (events per stream, ordered on the device).
+  TlasVersion ver[2];
+  int cur = -1;                  // the version launches read (-1: no TLAS)
+  uint64_t blas_gen = 0;         // bumped by every BLAS build / rebuild
+  uint64_t pool_gen = ~0ull;     // blas_gen the pool's BLAS part was laid out for
+  uint32_t pool_tlas_cap = 0;    // nodes of each version's TLAS slot in the pool
+  std::vector<uint32_t> node_base, tri_base;  // BLAS k's first node / triangle in the pools
+  rt::BuildArena tlas_arena;     // lbvh_build scratch of the TLAS builds (kept: no hipMalloc per update)
+  float* d_tlas_bb = nullptr;    // instance BLAS boxes / world boxes (scratch, grown on demand)
+  float* d_tlas_box = nullptr;
+  uint32_t tlas_scratch_cap = 0;
+  double tlas_wall_ms = 0.0;     // host wall time of the last rt_tlas_build
   // frame state
   rt::FrameParams fp{};
   bool have_camera = false, have_shading = false;
@@ -386,9 +423,10 @@ rt_status rt_destroy(rt_ctx_t c) {
   (void)hipSetDevice(c->device);
   (void)quiesce(c);  // launches on caller streams may still read the context's buffers
   for (auto& b : c->blas) b.release();
-  if (c->tlas_nodes) (void)hipFree(c->tlas_nodes);
-  if (c->inst) (void)hipFree(c->inst);
-  if (c->tlas_sorted) (void)hipFree(c->tlas_sorted);
+  for (auto& v : c->ver) v.release();
+  c->tlas_arena.release();
+  if (c->d_tlas_bb) (void)hipFree(c->d_tlas_bb);
+  if (c->d_tlas_box) (void)hipFree(c->d_tlas_box);
   if (c->d_stats) (void)hipFree(c->d_stats);
   for (auto& sl : c->rows.slots) slot_release(sl);
   for (auto& sl : c->ovf.slots) slot_release(sl);
@@ -415,6 +453,7 @@ rt_status rt_blas_build(rt_ctx_t c, const void* vtx, uint32_t vcount, uint32_t s
     return st;
   }
   c->blas.push_back(b);
+  ++c->blas_gen;
   *out = (rt_blas_t)(c->blas.size() - 1);
   return RT_OK;
 }
@@ -432,7 +471,8 @@ rt_status rt_blas_rebuild(rt_ctx_t c, rt_blas_t id, const void* vtx, uint32_t vc
   }
   c->blas[id].release();
   c->blas[id] = b;
-  c->tlas_stale = c->inst != nullptr;  // the scene pool holds the old tree until rt_tlas_build
+  ++c->blas_gen;
+  c->tlas_stale = c->cur >= 0;  // the scene pool holds the old tree until rt_tlas_build
   return RT_OK;
 }
 
@@ -470,27 +510,17 @@ rt_status rt_blas_export(rt_ctx_t c, rt_blas_t id, void* nodes, size_t nodes_byt
 
 rt_status rt_tlas_build(rt_ctx_t c, const rt_instance* in, uint32_t n, int update_only) {
   if (!c || !in || n == 0) return fail(c, RT_E_INVALID, "rt_tlas_build: need at least one instance");
+  const auto t_start = std::chrono::steady_clock::now();
   (void)hipSetDevice(c->device);
   if (update_only) {
-    if (!c->inst || n != c->ninst) return fail(c, RT_E_INVALID, "rt_tlas_build: update needs the same instance count");
+    const TlasVersion* cv = c->cur >= 0 ? &c->ver[c->cur] : nullptr;
+    if (!cv || c->tlas_stale || n != cv->ninst)
+      return fail(c, RT_E_INVALID, "rt_tlas_build: update needs the same instance count");
     for (uint32_t i = 0; i < n; ++i)
-      if (in[i].blas != c->inst_host[i].blas) return fail(c, RT_E_INVALID, "rt_tlas_build: update cannot change BLAS");
+      if (in[i].blas != cv->host[i].blas) return fail(c, RT_E_INVALID, "rt_tlas_build: update cannot change BLAS");
   }
   std::vector<rt::InstanceRec> recs(n);
   std::vector<float> bb((size_t)n * 6);
-  // scene pool layout: [TLAS (room for max(n-1,1) nodes) | BLAS 0 | BLAS 1 | ...], triangles
-  // [BLAS 0 | BLAS 1 | ...]
-  const uint32_t tlas_cap = n > 1 ? n - 1 : 1;
-  std::vector<uint32_t> node_base(c->blas.size()), tri_base(c->blas.size());
-  size_t pool_n = tlas_cap, pool_t = 0;
-  for (size_t k = 0; k < c->blas.size(); ++k) {
-    node_base[k] = (uint32_t)pool_n;
-    tri_base[k] = (uint32_t)pool_t;
-    pool_n += c->blas[k].nnodes;
-    pool_t += c->blas[k].ntri;
-  }
-  if (pool_n > 0x7fffffffull / sizeof(rt::Bvh4Node) || pool_t > 0x7fffffffull / sizeof(rt::TriRec))
-    return fail(c, RT_E_UNSUPPORTED, "rt_tlas_build: scene pool exceeds 2 GB of nodes or triangles");
   for (uint32_t i = 0; i < n; ++i) {
     if (in[i].blas >= c->blas.size()) return fail(c, RT_E_INVALID, "rt_tlas_build: unknown BLAS id");
     if (in[i].hit_group != RT_HITGROUP_MODEL && in[i].hit_group != RT_HITGROUP_PLANE)
@@ -506,100 +536,159 @@ rt_status rt_tlas_build(rt_ctx_t c, const rt_instance* in, uint32_t n, int updat
     r.tris = b.tris;
     r.vtx = b.vtx;
     r.idx = b.idx;
-    r.pool_root = node_base[in[i].blas];
     for (int k = 0; k < 6; ++k) bb[i * 6 + k] = b.bounds[k];
   }
+  const uint32_t tlas_cap = n > 1 ? n - 1 : 1;
   hipStream_t s = c->stream;
-  // every buffer below is overwritten in place or freed: no frame on any stream may still read it
-  HIPCHK(c, quiesce(c), "rt_tlas_build: wait for in-flight work");
-  // until this build completes, the scene must not be traced (a failure below leaves it stale;
-  // rt_dispatch_rays / rt_trace_rays refuse a stale scene instead of walking half-built pools)
-  c->tlas_stale = true;
-  if (!update_only || !c->inst) {
-    c->ninst = 0;  // an update needs a completed build of the same instance count
-    if (c->tlas_nodes) (void)hipFree(c->tlas_nodes);
-    if (c->inst) (void)hipFree(c->inst);
-    if (c->tlas_sorted) (void)hipFree(c->tlas_sorted);
-    c->tlas_nodes = nullptr;
-    c->inst = nullptr;
-    c->tlas_sorted = nullptr;
-    const uint32_t nn = n > 1 ? n - 1 : 1;
-    HIPCHK(c, hipMalloc(&c->tlas_nodes, (size_t)nn * sizeof(rt::Bvh4Node)), "hipMalloc(tlas)");
-    HIPCHK(c, hipMalloc(&c->inst, (size_t)n * sizeof(rt::InstanceRec)), "hipMalloc(instances)");
-    HIPCHK(c, hipMalloc(&c->tlas_sorted, (size_t)n * 4), "hipMalloc(tlas order)");
+  // Fast path (a per-frame update): the pool's BLAS part is current and each version's arrays and pool slot
+  // hold n instances. The version launches do not read is written after ITS last launches (device-side waits),
+  // with scratch kept from earlier builds: no device-wide synchronisation, no allocation. The host waits for
+  // this build alone (the tree's node count and stack bound come back to size the next launches).
+  const bool fast = c->pool_gen == c->blas_gen && c->pool_tlas_cap >= tlas_cap && c->ver[0].cap >= n &&
+                    c->ver[1].cap >= n && c->tlas_scratch_cap >= n;
+  if (!fast) {
+    // layout change (BLAS built or rebuilt, more instances): every launch that may read the pools or the
+    // instance records finishes first, as the reference waits on its fence before rebuilding (:1482-1568)
+    HIPCHK(c, quiesce(c), "rt_tlas_build: wait for in-flight work");
+    c->tlas_stale = true;  // until this build completes (a failure below leaves the scene unusable)
+    c->cur = -1;
+    size_t pool_n = 0, pool_t = 0;
+    c->node_base.assign(c->blas.size(), 0);
+    c->tri_base.assign(c->blas.size(), 0);
+    for (size_t k = 0; k < c->blas.size(); ++k) {
+      c->node_base[k] = (uint32_t)pool_n;
+      c->tri_base[k] = (uint32_t)pool_t;
+      pool_n += c->blas[k].nnodes;
+      pool_t += c->blas[k].ntri;
+    }
+    const uint32_t slot_cap = std::max(tlas_cap, c->pool_tlas_cap);
+    const size_t tlas0 = pool_n;
+    pool_n += 2 * (size_t)slot_cap;
+    if (pool_n > 0x7fffffffull / sizeof(rt::Bvh4Node) || pool_t > 0x7fffffffull / sizeof(rt::TriRec))
+      return fail(c, RT_E_UNSUPPORTED, "rt_tlas_build: scene pool exceeds 2 GB of nodes or triangles");
+    if (pool_n > c->pool_nodes_cap) {
+      if (c->pool_nodes) (void)hipFree(c->pool_nodes);
+      c->pool_nodes = nullptr;
+      c->pool_nodes_cap = 0;
+      HIPCHK(c, hipMalloc(&c->pool_nodes, pool_n * sizeof(rt::Bvh4Node)), "hipMalloc(node pool)");
+      c->pool_nodes_cap = pool_n;
+    }
+    if (pool_t > c->pool_tris_cap) {
+      if (c->pool_tris) (void)hipFree(c->pool_tris);
+      c->pool_tris = nullptr;
+      c->pool_tris_cap = 0;
+      HIPCHK(c, hipMalloc(&c->pool_tris, pool_t * sizeof(rt::TriRec)), "hipMalloc(triangle pool)");
+      c->pool_tris_cap = pool_t;
+    }
+    hipError_t e = hipSuccess;
+    for (size_t k = 0; k < c->blas.size() && e == hipSuccess; ++k) {  // the BLAS part: once per layout
+      const DeviceBlas& b = c->blas[k];
+      e = rt::pool_rebase(b.nodes, b.nnodes, c->node_base[k], c->tri_base[k], c->pool_nodes + c->node_base[k], s);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(c->pool_tris + c->tri_base[k], b.tris, (size_t)b.ntri * sizeof(rt::TriRec),
+                           hipMemcpyDeviceToDevice, s);
+    }
+    if (e != hipSuccess) return hip_fail(c, e, "scene pool");
+    for (int v = 0; v < 2; ++v) {
+      TlasVersion& tv = c->ver[v];
+      tv.valid = false;
+      tv.pool_base = (uint32_t)(tlas0 + (size_t)v * slot_cap);
+      if (tv.cap < n) {
+        if (tv.nodes) (void)hipFree(tv.nodes);
+        if (tv.inst) (void)hipFree(tv.inst);
+        if (tv.sorted) (void)hipFree(tv.sorted);
+        if (tv.staging) (void)hipHostFree(tv.staging);
+        tv.nodes = nullptr;
+        tv.inst = nullptr;
+        tv.sorted = nullptr;
+        tv.staging = nullptr;
+        tv.cap = 0;
+        HIPCHK(c, hipMalloc(&tv.nodes, (size_t)tlas_cap * sizeof(rt::Bvh4Node)), "hipMalloc(tlas)");
+        HIPCHK(c, hipMalloc(&tv.inst, (size_t)n * sizeof(rt::InstanceRec)), "hipMalloc(instances)");
+        HIPCHK(c, hipMalloc(&tv.sorted, (size_t)n * 4), "hipMalloc(tlas order)");
+        tv.staging_bytes = (size_t)n * sizeof(rt::InstanceRec) + (size_t)n * 24;
+        HIPCHK(c, hipHostMalloc((void**)&tv.staging, tv.staging_bytes, hipHostMallocDefault), "hipHostMalloc(tlas staging)");
+        tv.cap = n;
+      }
+      if (!tv.ready && !(tv.ready = new_sync_event())) return fail(c, RT_E_HIP, "rt_tlas_build: event");
+    }
+    if (c->tlas_scratch_cap < n) {
+      if (c->d_tlas_bb) (void)hipFree(c->d_tlas_bb);
+      if (c->d_tlas_box) (void)hipFree(c->d_tlas_box);
+      c->d_tlas_bb = c->d_tlas_box = nullptr;
+      c->tlas_scratch_cap = 0;
+      HIPCHK(c, hipMalloc(&c->d_tlas_bb, (size_t)n * 24), "hipMalloc(tlas scratch)");
+      HIPCHK(c, hipMalloc(&c->d_tlas_box, (size_t)n * 24), "hipMalloc(tlas scratch)");
+      c->tlas_scratch_cap = n;
+    }
+    c->pool_tlas_cap = slot_cap;
+    c->pool_gen = c->blas_gen;
   }
-  float* d_bb = nullptr;
-  float* d_box = nullptr;
-  auto free_fn = [&] {
-    if (d_bb) (void)hipFree(d_bb);
-    if (d_box) (void)hipFree(d_box);
-  };
-  ScopeExit<decltype(free_fn)> scratch(free_fn);
-  HIPCHK(c, hipMalloc(&d_bb, bb.size() * 4), "hipMalloc(scratch)");
-  HIPCHK(c, hipMalloc(&d_box, bb.size() * 4), "hipMalloc(scratch)");
-  hipError_t e = hipMemcpyAsync(c->inst, recs.data(), recs.size() * sizeof(rt::InstanceRec), hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(d_bb, bb.data(), bb.size() * 4, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = rt::tlas_prepare(c->inst, d_bb, n, d_box, s);
+  // the version launches do not read now
+  const int w = c->cur >= 0 ? 1 - c->cur : 0;
+  TlasVersion& tv = c->ver[w];
+  for (uint32_t i = 0; i < n; ++i) recs[i].pool_root = c->node_base[recs[i].blas];
+  // its previous readers on other streams finish before the upload overwrites it (device-side waits)
+  HIPCHK(c, slot_order_after_others(tv.use, s), "rt_tlas_build: order after the version's launches");
+  std::memcpy(tv.staging, recs.data(), recs.size() * sizeof(rt::InstanceRec));  // staging idle: its last build synced
+  float* bb_stage = (float*)((char*)tv.staging + (size_t)n * sizeof(rt::InstanceRec));
+  std::memcpy(bb_stage, bb.data(), bb.size() * 4);
+  hipError_t e = hipMemcpyAsync(tv.inst, tv.staging, recs.size() * sizeof(rt::InstanceRec), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(c->d_tlas_bb, bb_stage, bb.size() * 4, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = rt::tlas_prepare(tv.inst, c->d_tlas_bb, n, c->d_tlas_box, s);
   float ms = 0.0f;
-  // update_only rebuilds the hierarchy over the new boxes: an LBVH rebuild costs the same
-  // launches as a refit at these sizes and keeps the tree identical to a fresh build.
+  uint32_t nn = 0, depth = 0, mstack = 0;
+  float bounds[6];
+  // update_only rebuilds the hierarchy over the new boxes: an LBVH rebuild costs the same launches as a
+  // refit at these sizes and keeps the tree identical to a fresh build
   if (e == hipSuccess)
-    e = rt::lbvh_build(d_box, n, c->tlas_nodes, c->tlas_sorted, true, &c->tlas_nodes_n, &c->tlas_depth, &c->tlas_max_stack,
-                       c->tlas_bounds, &ms, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (e != hipSuccess) return hip_fail(c, e, "TLAS build");
-  // scene pools (rebased copies; the per-BLAS arrays stay for export and rebuilds)
-  if (pool_n > c->pool_nodes_cap) {
-    if (c->pool_nodes) (void)hipFree(c->pool_nodes);
-    c->pool_nodes = nullptr;
-    c->pool_nodes_cap = 0;
-    HIPCHK(c, hipMalloc(&c->pool_nodes, pool_n * sizeof(rt::Bvh4Node)), "hipMalloc(node pool)");
-    c->pool_nodes_cap = pool_n;
+    e = rt::lbvh_build(c->d_tlas_box, n, tv.nodes, tv.sorted, true, &nn, &depth, &mstack, bounds, &ms, s, nullptr,
+                       nullptr, &c->tlas_arena);
+  if (e == hipSuccess) e = rt::pool_rebase(tv.nodes, nn, tv.pool_base, -1, c->pool_nodes + tv.pool_base, s);
+  if (e == hipSuccess) e = hipEventRecord(tv.ready, s);
+  if (e != hipSuccess) {
+    tv.valid = false;
+    return hip_fail(c, e, "TLAS build");
   }
-  if (pool_t > c->pool_tris_cap) {
-    if (c->pool_tris) (void)hipFree(c->pool_tris);
-    c->pool_tris = nullptr;
-    c->pool_tris_cap = 0;
-    HIPCHK(c, hipMalloc(&c->pool_tris, pool_t * sizeof(rt::TriRec)), "hipMalloc(triangle pool)");
-    c->pool_tris_cap = pool_t;
-  }
-  e = rt::pool_rebase(c->tlas_nodes, c->tlas_nodes_n, 0, -1, c->pool_nodes, s);
-  for (size_t k = 0; k < c->blas.size() && e == hipSuccess; ++k) {
-    const DeviceBlas& b = c->blas[k];
-    e = rt::pool_rebase(b.nodes, b.nnodes, node_base[k], tri_base[k], c->pool_nodes + node_base[k], s);
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(c->pool_tris + tri_base[k], b.tris, (size_t)b.ntri * sizeof(rt::TriRec),
-                         hipMemcpyDeviceToDevice, s);
-  }
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (e != hipSuccess) return hip_fail(c, e, "scene pool");
+  tv.ready_pending = true;
+  tv.ninst = n;
+  tv.nodes_n = nn;
+  tv.depth = depth;
+  tv.max_stack = mstack;
+  std::memcpy(tv.bounds, bounds, sizeof(bounds));
+  tv.ms = ms;
+  tv.host.assign(in, in + n);
+  tv.valid = true;
+  c->cur = w;
   c->tlas_stale = false;
-  c->ninst = n;
-  c->tlas_ms = ms;
-  c->inst_host.assign(in, in + n);
+  c->tlas_wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
   return RT_OK;
 }
 
 rt_status rt_tlas_info(rt_ctx_t c, rt_bvh_info* out) {
-  if (!c || !out || !c->inst) return fail(c, RT_E_INVALID, "rt_tlas_info: no TLAS");
-  out->prim_count = c->ninst;
-  out->node_count = c->tlas_nodes_n;
-  out->depth = c->tlas_depth;
-  out->max_stack = c->tlas_max_stack;
+  if (!c || !out || c->cur < 0) return fail(c, RT_E_INVALID, "rt_tlas_info: no TLAS");
+  const TlasVersion& v = c->ver[c->cur];
+  out->prim_count = v.ninst;
+  out->node_count = v.nodes_n;
+  out->depth = v.depth;
+  out->max_stack = v.max_stack;
   for (int k = 0; k < 3; ++k) {
-    out->bounds_lo[k] = c->tlas_bounds[k];
-    out->bounds_hi[k] = c->tlas_bounds[3 + k];
+    out->bounds_lo[k] = v.bounds[k];
+    out->bounds_hi[k] = v.bounds[3 + k];
   }
-  out->build_ms = c->tlas_ms;
+  out->build_ms = v.ms;
   return RT_OK;
 }
 
+double rt_tlas_build_wall_ms(rt_ctx_t c) { return c ? c->tlas_wall_ms : 0.0; }
+
 rt_status rt_tlas_export(rt_ctx_t c, void* nodes, size_t nodes_bytes) {
-  if (!c || !nodes || !c->inst) return fail(c, RT_E_INVALID, "rt_tlas_export: no TLAS");
-  const size_t bytes = (size_t)c->tlas_nodes_n * sizeof(rt::Bvh4Node);
+  if (!c || !nodes || c->cur < 0) return fail(c, RT_E_INVALID, "rt_tlas_export: no TLAS");
+  const TlasVersion& v = c->ver[c->cur];
+  const size_t bytes = (size_t)v.nodes_n * sizeof(rt::Bvh4Node);
   if (nodes_bytes < bytes) return fail(c, RT_E_INVALID, "rt_tlas_export: buffer too small");
   (void)hipSetDevice(c->device);
-  HIPCHK(c, hipMemcpy(nodes, c->tlas_nodes, bytes, hipMemcpyDeviceToHost), "export tlas");
+  HIPCHK(c, hipMemcpy(nodes, v.nodes, bytes, hipMemcpyDeviceToHost), "export tlas");
   return RT_OK;
 }
 
@@ -656,25 +745,39 @@ rt_status rt_set_stats(rt_ctx_t c, int enable) {
 
 static rt::SceneView scene_view(rt_ctx* c) {
   rt::SceneView sv;
+  const TlasVersion& v = c->ver[c->cur];
   sv.pool_nodes = c->pool_nodes;
   sv.pool_tris = c->pool_tris;
-  sv.tlas = c->tlas_nodes;
-  sv.inst = c->inst;
+  sv.tlas = v.nodes;
+  sv.inst = v.inst;
+  sv.tlas_root = (int)v.pool_base;
   uint32_t maxb = 0, maxd = 0;
   for (const auto& b : c->blas) {
     maxb = b.max_stack > maxb ? b.max_stack : maxb;
     maxd = b.depth > maxd ? b.depth : maxd;
   }
   // worst case: the TLAS path's siblings, the TLAS->BLAS sentinel, the BLAS path's siblings
-  sv.stack_cap = (int)(c->tlas_max_stack + 1 + maxb);
+  sv.stack_cap = (int)(v.max_stack + 1 + maxb);
   // wave packets: the TLAS path's siblings, then at most one entry per BLAS level
-  sv.packet_cap = (int)(c->tlas_max_stack + maxd);
+  sv.packet_cap = (int)(v.max_stack + maxd);
   sv.lds_cap = sv.stack_cap < rt::kLdsStackEntries ? sv.stack_cap : rt::kLdsStackEntries;
   sv.ovf = nullptr;
   sv.ovf_lanes = 0;
   sv.cull_sense = 1.0f;
   sv.hybrid = maxb <= (uint32_t)rt::kHybridStack ? 1 : 0;
   return sv;
+}
+
+// A launch on s reads the current TLAS version: it waits (on the device) for that version's build, enqueued
+// on the context stream, unless s is that stream or the build is seen complete.
+static hipError_t order_after_tlas(rt_ctx* c, hipStream_t s) {
+  TlasVersion& v = c->ver[c->cur];
+  if (!v.ready_pending || s == c->stream) return hipSuccess;
+  if (hipEventQuery(v.ready) == hipSuccess) {
+    v.ready_pending = false;
+    return hipSuccess;
+  }
+  return hipStreamWaitEvent(s, v.ready, 0);
 }
 
 // Picks the ring slot a launch on s uses (see ScratchRing). `match` (row lists): a slot holding
@@ -898,7 +1001,7 @@ rt_status rt_raster_draw(rt_ctx_t c, const rt_blas_t* draws, uint32_t ndraws, co
 rt_status rt_dispatch_rays(rt_ctx_t c, uint32_t W, uint32_t H, const uint32_t* rows, uint32_t nrows,
                            void* rgba8, float* rgba32f, void* stream) {
   if (!c) return RT_E_INVALID;
-  if (!c->inst) return fail(c, RT_E_INVALID, "rt_dispatch_rays: no TLAS built");
+  if (c->cur < 0 && !c->tlas_stale) return fail(c, RT_E_INVALID, "rt_dispatch_rays: no TLAS built");
   if (c->tlas_stale)
     return fail(c, RT_E_INVALID, "rt_dispatch_rays: scene stale (BLAS rebuilt, or the last rt_tlas_build failed)");
   if (!c->have_camera || !c->have_shading) return fail(c, RT_E_INVALID, "rt_dispatch_rays: camera/shading not set");
@@ -928,9 +1031,11 @@ rt_status rt_dispatch_rays(rt_ctx_t c, uint32_t W, uint32_t H, const uint32_t* r
     if (st == RT_OK && rows) st = ensure_rows(c, rows, nrows, s, &rows_slot, &d_rows);
     if (st != RT_OK) return st;
   }
+  HIPCHK(c, order_after_tlas(c, s), "rt_dispatch_rays: order after the TLAS build");
   hipError_t e = rt::launch_trace_frame(sv, c->fp, d_rows, rgba8, rgba32f, c->d_stats, c->stats_on,
                                         c->schedule, s);
   if (e != hipSuccess) return hip_fail(c, e, "trace launch");
+  HIPCHK(c, slot_mark_use(c->ver[c->cur].use, s), "rt_dispatch_rays: record use");
   if (ovf_slot) HIPCHK(c, slot_mark_use(*ovf_slot, s), "overflow stack: record use");
   if (rows_slot) HIPCHK(c, slot_mark_use(*rows_slot, s), "rows: record use");
   if (c->stats_on) {
@@ -949,7 +1054,7 @@ rt_status rt_trace_rays(rt_ctx_t c, const float* rays, uint32_t n, uint32_t ray_
   const bool cull_back = (ray_flags & RT_RAY_FLAG_CULL_BACK_FACING_TRIANGLES) != 0;
   const bool cull_front = (ray_flags & RT_RAY_FLAG_CULL_FRONT_FACING_TRIANGLES) != 0;
   if (cull_back && cull_front) return fail(c, RT_E_INVALID, "rt_trace_rays: both cull flags set");
-  if (!c->inst) return fail(c, RT_E_INVALID, "rt_trace_rays: no TLAS built");
+  if (c->cur < 0 && !c->tlas_stale) return fail(c, RT_E_INVALID, "rt_trace_rays: no TLAS built");
   if (c->tlas_stale)
     return fail(c, RT_E_INVALID, "rt_trace_rays: scene stale (BLAS rebuilt, or the last rt_tlas_build failed)");
   (void)hipSetDevice(c->device);
@@ -964,9 +1069,11 @@ rt_status rt_trace_rays(rt_ctx_t c, const float* rays, uint32_t n, uint32_t ray_
     rt_status st = ensure_overflow(c, sv, (size_t)((n + 255) / 256) * 256, s, &ovf_slot);
     if (st != RT_OK) return st;
   }
+  HIPCHK(c, order_after_tlas(c, s), "rt_trace_rays: order after the TLAS build");
   hipError_t e = rt::launch_trace_rays(sv, rays, n, (ray_flags & RT_RAY_FLAG_ACCEPT_FIRST_HIT_AND_END_SEARCH) != 0,
                                        cull_back || cull_front, hits, uv, c->d_stats, c->stats_on, s);
   if (e != hipSuccess) return hip_fail(c, e, "trace_rays launch");
+  HIPCHK(c, slot_mark_use(c->ver[c->cur].use, s), "rt_trace_rays: record use");
   if (ovf_slot) HIPCHK(c, slot_mark_use(*ovf_slot, s), "overflow stack: record use");
   return RT_OK;
 }
@@ -1034,7 +1141,11 @@ rt_status rt_stats(rt_ctx_t c, uint64_t out[RT_STAT_COUNT]) {
 rt_status rt_stats_reset(rt_ctx_t c) {
   if (!c) return RT_E_INVALID;
   (void)hipSetDevice(c->device);
+  // hipMemset runs on the null stream, which the context's non-blocking stream does not wait for: drain the
+  // device, clear, and drain again, so no counting launch before or after can straddle the reset
+  HIPCHK(c, hipDeviceSynchronize(), "stats reset");
   HIPCHK(c, hipMemset(c->d_stats, 0, RT_STAT_COUNT * sizeof(unsigned long long)), "stats reset");
+  HIPCHK(c, hipDeviceSynchronize(), "stats reset");
   c->pixels = 0;
   c->dispatches = 0;
   return RT_OK;

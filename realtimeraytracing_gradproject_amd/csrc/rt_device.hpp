@@ -161,6 +161,7 @@ struct SceneView {
   float cull_sense;    // culling traces: +1 culls back faces, -1 front faces (DXR ray flags 0x10 / 0x20)
   int hybrid;          // every BLAS's worst-case stack fits kHybridStack: packet walks may hand subtrees to
                        // per-lane walks (lane_subtree)
+  int tlas_root;       // the TLAS root's index in the node pool (the TLAS version launches read)
 };
 
 // ------------------------------------------------------------------------------------------

@@ -21,10 +21,26 @@ void* ctx_stream(rt_ctx* c);
 // receives the leaf-order -> primitive permutation. Leaf refs are ~leaf_slot (BLAS, primitives
 // reordered afterwards) or ~primitive (TLAS). With d_tri_in the BLAS triangles are gathered into
 // leaf order (d_tri_out) as part of the build. Synchronous.
+// Device scratch of lbvh_build kept between builds (a per-frame TLAS update must not hipMalloc / hipFree:
+// both synchronise the device). Grown on demand; release() frees it.
+struct BuildArena {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipEvent_t e0 = nullptr, e1 = nullptr;  // build timing
+  void release() {
+    if (p) (void)hipFree(p);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    p = nullptr;
+    cap = 0;
+    e0 = e1 = nullptr;
+  }
+};
+
 hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uint32_t* d_sorted,
                       bool leaf_ref_is_prim, uint32_t* node_count, uint32_t* depth, uint32_t* max_stack,
                       float bounds[6], float* build_ms, hipStream_t stream, const TriRec* d_tri_in = nullptr,
-                      TriRec* d_tri_out = nullptr);
+                      TriRec* d_tri_out = nullptr, BuildArena* arena = nullptr);
 
 // Triangle setup: prim boxes + unsorted MT records from a {pos, normal} vertex array.
 hipError_t blas_prepare(const float* d_vtx, const uint32_t* d_idx, uint32_t ntri, TriRec* d_tris,

@@ -2064,7 +2064,8 @@ struct DevBuf {
 
 hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uint32_t* d_sorted,
                       bool leaf_ref_is_prim, uint32_t* node_count, uint32_t* depth, uint32_t* max_stack,
-                      float bounds[6], float* build_ms, hipStream_t s, const TriRec* d_tri_in, TriRec* d_tri_out) {
+                      float bounds[6], float* build_ms, hipStream_t s, const TriRec* d_tri_in, TriRec* d_tri_out,
+                      BuildArena* keep) {
   if (n == 0) return hipErrorInvalidValue;
   const uint32_t nblocks = (n + kRsTile - 1) / kRsTile;
   const uint32_t nbin = n > 1 ? n - 1 : 1;
@@ -2090,8 +2091,21 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
              p_order = part((size_t)nbin * 2), p_bfs = part((size_t)nbin * 2),
              p_k64 = part((size_t)n * 8), p_sbox = part((size_t)n * 24);
   DevBuf arena;
-  RT_TRY(hipMalloc(&arena.p, total));
-  char* A = (char*)arena.p;
+  char* A = nullptr;
+  if (keep) {  // the caller's scratch, kept between builds (no hipMalloc / hipFree on the way)
+    if (keep->cap < total) {
+      RT_TRY(hipStreamSynchronize(s));  // the previous build on s is the only user
+      if (keep->p) RT_TRY(hipFree(keep->p));
+      keep->p = nullptr;
+      keep->cap = 0;
+      RT_TRY(hipMalloc(&keep->p, total));
+      keep->cap = total;
+    }
+    A = (char*)keep->p;
+  } else {
+    RT_TRY(hipMalloc(&arena.p, total));
+    A = (char*)arena.p;
+  }
   struct View {
     void* p;
   };
@@ -2108,9 +2122,18 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
       if (b) (void)hipEventDestroy(b);
     }
   } ev;
-  RT_TRY(hipEventCreate(&ev.a));
-  RT_TRY(hipEventCreate(&ev.b));
-  hipEvent_t e0 = ev.a, e1 = ev.b;
+  hipEvent_t e0, e1;
+  if (keep) {
+    if (!keep->e0) RT_TRY(hipEventCreate(&keep->e0));
+    if (!keep->e1) RT_TRY(hipEventCreate(&keep->e1));
+    e0 = keep->e0;
+    e1 = keep->e1;
+  } else {
+    RT_TRY(hipEventCreate(&ev.a));
+    RT_TRY(hipEventCreate(&ev.b));
+    e0 = ev.a;
+    e1 = ev.b;
+  }
   RT_TRY(hipEventRecord(e0, s));
   float* cb = (float*)stats.p;
   const int path = build_path(n);

@@ -167,7 +167,7 @@ __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, H
   bool found = false;
   const int cap = stk.cap;
   int sp = 0;
-  int ref = 0;
+  int ref = sc.tlas_root;
   hit.t = tmax;
   hit.inst = 0xffffffffu;
   hit.prim = 0xffffffffu;
@@ -928,7 +928,7 @@ __device__ __forceinline__ void packet_walk(const SceneView& sc, const V3* o, co
   WaveStack stk;
   const int cap = sc.packet_cap;  // < kPacketStack (checked at launch): lane 63 stays spare
   int sp = 0;
-  int ref = 0;
+  int ref = sc.tlas_root;
   // TLAS walk; each instance leaf runs a nested BLAS walk on the stack above the TLAS entries
   // (the world rays are invariant here, the object rays inside: no ray state moves around).
   while (true) {
@@ -1606,6 +1606,18 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void k_trace_frame(SceneView 
 #ifndef RT_PACKET_WX_MS
 #define RT_PACKET_WX_MS 1  // multi-sample kernels (KS = 2, 4): one-wave workgroups (C5 -2.8 % vs 2 x 1)
 #endif
+#ifndef RT_MS_WIDE
+#define RT_MS_WIDE 0  // multi-sample waves: 1 = pixel tiles 8 (or 64 / samples) wide (32-B row stores), 0 = square
+#endif
+// pixel tile of one wave: 8 x 8 for one sample per pixel; with KS x KS samples per pixel in consecutive lanes
+// 64 / KS^2 pixels, square ((8 / KS) x (8 / KS)) or wide (RT_MS_WIDE: 8 x 2 at KS = 2)
+__host__ __device__ constexpr uint32_t ms_tile_w(int ks) {
+  return ks > 1 ? (RT_MS_WIDE ? (64u / (uint32_t)(ks * ks) < 8u ? 64u / (uint32_t)(ks * ks) : 8u) : 8u / (uint32_t)ks)
+                : 8u;
+}
+__host__ __device__ constexpr uint32_t ms_tile_h(int ks) {
+  return ks > 1 ? (64u / (uint32_t)(ks * ks)) / ms_tile_w(ks) : 8u;
+}
 // waves along x / y of a packet workgroup for the sample layout KS
 __host__ __device__ constexpr int packet_wx(int ks) { return ks > 1 ? RT_PACKET_WX_MS : RT_PACKET_WX; }
 __host__ __device__ constexpr int packet_wy(int ks) { return ks > 1 ? 1 : RT_PACKET_WY; }
@@ -1626,10 +1638,10 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
   constexpr uint32_t NS = KS > 1 ? KS * KS : 1;  // samples of a pixel held by consecutive lanes
-  constexpr uint32_t TP = KS > 1 ? 8 / KS : 8;    // tile side in pixels
+  constexpr uint32_t TP = ms_tile_w(KS);          // tile width in pixels (KS > 1: ms_tile_h(KS) rows)
   constexpr uint32_t WX = packet_wx(KS), WY = packet_wy(KS);
   // tile rows of a wave: TP, or 4 for 8 x 8 tiles at rt_set_tile_rows(4) (lanes past them idle)
-  const uint32_t TR = (KS <= 1 && fp.tile_rows == 4u) ? 4u : TP;
+  const uint32_t TR = (KS <= 1 && fp.tile_rows == 4u) ? 4u : ms_tile_h(KS);
   // the wave index is uniform: an SGPR, so the pixel of a lane can be re-derived from its lane id
   const uint32_t lane = threadIdx.x & 63u, w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t sample = lane % NS, pix = lane / NS;
@@ -1669,7 +1681,8 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
     acc[0] = sum;
     // the store index too (not kept live across the traces: the 7-wave budget has no VGPR to spare)
     const uint32_t xp = lid / NS, xx = blockIdx.x * (TP * WX) + (w % WX) * TP + (xp % TP);
-    const uint32_t orow = blockIdx.y * (TP * WY) + (w / WX) * TP + xp / TP;
+    constexpr uint32_t TH = ms_tile_h(KS);
+    const uint32_t orow = blockIdx.y * (TH * WY) + (w / WX) * TH + xp / TP;
     out[0] = (xx < fp.width && orow < fp.nrows && (lid % NS) == 0u) ? orow * fp.width + xx : 0xffffffffu;
   } else {
     for (uint32_t sy = 0; sy < k; ++sy)
@@ -1774,8 +1787,8 @@ hipError_t launch_mode(const SceneView& sc, const FrameParams& fp, const uint32_
     // KS: 1 one sample per pixel; 2 / 4 the k x k samples of a pixel in consecutive lanes; 0 the loop
     const int ks = fp.spp_side == 1 ? 1 : ((RT_SAMPLE_LANES && R == 1 && (fp.spp_side == 2 || fp.spp_side == 4))
                                                ? (int)fp.spp_side : 0);
-    const uint32_t tp = ks > 1 ? 8u / (uint32_t)ks : 8u;
-    const uint32_t tr = (ks <= 1 && fp.tile_rows == 4u) ? 4u : tp;  // as the kernel's TR (KS <= 1: 8 x 8 tiles)
+    const uint32_t tp = ms_tile_w(ks);
+    const uint32_t tr = (ks <= 1 && fp.tile_rows == 4u) ? 4u : ms_tile_h(ks);  // as the kernel's TR
     const uint32_t tw = tp * (uint32_t)packet_wx(ks), th = tr * R * (uint32_t)packet_wy(ks);
     dim3 gp((fp.width + tw - 1) / tw, (fp.nrows + th - 1) / th);
 #define RT_LAUNCH_PACKET(KS)                                                                                   \

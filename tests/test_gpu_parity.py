@@ -625,6 +625,45 @@ def test_raster_draws_on_two_streams():
     c.close()
 
 
+def test_per_frame_tlas_update_with_frames_in_flight():
+    """a per-frame TLAS update (OnUpdate -> TopLevelASGenerator update, D3D12HelloTriangle.cpp:421-433,
+    TopLevelASGenerator.cpp:202-222) with three frames in flight: C5's 257 instances move every frame, each frame is
+    dispatched on the next of three streams right after its update, with no host synchronisation in between. The
+    double-buffered TLAS keeps every frame on its own instance set: each equals the oracle's render of that set."""
+    spec = scenes.config("C5").with_size(192, 108)
+    c = fresh_ctx()
+    scenes.upload(c, spec)
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    outs, specs, walls = [], [], []
+    for k in range(7):
+        inst = []
+        for (m, x, iid, hg) in spec.instances:
+            x = np.asarray(x, np.float32).copy()
+            if hg == rt.RT_HITGROUP_MODEL:
+                if iid % 17 == 3:  # a few rotated, scaled instances (the general transform path)
+                    x = scenes._rot_scale((0.2, 1.0, 0.1), 11.0 * k + iid, (1.0, 1.0 + 0.05 * k, 1.0),
+                                          (float(x[3]), float(x[7]), float(x[11])))
+                else:
+                    x[3] += 0.15 * k * ((iid % 3) - 1)
+                    x[11] -= 0.1 * k * ((iid % 5) - 2)
+            inst.append((m, x, iid, hg))
+        c.tlas_build(inst, update_only=True)
+        walls.append(c.tlas_build_wall_ms())
+        out = torch.empty((spec.height, spec.width, 4), dtype=torch.uint8, device="cuda")
+        c.dispatch(spec.width, spec.height, out, None, stream=streams[k % 3].cuda_stream)
+        sk = scenes.SceneSpec(**{**spec.__dict__})
+        sk.instances = inst
+        outs.append(out)
+        specs.append(sk)
+    torch.cuda.synchronize()
+    for k, (out, sk) in enumerate(zip(outs, specs)):
+        o8, _, _ = oracle.Scene(sk).render_spec(sk, nthreads=16, want_float=False, schedule=1)
+        assert np.array_equal(out.cpu().numpy(), o8), f"frame {k}"
+    assert len({o.cpu().numpy().tobytes() for o in outs}) == len(outs)  # every frame saw its own scene
+    assert max(walls) > 0.0
+    c.close()
+
+
 def test_rejected_tlas_build_keeps_scene():
     """A TLAS build rejected by validation touches nothing: the previous scene still renders. (A
     build that fails after validation marks the scene stale until a build succeeds: rt_api.cpp.)"""
