@@ -213,10 +213,6 @@ struct rt_ctx {
   bool raster_pending = false;
 };
 
-namespace rt {
-int ctx_device(rt_ctx* c) { return c ? c->device : 0; }
-void* ctx_stream(rt_ctx* c) { return c ? (void*)c->stream : nullptr; }
-}  // namespace rt
 
 namespace {
 
@@ -878,6 +874,58 @@ static rt_status ensure_rows(rt_ctx* c, const uint32_t* rows, uint32_t nrows, hi
   return RT_OK;
 }
 
+}  // extern "C"
+
+namespace rt {
+
+int ctx_device(rt_ctx* c) { return c ? c->device : 0; }
+void* ctx_stream(rt_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+rt_status check_dispatch(rt_ctx* c, uint32_t W, uint32_t H, const void* rgba8) {
+  if (c->cur < 0 && !c->tlas_stale) return fail(c, RT_E_INVALID, "rt_dispatch_rays: no TLAS built");
+  if (c->tlas_stale)
+    return fail(c, RT_E_INVALID, "rt_dispatch_rays: scene stale (BLAS rebuilt, or the last rt_tlas_build failed)");
+  if (!c->have_camera || !c->have_shading) return fail(c, RT_E_INVALID, "rt_dispatch_rays: camera/shading not set");
+  if (W == 0 || H == 0 || !rgba8) return fail(c, RT_E_INVALID, "rt_dispatch_rays: bad size or output");
+  return RT_OK;
+}
+
+// The frame launch behind rt_dispatch_rays and rt_render_strips (d_rows: a device row list or null; the
+// caller validated the arguments with check_dispatch and keeps d_rows alive until the launch completed).
+rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_rows, uint32_t nrows, void* rgba8,
+                         float* rgba32f, hipStream_t s) {
+  c->fp.width = W;
+  c->fp.height = H;
+  c->fp.fwidth = (float)W;  // exact: W, H < 2^24
+  c->fp.fheight = (float)H;
+  c->fp.nrows = nrows;
+  c->fp.tile_rows = c->tile_rows;
+  rt::SceneView sv = scene_view(c);
+  if (sv.stack_cap > rt::kMaxTraversalStack)
+    return fail(c, RT_E_UNSUPPORTED, "rt_dispatch_rays: BVH too deep for the traversal stack");
+  ScratchSlot* ovf_slot = nullptr;
+  {
+    const size_t lanes = (size_t)((W + 15) / 16) * ((nrows + 15) / 16) * 256;
+    rt_status st = ensure_overflow(c, sv, lanes, s, &ovf_slot);
+    if (st != RT_OK) return st;
+  }
+  HIPCHK(c, order_after_tlas(c, s), "rt_dispatch_rays: order after the TLAS build");
+  hipError_t e = rt::launch_trace_frame(sv, c->fp, d_rows, rgba8, rgba32f, c->d_stats, c->stats_on,
+                                        c->schedule, s);
+  if (e != hipSuccess) return hip_fail(c, e, "trace launch");
+  HIPCHK(c, slot_mark_use(c->ver[c->cur].use, s), "rt_dispatch_rays: record use");
+  if (ovf_slot) HIPCHK(c, slot_mark_use(*ovf_slot, s), "overflow stack: record use");
+  if (c->stats_on) {
+    c->dispatches += 1;
+    c->pixels += (uint64_t)W * nrows;
+  }
+  return RT_OK;
+}
+
+}  // namespace rt
+
+extern "C" {
+
 rt_status rt_raster_draw(rt_ctx_t c, const rt_blas_t* draws, uint32_t ndraws, const float* object_to_world,
                          uint32_t W, uint32_t H, void* rgba8, float* depth32f, void* stream) {
   if (!c) return RT_E_INVALID;
@@ -1001,47 +1049,20 @@ rt_status rt_raster_draw(rt_ctx_t c, const rt_blas_t* draws, uint32_t ndraws, co
 rt_status rt_dispatch_rays(rt_ctx_t c, uint32_t W, uint32_t H, const uint32_t* rows, uint32_t nrows,
                            void* rgba8, float* rgba32f, void* stream) {
   if (!c) return RT_E_INVALID;
-  if (c->cur < 0 && !c->tlas_stale) return fail(c, RT_E_INVALID, "rt_dispatch_rays: no TLAS built");
-  if (c->tlas_stale)
-    return fail(c, RT_E_INVALID, "rt_dispatch_rays: scene stale (BLAS rebuilt, or the last rt_tlas_build failed)");
-  if (!c->have_camera || !c->have_shading) return fail(c, RT_E_INVALID, "rt_dispatch_rays: camera/shading not set");
-  if (W == 0 || H == 0 || !rgba8) return fail(c, RT_E_INVALID, "rt_dispatch_rays: bad size or output");
   if (!rows) nrows = H;
   if (nrows == 0 || nrows > H) return fail(c, RT_E_INVALID, "rt_dispatch_rays: bad row count");
-  (void)hipSetDevice(c->device);
-  hipStream_t s = pick_stream(c, stream);
-  const uint32_t* d_rows = nullptr;
   if (rows)
     for (uint32_t r = 0; r < nrows; ++r)
       if (rows[r] >= H) return fail(c, RT_E_INVALID, "rt_dispatch_rays: row index out of range");
-  c->fp.width = W;
-  c->fp.height = H;
-  c->fp.fwidth = (float)W;  // exact: W, H < 2^24
-  c->fp.fheight = (float)H;
-  c->fp.nrows = nrows;
-  c->fp.tile_rows = c->tile_rows;
-  rt::SceneView sv = scene_view(c);
-  if (sv.stack_cap > rt::kMaxTraversalStack)
-    return fail(c, RT_E_UNSUPPORTED, "rt_dispatch_rays: BVH too deep for the traversal stack");
-  ScratchSlot* ovf_slot = nullptr;
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  rt_status st = rt::check_dispatch(c, W, H, rgba8);
+  if (st != RT_OK) return st;
+  const uint32_t* d_rows = nullptr;
   ScratchSlot* rows_slot = nullptr;
-  {
-    const size_t lanes = (size_t)((W + 15) / 16) * ((nrows + 15) / 16) * 256;
-    rt_status st = ensure_overflow(c, sv, lanes, s, &ovf_slot);
-    if (st == RT_OK && rows) st = ensure_rows(c, rows, nrows, s, &rows_slot, &d_rows);
-    if (st != RT_OK) return st;
-  }
-  HIPCHK(c, order_after_tlas(c, s), "rt_dispatch_rays: order after the TLAS build");
-  hipError_t e = rt::launch_trace_frame(sv, c->fp, d_rows, rgba8, rgba32f, c->d_stats, c->stats_on,
-                                        c->schedule, s);
-  if (e != hipSuccess) return hip_fail(c, e, "trace launch");
-  HIPCHK(c, slot_mark_use(c->ver[c->cur].use, s), "rt_dispatch_rays: record use");
-  if (ovf_slot) HIPCHK(c, slot_mark_use(*ovf_slot, s), "overflow stack: record use");
+  if (rows && (st = ensure_rows(c, rows, nrows, s, &rows_slot, &d_rows)) != RT_OK) return st;
+  if ((st = rt::dispatch_frame(c, W, H, d_rows, nrows, rgba8, rgba32f, s)) != RT_OK) return st;
   if (rows_slot) HIPCHK(c, slot_mark_use(*rows_slot, s), "rows: record use");
-  if (c->stats_on) {
-    c->dispatches += 1;
-    c->pixels += (uint64_t)W * nrows;
-  }
   return RT_OK;
 }
 

@@ -15,6 +15,10 @@
 
 #include <dlfcn.h>
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -86,6 +90,11 @@ struct rt_comm {
   // frame geometry of the slots (re-planned when it changes)
   uint32_t W = 0, H = 0, strip = 0, rows_per_rank = 0;
   std::vector<uint32_t> rows;  // this rank's global rows, output order
+  uint32_t* d_rows = nullptr;  // ... on the device (uploaded once per plan)
+  // RT_COMM_TIMING=1 (diagnostics): host time per part of rt_render_strips, printed by rt_comm_destroy
+  bool timing = false;
+  double t_parts[5] = {0, 0, 0, 0, 0};
+  uint64_t t_calls = 0;
   Slot slots[kSlots];
   uint64_t next = 0;
 };
@@ -102,6 +111,8 @@ rt_status nccl_fail(rt_comm* c, ncclResult_t r, const char* what) {
 }
 
 void release_slots(rt_comm* c) {
+  if (c->d_rows) (void)hipFree(c->d_rows);
+  c->d_rows = nullptr;
   for (Slot& s : c->slots) {
     if (s.local) (void)hipFree(s.local);
     if (s.gathered) (void)hipFree(s.gathered);
@@ -123,6 +134,11 @@ rt_status plan(rt_comm* c, uint32_t W, uint32_t H, uint32_t strip) {
   const uint32_t n = rt_strip_rows(H, c->nranks, c->rank, strip, nullptr, 0);
   c->rows.assign(n, 0u);
   if (n) rt_strip_rows(H, c->nranks, c->rank, strip, c->rows.data(), n);
+  if (n) {
+    if (hipMalloc(&c->d_rows, (size_t)n * 4) != hipSuccess) return cfail(c, RT_E_OOM, "rt_render_strips: hipMalloc(rows)");
+    if (hipMemcpy(c->d_rows, c->rows.data(), (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess)
+      return cfail(c, RT_E_HIP, "rt_render_strips: upload rows");
+  }
   const uint32_t nstrips = (H + strip - 1) / strip;
   c->rows_per_rank = ((nstrips + c->nranks - 1) / c->nranks) * strip;
   const size_t local_bytes = (size_t)c->rows_per_rank * W * 4;
@@ -166,6 +182,8 @@ rt_status rt_comm_init(rt_ctx_t ctx, uint32_t nranks, uint32_t rank, const void*
   c->device = rt::ctx_device(ctx);
   c->nranks = nranks;
   c->rank = rank;
+  const char* tm = std::getenv("RT_COMM_TIMING");
+  c->timing = tm && tm[0] == '1';
   if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return RT_E_HIP;
@@ -188,6 +206,11 @@ rt_status rt_comm_destroy(rt_comm_t c) {
   (void)hipStreamSynchronize(c->stream);
   for (Slot& s : c->slots)
     if (s.used && s.freed) (void)hipEventSynchronize(s.freed);
+  if (c->timing && c->t_calls)
+    std::fprintf(stderr, "rt_comm timing (us per rt_render_strips over %llu calls): plan+checks %.2f, render %.2f, "
+                 "hand-off %.2f, ncclGather %.2f, assembly+record %.2f\n", (unsigned long long)c->t_calls,
+                 c->t_parts[0] / c->t_calls, c->t_parts[1] / c->t_calls, c->t_parts[2] / c->t_calls,
+                 c->t_parts[3] / c->t_calls, c->t_parts[4] / c->t_calls);
   if (c->comm) (void)rccl().commDestroy(c->comm);
   release_slots(c);
   (void)hipStreamDestroy(c->stream);
@@ -210,30 +233,47 @@ rt_status rt_render_strips(rt_comm_t c, uint32_t W, uint32_t H, uint32_t strip_r
   if (!c) return RT_E_INVALID;
   if (W == 0 || H == 0 || strip_rows == 0) return cfail(c, RT_E_INVALID, "rt_render_strips: bad size");
   if (c->rank == 0 && !frame_out) return cfail(c, RT_E_INVALID, "rt_render_strips: rank 0 needs frame_out");
+  using clk = std::chrono::steady_clock;
+  clk::time_point t0;
+  if (c->timing) t0 = clk::now();
+  auto lap = [&](int part) {
+    if (!c->timing) return;
+    const clk::time_point t1 = clk::now();
+    c->t_parts[part] += std::chrono::duration<double, std::micro>(t1 - t0).count();
+    t0 = t1;
+  };
   (void)hipSetDevice(c->device);
   rt_status st = plan(c, W, H, strip_rows);
   if (st != RT_OK) return st;
   hipStream_t rs = render_stream ? (hipStream_t)render_stream : (hipStream_t)rt::ctx_stream(c->ctx);
   Slot& s = c->slots[c->next % kSlots];
+  if (!c->rows.empty() && (st = rt::check_dispatch(c->ctx, W, H, s.local)) != RT_OK)
+    return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));
   ++c->next;
   // the slot's previous frame must have left it (its gather read `local`, its assembly `gathered`)
   if (s.used && hipStreamWaitEvent(rs, s.freed, 0) != hipSuccess)
     return cfail(c, RT_E_HIP, "rt_render_strips: order after the slot's last gather");
+  lap(0);
   if (!c->rows.empty()) {
-    st = rt_dispatch_rays(c->ctx, W, H, c->rows.data(), (uint32_t)c->rows.size(), s.local, nullptr, rs);
+    st = rt::dispatch_frame(c->ctx, W, H, c->d_rows, (uint32_t)c->rows.size(), s.local, nullptr, rs);
     if (st != RT_OK) return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));
   }
+  lap(1);
   if (hipEventRecord(s.rendered, rs) != hipSuccess || hipStreamWaitEvent(c->stream, s.rendered, 0) != hipSuccess)
     return cfail(c, RT_E_HIP, "rt_render_strips: render -> gather hand-off");
+  lap(2);
   const size_t count = (size_t)c->rows_per_rank * W * 4;
   ncclResult_t r = rccl().gather(s.local, c->rank == 0 ? s.gathered : nullptr, count, ncclUint8, 0, c->comm, c->stream);
   if (r != ncclSuccess) return nccl_fail(c, r, "rt_render_strips: ncclGather");
+  lap(3);
   if (c->rank == 0) {
     st = rt_assemble_strips(c->ctx, W, H, c->nranks, strip_rows, s.gathered, frame_out, c->stream);
     if (st != RT_OK) return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));
   }
   if (hipEventRecord(s.freed, c->stream) != hipSuccess) return cfail(c, RT_E_HIP, "rt_render_strips: record");
   s.used = true;
+  lap(4);
+  ++c->t_calls;
   return RT_OK;
 }
 

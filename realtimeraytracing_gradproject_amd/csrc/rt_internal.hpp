@@ -11,6 +11,11 @@ namespace rt {
 // --- context accessors for the other host translation units (rt_comm.cpp) ---------------------
 int ctx_device(rt_ctx* c);
 void* ctx_stream(rt_ctx* c);
+// rt_dispatch_rays' argument / scene checks and its launch with a device row list (rt_render_strips keeps its
+// rank's rows on the device and skips the host list's upload ring)
+rt_status check_dispatch(rt_ctx* c, uint32_t W, uint32_t H, const void* rgba8);
+rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_rows, uint32_t nrows, void* rgba8,
+                         float* rgba32f, hipStream_t s);
 
 // --- LBVH build (rt_lbvh.hip) ---------------------------------------------------------------
 
