@@ -193,7 +193,62 @@ def fullsize(names=None):
             json.dump(out, f, indent=1)
 
 
+def seam_leaks():
+    """tests/golden/seam_leaks.json: rays aimed AT the teapot's seam edges (the 1,036 boundary edges of its seam
+    duplicates, SURVEY A.2: each is the edge of a triangle whose neighbour references duplicated vertices at the
+    same positions), 16 points along each edge from 4 view directions: float32 Moller-Trumbore over the oracle's
+    BVH (the GPU's arithmetic) against the float64 brute force. A leak is a ray float64 stops on the teapot that
+    float32 lets through (misses, or hits the teapot farther away) -- the watertightness DXR's fixed-function
+    intersection guarantees and float32 Moller-Trumbore does not."""
+    rng = np.random.default_rng(0x5EA3)
+    verts, idx = scenes.load_model("teapot")
+    tri = idx.reshape(-1, 3)
+    edges = {}
+    for t in tri:
+        for a, b in ((t[0], t[1]), (t[1], t[2]), (t[2], t[0])):
+            k = (min(a, b), max(a, b))
+            edges[k] = edges.get(k, 0) + 1
+    seam = np.array([k for k, c in edges.items() if c == 1], np.int64)
+    p0, p1 = verts[seam[:, 0], :3].astype(np.float64), verts[seam[:, 1], :3].astype(np.float64)
+    ts = (np.arange(16) + 0.5) / 16.0
+    pts = (p0[:, None, :] * (1 - ts)[None, :, None] + p1[:, None, :] * ts[None, :, None]).reshape(-1, 3)
+    dirs = np.array([[1.0, 0.35, 0.6], [-0.8, 0.5, 0.3], [0.2, -0.4, -1.0], [-0.3, 0.9, -0.5]])
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    origins, ds = [], []
+    for dvec in dirs:
+        jit = rng.normal(scale=1e-7, size=pts.shape)  # off the exact edge by less than a float32 ulp of the coordinates
+        o = pts + jit - dvec * 20.0
+        origins.append(o)
+        ds.append(np.broadcast_to(dvec, o.shape))
+    O, D = np.concatenate(origins), np.concatenate(ds)
+    spec = scenes.SceneSpec("seams", [(verts, idx)], [(0, scenes.IDENTITY, 0, 0)], scenes.REFERENCE_LIGHTS[:1],
+                            scenes.REFERENCE_MATERIAL, scenes.REFERENCE_CAMERA, 64, 64, 1)
+    o32 = oracle.Scene(spec)
+    rays = np.zeros((O.shape[0], 8), np.float32)
+    rays[:, :3], rays[:, 4:7], rays[:, 7] = O, D, 100000.0
+    h32, _, _ = o32.trace_rays(rays)
+    # float64 on the float32 rays' exact values (the comparison is about the intersection arithmetic)
+    t64, i64, p64, _, _ = np_reference.Scene(spec).intersect(rays[:, :3].astype(np.float64),
+                                                              rays[:, 4:7].astype(np.float64), 0.0, 100000.0)
+    hit32 = h32[:, 3] == 1
+    hit64 = i64 >= 0
+    t32 = np.where(hit32, h32[:, 0].view(np.float32).astype(np.float64), np.inf)
+    leak = hit64 & (~hit32 | (t32 > t64 + 1e-4 * np.maximum(1.0, t64)))
+    extra = hit32 & ~hit64
+    out = {"seam_edges": int(seam.shape[0]), "rays": int(O.shape[0]), "points_per_edge": 16, "directions": 4,
+           "hit64": int(hit64.sum()), "hit32": int(hit32.sum()), "leaks": int(leak.sum()), "extra32": int(extra.sum()),
+           "same_triangle": int((hit32 & hit64 & (h32[:, 2].astype(np.int64) == p64)).sum()),
+           "leak_rays": [{"origin": O[j].tolist(), "dir": D[j].tolist(), "t64": float(t64[j]),
+                          "hit32": bool(hit32[j])} for j in np.nonzero(leak)[0][:20]]}
+    print(json.dumps({k: v for k, v in out.items() if k != "leak_rays"}))
+    with open(os.path.join(HERE, "seam_leaks.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 if __name__ == "__main__":
+    if "--seams" in sys.argv:
+        seam_leaks()
+        sys.exit(0)
     if "--fullsize" in sys.argv:
         fullsize([a for a in sys.argv[1:] if not a.startswith("--")] or None)
         sys.exit(0)

@@ -408,3 +408,26 @@ def test_fullsize_float64_crosscheck_fixture():
         rows = np.asarray(fx[name]["rows"], np.uint32)
         o8, _, _ = oracle.Scene(spec).render_spec(spec, rows=rows, nthreads=8, schedule=1)
         assert hashlib.sha256(o8.tobytes()).hexdigest() == fx[name]["oracle_rows_rgba8_sha256"], name
+
+
+def test_seam_watertightness_probe_fixture():
+    """tests/golden/seam_leaks.json (make_golden.py --seams): rays aimed at the teapot's 1,036 seam edges, float32
+    Moller-Trumbore over the oracle's BVH (the GPU's arithmetic) against the float64 brute force. The
+    counts are reproduced here from scratch (float32 leaks are a property of the pinned intersection test, DXR's
+    is watertight: DESIGN §5)."""
+    import json
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import make_golden
+    with open(os.path.join(os.path.dirname(__file__), "golden", "seam_leaks.json")) as f:
+        fx = json.load(f)
+    path = os.path.join(os.path.dirname(__file__), "golden", "seam_leaks.json")
+    before = open(path).read()
+    try:
+        make_golden.seam_leaks()
+        now = json.load(open(path))
+    finally:
+        with open(path, "w") as f:
+            f.write(before)
+    for k in ("seam_edges", "rays", "hit64", "hit32", "leaks", "extra32", "same_triangle"):
+        assert now[k] == fx[k], k
+    assert fx["seam_edges"] == 1036 and 0 < fx["leaks"] < fx["rays"] // 10
