@@ -419,12 +419,19 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
         dist.all_reduce(counts)
     rays_step = int(counts[0].item())  # strips: one frame over all ranks; frames mode: N frames
 
+    def drain():
+        """Everything issued so far has finished: with the native loop the library's issue thread first
+        enqueues the gathers it was handed (rt_comm_synchronize), then the device drains."""
+        if rcomm is not None:
+            rcomm.synchronize()
+        be.synchronize()
+
     # warmup (untimed)
     with on_comm():
         for _ in range(warmup):
             step(k)
             k += 1
-    be.synchronize()
+    drain()
     if distributed:
         dist.barrier()
     be.synchronize()
@@ -441,7 +448,7 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
             step(k)
             k += 1
     e1.record(render[0])
-    be.synchronize()
+    drain()
     if distributed:
         dist.barrier()
     be.synchronize()

@@ -10,6 +10,12 @@
 //
 // RCCL is bound at run time (dlopen of librccl.so.1): a process that already loaded RCCL (torch)
 // shares that copy, and a context that never creates a communicator never loads it.
+//
+// Two host threads issue a step: the caller's thread renders (wait for the slot, dispatch, record the
+// render event) and hands the slot to the communicator's issue thread, which orders the gather after
+// the render, issues the ncclGather and the assembly and records the slot's release. HIP and RCCL host
+// calls cost microseconds each, so one thread issuing both halves limited a step to their sum (≈ 26 us
+// measured, tools/native_strips_cost.py); split, a step costs the longer half.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -19,9 +25,12 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rt_api.h"
@@ -80,6 +89,13 @@ hipEvent_t pipeline_event() {
 
 }  // namespace
 
+struct Job {
+  uint32_t slot;
+  void* frame_out;
+  uint32_t W, H, strip, rows_per_rank;
+  uint64_t seq;
+};
+
 struct rt_comm {
   rt_ctx_t ctx = nullptr;
   int device = 0;
@@ -97,6 +113,18 @@ struct rt_comm {
   uint64_t t_calls = 0;
   Slot slots[kSlots];
   uint64_t next = 0;
+  // the issue thread of the gather side (see the header comment)
+  std::thread worker;
+  std::mutex mu;
+  std::condition_variable cv_job, cv_done;
+  std::deque<Job> jobs;
+  uint64_t issued = 0;          // jobs handed over (caller thread)
+  uint64_t done = 0;            // jobs whose gather, assembly and release are enqueued (issue thread)
+  uint64_t slot_seq[kSlots] = {0, 0, 0, 0};  // the last job of each slot
+  bool stop = false;
+  rt_status werr = RT_OK;       // the issue thread's first failure, returned by the next call
+  std::string wmsg;
+  double w_parts[3] = {0, 0, 0};  // RT_COMM_TIMING: issue-thread hand-off, ncclGather, assembly + record
 };
 
 namespace {
@@ -123,8 +151,11 @@ void release_slots(rt_comm* c) {
 }
 
 // (re)plans the strips of a W x H frame and sizes the pipeline slots; waits for the slots' last uses
+void wait_issued(rt_comm* c, uint64_t seq);
+
 rt_status plan(rt_comm* c, uint32_t W, uint32_t H, uint32_t strip) {
   if (c->W == W && c->H == H && c->strip == strip) return RT_OK;
+  wait_issued(c, c->issued);
   if (c->stream && hipStreamSynchronize(c->stream) != hipSuccess) return cfail(c, RT_E_HIP, "rt_render_strips: drain");
   for (Slot& s : c->slots)
     if (s.used && s.freed && hipEventSynchronize(s.freed) != hipSuccess)
@@ -152,6 +183,83 @@ rt_status plan(rt_comm* c, uint32_t W, uint32_t H, uint32_t strip) {
   c->W = W;
   c->H = H;
   c->strip = strip;
+  return RT_OK;
+}
+
+// issue thread: for each handed-over slot, the gather side of the step on the communicator's stream
+void issue_loop(rt_comm* c) {
+  (void)hipSetDevice(c->device);
+  using clk = std::chrono::steady_clock;
+  while (true) {
+    Job j;
+    {
+      std::unique_lock<std::mutex> lk(c->mu);
+      c->cv_job.wait(lk, [c] { return c->stop || !c->jobs.empty(); });
+      if (c->jobs.empty()) return;  // stop requested and nothing left
+      j = c->jobs.front();
+      c->jobs.pop_front();
+    }
+    clk::time_point t0, t1, t2, t3;
+    if (c->timing) t0 = clk::now();
+    Slot& s = c->slots[j.slot];
+    rt_status st = RT_OK;
+    std::string msg;
+    if (hipStreamWaitEvent(c->stream, s.rendered, 0) != hipSuccess) {
+      st = RT_E_HIP;
+      msg = "rt_render_strips: render -> gather hand-off";
+    }
+    if (c->timing) t1 = clk::now();
+    if (st == RT_OK) {
+      const size_t count = (size_t)j.rows_per_rank * j.W * 4;
+      ncclResult_t r = rccl().gather(s.local, c->rank == 0 ? s.gathered : nullptr, count, ncclUint8, 0, c->comm, c->stream);
+      if (r != ncclSuccess) {
+        st = RT_E_RCCL;
+        msg = std::string("rt_render_strips: ncclGather: ") + rccl().getErrorString(r);
+      }
+    }
+    if (c->timing) t2 = clk::now();
+    if (st == RT_OK && c->rank == 0) {
+      // the launcher itself, not rt_assemble_strips: the caller's thread owns the context's state
+      const hipError_t e = rt::launch_assemble_strips(j.W, j.H, c->nranks, j.strip, s.gathered, j.frame_out, c->stream);
+      if (e != hipSuccess) {
+        st = RT_E_HIP;
+        msg = std::string("rt_render_strips: assembly: ") + hipGetErrorString(e);
+      }
+    }
+    if (st == RT_OK && hipEventRecord(s.freed, c->stream) != hipSuccess) {
+      st = RT_E_HIP;
+      msg = "rt_render_strips: record";
+    }
+    if (c->timing) {
+      t3 = clk::now();
+      c->w_parts[0] += std::chrono::duration<double, std::micro>(t1 - t0).count();
+      c->w_parts[1] += std::chrono::duration<double, std::micro>(t2 - t1).count();
+      c->w_parts[2] += std::chrono::duration<double, std::micro>(t3 - t2).count();
+    }
+    {
+      std::lock_guard<std::mutex> lk(c->mu);
+      if (st != RT_OK && c->werr == RT_OK) {
+        c->werr = st;
+        c->wmsg = msg;
+      }
+      c->done = j.seq;
+    }
+    c->cv_done.notify_all();
+  }
+}
+
+// waits until the issue thread has enqueued every handed-over job up to `seq`
+void wait_issued(rt_comm* c, uint64_t seq) {
+  std::unique_lock<std::mutex> lk(c->mu);
+  c->cv_done.wait(lk, [c, seq] { return c->done >= seq; });
+}
+
+rt_status worker_status(rt_comm* c) {
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->werr != RT_OK) {
+    c->err = c->wmsg;
+    return c->werr;
+  }
   return RT_OK;
 }
 
@@ -196,21 +304,31 @@ rt_status rt_comm_init(rt_ctx_t ctx, uint32_t nranks, uint32_t rank, const void*
     delete c;
     return RT_E_RCCL;
   }
+  c->worker = std::thread(issue_loop, c);
   *out = c;
   return RT_OK;
 }
 
 rt_status rt_comm_destroy(rt_comm_t c) {
   if (!c) return RT_E_INVALID;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->stop = true;
+  }
+  c->cv_job.notify_all();
+  if (c->worker.joinable()) c->worker.join();  // the issue thread drains its queue first
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (Slot& s : c->slots)
     if (s.used && s.freed) (void)hipEventSynchronize(s.freed);
   if (c->timing && c->t_calls)
-    std::fprintf(stderr, "rt_comm timing (us per rt_render_strips over %llu calls): plan+checks %.2f, render %.2f, "
-                 "hand-off %.2f, ncclGather %.2f, assembly+record %.2f\n", (unsigned long long)c->t_calls,
+    std::fprintf(stderr, "rt_comm timing, caller thread (us per rt_render_strips over %llu calls): plan+checks %.2f, "
+                 "render %.2f, record+hand-over %.2f (%.2f, %.2f unused)\n", (unsigned long long)c->t_calls,
                  c->t_parts[0] / c->t_calls, c->t_parts[1] / c->t_calls, c->t_parts[2] / c->t_calls,
                  c->t_parts[3] / c->t_calls, c->t_parts[4] / c->t_calls);
+  if (c->timing && c->t_calls)
+    std::fprintf(stderr, "rt_comm timing, issue thread (us per step): hand-off %.2f, ncclGather %.2f, assembly+record "
+                 "%.2f\n", c->w_parts[0] / c->t_calls, c->w_parts[1] / c->t_calls, c->w_parts[2] / c->t_calls);
   if (c->comm) (void)rccl().commDestroy(c->comm);
   release_slots(c);
   (void)hipStreamDestroy(c->stream);
@@ -220,11 +338,18 @@ rt_status rt_comm_destroy(rt_comm_t c) {
 
 const char* rt_comm_last_error(rt_comm_t c) { return c ? c->err.c_str() : "null communicator"; }
 
-void* rt_comm_stream(rt_comm_t c) { return c ? (void*)c->stream : nullptr; }
+void* rt_comm_stream(rt_comm_t c) {
+  if (!c) return nullptr;
+  wait_issued(c, c->issued);  // every step handed over so far is enqueued on the stream returned
+  return (void*)c->stream;
+}
 
 rt_status rt_comm_synchronize(rt_comm_t c) {
   if (!c) return RT_E_INVALID;
+  wait_issued(c, c->issued);
   (void)hipSetDevice(c->device);
+  rt_status st = worker_status(c);
+  if (st != RT_OK) return st;
   return hipStreamSynchronize(c->stream) == hipSuccess ? RT_OK : cfail(c, RT_E_HIP, "rt_comm_synchronize");
 }
 
@@ -233,6 +358,8 @@ rt_status rt_render_strips(rt_comm_t c, uint32_t W, uint32_t H, uint32_t strip_r
   if (!c) return RT_E_INVALID;
   if (W == 0 || H == 0 || strip_rows == 0) return cfail(c, RT_E_INVALID, "rt_render_strips: bad size");
   if (c->rank == 0 && !frame_out) return cfail(c, RT_E_INVALID, "rt_render_strips: rank 0 needs frame_out");
+  rt_status st = worker_status(c);
+  if (st != RT_OK) return st;
   using clk = std::chrono::steady_clock;
   clk::time_point t0;
   if (c->timing) t0 = clk::now();
@@ -243,36 +370,36 @@ rt_status rt_render_strips(rt_comm_t c, uint32_t W, uint32_t H, uint32_t strip_r
     t0 = t1;
   };
   (void)hipSetDevice(c->device);
-  rt_status st = plan(c, W, H, strip_rows);
-  if (st != RT_OK) return st;
+  if ((st = plan(c, W, H, strip_rows)) != RT_OK) return st;
   hipStream_t rs = render_stream ? (hipStream_t)render_stream : (hipStream_t)rt::ctx_stream(c->ctx);
-  Slot& s = c->slots[c->next % kSlots];
+  const uint32_t si = (uint32_t)(c->next % kSlots);
+  Slot& s = c->slots[si];
   if (!c->rows.empty() && (st = rt::check_dispatch(c->ctx, W, H, s.local)) != RT_OK)
     return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));
   ++c->next;
-  // the slot's previous frame must have left it (its gather read `local`, its assembly `gathered`)
-  if (s.used && hipStreamWaitEvent(rs, s.freed, 0) != hipSuccess)
-    return cfail(c, RT_E_HIP, "rt_render_strips: order after the slot's last gather");
+  // the slot's previous frame must have left it: its release is recorded by the issue thread (wait for
+  // that, rarely: four slots), then this stream waits for it on the device
+  if (s.used) {
+    wait_issued(c, c->slot_seq[si]);
+    if (hipStreamWaitEvent(rs, s.freed, 0) != hipSuccess)
+      return cfail(c, RT_E_HIP, "rt_render_strips: order after the slot's last gather");
+  }
   lap(0);
   if (!c->rows.empty()) {
     st = rt::dispatch_frame(c->ctx, W, H, c->d_rows, (uint32_t)c->rows.size(), s.local, nullptr, rs);
     if (st != RT_OK) return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));
   }
   lap(1);
-  if (hipEventRecord(s.rendered, rs) != hipSuccess || hipStreamWaitEvent(c->stream, s.rendered, 0) != hipSuccess)
-    return cfail(c, RT_E_HIP, "rt_render_strips: render -> gather hand-off");
-  lap(2);
-  const size_t count = (size_t)c->rows_per_rank * W * 4;
-  ncclResult_t r = rccl().gather(s.local, c->rank == 0 ? s.gathered : nullptr, count, ncclUint8, 0, c->comm, c->stream);
-  if (r != ncclSuccess) return nccl_fail(c, r, "rt_render_strips: ncclGather");
-  lap(3);
-  if (c->rank == 0) {
-    st = rt_assemble_strips(c->ctx, W, H, c->nranks, strip_rows, s.gathered, frame_out, c->stream);
-    if (st != RT_OK) return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));
-  }
-  if (hipEventRecord(s.freed, c->stream) != hipSuccess) return cfail(c, RT_E_HIP, "rt_render_strips: record");
+  if (hipEventRecord(s.rendered, rs) != hipSuccess) return cfail(c, RT_E_HIP, "rt_render_strips: record render");
   s.used = true;
-  lap(4);
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    const uint64_t seq = ++c->issued;
+    c->slot_seq[si] = seq;
+    c->jobs.push_back(Job{si, frame_out, W, H, strip_rows, c->rows_per_rank, seq});
+  }
+  c->cv_job.notify_one();
+  lap(2);
   ++c->t_calls;
   return RT_OK;
 }

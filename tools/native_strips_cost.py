@@ -2,8 +2,9 @@
 assembly issued from C++) against bench.py's former Python step (torch.distributed gather + rt_event_* +
 rt_assemble_strips), both over a world-1 RCCL group on ONE GPU (the gather moves nothing: what is measured is the
 host and launch cost of a step). Per loop: the host time to ISSUE `frames` steps (no synchronisation inside the
-loop; the GPU is kept busy so issue is not throttled by an empty queue), and the wall time per frame once the
-GPU has drained, with 1 and 3 render streams (frames in flight).
+loop; the GPU is kept busy so issue is not throttled by an empty queue; for the native loop this is the caller's
+thread, the library's issue thread runs the gather half beside it), and the wall time per frame once everything
+has drained, with 1 and 3 render streams (frames in flight). RT_COMM_TIMING=1 prints both threads' breakdown.
 
   python tools/native_strips_cost.py --config C2 --frames 200 > gpurun_out/native_strips_cost.json
 """
@@ -69,17 +70,21 @@ def main():
     def native_step(k, nstream):
         comm.render_strips(W, H, frames[k % nslot], streams[(k % nslot) % nstream].cuda_stream)
 
+    def sync():
+        comm.synchronize()  # the library's issue thread has enqueued every handed-over gather
+        torch.cuda.synchronize()
+
     def measure(fn, nstream):
         best_issue, best_frame = float("inf"), float("inf")
         for _ in range(a.rounds):
             for k in range(20):
                 fn(k, nstream)
-            torch.cuda.synchronize()
+            sync()
             t0 = time.perf_counter()
             for k in range(a.frames):
                 fn(k, nstream)
             t1 = time.perf_counter()
-            torch.cuda.synchronize()
+            sync()
             t2 = time.perf_counter()
             best_issue = min(best_issue, (t1 - t0) * 1e6 / a.frames)
             best_frame = min(best_frame, (t2 - t0) * 1e3 / a.frames)
