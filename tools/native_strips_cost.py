@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--frames", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--size", default="", help="WxH: e.g. 1920x136, the rows one of 8 ranks renders, so the GPU "
+                                                "time per frame is small enough that the host issue shows")
     a = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29534")
@@ -36,6 +38,8 @@ def main():
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     spec = scenes.config(a.config)
+    if a.size:
+        spec = spec.with_size(*(int(v) for v in a.size.lower().split("x")))
     W, H = spec.width, spec.height
     ctx = rt.Context(0)
     scenes.upload(ctx, spec)
