@@ -292,13 +292,10 @@ rt_status rt_comm_init(rt_ctx_t ctx, uint32_t nranks, uint32_t rank, const void*
   c->rank = rank;
   const char* tm = std::getenv("RT_COMM_TIMING");
   c->timing = tm && tm[0] == '1';
-  // the gathers and assemblies get the device's highest stream priority: a hardware queue of their own (normal
-  // priority streams share GPU_MAX_HW_QUEUES queues round robin; a render stream on the gathers' queue serialises
-  // the two, tools/native_strips_cost.py under rocprofv3), and rank 0's frame completes as soon as its pieces land
-  int prio_lo = 0, prio_hi = 0;
-  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  if (hipSetDevice(c->device) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+  // normal priority: a high-priority stream gets a hardware queue of its own (normal streams share
+  // GPU_MAX_HW_QUEUES queues round robin, so a render stream can land on the gathers' queue), but its RCCL and
+  // assembly kernels ran 3.5x / 4x slower there (tools/trace_share.py): not taken
+  if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return RT_E_HIP;
   }
