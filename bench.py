@@ -373,6 +373,10 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
         nstream, flight_ms, measured = pick_in_flight(be, W, NR, rows)
     render = measured if measured else [be.stream() for _ in range(nstream)]
     native = strips and getattr(be, "native_strips", False)
+    if native:  # every rank must agree before the collective rt_comm_init (no RCCL: the torch.distributed loop)
+        ok = torch.tensor([1.0 if be.rt.comm_available() else 0.0], dtype=torch.float64, device=be.device)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        native = ok.item() == 1.0
     nslot = max(nstream, 2 if (strips and pipeline) else 1)
     local = [be.zeros((rows_per_rank, W, 4)) for _ in range(nslot)]
     gathered = ([be.zeros((world, rows_per_rank, W, 4)) if rank == 0 else None for _ in range(nslot)]

@@ -275,6 +275,9 @@ rt_status rt_stream_wait_event(void* hip_stream, void* ev);
  * renders on one GPU). RCCL is loaded at run time (librccl.so.1; RT_E_UNSUPPORTED when absent). */
 typedef struct rt_comm* rt_comm_t;
 #define RT_COMM_ID_BYTES 128 /* == sizeof(ncclUniqueId) */
+/* RT_OK when RCCL can be loaded (no collective, no GPU work): callers decide on the tiled-frame loop before
+ * the collective rt_comm_init. */
+rt_status rt_comm_available(void);
 /* ncclGetUniqueId: rank 0 creates the id; the caller hands the 128 bytes to every rank (MPI, a file, a
  * torch.distributed broadcast). */
 rt_status rt_comm_get_unique_id(void* id_out);

@@ -109,6 +109,7 @@ SIGNATURES = [
     ("rt_event_destroy", _I, [_P]),
     ("rt_event_record", _I, [_P, _P]),
     ("rt_stream_wait_event", _I, [_P, _P]),
+    ("rt_comm_available", _I, []),
     ("rt_comm_get_unique_id", _I, [_P]),
     ("rt_comm_init", _I, [_P, _U32, _U32, _P, ctypes.POINTER(_P)]),
     ("rt_comm_destroy", _I, [_P]),
@@ -376,6 +377,11 @@ class PipelineEvent:
 
 
 RT_COMM_ID_BYTES = 128
+
+
+def comm_available() -> bool:
+    """rt_comm_available: RCCL can be loaded (no collective, no GPU work)."""
+    return lib.rt_comm_available() == RT_OK
 
 
 def comm_unique_id() -> bytes:

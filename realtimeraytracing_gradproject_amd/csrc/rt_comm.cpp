@@ -267,6 +267,8 @@ rt_status worker_status(rt_comm* c) {
 
 extern "C" {
 
+rt_status rt_comm_available(void) { return rccl().ok ? RT_OK : RT_E_UNSUPPORTED; }
+
 rt_status rt_comm_get_unique_id(void* id_out) {
   if (!id_out) return RT_E_INVALID;
   RcclApi& api = rccl();
