@@ -822,19 +822,26 @@ static inline void osort4(float* t, int32_t* r) {
 /* Moller-Trumbore (the ray/triangle test DXR performs in hardware; formula pinned here).
  * face 0: both sides; +1/-1: RAY_FLAG_CULL_BACK_FACING_TRIANGLES, front = det * face > 0
  * (clockwise seen from the ray origin, DXR's default; face = -1 under a mirroring transform). */
+/* The test's cross products are pinned as fused multiply-adds (C99 fmaf rounds once, exactly as the GPU's
+ * v_fma_f32): cross_x = fma(a.y, b.z, -(a.z * b.y)) ...; its dot products stay unfused, (x + y) + z
+ * (rt_device.hpp RT_MT_FMA: fused dots would raise the seam-probe leak count by ~40%). */
+static inline float omt_dot(vec3 a, vec3 b) { return vdot(a, b); }
+static inline vec3 omt_cross(vec3 a, vec3 b) {
+  return mk(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
+}
 static inline int omt(vec3 o, vec3 d, const otri* tr, float face, float* t, float* u, float* v) {
   vec3 v0 = ld3(tr->v0), e1 = ld3(tr->e1), e2 = ld3(tr->e2);
-  vec3 p = vcross(d, e2);
-  float det = vdot(e1, p);
+  vec3 p = omt_cross(d, e2);
+  float det = omt_dot(e1, p);
   if (det == 0.0f || det * face < 0.0f) return 0;
   float inv = 1.0f / det;
   vec3 s = vsub(o, v0);
-  *u = vdot(s, p) * inv;
+  *u = omt_dot(s, p) * inv;
   if (!(*u >= 0.0f && *u <= 1.0f)) return 0;
-  vec3 q = vcross(s, e1);
-  *v = vdot(d, q) * inv;
+  vec3 q = omt_cross(s, e1);
+  *v = omt_dot(d, q) * inv;
   if (!(*v >= 0.0f && *u + *v <= 1.0f)) return 0;
-  *t = vdot(e2, q) * inv;
+  *t = omt_dot(e2, q) * inv;
   return 1;
 }
 

@@ -317,33 +317,57 @@ RT_HD void sort4(float t[4], int32_t r[4]) {
   cswap(t[1], r[1], t[2], r[2]);
 }
 
+#ifndef RT_MT_FMA
+#define RT_MT_FMA 2  // bit 0: the triangle test's dot products as fused multiply-add chains; bit 1: its cross products
+#endif
+// dot / cross for the triangle test. Default: cross products fused (fma(a.y, b.z, -(a.z * b.y)) ...), dot products
+// unfused, mirrored bit for bit by the oracle's omt_cross / omt_dot (as the slab test's fmas are by oslab4).
+// profiles/r03_ab_mt_fma.txt: fused cross 1-2% faster frames with the seam-probe leak count nearly unchanged
+// (1727 -> 1832 of 66,304 edge rays); fusing the dots as well gains 2-4% but raises it to 2514, so they stay unfused.
+// Any other setting renders frames the oracle no longer matches bit for bit.
+RT_HD float mt_dot(V3 a, V3 b) {
+#if RT_MT_FMA & 1
+  return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x));
+#else
+  return dot(a, b);
+#endif
+}
+RT_HD V3 mt_cross(V3 a, V3 b) {
+#if RT_MT_FMA & 2
+  return v3(__builtin_fmaf(a.y, b.z, -(a.z * b.y)), __builtin_fmaf(a.z, b.x, -(a.x * b.z)),
+            __builtin_fmaf(a.x, b.y, -(a.y * b.x)));
+#else
+  return cross(a, b);
+#endif
+}
+
 // Moller-Trumbore. Accepts u >= 0, v >= 0, u + v <= 1, det != 0; returns t (not yet range checked).
 // face: 0 accepts both sides; +1 / -1 accepts only det * face > 0, i.e. front faces under DXR's
 // RAY_FLAG_CULL_BACK_FACING_TRIANGLES (front = clockwise seen from the ray origin = det > 0 with
 // det = e1 . (d x e2), the sense flipped by a negative instance-transform determinant: face = -1).
 RT_HD bool moller_trumbore(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, float& t, float& u, float& v) {
 #if RT_MT_EARLY_EXIT
-  V3 p = cross(d, e2);
-  float det = dot(e1, p);
+  V3 p = mt_cross(d, e2);
+  float det = mt_dot(e1, p);
   if (det == 0.0f || det * face < 0.0f) return false;
   float inv = 1.0f / det;
   V3 s = sub(o, v0);
-  u = dot(s, p) * inv;
+  u = mt_dot(s, p) * inv;
   if (!(u >= 0.0f && u <= 1.0f)) return false;
-  V3 q = cross(s, e1);
-  v = dot(d, q) * inv;
+  V3 q = mt_cross(s, e1);
+  v = mt_dot(d, q) * inv;
   if (!(v >= 0.0f && u + v <= 1.0f)) return false;
-  t = dot(e2, q) * inv;
+  t = mt_dot(e2, q) * inv;
   return true;
 #else
-  const V3 p = cross(d, e2);
-  const float det = dot(e1, p);
+  const V3 p = mt_cross(d, e2);
+  const float det = mt_dot(e1, p);
   const float inv = 1.0f / det;
   const V3 s = sub(o, v0);
-  u = dot(s, p) * inv;
-  const V3 q = cross(s, e1);
-  v = dot(d, q) * inv;
-  t = dot(e2, q) * inv;
+  u = mt_dot(s, p) * inv;
+  const V3 q = mt_cross(s, e1);
+  v = mt_dot(d, q) * inv;
+  t = mt_dot(e2, q) * inv;
   return det != 0.0f && !(det * face < 0.0f) && u >= 0.0f && u <= 1.0f && v >= 0.0f && u + v <= 1.0f;
 #endif
 }
@@ -351,14 +375,14 @@ RT_HD bool moller_trumbore(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, float& t
 // Bitwise acceptance (no short-circuit, so no exec-mask branch around the u / v / t products):
 // the same predicate, every term evaluated.
 RT_HD bool moller_trumbore_bits(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, float& t, float& u, float& v) {
-  const V3 p = cross(d, e2);
-  const float det = dot(e1, p);
+  const V3 p = mt_cross(d, e2);
+  const float det = mt_dot(e1, p);
   const float inv = 1.0f / det;
   const V3 s = sub(o, v0);
-  u = dot(s, p) * inv;
-  const V3 q = cross(s, e1);
-  v = dot(d, q) * inv;
-  t = dot(e2, q) * inv;
+  u = mt_dot(s, p) * inv;
+  const V3 q = mt_cross(s, e1);
+  v = mt_dot(d, q) * inv;
+  t = mt_dot(e2, q) * inv;
   return (det != 0.0f) & !(det * face < 0.0f) & (u >= 0.0f) & (u <= 1.0f) & (v >= 0.0f) & (u + v <= 1.0f);
 }
 
@@ -366,14 +390,14 @@ RT_HD bool moller_trumbore_bits(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, flo
 // path, where a divergent early exit costs exec-mask SALU work on the busiest pipe). Accepts
 // exactly what moller_trumbore accepts, with the same u, v, t.
 RT_HD bool moller_trumbore_flat(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, float& t, float& u, float& v) {
-  const V3 p = cross(d, e2);
-  const float det = dot(e1, p);
+  const V3 p = mt_cross(d, e2);
+  const float det = mt_dot(e1, p);
   const float inv = 1.0f / det;
   const V3 s = sub(o, v0);
-  u = dot(s, p) * inv;
-  const V3 q = cross(s, e1);
-  v = dot(d, q) * inv;
-  t = dot(e2, q) * inv;
+  u = mt_dot(s, p) * inv;
+  const V3 q = mt_cross(s, e1);
+  v = mt_dot(d, q) * inv;
+  t = mt_dot(e2, q) * inv;
   return det != 0.0f && !(det * face < 0.0f) && u >= 0.0f && u <= 1.0f && v >= 0.0f && u + v <= 1.0f;
 }
 
