@@ -257,7 +257,8 @@ class HipBackend:
             return self.rt.Comm(self.ctx, world, rank, bytes(t.cpu().tolist()))
 
     def render_strips(self, comm, frame, stream):
-        comm.render_strips(self.spec.width, self.spec.height, frame, stream.cuda_stream, STRIP_ROWS)
+        comm.render_strips(self.spec.width, self.spec.height, frame, stream.cuda_stream if stream is not None else None,
+                           STRIP_ROWS)
 
     def close(self):
         if self.ctx is not None:
@@ -391,7 +392,9 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
         """One frame through rt_render_strips: render on this slot's stream, ncclGather + assembly on the
         communicator's stream, the slot pipeline and its events inside the library (one C call)."""
         s = k % nslot
-        be.render_strips(rcomm, frame[s] if rank == 0 else None, render[s % nstream])
+        # frames in flight: the communicator's own three render streams (NULL), which sit on hardware queues of
+        # their own, apart from the gathers' (DESIGN §7); one frame at a time: this rank's stream
+        be.render_strips(rcomm, frame[s] if rank == 0 else None, render[0] if nstream == 1 else None)
 
     def step(k: int):
         """One frame. In strips mode the caller holds `comm` as the current stream (the gather runs
@@ -486,7 +489,9 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
     return {"rays_step": rays_step, "primary": int(counts[1].item()), "shadow": int(counts[2].item()),
             "tmax": tmax, "kernel_ms": kernel_ms, "stats": st, "build": build, "rows_local": len(rows) if strips else H,
             "tile_rows": tile_rows, "tile_ms": tile_ms, "in_flight": nstream, "in_flight_ms": flight_ms,
-            "strips_loop": ("rt_render_strips (C-ABI: render -> ncclGather -> assembly)" if native else
+            "strips_loop": ("rt_render_strips (C-ABI: render -> ncclGather -> assembly; "
+                            + ("the communicator's 3 render streams)" if nstream > 1 else "one render stream)")
+                            if native else
                             "torch.distributed gather" if strips else None)}
 
 

@@ -289,8 +289,9 @@ const char* rt_comm_last_error(rt_comm_t comm);
 void* rt_comm_stream(rt_comm_t comm);
 rt_status rt_comm_synchronize(rt_comm_t comm);
 /* One tiled frame, collective over the ranks (every rank calls it, in the same frame order): this rank's
- * strips are rendered on render_stream (NULL = the context's stream) into one of the communicator's pipeline
- * slots; the communicator's stream waits for that render (a device-side event), gathers the slots of all ranks
+ * strips are rendered on render_stream into one of the communicator's pipeline slots (NULL: the communicator's
+ * own three render streams in turn, created beside its gather stream so that each sits on a hardware queue of
+ * its own: no render waits behind a gather in a shared queue); the communicator's stream waits for that render (a device-side event), gathers the slots of all ranks
  * into rank 0 and, on rank 0, assembles the W x H RGBA8 frame into frame_out (device buffer; ignored on other
  * ranks). A slot is re-rendered only after its gather and assembly finished (device-side events; no host
  * waits), so consecutive calls overlap frame k's gather with frame k + 1's render, and renders issued on

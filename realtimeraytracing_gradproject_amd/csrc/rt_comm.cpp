@@ -102,6 +102,10 @@ struct rt_comm {
   uint32_t nranks = 1, rank = 0;
   ncclComm_t comm = nullptr;
   hipStream_t stream = nullptr;  // gathers + assembly
+  // the communicator's own render streams (render_stream NULL: slot k renders on rstreams[k % kRenderStreams]),
+  // created right after `stream`, so the four take four different hardware queues (HIP deals a process's
+  // streams over GPU_MAX_HW_QUEUES = 4 queues in creation order): no render shares the gathers' queue
+  hipStream_t rstreams[3] = {nullptr, nullptr, nullptr};
   std::string err;
   // frame geometry of the slots (re-planned when it changes)
   uint32_t W = 0, H = 0, strip = 0, rows_per_rank = 0;
@@ -297,7 +301,16 @@ rt_status rt_comm_init(rt_ctx_t ctx, uint32_t nranks, uint32_t rank, const void*
   // normal priority: a high-priority stream gets a hardware queue of its own (normal streams share
   // GPU_MAX_HW_QUEUES queues round robin, so a render stream can land on the gathers' queue), but its RCCL and
   // assembly kernels ran 3.5x / 4x slower there (tools/trace_share.py): not taken
-  if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  auto destroy_streams = [c]() {
+    for (hipStream_t& r : c->rstreams)
+      if (r) (void)hipStreamDestroy(r);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+  };
+  bool ok = hipSetDevice(c->device) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
+  for (hipStream_t& r : c->rstreams) ok = ok && hipStreamCreateWithFlags(&r, hipStreamNonBlocking) == hipSuccess;
+  if (!ok) {
+    destroy_streams();
     delete c;
     return RT_E_HIP;
   }
@@ -305,7 +318,7 @@ rt_status rt_comm_init(rt_ctx_t ctx, uint32_t nranks, uint32_t rank, const void*
   std::memcpy(&uid, id, sizeof(uid));
   // collective: returns when every rank has joined
   if (api.commInitRank(&c->comm, (int)nranks, uid, (int)rank) != ncclSuccess) {
-    (void)hipStreamDestroy(c->stream);
+    destroy_streams();
     delete c;
     return RT_E_RCCL;
   }
@@ -328,7 +341,8 @@ rt_status rt_comm_destroy(rt_comm_t c) {
     if (s.used && s.freed) (void)hipEventSynchronize(s.freed);
   if (c->timing && c->t_calls)
     std::fprintf(stderr, "rt_comm timing, caller thread (us per rt_render_strips over %llu calls): plan+checks %.2f, "
-                 "render %.2f, record+hand-over %.2f (%.2f, %.2f unused)\n", (unsigned long long)c->t_calls,
+                 "render %.2f, record+hand-over %.2f, wait for the slot's hand-off %.2f, stream wait %.2f\n",
+                 (unsigned long long)c->t_calls,
                  c->t_parts[0] / c->t_calls, c->t_parts[1] / c->t_calls, c->t_parts[2] / c->t_calls,
                  c->t_parts[3] / c->t_calls, c->t_parts[4] / c->t_calls);
   if (c->timing && c->t_calls)
@@ -336,6 +350,10 @@ rt_status rt_comm_destroy(rt_comm_t c) {
                  "%.2f\n", c->w_parts[0] / c->t_calls, c->w_parts[1] / c->t_calls, c->w_parts[2] / c->t_calls);
   if (c->comm) (void)rccl().commDestroy(c->comm);
   release_slots(c);
+  for (hipStream_t r : c->rstreams) {
+    (void)hipStreamSynchronize(r);
+    (void)hipStreamDestroy(r);
+  }
   (void)hipStreamDestroy(c->stream);
   delete c;
   return RT_OK;
@@ -376,20 +394,22 @@ rt_status rt_render_strips(rt_comm_t c, uint32_t W, uint32_t H, uint32_t strip_r
   };
   (void)hipSetDevice(c->device);
   if ((st = plan(c, W, H, strip_rows)) != RT_OK) return st;
-  hipStream_t rs = render_stream ? (hipStream_t)render_stream : (hipStream_t)rt::ctx_stream(c->ctx);
   const uint32_t si = (uint32_t)(c->next % kSlots);
+  hipStream_t rs = render_stream ? (hipStream_t)render_stream : c->rstreams[si % 3];
   Slot& s = c->slots[si];
   if (!c->rows.empty() && (st = rt::check_dispatch(c->ctx, W, H, s.local)) != RT_OK)
     return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));
   ++c->next;
+  lap(0);
   // the slot's previous frame must have left it: its release is recorded by the issue thread (wait for
   // that, rarely: four slots), then this stream waits for it on the device
   if (s.used) {
     wait_issued(c, c->slot_seq[si]);
+    lap(3);
     if (hipStreamWaitEvent(rs, s.freed, 0) != hipSuccess)
       return cfail(c, RT_E_HIP, "rt_render_strips: order after the slot's last gather");
+    lap(4);
   }
-  lap(0);
   if (!c->rows.empty()) {
     st = rt::dispatch_frame(c->ctx, W, H, c->d_rows, (uint32_t)c->rows.size(), s.local, nullptr, rs);
     if (st != RT_OK) return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));

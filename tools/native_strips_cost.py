@@ -100,6 +100,10 @@ def main():
         out["python_step_3streams"] = measure(py_step, 3)
     out["native_step_1stream"] = measure(native_step, 1)
     out["native_step_3streams"] = measure(native_step, 3)
+
+    def native_own(k, nstream):  # render_stream NULL: the communicator's own three render streams
+        comm.render_strips(W, H, frames[k % nslot], None)
+    out["native_step_library_streams"] = measure(native_own, 3)
     # host cost of the call alone while the GPU is idle-free: the render itself issued alone
     t0 = time.perf_counter()
     for k in range(a.frames):
