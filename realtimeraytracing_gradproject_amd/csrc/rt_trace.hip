@@ -532,7 +532,7 @@ __device__ __forceinline__ uint32_t packet_slabs(const f4v (&pl6)[6], const Pack
       }
       const bool h = n <= f * 1.0000004f;  // only the lead's key is read
       hm[r][k] = wave_ballot(h);  // dead rays carry tbest = -inf: their h is false
-      vkey[r][k] = h ? (__float_as_uint(n) & 0x7fffffffu) : 0x7f800000u;
+      vkey[r][k] = __float_as_uint(h ? fabsf(n) : __builtin_inff());  // |n| folds into the select as a source modifier
     }
     if (STATS && ray_live(hit[r])) cnt.aabb += count;
   }
