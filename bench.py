@@ -382,16 +382,21 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
     local = [be.zeros((rows_per_rank, W, 4)) for _ in range(nslot)]
     gathered = ([be.zeros((world, rows_per_rank, W, 4)) if rank == 0 else None for _ in range(nslot)]
                 if strips and not native else None)
-    frame = [be.zeros((H, W, 4)) if rank == 0 else None for _ in range(nslot)] if strips else None
+    frame = ([be.zeros((H, W, 4)) if rank == 0 else None for _ in range(3 if native else nslot)]
+             if strips else None)
     rcomm = be.comm_open(world, rank) if native else None
     rendered = [be.sync_event() for _ in range(nslot)]
     freed = [be.sync_event() for _ in range(nslot)]
     parts = [D.gather_parts(gathered[s], world, rank) for s in range(nslot)] if strips and not native else None
 
+    ncall = [0]
+
     def step_native(k: int):
-        """One frame through rt_render_strips: render on this slot's stream, ncclGather + assembly on the
-        communicator's stream, the slot pipeline and its events inside the library (one C call)."""
-        s = k % nslot
+        """One frame through rt_render_strips: render on the slot's stream, ncclGather on the communicator's
+        gather stream, rank 0's assembly back on the slot's stream, the slot pipeline and its events inside the
+        library (one C call). The library's slot is its call count mod 3; frame buffer i serves slot i."""
+        s = ncall[0] % 3
+        ncall[0] += 1
         # frames in flight: the communicator's own three render streams (NULL), which sit on hardware queues of
         # their own, apart from the gathers' (DESIGN §7); one frame at a time: this rank's stream
         be.render_strips(rcomm, frame[s] if rank == 0 else None, render[0] if nstream == 1 else None)
@@ -481,7 +486,9 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
         kernel_ms = render_ms
 
     if save_image and rank == 0:
-        last = (k - 1) % nslot
+        last = (ncall[0] - 1) % 3 if native else (k - 1) % nslot
+        if native:
+            rcomm.synchronize()
         img = frame[last] if strips else local[last][:H]
         np.save(save_image, img.cpu().numpy())
     if rcomm is not None:

@@ -147,7 +147,8 @@ struct TlasVersion {
   std::vector<rt_instance> host;  // the instances as given
   rt::InstanceRec* staging = nullptr;  // pinned upload staging (records, then BLAS boxes)
   size_t staging_bytes = 0;
-  ScratchSlot use;                // launches that read this version
+  ScratchSlot use;                // launches that read this version: per-stream events, recorded when it stops being current
+  std::vector<hipStream_t> readers;  // streams that launched with it since it became current (no event per launch)
   hipEvent_t ready = nullptr;     // recorded on the context stream when the version's pool slot is written
   bool ready_pending = false;     // launches on other streams still wait for `ready`
   void release() {
@@ -160,6 +161,30 @@ struct TlasVersion {
     *this = TlasVersion();
   }
 };
+
+// A launch on s that read TLAS version v is noted host-side only (note_reader); when v stops being current,
+// one event per reader stream is recorded (note_swap_out): it covers every earlier launch on that stream, so a
+// later build into v orders after all of them without an event record per launch.
+hipError_t note_swap_out(TlasVersion& v) {
+  for (hipStream_t r : v.readers) {
+    hipError_t e = slot_mark_use(v.use, r);
+    if (e != hipSuccess) return e;
+  }
+  v.readers.clear();
+  return hipSuccess;
+}
+
+hipError_t note_reader(TlasVersion& v, hipStream_t s) {
+  for (hipStream_t r : v.readers)
+    if (r == s) return hipSuccess;
+  // many streams (a caller creating streams as it goes): record the uses so far now, keep the list short
+  if (v.readers.size() >= 16) {
+    hipError_t e = note_swap_out(v);
+    if (e != hipSuccess) return e;
+  }
+  v.readers.push_back(s);
+  return hipSuccess;
+}
 
 }  // namespace
 
@@ -548,6 +573,8 @@ rt_status rt_tlas_build(rt_ctx_t c, const rt_instance* in, uint32_t n, int updat
     HIPCHK(c, quiesce(c), "rt_tlas_build: wait for in-flight work");
     c->tlas_stale = true;  // until this build completes (a failure below leaves the scene unusable)
     c->cur = -1;
+    c->ver[0].readers.clear();  // every launch has completed
+    c->ver[1].readers.clear();
     size_t pool_n = 0, pool_t = 0;
     c->node_base.assign(c->blas.size(), 0);
     c->tri_base.assign(c->blas.size(), 0);
@@ -655,6 +682,8 @@ rt_status rt_tlas_build(rt_ctx_t c, const rt_instance* in, uint32_t n, int updat
   tv.ms = ms;
   tv.host.assign(in, in + n);
   tv.valid = true;
+  // the version launches read until now: its readers' events, recorded now, cover every launch that read it
+  if (c->cur >= 0 && c->cur != w) HIPCHK(c, note_swap_out(c->ver[c->cur]), "rt_tlas_build: record the readers");
   c->cur = w;
   c->tlas_stale = false;
   c->tlas_wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
@@ -913,7 +942,7 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
   hipError_t e = rt::launch_trace_frame(sv, c->fp, d_rows, rgba8, rgba32f, c->d_stats, c->stats_on,
                                         c->schedule, s);
   if (e != hipSuccess) return hip_fail(c, e, "trace launch");
-  HIPCHK(c, slot_mark_use(c->ver[c->cur].use, s), "rt_dispatch_rays: record use");
+  HIPCHK(c, note_reader(c->ver[c->cur], s), "rt_dispatch_rays: record use");
   if (ovf_slot) HIPCHK(c, slot_mark_use(*ovf_slot, s), "overflow stack: record use");
   if (c->stats_on) {
     c->dispatches += 1;
@@ -1094,7 +1123,7 @@ rt_status rt_trace_rays(rt_ctx_t c, const float* rays, uint32_t n, uint32_t ray_
   hipError_t e = rt::launch_trace_rays(sv, rays, n, (ray_flags & RT_RAY_FLAG_ACCEPT_FIRST_HIT_AND_END_SEARCH) != 0,
                                        cull_back || cull_front, hits, uv, c->d_stats, c->stats_on, s);
   if (e != hipSuccess) return hip_fail(c, e, "trace_rays launch");
-  HIPCHK(c, slot_mark_use(c->ver[c->cur].use, s), "rt_trace_rays: record use");
+  HIPCHK(c, note_reader(c->ver[c->cur], s), "rt_trace_rays: record use");
   if (ovf_slot) HIPCHK(c, slot_mark_use(*ovf_slot, s), "overflow stack: record use");
   return RT_OK;
 }

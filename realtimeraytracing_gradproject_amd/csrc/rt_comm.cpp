@@ -4,18 +4,21 @@
 // each with its own rt_ctx and the full scene; nothing but finished strips crosses xGMI.
 //
 // The frame being tiled is the reference's DispatchRays W x H (D3D12HelloTriangle.cpp:584-592),
-// issued once per OnRender (:436-471). The whole step is issued from C++ (render on the caller's
-// stream, gather + assembly on the communicator's stream, device-side events between them), so a
-// step costs one call of host issue instead of a Python loop of collectives.
+// issued once per OnRender (:436-471). The whole step is issued from C++, so a step costs one call of
+// host issue instead of a Python loop of collectives.
+//
+// Two host threads issue a step. The caller's thread renders the slot on its render stream and records the
+// render event; the communicator's issue thread orders the gather after it (one device-side wait), issues the
+// ncclGather on the gather stream and records its completion. The step's tail goes back to the slot's render
+// stream, issued by the caller's thread at its next call (or at rt_comm_stream / rt_comm_synchronize): a wait
+// for that gather, then rank 0's assembly. So the gather stream carries nothing but the gathers, and the
+// slot's next render on its stream follows its tail in stream order (no release event). HIP and RCCL host
+// calls cost microseconds each, so the calls of a step are split over the two threads. With the
+// communicator's own render streams (render_stream NULL), the gather stream and the three render streams sit
+// on the four hardware queues (GPU_MAX_HW_QUEUES), so no render queues behind a gather.
 //
 // RCCL is bound at run time (dlopen of librccl.so.1): a process that already loaded RCCL (torch)
 // shares that copy, and a context that never creates a communicator never loads it.
-//
-// Two host threads issue a step: the caller's thread renders (wait for the slot, dispatch, record the
-// render event) and hands the slot to the communicator's issue thread, which orders the gather after
-// the render, issues the ncclGather and the assembly and records the slot's release. HIP and RCCL host
-// calls cost microseconds each, so one thread issuing both halves limited a step to their sum (≈ 26 us
-// measured, tools/native_strips_cost.py); split, a step costs the longer half.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -25,6 +28,7 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include <atomic>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
@@ -74,11 +78,19 @@ RcclApi& rccl() {
 struct Slot {
   void* local = nullptr;     // this rank's strips, compact: rows_per_rank x W RGBA8
   void* gathered = nullptr;  // rank 0: nranks x rows_per_rank x W RGBA8
-  hipEvent_t rendered = nullptr, freed = nullptr;
+  hipEvent_t rendered = nullptr;  // on the slot's render stream, after its render
+  hipEvent_t gathered_ev = nullptr;  // on the gather stream, after its gather
+  hipEvent_t moved = nullptr;     // recorded on demand (a slot moved to another stream)
+  hipStream_t last = nullptr;     // the stream of the slot's last step (caller thread)
   bool used = false;
+  // the stream and frame of the slot's last assembly, an event recorded on demand (caller thread)
+  hipStream_t asm_stream = nullptr;
+  void* asm_frame = nullptr;
+  hipEvent_t asm_order = nullptr;
 };
 
-constexpr uint32_t kSlots = 4;  // frames in the render -> gather pipeline (frames in flight <= 4, bench.py)
+// frames in the pipeline (frames in flight <= 3; bench.py passes NULL, the communicator's streams)
+constexpr uint32_t kSlots = 3;
 
 hipEvent_t pipeline_event() {
   hipEvent_t e = nullptr;
@@ -92,6 +104,7 @@ hipEvent_t pipeline_event() {
 struct Job {
   uint32_t slot;
   void* frame_out;
+  hipStream_t rs;  // the slot's render stream: its assembly runs there
   uint32_t W, H, strip, rows_per_rank;
   uint64_t seq;
 };
@@ -101,11 +114,12 @@ struct rt_comm {
   int device = 0;
   uint32_t nranks = 1, rank = 0;
   ncclComm_t comm = nullptr;
-  hipStream_t stream = nullptr;  // gathers + assembly
-  // the communicator's own render streams (render_stream NULL: slot k renders on rstreams[k % kRenderStreams]),
-  // created right after `stream`, so the four take four different hardware queues (HIP deals a process's
-  // streams over GPU_MAX_HW_QUEUES = 4 queues in creation order): no render shares the gathers' queue
-  hipStream_t rstreams[3] = {nullptr, nullptr, nullptr};
+  hipStream_t stream = nullptr;  // the gathers
+  // the communicator's own render streams (render_stream NULL: slot k renders on rstreams[k]), created right
+  // after `stream`, so the four take four different hardware queues (HIP deals a process's streams over
+  // GPU_MAX_HW_QUEUES = 4 queues in creation order): no render shares the gathers' queue
+  hipStream_t rstreams[kSlots] = {nullptr, nullptr, nullptr};
+  hipEvent_t join[kSlots] = {nullptr, nullptr, nullptr};  // rt_comm_stream's joins
   std::string err;
   // frame geometry of the slots (re-planned when it changes)
   uint32_t W = 0, H = 0, strip = 0, rows_per_rank = 0;
@@ -113,7 +127,7 @@ struct rt_comm {
   uint32_t* d_rows = nullptr;  // ... on the device (uploaded once per plan)
   // RT_COMM_TIMING=1 (diagnostics): host time per part of rt_render_strips, printed by rt_comm_destroy
   bool timing = false;
-  double t_parts[5] = {0, 0, 0, 0, 0};
+  double t_parts[6] = {0, 0, 0, 0, 0, 0};
   uint64_t t_calls = 0;
   Slot slots[kSlots];
   uint64_t next = 0;
@@ -121,14 +135,20 @@ struct rt_comm {
   std::thread worker;
   std::mutex mu;
   std::condition_variable cv_job, cv_done;
+  std::atomic<uint64_t> posted{0};     // jobs handed over (read by the issue thread while it spins)
+  std::atomic<bool> sleeping{false};   // the issue thread waits on cv_job (the caller notifies only then)
   std::deque<Job> jobs;
   uint64_t issued = 0;          // jobs handed over (caller thread)
-  uint64_t done = 0;            // jobs whose gather, assembly and release are enqueued (issue thread)
-  uint64_t slot_seq[kSlots] = {0, 0, 0, 0};  // the last job of each slot
+  uint64_t done = 0;            // jobs whose gather (and its event) are enqueued (issue thread)
+  uint64_t slot_seq[kSlots] = {0, 0, 0};  // the last job of each slot
+  // the step whose tail (back on its render stream: the wait for its gather, rank 0's assembly) the caller
+  // thread issues at its next call, once the issue thread has enqueued the gather
+  bool pend = false;
+  Job pend_job{};
   bool stop = false;
   rt_status werr = RT_OK;       // the issue thread's first failure, returned by the next call
   std::string wmsg;
-  double w_parts[3] = {0, 0, 0};  // RT_COMM_TIMING: issue-thread hand-off, ncclGather, assembly + record
+  double w_parts[3] = {0, 0, 0};  // RT_COMM_TIMING: issue-thread hand-off, ncclGather, gather event
 };
 
 namespace {
@@ -148,22 +168,32 @@ void release_slots(rt_comm* c) {
   for (Slot& s : c->slots) {
     if (s.local) (void)hipFree(s.local);
     if (s.gathered) (void)hipFree(s.gathered);
-    if (s.rendered) (void)hipEventDestroy(s.rendered);
-    if (s.freed) (void)hipEventDestroy(s.freed);
+    for (hipEvent_t e : {s.rendered, s.gathered_ev, s.moved, s.asm_order})
+      if (e) (void)hipEventDestroy(e);
     s = Slot();
   }
 }
 
-// (re)plans the strips of a W x H frame and sizes the pipeline slots; waits for the slots' last uses
 void wait_issued(rt_comm* c, uint64_t seq);
+rt_status issue_tail(rt_comm* c);
 
-rt_status plan(rt_comm* c, uint32_t W, uint32_t H, uint32_t strip) {
-  if (c->W == W && c->H == H && c->strip == strip) return RT_OK;
+// waits (host) for every step handed over so far: its gather on the gather stream, its assembly on its
+// render stream
+rt_status drain(rt_comm* c) {
+  rt_status st = issue_tail(c);
+  if (st != RT_OK) return st;
   wait_issued(c, c->issued);
   if (c->stream && hipStreamSynchronize(c->stream) != hipSuccess) return cfail(c, RT_E_HIP, "rt_render_strips: drain");
   for (Slot& s : c->slots)
-    if (s.used && s.freed && hipEventSynchronize(s.freed) != hipSuccess)
-      return cfail(c, RT_E_HIP, "rt_render_strips: drain");
+    if (s.used && hipStreamSynchronize(s.last) != hipSuccess) return cfail(c, RT_E_HIP, "rt_render_strips: drain");
+  return RT_OK;
+}
+
+// (re)plans the strips of a W x H frame and sizes the pipeline slots; waits for the slots' last uses
+rt_status plan(rt_comm* c, uint32_t W, uint32_t H, uint32_t strip) {
+  if (c->W == W && c->H == H && c->strip == strip) return RT_OK;
+  rt_status st = drain(c);
+  if (st != RT_OK) return st;
   release_slots(c);
   c->W = c->H = c->strip = 0;
   const uint32_t n = rt_strip_rows(H, c->nranks, c->rank, strip, nullptr, 0);
@@ -181,7 +211,8 @@ rt_status plan(rt_comm* c, uint32_t W, uint32_t H, uint32_t strip) {
     if (hipMalloc(&s.local, local_bytes) != hipSuccess) return cfail(c, RT_E_OOM, "rt_render_strips: hipMalloc(local)");
     if (c->rank == 0 && hipMalloc(&s.gathered, local_bytes * c->nranks) != hipSuccess)
       return cfail(c, RT_E_OOM, "rt_render_strips: hipMalloc(gathered)");
-    if (!(s.rendered = pipeline_event()) || !(s.freed = pipeline_event()))
+    if (!(s.rendered = pipeline_event()) || !(s.gathered_ev = pipeline_event()) || !(s.moved = pipeline_event()) ||
+        !(s.asm_order = pipeline_event()))
       return cfail(c, RT_E_HIP, "rt_render_strips: events");
   }
   c->W = W;
@@ -190,15 +221,22 @@ rt_status plan(rt_comm* c, uint32_t W, uint32_t H, uint32_t strip) {
   return RT_OK;
 }
 
-// issue thread: for each handed-over slot, the gather side of the step on the communicator's stream
+// issue thread: for each handed-over slot, the gather half of the step on the gather stream
 void issue_loop(rt_comm* c) {
   (void)hipSetDevice(c->device);
   using clk = std::chrono::steady_clock;
   while (true) {
     Job j;
     {
+      // spin briefly for the next hand-over (a futex sleep + wake costs microseconds per step at frame
+      // rates), then sleep until notified
+      const uint64_t seen = c->done;
+      const auto spin_end = clk::now() + std::chrono::microseconds(200);
+      while (c->posted.load(std::memory_order_acquire) == seen && clk::now() < spin_end) __builtin_ia32_pause();
       std::unique_lock<std::mutex> lk(c->mu);
+      c->sleeping.store(true, std::memory_order_seq_cst);
       c->cv_job.wait(lk, [c] { return c->stop || !c->jobs.empty(); });
+      c->sleeping.store(false, std::memory_order_relaxed);
       if (c->jobs.empty()) return;  // stop requested and nothing left
       j = c->jobs.front();
       c->jobs.pop_front();
@@ -208,7 +246,7 @@ void issue_loop(rt_comm* c) {
     Slot& s = c->slots[j.slot];
     rt_status st = RT_OK;
     std::string msg;
-    if (hipStreamWaitEvent(c->stream, s.rendered, 0) != hipSuccess) {
+    if (j.rs != c->stream && hipStreamWaitEvent(c->stream, s.rendered, 0) != hipSuccess) {
       st = RT_E_HIP;
       msg = "rt_render_strips: render -> gather hand-off";
     }
@@ -222,17 +260,10 @@ void issue_loop(rt_comm* c) {
       }
     }
     if (c->timing) t2 = clk::now();
-    if (st == RT_OK && c->rank == 0) {
-      // the launcher itself, not rt_assemble_strips: the caller's thread owns the context's state
-      const hipError_t e = rt::launch_assemble_strips(j.W, j.H, c->nranks, j.strip, s.gathered, j.frame_out, c->stream);
-      if (e != hipSuccess) {
-        st = RT_E_HIP;
-        msg = std::string("rt_render_strips: assembly: ") + hipGetErrorString(e);
-      }
-    }
-    if (st == RT_OK && hipEventRecord(s.freed, c->stream) != hipSuccess) {
+    // the gather's completion, for the step's tail on the slot's render stream (issue_tail, caller thread)
+    if (st == RT_OK && j.rs != c->stream && hipEventRecord(s.gathered_ev, c->stream) != hipSuccess) {
       st = RT_E_HIP;
-      msg = "rt_render_strips: record";
+      msg = "rt_render_strips: record gather";
     }
     if (c->timing) {
       t3 = clk::now();
@@ -256,6 +287,30 @@ void issue_loop(rt_comm* c) {
 void wait_issued(rt_comm* c, uint64_t seq) {
   std::unique_lock<std::mutex> lk(c->mu);
   c->cv_done.wait(lk, [c, seq] { return c->done >= seq; });
+}
+
+// caller thread: the pending step's tail on its render stream, behind its gather (device-side wait): rank 0
+// assembles the frame there, off the gather stream, and the slot's next render on that stream follows
+rt_status issue_tail(rt_comm* c) {
+  if (!c->pend) return RT_OK;
+  const Job& j = c->pend_job;
+  c->pend = false;
+  wait_issued(c, j.seq);
+  Slot& s = c->slots[j.slot];
+  if (j.rs != c->stream && hipStreamWaitEvent(j.rs, s.gathered_ev, 0) != hipSuccess)
+    return cfail(c, RT_E_HIP, "rt_render_strips: gather -> render stream hand-off");
+  if (c->rank != 0) return RT_OK;
+  // two assemblies into one frame buffer on different streams stay in call order
+  for (Slot& o : c->slots) {
+    if (&o == &s || o.asm_frame != j.frame_out || !o.asm_stream || o.asm_stream == j.rs) continue;
+    if (hipEventRecord(o.asm_order, o.asm_stream) != hipSuccess || hipStreamWaitEvent(j.rs, o.asm_order, 0) != hipSuccess)
+      return cfail(c, RT_E_HIP, "rt_render_strips: order after an assembly into the same frame");
+  }
+  const hipError_t e = rt::launch_assemble_strips(j.W, j.H, c->nranks, j.strip, s.gathered, j.frame_out, j.rs);
+  if (e != hipSuccess) return cfail(c, RT_E_HIP, std::string("rt_render_strips: assembly: ") + hipGetErrorString(e));
+  s.asm_stream = j.rs;
+  s.asm_frame = j.frame_out;
+  return RT_OK;
 }
 
 rt_status worker_status(rt_comm* c) {
@@ -305,10 +360,13 @@ rt_status rt_comm_init(rt_ctx_t ctx, uint32_t nranks, uint32_t rank, const void*
     for (hipStream_t& r : c->rstreams)
       if (r) (void)hipStreamDestroy(r);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    for (hipEvent_t& j : c->join)
+      if (j) (void)hipEventDestroy(j);
   };
   bool ok = hipSetDevice(c->device) == hipSuccess &&
             hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
   for (hipStream_t& r : c->rstreams) ok = ok && hipStreamCreateWithFlags(&r, hipStreamNonBlocking) == hipSuccess;
+  for (hipEvent_t& j : c->join) ok = ok && (j = pipeline_event()) != nullptr;
   if (!ok) {
     destroy_streams();
     delete c;
@@ -336,17 +394,15 @@ rt_status rt_comm_destroy(rt_comm_t c) {
   c->cv_job.notify_all();
   if (c->worker.joinable()) c->worker.join();  // the issue thread drains its queue first
   (void)hipSetDevice(c->device);
-  (void)hipStreamSynchronize(c->stream);
-  for (Slot& s : c->slots)
-    if (s.used && s.freed) (void)hipEventSynchronize(s.freed);
+  (void)drain(c);
   if (c->timing && c->t_calls)
     std::fprintf(stderr, "rt_comm timing, caller thread (us per rt_render_strips over %llu calls): plan+checks %.2f, "
-                 "render %.2f, record+hand-over %.2f, wait for the slot's hand-off %.2f, stream wait %.2f\n",
-                 (unsigned long long)c->t_calls,
+                 "render %.2f, record+hand-over %.2f, wait for the slot's last step %.2f, move to another stream %.2f, "
+                 "previous step's tail %.2f\n", (unsigned long long)c->t_calls,
                  c->t_parts[0] / c->t_calls, c->t_parts[1] / c->t_calls, c->t_parts[2] / c->t_calls,
-                 c->t_parts[3] / c->t_calls, c->t_parts[4] / c->t_calls);
+                 c->t_parts[3] / c->t_calls, c->t_parts[4] / c->t_calls, c->t_parts[5] / c->t_calls);
   if (c->timing && c->t_calls)
-    std::fprintf(stderr, "rt_comm timing, issue thread (us per step): hand-off %.2f, ncclGather %.2f, assembly+record "
+    std::fprintf(stderr, "rt_comm timing, issue thread (us per step): hand-off %.2f, ncclGather %.2f, gather event "
                  "%.2f\n", c->w_parts[0] / c->t_calls, c->w_parts[1] / c->t_calls, c->w_parts[2] / c->t_calls);
   if (c->comm) (void)rccl().commDestroy(c->comm);
   release_slots(c);
@@ -355,6 +411,7 @@ rt_status rt_comm_destroy(rt_comm_t c) {
     (void)hipStreamDestroy(r);
   }
   (void)hipStreamDestroy(c->stream);
+  for (hipEvent_t j : c->join) (void)hipEventDestroy(j);
   delete c;
   return RT_OK;
 }
@@ -363,17 +420,33 @@ const char* rt_comm_last_error(rt_comm_t c) { return c ? c->err.c_str() : "null 
 
 void* rt_comm_stream(rt_comm_t c) {
   if (!c) return nullptr;
-  wait_issued(c, c->issued);  // every step handed over so far is enqueued on the stream returned
+  if (issue_tail(c) != RT_OK) return nullptr;
+  wait_issued(c, c->issued);  // every step handed over so far is enqueued
+  (void)hipSetDevice(c->device);
+  // join: the stream returned (the gathers') waits, on the device, for the slots' render streams, where the
+  // assemblies run
+  hipStream_t seen[kSlots];
+  uint32_t k = 0;
+  for (const Slot& s : c->slots) {
+    if (!s.used || s.last == c->stream) continue;
+    bool dup = false;
+    for (uint32_t i = 0; i < k; ++i) dup = dup || seen[i] == s.last;
+    if (dup) continue;
+    if (hipEventRecord(c->join[k], s.last) != hipSuccess || hipStreamWaitEvent(c->stream, c->join[k], 0) != hipSuccess) {
+      cfail(c, RT_E_HIP, "rt_comm_stream: join");
+      return nullptr;
+    }
+    seen[k++] = s.last;
+  }
   return (void*)c->stream;
 }
 
 rt_status rt_comm_synchronize(rt_comm_t c) {
   if (!c) return RT_E_INVALID;
-  wait_issued(c, c->issued);
   (void)hipSetDevice(c->device);
-  rt_status st = worker_status(c);
+  rt_status st = drain(c);
   if (st != RT_OK) return st;
-  return hipStreamSynchronize(c->stream) == hipSuccess ? RT_OK : cfail(c, RT_E_HIP, "rt_comm_synchronize");
+  return worker_status(c);
 }
 
 rt_status rt_render_strips(rt_comm_t c, uint32_t W, uint32_t H, uint32_t strip_rows, void* frame_out,
@@ -395,19 +468,22 @@ rt_status rt_render_strips(rt_comm_t c, uint32_t W, uint32_t H, uint32_t strip_r
   (void)hipSetDevice(c->device);
   if ((st = plan(c, W, H, strip_rows)) != RT_OK) return st;
   const uint32_t si = (uint32_t)(c->next % kSlots);
-  hipStream_t rs = render_stream ? (hipStream_t)render_stream : c->rstreams[si % 3];
+  hipStream_t rs = render_stream ? (hipStream_t)render_stream : c->rstreams[si];
   Slot& s = c->slots[si];
   if (!c->rows.empty() && (st = rt::check_dispatch(c->ctx, W, H, s.local)) != RT_OK)
     return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));
   ++c->next;
   lap(0);
-  // the slot's previous frame must have left it: its release is recorded by the issue thread (wait for
-  // that, rarely: four slots), then this stream waits for it on the device
+  // the slot's previous frame must have left it: the issue thread has enqueued the tail of that step on the
+  // slot's stream (wait for that, rarely: the issue thread keeps up), so a render on the same stream follows
+  // it in stream order; a slot moved to another stream waits for it with an event
   if (s.used) {
+    if (c->pend && c->pend_job.slot == si && (st = issue_tail(c)) != RT_OK) return st;
     wait_issued(c, c->slot_seq[si]);
     lap(3);
-    if (hipStreamWaitEvent(rs, s.freed, 0) != hipSuccess)
-      return cfail(c, RT_E_HIP, "rt_render_strips: order after the slot's last gather");
+    if (s.last != rs &&
+        (hipEventRecord(s.moved, s.last) != hipSuccess || hipStreamWaitEvent(rs, s.moved, 0) != hipSuccess))
+      return cfail(c, RT_E_HIP, "rt_render_strips: order after the slot's last step");
     lap(4);
   }
   if (!c->rows.empty()) {
@@ -415,16 +491,26 @@ rt_status rt_render_strips(rt_comm_t c, uint32_t W, uint32_t H, uint32_t strip_r
     if (st != RT_OK) return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));
   }
   lap(1);
-  if (hipEventRecord(s.rendered, rs) != hipSuccess) return cfail(c, RT_E_HIP, "rt_render_strips: record render");
+  if (rs != c->stream && hipEventRecord(s.rendered, rs) != hipSuccess)
+    return cfail(c, RT_E_HIP, "rt_render_strips: record render");
   s.used = true;
+  s.last = rs;
+  Job job{si, frame_out, rs, W, H, strip_rows, c->rows_per_rank, 0};
   {
     std::lock_guard<std::mutex> lk(c->mu);
-    const uint64_t seq = ++c->issued;
-    c->slot_seq[si] = seq;
-    c->jobs.push_back(Job{si, frame_out, W, H, strip_rows, c->rows_per_rank, seq});
+    job.seq = ++c->issued;
+    c->slot_seq[si] = job.seq;
+    c->jobs.push_back(job);
+    c->posted.store(job.seq, std::memory_order_release);
   }
-  c->cv_job.notify_one();
+  if (c->sleeping.load(std::memory_order_seq_cst)) c->cv_job.notify_one();
   lap(2);
+  // the previous step's tail (its gather is enqueued by now, or soon), then this step's is pending
+  st = issue_tail(c);
+  lap(5);
+  c->pend = true;
+  c->pend_job = job;
+  if (st != RT_OK) return st;
   ++c->t_calls;
   return RT_OK;
 }

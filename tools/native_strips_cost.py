@@ -71,8 +71,12 @@ def main():
         freed[s].record(cstream.cuda_stream)
         used[s] = True
 
+    ncall = [0]  # the library's slot is its call count mod 3: stream i serves slot i (no slot moves streams)
+
     def native_step(k, nstream):
-        comm.render_strips(W, H, frames[k % nslot], streams[(k % nslot) % nstream].cuda_stream)
+        si = ncall[0] % 3
+        ncall[0] += 1
+        comm.render_strips(W, H, frames[si], streams[si % nstream].cuda_stream)
 
     def sync():
         comm.synchronize()  # the library's issue thread has enqueued every handed-over gather
@@ -102,7 +106,9 @@ def main():
     out["native_step_3streams"] = measure(native_step, 3)
 
     def native_own(k, nstream):  # render_stream NULL: the communicator's own three render streams
-        comm.render_strips(W, H, frames[k % nslot], None)
+        si = ncall[0] % 3
+        ncall[0] += 1
+        comm.render_strips(W, H, frames[si], None)
     out["native_step_library_streams"] = measure(native_own, 3)
     # host cost of the call alone while the GPU is idle-free: the render itself issued alone
     t0 = time.perf_counter()
