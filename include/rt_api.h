@@ -285,18 +285,23 @@ rt_status rt_comm_get_unique_id(void* id_out);
 rt_status rt_comm_init(rt_ctx_t ctx, uint32_t nranks, uint32_t rank, const void* id, rt_comm_t* out);
 rt_status rt_comm_destroy(rt_comm_t comm);
 const char* rt_comm_last_error(rt_comm_t comm);
-/* hipStream_t of the communicator: the gathers and rank 0's assembly run on it. */
+/* The communicator's gather stream, made to wait (on the device) for every step issued so far, the
+ * assemblies on the render streams included: work the caller enqueues on it after this call sees rank 0's
+ * frames complete. */
 void* rt_comm_stream(rt_comm_t comm);
 rt_status rt_comm_synchronize(rt_comm_t comm);
 /* One tiled frame, collective over the ranks (every rank calls it, in the same frame order): this rank's
- * strips are rendered on render_stream into one of the communicator's pipeline slots (NULL: the communicator's
- * own three render streams in turn, created beside its gather stream so that each sits on a hardware queue of
- * its own: no render waits behind a gather in a shared queue); the communicator's stream waits for that render (a device-side event), gathers the slots of all ranks
- * into rank 0 and, on rank 0, assembles the W x H RGBA8 frame into frame_out (device buffer; ignored on other
- * ranks). A slot is re-rendered only after its gather and assembly finished (device-side events; no host
- * waits), so consecutive calls overlap frame k's gather with frame k + 1's render, and renders issued on
- * different streams overlap each other (frames in flight). Asynchronous: frame_out is complete once the work
- * issued so far on rt_comm_stream(comm) has finished. */
+ * strips are rendered on render_stream into one of the communicator's three pipeline slots (NULL: slot k's own
+ * stream of the communicator; its three render streams and its gather stream sit on separate hardware
+ * queues). The gather stream waits for that render (a device-side event) and runs ONE ncclGather of every
+ * rank's slot into rank 0; the step's tail returns to render_stream: a wait for that gather and, on rank 0, the
+ * assembly of the W x H RGBA8 frame into frame_out (device buffer; ignored on other ranks). The tail is issued
+ * by the next call (or by rt_comm_stream / rt_comm_synchronize). The slot's next render on the same stream
+ * follows its tail in stream order; a slot moved to another stream, and two assemblies into one frame_out on
+ * different streams, are ordered by events. No host waits: frame k's gather overlaps frame k + 1's render, and
+ * frames on different streams overlap (frames in flight). Asynchronous: frame_out is complete once the work
+ * enqueued on rt_comm_stream(comm) after that call has run, or after rt_comm_synchronize. Streams passed must
+ * stay valid until then. */
 rt_status rt_render_strips(rt_comm_t comm, uint32_t W, uint32_t H, uint32_t strip_rows, void* frame_out,
                            void* render_stream);
 
