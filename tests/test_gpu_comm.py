@@ -38,3 +38,30 @@ def test_render_strips_world1_equals_oracle():
         comm.render_strips(spec.width, spec.height, None)  # rank 0 needs the frame buffer
     comm.close()
     c.close()
+
+
+def test_render_strips_moved_slots_shared_frames_and_join():
+    """Slots moved between caller streams (events), two frame buffers shared by six frames on three streams (the
+    assemblies into one buffer stay in call order, so each holds its LAST frame), a camera change per frame, and
+    completion seen through rt_comm_stream alone (it joins the render streams, where the assemblies run)."""
+    base = scenes.config("C2F").with_size(480, 272)
+    c = rt.Context(0)
+    scenes.upload(c, base)
+    comm = rt.Comm(c, 1, 0, rt.comm_unique_id())
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    bufs = [torch.zeros((base.height, base.width, 4), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    eyes = [(1.5 + 0.4 * k, 1.2 + 0.1 * k, 3.5 - 0.3 * k) for k in range(6)]
+    order = [2, 0, 1, 1, 0, 2]  # call k's stream: slot k % 3 lands on another stream than its last use
+    specs = []
+    for k in range(6):
+        sp = base.with_size(base.width, base.height)
+        sp.camera = (eyes[k], (0.0, 0.5, 0.0), (0.0, 1.0, 0.0))
+        specs.append(sp)
+        c.set_camera(sp.camera_buffer())
+        comm.render_strips(sp.width, sp.height, bufs[k % 2], streams[order[k]].cuda_stream)
+    torch.cuda.ExternalStream(comm.stream).synchronize()  # no rt_comm_synchronize: the join alone
+    for b, last in ((0, 4), (1, 5)):
+        o8, _, _ = oracle.Scene(specs[last]).render_spec(specs[last], nthreads=16, want_float=False, schedule=1)
+        assert np.array_equal(bufs[b].cpu().numpy(), o8), f"buffer {b} != frame {last}"
+    comm.close()
+    c.close()
