@@ -195,6 +195,226 @@ static void wwalk(const otri* tris, const vec3* o, const vec3* d, const int* ali
   }
 }
 
+/* --- sweep-SAH binary tree over the LBVH's leaves (design study: the quality gap of the Morton build) --- */
+typedef struct { int ref; float b[6]; float c[3]; } sleaf;
+static sleaf* s_lv;
+static onode* s_out;
+static int s_n;
+static int s_axis;
+static int s_cmp(const void* a, const void* b) {
+  float x = ((const sleaf*)a)->c[s_axis], y = ((const sleaf*)b)->c[s_axis];
+  return x < y ? -1 : x > y ? 1 : (((const sleaf*)a)->ref < ((const sleaf*)b)->ref ? -1 : 1);
+}
+static void s_box(const sleaf* v, int n, float* bb) {
+  for (int a = 0; a < 3; ++a) { bb[a] = INFINITY; bb[3 + a] = -INFINITY; }
+  for (int i = 0; i < n; ++i)
+    for (int a = 0; a < 3; ++a) { bb[a] = fminf(bb[a], v[i].b[a]); bb[3 + a] = fmaxf(bb[3 + a], v[i].b[3 + a]); }
+}
+/* returns the child ref (node index >= 0, or the leaf's ~tri ref) of the subtree over v[0, n) */
+static int s_build(sleaf* v, int n) {
+  if (n == 1) return v[0].ref;
+  float* rarea = (float*)malloc((size_t)n * 4);
+  int best_axis = 0, best_i = n / 2;
+  float best = INFINITY;
+  for (int a = 0; a < 3; ++a) {
+    s_axis = a;
+    qsort(v, (size_t)n, sizeof(sleaf), s_cmp);
+    float bb[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    for (int i = n - 1; i > 0; --i) {
+      for (int k = 0; k < 3; ++k) { bb[k] = fminf(bb[k], v[i].b[k]); bb[3 + k] = fmaxf(bb[3 + k], v[i].b[3 + k]); }
+      rarea[i] = half_area(bb);
+    }
+    float lb[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    for (int i = 1; i < n; ++i) {
+      for (int k = 0; k < 3; ++k) { lb[k] = fminf(lb[k], v[i - 1].b[k]); lb[3 + k] = fmaxf(lb[3 + k], v[i - 1].b[3 + k]); }
+      float c = half_area(lb) * (float)i + rarea[i] * (float)(n - i);
+      if (c < best) { best = c; best_axis = a; best_i = i; }
+    }
+  }
+  free(rarea);
+  s_axis = best_axis;
+  qsort(v, (size_t)n, sizeof(sleaf), s_cmp);
+  const int me = s_n++;
+  float l[6], r[6];
+  s_box(v, best_i, l);
+  s_box(v + best_i, n - best_i, r);
+  const int c0 = s_build(v, best_i);
+  const int c1 = s_build(v + best_i, n - best_i);
+  onode* o = &s_out[me];
+  memset(o, 0, sizeof(*o));
+  for (int a = 0; a < 3; ++a) { o->lo0[a] = l[a]; o->hi0[a] = l[3 + a]; o->lo1[a] = r[a]; o->hi1[a] = r[3 + a]; }
+  o->c0 = c0;
+  o->c1 = c1;
+  return me;
+}
+/* replaces the kept binary LBVH with a sweep-SAH tree over the same leaves (same triangle refs) */
+int wide_study_sah(void) {
+  if (!g_bin) return 1;
+  const onode* bin = (const onode*)g_bin;
+  s_lv = (sleaf*)malloc(((size_t)g_nbin + 2) * sizeof(sleaf));
+  int nl = 0;
+  for (uint32_t i = 0; i < g_nbin; ++i)
+    for (int side = 0; side < 2; ++side) {
+      const int c = side ? bin[i].c1 : bin[i].c0;
+      if (c >= 0 || c == O_EMPTY) continue;
+      sleaf* L = &s_lv[nl++];
+      L->ref = c;
+      const float* lo = side ? bin[i].lo1 : bin[i].lo0;
+      const float* hi = side ? bin[i].hi1 : bin[i].hi0;
+      for (int a = 0; a < 3; ++a) { L->b[a] = lo[a]; L->b[3 + a] = hi[a]; L->c[a] = 0.5f * (lo[a] + hi[a]); }
+    }
+  s_out = (onode*)calloc((size_t)nl + 2, sizeof(onode));
+  s_n = 0;
+  s_build(s_lv, nl);
+  free(s_lv);
+  free(g_bin);
+  g_bin = s_out;
+  g_nbin = (uint32_t)s_n;
+  return 0;
+}
+
+/* --- treelet restructuring of the binary LBVH (Karras & Aila 2013), design study ------------------------
+ * cost of a subtree = sum of its internal nodes' half areas (every leaf is one triangle, so the leaves' terms are
+ * the same in any topology); each node, children before parents, regroups the up to 7 subtrees under its treelet
+ * (grown by opening the largest-area internal leaf, lowest position on ties) into the cost-optimal binary
+ * topology (DP over the subsets), reusing the treelet's node slots. */
+#define TL 7
+static float t_box_area(const float* b) { return half_area(b); }
+static void t_union(const float* a, const float* b, float* o) {
+  for (int k = 0; k < 3; ++k) { o[k] = fminf(a[k], b[k]); o[3 + k] = fmaxf(a[3 + k], b[3 + k]); }
+}
+static float* t_cost; /* per binary node: its subtree cost */
+static void t_node_box(const onode* b, float* bb) {
+  for (int a = 0; a < 3; ++a) { bb[a] = fminf(b->lo0[a], b->lo1[a]); bb[3 + a] = fmaxf(b->hi0[a], b->hi1[a]); }
+}
+static void t_restructure(onode* bin, int n) {
+  int lref[TL];
+  float lbox[TL][6];
+  int internal[TL];
+  int nl = 2, ni = 1;
+  internal[0] = n;
+  lref[0] = bin[n].c0;
+  lref[1] = bin[n].c1;
+  for (int a = 0; a < 3; ++a) {
+    lbox[0][a] = bin[n].lo0[a]; lbox[0][3 + a] = bin[n].hi0[a];
+    lbox[1][a] = bin[n].lo1[a]; lbox[1][3 + a] = bin[n].hi1[a];
+  }
+  while (nl < TL) {
+    int best = -1;
+    float ba = -1.0f;
+    for (int j = 0; j < nl; ++j)
+      if (lref[j] >= 0 && t_box_area(lbox[j]) > ba) { ba = t_box_area(lbox[j]); best = j; }
+    if (best < 0) break;
+    const onode* g = &bin[lref[best]];
+    internal[ni++] = lref[best];
+    lref[best] = g->c0;
+    lref[nl] = g->c1;
+    for (int a = 0; a < 3; ++a) {
+      lbox[best][a] = g->lo0[a]; lbox[best][3 + a] = g->hi0[a];
+      lbox[nl][a] = g->lo1[a]; lbox[nl][3 + a] = g->hi1[a];
+    }
+    ++nl;
+  }
+  if (nl < 3) return;
+  const int full = (1 << nl) - 1;
+  float area[1 << TL], copt[1 << TL];
+  int8_t split[1 << TL];
+  float ubox[1 << TL][6];
+  for (int m = 1; m <= full; ++m) {
+    int first = __builtin_ctz(m);
+    if ((m & (m - 1)) == 0) {
+      memcpy(ubox[m], lbox[first], 24);
+      copt[m] = lref[first] >= 0 ? t_cost[lref[first]] : 0.0f;
+      area[m] = t_box_area(lbox[first]);
+      split[m] = 0;
+      continue;
+    }
+    t_union(ubox[m & (m - 1)], lbox[first], ubox[m]);
+    area[m] = t_box_area(ubox[m]);
+  }
+  for (int m = 1; m <= full; ++m) {
+    if ((m & (m - 1)) == 0) continue;
+    /* partitions P | R with P holding m's lowest bit; the first strict minimum in ascending P */
+    const int low = m & -m, rest = m ^ low;
+    float best = INFINITY;
+    int bp = low;
+    for (int sub = rest;; sub = (sub - 1) & rest) {
+      const int P = low | sub;
+      if (P != m) {
+        const float c = copt[P] + copt[m ^ P];
+        if (c < best) { best = c; bp = P; }
+      }
+      if (sub == 0) break;
+    }
+    copt[m] = area[m] + best;
+    split[m] = (int8_t)0;
+    /* keep P in a side table: masks fit 7 bits */
+    ((int8_t*)split)[m] = (int8_t)bp;
+  }
+  /* current cost of the treelet */
+  float cur = 0.0f;
+  for (int j = 0; j < ni; ++j) { float bb[6]; t_node_box(&bin[internal[j]], bb); cur += t_box_area(bb); }
+  for (int j = 0; j < nl; ++j) cur += lref[j] >= 0 ? t_cost[lref[j]] : 0.0f;
+  if (!(copt[full] < cur)) return;
+  /* rebuild: node slots in order internal[0] (= n, the root), internal[1] ... */
+  int slot = 0;
+  int stack_m[TL * 2], stack_node[TL * 2], sp = 0;
+  stack_m[sp] = full; stack_node[sp] = internal[slot++]; ++sp;
+  while (sp) {
+    --sp;
+    const int m = stack_m[sp], nd = stack_node[sp];
+    const int P = (uint8_t)split[m], R = m ^ P;
+    int kids[2] = {P, R};
+    int refs[2];
+    for (int k = 0; k < 2; ++k) {
+      const int km = kids[k];
+      if ((km & (km - 1)) == 0) refs[k] = lref[__builtin_ctz(km)];
+      else { refs[k] = internal[slot++]; stack_m[sp] = km; stack_node[sp] = refs[k]; ++sp; }
+    }
+    onode* o = &bin[nd];
+    o->c0 = refs[0];
+    o->c1 = refs[1];
+    for (int a = 0; a < 3; ++a) {
+      o->lo0[a] = ubox[P][a]; o->hi0[a] = ubox[P][3 + a];
+      o->lo1[a] = ubox[R][a]; o->hi1[a] = ubox[R][3 + a];
+    }
+    t_cost[nd] = copt[m];
+  }
+}
+/* binary cost of the kept tree: sum of internal half areas */
+double wide_study_cost(void) {
+  const onode* bin = (const onode*)g_bin;
+  double c = 0.0;
+  for (uint32_t i = 0; i < g_nbin; ++i) { float bb[6]; t_node_box(&bin[i], bb); c += t_box_area(bb); }
+  return c;
+}
+int wide_study_treelet(int passes) {
+  if (!g_bin) return 1;
+  onode* bin = (onode*)g_bin;
+  t_cost = (float*)calloc(g_nbin, sizeof(float));
+  int* order = (int*)malloc((size_t)g_nbin * 4 + 4);
+  int* st = (int*)malloc((size_t)g_nbin * 8 + 8);
+  for (int pass = 0; pass < passes; ++pass) {
+    int top = 0, no = 0;
+    st[top++] = 0;
+    while (top) {
+      const int v = st[--top];
+      order[no++] = v;
+      if (bin[v].c0 >= 0) st[top++] = bin[v].c0;
+      if (bin[v].c1 >= 0) st[top++] = bin[v].c1;
+    }
+    for (int q = no - 1; q >= 0; --q) { /* children before parents */
+      const int v = order[q];
+      float bb[6];
+      t_node_box(&bin[v], bb);
+      t_cost[v] = t_box_area(bb) + (bin[v].c0 >= 0 ? t_cost[bin[v].c0] : 0.0f) + (bin[v].c1 >= 0 ? t_cost[bin[v].c1] : 0.0f);
+      t_restructure(bin, v);
+    }
+  }
+  free(order); free(st); free(t_cost);
+  return 0;
+}
+
 /* out: [0] primary nodes [1] primary aabb [2] primary tris [3] shadow nodes [4] shadow aabb [5] shadow tris
  *      [6] primary packets [7] shadow packets [8] wide nodes */
 int wide_study(const oracle_scene* s, const float cb[64], const oracle_light* L, uint32_t W, uint32_t H, int width,
