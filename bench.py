@@ -382,9 +382,9 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
     local = [be.zeros((rows_per_rank, W, 4)) for _ in range(nslot)]
     gathered = ([be.zeros((world, rows_per_rank, W, 4)) if rank == 0 else None for _ in range(nslot)]
                 if strips and not native else None)
-    frame = ([be.zeros((H, W, 4)) if rank == 0 else None for _ in range(3 if native else nslot)]
-             if strips else None)
     rcomm = be.comm_open(world, rank) if native else None
+    frame = ([be.zeros((H, W, 4)) if rank == 0 else None for _ in range(rcomm.depth if native else nslot)]
+             if strips else None)
     rendered = [be.sync_event() for _ in range(nslot)]
     freed = [be.sync_event() for _ in range(nslot)]
     parts = [D.gather_parts(gathered[s], world, rank) for s in range(nslot)] if strips and not native else None
@@ -394,8 +394,8 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
     def step_native(k: int):
         """One frame through rt_render_strips: render on the slot's stream, ncclGather on the communicator's
         gather stream, rank 0's assembly back on the slot's stream, the slot pipeline and its events inside the
-        library (one C call). The library's slot is its call count mod 3; frame buffer i serves slot i."""
-        s = ncall[0] % 3
+        library (one C call). The library's slot is its call count mod its depth; frame buffer i serves slot i."""
+        s = ncall[0] % rcomm.depth
         ncall[0] += 1
         # frames in flight: the communicator's own three render streams (NULL), which sit on hardware queues of
         # their own, apart from the gathers' (DESIGN §7); one frame at a time: this rank's stream
@@ -486,7 +486,7 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
         kernel_ms = render_ms
 
     if save_image and rank == 0:
-        last = (ncall[0] - 1) % 3 if native else (k - 1) % nslot
+        last = (ncall[0] - 1) % rcomm.depth if native else (k - 1) % nslot
         if native:
             rcomm.synchronize()
         img = frame[last] if strips else local[last][:H]

@@ -290,10 +290,13 @@ const char* rt_comm_last_error(rt_comm_t comm);
  * frames complete. */
 void* rt_comm_stream(rt_comm_t comm);
 rt_status rt_comm_synchronize(rt_comm_t comm);
+/* Pipeline slots (= the communicator's render streams, frames in flight with render_stream NULL): one per
+ * hardware queue beside the gather stream's (GPU_MAX_HW_QUEUES - 1, HIP's default 4 gives 3; RT_COMM_SLOTS
+ * overrides, 1..8). Call k uses slot k mod depth. */
+uint32_t rt_comm_pipeline_depth(rt_comm_t comm);
 /* One tiled frame, collective over the ranks (every rank calls it, in the same frame order): this rank's
- * strips are rendered on render_stream into one of the communicator's three pipeline slots (NULL: slot k's own
- * stream of the communicator; its three render streams and its gather stream sit on separate hardware
- * queues). The gather stream waits for that render (a device-side event) and runs ONE ncclGather of every
+ * strips are rendered on render_stream into one of the communicator's pipeline slots (NULL: slot k's own
+ * stream of the communicator; its render streams and its gather stream sit on separate hardware queues). The gather stream waits for that render (a device-side event) and runs ONE ncclGather of every
  * rank's slot into rank 0; the step's tail returns to render_stream: a wait for that gather and, on rank 0, the
  * assembly of the W x H RGBA8 frame into frame_out (device buffer; ignored on other ranks). The tail is issued
  * by the next call (or by rt_comm_stream / rt_comm_synchronize). The slot's next render on the same stream

@@ -117,6 +117,7 @@ SIGNATURES = [
     ("rt_comm_stream", _P, [_P]),
     ("rt_comm_synchronize", _I, [_P]),
     ("rt_render_strips", _I, [_P, _U32, _U32, _U32, _P, _P]),
+    ("rt_comm_pipeline_depth", _U32, [_P]),
     ("rt_stats", _I, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     ("rt_stats_reset", _I, [_P]),
     ("rt_mesh_load_obj", _I, [ctypes.c_char_p, ctypes.POINTER(_P)]),
@@ -421,8 +422,13 @@ class Comm:
 
     @property
     def stream(self) -> int:
-        """hipStream_t of the gathers and the assembly."""
+        """hipStream_t of the gathers, made to wait for every step issued so far (rt_comm_stream)."""
         return self._lib.rt_comm_stream(self._h)
+
+    @property
+    def depth(self) -> int:
+        """Pipeline slots: render_strips call k uses slot k mod depth (one render stream each)."""
+        return int(self._lib.rt_comm_pipeline_depth(self._h))
 
     def synchronize(self):
         self._check(self._lib.rt_comm_synchronize(self._h), "rt_comm_synchronize")

@@ -28,6 +28,7 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <cstring>
@@ -89,8 +90,9 @@ struct Slot {
   hipEvent_t asm_order = nullptr;
 };
 
-// frames in the pipeline (frames in flight <= 3; bench.py passes NULL, the communicator's streams)
-constexpr uint32_t kSlots = 3;
+// frames in the pipeline: one slot per render stream of the communicator, as many as the hardware queues
+// beside the gather stream's allow (GPU_MAX_HW_QUEUES - 1: 3 at HIP's default of 4), at most kMaxSlots
+constexpr uint32_t kMaxSlots = 8;
 
 hipEvent_t pipeline_event() {
   hipEvent_t e = nullptr;
@@ -118,8 +120,9 @@ struct rt_comm {
   // the communicator's own render streams (render_stream NULL: slot k renders on rstreams[k]), created right
   // after `stream`, so the four take four different hardware queues (HIP deals a process's streams over
   // GPU_MAX_HW_QUEUES = 4 queues in creation order): no render shares the gathers' queue
-  hipStream_t rstreams[kSlots] = {nullptr, nullptr, nullptr};
-  hipEvent_t join[kSlots] = {nullptr, nullptr, nullptr};  // rt_comm_stream's joins
+  uint32_t nslots = 3;
+  hipStream_t rstreams[kMaxSlots] = {};
+  hipEvent_t join[kMaxSlots] = {};  // rt_comm_stream's joins
   std::string err;
   // frame geometry of the slots (re-planned when it changes)
   uint32_t W = 0, H = 0, strip = 0, rows_per_rank = 0;
@@ -129,7 +132,7 @@ struct rt_comm {
   bool timing = false;
   double t_parts[6] = {0, 0, 0, 0, 0, 0};
   uint64_t t_calls = 0;
-  Slot slots[kSlots];
+  Slot slots[kMaxSlots];
   uint64_t next = 0;
   // the issue thread of the gather side (see the header comment)
   std::thread worker;
@@ -140,7 +143,7 @@ struct rt_comm {
   std::deque<Job> jobs;
   uint64_t issued = 0;          // jobs handed over (caller thread)
   uint64_t done = 0;            // jobs whose gather (and its event) are enqueued (issue thread)
-  uint64_t slot_seq[kSlots] = {0, 0, 0};  // the last job of each slot
+  uint64_t slot_seq[kMaxSlots] = {};  // the last job of each slot
   // the step whose tail (back on its render stream: the wait for its gather, rank 0's assembly) the caller
   // thread issues at its next call, once the issue thread has enqueued the gather
   bool pend = false;
@@ -207,7 +210,8 @@ rt_status plan(rt_comm* c, uint32_t W, uint32_t H, uint32_t strip) {
   const uint32_t nstrips = (H + strip - 1) / strip;
   c->rows_per_rank = ((nstrips + c->nranks - 1) / c->nranks) * strip;
   const size_t local_bytes = (size_t)c->rows_per_rank * W * 4;
-  for (Slot& s : c->slots) {
+  for (uint32_t k = 0; k < c->nslots; ++k) {
+    Slot& s = c->slots[k];
     if (hipMalloc(&s.local, local_bytes) != hipSuccess) return cfail(c, RT_E_OOM, "rt_render_strips: hipMalloc(local)");
     if (c->rank == 0 && hipMalloc(&s.gathered, local_bytes * c->nranks) != hipSuccess)
       return cfail(c, RT_E_OOM, "rt_render_strips: hipMalloc(gathered)");
@@ -365,8 +369,16 @@ rt_status rt_comm_init(rt_ctx_t ctx, uint32_t nranks, uint32_t rank, const void*
   };
   bool ok = hipSetDevice(c->device) == hipSuccess &&
             hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
-  for (hipStream_t& r : c->rstreams) ok = ok && hipStreamCreateWithFlags(&r, hipStreamNonBlocking) == hipSuccess;
-  for (hipEvent_t& j : c->join) ok = ok && (j = pipeline_event()) != nullptr;
+  // one render stream (and pipeline slot) per hardware queue beside the gather stream's: GPU_MAX_HW_QUEUES is
+  // HIP's queue count per process (4 by default); RT_COMM_SLOTS overrides (1..8)
+  const char* hq = std::getenv("GPU_MAX_HW_QUEUES");
+  const char* ns = std::getenv("RT_COMM_SLOTS");
+  int queues = hq && std::atoi(hq) > 0 ? std::atoi(hq) : 4;
+  int slots = ns && std::atoi(ns) > 0 ? std::atoi(ns) : queues - 1;
+  c->nslots = (uint32_t)std::min<int>((int)kMaxSlots, std::max(1, slots));
+  for (uint32_t k = 0; k < c->nslots; ++k)
+    ok = ok && hipStreamCreateWithFlags(&c->rstreams[k], hipStreamNonBlocking) == hipSuccess;
+  for (uint32_t k = 0; k < c->nslots; ++k) ok = ok && (c->join[k] = pipeline_event()) != nullptr;
   if (!ok) {
     destroy_streams();
     delete c;
@@ -407,11 +419,13 @@ rt_status rt_comm_destroy(rt_comm_t c) {
   if (c->comm) (void)rccl().commDestroy(c->comm);
   release_slots(c);
   for (hipStream_t r : c->rstreams) {
+    if (!r) continue;
     (void)hipStreamSynchronize(r);
     (void)hipStreamDestroy(r);
   }
   (void)hipStreamDestroy(c->stream);
-  for (hipEvent_t j : c->join) (void)hipEventDestroy(j);
+  for (hipEvent_t j : c->join)
+    if (j) (void)hipEventDestroy(j);
   delete c;
   return RT_OK;
 }
@@ -425,7 +439,7 @@ void* rt_comm_stream(rt_comm_t c) {
   (void)hipSetDevice(c->device);
   // join: the stream returned (the gathers') waits, on the device, for the slots' render streams, where the
   // assemblies run
-  hipStream_t seen[kSlots];
+  hipStream_t seen[kMaxSlots];
   uint32_t k = 0;
   for (const Slot& s : c->slots) {
     if (!s.used || s.last == c->stream) continue;
@@ -440,6 +454,8 @@ void* rt_comm_stream(rt_comm_t c) {
   }
   return (void*)c->stream;
 }
+
+uint32_t rt_comm_pipeline_depth(rt_comm_t c) { return c ? c->nslots : 0; }
 
 rt_status rt_comm_synchronize(rt_comm_t c) {
   if (!c) return RT_E_INVALID;
@@ -467,7 +483,7 @@ rt_status rt_render_strips(rt_comm_t c, uint32_t W, uint32_t H, uint32_t strip_r
   };
   (void)hipSetDevice(c->device);
   if ((st = plan(c, W, H, strip_rows)) != RT_OK) return st;
-  const uint32_t si = (uint32_t)(c->next % kSlots);
+  const uint32_t si = (uint32_t)(c->next % c->nslots);
   hipStream_t rs = render_stream ? (hipStream_t)render_stream : c->rstreams[si];
   Slot& s = c->slots[si];
   if (!c->rows.empty() && (st = rt::check_dispatch(c->ctx, W, H, s.local)) != RT_OK)

@@ -45,7 +45,7 @@ def main():
     scenes.upload(ctx, spec)
     comm = rt.Comm(ctx, 1, 0, rt.comm_unique_id())
     nslot = 4
-    frames = [torch.zeros((H, W, 4), dtype=torch.uint8, device=dev) for _ in range(nslot)]
+    frames = [torch.zeros((H, W, 4), dtype=torch.uint8, device=dev) for _ in range(max(nslot, comm.depth))]
     streams = [torch.cuda.Stream(dev) for _ in range(3)]
 
     # --- the former Python step (bench.py before rt_render_strips) ---------------------------------
@@ -71,10 +71,11 @@ def main():
         freed[s].record(cstream.cuda_stream)
         used[s] = True
 
-    ncall = [0]  # the library's slot is its call count mod 3: stream i serves slot i (no slot moves streams)
+    depth = comm.depth
+    ncall = [0]  # the library's slot is its call count mod depth: stream i serves slot i (no slot moves streams)
 
     def native_step(k, nstream):
-        si = ncall[0] % 3
+        si = ncall[0] % depth
         ncall[0] += 1
         comm.render_strips(W, H, frames[si], streams[si % nstream].cuda_stream)
 
@@ -98,7 +99,8 @@ def main():
             best_frame = min(best_frame, (t2 - t0) * 1e3 / a.frames)
         return {"host_issue_us_per_step": round(best_issue, 2), "ms_per_frame": round(best_frame, 4)}
 
-    out = {"config": a.config, "size": f"{W}x{H}", "frames": a.frames, "world": 1}
+    out = {"config": a.config, "size": f"{W}x{H}", "frames": a.frames, "world": 1, "pipeline_depth": comm.depth,
+           "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES")}
     with torch.cuda.stream(cstream):
         out["python_step_1stream"] = measure(py_step, 1)
         out["python_step_3streams"] = measure(py_step, 3)
@@ -106,7 +108,7 @@ def main():
     out["native_step_3streams"] = measure(native_step, 3)
 
     def native_own(k, nstream):  # render_stream NULL: the communicator's own three render streams
-        si = ncall[0] % 3
+        si = ncall[0] % depth
         ncall[0] += 1
         comm.render_strips(W, H, frames[si], None)
     out["native_step_library_streams"] = measure(native_own, 3)
