@@ -12,6 +12,8 @@
  *   mode 4  per wave, per light, rays sorted by hit instance before packing (live ones only)
  *   mode 5  per group of G waves, per light, sorted by hit instance (then pixel)
  *   mode 6  per group of G waves, per light, sorted by the 30-bit Morton code of the origin
+ *   mode 7  whole frame, per light, sorted by hit instance then origin Morton (a global wavefront sort)
+ *   mode 8  whole frame, per light, sorted by origin Morton only
  */
 #include "../oracle/rt_oracle.c"
 
@@ -76,6 +78,11 @@ int study_shadow(const oracle_scene* s, const float cb[64], const oracle_light* 
   sray* buf = (sray*)malloc(sizeof(sray) * (size_t)OPK * 16 * (G > 0 ? G : 1));
   uint64_t packets = 0, nrays = 0;
   const int gsz = (mode == 2 || mode == 3 || mode == 5 || mode == 6) ? G : 1;
+  const int global = mode == 7 || mode == 8;
+  sray* gl[16] = {0};
+  size_t gn[16] = {0};
+  if (global)
+    for (uint32_t li = 0; li < nl; ++li) gl[li] = (sray*)malloc(sizeof(sray) * (size_t)W * H);
   for (uint32_t ty = 0; ty < th; ++ty)
     for (uint32_t tx0 = 0; tx0 < tw; tx0 += (uint32_t)gsz) {
       int n_all = 0;
@@ -111,7 +118,16 @@ int study_shadow(const oracle_scene* s, const float cb[64], const oracle_light* 
           }
         }
       }
-      if (mode == 0 || mode == 2 || mode == 4 || mode == 5 || mode == 6) {
+      if (global) {
+        for (uint32_t li = 0; li < nl; ++li)
+          for (int q = 0; q < n_light[li]; ++q) {
+            sray r = tmp[li][q];
+            r.pix = (ty * tw + tx0) * OPK + (uint32_t)q;
+            const uint32_t m = morton_of(r.P);
+            r.inst = mode == 7 ? (r.inst << 20) | (m >> 10) : m;
+            gl[li][gn[li]++] = r;
+          }
+      } else if (mode == 0 || mode == 2 || mode == 4 || mode == 5 || mode == 6) {
         for (uint32_t li = 0; li < nl; ++li) {
           if (mode == 4 || mode == 5) qsort(tmp[li], (size_t)n_light[li], sizeof(sray), cmp_inst);
           if (mode == 6) {
@@ -127,6 +143,13 @@ int study_shadow(const oracle_scene* s, const float cb[64], const oracle_light* 
         packets += trace_groups(s, buf, n_all, &st);
         nrays += (uint64_t)n_all;
       }
+    }
+  if (global)
+    for (uint32_t li = 0; li < nl; ++li) {
+      qsort(gl[li], gn[li], sizeof(sray), cmp_key);
+      packets += trace_groups(s, gl[li], (int)gn[li], &st);
+      nrays += gn[li];
+      free(gl[li]);
     }
   free(buf);
   out[0] = packets;

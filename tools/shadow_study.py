@@ -15,7 +15,8 @@ sys.path.insert(0, ROOT)
 
 MODES = {0: "per wave, per light (kernel)", 1: "per wave, lights compacted", 2: "G waves, per light compacted",
          3: "G waves, lights compacted", 4: "per wave, per light, sorted by instance",
-         5: "G waves, per light, sorted by instance", 6: "G waves, per light, sorted by origin Morton"}
+         5: "G waves, per light, sorted by instance", 6: "G waves, per light, sorted by origin Morton",
+         7: "frame, per light, sorted by instance, Morton", 8: "frame, per light, sorted by origin Morton"}
 
 
 def main():
