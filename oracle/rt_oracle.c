@@ -487,10 +487,17 @@ static uint32_t lbvh(const float* primbox, uint32_t n, o4node** out4, uint32_t* 
   uint32_t* keys = (uint32_t*)malloc((size_t)n * 4);
   uint32_t* k2 = (uint32_t*)malloc((size_t)n * 4);
   uint32_t* v2 = (uint32_t*)malloc((size_t)n * 4);
+#ifdef ORACLE_STUDY_MORTON_CUBIC /* design study only (tools/morton_study.py): one scale for all axes */
+  const float cext = fmaxf(fmaxf(cb[3] - cb[0], cb[4] - cb[1]), cb[5] - cb[2]);
+#endif
   for (uint32_t i = 0; i < n; ++i) {
     uint32_t q[3];
     for (int k = 0; k < 3; ++k) {
+#ifdef ORACLE_STUDY_MORTON_CUBIC
+      float ext = cext;
+#else
       float ext = cb[3 + k] - cb[k];
+#endif
       float inv = ext > 0.0f ? 1.0f / ext : 0.0f;
       float c = (primbox[i * 6 + k] + primbox[i * 6 + 3 + k]) * 0.5f;
       float s = ((c - cb[k]) * inv) * 1024.0f;
