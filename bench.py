@@ -28,8 +28,9 @@ x steps / max-over-ranks wall time of the timed region.
 
 Untimed before the W warmup frames: a clock settle (--settle-ms of frames: the GPU needs ~20 ms of
 load to reach its steady clock; with 5 warmup frames alone the same build read 0.20 ms instead of
-0.15 ms per frame; the ranks agree on its length), the tile-rows and frames-in-flight autotunes
-and the counter pass.
+0.15 ms per frame; the ranks agree on its length), the tile-rows and frames-in-flight autotunes,
+the counter pass, and a re-settle (--resettle-ms of frames on the timed loop's own streams and
+buffers, renders only).
 """
 from __future__ import annotations
 
@@ -71,6 +72,9 @@ def parse(argv=None):
     p.add_argument("--warmup", type=int, default=100)
     p.add_argument("--settle-ms", type=float, default=300.0,
                    help="untimed frames before the warmup until this much GPU time has passed (clock ramp)")
+    p.add_argument("--resettle-ms", type=float, default=30.0,
+                   help="untimed frames on the timed loop's own streams right before the warmup (after the autotunes "
+                        "and the counter pass)")
     p.add_argument("--config", default="C2")
     p.add_argument("--size", default="", help="WxH override (tests)")
     p.add_argument("--schedule", default="packet", choices=["packet", "lane"])
@@ -336,7 +340,7 @@ def pick_in_flight(be, W, NR, rows, frames: int = 16, rounds: int = 3, choices=(
 
 
 def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_ms: float, strips: bool,
-               pipeline: bool, schedule: str, save_image: str = "", in_flight: int = 0):
+               pipeline: bool, schedule: str, save_image: str = "", in_flight: int = 0, resettle_ms: float = 0.0):
     """Builds the scene, counts one step's rays (untimed), settles, warms up, then times exactly
     `steps` steps between barrier + synchronize on both sides. Returns a dict (rank 0 meaningful).
     in_flight: frames in flight (render streams, each with its own buffer slot); 0 = autotune."""
@@ -350,20 +354,29 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
         rows, rows_per_rank = None, H
     NR = rows_per_rank
     comm = be.stream() if strips else None
-    # clock settle (untimed) on a plain single-stream loop before any autotune
-    if settle_ms > 0:
-        probe_s, probe_b = be.stream(), be.zeros((NR, W, 4))
+
+    def settle(ms, bufs, streams):
+        """Untimed frames on `streams` (round robin into `bufs`) until `ms` of wall time has passed; the ranks
+        agree on the length (every 4 frames an all-reduce MAX of "still settling"), so no collective is left
+        unmatched. Renders only: no gather."""
         t0 = time.perf_counter()
+        n = 0
         while True:
             for _ in range(4):
-                be.dispatch(probe_b, rows, probe_s)
+                be.dispatch(bufs[n % len(bufs)], rows, streams[n % len(streams)])
+                n += 1
             be.synchronize()
-            more = torch.tensor([1.0 if (time.perf_counter() - t0) * 1e3 < settle_ms else 0.0],
+            more = torch.tensor([1.0 if (time.perf_counter() - t0) * 1e3 < ms else 0.0],
                                 dtype=torch.float64, device=be.device)
             if distributed:
                 dist.all_reduce(more, op=dist.ReduceOp.MAX)
             if more.item() == 0.0:
                 break
+
+    # clock settle (untimed) on a plain single-stream loop before any autotune
+    if settle_ms > 0:
+        probe_b = be.zeros((NR, W, 4))
+        settle(settle_ms, [probe_b], [be.stream()])
         del probe_b
 
     tile_rows, tile_ms = pick_tile_rows(be, be.zeros((NR, W, 4)), rows, be.stream())
@@ -437,6 +450,11 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
         if rcomm is not None:
             rcomm.synchronize()
         be.synchronize()
+
+    # re-settle (untimed): the autotunes and the counter pass leave the GPU between loads; frames on the very
+    # streams and buffers of the timed loop bring it back to its steady state before the warmup
+    if resettle_ms > 0:
+        settle(resettle_ms, local, render)
 
     # warmup (untimed)
     with on_comm():
@@ -720,7 +738,7 @@ def main(argv=None) -> int:
 
     spec = spec_of(a.config)
     r = run_config(be, spec, world, rank, a.steps, a.warmup, a.settle_ms, strips, not a.no_pipeline, a.schedule,
-                   a.save_image, a.in_flight)
+                   a.save_image, a.in_flight, a.resettle_ms)
 
     extra = []
     names = a.extra if a.extra is not None else ("C4,C5" if distributed else "C1,C2F,C3,C4,C5,REF")
@@ -729,7 +747,7 @@ def main(argv=None) -> int:
         # few frames: C5 is ~8 ms per frame on one GPU
         n_steps = max(3, a.steps // (20 if es.spp > 1 else 4))
         x = run_config(be, es, world, rank, n_steps, 2, 0.0, strips, not a.no_pipeline, a.schedule,
-                       in_flight=a.in_flight)
+                       in_flight=a.in_flight, resettle_ms=a.resettle_ms)
         if rank == 0:
             st = x["stats"]
             rays = max(x["rays_step"], 1)
@@ -776,7 +794,7 @@ def main(argv=None) -> int:
                        "frames_in_flight": r["in_flight"], "in_flight_ms_rank0": r["in_flight_ms"],
                        # SURVEY 8(d)'s frame latency: one frame alone, enqueue -> complete (one stream, back to back)
                        "frame_ms_one_stream": round(r["kernel_ms"], 4),
-                       "settle_ms": a.settle_ms},
+                       "settle_ms": a.settle_ms, "resettle_ms": a.resettle_ms},
             "roofline": rf,
             "cpu_baseline": cpu,
             "build_ms": dict(zip(("blas", "tlas", "blas_warm", "tlas_warm", "tlas_update_wall", "tlas_update_kernel"),

@@ -1,14 +1,16 @@
+# bench.py at the driver's short settings (--steps 20 --warmup 5) with and without the pre-warmup re-settle,
+# interleaved, C2 only; then two steady-state lines. Results: gpurun_out/short20*.jsonl, long200.jsonl
 set -u
 mkdir -p gpurun_out
 for i in 1 2 3; do
-  timeout -k 10 120 python3 bench.py --steps 20 --warmup 5 --extra= --no-cpu-baseline >> gpurun_out/short20.jsonl 2>/dev/null || exit 1
-done
-for i in 1 2; do
-  timeout -k 10 120 python3 bench.py --steps 200 --warmup 100 --extra= --no-cpu-baseline >> gpurun_out/long200.jsonl 2>/dev/null || exit 1
+  for rs in 0 30; do
+    timeout -k 10 120 python3 bench.py --steps 20 --warmup 5 --extra= --no-cpu-baseline --resettle-ms $rs \
+      >> gpurun_out/short20_rs$rs.jsonl 2>/dev/null || exit 1
+  done
 done
 python3 - <<'PY'
-import json
-for f in ("gpurun_out/short20.jsonl","gpurun_out/long200.jsonl"):
+import json, glob
+for f in sorted(glob.glob("gpurun_out/short20_rs*.jsonl")):
     for l in open(f):
-        d=json.loads(l); print(f, d["value"], d["ms_per_step"], d["config"]["frames_in_flight"], d["config"]["in_flight_ms_rank0"], d["config"]["frame_ms_one_stream"])
+        d=json.loads(l); print(f, d["value"], d["ms_per_step"], d["config"]["frames_in_flight"], d["config"]["in_flight_ms_rank0"])
 PY
