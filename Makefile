@@ -26,10 +26,11 @@ LIB       := $(LIBDIR)/librtamd.so
 APP       := $(LIBDIR)/rt_app
 ORACLE    := oracle/liboracle.so
 BASELINE  := oracle/libbaseline.so
+RCPCHECK  := tools/bin/recip_check
 
 HDRS      := include/rt_api.h $(SRC)/rt_device.hpp $(SRC)/rt_internal.hpp
 
-all: $(LIB) $(APP) $(ORACLE) $(BASELINE)
+all: $(LIB) $(APP) $(ORACLE) $(BASELINE) $(RCPCHECK)
 
 $(BUILD)/%.o: $(SRC)/%.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -66,10 +67,15 @@ $(BASELINE): oracle/rt_oracle.c oracle/rt_raster_oracle.c oracle/rt_oracle.h
 ref:
 	$(MAKE) -C oracle -f Makefile.ref
 
+# exhaustive GPU check of rt::rcp_exact (the triangle test's 1 / det) against the IEEE division (tests/test_gpu_rcp.py)
+$(RCPCHECK): tools/recip_check.hip $(SRC)/rt_device.hpp include/rt_api.h
+	mkdir -p tools/bin
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off -o $@ $<
+
 $(BUILD) $(LIBDIR):
 	mkdir -p $@
 
 clean:
-	rm -rf $(BUILD) $(LIB) $(APP) $(ORACLE) $(BASELINE)
+	rm -rf $(BUILD) $(LIB) $(APP) $(ORACLE) $(BASELINE) $(RCPCHECK)
 
 .PHONY: all clean ref

@@ -182,9 +182,41 @@ RT_HD float dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 RT_HD V3 cross(V3 a, V3 b) {
   return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
+#ifndef RT_RCP_EXACT
+#define RT_RCP_EXACT 2  // 1 / x by rcp + one Newton step (same bits as the division): bit 0 normalize / safe_inv /
+                        // shading, bit 1 the triangle test's 1 / det
+#endif
+// 1 / x, bit-equal to the IEEE quotient `1.0f / x` (what the oracle computes on the CPU) in a third of the
+// instructions of the compiler's correctly rounded division (div_scale / rcp / 4 fma / div_fmas / div_fixup):
+// v_rcp_f32 (<= 1 ulp) refined by one fused Newton step is bit-equal to 1.0f / x for EVERY float whose biased
+// exponent is in [20, 234] (|x| in [2^-107, 2^108); both signs, all 3.6e9 patterns checked on the GPU,
+// tools/recip_check.hip). A wave with any lane outside that range (zero, denormal, huge, inf / NaN) takes the
+// IEEE division instead, so the result is the IEEE quotient for every input.
+RT_HD float rcp_exact(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t b = __builtin_bit_cast(uint32_t, x);
+  const bool in = (b << 1) - (20u << 24) < (215u << 24);  // exponent field in [20, 234], sign dropped
+  const float r = __builtin_amdgcn_rcpf(x);
+  float q = __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
+  if (__builtin_amdgcn_ballot_w64(!in)) q = in ? q : 1.0f / x;  // wave-uniform, rare
+  return q;
+#else
+  return 1.0f / x;
+#endif
+}
+
+// 1 / x of the ray setup and the shading (RT_RCP_EXACT bit 0: rcp_exact; off: the division, same bits)
+RT_HD float sh_rcp(float x) {
+#if RT_RCP_EXACT & 1
+  return rcp_exact(x);
+#else
+  return 1.0f / x;
+#endif
+}
+
 // HLSL normalize pinned as v * (1 / sqrt(dot(v, v))) (glm's compute_normalize form).
 RT_HD V3 normalize(V3 a) {
-  float inv = 1.0f / sqrtf(dot(a, a));
+  float inv = sh_rcp(sqrtf(dot(a, a)));
   return muls(a, inv);
 }
 RT_HD float length(V3 a) { return sqrtf(dot(a, a)); }
@@ -221,7 +253,11 @@ RT_HD void hlsl_mul4(const float* mem, const float v[4], float r[4]) {
 }
 
 // 1/d with zero components replaced by +-1e20 so slab products never form inf*0.
-RT_HD float safe_inv(float d) { return fabsf(d) > 1e-20f ? 1.0f / d : (d < 0.0f ? -1e20f : 1e20f); }
+RT_HD float safe_inv(float d) {
+  const bool big = fabsf(d) > 1e-20f;
+  const float q = sh_rcp(big ? d : 1.0f);  // the replaced components never send the wave to the slow path
+  return big ? q : (d < 0.0f ? -1e20f : 1e20f);
+}
 
 // Deterministic log2 / exp2 / pow for x in [0, inf): pure +,-,*,/ and bit operations so the GPU
 // and the oracle agree to the bit. |rel err| ~ 2e-7.
@@ -341,6 +377,15 @@ RT_HD V3 mt_cross(V3 a, V3 b) {
 #endif
 }
 
+// 1 / det of the triangle test (RT_RCP_EXACT bit 1: rcp_exact; off: the division, same bits)
+RT_HD float mt_rcp(float det) {
+#if RT_RCP_EXACT & 2
+  return rcp_exact(det);
+#else
+  return 1.0f / det;
+#endif
+}
+
 // Moller-Trumbore. Accepts u >= 0, v >= 0, u + v <= 1, det != 0; returns t (not yet range checked).
 // face: 0 accepts both sides; +1 / -1 accepts only det * face > 0, i.e. front faces under DXR's
 // RAY_FLAG_CULL_BACK_FACING_TRIANGLES (front = clockwise seen from the ray origin = det > 0 with
@@ -350,7 +395,7 @@ RT_HD bool moller_trumbore(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, float& t
   V3 p = mt_cross(d, e2);
   float det = mt_dot(e1, p);
   if (det == 0.0f || det * face < 0.0f) return false;
-  float inv = 1.0f / det;
+  float inv = mt_rcp(det);
   V3 s = sub(o, v0);
   u = mt_dot(s, p) * inv;
   if (!(u >= 0.0f && u <= 1.0f)) return false;
@@ -362,7 +407,7 @@ RT_HD bool moller_trumbore(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, float& t
 #else
   const V3 p = mt_cross(d, e2);
   const float det = mt_dot(e1, p);
-  const float inv = 1.0f / det;
+  const float inv = mt_rcp(det);
   const V3 s = sub(o, v0);
   u = mt_dot(s, p) * inv;
   const V3 q = mt_cross(s, e1);
@@ -377,7 +422,7 @@ RT_HD bool moller_trumbore(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, float& t
 RT_HD bool moller_trumbore_bits(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, float& t, float& u, float& v) {
   const V3 p = mt_cross(d, e2);
   const float det = mt_dot(e1, p);
-  const float inv = 1.0f / det;
+  const float inv = mt_rcp(det);
   const V3 s = sub(o, v0);
   u = mt_dot(s, p) * inv;
   const V3 q = mt_cross(s, e1);
@@ -392,7 +437,7 @@ RT_HD bool moller_trumbore_bits(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, flo
 RT_HD bool moller_trumbore_flat(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, float& t, float& u, float& v) {
   const V3 p = mt_cross(d, e2);
   const float det = mt_dot(e1, p);
-  const float inv = 1.0f / det;
+  const float inv = mt_rcp(det);
   const V3 s = sub(o, v0);
   u = mt_dot(s, p) * inv;
   const V3 q = mt_cross(s, e1);

@@ -1095,7 +1095,7 @@ __device__ V3 pbr_shading(const FrameParams& fp, V3 n, V3 cam, V3 P) {
     const V3 L = normalize(sub(lp, P));
     const V3 H = normalize(add(V, L));
     const float dist = length(sub(lp, P));
-    const float att = 1.0f / maxf(dist * dist, 1.0f);
+    const float att = sh_rcp(maxf(dist * dist, 1.0f));
     const V3 radiance = muls(lc, att);
     const float x = clamp01(1.0f - maxf(dot(H, V), 0.0f));
     const float x2 = x * x;
