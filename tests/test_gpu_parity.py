@@ -215,6 +215,31 @@ def test_frame_parity_small(name, sched):
     c.close()
 
 
+RAGGED = [(1, 1), (1, 19), (23, 1), (7, 3), (65, 9), (9, 65), (129, 17)]
+
+
+@pytest.mark.parametrize("sched", list(SCHEDULES))
+@pytest.mark.parametrize("spp", [1, 4, 9])
+def test_ragged_frame_sizes(sched, spp):
+    """Frames whose sides are not multiples of the 8 x 8 (or 4 x 4 pixels x 4 samples) wave tile: single pixels,
+    single rows and columns, odd rectangles -- the lanes outside the image must neither write nor change the
+    packet walk of the lanes inside. Every kernel variant: one sample, the sample-lane kernel (4 spp) and the
+    sample loop (9 spp), both schedules; C4 (two lights, 65 instances) under the reference camera's grid view."""
+    base = scenes.config("C4")
+    c = fresh_ctx()
+    scenes.upload(c, base.with_size(64, 36))
+    o = oracle.Scene(base)
+    for (w, h) in RAGGED:
+        spec = base.with_size(w, h)
+        spec.spp = spp
+        c.set_camera(spec.camera_buffer())
+        c.set_shading(spec.lights, spec.material, spec.mode, spec.spp)
+        g8, g32 = gpu_render(c, spec, schedule=SCHEDULES[sched])
+        o8, o32, _ = o.render_spec(spec, nthreads=4)
+        assert_images_equal(g8, g32, o8, o32, f"C4 {w}x{h} spp {spp} {sched}")
+    c.close()
+
+
 def sweep_cameras(n, seed=0x5EED):
     """a seeded camera sweep. Eyes on spheres of radius 0.5..40 around points near the
     scene (some inside a model, some grazing the plane), looking at random targets; random up
