@@ -10,8 +10,9 @@
 // Two host threads issue a step. The caller's thread renders the slot on its render stream and records the
 // render event; the communicator's issue thread orders the gather after it (one device-side wait), issues the
 // ncclGather on the gather stream and records its completion. The step's tail goes back to the slot's render
-// stream, issued by the caller's thread at its next call (or at rt_comm_stream / rt_comm_synchronize): a wait
-// for that gather, then rank 0's assembly. So the gather stream carries nothing but the gathers, and the
+// stream, issued by the caller's thread: a wait for that gather, then rank 0's assembly. The caller issues a tail
+// at a later call once the issue thread has enqueued its gather, so it does not wait for the issue thread, and at
+// the latest before the slot renders again (or at rt_comm_stream / rt_comm_synchronize). So the gather stream carries nothing but the gathers, and the
 // slot's next render on its stream follows its tail in stream order (no release event). HIP and RCCL host
 // calls cost microseconds each, so the calls of a step are split over the two threads. With the
 // communicator's own render streams (render_stream NULL), the gather stream and the three render streams sit
@@ -144,10 +145,10 @@ struct rt_comm {
   uint64_t issued = 0;          // jobs handed over (caller thread)
   uint64_t done = 0;            // jobs whose gather (and its event) are enqueued (issue thread)
   uint64_t slot_seq[kMaxSlots] = {};  // the last job of each slot
-  // the step whose tail (back on its render stream: the wait for its gather, rank 0's assembly) the caller
-  // thread issues at its next call, once the issue thread has enqueued the gather
-  bool pend = false;
-  Job pend_job{};
+  // the steps whose tail (back on its render stream: the wait for its gather, rank 0's assembly) the caller thread
+  // has not issued yet, oldest first. A tail is issued at a later call once the issue thread has enqueued its
+  // gather (no waiting), and at the latest before its slot renders again (waiting if the issue thread is behind)
+  std::deque<Job> tails;
   bool stop = false;
   rt_status werr = RT_OK;       // the issue thread's first failure, returned by the next call
   std::string wmsg;
@@ -178,12 +179,12 @@ void release_slots(rt_comm* c) {
 }
 
 void wait_issued(rt_comm* c, uint64_t seq);
-rt_status issue_tail(rt_comm* c);
+rt_status issue_tails(rt_comm* c, uint64_t upto);
 
 // waits (host) for every step handed over so far: its gather on the gather stream, its assembly on its
 // render stream
 rt_status drain(rt_comm* c) {
-  rt_status st = issue_tail(c);
+  rt_status st = issue_tails(c, ~0ull);
   if (st != RT_OK) return st;
   wait_issued(c, c->issued);
   if (c->stream && hipStreamSynchronize(c->stream) != hipSuccess) return cfail(c, RT_E_HIP, "rt_render_strips: drain");
@@ -264,7 +265,7 @@ void issue_loop(rt_comm* c) {
       }
     }
     if (c->timing) t2 = clk::now();
-    // the gather's completion, for the step's tail on the slot's render stream (issue_tail, caller thread)
+    // the gather's completion, for the step's tail on the slot's render stream (issue_tail_job, caller thread)
     if (st == RT_OK && j.rs != c->stream && hipEventRecord(s.gathered_ev, c->stream) != hipSuccess) {
       st = RT_E_HIP;
       msg = "rt_render_strips: record gather";
@@ -293,12 +294,9 @@ void wait_issued(rt_comm* c, uint64_t seq) {
   c->cv_done.wait(lk, [c, seq] { return c->done >= seq; });
 }
 
-// caller thread: the pending step's tail on its render stream, behind its gather (device-side wait): rank 0
-// assembles the frame there, off the gather stream, and the slot's next render on that stream follows
-rt_status issue_tail(rt_comm* c) {
-  if (!c->pend) return RT_OK;
-  const Job& j = c->pend_job;
-  c->pend = false;
+// caller thread: a step's tail on its render stream, behind its gather (device-side wait): rank 0 assembles the
+// frame there, off the gather stream, and the slot's next render on that stream follows it
+rt_status issue_tail_job(rt_comm* c, const Job& j) {
   wait_issued(c, j.seq);
   Slot& s = c->slots[j.slot];
   if (j.rs != c->stream && hipStreamWaitEvent(j.rs, s.gathered_ev, 0) != hipSuccess)
@@ -314,6 +312,24 @@ rt_status issue_tail(rt_comm* c) {
   if (e != hipSuccess) return cfail(c, RT_E_HIP, std::string("rt_render_strips: assembly: ") + hipGetErrorString(e));
   s.asm_stream = j.rs;
   s.asm_frame = j.frame_out;
+  return RT_OK;
+}
+
+// issues the pending tails in call order: every one up to step `upto` (waiting for the issue thread where it is
+// behind), then those whose gather the issue thread has already enqueued (no waiting)
+rt_status issue_tails(rt_comm* c, uint64_t upto) {
+  uint64_t done;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    done = c->done;
+  }
+  while (!c->tails.empty()) {
+    const Job j = c->tails.front();
+    if (j.seq > upto && j.seq > done) break;
+    c->tails.pop_front();
+    const rt_status st = issue_tail_job(c, j);
+    if (st != RT_OK) return st;
+  }
   return RT_OK;
 }
 
@@ -434,7 +450,7 @@ const char* rt_comm_last_error(rt_comm_t c) { return c ? c->err.c_str() : "null 
 
 void* rt_comm_stream(rt_comm_t c) {
   if (!c) return nullptr;
-  if (issue_tail(c) != RT_OK) return nullptr;
+  if (issue_tails(c, ~0ull) != RT_OK) return nullptr;
   wait_issued(c, c->issued);  // every step handed over so far is enqueued
   (void)hipSetDevice(c->device);
   // join: the stream returned (the gathers') waits, on the device, for the slots' render streams, where the
@@ -494,7 +510,8 @@ rt_status rt_render_strips(rt_comm_t c, uint32_t W, uint32_t H, uint32_t strip_r
   // slot's stream (wait for that, rarely: the issue thread keeps up), so a render on the same stream follows
   // it in stream order; a slot moved to another stream waits for it with an event
   if (s.used) {
-    if (c->pend && c->pend_job.slot == si && (st = issue_tail(c)) != RT_OK) return st;
+    // the slot's last tail goes on its stream before this render (and every older pending tail with it)
+    if ((st = issue_tails(c, c->slot_seq[si])) != RT_OK) return st;
     wait_issued(c, c->slot_seq[si]);
     lap(3);
     if (s.last != rs &&
@@ -521,11 +538,10 @@ rt_status rt_render_strips(rt_comm_t c, uint32_t W, uint32_t H, uint32_t strip_r
   }
   if (c->sleeping.load(std::memory_order_seq_cst)) c->cv_job.notify_one();
   lap(2);
-  // the previous step's tail (its gather is enqueued by now, or soon), then this step's is pending
-  st = issue_tail(c);
+  // the tails whose gathers the issue thread has enqueued by now (no waiting); this step's is pending
+  st = issue_tails(c, 0);
   lap(5);
-  c->pend = true;
-  c->pend_job = job;
+  c->tails.push_back(job);
   if (st != RT_OK) return st;
   ++c->t_calls;
   return RT_OK;
