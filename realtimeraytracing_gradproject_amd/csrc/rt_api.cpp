@@ -204,8 +204,7 @@ struct rt_ctx {
   uint32_t pool_tlas_cap = 0;    // nodes of each version's TLAS slot in the pool
   std::vector<uint32_t> node_base, tri_base;  // BLAS k's first node / triangle in the pools
   rt::BuildArena tlas_arena;     // lbvh_build scratch of the TLAS builds (kept: no hipMalloc per update)
-  float* d_tlas_bb = nullptr;    // instance BLAS boxes / world boxes (scratch, grown on demand)
-  float* d_tlas_box = nullptr;
+  float* d_tlas_box = nullptr;   // instance world boxes (scratch, grown on demand)
   uint32_t tlas_scratch_cap = 0;
   double tlas_wall_ms = 0.0;     // host wall time of the last rt_tlas_build
   // frame state
@@ -446,7 +445,6 @@ rt_status rt_destroy(rt_ctx_t c) {
   for (auto& b : c->blas) b.release();
   for (auto& v : c->ver) v.release();
   c->tlas_arena.release();
-  if (c->d_tlas_bb) (void)hipFree(c->d_tlas_bb);
   if (c->d_tlas_box) (void)hipFree(c->d_tlas_box);
   if (c->d_stats) (void)hipFree(c->d_stats);
   for (auto& sl : c->rows.slots) slot_release(sl);
@@ -627,7 +625,8 @@ rt_status rt_tlas_build(rt_ctx_t c, const rt_instance* in, uint32_t n, int updat
         tv.staging = nullptr;
         tv.cap = 0;
         HIPCHK(c, hipMalloc(&tv.nodes, (size_t)tlas_cap * sizeof(rt::Bvh4Node)), "hipMalloc(tlas)");
-        HIPCHK(c, hipMalloc(&tv.inst, (size_t)n * sizeof(rt::InstanceRec)), "hipMalloc(instances)");
+        // the instance records, then the BLAS boxes of the build (one upload from the staging, same layout)
+        HIPCHK(c, hipMalloc(&tv.inst, (size_t)n * (sizeof(rt::InstanceRec) + 24)), "hipMalloc(instances)");
         HIPCHK(c, hipMalloc(&tv.sorted, (size_t)n * 4), "hipMalloc(tlas order)");
         tv.staging_bytes = (size_t)n * sizeof(rt::InstanceRec) + (size_t)n * 24;
         HIPCHK(c, hipHostMalloc((void**)&tv.staging, tv.staging_bytes, hipHostMallocDefault), "hipHostMalloc(tlas staging)");
@@ -636,11 +635,9 @@ rt_status rt_tlas_build(rt_ctx_t c, const rt_instance* in, uint32_t n, int updat
       if (!tv.ready && !(tv.ready = new_sync_event())) return fail(c, RT_E_HIP, "rt_tlas_build: event");
     }
     if (c->tlas_scratch_cap < n) {
-      if (c->d_tlas_bb) (void)hipFree(c->d_tlas_bb);
       if (c->d_tlas_box) (void)hipFree(c->d_tlas_box);
-      c->d_tlas_bb = c->d_tlas_box = nullptr;
+      c->d_tlas_box = nullptr;
       c->tlas_scratch_cap = 0;
-      HIPCHK(c, hipMalloc(&c->d_tlas_bb, (size_t)n * 24), "hipMalloc(tlas scratch)");
       HIPCHK(c, hipMalloc(&c->d_tlas_box, (size_t)n * 24), "hipMalloc(tlas scratch)");
       c->tlas_scratch_cap = n;
     }
@@ -656,9 +653,11 @@ rt_status rt_tlas_build(rt_ctx_t c, const rt_instance* in, uint32_t n, int updat
   std::memcpy(tv.staging, recs.data(), recs.size() * sizeof(rt::InstanceRec));  // staging idle: its last build synced
   float* bb_stage = (float*)((char*)tv.staging + (size_t)n * sizeof(rt::InstanceRec));
   std::memcpy(bb_stage, bb.data(), bb.size() * 4);
-  hipError_t e = hipMemcpyAsync(tv.inst, tv.staging, recs.size() * sizeof(rt::InstanceRec), hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(c->d_tlas_bb, bb_stage, bb.size() * 4, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = rt::tlas_prepare(tv.inst, c->d_tlas_bb, n, c->d_tlas_box, s);
+  // records and boxes in one copy: the version's buffer holds the n records, then the n BLAS boxes
+  const float* d_bb = (const float*)((const char*)tv.inst + (size_t)n * sizeof(rt::InstanceRec));
+  hipError_t e = hipMemcpyAsync(tv.inst, tv.staging, (size_t)n * sizeof(rt::InstanceRec) + bb.size() * 4,
+                                hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = rt::tlas_prepare(tv.inst, d_bb, n, c->d_tlas_box, s);
   float ms = 0.0f;
   uint32_t nn = 0, depth = 0, mstack = 0;
   float bounds[6];

@@ -32,8 +32,11 @@ struct BuildArena {
   void* p = nullptr;
   size_t cap = 0;
   hipEvent_t e0 = nullptr, e1 = nullptr;  // build timing
+  void* host = nullptr;                    // pinned readback of the build's bounds + node count / depth / stack
   void release() {
     if (p) (void)hipFree(p);
+    if (host) (void)hipHostFree(host);
+    host = nullptr;
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
     p = nullptr;

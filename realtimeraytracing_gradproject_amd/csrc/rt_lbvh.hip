@@ -2079,8 +2079,9 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
     total += (bytes + 255) & ~(size_t)255;
     return q;
   };
-  const Part p_stats = part(12 * sizeof(float)), p_keys0 = part((size_t)n * 4), p_keys1 = part((size_t)n * 4),
-             p_vals1 = part((size_t)n * 4), p_hist = part((size_t)256 * nblocks * 4), p_info = part(32),
+  // stats and info first and adjacent: one readback copies both
+  const Part p_stats = part(12 * sizeof(float)), p_info = part(32), p_keys0 = part((size_t)n * 4),
+             p_keys1 = part((size_t)n * 4), p_vals1 = part((size_t)n * 4), p_hist = part((size_t)256 * nblocks * 4),
              p_ps = part((size_t)nbin * 4), p_bin = part((size_t)nbin * sizeof(BinNode)), p_la = part((size_t)nbin * 4),
              p_lb = part((size_t)nbin * 4), p_child = part((size_t)nbin * 8), p_pint = part((size_t)nbin * 4),
              p_pleaf = part((size_t)n * 4), p_nbox = part((size_t)nbin * 24), p_flags = part((size_t)nbin * 4),
@@ -2212,9 +2213,18 @@ hipError_t lbvh_build(const float* d_primbox, uint32_t n, Bvh4Node* d_nodes, uin
   RT_TRY(hipEventRecord(e1, s));
   float hb[12];
   uint32_t hinfo[3];
-  RT_TRY(hipMemcpyAsync(hb, cb, sizeof(hb), hipMemcpyDeviceToHost, s));
-  RT_TRY(hipMemcpyAsync(hinfo, info.p, 12, hipMemcpyDeviceToHost, s));
-  RT_TRY(hipStreamSynchronize(s));
+  const size_t info_off = p_info.off - p_stats.off;  // 256: the parts are adjacent
+  if (keep) {  // one copy of both into the arena's pinned buffer (a pageable destination is staged by the runtime)
+    if (!keep->host) RT_TRY(hipHostMalloc(&keep->host, info_off + 32, hipHostMallocDefault));
+    RT_TRY(hipMemcpyAsync(keep->host, cb, info_off + 12, hipMemcpyDeviceToHost, s));
+    RT_TRY(hipStreamSynchronize(s));
+    std::memcpy(hb, keep->host, sizeof(hb));
+    std::memcpy(hinfo, (const char*)keep->host + info_off, sizeof(hinfo));
+  } else {
+    RT_TRY(hipMemcpyAsync(hb, cb, sizeof(hb), hipMemcpyDeviceToHost, s));
+    RT_TRY(hipMemcpyAsync(hinfo, info.p, 12, hipMemcpyDeviceToHost, s));
+    RT_TRY(hipStreamSynchronize(s));
+  }
   for (int k = 0; k < 6; ++k) bounds[k] = hb[6 + k];
   *node_count = hinfo[0];
   *depth = hinfo[1];
