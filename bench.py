@@ -391,11 +391,23 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
         ok = torch.tensor([1.0 if be.rt.comm_available() else 0.0], dtype=torch.float64, device=be.device)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         native = ok.item() == 1.0
+    rcomm = None
+    if native:  # a communicator that fails to come up on any rank sends every rank to the torch.distributed loop
+        try:
+            rcomm = be.comm_open(world, rank)
+        except Exception as ex:  # noqa: BLE001  (RtError from rt_comm_init: reported, then the fallback)
+            print(f"bench: rt_comm_init failed on rank {rank} ({ex}); using the torch.distributed strips loop",
+                  file=sys.stderr, flush=True)
+        up = torch.tensor([1.0 if rcomm is not None else 0.0], dtype=torch.float64, device=be.device)
+        dist.all_reduce(up, op=dist.ReduceOp.MIN)
+        if up.item() != 1.0:
+            if rcomm is not None:
+                rcomm.close()
+            rcomm, native = None, False
     nslot = max(nstream, 2 if (strips and pipeline) else 1)
     local = [be.zeros((rows_per_rank, W, 4)) for _ in range(nslot)]
     gathered = ([be.zeros((world, rows_per_rank, W, 4)) if rank == 0 else None for _ in range(nslot)]
                 if strips and not native else None)
-    rcomm = be.comm_open(world, rank) if native else None
     frame = ([be.zeros((H, W, 4)) if rank == 0 else None for _ in range(rcomm.depth if native else nslot)]
              if strips else None)
     rendered = [be.sync_event() for _ in range(nslot)]

@@ -96,3 +96,27 @@ class CpuBackend:
 
     def close(self):
         pass
+
+
+class _CommAvailable:
+    @staticmethod
+    def comm_available():
+        return True
+
+
+class CpuBackendCommFails(CpuBackend):
+    """The native strips loop requested and RCCL reported available, but rt_comm_init fails on rank 1 only
+    (RCCL_FAIL_RANK): every rank must fall back to the torch.distributed strips loop together."""
+    native_strips = True
+    rt = _CommAvailable()
+
+    def comm_open(self, world, rank):
+        if rank == int(os.environ.get("RCCL_FAIL_RANK", "1")):
+            raise RuntimeError("rt_comm_init: simulated RCCL failure")
+
+        class _Comm:
+            depth = 3
+
+            def close(self):
+                pass
+        return _Comm()

@@ -159,3 +159,30 @@ def test_bench_spawn_path_gloo(tmp_path, world):
     assert np.array_equal(np.load(img), o8)  # assembled from both ranks' strips, bit for bit
     assert [e["config"] for e in out["extra"]] == ["C4"] and out["extra"][0]["n_gpus"] == world
     assert out["roofline"]["frac"] <= 1.0
+
+
+def test_bench_native_comm_failure_falls_back_together(tmp_path):
+    """bench.py asked for the native RCCL loop, but the communicator fails to come up on one rank: the ranks agree
+    (all-reduce MIN) and all of them run the torch.distributed strips loop instead of hanging in mismatched
+    collectives; the assembled frame is still the oracle's."""
+    import json
+    import subprocess
+    import sys
+    sys.path.insert(0, ROOT)
+    import oracle
+    from realtimeraytracing_gradproject_amd import scenes
+    img = tmp_path / "frame.npy"
+    env = dict(os.environ, RT_BENCH_TEST_BACKEND="tests.bench_cpu_backend:CpuBackendCommFails", RCCL_FAIL_RANK="1",
+               PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""), OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "C2F", "--size", "64x44",
+           "--steps", "3", "--warmup", "1", "--settle-ms", "10", "--resettle-ms", "0", "--extra=", "--no-cpu-baseline",
+           "--save-image", str(img)]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    assert "simulated RCCL failure" in p.stderr
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["config"]["strips_loop"] == "torch.distributed gather"
+    spec = scenes.config("C2F").with_size(64, 44)
+    o8, _, _ = oracle.Scene(spec).render_spec(spec, nthreads=2, want_float=False)
+    assert np.array_equal(np.load(img), o8)
