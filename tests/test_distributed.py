@@ -162,9 +162,10 @@ def test_bench_spawn_path_gloo(tmp_path, world):
 
 
 def test_bench_native_comm_failure_falls_back_together(tmp_path):
-    """bench.py asked for the native RCCL loop, but the communicator fails to come up on one rank: the ranks agree
-    (all-reduce MIN) and all of them run the torch.distributed strips loop instead of hanging in mismatched
-    collectives; the assembled frame is still the oracle's."""
+    """bench.py asked for the native RCCL loop, but rt_comm_init returns an error on one rank (here simulated on rank
+    1 alone, the other rank's init returning normally): the ranks agree (all-reduce MIN) and all of them run the
+    torch.distributed strips loop rather than issuing gathers on a communicator that one rank lacks; the assembled
+    frame is still the oracle's. (A rank that never returns from ncclCommInitRank cannot be recovered this way.)"""
     import json
     import subprocess
     import sys
