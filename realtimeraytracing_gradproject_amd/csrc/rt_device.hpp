@@ -184,7 +184,7 @@ RT_HD V3 cross(V3 a, V3 b) {
 }
 #ifndef RT_RCP_EXACT
 #define RT_RCP_EXACT 2  // 1 / x by rcp + one Newton step (same bits as the division): bit 0 normalize / safe_inv /
-                        // shading, bit 1 the triangle test's 1 / det
+                        // shading, bit 1 the triangle test's 1 / det, bit 2 safe_inv alone (the walks' inverse directions)
 #endif
 // 1 / x, bit-equal to the IEEE quotient `1.0f / x` (what the oracle computes on the CPU) in a third of the
 // instructions of the compiler's correctly rounded division (div_scale / rcp / 4 fma / div_fmas / div_fixup):
@@ -255,7 +255,11 @@ RT_HD void hlsl_mul4(const float* mem, const float v[4], float r[4]) {
 // 1/d with zero components replaced by +-1e20 so slab products never form inf*0.
 RT_HD float safe_inv(float d) {
   const bool big = fabsf(d) > 1e-20f;
-  const float q = sh_rcp(big ? d : 1.0f);  // the replaced components never send the wave to the slow path
+#if RT_RCP_EXACT & 4
+  const float q = rcp_exact(big ? d : 1.0f);  // the replaced components never send the wave to the slow path
+#else
+  const float q = sh_rcp(big ? d : 1.0f);
+#endif
   return big ? q : (d < 0.0f ? -1e20f : 1e20f);
 }
 
