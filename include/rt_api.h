@@ -299,7 +299,8 @@ uint32_t rt_comm_pipeline_depth(rt_comm_t comm);
  * stream of the communicator; its render streams and its gather stream sit on separate hardware queues). The gather stream waits for that render (a device-side event) and runs ONE ncclGather of every
  * rank's slot into rank 0; the step's tail returns to render_stream: a wait for that gather and, on rank 0, the
  * assembly of the W x H RGBA8 frame into frame_out (device buffer; ignored on other ranks). The tail is issued
- * by the next call (or by rt_comm_stream / rt_comm_synchronize). The slot's next render on the same stream
+ * by a later call once the gather is enqueued, at the latest before the slot renders again (or by rt_comm_stream /
+ * rt_comm_synchronize). The slot's next render on the same stream
  * follows its tail in stream order; a slot moved to another stream, and two assemblies into one frame_out on
  * different streams, are ordered by events. No host waits: frame k's gather overlaps frame k + 1's render, and
  * frames on different streams overlap (frames in flight). Asynchronous: frame_out is complete once the work
