@@ -381,6 +381,23 @@ RT_HD V3 mt_cross(V3 a, V3 b) {
 #endif
 }
 
+#ifndef RT_FLAT_BITS
+#define RT_FLAT_BITS 1  // the packet walk's triangle acceptance as bitwise & (no exec-mask region; A/B knob)
+#endif
+#ifndef RT_FACE_FOLD
+#define RT_FACE_FOLD 1  // the culling term skipped where face is the constant 0 (same acceptance)
+#endif
+// The culling term of the triangle test: det * face < 0 rejects. With face == 0 (no culling: primary and shadow
+// rays) det * 0 is +-0 or NaN, never < 0, so the term is always false; written so the compiler folds it away when
+// face is the constant 0 after inlining (it does not fold x * 0 < 0 itself) instead of a multiply and a compare.
+RT_HD bool culled(float det, float face) {
+#if RT_FACE_FOLD
+  return face != 0.0f && det * face < 0.0f;
+#else
+  return det * face < 0.0f;
+#endif
+}
+
 // 1 / det of the triangle test (RT_RCP_EXACT bit 1: rcp_exact; off: the division, same bits)
 RT_HD float mt_rcp(float det) {
 #if RT_RCP_EXACT & 2
@@ -398,7 +415,7 @@ RT_HD bool moller_trumbore(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, float& t
 #if RT_MT_EARLY_EXIT
   V3 p = mt_cross(d, e2);
   float det = mt_dot(e1, p);
-  if (det == 0.0f || det * face < 0.0f) return false;
+  if (det == 0.0f || culled(det, face)) return false;
   float inv = mt_rcp(det);
   V3 s = sub(o, v0);
   u = mt_dot(s, p) * inv;
@@ -417,7 +434,7 @@ RT_HD bool moller_trumbore(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, float& t
   const V3 q = mt_cross(s, e1);
   v = mt_dot(d, q) * inv;
   t = mt_dot(e2, q) * inv;
-  return det != 0.0f && !(det * face < 0.0f) && u >= 0.0f && u <= 1.0f && v >= 0.0f && u + v <= 1.0f;
+  return det != 0.0f && !culled(det, face) && u >= 0.0f && u <= 1.0f && v >= 0.0f && u + v <= 1.0f;
 #endif
 }
 
@@ -432,7 +449,7 @@ RT_HD bool moller_trumbore_bits(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, flo
   const V3 q = mt_cross(s, e1);
   v = mt_dot(d, q) * inv;
   t = mt_dot(e2, q) * inv;
-  return (det != 0.0f) & !(det * face < 0.0f) & (u >= 0.0f) & (u <= 1.0f) & (v >= 0.0f) & (u + v <= 1.0f);
+  return (det != 0.0f) & !culled(det, face) & (u >= 0.0f) & (u <= 1.0f) & (v >= 0.0f) & (u + v <= 1.0f);
 }
 
 // Moller-Trumbore without early exits: every lane runs the same instructions (the wave-packet
@@ -447,7 +464,11 @@ RT_HD bool moller_trumbore_flat(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, flo
   const V3 q = mt_cross(s, e1);
   v = mt_dot(d, q) * inv;
   t = mt_dot(e2, q) * inv;
-  return det != 0.0f && !(det * face < 0.0f) && u >= 0.0f && u <= 1.0f && v >= 0.0f && u + v <= 1.0f;
+#if RT_FLAT_BITS
+  return (det != 0.0f) & !culled(det, face) & (u >= 0.0f) & (u <= 1.0f) & (v >= 0.0f) & (u + v <= 1.0f);
+#else
+  return det != 0.0f && !culled(det, face) && u >= 0.0f && u <= 1.0f && v >= 0.0f && u + v <= 1.0f;
+#endif
 }
 
 // HLSL reflect(i, n) = i - 2 * n * dot(i, n), evaluated as i - (2 n) * dot(i, n).
