@@ -87,6 +87,9 @@ typedef float f8v __attribute__((ext_vector_type(8)));
 #ifndef RT_TBEST_ASM
 #define RT_TBEST_ASM 1  // slab tests: the min with the ray's t as v_min asm (no per-node canonicalise: C2 -2 % median, C4/C5 -0.3..0.6 %)
 #endif
+#ifndef RT_KEY64
+#define RT_KEY64 1  // closest-hit tie-break (instance, primitive) as one 64-bit compare (C2 -1.4 %)
+#endif
 #ifndef RT_PACKET_OCT
 #define RT_PACKET_OCT 1  // uniform-octant BLAS walks load near/far planes directly (no min/max pairs)
 #endif
@@ -470,8 +473,14 @@ __device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref
     // bitwise & / | (no short-circuit): no exec-mask branches around the compares (-2 %)
     // a ray that is not live has t = -inf and takes nothing; a live any-hit ray still holds
     // {tmax, ~0, ~0}, for which the (t, instance, primitive) order reduces to t <= tmax
+#if RT_KEY64
+    // (instance, primitive) order as ONE unsigned 64-bit compare (v_cmp_lt_u64; the uniform side in an SGPR pair)
+    const bool id_less = (((uint64_t)cur << 32) | prim) < (((uint64_t)h.inst << 32) | h.prim);
+    const bool better = ANY_HIT ? (t <= h.t) : (t < h.t) | ((t == h.t) & id_less);
+#else
     const bool better = ANY_HIT ? (t <= h.t)
                                 : (t < h.t) | ((t == h.t) & ((cur < h.inst) | ((cur == h.inst) & (prim < h.prim))));
+#endif
     const bool take = ok & (t >= tmin) & better;
     // an any-hit ray that accepts leaves the packet with t = -inf: every later slab test rejects it
     h.t = take ? (ANY_HIT ? -__builtin_inff() : t) : h.t;
