@@ -384,6 +384,9 @@ RT_HD V3 mt_cross(V3 a, V3 b) {
 #ifndef RT_FLAT_BITS
 #define RT_FLAT_BITS 1  // the packet walk's triangle acceptance as bitwise & (no exec-mask region; A/B knob)
 #endif
+#ifndef RT_FLAT_UV2
+#define RT_FLAT_UV2 1  // the bitwise acceptance with the implied u <= 1 dropped and min(u, v) >= 0
+#endif
 #ifndef RT_FACE_FOLD
 #define RT_FACE_FOLD 1  // the culling term skipped where face is the constant 0 (same acceptance)
 #endif
@@ -464,7 +467,12 @@ RT_HD bool moller_trumbore_flat(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, flo
   const V3 q = mt_cross(s, e1);
   v = mt_dot(d, q) * inv;
   t = mt_dot(e2, q) * inv;
-#if RT_FLAT_BITS
+#if RT_FLAT_BITS && RT_FLAT_UV2
+  // The same acceptance with two terms fewer. u <= 1 is implied: v >= 0 (not NaN) makes u + v >= u exactly, and
+  // rounding is monotone, so fl(u + v) <= 1 gives u <= 1 (a NaN u fails u + v <= 1). min(u, v) >= 0 is u >= 0 and
+  // v >= 0 for non-NaN u, v (-0 included); a NaN one (the min returns the other) fails u + v <= 1 anyway.
+  return (det != 0.0f) & !culled(det, face) & (__builtin_fminf(u, v) >= 0.0f) & (u + v <= 1.0f);
+#elif RT_FLAT_BITS
   return (det != 0.0f) & !culled(det, face) & (u >= 0.0f) & (u <= 1.0f) & (v >= 0.0f) & (u + v <= 1.0f);
 #else
   return det != 0.0f && !culled(det, face) && u >= 0.0f && u <= 1.0f && v >= 0.0f && u + v <= 1.0f;
