@@ -82,6 +82,9 @@ def parse(argv=None):
                    help="N>1: strips = one frame tiled over ranks + RCCL gather (default); frames = N "
                         "independent replicas (no collective)")
     p.add_argument("--no-pipeline", action="store_true", help="strips: gather after each frame, no overlap")
+    p.add_argument("--frames-per-gather", type=int, default=4,
+                   help="strips through the native loop: consecutive frames whose strips one ncclGather moves "
+                        "(rt_comm_set_batch; the gather half of a step is paid once per this many frames)")
     p.add_argument("--in-flight", type=int, default=0,
                    help="frames in flight (render streams, one buffer each); 0 = untimed autotune over 1..4")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -340,7 +343,8 @@ def pick_in_flight(be, W, NR, rows, frames: int = 16, rounds: int = 3, choices=(
 
 
 def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_ms: float, strips: bool,
-               pipeline: bool, schedule: str, save_image: str = "", in_flight: int = 0, resettle_ms: float = 0.0):
+               pipeline: bool, schedule: str, save_image: str = "", in_flight: int = 0, resettle_ms: float = 0.0,
+               frames_per_gather: int = 1):
     """Builds the scene, counts one step's rays (untimed), settles, warms up, then times exactly
     `steps` steps between barrier + synchronize on both sides. Returns a dict (rank 0 meaningful).
     in_flight: frames in flight (render streams, each with its own buffer slot); 0 = autotune."""
@@ -404,6 +408,8 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
             if rcomm is not None:
                 rcomm.close()
             rcomm, native = None, False
+        elif frames_per_gather > 1:  # the same on every rank (it sizes the collective)
+            rcomm.set_batch(frames_per_gather)
     nslot = max(nstream, 2 if (strips and pipeline) else 1)
     local = [be.zeros((rows_per_rank, W, 4)) for _ in range(nslot)]
     gathered = ([be.zeros((world, rows_per_rank, W, 4)) if rank == 0 else None for _ in range(nslot)]
@@ -521,9 +527,10 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
             rcomm.synchronize()
         img = frame[last] if strips else local[last][:H]
         np.save(save_image, img.cpu().numpy())
+    fpg = rcomm.batch if rcomm is not None else None
     if rcomm is not None:
         rcomm.close()
-    return {"rays_step": rays_step, "primary": int(counts[1].item()), "shadow": int(counts[2].item()),
+    return {"rays_step": rays_step, "primary": int(counts[1].item()), "shadow": int(counts[2].item()), "fpg": fpg,
             "tmax": tmax, "kernel_ms": kernel_ms, "stats": st, "build": build, "rows_local": len(rows) if strips else H,
             "tile_rows": tile_rows, "tile_ms": tile_ms, "in_flight": nstream, "in_flight_ms": flight_ms,
             "strips_loop": ("rt_render_strips (C-ABI: render -> ncclGather -> assembly; "
@@ -750,7 +757,7 @@ def main(argv=None) -> int:
 
     spec = spec_of(a.config)
     r = run_config(be, spec, world, rank, a.steps, a.warmup, a.settle_ms, strips, not a.no_pipeline, a.schedule,
-                   a.save_image, a.in_flight, a.resettle_ms)
+                   a.save_image, a.in_flight, a.resettle_ms, a.frames_per_gather)
 
     extra = []
     names = a.extra if a.extra is not None else ("C4,C5" if distributed else "C1,C2F,C3,C4,C5,REF")
@@ -759,7 +766,7 @@ def main(argv=None) -> int:
         # few frames: C5 is ~8 ms per frame on one GPU
         n_steps = max(3, a.steps // (20 if es.spp > 1 else 4))
         x = run_config(be, es, world, rank, n_steps, 2, 0.0, strips, not a.no_pipeline, a.schedule,
-                       in_flight=a.in_flight, resettle_ms=a.resettle_ms)
+                       in_flight=a.in_flight, resettle_ms=a.resettle_ms, frames_per_gather=a.frames_per_gather)
         if rank == 0:
             st = x["stats"]
             rays = max(x["rays_step"], 1)
@@ -801,6 +808,7 @@ def main(argv=None) -> int:
                        "parallelism": (f"strips{world}+gather" + ("" if a.no_pipeline else " (pipelined)")) if strips
                        else f"frames{world}",
                        "rccl_world_size": world if (distributed or strips) else None, "strips_loop": r["strips_loop"],
+                       "frames_per_gather": r["fpg"],
                        "schedule": a.schedule,
                        "tile_rows": r["tile_rows"], "tile_ms_rank0": r["tile_ms"],
                        "frames_in_flight": r["in_flight"], "in_flight_ms_rank0": r["in_flight_ms"],

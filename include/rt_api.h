@@ -294,6 +294,16 @@ rt_status rt_comm_synchronize(rt_comm_t comm);
  * hardware queue beside the gather stream's (GPU_MAX_HW_QUEUES - 1, HIP's default 4 gives 3; RT_COMM_SLOTS
  * overrides, 1..8). Call k uses slot k mod depth. */
 uint32_t rt_comm_pipeline_depth(rt_comm_t comm);
+
+/* Frames per gather (1 .. 4; default 1): consecutive rt_render_strips calls render into one pipeline slot and ONE
+ * ncclGather moves all their strips, so the gather half of a step (a stream wait, the RCCL call, an event) is paid
+ * once per `frames_per_gather` frames; the bytes moved per frame are the same. A frame's assembly then waits for the
+ * last frame of its slot (or for rt_comm_stream / rt_comm_synchronize, which gather a partly filled slot as it is).
+ * Every rank must set the same value between the same two calls (it changes the collective's size). Drains the
+ * pipeline. rt_comm_pipeline_depth becomes slots x frames_per_gather. Replaces: nothing in the reference (the
+ * multi-GPU loop is this library's). */
+rt_status rt_comm_set_batch(rt_comm_t comm, uint32_t frames_per_gather);
+uint32_t rt_comm_batch(rt_comm_t comm);
 /* One tiled frame, collective over the ranks (every rank calls it, in the same frame order): this rank's
  * strips are rendered on render_stream into one of the communicator's pipeline slots (NULL: slot k's own
  * stream of the communicator; its render streams and its gather stream sit on separate hardware queues). The gather stream waits for that render (a device-side event) and runs ONE ncclGather of every

@@ -118,6 +118,8 @@ SIGNATURES = [
     ("rt_comm_synchronize", _I, [_P]),
     ("rt_render_strips", _I, [_P, _U32, _U32, _U32, _P, _P]),
     ("rt_comm_pipeline_depth", _U32, [_P]),
+    ("rt_comm_set_batch", _I, [_P, _U32]),
+    ("rt_comm_batch", _U32, [_P]),
     ("rt_stats", _I, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     ("rt_stats_reset", _I, [_P]),
     ("rt_mesh_load_obj", _I, [ctypes.c_char_p, ctypes.POINTER(_P)]),
@@ -427,8 +429,17 @@ class Comm:
 
     @property
     def depth(self) -> int:
-        """Pipeline slots: render_strips call k uses slot k mod depth (one render stream each)."""
+        """Frames in the pipeline: slots (one render stream each) x frames per gather; a caller that gives each
+        call its own frame buffer needs this many to never wait on a frame buffer's previous assembly."""
         return int(self._lib.rt_comm_pipeline_depth(self._h))
+
+    def set_batch(self, frames_per_gather: int):
+        """rt_comm_set_batch: frames whose strips go in one ncclGather (every rank the same, between the same calls)."""
+        self._check(self._lib.rt_comm_set_batch(self._h, frames_per_gather), "rt_comm_set_batch")
+
+    @property
+    def batch(self) -> int:
+        return int(self._lib.rt_comm_batch(self._h))
 
     def synchronize(self):
         self._check(self._lib.rt_comm_synchronize(self._h), "rt_comm_synchronize")

@@ -77,17 +77,21 @@ RcclApi& rccl() {
   return api;
 }
 
+// frames per gather (rt_comm_set_batch): a slot holds up to this many consecutive frames' strips
+constexpr uint32_t kMaxBatch = 4;
+
 struct Slot {
-  void* local = nullptr;     // this rank's strips, compact: rows_per_rank x W RGBA8
-  void* gathered = nullptr;  // rank 0: nranks x rows_per_rank x W RGBA8
+  void* local = nullptr;     // this rank's strips, compact: batch x rows_per_rank x W RGBA8 (frame-major)
+  void* gathered = nullptr;  // rank 0: nranks x (batch x rows_per_rank) x W RGBA8 (rank-major, as ncclGather lays it)
   hipEvent_t rendered = nullptr;  // on the slot's render stream, after its render
   hipEvent_t gathered_ev = nullptr;  // on the gather stream, after its gather
   hipEvent_t moved = nullptr;     // recorded on demand (a slot moved to another stream)
   hipStream_t last = nullptr;     // the stream of the slot's last step (caller thread)
   bool used = false;
-  // the stream and frame of the slot's last assembly, an event recorded on demand (caller thread)
+  // the stream and frames of the slot's last assemblies, an event recorded on demand (caller thread)
   hipStream_t asm_stream = nullptr;
-  void* asm_frame = nullptr;
+  void* asm_frames[kMaxBatch] = {};
+  uint32_t asm_n = 0;
   hipEvent_t asm_order = nullptr;
 };
 
@@ -106,7 +110,8 @@ hipEvent_t pipeline_event() {
 
 struct Job {
   uint32_t slot;
-  void* frame_out;
+  uint32_t nframes;                // frames in the slot (their strips are gathered by one ncclGather)
+  void* frame_out[kMaxBatch];      // rank 0's output frame of each
   hipStream_t rs;  // the slot's render stream: its assembly runs there
   uint32_t W, H, strip, rows_per_rank;
   uint64_t seq;
@@ -134,7 +139,11 @@ struct rt_comm {
   double t_parts[6] = {0, 0, 0, 0, 0, 0};
   uint64_t t_calls = 0;
   Slot slots[kMaxSlots];
-  uint64_t next = 0;
+  uint64_t next = 0;  // slots started
+  // frames per gather (rt_comm_set_batch, the same on every rank) and the slot being filled: its frames so far
+  uint32_t batch = 1, planned_batch = 0;
+  uint32_t fill = 0;
+  Job cur{};
   // the issue thread of the gather side (see the header comment)
   std::thread worker;
   std::mutex mu;
@@ -183,8 +192,12 @@ rt_status issue_tails(rt_comm* c, uint64_t upto);
 
 // waits (host) for every step handed over so far: its gather on the gather stream, its assembly on its
 // render stream
+rt_status finish_slot(rt_comm* c);
+
 rt_status drain(rt_comm* c) {
-  rt_status st = issue_tails(c, ~0ull);
+  rt_status st = finish_slot(c);  // a partly filled slot is gathered as it is (every rank has filled it alike)
+  if (st != RT_OK) return st;
+  st = issue_tails(c, ~0ull);
   if (st != RT_OK) return st;
   wait_issued(c, c->issued);
   if (c->stream && hipStreamSynchronize(c->stream) != hipSuccess) return cfail(c, RT_E_HIP, "rt_render_strips: drain");
@@ -195,7 +208,7 @@ rt_status drain(rt_comm* c) {
 
 // (re)plans the strips of a W x H frame and sizes the pipeline slots; waits for the slots' last uses
 rt_status plan(rt_comm* c, uint32_t W, uint32_t H, uint32_t strip) {
-  if (c->W == W && c->H == H && c->strip == strip) return RT_OK;
+  if (c->W == W && c->H == H && c->strip == strip && c->planned_batch == c->batch) return RT_OK;
   rt_status st = drain(c);
   if (st != RT_OK) return st;
   release_slots(c);
@@ -210,7 +223,7 @@ rt_status plan(rt_comm* c, uint32_t W, uint32_t H, uint32_t strip) {
   }
   const uint32_t nstrips = (H + strip - 1) / strip;
   c->rows_per_rank = ((nstrips + c->nranks - 1) / c->nranks) * strip;
-  const size_t local_bytes = (size_t)c->rows_per_rank * W * 4;
+  const size_t local_bytes = (size_t)c->rows_per_rank * W * 4 * c->batch;
   for (uint32_t k = 0; k < c->nslots; ++k) {
     Slot& s = c->slots[k];
     if (hipMalloc(&s.local, local_bytes) != hipSuccess) return cfail(c, RT_E_OOM, "rt_render_strips: hipMalloc(local)");
@@ -223,6 +236,7 @@ rt_status plan(rt_comm* c, uint32_t W, uint32_t H, uint32_t strip) {
   c->W = W;
   c->H = H;
   c->strip = strip;
+  c->planned_batch = c->batch;
   return RT_OK;
 }
 
@@ -257,7 +271,7 @@ void issue_loop(rt_comm* c) {
     }
     if (c->timing) t1 = clk::now();
     if (st == RT_OK) {
-      const size_t count = (size_t)j.rows_per_rank * j.W * 4;
+      const size_t count = (size_t)j.nframes * j.rows_per_rank * j.W * 4;  // every frame of the slot, one call
       ncclResult_t r = rccl().gather(s.local, c->rank == 0 ? s.gathered : nullptr, count, ncclUint8, 0, c->comm, c->stream);
       if (r != ncclSuccess) {
         st = RT_E_RCCL;
@@ -304,14 +318,24 @@ rt_status issue_tail_job(rt_comm* c, const Job& j) {
   if (c->rank != 0) return RT_OK;
   // two assemblies into one frame buffer on different streams stay in call order
   for (Slot& o : c->slots) {
-    if (&o == &s || o.asm_frame != j.frame_out || !o.asm_stream || o.asm_stream == j.rs) continue;
+    if (&o == &s || !o.asm_stream || o.asm_stream == j.rs) continue;
+    bool shared = false;
+    for (uint32_t a = 0; a < o.asm_n; ++a)
+      for (uint32_t b = 0; b < j.nframes; ++b) shared = shared || o.asm_frames[a] == j.frame_out[b];
+    if (!shared) continue;
     if (hipEventRecord(o.asm_order, o.asm_stream) != hipSuccess || hipStreamWaitEvent(j.rs, o.asm_order, 0) != hipSuccess)
       return cfail(c, RT_E_HIP, "rt_render_strips: order after an assembly into the same frame");
   }
-  const hipError_t e = rt::launch_assemble_strips(j.W, j.H, c->nranks, j.strip, s.gathered, j.frame_out, j.rs);
-  if (e != hipSuccess) return cfail(c, RT_E_HIP, std::string("rt_render_strips: assembly: ") + hipGetErrorString(e));
+  // rank r's block of the gathered slot holds its strips of every frame in turn: frame b starts b frames into it
+  const size_t frame_bytes = (size_t)j.rows_per_rank * j.W * 4;
+  for (uint32_t b = 0; b < j.nframes; ++b) {
+    const hipError_t e = rt::launch_assemble_strips(j.W, j.H, c->nranks, j.strip, (const char*)s.gathered + b * frame_bytes,
+                                                    j.frame_out[b], j.rs, j.nframes * j.rows_per_rank);
+    if (e != hipSuccess) return cfail(c, RT_E_HIP, std::string("rt_render_strips: assembly: ") + hipGetErrorString(e));
+    s.asm_frames[b] = j.frame_out[b];
+  }
   s.asm_stream = j.rs;
-  s.asm_frame = j.frame_out;
+  s.asm_n = j.nframes;
   return RT_OK;
 }
 
@@ -330,6 +354,30 @@ rt_status issue_tails(rt_comm* c, uint64_t upto) {
     const rt_status st = issue_tail_job(c, j);
     if (st != RT_OK) return st;
   }
+  return RT_OK;
+}
+
+// caller thread: the slot being filled is complete (its batch of frames, or fewer at a flush): the render event on
+// its stream, then the gather half handed to the issue thread; its tail becomes pending
+rt_status finish_slot(rt_comm* c) {
+  if (c->fill == 0) return RT_OK;
+  Job job = c->cur;
+  job.nframes = c->fill;
+  c->fill = 0;
+  Slot& s = c->slots[job.slot];
+  if (job.rs != c->stream && hipEventRecord(s.rendered, job.rs) != hipSuccess)
+    return cfail(c, RT_E_HIP, "rt_render_strips: record render");
+  s.used = true;
+  s.last = job.rs;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    job.seq = ++c->issued;
+    c->slot_seq[job.slot] = job.seq;
+    c->jobs.push_back(job);
+    c->posted.store(job.seq, std::memory_order_release);
+  }
+  if (c->sleeping.load(std::memory_order_seq_cst)) c->cv_job.notify_one();
+  c->tails.push_back(job);
   return RT_OK;
 }
 
@@ -450,7 +498,8 @@ const char* rt_comm_last_error(rt_comm_t c) { return c ? c->err.c_str() : "null 
 
 void* rt_comm_stream(rt_comm_t c) {
   if (!c) return nullptr;
-  if (issue_tails(c, ~0ull) != RT_OK) return nullptr;
+  (void)hipSetDevice(c->device);
+  if (finish_slot(c) != RT_OK || issue_tails(c, ~0ull) != RT_OK) return nullptr;
   wait_issued(c, c->issued);  // every step handed over so far is enqueued
   (void)hipSetDevice(c->device);
   // join: the stream returned (the gathers') waits, on the device, for the slots' render streams, where the
@@ -471,7 +520,7 @@ void* rt_comm_stream(rt_comm_t c) {
   return (void*)c->stream;
 }
 
-uint32_t rt_comm_pipeline_depth(rt_comm_t c) { return c ? c->nslots : 0; }
+uint32_t rt_comm_pipeline_depth(rt_comm_t c) { return c ? c->nslots * c->batch : 0; }
 
 rt_status rt_comm_synchronize(rt_comm_t c) {
   if (!c) return RT_E_INVALID;
@@ -498,53 +547,65 @@ rt_status rt_render_strips(rt_comm_t c, uint32_t W, uint32_t H, uint32_t strip_r
     t0 = t1;
   };
   (void)hipSetDevice(c->device);
-  if ((st = plan(c, W, H, strip_rows)) != RT_OK) return st;
-  const uint32_t si = (uint32_t)(c->next % c->nslots);
-  hipStream_t rs = render_stream ? (hipStream_t)render_stream : c->rstreams[si];
-  Slot& s = c->slots[si];
-  if (!c->rows.empty() && (st = rt::check_dispatch(c->ctx, W, H, s.local)) != RT_OK)
-    return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));
-  ++c->next;
-  lap(0);
-  // the slot's previous frame must have left it: the issue thread has enqueued the tail of that step on the
-  // slot's stream (wait for that, rarely: the issue thread keeps up), so a render on the same stream follows
-  // it in stream order; a slot moved to another stream waits for it with an event
-  if (s.used) {
-    // the slot's last tail goes on its stream before this render (and every older pending tail with it)
-    if ((st = issue_tails(c, c->slot_seq[si])) != RT_OK) return st;
-    wait_issued(c, c->slot_seq[si]);
-    lap(3);
-    if (s.last != rs &&
-        (hipEventRecord(s.moved, s.last) != hipSuccess || hipStreamWaitEvent(rs, s.moved, 0) != hipSuccess))
-      return cfail(c, RT_E_HIP, "rt_render_strips: order after the slot's last step");
-    lap(4);
+  if (c->fill && (c->W != W || c->H != H || c->strip != strip_rows)) {
+    if ((st = finish_slot(c)) != RT_OK) return st;  // a new frame size: the slot being filled goes as it is
   }
+  if ((st = plan(c, W, H, strip_rows)) != RT_OK) return st;
+  if (c->fill == 0) {  // a new slot: its first frame picks the render stream every frame of the slot uses
+    const uint32_t si = (uint32_t)(c->next % c->nslots);
+    hipStream_t rs = render_stream ? (hipStream_t)render_stream : c->rstreams[si];
+    Slot& s = c->slots[si];
+    if (!c->rows.empty() && (st = rt::check_dispatch(c->ctx, W, H, s.local)) != RT_OK)
+      return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));
+    ++c->next;
+    lap(0);
+    // the slot's previous frames must have left it: the tail of that step goes on the slot's stream first (waiting
+    // for the issue thread to enqueue its gather, rarely: it keeps up), so a render on the same stream follows it in
+    // stream order; a slot moved to another stream waits for it with an event
+    if (s.used) {
+      if ((st = issue_tails(c, c->slot_seq[si])) != RT_OK) return st;
+      wait_issued(c, c->slot_seq[si]);
+      lap(3);
+      if (s.last != rs &&
+          (hipEventRecord(s.moved, s.last) != hipSuccess || hipStreamWaitEvent(rs, s.moved, 0) != hipSuccess))
+        return cfail(c, RT_E_HIP, "rt_render_strips: order after the slot's last step");
+      lap(4);
+    }
+    c->cur = Job{si, 0, {}, rs, W, H, strip_rows, c->rows_per_rank, 0};
+  } else {
+    lap(0);
+  }
+  Slot& s = c->slots[c->cur.slot];
   if (!c->rows.empty()) {
-    st = rt::dispatch_frame(c->ctx, W, H, c->d_rows, (uint32_t)c->rows.size(), s.local, nullptr, rs);
+    // frame b of the slot: its strips b frames into the slot's buffer, on the slot's render stream
+    char* dst = (char*)s.local + (size_t)c->fill * c->rows_per_rank * W * 4;
+    st = rt::dispatch_frame(c->ctx, W, H, c->d_rows, (uint32_t)c->rows.size(), dst, nullptr, c->cur.rs);
     if (st != RT_OK) return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));
   }
   lap(1);
-  if (rs != c->stream && hipEventRecord(s.rendered, rs) != hipSuccess)
-    return cfail(c, RT_E_HIP, "rt_render_strips: record render");
-  s.used = true;
-  s.last = rs;
-  Job job{si, frame_out, rs, W, H, strip_rows, c->rows_per_rank, 0};
-  {
-    std::lock_guard<std::mutex> lk(c->mu);
-    job.seq = ++c->issued;
-    c->slot_seq[si] = job.seq;
-    c->jobs.push_back(job);
-    c->posted.store(job.seq, std::memory_order_release);
-  }
-  if (c->sleeping.load(std::memory_order_seq_cst)) c->cv_job.notify_one();
+  c->cur.frame_out[c->fill++] = frame_out;
+  if (c->fill == c->batch && (st = finish_slot(c)) != RT_OK) return st;
   lap(2);
-  // the tails whose gathers the issue thread has enqueued by now (no waiting); this step's is pending
+  // the tails whose gathers the issue thread has enqueued by now (no waiting)
   st = issue_tails(c, 0);
   lap(5);
-  c->tails.push_back(job);
   if (st != RT_OK) return st;
   ++c->t_calls;
   return RT_OK;
 }
+
+rt_status rt_comm_set_batch(rt_comm_t c, uint32_t frames_per_gather) {
+  if (!c) return RT_E_INVALID;
+  if (frames_per_gather == 0 || frames_per_gather > kMaxBatch)
+    return cfail(c, RT_E_INVALID, "rt_comm_set_batch: 1 .. 4 frames per gather");
+  if (frames_per_gather == c->batch) return RT_OK;
+  (void)hipSetDevice(c->device);
+  const rt_status st = drain(c);  // the slots are re-planned for the new size at the next frame
+  if (st != RT_OK) return st;
+  c->batch = frames_per_gather;
+  return RT_OK;
+}
+
+uint32_t rt_comm_batch(rt_comm_t c) { return c ? c->batch : 0; }
 
 }  // extern "C"

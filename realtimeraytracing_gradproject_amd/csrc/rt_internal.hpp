@@ -74,8 +74,10 @@ hipError_t launch_trace_rays(const SceneView& scene, const float* rays, uint32_t
                              uint32_t* hits, float* uv, unsigned long long* d_stats, bool stats,
                              hipStream_t stream);
 
+// rank_stride_rows: rows from one rank's block of `gathered` to the next (0: rows_per_rank, one frame per block;
+// a batched gather holds several frames per rank block and passes their total)
 hipError_t launch_assemble_strips(uint32_t W, uint32_t H, uint32_t nranks, uint32_t strip_rows,
-                                  const void* gathered, void* out, hipStream_t stream);
+                                  const void* gathered, void* out, hipStream_t stream, uint32_t rank_stride_rows = 0);
 
 // --- Raster fallback (rt_raster.hip) -------------------------------------------------------
 

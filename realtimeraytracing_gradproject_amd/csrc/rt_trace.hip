@@ -1863,10 +1863,10 @@ hipError_t launch_trace_rays(const SceneView& sc, const float* rays, uint32_t n,
 }
 
 hipError_t launch_assemble_strips(uint32_t W, uint32_t H, uint32_t nranks, uint32_t strip_rows,
-                                  const void* gathered, void* out, hipStream_t s) {
+                                  const void* gathered, void* out, hipStream_t s, uint32_t rank_stride_rows) {
   const uint32_t nstrips = (H + strip_rows - 1) / strip_rows;
   const uint32_t strips_per_rank = (nstrips + nranks - 1) / nranks;
-  const uint32_t rows_per_rank = strips_per_rank * strip_rows;
+  const uint32_t rows_per_rank = rank_stride_rows ? rank_stride_rows : strips_per_rank * strip_rows;  // rank stride
   if (W % 4 == 0 && ((uintptr_t)gathered | (uintptr_t)out) % 16 == 0) {
     const uint32_t W4 = W / 4;
     dim3 grid((W4 + 255) / 256, (H + kAsmRows - 1) / kAsmRows);

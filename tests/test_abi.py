@@ -48,6 +48,8 @@ def test_comm_argument_errors_without_gpu():
     assert rt.lib.rt_render_strips(None, 8, 8, 8, None, None) == rt.RT_E_INVALID
     assert rt.lib.rt_comm_stream(None) is None
     assert rt.lib.rt_comm_pipeline_depth(None) == 0
+    assert rt.lib.rt_comm_set_batch(None, 2) == rt.RT_E_INVALID
+    assert rt.lib.rt_comm_batch(None) == 0
     assert rt.comm_available()  # librccl.so.1 is in the image (dlopen only: no GPU work)
     with pytest.raises(ValueError):
         rt.Comm.__new__(rt.Comm).__init__(type("C", (), {"_lib": rt.lib, "_h": None})(), 1, 0, b"short")

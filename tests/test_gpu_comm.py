@@ -65,3 +65,44 @@ def test_render_strips_moved_slots_shared_frames_and_join():
         assert np.array_equal(bufs[b].cpu().numpy(), o8), f"buffer {b} != frame {last}"
     comm.close()
     c.close()
+
+
+@pytest.mark.parametrize("batch", [2, 3])
+def test_render_strips_batched_gathers(batch):
+    """rt_comm_set_batch: `batch` consecutive frames share one slot and ONE ncclGather. Seven frames with a camera
+    change each (the last slot only partly filled: gathered as it is at rt_comm_synchronize), every frame into its
+    own buffer, the library's own render streams; then two buffers shared by five frames on caller streams. Every
+    frame equals the oracle's."""
+    base = scenes.config("C2F").with_size(320, 184)
+    c = rt.Context(0)
+    scenes.upload(c, base)
+    comm = rt.Comm(c, 1, 0, rt.comm_unique_id())
+    comm.set_batch(batch)
+    assert comm.batch == batch and comm.depth % batch == 0
+    specs, bufs = [], []
+    for k in range(7):
+        sp = base.with_size(base.width, base.height)
+        sp.camera = ((1.5 + 0.3 * k, 1.0 + 0.1 * k, 3.0 - 0.2 * k), (0.0, 0.5, 0.0), (0.0, 1.0, 0.0))
+        specs.append(sp)
+        bufs.append(torch.zeros((sp.height, sp.width, 4), dtype=torch.uint8, device="cuda"))
+        c.set_camera(sp.camera_buffer())
+        comm.render_strips(sp.width, sp.height, bufs[k], None)
+    comm.synchronize()
+    for k in range(7):
+        o8, _, _ = oracle.Scene(specs[k]).render_spec(specs[k], nthreads=16, want_float=False, schedule=1)
+        assert np.array_equal(bufs[k].cpu().numpy(), o8), f"frame {k}"
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    shared = [torch.zeros((base.height, base.width, 4), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    for k in range(5):
+        c.set_camera(specs[k].camera_buffer())
+        comm.render_strips(base.width, base.height, shared[k % 2], streams[k % 2].cuda_stream)
+    torch.cuda.ExternalStream(comm.stream).synchronize()
+    for b, last in ((0, 4), (1, 3)):
+        o8, _, _ = oracle.Scene(specs[last]).render_spec(specs[last], nthreads=16, want_float=False, schedule=1)
+        assert np.array_equal(shared[b].cpu().numpy(), o8), f"shared buffer {b} != frame {last}"
+    with pytest.raises(rt.RtError):
+        comm.set_batch(0)
+    with pytest.raises(rt.RtError):
+        comm.set_batch(5)
+    comm.close()
+    c.close()

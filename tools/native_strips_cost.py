@@ -112,6 +112,15 @@ def main():
         ncall[0] += 1
         comm.render_strips(W, H, frames[si], None)
     out["native_step_library_streams"] = measure(native_own, 3)
+    for b in (2, 4):  # rt_comm_set_batch: b frames per ncclGather (the gather half paid once per b frames)
+        comm.set_batch(b)
+        depth = comm.depth
+        while len(frames) < depth:
+            frames.append(torch.zeros((H, W, 4), dtype=torch.uint8, device=dev))
+        ncall[0] = 0
+        out[f"native_step_library_streams_batch{b}"] = measure(native_own, 3)
+    comm.set_batch(1)
+    depth = comm.depth
     # host cost of the call alone while the GPU is idle-free: the render itself issued alone
     t0 = time.perf_counter()
     for k in range(a.frames):
