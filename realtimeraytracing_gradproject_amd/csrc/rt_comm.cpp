@@ -551,12 +551,13 @@ rt_status rt_render_strips(rt_comm_t c, uint32_t W, uint32_t H, uint32_t strip_r
     if ((st = finish_slot(c)) != RT_OK) return st;  // a new frame size: the slot being filled goes as it is
   }
   if ((st = plan(c, W, H, strip_rows)) != RT_OK) return st;
+  // every frame is validated (the scene may have changed since the slot's first frame)
+  if (!c->rows.empty() && (st = rt::check_dispatch(c->ctx, W, H, c->slots[0].local)) != RT_OK)
+    return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));
   if (c->fill == 0) {  // a new slot: its first frame picks the render stream every frame of the slot uses
     const uint32_t si = (uint32_t)(c->next % c->nslots);
     hipStream_t rs = render_stream ? (hipStream_t)render_stream : c->rstreams[si];
     Slot& s = c->slots[si];
-    if (!c->rows.empty() && (st = rt::check_dispatch(c->ctx, W, H, s.local)) != RT_OK)
-      return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));
     ++c->next;
     lap(0);
     // the slot's previous frames must have left it: the tail of that step goes on the slot's stream first (waiting
