@@ -408,8 +408,8 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
             if rcomm is not None:
                 rcomm.close()
             rcomm, native = None, False
-        elif frames_per_gather > 1:  # the same on every rank (it sizes the collective)
-            rcomm.set_batch(frames_per_gather)
+        elif frames_per_gather > 1:  # the same on every rank (it sizes the collective); the library takes 1 .. 4
+            rcomm.set_batch(min(frames_per_gather, 4))
     nslot = max(nstream, 2 if (strips and pipeline) else 1)
     local = [be.zeros((rows_per_rank, W, 4)) for _ in range(nslot)]
     gathered = ([be.zeros((world, rows_per_rank, W, 4)) if rank == 0 else None for _ in range(nslot)]
