@@ -12,7 +12,8 @@
 // ncclGather on the gather stream and records its completion. The step's tail goes back to the slot's render
 // stream, issued by the caller's thread: a wait for that gather, then rank 0's assembly. The caller issues a tail
 // at a later call once the issue thread has enqueued its gather, so it does not wait for the issue thread, and at
-// the latest before the slot renders again (or at rt_comm_stream / rt_comm_synchronize). So the gather stream carries nothing but the gathers, and the
+// the latest before the slot renders again (or at rt_comm_stream / rt_comm_synchronize). With rt_comm_set_batch(b),
+// b consecutive frames fill one slot (each at its own offset) and share ONE ncclGather and one tail. So the gather stream carries nothing but the gathers, and the
 // slot's next render on its stream follows its tail in stream order (no release event). HIP and RCCL host
 // calls cost microseconds each, so the calls of a step are split over the two threads. With the
 // communicator's own render streams (render_stream NULL), the gather stream and the three render streams sit
@@ -190,10 +191,10 @@ void release_slots(rt_comm* c) {
 void wait_issued(rt_comm* c, uint64_t seq);
 rt_status issue_tails(rt_comm* c, uint64_t upto);
 
-// waits (host) for every step handed over so far: its gather on the gather stream, its assembly on its
-// render stream
 rt_status finish_slot(rt_comm* c);
 
+// waits (host) for every step handed over so far (a partly filled slot is handed over first): its gather on the
+// gather stream, its assembly on its render stream
 rt_status drain(rt_comm* c) {
   rt_status st = finish_slot(c);  // a partly filled slot is gathered as it is (every rank has filled it alike)
   if (st != RT_OK) return st;
