@@ -319,7 +319,7 @@ def pick_tile_rows(be, buf, rows, stream, frames: int = 8, rounds: int = 3):
 def pick_in_flight(be, W, NR, rows, frames: int = 16, rounds: int = 3, choices=(1, 2, 3, 4)):
     """Untimed autotune of the frames in flight: `frames` renders of this rank's share issued round
     robin over the first S streams of one stream pool into S buffers, S in `choices`, interleaved,
-    best of `rounds` (host wall clock around the synchronised loop). With S > 1 the waves of frame
+    best of `rounds` (host wall clock around the synchronised loop); the largest S within 1 % of the fastest. With S > 1 the waves of frame
     k + 1 fill the wave slots the tail of frame k leaves idle (a frame ends with its slowest 8 x 8
     tile; tools/overlap_probe.py). Which streams share a hardware queue is the HIP runtime's choice
     (two streams can land on one queue and then run one after the other), so the count is
@@ -338,7 +338,11 @@ def pick_in_flight(be, W, NR, rows, frames: int = 16, rounds: int = 3, choices=(
                 be.dispatch(bufs[k % n], rows, pool[k % n])
             be.synchronize()
             best[n] = min(best[n], (time.perf_counter() - t0) * 1e3 / frames)
-    pick = min(choices, key=lambda n: (best[n], n))
+    # near-ties (within 1 %, the measurement's noise) go to the most frames in flight: in a short timed region
+    # (the driver's 20 frames) two streams run their frames in lockstep pairs, three or four keep the SIMDs fuller
+    # (profiles/r03_short_region_probe.txt, tools/short_inflight.sh)
+    fastest = min(best.values())
+    pick = max(n for n in choices if best[n] <= fastest * 1.01)
     return pick, {n: round(v, 4) for n, v in best.items()}, pool[:pick]
 
 
