@@ -54,3 +54,23 @@ def test_pick_in_flight_keeps_one_without_streams():
     class NoStreams:
         pass
     assert bench.pick_in_flight(NoStreams(), 8, 8, None) == (1, None, None)
+
+
+def test_pick_in_flight_near_ties_take_more_streams(monkeypatch):
+    """Measured times within 1 % of the fastest count as a tie: the autotune then takes the most frames in flight
+    (a short timed region runs two streams' frames in lockstep pairs)."""
+    be = FakeBackend([0, 1, 2, 3])
+    fake = {1: 0.130, 2: 0.1150, 3: 0.1155, 4: 0.1170}
+    times = iter([])
+
+    def fake_counter():
+        return next(times)
+    # one round over choices 1..4: each measurement is two perf_counter reads (start, end)
+    seq = []
+    for n in (1, 2, 3, 4):
+        seq += [0.0, fake[n] * 16 / 1e3]
+    times = iter(seq)
+    monkeypatch.setattr(bench.time, "perf_counter", fake_counter)
+    s, ms, streams = bench.pick_in_flight(be, 8, 8, None, frames=16, rounds=1)
+    assert s == 3 and len(streams) == 3  # 3 is within 1 % of 2's 0.1150; 4 is not
+    assert ms[2] == 0.115 and ms[3] == 0.1155
