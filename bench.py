@@ -7,14 +7,19 @@ reference's DispatchRays, D3D12HelloTriangle.cpp:558-592). The scene is static: 
 runs once before the timed region and is reported separately (build_ms).
 
 Multi-GPU (north star "frames are tiled across GPUs with an RCCL gather"): with
-N > 1 a step is ONE frame split into interleaved 8-row strips (strip s -> rank s mod N), each rank
-renders its strips into a compact buffer, one RCCL gather brings them to rank 0 and
-rt_assemble_strips un-interleaves them there: total work fixed, "scaling": "strong". The gather
-and assembly of frame k run on a second stream, overlapped with the render of frame k+1 (two
-buffer slots; a slot is re-rendered only after its gather finished). `bench.py --gpus N` without
+N > 1 a step is ONE frame split into interleaved 8-row strips (strip s -> rank s mod N): total work
+fixed, "scaling": "strong". The loop is the library's own (rt_comm_* / rt_render_strips_frames behind
+the C-ABI, csrc/rt_comm.cpp): each rank renders its strips as RGB8 into a pipeline slot on one of the
+communicator's render streams, --frames-per-gather consecutive frames share a slot and ONE ncclGather
+into rank 0 (--frames-per-launch of them rendered by one launch), and rank 0 assembles the RGBA8 frames
+back on the slot's stream; gathers of one slot overlap the renders of the next. The frame latency
+(enqueue -> frame assembled on rank 0, gather included) is timed after the timed region with
+one frame per gather, one frame at a time (config.frame_latency_ms). `bench.py --gpus N` without
 torchrun re-launches itself under torch.distributed.run (N processes, one per GPU) before anything
 touches the GPU. The multi-GPU configs C4 (rabbit x64, 2 lights) and C5 (rabbit x256, 4 lights,
-4K, 4 spp) are timed the same way at the same N and reported under "extra".
+4K, 4 spp) are timed the same way at the same N and reported under "extra". When RCCL cannot be
+used, the ranks fall back to a torch.distributed gather loop (config.strips_loop names the loop).
+--loopback N (rehearsal, world 1): the library's loopback transport emulates N ranks on one GPU.
 
 Frames in flight: consecutive frames are issued round robin over S render streams, each frame into
 its own buffer slot, so the waves of frame k + 1 fill the wave slots the tail of frame k leaves
@@ -85,6 +90,14 @@ def parse(argv=None):
     p.add_argument("--frames-per-gather", type=int, default=4,
                    help="strips through the native loop: consecutive frames whose strips one ncclGather moves "
                         "(rt_comm_set_batch; the gather half of a step is paid once per this many frames)")
+    p.add_argument("--frames-per-launch", type=int, default=0,
+                   help="strips through the native loop: frames rendered by one launch per rank "
+                        "(rt_render_strips_frames); 0 = --frames-per-gather")
+    p.add_argument("--loopback", type=int, default=0,
+                   help="rehearsal at world 1 (tests): the native strips loop over the library's loopback transport "
+                        "emulating this many ranks on one GPU (rt_comm_init_loopback)")
+    p.add_argument("--latency-frames", type=int, default=20,
+                   help="strips: single frames timed enqueue -> assembled on rank 0 (config.frame_latency_ms)")
     p.add_argument("--in-flight", type=int, default=0,
                    help="frames in flight (render streams, one buffer each); 0 = untimed autotune over 1..4")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -255,17 +268,24 @@ class HipBackend:
         issued from C++); the gloo rehearsal on one device keeps the torch.distributed loop."""
         return os.environ.get("RT_BENCH_ONE_DEVICE") != "1" and os.environ.get("RT_BENCH_TORCH_STRIPS") != "1"
 
-    def comm_open(self, world: int, rank: int):
-        """rt_comm over this rank's context: rank 0's ncclUniqueId is broadcast over the torch process group."""
+    def comm_open(self, world: int, rank: int, loopback: int = 0):
+        """rt_comm over this rank's context: rank 0's ncclUniqueId is broadcast over the torch process group.
+        loopback N (world 1): the library's loopback transport emulating N ranks on this GPU."""
+        if loopback:
+            return self.rt.Comm.loopback(self.ctx, loopback)
         with stdout_to_stderr():
             uid = self.rt.comm_unique_id() if rank == 0 else bytes(self.rt.RT_COMM_ID_BYTES)
             t = torch.tensor(list(uid), dtype=torch.uint8, device=self.device)
             dist.broadcast(t, 0)
             return self.rt.Comm(self.ctx, world, rank, bytes(t.cpu().tolist()))
 
-    def render_strips(self, comm, frame, stream):
-        comm.render_strips(self.spec.width, self.spec.height, frame, stream.cuda_stream if stream is not None else None,
-                           STRIP_ROWS)
+    def render_strips(self, comm, frames, stream):
+        """len(frames) frames in one rt_render_strips_frames call (one launch per rank)."""
+        s = stream.cuda_stream if stream is not None else None
+        if len(frames) == 1:
+            comm.render_strips(self.spec.width, self.spec.height, frames[0], s, STRIP_ROWS)
+        else:
+            comm.render_strips_frames(self.spec.width, self.spec.height, frames, None, s, STRIP_ROWS)
 
     def close(self):
         if self.ctx is not None:
@@ -348,7 +368,7 @@ def pick_in_flight(be, W, NR, rows, frames: int = 16, rounds: int = 3, choices=(
 
 def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_ms: float, strips: bool,
                pipeline: bool, schedule: str, save_image: str = "", in_flight: int = 0, resettle_ms: float = 0.0,
-               frames_per_gather: int = 1):
+               frames_per_gather: int = 1, frames_per_launch: int = 0, loopback: int = 0, latency_frames: int = 20):
     """Builds the scene, counts one step's rays (untimed), settles, warms up, then times exactly
     `steps` steps between barrier + synchronize on both sides. Returns a dict (rank 0 meaningful).
     in_flight: frames in flight (render streams, each with its own buffer slot); 0 = autotune."""
@@ -356,7 +376,9 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
     distributed = world > 1
     W, H = spec.width, spec.height
     build = be.load(spec, schedule)
-    if strips:
+    if strips and loopback:  # one process renders every emulated rank's strips: time and count the whole frame
+        rows, rows_per_rank = None, H
+    elif strips:
         rows, rows_per_rank = strip_plan(H, world, rank)
     else:
         rows, rows_per_rank = None, H
@@ -395,14 +417,14 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
         nstream, flight_ms, measured = pick_in_flight(be, W, NR, rows)
     render = measured if measured else [be.stream() for _ in range(nstream)]
     native = strips and getattr(be, "native_strips", False)
-    if native:  # every rank must agree before the collective rt_comm_init (no RCCL: the torch.distributed loop)
+    if native and not loopback:  # every rank agrees before the collective rt_comm_init (no RCCL: the torch loop)
         ok = torch.tensor([1.0 if be.rt.comm_available() else 0.0], dtype=torch.float64, device=be.device)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         native = ok.item() == 1.0
     rcomm = None
     if native:  # a communicator that fails to come up on any rank sends every rank to the torch.distributed loop
         try:
-            rcomm = be.comm_open(world, rank)
+            rcomm = be.comm_open(world, rank, loopback) if loopback else be.comm_open(world, rank)
         except Exception as ex:  # noqa: BLE001  (RtError from rt_comm_init: reported, then the fallback)
             print(f"bench: rt_comm_init failed on rank {rank} ({ex}); using the torch.distributed strips loop",
                   file=sys.stderr, flush=True)
@@ -425,16 +447,27 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
     parts = [D.gather_parts(gathered[s], world, rank) for s in range(nslot)] if strips and not native else None
 
     ncall = [0]
+    fpl = max(1, min(frames_per_launch or (rcomm.batch if rcomm is not None else 1), 4))
+    if rcomm is not None:
+        fpl = min(fpl, rcomm.batch)
 
-    def step_native(k: int):
-        """One frame through rt_render_strips: render on the slot's stream, ncclGather on the communicator's
-        gather stream, rank 0's assembly back on the slot's stream, the slot pipeline and its events inside the
-        library (one C call). The library's slot is its call count mod its depth; frame buffer i serves slot i."""
-        s = ncall[0] % rcomm.depth
-        ncall[0] += 1
+    def issue_native(n: int, per_call: int):
+        """n frames through rt_render_strips_frames, `per_call` per call (one launch per call on this rank): render
+        on a slot's stream, ncclGather on the communicator's gather stream, rank 0's assembly back on the slot's
+        stream, the slot pipeline and its events inside the library. Frame buffer i serves the i-th frame mod the
+        pipeline depth."""
         # frames in flight: the communicator's own three render streams (NULL), which sit on hardware queues of
         # their own, apart from the gathers' (DESIGN §7); one frame at a time: this rank's stream
-        be.render_strips(rcomm, frame[s] if rank == 0 else None, render[0] if nstream == 1 else None)
+        rs = render[0] if nstream == 1 else None
+        while n > 0:
+            m = min(n, per_call)
+            bufs = [frame[(ncall[0] + j) % rcomm.depth] if rank == 0 else None for j in range(m)]
+            ncall[0] += m
+            be.render_strips(rcomm, bufs, rs)
+            n -= m
+
+    def step_native(k: int):
+        issue_native(1, 1)
 
     def step(k: int):
         """One frame. In strips mode the caller holds `comm` as the current stream (the gather runs
@@ -480,9 +513,13 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
 
     # warmup (untimed)
     with on_comm():
-        for _ in range(warmup):
-            step(k)
-            k += 1
+        if native:
+            issue_native(warmup, fpl)
+            k += warmup
+        else:
+            for _ in range(warmup):
+                step(k)
+                k += 1
     drain()
     if distributed:
         dist.barrier()
@@ -496,9 +533,13 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
     t0 = time.perf_counter()
     e0.record(render[0])
     with on_comm():
-        for _ in range(steps):
-            step(k)
-            k += 1
+        if native:
+            issue_native(steps, fpl)
+            k += steps
+        else:
+            for _ in range(steps):
+                step(k)
+                k += 1
     e1.record(render[0])
     drain()
     if distributed:
@@ -525,6 +566,28 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
     else:
         kernel_ms = render_ms
 
+    # frame latency (dispatch enqueue -> the RGBA8 frame complete on the root GPU, the RCCL gather
+    # included; the reference's frame time spans submit -> fence, D3D12HelloTriangle.cpp:436-470): strips mode, one
+    # frame per gather, one frame at a time, host clock from the call to the synchronised drain; rank 0's median
+    latency_ms = None
+    if strips and latency_frames > 0:
+        if rcomm is not None:
+            rcomm.set_batch(1)
+        lat = []
+        with on_comm():
+            for _ in range(latency_frames):
+                if distributed:
+                    dist.barrier()
+                t1 = time.perf_counter()
+                if native:
+                    issue_native(1, 1)
+                else:
+                    step(k)
+                    k += 1
+                drain()
+                lat.append(time.perf_counter() - t1)
+        latency_ms = float(np.median(lat)) * 1e3
+
     if save_image and rank == 0:
         last = (ncall[0] - 1) % rcomm.depth if native else (k - 1) % nslot
         if native:
@@ -535,9 +598,12 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
     if rcomm is not None:
         rcomm.close()
     return {"rays_step": rays_step, "primary": int(counts[1].item()), "shadow": int(counts[2].item()), "fpg": fpg,
+            "fpl": fpl if native else None, "latency_ms": latency_ms, "loopback": loopback if native else 0,
             "tmax": tmax, "kernel_ms": kernel_ms, "stats": st, "build": build, "rows_local": len(rows) if strips else H,
             "tile_rows": tile_rows, "tile_ms": tile_ms, "in_flight": nstream, "in_flight_ms": flight_ms,
-            "strips_loop": ("rt_render_strips (C-ABI: render -> ncclGather -> assembly; "
+            "strips_loop": ("rt_render_strips_frames (C-ABI: render RGB8 strips -> "
+                            + (f"loopback gather of {loopback} emulated ranks" if loopback else "ncclGather")
+                            + " -> RGBA8 assembly; "
                             + ("the communicator's 3 render streams)" if nstream > 1 else "one render stream)")
                             if native else
                             "torch.distributed gather" if strips else None)}
@@ -761,7 +827,8 @@ def main(argv=None) -> int:
 
     spec = spec_of(a.config)
     r = run_config(be, spec, world, rank, a.steps, a.warmup, a.settle_ms, strips, not a.no_pipeline, a.schedule,
-                   a.save_image, a.in_flight, a.resettle_ms, a.frames_per_gather)
+                   a.save_image, a.in_flight, a.resettle_ms, a.frames_per_gather, a.frames_per_launch, a.loopback,
+                   a.latency_frames)
 
     extra = []
     names = a.extra if a.extra is not None else ("C4,C5" if distributed else "C1,C2F,C3,C4,C5,REF")
@@ -770,7 +837,9 @@ def main(argv=None) -> int:
         # few frames: C5 is ~8 ms per frame on one GPU
         n_steps = max(3, a.steps // (20 if es.spp > 1 else 4))
         x = run_config(be, es, world, rank, n_steps, 2, 0.0, strips, not a.no_pipeline, a.schedule,
-                       in_flight=a.in_flight, resettle_ms=a.resettle_ms, frames_per_gather=a.frames_per_gather)
+                       in_flight=a.in_flight, resettle_ms=a.resettle_ms, frames_per_gather=a.frames_per_gather,
+                       frames_per_launch=a.frames_per_launch, loopback=a.loopback,
+                       latency_frames=min(a.latency_frames, 5))
         if rank == 0:
             st = x["stats"]
             rays = max(x["rays_step"], 1)
@@ -779,6 +848,7 @@ def main(argv=None) -> int:
                           "rays_per_step": x["rays_step"], "resolution": f"{es.width}x{es.height}", "spp": es.spp,
                           "n_gpus": world, "parallelism": f"strips{world}+gather" if strips else f"frames{world}",
                           "tile_rows": x["tile_rows"], "frames_in_flight": x["in_flight"],
+                          "frame_latency_ms": None if x["latency_ms"] is None else round(x["latency_ms"], 4),
                           "aabb_tests_per_ray_rank0": round(st["aabb_tests"] / rays, 2) if not distributed else None,
                           "node_fetches": int(st["node_fetches"]), "tri_fetches": int(st["tri_fetches"])})
     if not distributed and (a.extra is None) and isinstance(be, HipBackend):
@@ -812,12 +882,18 @@ def main(argv=None) -> int:
                        "parallelism": (f"strips{world}+gather" + ("" if a.no_pipeline else " (pipelined)")) if strips
                        else f"frames{world}",
                        "rccl_world_size": world if (distributed or strips) else None, "strips_loop": r["strips_loop"],
-                       "frames_per_gather": r["fpg"],
+                       "frames_per_gather": r["fpg"], "frames_per_launch": r["fpl"],
+                       "loopback_ranks": r["loopback"] or None,
+                       # SURVEY 8(d)'s frame latency in strips mode: enqueue -> assembled on rank 0, gather included,
+                       # one frame per gather, one at a time (the batched throughput is `value`)
+                       "frame_latency_ms": None if r["latency_ms"] is None else round(r["latency_ms"], 4),
                        "schedule": a.schedule,
                        "tile_rows": r["tile_rows"], "tile_ms_rank0": r["tile_ms"],
                        "frames_in_flight": r["in_flight"], "in_flight_ms_rank0": r["in_flight_ms"],
-                       # SURVEY 8(d)'s frame latency: one frame alone, enqueue -> complete (one stream, back to back)
+                       # one frame alone on one stream, back to back (this rank's render; at N = 1 without strips
+                       # this is SURVEY 8(d)'s frame latency: enqueue -> complete)
                        "frame_ms_one_stream": round(r["kernel_ms"], 4),
+                       "frame_ms_one_stream_is_latency": not strips,
                        "settle_ms": a.settle_ms, "resettle_ms": a.resettle_ms},
             "roofline": rf,
             "cpu_baseline": cpu,

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RT_API_VERSION 3
+#define RT_API_VERSION 4
 
 typedef struct rt_ctx* rt_ctx_t;
 typedef struct rt_mesh* rt_mesh_t;
@@ -208,6 +208,12 @@ rt_status rt_set_stats(rt_ctx_t ctx, int enable);
  * small ring of slots, each ordered on the device after the other streams' last uses of it (no host wait). */
 rt_status rt_dispatch_rays(rt_ctx_t ctx, uint32_t W, uint32_t H, const uint32_t* rows,
                            uint32_t nrows, void* rgba8_dev, float* rgba32f_dev, void* hip_stream);
+/* Stream lifetime: the context notes (host-side, no event per launch) which streams launched with the current
+ * TLAS version, and records one event on each of them when the next rt_tlas_build swaps that version out. A caller
+ * that destroys a stream it launched on (rt_dispatch_rays, rt_trace_rays) before that build calls
+ * rt_forget_stream(ctx, stream) first: the event is recorded now, while the stream is valid. (The reference's
+ * command lists and fences have no equivalent: D3D12HelloTriangle.cpp:627-647 waits for the GPU every frame.) */
+rt_status rt_forget_stream(rt_ctx_t ctx, void* hip_stream);
 
 /* TraceRay ray flags (the D3D12_RAY_FLAG values the reference passes, Common.hlsl:44-82). */
 enum {
@@ -283,6 +289,14 @@ rt_status rt_comm_available(void);
 rt_status rt_comm_get_unique_id(void* id_out);
 /* ncclCommInitRank on the context's device. Collective: returns once all nranks ranks have joined. */
 rt_status rt_comm_init(rt_ctx_t ctx, uint32_t nranks, uint32_t rank, const void* id, rt_comm_t* out);
+/* Test transport, no RCCL: ONE process stands in for all `nranks` ranks on the context's GPU (1 .. 64). Each
+ * rt_render_strips renders every rank's strips into that rank's block of the pipeline slot, and the gather is a
+ * device copy into rank 0's rank-major buffer, issued on the gather stream by the issue thread at the point where
+ * the RCCL communicator calls ncclGather. Strip plan, frame batching, events, tails and the rank-strided assembly
+ * are the RCCL path's, so the N > 1 frame layout runs on a one-GPU box. The communicator is rank 0. */
+rt_status rt_comm_init_loopback(rt_ctx_t ctx, uint32_t nranks, rt_comm_t* out);
+/* Drains the pipeline first (a partly filled slot is gathered and assembled as it is, every rank alike: destroy
+ * is collective like the frames), then stops the issue thread. Destroy communicators before their context. */
 rt_status rt_comm_destroy(rt_comm_t comm);
 const char* rt_comm_last_error(rt_comm_t comm);
 /* The communicator's gather stream, made to wait (on the device) for every step issued so far, the
@@ -306,18 +320,30 @@ rt_status rt_comm_set_batch(rt_comm_t comm, uint32_t frames_per_gather);
 uint32_t rt_comm_batch(rt_comm_t comm);
 /* One tiled frame, collective over the ranks (every rank calls it, in the same frame order): this rank's
  * strips are rendered on render_stream into one of the communicator's pipeline slots (NULL: slot k's own
- * stream of the communicator; its render streams and its gather stream sit on separate hardware queues). The gather stream waits for that render (a device-side event) and runs ONE ncclGather of every
- * rank's slot into rank 0; the step's tail returns to render_stream: a wait for that gather and, on rank 0, the
- * assembly of the W x H RGBA8 frame into frame_out (device buffer; ignored on other ranks). The tail is issued
- * by a later call once the gather is enqueued, at the latest before the slot renders again (or by rt_comm_stream /
- * rt_comm_synchronize). The slot's next render on the same stream
- * follows its tail in stream order; a slot moved to another stream, and two assemblies into one frame_out on
- * different streams, are ordered by events. No host waits: frame k's gather overlaps frame k + 1's render, and
+ * stream of the communicator; its render streams and its gather stream sit on separate hardware queues). The
+ * strips are RGB8 (3 bytes a pixel: the alpha byte of the frame is the constant 255 and is restored by the
+ * assembly, so it never crosses xGMI). The gather stream waits for that render (a device-side event) and runs ONE
+ * ncclGather of every rank's slot into rank 0; the step's tail returns to render_stream: a wait for that gather
+ * and, on rank 0, the assembly of the W x H RGBA8 frame into frame_out (device buffer; ignored on other ranks).
+ * The tail is issued by a later call once the gather is enqueued, at the latest before the slot renders again (or
+ * by rt_comm_stream / rt_comm_synchronize). The slot's next render on the same stream follows its tail in stream
+ * order; a slot moved to another stream, and two assemblies into one frame_out on different streams, are ordered
+ * by events. With rt_comm_set_batch(b > 1) a slot's later frames may name another render_stream than its first:
+ * the slot's stream then waits for the work already queued on that stream before rendering the frame, and the
+ * frame's tail is returned to it by an event. No host waits: frame k's gather overlaps frame k + 1's render, and
  * frames on different streams overlap (frames in flight). Asynchronous: frame_out is complete once the work
  * enqueued on rt_comm_stream(comm) after that call has run, or after rt_comm_synchronize. Streams passed must
  * stay valid until then. */
 rt_status rt_render_strips(rt_comm_t comm, uint32_t W, uint32_t H, uint32_t strip_rows, void* frame_out,
                            void* render_stream);
+/* nframes (1 .. rt_comm_batch, at most 4) consecutive frames of the loop in ONE call: this rank renders their
+ * strips in ONE launch (the frame index is the launch's third grid dimension, so a rank's share of several frames
+ * fills the GPU as one grid and pays one launch) into one pipeline slot; frame b uses the camera buffer
+ * cameras[64 b .. 64 b + 63] (rt_set_camera's layout; NULL: the context's camera for every frame) and is assembled
+ * on rank 0 into frames_out[b]. Frames that do not fit the slot being filled start a new slot. Otherwise exactly
+ * nframes calls of rt_render_strips (lights, material, TLAS are the context's at the call). */
+rt_status rt_render_strips_frames(rt_comm_t comm, uint32_t W, uint32_t H, uint32_t strip_rows, uint32_t nframes,
+                                  const float* cameras, void* const* frames_out, void* render_stream);
 
 /* Copies the counters (RT_STAT_*) to out[RT_STAT_COUNT]; synchronises the context. */
 rt_status rt_stats(rt_ctx_t ctx, uint64_t out[RT_STAT_COUNT]);

@@ -105,6 +105,7 @@ SIGNATURES = [
     ("rt_raster_draw", _I, [_P, _UP, _U32, _FP, _U32, _U32, _P, _P, _P]),
     ("rt_assemble_strips", _I, [_P, _U32, _U32, _U32, _U32, _P, _P, _P]),
     ("rt_strip_rows", _U32, [_U32, _U32, _U32, _U32, _P, _U32]),
+    ("rt_forget_stream", _I, [_P, _P]),
     ("rt_event_create", _I, [ctypes.POINTER(_P)]),
     ("rt_event_destroy", _I, [_P]),
     ("rt_event_record", _I, [_P, _P]),
@@ -112,11 +113,13 @@ SIGNATURES = [
     ("rt_comm_available", _I, []),
     ("rt_comm_get_unique_id", _I, [_P]),
     ("rt_comm_init", _I, [_P, _U32, _U32, _P, ctypes.POINTER(_P)]),
+    ("rt_comm_init_loopback", _I, [_P, _U32, ctypes.POINTER(_P)]),
     ("rt_comm_destroy", _I, [_P]),
     ("rt_comm_last_error", ctypes.c_char_p, [_P]),
     ("rt_comm_stream", _P, [_P]),
     ("rt_comm_synchronize", _I, [_P]),
     ("rt_render_strips", _I, [_P, _U32, _U32, _U32, _P, _P]),
+    ("rt_render_strips_frames", _I, [_P, _U32, _U32, _U32, _U32, _FP, ctypes.POINTER(_P), _P]),
     ("rt_comm_pipeline_depth", _U32, [_P]),
     ("rt_comm_set_batch", _I, [_P, _U32]),
     ("rt_comm_batch", _U32, [_P]),
@@ -400,17 +403,32 @@ class Comm:
     """rt_comm_*: the native multi-GPU frame loop (strips -> ncclGather -> assembly on rank 0) of one context.
     Collective: every rank constructs it with the same 128-byte id and calls render_strips in the same order."""
 
-    def __init__(self, ctx: "Context", nranks: int, rank: int, uid: bytes):
-        if len(uid) != RT_COMM_ID_BYTES:
-            raise ValueError("the communicator id is 128 bytes")
+    def __init__(self, ctx: "Context", nranks: int, rank: int, uid: Optional[bytes]):
+        """uid None: a loopback communicator (rt_comm_init_loopback, tests): this process renders every one of
+        the nranks ranks on its one GPU and the gather is a device copy (rank must be 0)."""
         self._lib = ctx._lib
         self.ctx, self.nranks, self.rank = ctx, nranks, rank
         h = _P()
+        if uid is None:
+            if rank != 0:
+                raise ValueError("a loopback communicator is rank 0")
+            st = self._lib.rt_comm_init_loopback(ctx._h, nranks, ctypes.byref(h))
+            if st != RT_OK:
+                raise RtError(st, f"rt_comm_init_loopback(nranks={nranks})")
+            self._h = h
+            return
+        if len(uid) != RT_COMM_ID_BYTES:
+            raise ValueError("the communicator id is 128 bytes")
         self._idbuf = ctypes.create_string_buffer(uid, RT_COMM_ID_BYTES)
         st = self._lib.rt_comm_init(ctx._h, nranks, rank, self._idbuf, ctypes.byref(h))
         if st != RT_OK:
             raise RtError(st, f"rt_comm_init(nranks={nranks}, rank={rank})")
         self._h = h
+
+    @classmethod
+    def loopback(cls, ctx: "Context", nranks: int) -> "Comm":
+        """rt_comm_init_loopback: nranks ranks emulated by this process on its one GPU (no RCCL)."""
+        return cls(ctx, nranks, 0, None)
 
     def _check(self, st: int, what: str):
         if st != RT_OK:
@@ -421,6 +439,17 @@ class Comm:
         """One tiled frame (rt_render_strips): frame_out is rank 0's H x W x 4 device buffer."""
         self._check(self._lib.rt_render_strips(self._h, width, height, strip_rows_, _ptr(frame_out), stream),
                     "rt_render_strips")
+
+    def render_strips_frames(self, width: int, height: int, frames_out, cameras=None, stream: Optional[int] = None,
+                             strip_rows_: int = 8):
+        """rt_render_strips_frames: len(frames_out) frames in one launch per rank (cameras: n x 64 floats or None =
+        the context's camera); frames_out: rank 0's device buffers (None entries on other ranks)."""
+        n = len(frames_out)
+        ptrs = (_P * n)(*[_ptr(f) for f in frames_out])
+        cams = None if cameras is None else _f32(cameras, 64 * n)
+        self._check(self._lib.rt_render_strips_frames(self._h, width, height, strip_rows_, n,
+                                                      None if cams is None else _fptr(cams), ptrs, stream),
+                    "rt_render_strips_frames")
 
     @property
     def stream(self) -> int:
@@ -445,9 +474,12 @@ class Comm:
         self._check(self._lib.rt_comm_synchronize(self._h), "rt_comm_synchronize")
 
     def close(self):
+        """rt_comm_destroy: drains the pipeline (a partly filled batch included), then frees the communicator."""
         if getattr(self, "_h", None):
-            self._lib.rt_comm_destroy(self._h)
-            self._h = None
+            h, self._h = self._h, None
+            st = self._lib.rt_comm_destroy(h)
+            if st != RT_OK:
+                raise RtError(st, "rt_comm_destroy")
 
     def __del__(self):
         try:
@@ -633,6 +665,10 @@ class Context:
         self._check(self._lib.rt_raster_draw(self._h, d.ctypes.data_as(_UP), len(d),
                                              None if x is None else _fptr(x), width, height, _ptr(rgba8),
                                              _ptr(depth), stream), "rt_raster_draw")
+
+    def forget_stream(self, stream: int):
+        """rt_forget_stream: call before destroying a stream this context launched on (see rt_api.h)."""
+        self._check(self._lib.rt_forget_stream(self._h, stream), "rt_forget_stream")
 
     def assemble_strips(self, width: int, height: int, nranks: int, strip_rows_: int, gathered, out,
                         stream: Optional[int] = None):

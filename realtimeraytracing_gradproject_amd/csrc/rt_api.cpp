@@ -165,13 +165,18 @@ struct TlasVersion {
 // A launch on s that read TLAS version v is noted host-side only (note_reader); when v stops being current,
 // one event per reader stream is recorded (note_swap_out): it covers every earlier launch on that stream, so a
 // later build into v orders after all of them without an event record per launch.
+// The readers list is cleared on every path: a failed record (a stream the caller destroyed without
+// rt_forget_stream) would otherwise fail every later update. After a failure the launches of the failed readers
+// are not covered by an event, so the device is drained instead (their buffers may be rewritten next).
 hipError_t note_swap_out(TlasVersion& v) {
+  hipError_t first = hipSuccess;
   for (hipStream_t r : v.readers) {
-    hipError_t e = slot_mark_use(v.use, r);
-    if (e != hipSuccess) return e;
+    const hipError_t e = slot_mark_use(v.use, r);
+    if (e != hipSuccess && first == hipSuccess) first = e;
   }
   v.readers.clear();
-  return hipSuccess;
+  if (first != hipSuccess) (void)hipDeviceSynchronize();
+  return first;
 }
 
 hipError_t note_reader(TlasVersion& v, hipStream_t s) {
@@ -718,13 +723,7 @@ rt_status rt_tlas_export(rt_ctx_t c, void* nodes, size_t nodes_bytes) {
 
 rt_status rt_set_camera(rt_ctx_t c, const float cb[64]) {
   if (!c || !cb) return fail(c, RT_E_INVALID, "rt_set_camera: null argument");
-  std::memcpy(c->fp.cb, cb, 64 * sizeof(float));
-  {
-    // RayGen's origin, uniform over the frame: the device's own hlsl_mul4 (RT_HD, no contraction)
-    // evaluated once here gives the bits the kernel would compute
-    const float zero_one[4] = {0.0f, 0.0f, 0.0f, 1.0f};
-    rt::hlsl_mul4(c->fp.cb + 32, zero_one, c->fp.cam_origin);
-  }
+  std::memcpy(c->fp.cb, cb, 64 * sizeof(float));  // RayGen's constants are derived per launch (frame_cam)
   c->have_camera = true;
   return RT_OK;
 }
@@ -907,6 +906,19 @@ static rt_status ensure_rows(rt_ctx* c, const uint32_t* rows, uint32_t nrows, hi
 namespace rt {
 
 int ctx_device(rt_ctx* c) { return c ? c->device : 0; }
+
+hipError_t ctx_forget_stream(rt_ctx* c, hipStream_t s) {
+  if (!c || !s) return hipSuccess;
+  hipError_t first = hipSuccess;
+  for (TlasVersion& v : c->ver) {
+    auto it = std::find(v.readers.begin(), v.readers.end(), s);
+    if (it == v.readers.end()) continue;
+    v.readers.erase(it);
+    const hipError_t e = slot_mark_use(v.use, s);  // covers every launch of s so far
+    if (e != hipSuccess && first == hipSuccess) first = e;
+  }
+  return first;
+}
 void* ctx_stream(rt_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 rt_status check_dispatch(rt_ctx* c, uint32_t W, uint32_t H, const void* rgba8) {
@@ -918,22 +930,45 @@ rt_status check_dispatch(rt_ctx* c, uint32_t W, uint32_t H, const void* rgba8) {
   return RT_OK;
 }
 
+// RayGen's per-frame constants from a camera buffer (UpdateCameraBuffer's 256 B, D3D12HelloTriangle.cpp:1144-1170):
+// viewInverse and projectionInverse as the HLSL reads them, and the origin mul(viewInverse, (0, 0, 0, 1)) by the
+// device's own hlsl_mul4 (RT_HD, no contraction), so the kernel gets the bits it would compute.
+void frame_cam(const float cb[64], FrameCam& cam) {
+  std::memcpy(cam.view_inv, cb + 32, 16 * sizeof(float));
+  std::memcpy(cam.proj_inv, cb + 48, 16 * sizeof(float));
+  const float zero_one[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+  rt::hlsl_mul4(cb + 32, zero_one, cam.origin);
+}
+
 // The frame launch behind rt_dispatch_rays and rt_render_strips (d_rows: a device row list or null; the
 // caller validated the arguments with check_dispatch and keeps d_rows alive until the launch completed).
+// nframes frames in one launch (the grid's z): frame z with camera buffer cams[64 z ..] (null: the context's
+// camera for every frame) into out + z * frame_stride bytes (0: nrows * W * out_bpp, compact); out_bpp 4 = RGBA8,
+// 3 = RGB8 (strips).
 rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_rows, uint32_t nrows, void* rgba8,
-                         float* rgba32f, hipStream_t s) {
+                         float* rgba32f, hipStream_t s, uint32_t out_bpp, uint32_t nframes, const float* cams,
+                         uint64_t frame_stride) {
+  if (nframes < 1 || nframes > (uint32_t)rt::kMaxLaunchFrames || (out_bpp != 3 && out_bpp != 4) ||
+      (nframes > 1 && rgba32f))
+    return fail(c, RT_E_INVALID, "dispatch: 1..4 frames per launch, RGBA8 or RGB8, float output for one frame only");
+  const uint64_t frame_bytes = frame_stride ? frame_stride : (uint64_t)nrows * W * out_bpp;
+  if (frame_bytes * nframes >= 0xffffffffull) return fail(c, RT_E_UNSUPPORTED, "dispatch: frame exceeds 4 GB");
   c->fp.width = W;
   c->fp.height = H;
   c->fp.fwidth = (float)W;  // exact: W, H < 2^24
   c->fp.fheight = (float)H;
   c->fp.nrows = nrows;
   c->fp.tile_rows = c->tile_rows;
+  c->fp.out_bpp = out_bpp;
+  c->fp.nframes = nframes;
+  c->fp.frame_bytes = (uint32_t)frame_bytes;
+  for (uint32_t z = 0; z < nframes; ++z) frame_cam(cams ? cams + 64 * z : c->fp.cb, c->fp.cam[z]);
   rt::SceneView sv = scene_view(c);
   if (sv.stack_cap > rt::kMaxTraversalStack)
     return fail(c, RT_E_UNSUPPORTED, "rt_dispatch_rays: BVH too deep for the traversal stack");
   ScratchSlot* ovf_slot = nullptr;
   {
-    const size_t lanes = (size_t)((W + 15) / 16) * ((nrows + 15) / 16) * 256;
+    const size_t lanes = (size_t)((W + 15) / 16) * ((nrows + 15) / 16) * 256 * nframes;
     rt_status st = ensure_overflow(c, sv, lanes, s, &ovf_slot);
     if (st != RT_OK) return st;
   }
@@ -944,8 +979,8 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
   HIPCHK(c, note_reader(c->ver[c->cur], s), "rt_dispatch_rays: record use");
   if (ovf_slot) HIPCHK(c, slot_mark_use(*ovf_slot, s), "overflow stack: record use");
   if (c->stats_on) {
-    c->dispatches += 1;
-    c->pixels += (uint64_t)W * nrows;
+    c->dispatches += nframes;
+    c->pixels += (uint64_t)W * nrows * nframes;
   }
   return RT_OK;
 }
@@ -1089,7 +1124,7 @@ rt_status rt_dispatch_rays(rt_ctx_t c, uint32_t W, uint32_t H, const uint32_t* r
   const uint32_t* d_rows = nullptr;
   ScratchSlot* rows_slot = nullptr;
   if (rows && (st = ensure_rows(c, rows, nrows, s, &rows_slot, &d_rows)) != RT_OK) return st;
-  if ((st = rt::dispatch_frame(c, W, H, d_rows, nrows, rgba8, rgba32f, s)) != RT_OK) return st;
+  if ((st = rt::dispatch_frame(c, W, H, d_rows, nrows, rgba8, rgba32f, s, 4, 1, nullptr, 0)) != RT_OK) return st;
   if (rows_slot) HIPCHK(c, slot_mark_use(*rows_slot, s), "rows: record use");
   return RT_OK;
 }
@@ -1148,6 +1183,13 @@ uint32_t rt_strip_rows(uint32_t H, uint32_t nranks, uint32_t rank, uint32_t stri
       ++n;
     }
   return n;
+}
+
+rt_status rt_forget_stream(rt_ctx_t c, void* stream) {
+  if (!c || !stream) return RT_E_INVALID;
+  (void)hipSetDevice(c->device);
+  HIPCHK(c, rt::ctx_forget_stream(c, (hipStream_t)stream), "rt_forget_stream");
+  return RT_OK;
 }
 
 rt_status rt_event_create(void** ev_out) {

@@ -19,8 +19,15 @@
 // communicator's own render streams (render_stream NULL), the gather stream and the three render streams sit
 // on the four hardware queues (GPU_MAX_HW_QUEUES), so no render queues behind a gather.
 //
+// The strips cross xGMI as RGB8 (3 bytes a pixel): the frame's alpha byte is the constant 255, restored by the
+// assembly. rt_render_strips_frames renders up to rt_comm_batch frames (one camera each) in ONE launch per rank.
+//
 // RCCL is bound at run time (dlopen of librccl.so.1): a process that already loaded RCCL (torch)
-// shares that copy, and a context that never creates a communicator never loads it.
+// shares that copy, and a context that never creates a communicator never loads it. A loopback communicator
+// (rt_comm_init_loopback, tests) stands in for N ranks on one GPU without RCCL: every rank's strips are rendered
+// by this process into that rank's block of the slot, and the "gather" is a device copy into rank 0's rank-major
+// layout on the gather stream, issued by the issue thread where ncclGather would be; plan, batching, events, tails
+// and the rank-strided assembly are those of the RCCL path.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -81,12 +88,17 @@ RcclApi& rccl() {
 // frames per gather (rt_comm_set_batch): a slot holds up to this many consecutive frames' strips
 constexpr uint32_t kMaxBatch = 4;
 
+// bytes per pixel of the strips moved by the gather: RGB8 (the alpha byte, always 255, is restored on rank 0)
+constexpr uint32_t kStripBpp = 3;
+
 struct Slot {
-  void* local = nullptr;     // this rank's strips, compact: batch x rows_per_rank x W RGBA8 (frame-major)
-  void* gathered = nullptr;  // rank 0: nranks x (batch x rows_per_rank) x W RGBA8 (rank-major, as ncclGather lays it)
+  void* local = nullptr;     // this rank's strips, compact: batch x rows_per_rank x W RGB8 (frame-major); loopback:
+                             // one such block per emulated rank, rank r's at r x local_bytes
+  void* gathered = nullptr;  // rank 0: nranks x (batch x rows_per_rank) x W RGB8 (rank-major, as ncclGather lays it)
   hipEvent_t rendered = nullptr;  // on the slot's render stream, after its render
   hipEvent_t gathered_ev = nullptr;  // on the gather stream, after its gather
   hipEvent_t moved = nullptr;     // recorded on demand (a slot moved to another stream)
+  hipEvent_t fin[kMaxBatch] = {};  // on the slot's render stream after frame b's tail, for a frame issued on another
   hipStream_t last = nullptr;     // the stream of the slot's last step (caller thread)
   bool used = false;
   // the stream and frames of the slot's last assemblies, an event recorded on demand (caller thread)
@@ -110,18 +122,21 @@ hipEvent_t pipeline_event() {
 }  // namespace
 
 struct Job {
-  uint32_t slot;
-  uint32_t nframes;                // frames in the slot (their strips are gathered by one ncclGather)
-  void* frame_out[kMaxBatch];      // rank 0's output frame of each
-  hipStream_t rs;  // the slot's render stream: its assembly runs there
-  uint32_t W, H, strip, rows_per_rank;
-  uint64_t seq;
+  uint32_t slot = 0;
+  uint32_t nframes = 0;              // frames in the slot (their strips are gathered by one ncclGather)
+  void* frame_out[kMaxBatch] = {};   // rank 0's output frame of each
+  hipStream_t fs[kMaxBatch] = {};    // the render stream a frame was issued on when it is not the slot's (or null):
+                                     // its render waited for that stream, its tail is returned to it by an event
+  hipStream_t rs = nullptr;          // the slot's render stream: its assembly runs there
+  uint32_t W = 0, H = 0, strip = 0, rows_per_rank = 0;
+  uint64_t seq = 0;
 };
 
 struct rt_comm {
   rt_ctx_t ctx = nullptr;
   int device = 0;
   uint32_t nranks = 1, rank = 0;
+  bool loopback = false;  // rt_comm_init_loopback: every rank emulated by this process, no RCCL
   ncclComm_t comm = nullptr;
   hipStream_t stream = nullptr;  // the gathers
   // the communicator's own render streams (render_stream NULL: slot k renders on rstreams[k]), created right
@@ -133,8 +148,11 @@ struct rt_comm {
   std::string err;
   // frame geometry of the slots (re-planned when it changes)
   uint32_t W = 0, H = 0, strip = 0, rows_per_rank = 0;
-  std::vector<uint32_t> rows;  // this rank's global rows, output order
+  std::vector<uint32_t> rows;  // this rank's global rows, output order (loopback: every rank's in turn)
   uint32_t* d_rows = nullptr;  // ... on the device (uploaded once per plan)
+  std::vector<uint32_t> lb_first, lb_count;  // loopback: rank r's rows are rows[lb_first[r] ..][0 .. lb_count[r])
+  size_t local_bytes = 0;      // one rank's block of a slot: batch x rows_per_rank x W x kStripBpp
+  hipEvent_t xev = nullptr;    // a frame issued on another stream than its slot's: the slot's stream waits for it
   // RT_COMM_TIMING=1 (diagnostics): host time per part of rt_render_strips, printed by rt_comm_destroy
   bool timing = false;
   double t_parts[6] = {0, 0, 0, 0, 0, 0};
@@ -184,6 +202,8 @@ void release_slots(rt_comm* c) {
     if (s.gathered) (void)hipFree(s.gathered);
     for (hipEvent_t e : {s.rendered, s.gathered_ev, s.moved, s.asm_order})
       if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : s.fin)
+      if (e) (void)hipEventDestroy(e);
     s = Slot();
   }
 }
@@ -214,25 +234,39 @@ rt_status plan(rt_comm* c, uint32_t W, uint32_t H, uint32_t strip) {
   if (st != RT_OK) return st;
   release_slots(c);
   c->W = c->H = c->strip = 0;
-  const uint32_t n = rt_strip_rows(H, c->nranks, c->rank, strip, nullptr, 0);
-  c->rows.assign(n, 0u);
-  if (n) rt_strip_rows(H, c->nranks, c->rank, strip, c->rows.data(), n);
+  c->rows.clear();
+  c->lb_first.clear();
+  c->lb_count.clear();
+  // the ranks this process renders: its own, or (loopback) all of them
+  const uint32_t r0 = c->loopback ? 0 : c->rank, r1 = c->loopback ? c->nranks : c->rank + 1;
+  for (uint32_t r = r0; r < r1; ++r) {
+    const uint32_t n = rt_strip_rows(H, c->nranks, r, strip, nullptr, 0);
+    c->lb_first.push_back((uint32_t)c->rows.size());
+    c->lb_count.push_back(n);
+    c->rows.resize(c->rows.size() + n);
+    if (n) rt_strip_rows(H, c->nranks, r, strip, c->rows.data() + c->lb_first.back(), n);
+  }
+  const size_t n = c->rows.size();
   if (n) {
-    if (hipMalloc(&c->d_rows, (size_t)n * 4) != hipSuccess) return cfail(c, RT_E_OOM, "rt_render_strips: hipMalloc(rows)");
-    if (hipMemcpy(c->d_rows, c->rows.data(), (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess)
+    if (hipMalloc(&c->d_rows, n * 4) != hipSuccess) return cfail(c, RT_E_OOM, "rt_render_strips: hipMalloc(rows)");
+    if (hipMemcpy(c->d_rows, c->rows.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess)
       return cfail(c, RT_E_HIP, "rt_render_strips: upload rows");
   }
   const uint32_t nstrips = (H + strip - 1) / strip;
   c->rows_per_rank = ((nstrips + c->nranks - 1) / c->nranks) * strip;
-  const size_t local_bytes = (size_t)c->rows_per_rank * W * 4 * c->batch;
+  c->local_bytes = (size_t)c->rows_per_rank * W * kStripBpp * c->batch;
+  const size_t blocks = c->loopback ? c->nranks : 1;
   for (uint32_t k = 0; k < c->nslots; ++k) {
     Slot& s = c->slots[k];
-    if (hipMalloc(&s.local, local_bytes) != hipSuccess) return cfail(c, RT_E_OOM, "rt_render_strips: hipMalloc(local)");
-    if (c->rank == 0 && hipMalloc(&s.gathered, local_bytes * c->nranks) != hipSuccess)
+    if (hipMalloc(&s.local, c->local_bytes * blocks) != hipSuccess)
+      return cfail(c, RT_E_OOM, "rt_render_strips: hipMalloc(local)");
+    if (c->rank == 0 && hipMalloc(&s.gathered, c->local_bytes * c->nranks) != hipSuccess)
       return cfail(c, RT_E_OOM, "rt_render_strips: hipMalloc(gathered)");
     if (!(s.rendered = pipeline_event()) || !(s.gathered_ev = pipeline_event()) || !(s.moved = pipeline_event()) ||
         !(s.asm_order = pipeline_event()))
       return cfail(c, RT_E_HIP, "rt_render_strips: events");
+    for (hipEvent_t& e : s.fin)
+      if (!(e = pipeline_event())) return cfail(c, RT_E_HIP, "rt_render_strips: events");
   }
   c->W = W;
   c->H = H;
@@ -272,11 +306,22 @@ void issue_loop(rt_comm* c) {
     }
     if (c->timing) t1 = clk::now();
     if (st == RT_OK) {
-      const size_t count = (size_t)j.nframes * j.rows_per_rank * j.W * 4;  // every frame of the slot, one call
-      ncclResult_t r = rccl().gather(s.local, c->rank == 0 ? s.gathered : nullptr, count, ncclUint8, 0, c->comm, c->stream);
-      if (r != ncclSuccess) {
-        st = RT_E_RCCL;
-        msg = std::string("rt_render_strips: ncclGather: ") + rccl().getErrorString(r);
+      const size_t count = (size_t)j.nframes * j.rows_per_rank * j.W * kStripBpp;  // every frame of the slot, one call
+      if (c->loopback) {
+        // rank r's block (its first `count` bytes) to r x count in rank 0's buffer: ncclGather's layout
+        const hipError_t e = hipMemcpy2DAsync(s.gathered, count, s.local, c->local_bytes, count, c->nranks,
+                                              hipMemcpyDeviceToDevice, c->stream);
+        if (e != hipSuccess) {
+          st = RT_E_HIP;
+          msg = std::string("rt_render_strips: loopback gather: ") + hipGetErrorString(e);
+        }
+      } else {
+        ncclResult_t r =
+            rccl().gather(s.local, c->rank == 0 ? s.gathered : nullptr, count, ncclUint8, 0, c->comm, c->stream);
+        if (r != ncclSuccess) {
+          st = RT_E_RCCL;
+          msg = std::string("rt_render_strips: ncclGather: ") + rccl().getErrorString(r);
+        }
       }
     }
     if (c->timing) t2 = clk::now();
@@ -309,34 +354,46 @@ void wait_issued(rt_comm* c, uint64_t seq) {
   c->cv_done.wait(lk, [c, seq] { return c->done >= seq; });
 }
 
+rt_status worker_status(rt_comm* c);
+
 // caller thread: a step's tail on its render stream, behind its gather (device-side wait): rank 0 assembles the
-// frame there, off the gather stream, and the slot's next render on that stream follows it
+// frame there, off the gather stream, and the slot's next render on that stream follows it. A gather the issue
+// thread failed to enqueue leaves its event stale: the assembly is skipped and the failure returned.
 rt_status issue_tail_job(rt_comm* c, const Job& j) {
   wait_issued(c, j.seq);
+  rt_status st = worker_status(c);
+  if (st != RT_OK) return st;
   Slot& s = c->slots[j.slot];
   if (j.rs != c->stream && hipStreamWaitEvent(j.rs, s.gathered_ev, 0) != hipSuccess)
     return cfail(c, RT_E_HIP, "rt_render_strips: gather -> render stream hand-off");
-  if (c->rank != 0) return RT_OK;
-  // two assemblies into one frame buffer on different streams stay in call order
-  for (Slot& o : c->slots) {
-    if (&o == &s || !o.asm_stream || o.asm_stream == j.rs) continue;
-    bool shared = false;
-    for (uint32_t a = 0; a < o.asm_n; ++a)
-      for (uint32_t b = 0; b < j.nframes; ++b) shared = shared || o.asm_frames[a] == j.frame_out[b];
-    if (!shared) continue;
-    if (hipEventRecord(o.asm_order, o.asm_stream) != hipSuccess || hipStreamWaitEvent(j.rs, o.asm_order, 0) != hipSuccess)
-      return cfail(c, RT_E_HIP, "rt_render_strips: order after an assembly into the same frame");
+  if (c->rank == 0) {
+    // two assemblies into one frame buffer on different streams stay in call order
+    for (Slot& o : c->slots) {
+      if (&o == &s || !o.asm_stream || o.asm_stream == j.rs) continue;
+      bool shared = false;
+      for (uint32_t a = 0; a < o.asm_n; ++a)
+        for (uint32_t b = 0; b < j.nframes; ++b) shared = shared || o.asm_frames[a] == j.frame_out[b];
+      if (!shared) continue;
+      if (hipEventRecord(o.asm_order, o.asm_stream) != hipSuccess || hipStreamWaitEvent(j.rs, o.asm_order, 0) != hipSuccess)
+        return cfail(c, RT_E_HIP, "rt_render_strips: order after an assembly into the same frame");
+    }
+    // rank r's block of the gathered slot holds its strips of every frame in turn: frame b starts b frames into it
+    const size_t frame_bytes = (size_t)j.rows_per_rank * j.W * kStripBpp;
+    for (uint32_t b = 0; b < j.nframes; ++b) {
+      const hipError_t e = rt::launch_assemble_strips(j.W, j.H, c->nranks, j.strip, (const char*)s.gathered + b * frame_bytes,
+                                                      j.frame_out[b], j.rs, j.nframes * j.rows_per_rank, kStripBpp);
+      if (e != hipSuccess) return cfail(c, RT_E_HIP, std::string("rt_render_strips: assembly: ") + hipGetErrorString(e));
+      s.asm_frames[b] = j.frame_out[b];
+    }
+    s.asm_stream = j.rs;
+    s.asm_n = j.nframes;
   }
-  // rank r's block of the gathered slot holds its strips of every frame in turn: frame b starts b frames into it
-  const size_t frame_bytes = (size_t)j.rows_per_rank * j.W * 4;
+  // a frame issued on another stream than its slot's: its tail returns to that stream (rt_api.h)
   for (uint32_t b = 0; b < j.nframes; ++b) {
-    const hipError_t e = rt::launch_assemble_strips(j.W, j.H, c->nranks, j.strip, (const char*)s.gathered + b * frame_bytes,
-                                                    j.frame_out[b], j.rs, j.nframes * j.rows_per_rank);
-    if (e != hipSuccess) return cfail(c, RT_E_HIP, std::string("rt_render_strips: assembly: ") + hipGetErrorString(e));
-    s.asm_frames[b] = j.frame_out[b];
+    if (!j.fs[b]) continue;
+    if (hipEventRecord(s.fin[b], j.rs) != hipSuccess || hipStreamWaitEvent(j.fs[b], s.fin[b], 0) != hipSuccess)
+      return cfail(c, RT_E_HIP, "rt_render_strips: tail -> the frame's render stream");
   }
-  s.asm_stream = j.rs;
-  s.asm_n = j.nframes;
   return RT_OK;
 }
 
@@ -408,30 +465,22 @@ rt_status rt_comm_get_unique_id(void* id_out) {
   return RT_OK;
 }
 
-rt_status rt_comm_init(rt_ctx_t ctx, uint32_t nranks, uint32_t rank, const void* id, rt_comm_t* out) {
-  if (!out) return RT_E_INVALID;
-  *out = nullptr;
-  if (!ctx || !id || nranks == 0 || rank >= nranks) return RT_E_INVALID;
-  RcclApi& api = rccl();
-  if (!api.ok) return RT_E_UNSUPPORTED;
+namespace {
+
+// the communicator's streams, events and issue thread (no collective yet)
+rt_comm* comm_create(rt_ctx_t ctx, uint32_t nranks, uint32_t rank, bool loopback) {
   rt_comm* c = new (std::nothrow) rt_comm();
-  if (!c) return RT_E_OOM;
+  if (!c) return nullptr;
   c->ctx = ctx;
   c->device = rt::ctx_device(ctx);
   c->nranks = nranks;
   c->rank = rank;
+  c->loopback = loopback;
   const char* tm = std::getenv("RT_COMM_TIMING");
   c->timing = tm && tm[0] == '1';
   // normal priority: a high-priority stream gets a hardware queue of its own (normal streams share
   // GPU_MAX_HW_QUEUES queues round robin, so a render stream can land on the gathers' queue), but its RCCL and
   // assembly kernels ran 3.5x / 4x slower there (tools/trace_share.py): not taken
-  auto destroy_streams = [c]() {
-    for (hipStream_t& r : c->rstreams)
-      if (r) (void)hipStreamDestroy(r);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
-    for (hipEvent_t& j : c->join)
-      if (j) (void)hipEventDestroy(j);
-  };
   bool ok = hipSetDevice(c->device) == hipSuccess &&
             hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
   // one render stream (and pipeline slot) per hardware queue beside the gather stream's: GPU_MAX_HW_QUEUES is
@@ -444,17 +493,54 @@ rt_status rt_comm_init(rt_ctx_t ctx, uint32_t nranks, uint32_t rank, const void*
   for (uint32_t k = 0; k < c->nslots; ++k)
     ok = ok && hipStreamCreateWithFlags(&c->rstreams[k], hipStreamNonBlocking) == hipSuccess;
   for (uint32_t k = 0; k < c->nslots; ++k) ok = ok && (c->join[k] = pipeline_event()) != nullptr;
+  ok = ok && (c->xev = pipeline_event()) != nullptr;
   if (!ok) {
-    destroy_streams();
+    for (hipStream_t& r : c->rstreams)
+      if (r) (void)hipStreamDestroy(r);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    for (hipEvent_t& j : c->join)
+      if (j) (void)hipEventDestroy(j);
+    if (c->xev) (void)hipEventDestroy(c->xev);
     delete c;
-    return RT_E_HIP;
+    return nullptr;
   }
+  return c;
+}
+
+void comm_free(rt_comm* c) {
+  for (hipStream_t r : c->rstreams) {
+    if (!r) continue;
+    (void)hipStreamSynchronize(r);
+    (void)rt::ctx_forget_stream(c->ctx, r);  // the context must not record on it at its next TLAS update
+    (void)hipStreamDestroy(r);
+  }
+  if (c->stream) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamDestroy(c->stream);
+  }
+  release_slots(c);
+  for (hipEvent_t j : c->join)
+    if (j) (void)hipEventDestroy(j);
+  if (c->xev) (void)hipEventDestroy(c->xev);
+  delete c;
+}
+
+}  // namespace
+
+rt_status rt_comm_init(rt_ctx_t ctx, uint32_t nranks, uint32_t rank, const void* id, rt_comm_t* out) {
+  if (!out) return RT_E_INVALID;
+  *out = nullptr;
+  if (!ctx || !id || nranks == 0 || rank >= nranks) return RT_E_INVALID;
+  RcclApi& api = rccl();
+  if (!api.ok) return RT_E_UNSUPPORTED;
+  rt_comm* c = comm_create(ctx, nranks, rank, false);
+  if (!c) return RT_E_HIP;
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof(uid));
   // collective: returns when every rank has joined
   if (api.commInitRank(&c->comm, (int)nranks, uid, (int)rank) != ncclSuccess) {
-    destroy_streams();
-    delete c;
+    c->comm = nullptr;
+    comm_free(c);
     return RT_E_RCCL;
   }
   c->worker = std::thread(issue_loop, c);
@@ -462,8 +548,22 @@ rt_status rt_comm_init(rt_ctx_t ctx, uint32_t nranks, uint32_t rank, const void*
   return RT_OK;
 }
 
+rt_status rt_comm_init_loopback(rt_ctx_t ctx, uint32_t nranks, rt_comm_t* out) {
+  if (!out) return RT_E_INVALID;
+  *out = nullptr;
+  if (!ctx || nranks == 0 || nranks > 64) return RT_E_INVALID;
+  rt_comm* c = comm_create(ctx, nranks, 0, true);
+  if (!c) return RT_E_HIP;
+  c->worker = std::thread(issue_loop, c);
+  *out = c;
+  return RT_OK;
+}
+
 rt_status rt_comm_destroy(rt_comm_t c) {
   if (!c) return RT_E_INVALID;
+  (void)hipSetDevice(c->device);
+  // every step first, a partly filled slot included: its gather goes to the issue thread, which must still run
+  const rt_status st = drain(c);
   {
     std::lock_guard<std::mutex> lk(c->mu);
     c->stop = true;
@@ -471,7 +571,6 @@ rt_status rt_comm_destroy(rt_comm_t c) {
   c->cv_job.notify_all();
   if (c->worker.joinable()) c->worker.join();  // the issue thread drains its queue first
   (void)hipSetDevice(c->device);
-  (void)drain(c);
   if (c->timing && c->t_calls)
     std::fprintf(stderr, "rt_comm timing, caller thread (us per rt_render_strips over %llu calls): plan+checks %.2f, "
                  "render %.2f, record+hand-over %.2f, wait for the slot's last step %.2f, move to another stream %.2f, "
@@ -482,17 +581,8 @@ rt_status rt_comm_destroy(rt_comm_t c) {
     std::fprintf(stderr, "rt_comm timing, issue thread (us per step): hand-off %.2f, ncclGather %.2f, gather event "
                  "%.2f\n", c->w_parts[0] / c->t_calls, c->w_parts[1] / c->t_calls, c->w_parts[2] / c->t_calls);
   if (c->comm) (void)rccl().commDestroy(c->comm);
-  release_slots(c);
-  for (hipStream_t r : c->rstreams) {
-    if (!r) continue;
-    (void)hipStreamSynchronize(r);
-    (void)hipStreamDestroy(r);
-  }
-  (void)hipStreamDestroy(c->stream);
-  for (hipEvent_t j : c->join)
-    if (j) (void)hipEventDestroy(j);
-  delete c;
-  return RT_OK;
+  comm_free(c);
+  return st;
 }
 
 const char* rt_comm_last_error(rt_comm_t c) { return c ? c->err.c_str() : "null communicator"; }
@@ -531,11 +621,17 @@ rt_status rt_comm_synchronize(rt_comm_t c) {
   return worker_status(c);
 }
 
-rt_status rt_render_strips(rt_comm_t c, uint32_t W, uint32_t H, uint32_t strip_rows, void* frame_out,
-                           void* render_stream) {
+rt_status rt_render_strips_frames(rt_comm_t c, uint32_t W, uint32_t H, uint32_t strip_rows, uint32_t nframes,
+                                  const float* cameras, void* const* frames_out, void* render_stream) {
   if (!c) return RT_E_INVALID;
   if (W == 0 || H == 0 || strip_rows == 0) return cfail(c, RT_E_INVALID, "rt_render_strips: bad size");
-  if (c->rank == 0 && !frame_out) return cfail(c, RT_E_INVALID, "rt_render_strips: rank 0 needs frame_out");
+  if (nframes == 0 || nframes > c->batch || nframes > (uint32_t)rt::kMaxLaunchFrames)
+    return cfail(c, RT_E_INVALID, "rt_render_strips_frames: 1 .. rt_comm_batch frames per call");
+  if (c->rank == 0) {
+    bool ok = frames_out != nullptr;
+    for (uint32_t b = 0; ok && b < nframes; ++b) ok = frames_out[b] != nullptr;
+    if (!ok) return cfail(c, RT_E_INVALID, "rt_render_strips: rank 0 needs frame_out");
+  }
   rt_status st = worker_status(c);
   if (st != RT_OK) return st;
   using clk = std::chrono::steady_clock;
@@ -548,13 +644,16 @@ rt_status rt_render_strips(rt_comm_t c, uint32_t W, uint32_t H, uint32_t strip_r
     t0 = t1;
   };
   (void)hipSetDevice(c->device);
-  if (c->fill && (c->W != W || c->H != H || c->strip != strip_rows)) {
-    if ((st = finish_slot(c)) != RT_OK) return st;  // a new frame size: the slot being filled goes as it is
+  // a new frame size, or frames that do not fit the slot being filled (one launch renders them: one slot): the
+  // slot goes as it is
+  if (c->fill && (c->W != W || c->H != H || c->strip != strip_rows || c->fill + nframes > c->batch)) {
+    if ((st = finish_slot(c)) != RT_OK) return st;
   }
   if ((st = plan(c, W, H, strip_rows)) != RT_OK) return st;
   // every frame is validated (the scene may have changed since the slot's first frame)
   if (!c->rows.empty() && (st = rt::check_dispatch(c->ctx, W, H, c->slots[0].local)) != RT_OK)
     return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));
+  hipStream_t fs = nullptr;  // the caller's stream when it is not the slot's
   if (c->fill == 0) {  // a new slot: its first frame picks the render stream every frame of the slot uses
     const uint32_t si = (uint32_t)(c->next % c->nslots);
     hipStream_t rs = render_stream ? (hipStream_t)render_stream : c->rstreams[si];
@@ -573,19 +672,40 @@ rt_status rt_render_strips(rt_comm_t c, uint32_t W, uint32_t H, uint32_t strip_r
         return cfail(c, RT_E_HIP, "rt_render_strips: order after the slot's last step");
       lap(4);
     }
-    c->cur = Job{si, 0, {}, rs, W, H, strip_rows, c->rows_per_rank, 0};
+    c->cur = Job{};
+    c->cur.slot = si;
+    c->cur.rs = rs;
+    c->cur.W = W;
+    c->cur.H = H;
+    c->cur.strip = strip_rows;
+    c->cur.rows_per_rank = c->rows_per_rank;
   } else {
     lap(0);
+    // a later frame of the slot issued on another stream: the slot's stream waits for the work the caller
+    // queued there first (the frame's inputs); the tail comes back to it by an event (issue_tail_job)
+    if (render_stream && (hipStream_t)render_stream != c->cur.rs) {
+      fs = (hipStream_t)render_stream;
+      if (hipEventRecord(c->xev, fs) != hipSuccess || hipStreamWaitEvent(c->cur.rs, c->xev, 0) != hipSuccess)
+        return cfail(c, RT_E_HIP, "rt_render_strips: order after the frame's render stream");
+    }
   }
   Slot& s = c->slots[c->cur.slot];
-  if (!c->rows.empty()) {
-    // frame b of the slot: its strips b frames into the slot's buffer, on the slot's render stream
-    char* dst = (char*)s.local + (size_t)c->fill * c->rows_per_rank * W * 4;
-    st = rt::dispatch_frame(c->ctx, W, H, c->d_rows, (uint32_t)c->rows.size(), dst, nullptr, c->cur.rs);
+  // frames fill..fill+nframes-1 of the slot, one launch per rendered rank: frame b's strips b frames into the
+  // rank's block, on the slot's render stream
+  const uint64_t frame_bytes = (uint64_t)c->rows_per_rank * W * kStripBpp;
+  for (size_t r = 0; r < c->lb_count.size(); ++r) {
+    if (!c->lb_count[r]) continue;  // a rank with no rows (H < nranks x strip_rows) renders nothing
+    char* dst = (char*)s.local + r * c->local_bytes + (size_t)c->fill * frame_bytes;
+    st = rt::dispatch_frame(c->ctx, W, H, c->d_rows + c->lb_first[r], c->lb_count[r], dst, nullptr, c->cur.rs,
+                            kStripBpp, nframes, cameras, frame_bytes);
     if (st != RT_OK) return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));
   }
   lap(1);
-  c->cur.frame_out[c->fill++] = frame_out;
+  for (uint32_t b = 0; b < nframes; ++b) {
+    c->cur.frame_out[c->fill] = frames_out ? frames_out[b] : nullptr;
+    c->cur.fs[c->fill] = fs;
+    ++c->fill;
+  }
   if (c->fill == c->batch && (st = finish_slot(c)) != RT_OK) return st;
   lap(2);
   // the tails whose gathers the issue thread has enqueued by now (no waiting)
@@ -594,6 +714,11 @@ rt_status rt_render_strips(rt_comm_t c, uint32_t W, uint32_t H, uint32_t strip_r
   if (st != RT_OK) return st;
   ++c->t_calls;
   return RT_OK;
+}
+
+rt_status rt_render_strips(rt_comm_t c, uint32_t W, uint32_t H, uint32_t strip_rows, void* frame_out,
+                           void* render_stream) {
+  return rt_render_strips_frames(c, W, H, strip_rows, 1, nullptr, &frame_out, render_stream);
 }
 
 rt_status rt_comm_set_batch(rt_comm_t c, uint32_t frames_per_gather) {

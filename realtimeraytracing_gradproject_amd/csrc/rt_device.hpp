@@ -125,9 +125,22 @@ struct MaterialRec {
   float roughness, metallic, reflectivity;
 };
 
+// Frames one launch renders (rt_render_strips_frames: a batch of a tiled-frame loop's frames, one camera each,
+// the frame index = blockIdx.z)
+constexpr int kMaxLaunchFrames = 4;
+
+// What RayGen reads of one frame's camera buffer (RayGen.hlsl:33-38): viewInverse, projectionInverse (XMMATRIX
+// memory order, cb[32..63] of UpdateCameraBuffer) and the origin mul(viewInverse, (0, 0, 0, 1)), evaluated once
+// on the host with the device's own arithmetic (a uniform value the kernel would otherwise compute per lane).
+struct FrameCam {
+  float view_inv[16];
+  float proj_inv[16];
+  float origin[4];
+};
+
 // Everything a frame needs besides the scene buffers; passed by value as a kernel argument.
 struct FrameParams {
-  float cb[64];  // view, proj, viewInv, projInv in XMMATRIX memory order
+  float cb[64];  // view, proj, viewInv, projInv in XMMATRIX memory order (the context's camera)
   LightRec lights[kMaxLights];
   MaterialRec material;
   uint32_t nlights;
@@ -135,12 +148,17 @@ struct FrameParams {
   uint32_t spp_side;  // k for k x k stratified samples
   uint32_t width, height;
   uint32_t nrows;
-  // frame constants the host evaluates once with the device's own arithmetic (uniform values the
-  // kernel would otherwise compute per lane into VGPRs): the RayGen origin
-  // mul(viewInverse, (0, 0, 0, 1)) and the dimensions as floats
-  float cam_origin[4];
+  // the dimensions as floats (frame constants evaluated once on the host)
   float fwidth, fheight;
   uint32_t tile_rows;  // packet schedule, one-sample frames: rows of a wave's 8-wide tile (8 or 4)
+  // output format: 4 = RGBA8 (R8G8B8A8_UNORM, D3D12HelloTriangle.cpp:971), 3 = RGB8 (the tiled-frame loop's
+  // strips: alpha is the constant 255, restored by the assembly, so a quarter fewer bytes cross xGMI)
+  uint32_t out_bpp;
+  // frames of the launch (grid z): frame z reads cam[z] and writes its nrows x width pixels frame_bytes * z
+  // bytes into the output (the float output, when given, holds frame 0 only)
+  uint32_t nframes;
+  uint32_t frame_bytes;
+  FrameCam cam[kMaxLaunchFrames];
 };
 
 // The trace kernels read one node pool and one triangle pool per scene: [TLAS | BLAS 0 | BLAS 1 ..]

@@ -14,8 +14,15 @@ void* ctx_stream(rt_ctx* c);
 // rt_dispatch_rays' argument / scene checks and its launch with a device row list (rt_render_strips keeps its
 // rank's rows on the device and skips the host list's upload ring)
 rt_status check_dispatch(rt_ctx* c, uint32_t W, uint32_t H, const void* rgba8);
+// nframes (1 .. kMaxLaunchFrames) frames in one launch, frame z with camera buffer cams[64 z ..] (null: the
+// context's camera) into rgba8 + z * frame_stride bytes (0: nrows * W * out_bpp); out_bpp 4 = RGBA8, 3 = RGB8
+// (the strips of rt_comm)
 rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_rows, uint32_t nrows, void* rgba8,
-                         float* rgba32f, hipStream_t s);
+                         float* rgba32f, hipStream_t s, uint32_t out_bpp, uint32_t nframes, const float* cams,
+                         uint64_t frame_stride);
+// A stream that launched work on the context is going away (rt_forget_stream): the TLAS version it read gets
+// that stream's completion event now, so a later rt_tlas_build never records on the destroyed handle.
+hipError_t ctx_forget_stream(rt_ctx* c, hipStream_t s);
 
 // --- LBVH build (rt_lbvh.hip) ---------------------------------------------------------------
 
@@ -76,8 +83,10 @@ hipError_t launch_trace_rays(const SceneView& scene, const float* rays, uint32_t
 
 // rank_stride_rows: rows from one rank's block of `gathered` to the next (0: rows_per_rank, one frame per block;
 // a batched gather holds several frames per rank block and passes their total)
+// in_bpp: bytes per pixel of the gathered strips (4 RGBA8, 3 RGB8: the alpha byte restored as 255); out is RGBA8
 hipError_t launch_assemble_strips(uint32_t W, uint32_t H, uint32_t nranks, uint32_t strip_rows,
-                                  const void* gathered, void* out, hipStream_t stream, uint32_t rank_stride_rows = 0);
+                                  const void* gathered, void* out, hipStream_t stream, uint32_t rank_stride_rows = 0,
+                                  uint32_t in_bpp = 4);
 
 // --- Raster fallback (rt_raster.hip) -------------------------------------------------------
 

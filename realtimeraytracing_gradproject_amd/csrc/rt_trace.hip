@@ -1223,16 +1223,16 @@ __device__ V3 shade_ref(const SceneView& sc, const FrameParams& fp, uint32_t py,
 
 // One camera sample -> color (RayGen.hlsl:28-43 and the hit/miss programs).
 template <int MODE, bool STATS>
-__device__ V3 shade_sample(const SceneView& sc, const FrameParams& fp, uint32_t px, uint32_t py,
+__device__ V3 shade_sample(const SceneView& sc, const FrameParams& fp, const FrameCam& cam, uint32_t px, uint32_t py,
                            float ox, float oy, const LaneStack& stk, Counters& cnt) {
   const float dx = (((float)px + ox) / fp.fwidth) * 2.0f - 1.0f;
   const float dy = (((float)py + oy) / fp.fheight) * 2.0f - 1.0f;
   float dc[4], dw[4];
   const float ndc[4] = {dx, -dy, 1.0f, 1.0f};
-  hlsl_mul4(fp.cb + 48, ndc, dc);
+  hlsl_mul4(cam.proj_inv, ndc, dc);
   const float dcam[4] = {dc[0], dc[1], dc[2], 0.0f};
-  hlsl_mul4(fp.cb + 32, dcam, dw);
-  const V3 O = v3(fp.cam_origin[0], fp.cam_origin[1], fp.cam_origin[2]);  // mul(viewInverse, (0,0,0,1))
+  hlsl_mul4(cam.view_inv, dcam, dw);
+  const V3 O = v3(cam.origin[0], cam.origin[1], cam.origin[2]);  // mul(viewInverse, (0,0,0,1))
   const V3 D = normalize(v3(dw[0], dw[1], dw[2]));  // CastDefaultRay
   HitRec hit;
   if (STATS) ++cnt.primary;
@@ -1344,7 +1344,7 @@ __device__ bool shadow_compact(const SceneView& sc, V3 P, V3 d, bool need, uint3
 #define RT_PHASE_TIMING 0  // 1: sampled waves printf s_memtime per phase (diagnostics only)
 #endif
 template <int MODE, bool STATS, int R>
-__device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, const uint32_t* px,
+__device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, const FrameCam& cam, const uint32_t* px,
                                     const uint32_t* py, float ox, float oy, const bool* inimg, V3* color,
                                     Counters& cnt) {
 #if RT_PHASE_TIMING
@@ -1363,10 +1363,10 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
     const float dy = (((float)py[r] + oy) / fp.fheight) * 2.0f - 1.0f;
     float dc[4], dw[4];
     const float ndc[4] = {dx, -dy, 1.0f, 1.0f};
-    hlsl_mul4(fp.cb + 48, ndc, dc);
+    hlsl_mul4(cam.proj_inv, ndc, dc);
     const float dcam[4] = {dc[0], dc[1], dc[2], 0.0f};
-    hlsl_mul4(fp.cb + 32, dcam, dw);
-    O[r] = v3(fp.cam_origin[0], fp.cam_origin[1], fp.cam_origin[2]);  // mul(viewInverse, (0,0,0,1))
+    hlsl_mul4(cam.view_inv, dcam, dw);
+    O[r] = v3(cam.origin[0], cam.origin[1], cam.origin[2]);  // mul(viewInverse, (0,0,0,1))
     D[r] = normalize(v3(dw[0], dw[1], dw[2]));  // CastDefaultRay
     if (STATS && inimg[r]) ++cnt.primary;
   }
@@ -1524,6 +1524,22 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
 #endif
 }
 
+// The pixel store (RayGen.hlsl:42, gOutput = float4(color, 1) into the R8G8B8A8_UNORM UAV): frame blockIdx.z of
+// the launch, RGBA8 or, for the tiled-frame loop's strips, RGB8 (the alpha byte is the constant 255: the assembly
+// restores it, so it never crosses xGMI). out_bpp is uniform: one branch per wave.
+__device__ __forceinline__ void store_pixel(const FrameParams& fp, uint32_t* out, uint32_t o, V3 a) {
+  const uint32_t r = unorm8(a.x), g = unorm8(a.y), b = unorm8(a.z);
+  char* base = (char*)out + (size_t)blockIdx.z * fp.frame_bytes;
+  if (fp.out_bpp == 3u) {
+    uint8_t* p = (uint8_t*)base + (size_t)o * 3u;
+    p[0] = (uint8_t)r;
+    p[1] = (uint8_t)g;
+    p[2] = (uint8_t)b;
+  } else {
+    ((uint32_t*)base)[o] = r | (g << 8) | (b << 16) | (255u << 24);
+  }
+}
+
 // WAVE_FETCH: the fetch counters are wave-uniform (packet schedule) and count once per wave.
 template <bool WAVE_FETCH>
 __device__ __forceinline__ void flush_stats(const Counters& c, unsigned long long* stats) {
@@ -1557,21 +1573,22 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void k_trace_frame(SceneView 
   Counters cnt;
   if (px < fp.width && orow < fp.nrows) {
     const uint32_t py = rows ? rows[orow] : orow;
-    const LaneStack stk = lane_stack(sc, s_stack, (blockIdx.y * gridDim.x + blockIdx.x) * kBlock + threadIdx.x);
+    const LaneStack stk =
+        lane_stack(sc, s_stack, ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * kBlock + threadIdx.x);
     const uint32_t k = fp.spp_side;
     V3 acc = v3(0.0f, 0.0f, 0.0f);
     for (uint32_t sy = 0; sy < k; ++sy)
       for (uint32_t sx = 0; sx < k; ++sx) {
         const float ox = ((float)sx + 0.5f) / (float)k;
         const float oy = ((float)sy + 0.5f) / (float)k;
-        acc = add(acc, shade_sample<MODE, STATS>(sc, fp, px, py, ox, oy, stk, cnt));
+        acc = add(acc, shade_sample<MODE, STATS>(sc, fp, fp.cam[blockIdx.z], px, py, ox, oy, stk, cnt));
       }
     if (k > 1) {
       const float ns = (float)(k * k);
       acc = v3(acc.x / ns, acc.y / ns, acc.z / ns);
     }
     const size_t o = (size_t)orow * fp.width + px;
-    rgba8[o] = unorm8(acc.x) | (unorm8(acc.y) << 8) | (unorm8(acc.z) << 16) | (255u << 24);
+    store_pixel(fp, rgba8, (uint32_t)o, acc);
     if (rgba32f) rgba32f[o] = make_float4(acc.x, acc.y, acc.z, 1.0f);
   }
   if (STATS) flush_stats<false>(cnt, stats);
@@ -1671,12 +1688,12 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
   Counters cnt;
   const uint32_t k = KS == 1 ? 1u : (KS > 1 ? (uint32_t)KS : fp.spp_side);
   if (KS == 1) {
-    shade_sample_packet<MODE, STATS, R>(sc, fp, px, py, 0.5f, 0.5f, inimg, acc, cnt);  // (0 + 0.5) / 1
+    shade_sample_packet<MODE, STATS, R>(sc, fp, fp.cam[blockIdx.z], px, py, 0.5f, 0.5f, inimg, acc, cnt);  // (0 + 0.5) / 1
   } else if (KS > 1) {
     // this lane's sample (sx, sy) of the k x k grid, the sample loop's offsets
     const float ox = ((float)(sample % KS) + 0.5f) / (float)KS;
     const float oy = ((float)(sample / KS) + 0.5f) / (float)KS;
-    shade_sample_packet<MODE, STATS, R>(sc, fp, px, py, ox, oy, inimg, col, cnt);
+    shade_sample_packet<MODE, STATS, R>(sc, fp, fp.cam[blockIdx.z], px, py, ox, oy, inimg, col, cnt);
     // sum in sample order: ((0 + c0) + c1) + ... exactly as the loop adds them (0 + c0 == c0).
     // The lane id is re-read here (v_mbcnt) rather than kept live across the traces.
     uint32_t lid;
@@ -1698,7 +1715,7 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
       for (uint32_t sx = 0; sx < k; ++sx) {
         const float ox = ((float)sx + 0.5f) / (float)k;
         const float oy = ((float)sy + 0.5f) / (float)k;
-        shade_sample_packet<MODE, STATS, R>(sc, fp, px, py, ox, oy, inimg, col, cnt);
+        shade_sample_packet<MODE, STATS, R>(sc, fp, fp.cam[blockIdx.z], px, py, ox, oy, inimg, col, cnt);
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = add(acc[r], col[r]);
       }
@@ -1712,7 +1729,7 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
     }
     if (out[r] != 0xffffffffu) {
       const uint32_t o = out[r];
-      rgba8[o] = unorm8(a.x) | (unorm8(a.y) << 8) | (unorm8(a.z) << 16) | (255u << 24);
+      store_pixel(fp, rgba8, o, a);
       if (rgba32f && !RT_WAVE_TIMES) rgba32f[o] = make_float4(a.x, a.y, a.z, 1.0f);
     }
   }
@@ -1753,9 +1770,11 @@ __global__ __launch_bounds__(kBlock) void k_trace_rays(SceneView sc, const float
   if (STATS) flush_stats<false>(cnt, stats);
 }
 
+// Un-interleaves the gathered strips (rank-major blocks; rank k holds strips s % nranks == k) into the RGBA8 frame.
+// in_bpp 3: the strips are RGB8 and the constant alpha 255 is restored here (RayGen.hlsl:42 writes float4(c, 1)).
 __global__ void k_assemble(uint32_t W, uint32_t H, uint32_t nranks, uint32_t strip_rows,
-                           const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                           uint32_t rows_per_rank) {
+                           const uint8_t* __restrict__ in, uint32_t* __restrict__ out,
+                           uint32_t rows_per_rank, uint32_t in_bpp) {
   // one thread per output pixel (4 B), coalesced along x
   const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t y = blockIdx.y;
@@ -1763,7 +1782,15 @@ __global__ void k_assemble(uint32_t W, uint32_t H, uint32_t nranks, uint32_t str
   const uint32_t s = y / strip_rows, within = y % strip_rows;
   const uint32_t rank = s % nranks, local_strip = s / nranks;
   const uint32_t lrow = local_strip * strip_rows + within;
-  out[(size_t)y * W + x] = in[((size_t)rank * rows_per_rank + lrow) * W + x];
+  const size_t src = ((size_t)rank * rows_per_rank + lrow) * W + x;
+  uint32_t v;
+  if (in_bpp == 3u) {
+    const uint8_t* p = in + src * 3u;
+    v = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | (255u << 24);
+  } else {
+    v = ((const uint32_t*)in)[src];
+  }
+  out[(size_t)y * W + x] = v;
 }
 
 // 16 B per thread (W % 4 == 0, 16-B aligned buffers): kAsmRows output rows per workgroup, so the
@@ -1787,10 +1814,32 @@ __global__ __launch_bounds__(256) void k_assemble16(uint32_t W4, uint32_t H, uin
   }
 }
 
+// The same from RGB8 strips: 4 pixels = 12 B (three dwords, 4-B aligned: a strip row is 3 W bytes with W % 4 == 0)
+// in, 16 B out with the alpha bytes set. Dwords a, b, c hold r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3.
+__global__ __launch_bounds__(256) void k_assemble16_rgb(uint32_t W4, uint32_t H, uint32_t nranks, uint32_t strip_rows,
+                                                        const uint32_t* __restrict__ in, uint4* __restrict__ out,
+                                                        uint32_t rows_per_rank) {
+  const uint32_t x = blockIdx.x * 256u + threadIdx.x;
+  if (x >= W4) return;
+  const uint32_t y0 = blockIdx.y * kAsmRows;
+#pragma unroll
+  for (uint32_t i = 0; i < kAsmRows; ++i) {
+    const uint32_t y = y0 + i;
+    if (y >= H) break;
+    const uint32_t s = y / strip_rows, within = y % strip_rows;
+    const uint32_t rank = s % nranks, local_strip = s / nranks;
+    const uint32_t lrow = local_strip * strip_rows + within;
+    const uint32_t* p = in + (((size_t)rank * rows_per_rank + lrow) * W4 + x) * 3u;
+    const uint32_t a = p[0], b = p[1], c = p[2];
+    out[(size_t)y * W4 + x] = make_uint4((a & 0xffffffu) | 0xff000000u, (a >> 24) | ((b & 0xffffu) << 8) | 0xff000000u,
+                                         (b >> 16) | ((c & 0xffu) << 16) | 0xff000000u, (c >> 8) | 0xff000000u);
+  }
+}
+
 template <int MODE, bool STATS>
 hipError_t launch_mode(const SceneView& sc, const FrameParams& fp, const uint32_t* rows, void* rgba8,
                        float* rgba32f, unsigned long long* stats, int schedule, hipStream_t s) {
-  dim3 grid((fp.width + 15) / 16, (fp.nrows + 15) / 16);
+  dim3 grid((fp.width + 15) / 16, (fp.nrows + 15) / 16, fp.nframes);
   if (schedule == RT_SCHED_PACKET && sc.packet_cap < kPacketStack) {
     constexpr int R = RT_PACKET_RAYS;
     // KS: 1 one sample per pixel; 2 / 4 the k x k samples of a pixel in consecutive lanes; 0 the loop
@@ -1799,7 +1848,7 @@ hipError_t launch_mode(const SceneView& sc, const FrameParams& fp, const uint32_
     const uint32_t tp = ms_tile_w(ks);
     const uint32_t tr = (ks <= 1 && fp.tile_rows == 4u) ? 4u : ms_tile_h(ks);  // as the kernel's TR
     const uint32_t tw = tp * (uint32_t)packet_wx(ks), th = tr * R * (uint32_t)packet_wy(ks);
-    dim3 gp((fp.width + tw - 1) / tw, (fp.nrows + th - 1) / th);
+    dim3 gp((fp.width + tw - 1) / tw, (fp.nrows + th - 1) / th, fp.nframes);
 #define RT_LAUNCH_PACKET(KS)                                                                                   \
   hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R, (R == 1 ? KS : 0)>), gp, dim3(packet_block(R == 1 ? KS : 0)), 0, s, sc, fp, \
                      rows, (uint32_t*)rgba8, (float4*)rgba32f, stats)
@@ -1863,20 +1912,27 @@ hipError_t launch_trace_rays(const SceneView& sc, const float* rays, uint32_t n,
 }
 
 hipError_t launch_assemble_strips(uint32_t W, uint32_t H, uint32_t nranks, uint32_t strip_rows,
-                                  const void* gathered, void* out, hipStream_t s, uint32_t rank_stride_rows) {
+                                  const void* gathered, void* out, hipStream_t s, uint32_t rank_stride_rows,
+                                  uint32_t in_bpp) {
   const uint32_t nstrips = (H + strip_rows - 1) / strip_rows;
   const uint32_t strips_per_rank = (nstrips + nranks - 1) / nranks;
   const uint32_t rows_per_rank = rank_stride_rows ? rank_stride_rows : strips_per_rank * strip_rows;  // rank stride
-  if (W % 4 == 0 && ((uintptr_t)gathered | (uintptr_t)out) % 16 == 0) {
+  if (in_bpp != 3u && in_bpp != 4u) return hipErrorInvalidValue;
+  const uintptr_t align = (uintptr_t)gathered % (in_bpp == 4u ? 16u : 4u) | (uintptr_t)out % 16u;
+  if (W % 4 == 0 && align == 0) {
     const uint32_t W4 = W / 4;
     dim3 grid((W4 + 255) / 256, (H + kAsmRows - 1) / kAsmRows);
-    hipLaunchKernelGGL(k_assemble16, grid, dim3(256), 0, s, W4, H, nranks, strip_rows, (const uint4*)gathered,
-                       (uint4*)out, rows_per_rank);
+    if (in_bpp == 4u)
+      hipLaunchKernelGGL(k_assemble16, grid, dim3(256), 0, s, W4, H, nranks, strip_rows, (const uint4*)gathered,
+                         (uint4*)out, rows_per_rank);
+    else
+      hipLaunchKernelGGL(k_assemble16_rgb, grid, dim3(256), 0, s, W4, H, nranks, strip_rows, (const uint32_t*)gathered,
+                         (uint4*)out, rows_per_rank);
     return hipGetLastError();
   }
   dim3 grid((W + 255) / 256, H);
-  hipLaunchKernelGGL(k_assemble, grid, dim3(256), 0, s, W, H, nranks, strip_rows, (const uint32_t*)gathered,
-                     (uint32_t*)out, rows_per_rank);
+  hipLaunchKernelGGL(k_assemble, grid, dim3(256), 0, s, W, H, nranks, strip_rows, (const uint8_t*)gathered,
+                     (uint32_t*)out, rows_per_rank, in_bpp);
   return hipGetLastError();
 }
 

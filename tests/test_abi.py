@@ -34,7 +34,7 @@ def test_python_binding_covers_header():
 
 
 def test_status_strings_and_version():
-    assert rt.lib.rt_api_version() == 3
+    assert rt.lib.rt_api_version() == 4
     assert rt.lib.rt_status_string(rt.RT_E_IO) == b"RT_E_IO"
     assert rt.lib.rt_status_string(rt.RT_OK) == b"RT_OK"
 
@@ -46,6 +46,9 @@ def test_comm_argument_errors_without_gpu():
     assert rt.lib.rt_comm_get_unique_id(None) == rt.RT_E_INVALID
     assert rt.lib.rt_comm_destroy(None) == rt.RT_E_INVALID
     assert rt.lib.rt_render_strips(None, 8, 8, 8, None, None) == rt.RT_E_INVALID
+    assert rt.lib.rt_render_strips_frames(None, 8, 8, 8, 1, None, None, None) == rt.RT_E_INVALID
+    assert rt.lib.rt_comm_init_loopback(None, 2, ctypes.byref(out)) == rt.RT_E_INVALID
+    assert rt.lib.rt_forget_stream(None, None) == rt.RT_E_INVALID
     assert rt.lib.rt_comm_stream(None) is None
     assert rt.lib.rt_comm_pipeline_depth(None) == 0
     assert rt.lib.rt_comm_set_batch(None, 2) == rt.RT_E_INVALID

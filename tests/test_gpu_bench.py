@@ -63,18 +63,23 @@ def test_bench_one_gpu_frames_in_flight(tmp_path, in_flight):
     assert np.array_equal(np.load(img), o8)
 
 
-@pytest.mark.parametrize("config,size,in_flight", [("C2F", "640x368", "0"), ("C4", "256x136", "3")])
-def test_bench_native_strips_world1(tmp_path, config, size, in_flight):
-    """bench.py --mode strips at N = 1: the tiled-frame loop through the C-ABI's rt_render_strips (render ->
+@pytest.mark.parametrize("config,size,in_flight,extra", [("C2F", "640x368", "0", []), ("C4", "256x136", "3", []),
+                                                         ("C2F", "640x371", "0", ["--loopback", "3"]),
+                                                         ("C4", "256x136", "3", ["--loopback", "8",
+                                                                                 "--frames-per-launch", "2"])])
+def test_bench_native_strips_world1(tmp_path, config, size, in_flight, extra):
+    """bench.py --mode strips at N = 1: the tiled-frame loop through the C-ABI's rt_render_strips_frames (render ->
     ncclGather over a world-1 RCCL communicator -> rt_assemble_strips), the path `--gpus N` takes on the 8-GPU
-    node. The assembled frame equals the oracle's and the JSON names the native loop."""
+    node; with --loopback N the library's loopback transport emulates N ranks (the N > 1 layout: batched
+    rank-strided gathers, RGB8 strips, frames per launch). The assembled frame equals the oracle's, the JSON names
+    the native loop and carries the frame latency (enqueue -> assembled on rank 0, gather included)."""
     sys.path.insert(0, ROOT)
     import oracle
     from realtimeraytracing_gradproject_amd import scenes
     img = tmp_path / "frame.npy"
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--mode", "strips", "--config", config, "--size", size,
            "--steps", "6", "--warmup", "2", "--settle-ms", "0", "--extra=", "--no-cpu-baseline",
-           "--save-image", str(img), "--in-flight", in_flight]
+           "--save-image", str(img), "--in-flight", in_flight, "--latency-frames", "3"] + extra
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "MASTER_PORT"):
         env.pop(k, None)
@@ -83,6 +88,10 @@ def test_bench_native_strips_world1(tmp_path, config, size, in_flight):
     out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert out["config"]["strips_loop"].startswith("rt_render_strips")
     assert out["config"]["rccl_world_size"] == 1
+    assert out["config"]["frame_latency_ms"] > 0 and out["config"]["frames_per_gather"] == 4
+    assert out["config"]["frame_ms_one_stream_is_latency"] is False
+    if extra:
+        assert out["config"]["loopback_ranks"] == int(extra[1])
     w, h = (int(v) for v in size.split("x"))
     spec = scenes.config(config).with_size(w, h)
     o8, _, st = oracle.Scene(spec).render_spec(spec, nthreads=8, want_float=False)

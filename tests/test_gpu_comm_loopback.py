@@ -1,0 +1,175 @@
+"""The N > 1 layout of the native multi-GPU frame loop (rt_comm_*, rt_render_strips) on
+one GPU, through the library's loopback transport (rt_comm_init_loopback): this process renders every emulated
+rank's interleaved strips into that rank's block of a pipeline slot, and the "gather" is a device copy into rank 0's
+rank-major buffer issued where ncclGather is. Plan, frame batching (one gather per b frames, frame b at b frames
+into each rank's block, the rank-strided RGB8 -> RGBA8 assembly), events and tails are the RCCL path's. Every
+assembled frame equals the oracle's frame of the reference's DispatchRays W x H (D3D12HelloTriangle.cpp:584-592)
+bit for bit, with a camera change per frame."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import realtimeraytracing_gradproject_amd as rt  # noqa: E402
+from realtimeraytracing_gradproject_amd import scenes  # noqa: E402
+
+import oracle  # noqa: E402
+
+# C2 (the BASELINE frame) and a ragged frame: 1083 rows = 135 full 8-row strips + a 3-row one, which leaves the
+# ranks with different row counts (some a strip short) at N = 2, 3 and 8
+SIZES = [(1920, 1080), (1920, 1083)]
+EYES = [(1.5, 1.5, 1.5), (2.2, 1.4, 1.1), (1.1, 1.9, 2.4), (3.0, 2.0, 0.5)]  # the first is the reference camera
+_ORACLE = {}
+
+
+def _spec(size, k):
+    sp = scenes.config("C2").with_size(*size)
+    sp.camera = (EYES[k], (0.0, 0.0, 0.0), (0.0, 1.0, 0.0))
+    return sp
+
+
+def _oracle_frame(size, k):
+    key = (size, k)
+    if key not in _ORACLE:
+        sp = _spec(size, k)
+        o8, _, _ = oracle.Scene(sp).render_spec(sp, nthreads=16, want_float=False, schedule=1)
+        _ORACLE[key] = o8
+    return _ORACLE[key]
+
+
+def _check(frames, size, cams, what):
+    for k, f in enumerate(frames):
+        got = f.cpu().numpy()
+        want = _oracle_frame(size, cams[k])
+        bad = int((got != want).any(axis=2).sum())
+        assert bad == 0, f"{what}: frame {k} (camera {cams[k]}): {bad} pixels differ"
+
+
+@pytest.mark.parametrize("size", SIZES, ids=["1920x1080", "1920x1083"])
+@pytest.mark.parametrize("nranks", [2, 3, 8])
+def test_loopback_strips_every_batch_equals_oracle(size, nranks):
+    """N ranks x frames per gather 1, 2, 4: 2 x depth + 1 frames (every slot reused, the last batch partly filled
+    and gathered as it is at rt_comm_synchronize), a camera change per frame, each frame into its own buffer, the
+    library's own render streams (frames in flight)."""
+    W, H = size
+    c = rt.Context(0)
+    scenes.upload(c, _spec(size, 0))
+    for batch in (1, 2, 4):
+        comm = rt.Comm.loopback(c, nranks)
+        comm.set_batch(batch)
+        assert comm.batch == batch
+        n = 2 * comm.depth + 1
+        frames = [torch.full((H, W, 4), 7, dtype=torch.uint8, device="cuda") for _ in range(n)]
+        cams = [k % len(EYES) for k in range(n)]
+        for k in range(n):
+            c.set_camera(_spec(size, cams[k]).camera_buffer())
+            comm.render_strips(W, H, frames[k], None)
+        comm.synchronize()
+        _check(frames, size, cams, f"N={nranks} batch={batch}")
+        comm.close()
+    c.close()
+
+
+@pytest.mark.parametrize("nranks", [2, 8])
+def test_loopback_frames_in_one_launch_equal_oracle(nranks):
+    """rt_render_strips_frames: b frames, one camera each, rendered by ONE launch per rank into one slot (grid z =
+    frame), one gather; calls of 4, 3 (a new slot after the 4), 1 and 2 frames at batch 4, on a caller stream."""
+    size = (1920, 1083)
+    W, H = size
+    c = rt.Context(0)
+    scenes.upload(c, _spec(size, 0))
+    comm = rt.Comm.loopback(c, nranks)
+    comm.set_batch(4)
+    stream = torch.cuda.Stream()
+    frames, cams = [], []
+    k = 0
+    for nf in (4, 3, 1, 2, 4):
+        fs = [torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(nf)]
+        cs = [(k + j) % len(EYES) for j in range(nf)]
+        cb = np.concatenate([_spec(size, q).camera_buffer().ravel() for q in cs])
+        comm.render_strips_frames(W, H, fs, cameras=cb, stream=stream.cuda_stream)
+        frames += fs
+        cams += cs
+        k += nf
+    comm.synchronize()
+    _check(frames, size, cams, f"N={nranks} frames-per-launch")
+    with pytest.raises(rt.RtError):  # more frames than a slot holds
+        comm.render_strips_frames(W, H, [frames[0]] * 5)
+    comm.close()
+    c.close()
+
+
+@pytest.mark.parametrize("loop", ["loopback8", "rccl1"])
+def test_close_with_partly_filled_batch_returns(loop):
+    """rt_comm_destroy with a partly filled slot and no rt_comm_synchronize: 2 frames at 3
+    frames per gather, then close(). The destroy drains the slot through the issue thread before stopping it, so it
+    returns (the test runs under pytest's timeout) and both frames are complete and correct."""
+    size = (960, 544)
+    W, H = size
+    c = rt.Context(0)
+    scenes.upload(c, _spec(size, 0))
+    comm = rt.Comm.loopback(c, 8) if loop == "loopback8" else rt.Comm(c, 1, 0, rt.comm_unique_id())
+    comm.set_batch(3)
+    frames = [torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    cams = [1, 2]
+    for k in range(2):
+        c.set_camera(_spec(size, cams[k]).camera_buffer())
+        comm.render_strips(W, H, frames[k], None)
+    comm.close()  # no synchronize
+    torch.cuda.synchronize()
+    _check(frames, size, cams, f"{loop} close()")
+    c.close()
+
+
+def test_later_frames_on_other_streams_are_ordered():
+    """A slot's later frames issued on other streams than its first: each frame's render waits for the
+    work already queued on its own stream, and its tail comes back to that stream. Each frame's stream first fills
+    the frame buffer with a pattern (queued, not synchronised) and the render must come after it; then that stream
+    alone is synchronised and must see its assembled frame."""
+    size = (640, 360)
+    W, H = size
+    c = rt.Context(0)
+    scenes.upload(c, _spec(size, 0))
+    comm = rt.Comm.loopback(c, 3)
+    comm.set_batch(3)
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    frames = [torch.empty((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(3)]
+    cams = [0, 3, 2]
+    for k in range(3):
+        with torch.cuda.stream(streams[k]):
+            torch.cuda._sleep(2_000_000)  # keeps the stream busy, so an unordered render would run first
+            frames[k].fill_(9)
+        c.set_camera(_spec(size, cams[k]).camera_buffer())
+        comm.render_strips(W, H, frames[k], streams[k].cuda_stream)
+    torch.cuda.ExternalStream(comm.stream).synchronize()  # the slot is gathered and its tails issued
+    for k in (2, 1, 0):
+        streams[k].synchronize()
+        _check([frames[k]], size, [cams[k]], f"stream {k}")
+    comm.close()
+    c.close()
+
+
+def test_forget_stream_then_tlas_update():
+    """rt_forget_stream: a stream that launched frames is destroyed; the next rt_tlas_build(update_only) must not
+    record on it. The communicator's own render streams go through the same path at rt_comm_destroy."""
+    spec = scenes.config("C2F").with_size(256, 144)
+    c = rt.Context(0)
+    scenes.upload(c, spec)
+    out = torch.zeros((spec.height, spec.width, 4), dtype=torch.uint8, device="cuda")
+    s = torch.cuda.Stream()
+    c.dispatch(spec.width, spec.height, out, stream=s.cuda_stream)
+    c.forget_stream(s.cuda_stream)
+    comm = rt.Comm.loopback(c, 2)
+    comm.render_strips(spec.width, spec.height, out, None)
+    comm.close()  # its render streams read the TLAS: forgotten before they are destroyed
+    torch.cuda.synchronize()
+    del s
+    inst = [(m, x, iid, hg) for (m, x, iid, hg) in spec.instances]
+    for _ in range(3):
+        c.tlas_build(inst, update_only=True)
+    c.dispatch(spec.width, spec.height, out, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    o8, _, _ = oracle.Scene(spec).render_spec(spec, nthreads=16, want_float=False, schedule=1)
+    assert np.array_equal(out.cpu().numpy(), o8)
+    c.close()
