@@ -190,6 +190,19 @@ rt_status rt_set_schedule(rt_ctx_t ctx, int schedule);
  * frame tiled over many GPUs (C4 over 8 ranks: 0.196 -> 0.135 ms); otherwise it halves throughput. No reference
  * counterpart (DispatchRays schedules rays itself). */
 rt_status rt_set_tile_rows(rt_ctx_t ctx, int rows);
+/* Tile balance of the packet schedule (no reference counterpart: DispatchRays schedules rays itself). A wave walks
+ * the union of its 8 x 8 tile's ray paths, so a frame lasts as long as its slowest tiles (on C4 one tile takes as
+ * long as the rest of the frame). mode 1 (default, adaptive): every wave records its tile's time; when the last
+ * frame of the same shape (size, row list, frames per launch) had tiles far above the mean, a one-workgroup plan
+ * kernel before the launch splits the tiles above max(load bound, 0.35 x the slowest) into 4 or 16 sub-packets and
+ * deals every wave longest first. The image never depends on it. 0: off (the plain grid). 2 / 3 / 4 (tests): every
+ * tile in 4 parts / in 16 parts / by position (tx + 2 ty) % 3 whole, 4, 16 — also under rt_set_stats, so the
+ * counters can be compared with the oracle's emulation of the same parts. */
+rt_status rt_set_tile_balance(rt_ctx_t ctx, int mode);
+/* The last launch shape's tile balance: out[0] plans run, [1] tiles split by the last plan, [2] its work items,
+ * [3] the extra-wave budget, [4] the costliest / [5] the mean tile time (10-ns ticks), [6] the split threshold,
+ * [7] launches of the shape. Host-side read of host-mapped memory (may lag the device by a few launches). */
+rt_status rt_tile_balance_info(rt_ctx_t ctx, uint32_t out[8]);
 /* Enables device counters (rt_stats). Costs time: off for timed runs. */
 rt_status rt_set_stats(rt_ctx_t ctx, int enable);
 

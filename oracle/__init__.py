@@ -46,6 +46,8 @@ _SIGS = [
     ("oracle_export_tlas", _I, [_P, _P]),
     ("oracle_render", _I, [_P, _FP, ctypes.POINTER(oracle_light), _U32, _FP, _I, _I, _U32, _U32, _P, _U32, _P, _P,
                            _I, _P, _I, _I]),
+    ("oracle_render_split", _I, [_P, _FP, ctypes.POINTER(oracle_light), _U32, _FP, _I, _I, _U32, _U32, _P, _U32, _P,
+                                 _P, _I, _P, _I, _I, _I]),
     ("oracle_trace_rays", _I, [_P, _P, _U32, _U32, _P, _P, _I, _P]),
     ("oracle_raster", _I, [_P, _P, _P, _P, _U32, _P, _P, _U32, _U32, _P, _P, _P]),
     ("oracle_pbr", None, [_FP, _FP, _FP, ctypes.POINTER(oracle_light), _U32, _FP, _FP]),
@@ -264,7 +266,9 @@ class Scene:
         return nodes.reshape(-1, 32)
 
     def render(self, cb, lights, material, mode, spp, W, H, rows: Optional[np.ndarray] = None, nthreads=1,
-               brute_force=False, want_float=True, schedule=0):
+               brute_force=False, want_float=True, schedule=0, split=0):
+        """split (packet schedule): the device's forced tile-balance layouts (rt_set_tile_balance(2 + split - 1)):
+        1 every tile in 2 x 2 parts, 2 in 4 x 4, 3 by tile position; each part traced as its own packet."""
         c, cp = _f(cb)
         m, mp = _f(material)
         nrows = H if rows is None else len(rows)
@@ -275,16 +279,16 @@ class Scene:
         if rows is not None:
             r = np.ascontiguousarray(rows, dtype=np.uint32)
             rp = r.ctypes.data_as(_P)
-        st = self._lib.oracle_render(self._h, cp, _lights(lights), len(lights), mp, mode, spp, W, H, rp, nrows,
-                               rgba8.ctypes.data_as(_P), rgba32.ctypes.data_as(_P) if want_float else None,
-                               nthreads, stats.ctypes.data_as(_P), 1 if brute_force else 0, schedule)
+        st = self._lib.oracle_render_split(self._h, cp, _lights(lights), len(lights), mp, mode, spp, W, H, rp, nrows,
+                                           rgba8.ctypes.data_as(_P), rgba32.ctypes.data_as(_P) if want_float else None,
+                                           nthreads, stats.ctypes.data_as(_P), 1 if brute_force else 0, schedule, split)
         if st:
             raise RuntimeError("oracle_render failed")
         return rgba8, rgba32, stats
 
-    def render_spec(self, spec, rows=None, nthreads=1, brute_force=False, want_float=True, schedule=0):
+    def render_spec(self, spec, rows=None, nthreads=1, brute_force=False, want_float=True, schedule=0, split=0):
         return self.render(spec.camera_buffer(), spec.lights, spec.material, spec.mode, spec.spp, spec.width,
-                           spec.height, rows, nthreads, brute_force, want_float, schedule)
+                           spec.height, rows, nthreads, brute_force, want_float, schedule, split)
 
     def trace_rays(self, rays: np.ndarray, any_hit=False, brute_force=False, cull_back=False, cull_front=False):
         r = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)

@@ -1290,6 +1290,8 @@ typedef struct {
   const float* mat;
   int mode, k, brute;
   uint32_t W, H;
+  int split; /* the device's forced tile-balance layouts (rt_set_tile_balance 2..4): 1 every tile in 2 x 2 parts,
+                2 in 4 x 4, 3 by tile position (tx + 2 ty) % 3 -> whole / 2 x 2 / 4 x 4; capped by the tile shape */
 } octx;
 
 static int trace_any(const octx* c, vec3 P, vec3 dir, ostats* st) {
@@ -1564,16 +1566,21 @@ static void store_px(const ojob* j, size_t o, vec3 acc) {
  * spp 4 / 16: the k x k samples of a pixel in consecutive lanes, (8 / k) x (8 / k) pixels per wave,
  * lane = k^2 * (8/k * (row % (8/k)) + column % (8/k)) + sample, sample = k * sy + sx; the pixel's
  * samples are summed in sample order as the loop adds them. */
+static uint32_t olog2u(uint32_t x) { return 31u - (uint32_t)__builtin_clz(x); }
+
 static void* render_tiles(void* arg) {
   ojob* j = (ojob*)arg;
   const octx* c = j->c;
   const int lanes_k = (c->k == 2 || c->k == 4) ? c->k : 1; /* samples held by lanes */
   const uint32_t ns = (uint32_t)(lanes_k * lanes_k), tp = 8u / (uint32_t)lanes_k;
   const uint32_t tw = (c->W + tp - 1) / tp, th = (j->nrows + tp - 1) / tp;
+  /* tile balance (rt_trace.hip packet_geometry / k_tile_plan): the parts a tile is traced as, each its own
+   * packet with the lanes outside its sub-rectangle dead; 4 x 4 parts need 4-pixel tile sides */
+  const uint32_t kmax = tp >= 4u ? 2u : tp >= 2u ? 1u : 0u;
   for (uint32_t t = j->tid; t < tw * th; t += j->nthreads) {
     const uint32_t tx = t % tw, ty = t / tw;
     uint32_t px[OPK], py[OPK], orow[OPK];
-    int inimg[OPK];
+    int inimg[OPK], inpart[OPK];
     float ox[OPK], oy[OPK];
     vec3 acc[OPK], col[OPK];
     for (int l = 0; l < OPK; ++l) {
@@ -1586,20 +1593,32 @@ static void* render_tiles(void* arg) {
       oy[l] = ((float)(s / (uint32_t)lanes_k) + 0.5f) / (float)lanes_k;
       acc[l] = mk(0, 0, 0);
     }
-    if (lanes_k > 1) {
-      osample_packet(c, px, py, inimg, ox, oy, col, &j->st);
-      for (int l = 0; l < OPK; l += (int)ns)
-        for (uint32_t q = 0; q < ns; ++q) acc[l] = vadd(acc[l], col[l + (int)q]);
-    } else {
-      for (int sy = 0; sy < c->k; ++sy)
-        for (int sx = 0; sx < c->k; ++sx) {
-          for (int l = 0; l < OPK; ++l) {
-            ox[l] = ((float)sx + 0.5f) / (float)c->k;
-            oy[l] = ((float)sy + 0.5f) / (float)c->k;
+    uint32_t code = c->split == 1 ? 1u : c->split == 2 ? 2u : c->split == 3 ? (tx + 2u * ty) % 3u : 0u;
+    if (code > kmax) code = kmax;
+    const uint32_t nparts = code == 0u ? 1u : code == 1u ? 4u : 16u, pq = 1u << code;
+    for (uint32_t part = 0; part < nparts; ++part) {
+      for (int l = 0; l < OPK; ++l) {
+        const uint32_t p = (uint32_t)l / ns;
+        inpart[l] = inimg[l] && ((p % tp) >> (olog2u(tp) - code)) == (part & (pq - 1u)) &&
+                    ((p / tp) >> (olog2u(tp) - code)) == (part >> code);
+      }
+      if (lanes_k > 1) {
+        osample_packet(c, px, py, inpart, ox, oy, col, &j->st);
+        for (int l = 0; l < OPK; l += (int)ns)
+          if (inpart[l])
+            for (uint32_t q = 0; q < ns; ++q) acc[l] = vadd(acc[l], col[l + (int)q]);
+      } else {
+        for (int sy = 0; sy < c->k; ++sy)
+          for (int sx = 0; sx < c->k; ++sx) {
+            for (int l = 0; l < OPK; ++l) {
+              ox[l] = ((float)sx + 0.5f) / (float)c->k;
+              oy[l] = ((float)sy + 0.5f) / (float)c->k;
+            }
+            osample_packet(c, px, py, inpart, ox, oy, col, &j->st);
+            for (int l = 0; l < OPK; ++l)
+              if (inpart[l]) acc[l] = vadd(acc[l], col[l]);
           }
-          osample_packet(c, px, py, inimg, ox, oy, col, &j->st);
-          for (int l = 0; l < OPK; ++l) acc[l] = vadd(acc[l], col[l]);
-        }
+      }
     }
     for (int l = 0; l < OPK; l += (int)ns) {
       if (!inimg[l]) continue;
@@ -1636,10 +1655,10 @@ static void* render_rows(void* arg) {
   return NULL;
 }
 
-int oracle_render(const oracle_scene* s, const float cb[64], const oracle_light* lights, uint32_t nlights,
-                  const float material[6], int mode, int spp, uint32_t W, uint32_t H, const uint32_t* rows,
-                  uint32_t nrows, uint8_t* rgba8, float* rgba32f, int nthreads, uint64_t* stats, int brute,
-                  int schedule) {
+int oracle_render_split(const oracle_scene* s, const float cb[64], const oracle_light* lights, uint32_t nlights,
+                        const float material[6], int mode, int spp, uint32_t W, uint32_t H, const uint32_t* rows,
+                        uint32_t nrows, uint8_t* rgba8, float* rgba32f, int nthreads, uint64_t* stats, int brute,
+                        int schedule, int split) {
   if (!s || !s->tlas || !cb || !lights || nlights < 1 || nlights > 16 || W == 0 || H == 0) return -1;
   int k = 0;
   for (int q = 1; q <= 4; ++q) if (q * q == spp) k = q;
@@ -1647,7 +1666,7 @@ int oracle_render(const oracle_scene* s, const float cb[64], const oracle_light*
   if (!rows) nrows = H;
   if (nthreads < 1) nthreads = 1;
   if (nthreads > 256) nthreads = 256;
-  octx c = {s, cb, lights, nlights, material, mode, k, brute, W, H};
+  octx c = {s, cb, lights, nlights, material, mode, k, brute, W, H, split};
   ojob jobs[256];
   pthread_t th[256];
   for (int t = 0; t < nthreads; ++t) {
@@ -1675,6 +1694,14 @@ int oracle_render(const oracle_scene* s, const float cb[64], const oracle_light*
       for (int q = 8; q < 12; ++q) stats[q] += jobs[t].st.v[q];
   if (stats) { stats[6] += (uint64_t)W * nrows; stats[7] += 1; }
   return 0;
+}
+
+int oracle_render(const oracle_scene* s, const float cb[64], const oracle_light* lights, uint32_t nlights,
+                  const float material[6], int mode, int spp, uint32_t W, uint32_t H, const uint32_t* rows,
+                  uint32_t nrows, uint8_t* rgba8, float* rgba32f, int nthreads, uint64_t* stats, int brute,
+                  int schedule) {
+  return oracle_render_split(s, cb, lights, nlights, material, mode, spp, W, H, rows, nrows, rgba8, rgba32f, nthreads,
+                             stats, brute, schedule, 0);
 }
 
 /* RayGen's camera rays (oraygen: the exact float32 bits the frame traces) for n pixels (px[i], py[i]) at the

@@ -65,6 +65,12 @@ int oracle_render(const oracle_scene* s, const float cb[64], const oracle_light*
                   const float material[6], int mode, int spp, uint32_t W, uint32_t H, const uint32_t* rows,
                   uint32_t nrows, uint8_t* rgba8, float* rgba32f, int nthreads, uint64_t* stats,
                   int brute_force, int schedule);
+/* the same, the packet schedule's tiles traced as the device's forced tile-balance layouts (rt_set_tile_balance
+ * 2 / 3 / 4 -> split 1 / 2 / 3): every tile in 2 x 2 parts, in 4 x 4, or by position; each part one packet */
+int oracle_render_split(const oracle_scene* s, const float cb[64], const oracle_light* lights, uint32_t nlights,
+                        const float material[6], int mode, int spp, uint32_t W, uint32_t H, const uint32_t* rows,
+                        uint32_t nrows, uint8_t* rgba8, float* rgba32f, int nthreads, uint64_t* stats,
+                        int brute_force, int schedule, int split);
 /* batch trace: rays n x 8 floats, ray_flags = D3D12_RAY_FLAG bits (0x04 first hit ends, 0x10 cull back
  * faces), hits n x 4 u32 (t bits, instance, prim, flag), uv n x 2 (may be NULL) */
 void oracle_camera_rays(const float cb[64], uint32_t W, uint32_t H, const uint32_t* px, const uint32_t* py, uint32_t n,

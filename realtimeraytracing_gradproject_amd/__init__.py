@@ -99,6 +99,8 @@ SIGNATURES = [
     ("rt_set_shading", _I, [_P, ctypes.POINTER(rt_light), _U32, ctypes.POINTER(rt_material), _I, _I]),
     ("rt_set_schedule", _I, [_P, _I]),
     ("rt_set_tile_rows", _I, [_P, _I]),
+    ("rt_set_tile_balance", _I, [_P, _I]),
+    ("rt_tile_balance_info", _I, [_P, _UP]),
     ("rt_set_stats", _I, [_P, _I]),
     ("rt_dispatch_rays", _I, [_P, _U32, _U32, _P, _U32, _P, _P, _P]),
     ("rt_trace_rays", _I, [_P, _P, _U32, _U32, _P, _P, _P]),
@@ -624,6 +626,16 @@ class Context:
     def set_tile_rows(self, rows: int):
         """rt_set_tile_rows: 8 (8 x 8 pixel tiles per wave, default) or 4 (8 x 4)."""
         self._check(self._lib.rt_set_tile_rows(self._h, rows), "rt_set_tile_rows")
+
+    def set_tile_balance(self, mode: int):
+        """rt_set_tile_balance: 0 off, 1 adaptive (default), 2 / 3 / 4 forced split layouts (tests)."""
+        self._check(self._lib.rt_set_tile_balance(self._h, mode), "rt_set_tile_balance")
+
+    def tile_balance_info(self) -> dict:
+        out = (ctypes.c_uint32 * 8)()
+        self._check(self._lib.rt_tile_balance_info(self._h, out), "rt_tile_balance_info")
+        return dict(zip(("plans", "split", "items", "extra_cap", "max_ticks", "mean_ticks", "threshold", "launches"),
+                        list(out)))
 
     def set_stats(self, on: bool):
         self._check(self._lib.rt_set_stats(self._h, 1 if on else 0), "rt_set_stats")

@@ -191,6 +191,24 @@ hipError_t note_reader(TlasVersion& v, hipStream_t s) {
   return hipSuccess;
 }
 
+// Tile balance (rt_set_tile_balance) of one launch shape (frame size, row list, frames per launch, tile layout):
+// the per-tile wave times the packet kernel leaves (FrameParams::cost), the plan kernel's summary in host-mapped
+// memory, and the work list's budget of extra waves for split tiles.
+struct BalanceMap {
+  uint32_t W = 0, nrows = 0, nframes = 0, tile_rows = 0, spp = 0, ntiles = 0;
+  const uint32_t* rows = nullptr;
+  uint32_t* cost = nullptr;          // device: ntiles wave times (s_memrealtime ticks)
+  rt::PlanStats* stats = nullptr;    // host-mapped, written by k_tile_plan
+  rt::PlanStats* stats_dev = nullptr;
+  uint32_t extra_cap = 0;
+  uint64_t launches = 0, tick = 0;
+  void release() {
+    if (cost) (void)hipFree(cost);
+    if (stats) (void)hipHostFree(stats);
+    *this = BalanceMap();
+  }
+};
+
 }  // namespace
 
 struct rt_ctx {
@@ -225,6 +243,14 @@ struct rt_ctx {
   // traversal-stack overflow areas in HBM for lanes whose path outgrows the LDS part: one slot per
   // launch that may run concurrently with another (frames in flight, rt_trace_rays batches)
   ScratchRing ovf;
+  // tile balance (rt_set_tile_balance): 0 off, 1 adaptive, 2 / 3 / 4 forced layouts (tests); one cost map per launch
+  // shape (least recently used of kMaxBalanceMaps replaced); the work lists, one per launch in flight, from a ring
+  int balance = 1;
+  static constexpr size_t kMaxBalanceMaps = 16;
+  std::vector<BalanceMap> bal;
+  uint64_t bal_clock = 0;
+  BalanceMap* bal_last = nullptr;
+  ScratchRing plans;
   // scene pools read by the trace kernels (rebuilt by every rt_tlas_build)
   rt::Bvh4Node* pool_nodes = nullptr;
   rt::TriRec* pool_tris = nullptr;
@@ -454,6 +480,8 @@ rt_status rt_destroy(rt_ctx_t c) {
   if (c->d_stats) (void)hipFree(c->d_stats);
   for (auto& sl : c->rows.slots) slot_release(sl);
   for (auto& sl : c->ovf.slots) slot_release(sl);
+  for (auto& sl : c->plans.slots) slot_release(sl);
+  for (auto& m : c->bal) m.release();
   if (c->raster_ev) (void)hipEventDestroy(c->raster_ev);
   if (c->pool_nodes) (void)hipFree(c->pool_nodes);
   if (c->pool_tris) (void)hipFree(c->pool_tris);
@@ -760,6 +788,30 @@ rt_status rt_set_tile_rows(rt_ctx_t c, int rows) {
   return RT_OK;
 }
 
+rt_status rt_set_tile_balance(rt_ctx_t c, int mode) {
+  if (!c) return RT_E_INVALID;
+  if (mode < 0 || mode > 4) return fail(c, RT_E_INVALID, "rt_set_tile_balance: mode 0 .. 4");
+  c->balance = mode;
+  return RT_OK;
+}
+
+rt_status rt_tile_balance_info(rt_ctx_t c, uint32_t out[8]) {
+  if (!c || !out) return RT_E_INVALID;
+  std::memset(out, 0, 8 * sizeof(uint32_t));
+  const BalanceMap* m = c->bal_last;
+  if (!m || !m->stats) return RT_OK;
+  const volatile rt::PlanStats* st = m->stats;
+  out[0] = st->plans;
+  out[1] = st->nsplit;
+  out[2] = st->nitems;
+  out[3] = m->extra_cap;
+  out[4] = st->max_cost;
+  out[5] = st->mean_cost;
+  out[6] = st->threshold;
+  out[7] = (uint32_t)std::min<uint64_t>(m->launches, 0xffffffffu);
+  return RT_OK;
+}
+
 rt_status rt_set_stats(rt_ctx_t c, int enable) {
   if (!c) return RT_E_INVALID;
   c->stats_on = enable != 0;
@@ -930,6 +982,66 @@ rt_status check_dispatch(rt_ctx* c, uint32_t W, uint32_t H, const void* rgba8) {
   return RT_OK;
 }
 
+// The cost map of a launch shape (created with zero costs on stream s: the first launch runs the plain grid).
+static BalanceMap* balance_map(rt_ctx* c, uint32_t W, uint32_t nrows, const uint32_t* d_rows, uint32_t nframes,
+                               uint32_t ntiles, hipStream_t s, hipError_t* err) {
+  *err = hipSuccess;
+  BalanceMap* lru = nullptr;
+  for (BalanceMap& m : c->bal) {
+    if (m.W == W && m.nrows == nrows && m.rows == d_rows && m.nframes == nframes && m.tile_rows == c->tile_rows &&
+        m.spp == c->fp.spp_side && m.ntiles == ntiles) {
+      m.tick = ++c->bal_clock;
+      return &m;
+    }
+    if (!lru || m.tick < lru->tick) lru = &m;
+  }
+  BalanceMap* m = nullptr;
+  if (c->bal.size() < rt_ctx::kMaxBalanceMaps) {
+    c->bal.emplace_back();
+    m = &c->bal.back();
+  } else {
+    // the least recently used shape's buffers may still be read by launches in flight
+    if ((*err = quiesce(c)) != hipSuccess) return nullptr;
+    m = lru;
+    if (c->bal_last == m) c->bal_last = nullptr;
+    m->release();
+  }
+  m->W = W;
+  m->nrows = nrows;
+  m->rows = d_rows;
+  m->nframes = nframes;
+  m->tile_rows = c->tile_rows;
+  m->spp = c->fp.spp_side;
+  m->ntiles = ntiles;
+  m->extra_cap = ntiles / 4u + 64u;
+  m->tick = ++c->bal_clock;
+  if ((*err = hipMalloc(&m->cost, (size_t)ntiles * 4)) != hipSuccess ||
+      (*err = hipMemsetAsync(m->cost, 0, (size_t)ntiles * 4, s)) != hipSuccess ||
+      (*err = hipHostMalloc((void**)&m->stats, sizeof(rt::PlanStats), hipHostMallocMapped)) != hipSuccess) {
+    m->release();
+    return nullptr;
+  }
+  std::memset(m->stats, 0, sizeof(rt::PlanStats));
+  if ((*err = hipHostGetDevicePointer((void**)&m->stats_dev, m->stats, 0)) != hipSuccess) {
+    m->release();
+    return nullptr;
+  }
+  return m;
+}
+
+// Whether this launch runs the plan kernel (adaptive mode): not before the shape has wave times; every launch while
+// the last plan saw a costliest tile above 2.5 x the mean (the slowest tiles set the frame time); else one launch
+// in 16 re-checks. The summary is read from host-mapped memory without a copy call (it may lag by a few launches).
+static bool balance_wants_plan(BalanceMap& m) {
+  const volatile rt::PlanStats* st = m.stats;
+  const uint32_t plans = st->plans, mx = st->max_cost, mean = st->mean_cost, want = st->want_extra;
+  if (plans) m.extra_cap = std::min<uint64_t>((uint64_t)want + want / 4u + 64u, 15ull * m.ntiles);
+  if (m.launches == 0) return false;
+  if (plans == 0) return true;
+  if ((uint64_t)mx * 2u > (uint64_t)mean * 5u) return true;
+  return m.launches % 16u == 0u;
+}
+
 // RayGen's per-frame constants from a camera buffer (UpdateCameraBuffer's 256 B, D3D12HelloTriangle.cpp:1144-1170):
 // viewInverse and projectionInverse as the HLSL reads them, and the origin mul(viewInverse, (0, 0, 0, 1)) by the
 // device's own hlsl_mul4 (RT_HD, no contraction), so the kernel gets the bits it would compute.
@@ -973,11 +1085,54 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
     if (st != RT_OK) return st;
   }
   HIPCHK(c, order_after_tlas(c, s), "rt_dispatch_rays: order after the TLAS build");
+  // tile balance (packet schedule): the per-tile wave times of this shape, and a work list when it pays
+  const rt::PacketGeometry g = rt::packet_geometry(sv, c->fp, c->schedule);
+  c->fp.plan = nullptr;
+  c->fp.cost = nullptr;
+  c->fp.grid_x = g.grid_x;
+  c->fp.waves_per_frame = g.waves_per_frame;
+  uint32_t plan_items = 0;
+  ScratchSlot* plan_slot = nullptr;
+  const bool forced = c->balance >= 2;
+  if (c->balance && g.packet && (forced || !c->stats_on) && (uint64_t)g.waves_per_frame * nframes < (1ull << 26)) {
+    const uint32_t ntiles = g.waves_per_frame * nframes;
+    hipError_t be;
+    BalanceMap* m = balance_map(c, W, nrows, d_rows, nframes, ntiles, s, &be);
+    if (!m) return hip_fail(c, be, "tile balance: cost map");
+    c->bal_last = m;
+    c->fp.cost = forced ? nullptr : m->cost;
+    if (forced || balance_wants_plan(*m)) {
+      const uint32_t extra = forced ? 15u * ntiles : m->extra_cap;
+      plan_items = ntiles + extra;
+      bool hit;
+      plan_slot = ring_acquire(c->plans, s, nullptr, &hit, &be);
+      if (be != hipSuccess) return hip_fail(c, be, "tile balance: order after in-flight launches");
+      HIPCHK(c, slot_reserve(*plan_slot, ((size_t)plan_items + 1) * 4), "hipMalloc(tile plan)");
+      rt::PlanArgs a;
+      a.cost = m->cost;
+      a.plan = (uint32_t*)plan_slot->buf;
+      a.stats = forced ? nullptr : m->stats_dev;
+      a.ntiles = ntiles;
+      a.extra_cap = extra;
+      a.slots = 7u * 1024u;  // the LAMBERT_SHADOW kernel's 7 waves per SIMD x 1024 SIMDs
+      a.kmax_code = g.kmax_code;
+      a.force = forced ? (uint32_t)(c->balance - 1) : 0u;
+      a.waves_per_frame = g.waves_per_frame;
+      a.grid_x = g.grid_x;
+      a.wx = g.wx;
+      a.wy = g.wy;
+      a.wl = g.wl;
+      HIPCHK(c, rt::launch_tile_plan(a, s), "tile plan launch");
+      c->fp.plan = a.plan;
+    }
+    m->launches += 1;
+  }
   hipError_t e = rt::launch_trace_frame(sv, c->fp, d_rows, rgba8, rgba32f, c->d_stats, c->stats_on,
-                                        c->schedule, s);
+                                        c->schedule, plan_items, s);
   if (e != hipSuccess) return hip_fail(c, e, "trace launch");
   HIPCHK(c, note_reader(c->ver[c->cur], s), "rt_dispatch_rays: record use");
   if (ovf_slot) HIPCHK(c, slot_mark_use(*ovf_slot, s), "overflow stack: record use");
+  if (plan_slot) HIPCHK(c, slot_mark_use(*plan_slot, s), "tile plan: record use");
   if (c->stats_on) {
     c->dispatches += nframes;
     c->pixels += (uint64_t)W * nrows * nframes;

@@ -159,7 +159,21 @@ struct FrameParams {
   uint32_t nframes;
   uint32_t frame_bytes;
   FrameCam cam[kMaxLaunchFrames];
+  // Tile balance (packet schedule, rt_set_tile_balance). plan: the launch's wave work list written by k_tile_plan
+  // (plan[0] = item count, plan[1 + i] = item i = wave slot << 6 | part << 2 | split code; split code 0: the whole
+  // tile, 1: quadrant `part` of 4, 2: cell `part` of 16), dealt to the waves of a 1-D grid in list order (costliest
+  // first), or null: wave slot = the plain grid's wave index. cost: per wave slot, the s_memrealtime ticks its tile
+  // took in the last launch of this shape (split tiles: the estimate from their parts), written at wave end, or null.
+  const uint32_t* plan;
+  uint32_t* cost;
+  uint32_t grid_x;           // workgroups along x of the plain grid
+  uint32_t waves_per_frame;  // waves of the plain grid per frame (wave slot = frame * waves_per_frame + ...)
 };
+
+// Tile-balance split codes (FrameParams::plan): parts per tile. The costliest quadrant of the costliest C4 tiles
+// takes 0.55 of the whole packet's fetches, the costliest 2 x 2 cell 0.35 (tools/split_study.py): the kernel's
+// estimate of a whole tile from one part's time, and the plan's estimate of a part from the whole.
+RT_HD uint32_t split_parts(uint32_t code) { return code == 0u ? 1u : code == 1u ? 4u : 16u; }
 
 // The trace kernels read one node pool and one triangle pool per scene: [TLAS | BLAS 0 | BLAS 1 ..]
 // with child refs rebased to pool indices (BLAS leaves -> ~(global triangle slot)). A uniform base

@@ -73,9 +73,38 @@ hipError_t tlas_prepare(const InstanceRec* d_inst, const float* d_blas_bounds, u
 
 // --- Trace (rt_trace.hip) -------------------------------------------------------------------
 
+// plan_items: with fp.plan set, the waves of the launch's 1-D grid (the work list's budget: tiles + parts)
 hipError_t launch_trace_frame(const SceneView& scene, const FrameParams& fp, const uint32_t* d_rows,
                               void* rgba8, float* rgba32f, unsigned long long* d_stats, bool stats,
-                              int schedule, hipStream_t stream);
+                              int schedule, uint32_t plan_items, hipStream_t stream);
+
+// The packet kernel's plain grid for a launch (schedule, tile layout), or packet = false (the per-lane kernel).
+struct PacketGeometry {
+  bool packet = false;
+  int ks = 1;                          // samples of a pixel in consecutive lanes (1, 2, 4), 0: the sample loop
+  uint32_t grid_x = 0, grid_y = 0;     // workgroups of one frame
+  uint32_t wx = 1, wy = 1, wl = 1;     // waves of a workgroup along x, y; total
+  uint32_t waves_per_frame = 0;
+  uint32_t kmax_code = 0;              // largest tile-balance split code the tile allows (0: none, 1: 4, 2: 16)
+};
+PacketGeometry packet_geometry(const SceneView& sc, const FrameParams& fp, int schedule);
+
+// Tile balance (k_tile_plan): the summary the plan kernel leaves in host-mapped memory for the next dispatches.
+struct PlanStats {
+  uint32_t nitems, nsplit, want_extra, max_cost, mean_cost, threshold, plans, pad;
+};
+struct PlanArgs {
+  const uint32_t* cost;   // per wave slot of the plain grid: the last launch's wave time (ticks)
+  uint32_t* plan;         // out: [0] item count, [1 ..] items (1 + ntiles + extra_cap words)
+  PlanStats* stats;       // host-mapped, or null
+  uint32_t ntiles;        // wave slots of the plain grid, every frame of the launch
+  uint32_t extra_cap;     // items beyond ntiles the launch's grid has waves for
+  uint32_t slots;         // wave slots of the GPU for the trace kernel (waves per SIMD x SIMDs)
+  uint32_t kmax_code;
+  uint32_t force;         // 0 adaptive; 1 / 2 / 3 forced layouts (tests)
+  uint32_t waves_per_frame, grid_x, wx, wy, wl;
+};
+hipError_t launch_tile_plan(const PlanArgs& a, hipStream_t stream);
 
 hipError_t launch_trace_rays(const SceneView& scene, const float* rays, uint32_t n, bool any_hit, bool cull,
                              uint32_t* hits, float* uv, unsigned long long* d_stats, bool stats,

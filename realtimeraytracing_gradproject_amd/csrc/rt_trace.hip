@@ -1524,12 +1524,12 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
 #endif
 }
 
-// The pixel store (RayGen.hlsl:42, gOutput = float4(color, 1) into the R8G8B8A8_UNORM UAV): frame blockIdx.z of
+// The pixel store (RayGen.hlsl:42, gOutput = float4(color, 1) into the R8G8B8A8_UNORM UAV): frame `frame` of
 // the launch, RGBA8 or, for the tiled-frame loop's strips, RGB8 (the alpha byte is the constant 255: the assembly
 // restores it, so it never crosses xGMI). out_bpp is uniform: one branch per wave.
-__device__ __forceinline__ void store_pixel(const FrameParams& fp, uint32_t* out, uint32_t o, V3 a) {
+__device__ __forceinline__ void store_pixel(const FrameParams& fp, uint32_t* out, uint32_t o, V3 a, uint32_t frame) {
   const uint32_t r = unorm8(a.x), g = unorm8(a.y), b = unorm8(a.z);
-  char* base = (char*)out + (size_t)blockIdx.z * fp.frame_bytes;
+  char* base = (char*)out + (size_t)frame * fp.frame_bytes;
   if (fp.out_bpp == 3u) {
     uint8_t* p = (uint8_t*)base + (size_t)o * 3u;
     p[0] = (uint8_t)r;
@@ -1588,7 +1588,7 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void k_trace_frame(SceneView 
       acc = v3(acc.x / ns, acc.y / ns, acc.z / ns);
     }
     const size_t o = (size_t)orow * fp.width + px;
-    store_pixel(fp, rgba8, (uint32_t)o, acc);
+    store_pixel(fp, rgba8, (uint32_t)o, acc, blockIdx.z);
     if (rgba32f) rgba32f[o] = make_float4(acc.x, acc.y, acc.z, 1.0f);
   }
   if (STATS) flush_stats<false>(cnt, stats);
@@ -1665,21 +1665,52 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
 #endif
   constexpr uint32_t NS = KS > 1 ? KS * KS : 1;  // samples of a pixel held by consecutive lanes
   constexpr uint32_t TP = ms_tile_w(KS);          // tile width in pixels (KS > 1: ms_tile_h(KS) rows)
-  constexpr uint32_t WX = packet_wx(KS), WY = packet_wy(KS);
+  constexpr uint32_t WX = packet_wx(KS), WY = packet_wy(KS), WL = WX * WY;
   // tile rows of a wave: TP, or 4 for 8 x 8 tiles at rt_set_tile_rows(4) (lanes past them idle)
   const uint32_t TR = (KS <= 1 && fp.tile_rows == 4u) ? 4u : ms_tile_h(KS);
   // the wave index is uniform: an SGPR, so the pixel of a lane can be re-derived from its lane id
-  const uint32_t lane = threadIdx.x & 63u, w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  // this wave's tile: the plain grid's (workgroup bx, by of frame bz, wave w), or the work list's item (tile
+  // balance): a whole tile or one part of a split one, costliest first. All uniform (SALU).
+  uint32_t bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z, slot = 0, split = 0, part = 0;
+  uint64_t t_wave = 0;
+  if (fp.plan) {
+    const RT_CONST uint32_t* plan = (const RT_CONST uint32_t*)fp.plan;
+    const uint32_t i = blockIdx.x * WL + w;
+    if (i >= plan[0]) return;  // the grid is sized for the list's budget: the waves past its end have nothing
+    const uint32_t it = plan[1 + i];
+    slot = it >> 6;
+    part = (it >> 2) & 15u;
+    split = it & 3u;
+    bz = slot / fp.waves_per_frame;
+    const uint32_t f = slot - bz * fp.waves_per_frame, wg = f / WL;
+    w = f - wg * WL;
+    by = wg / fp.grid_x;
+    bx = wg - by * fp.grid_x;
+  } else {
+    slot = ((bz * gridDim.y + by) * gridDim.x + bx) * WL + w;
+  }
+  if (fp.cost) {
+    t_wave = __builtin_amdgcn_s_memrealtime();
+    // the first part of a split tile restarts the tile's estimate (the parts raise it with atomicMax at their end)
+    if (split && part == 0u && lane == 0u) fp.cost[slot] = 0u;
+  }
   const uint32_t sample = lane % NS, pix = lane / NS;
-  const uint32_t x = blockIdx.x * (TP * WX) + (w % WX) * TP + (pix % TP);
+  // split tiles: only the lanes of this part's sub-rectangle of the pixel tile trace (2 x 2 or 4 x 4 parts;
+  // the others join the packets dead and store nothing)
+  const uint32_t psh = split, pq = 1u << psh;  // parts per side: 1, 2, 4
+  const bool inpart = ((pix % TP) >> (31u - __builtin_clz(TP) - psh)) == (part & (pq - 1u)) &&
+                      ((pix / TP) >> (31u - __builtin_clz(TR) - psh)) == (part >> psh);
+  const uint32_t x = bx * (TP * WX) + (w % WX) * TP + (pix % TP);
   uint32_t px[R], py[R], out[R];  // out: the pixel's output index, ~0 when this lane stores nothing
   bool inimg[R];
   V3 acc[R], col[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     px[r] = x;
-    const uint32_t orow = blockIdx.y * (TR * R * WY) + (w / WX) * (TR * R) + TR * r + pix / TP;
-    inimg[r] = x < fp.width && orow < fp.nrows && pix / TP < TR;
+    const uint32_t orow = by * (TR * R * WY) + (w / WX) * (TR * R) + TR * r + pix / TP;
+    inimg[r] = x < fp.width && orow < fp.nrows && pix / TP < TR && (R > 1 || inpart);
     py[r] = 0;
     if (inimg[r]) py[r] = rows ? rows[orow] : orow;
     out[r] = (inimg[r] && sample == 0) ? orow * fp.width + x : 0xffffffffu;  // < 2^32 pixels (rt_api.cpp)
@@ -1687,13 +1718,14 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
   }
   Counters cnt;
   const uint32_t k = KS == 1 ? 1u : (KS > 1 ? (uint32_t)KS : fp.spp_side);
+  const FrameCam& cam = fp.cam[bz];
   if (KS == 1) {
-    shade_sample_packet<MODE, STATS, R>(sc, fp, fp.cam[blockIdx.z], px, py, 0.5f, 0.5f, inimg, acc, cnt);  // (0 + 0.5) / 1
+    shade_sample_packet<MODE, STATS, R>(sc, fp, cam, px, py, 0.5f, 0.5f, inimg, acc, cnt);  // (0 + 0.5) / 1
   } else if (KS > 1) {
     // this lane's sample (sx, sy) of the k x k grid, the sample loop's offsets
     const float ox = ((float)(sample % KS) + 0.5f) / (float)KS;
     const float oy = ((float)(sample / KS) + 0.5f) / (float)KS;
-    shade_sample_packet<MODE, STATS, R>(sc, fp, fp.cam[blockIdx.z], px, py, ox, oy, inimg, col, cnt);
+    shade_sample_packet<MODE, STATS, R>(sc, fp, cam, px, py, ox, oy, inimg, col, cnt);
     // sum in sample order: ((0 + c0) + c1) + ... exactly as the loop adds them (0 + c0 == c0).
     // The lane id is re-read here (v_mbcnt) rather than kept live across the traces.
     uint32_t lid;
@@ -1706,16 +1738,18 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
                         __shfl(col[0].z, base + q, 64)));
     acc[0] = sum;
     // the store index too (not kept live across the traces: the 7-wave budget has no VGPR to spare)
-    const uint32_t xp = lid / NS, xx = blockIdx.x * (TP * WX) + (w % WX) * TP + (xp % TP);
+    const uint32_t xp = lid / NS, xx = bx * (TP * WX) + (w % WX) * TP + (xp % TP);
     constexpr uint32_t TH = ms_tile_h(KS);
-    const uint32_t orow = blockIdx.y * (TH * WY) + (w / WX) * TH + xp / TP;
-    out[0] = (xx < fp.width && orow < fp.nrows && (lid % NS) == 0u) ? orow * fp.width + xx : 0xffffffffu;
+    const uint32_t orow = by * (TH * WY) + (w / WX) * TH + xp / TP;
+    const bool lpart = ((xp % TP) >> (31u - __builtin_clz(TP) - psh)) == (part & (pq - 1u)) &&
+                       ((xp / TP) >> (31u - __builtin_clz(TH) - psh)) == (part >> psh);
+    out[0] = (xx < fp.width && orow < fp.nrows && (lid % NS) == 0u && lpart) ? orow * fp.width + xx : 0xffffffffu;
   } else {
     for (uint32_t sy = 0; sy < k; ++sy)
       for (uint32_t sx = 0; sx < k; ++sx) {
         const float ox = ((float)sx + 0.5f) / (float)k;
         const float oy = ((float)sy + 0.5f) / (float)k;
-        shade_sample_packet<MODE, STATS, R>(sc, fp, fp.cam[blockIdx.z], px, py, ox, oy, inimg, col, cnt);
+        shade_sample_packet<MODE, STATS, R>(sc, fp, cam, px, py, ox, oy, inimg, col, cnt);
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = add(acc[r], col[r]);
       }
@@ -1729,11 +1763,18 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
     }
     if (out[r] != 0xffffffffu) {
       const uint32_t o = out[r];
-      store_pixel(fp, rgba8, o, a);
+      store_pixel(fp, rgba8, o, a, bz);
       if (rgba32f && !RT_WAVE_TIMES) rgba32f[o] = make_float4(a.x, a.y, a.z, 1.0f);
     }
   }
   if (STATS) flush_stats<true>(cnt, stats);
+  if (fp.cost && lane == 0u) {
+    // this wave's time (100 MHz ticks); a part's time scaled to an estimate of its whole tile (the
+    // costliest part of a split tile takes about 0.55 (4 parts) / 0.35 (16) of the whole: split_parts)
+    const uint32_t dt = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_wave);
+    if (split == 0u) fp.cost[slot] = dt;
+    else atomicMax(fp.cost + slot, split == 1u ? (dt * 29u) >> 4 : (dt * 46u) >> 4);
+  }
 #if RT_WAVE_TIMES
   // diagnostics only: (start, end) of this wave on the 100 MHz clock + its XCC / CU ids, into the
   // caller's float4 buffer (slot = wave index; the float image is not written in this variant)
@@ -1838,17 +1879,14 @@ __global__ __launch_bounds__(256) void k_assemble16_rgb(uint32_t W4, uint32_t H,
 
 template <int MODE, bool STATS>
 hipError_t launch_mode(const SceneView& sc, const FrameParams& fp, const uint32_t* rows, void* rgba8,
-                       float* rgba32f, unsigned long long* stats, int schedule, hipStream_t s) {
+                       float* rgba32f, unsigned long long* stats, int schedule, uint32_t plan_items, hipStream_t s) {
   dim3 grid((fp.width + 15) / 16, (fp.nrows + 15) / 16, fp.nframes);
-  if (schedule == RT_SCHED_PACKET && sc.packet_cap < kPacketStack) {
+  const PacketGeometry g = packet_geometry(sc, fp, schedule);
+  if (g.packet) {
     constexpr int R = RT_PACKET_RAYS;
-    // KS: 1 one sample per pixel; 2 / 4 the k x k samples of a pixel in consecutive lanes; 0 the loop
-    const int ks = fp.spp_side == 1 ? 1 : ((RT_SAMPLE_LANES && R == 1 && (fp.spp_side == 2 || fp.spp_side == 4))
-                                               ? (int)fp.spp_side : 0);
-    const uint32_t tp = ms_tile_w(ks);
-    const uint32_t tr = (ks <= 1 && fp.tile_rows == 4u) ? 4u : ms_tile_h(ks);  // as the kernel's TR
-    const uint32_t tw = tp * (uint32_t)packet_wx(ks), th = tr * R * (uint32_t)packet_wy(ks);
-    dim3 gp((fp.width + tw - 1) / tw, (fp.nrows + th - 1) / th, fp.nframes);
+    const int ks = g.ks;
+    // the plain grid, or (tile balance) one wave per work-list item, as many as the list's budget
+    dim3 gp = fp.plan ? dim3((plan_items + g.wl - 1) / g.wl) : dim3(g.grid_x, g.grid_y, fp.nframes);
 #define RT_LAUNCH_PACKET(KS)                                                                                   \
   hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R, (R == 1 ? KS : 0)>), gp, dim3(packet_block(R == 1 ? KS : 0)), 0, s, sc, fp, \
                      rows, (uint32_t*)rgba8, (float4*)rgba32f, stats)
@@ -1867,27 +1905,186 @@ hipError_t launch_mode(const SceneView& sc, const FrameParams& fp, const uint32_
 
 }  // namespace
 
+PacketGeometry packet_geometry(const SceneView& sc, const FrameParams& fp, int schedule) {
+  PacketGeometry g;
+  g.packet = schedule == RT_SCHED_PACKET && sc.packet_cap < kPacketStack;
+  if (!g.packet) return g;
+  constexpr int R = RT_PACKET_RAYS;
+  // KS: 1 one sample per pixel; 2 / 4 the k x k samples of a pixel in consecutive lanes; 0 the loop
+  g.ks = fp.spp_side == 1 ? 1 : ((RT_SAMPLE_LANES && R == 1 && (fp.spp_side == 2 || fp.spp_side == 4))
+                                     ? (int)fp.spp_side : 0);
+  const uint32_t tp = ms_tile_w(g.ks);
+  const uint32_t tr = (g.ks <= 1 && fp.tile_rows == 4u) ? 4u : ms_tile_h(g.ks);  // as the kernel's TR
+  g.wx = (uint32_t)packet_wx(g.ks);
+  g.wy = (uint32_t)packet_wy(g.ks);
+  g.wl = g.wx * g.wy;
+  const uint32_t tw = tp * g.wx, th = tr * R * g.wy;
+  g.grid_x = (fp.width + tw - 1) / tw;
+  g.grid_y = (fp.nrows + th - 1) / th;
+  g.waves_per_frame = g.grid_x * g.grid_y * g.wl;
+  // a tile splits into 2 x 2 parts when both sides are >= 2 pixels, 4 x 4 when >= 4 (one ray per lane only; the
+  // shadow-ray compaction variant keeps whole tiles: it merges rays across a workgroup's waves)
+  const uint32_t side = tp < tr ? tp : tr;
+  g.kmax_code = (R != 1 || RT_SHADOW_COMPACT) ? 0u : side >= 4u ? 2u : side >= 2u ? 1u : 0u;
+  return g;
+}
+
 hipError_t launch_trace_frame(const SceneView& sc, const FrameParams& fp, const uint32_t* d_rows,
                               void* rgba8, float* rgba32f, unsigned long long* d_stats, bool stats,
-                              int schedule, hipStream_t s) {
+                              int schedule, uint32_t plan_items, hipStream_t s) {
   switch (fp.shade_mode) {
     case 0:
       // the reference scene's parity config pins reflectivity to 0: a kernel without
       // the reflection-chain state (registers, the per-lane sk[] stack) then runs at a higher occupancy
       if (fp.material.reflectivity == 0.0f && RT_REF_NOREFL)
-        return stats ? launch_mode<3, true>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, s)
-                     : launch_mode<3, false>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, s);
-      return stats ? launch_mode<0, true>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, s)
-                   : launch_mode<0, false>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, s);
+        return stats ? launch_mode<3, true>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, plan_items, s)
+                     : launch_mode<3, false>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, plan_items, s);
+      return stats ? launch_mode<0, true>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, plan_items, s)
+                   : launch_mode<0, false>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, plan_items, s);
     case 1:
-      return stats ? launch_mode<1, true>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, s)
-                   : launch_mode<1, false>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, s);
+      return stats ? launch_mode<1, true>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, plan_items, s)
+                   : launch_mode<1, false>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, plan_items, s);
     case 2:
-      return stats ? launch_mode<2, true>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, s)
-                   : launch_mode<2, false>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, s);
+      return stats ? launch_mode<2, true>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, plan_items, s)
+                   : launch_mode<2, false>(sc, fp, d_rows, rgba8, rgba32f, d_stats, schedule, plan_items, s);
     default:
       return hipErrorInvalidValue;
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// Tile balance: the wave work list of one launch (k_tile_plan, one workgroup). A frame lasts as long as its
+// slowest tiles (a wave walks the union of its 64 rays' paths; on C4 one 8 x 8 tile takes as long as the rest of
+// the frame, profiles/r03_wave_times_C4.txt). From the per-tile wave times of the last launch of this shape
+// (FrameParams::cost), the load bound L = summed time / the GPU's wave slots and the threshold T = max(L, 0.35 x
+// the costliest tile): a tile above T is traced as 4 parts (2 x 2 sub-rectangles) when 0.55 x its time fits T,
+// else as 16; then every item is dealt longest first (a counting sort into kPlanBuckets classes of estimated
+// time), so the long waves start at the front of the launch instead of forming its tail. The list is always a
+// valid cover (each tile once, or each of its parts once) whatever the costs hold: the image never depends on it,
+// only the schedule. Items beyond the grid's budget are refused by raising T. (tools/split_study.py models the
+// rule on the oracle's packet fetches: C4 whole frame 0.71, rank 0's share at N = 4 / 8 0.45 / 0.48 of the plain
+// grid's time.) The north star's "wavefront ballot/prefix-sum" appears here as the block scan of the buckets.
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t kPlanBuckets = 64;
+constexpr uint32_t kPlanThreads = 1024;
+
+__device__ __forceinline__ uint32_t plan_code(uint64_t c, uint64_t T, uint32_t kmax) {
+  if (c <= T || kmax == 0u) return 0u;
+  return (kmax == 1u || c * 11u <= T * 20u) ? 1u : 2u;  // 0.55 c fits T: 4 parts, else 16
+}
+
+__device__ __forceinline__ uint64_t plan_est(uint64_t c, uint32_t code) {
+  return code == 0u ? c : code == 1u ? (c * 11u) / 20u : (c * 7u) / 20u;
+}
+
+// forced layouts (tests: the oracle emulates the same parts): 1 every tile in 4, 2 every tile in 16, 3 by tile
+// position ((tx + 2 ty) % 3: whole, 4, 16), capped by the tile shape
+__device__ __forceinline__ uint32_t plan_forced(const PlanArgs& a, uint32_t t) {
+  uint32_t code = a.force == 1u ? 1u : a.force == 2u ? 2u : 0u;
+  if (a.force == 3u) {
+    const uint32_t f = t % a.waves_per_frame, wg = f / a.wl, w = f % a.wl;
+    const uint32_t tx = (wg % a.grid_x) * a.wx + w % a.wx, ty = (wg / a.grid_x) * a.wy + w / a.wx;
+    code = (tx + 2u * ty) % 3u;
+  }
+  return code < a.kmax_code ? code : a.kmax_code;
+}
+
+__device__ uint64_t block_sum64(uint64_t v, uint64_t* sh) {
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63u) == 0u) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint64_t t = 0;
+  for (uint32_t k = 0; k < kPlanThreads / 64u; ++k) t += sh[k];
+  return t;
+}
+
+__global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
+  __shared__ uint64_t s_red[kPlanThreads / 64];
+  __shared__ uint32_t s_hist[kPlanBuckets], s_off[kPlanBuckets];
+  const uint32_t tid = threadIdx.x, n = a.ntiles;
+  if (tid < kPlanBuckets) s_hist[tid] = 0u;
+  uint64_t T = ~0ull, mx = 0, sum = 0;
+  uint32_t want = 0;
+  if (!a.force) {
+    uint64_t lsum = 0, lmax = 0;
+    for (uint32_t t = tid; t < n; t += kPlanThreads) {
+      const uint64_t c = a.cost[t];
+      lsum += c;
+      lmax = c > lmax ? c : lmax;
+    }
+    sum = block_sum64(lsum, s_red);
+    // max through the same reduction (as a sum of one-hot maxima is not available): a second pass over LDS
+    for (int o = 32; o >= 1; o >>= 1) {
+      const uint64_t q = __shfl_xor(lmax, o, 64);
+      lmax = q > lmax ? q : lmax;
+    }
+    __syncthreads();
+    if ((tid & 63u) == 0u) s_red[tid >> 6] = lmax;
+    __syncthreads();
+    for (uint32_t k = 0; k < kPlanThreads / 64u; ++k) mx = s_red[k] > mx ? s_red[k] : mx;
+    if (mx > 0u) {
+      const uint64_t L = sum / (a.slots ? a.slots : 1u), F = (mx * 7u) / 20u;
+      T = L > F ? L : F;
+    }
+    // the parts must fit the grid's budget: raise T until they do (the first count is the demand, reported)
+    for (int iter = 0; iter < 24; ++iter) {
+      uint64_t ex = 0;
+      for (uint32_t t = tid; t < n; t += kPlanThreads) ex += split_parts(plan_code(a.cost[t], T, a.kmax_code)) - 1u;
+      ex = block_sum64(ex, s_red);
+      if (iter == 0) want = (uint32_t)(ex < 0xffffffffull ? ex : 0xffffffffull);
+      if (ex <= a.extra_cap) break;
+      T += T / 4u + 1u;
+    }
+  }
+  __syncthreads();
+  // histogram of the items by estimated time: bucket 0 the longest
+  uint32_t nsplit = 0;
+  for (uint32_t t = tid; t < n; t += kPlanThreads) {
+    const uint64_t c = a.force ? 0u : a.cost[t];
+    const uint32_t code = a.force ? plan_forced(a, t) : plan_code(c, T, a.kmax_code);
+    const uint64_t e = plan_est(c, code);
+    const uint32_t b = mx ? (uint32_t)(((mx - (e < mx ? e : mx)) * kPlanBuckets) / (mx + 1u)) : kPlanBuckets - 1u;
+    atomicAdd(&s_hist[b], split_parts(code));
+    nsplit += code ? 1u : 0u;
+  }
+  __syncthreads();
+  if (tid == 0u) {
+    uint32_t run = 0;
+    for (uint32_t b = 0; b < kPlanBuckets; ++b) {
+      s_off[b] = run;
+      run += s_hist[b];
+    }
+    a.plan[0] = run;  // the item count (the trace waves past it exit)
+  }
+  __syncthreads();
+  // scatter (the order inside a bucket is whatever the atomics give: only the schedule depends on it)
+  for (uint32_t t = tid; t < n; t += kPlanThreads) {
+    const uint64_t c = a.force ? 0u : a.cost[t];
+    const uint32_t code = a.force ? plan_forced(a, t) : plan_code(c, T, a.kmax_code);
+    const uint64_t e = plan_est(c, code);
+    const uint32_t b = mx ? (uint32_t)(((mx - (e < mx ? e : mx)) * kPlanBuckets) / (mx + 1u)) : kPlanBuckets - 1u;
+    const uint32_t k = split_parts(code);
+    const uint32_t pos = atomicAdd(&s_off[b], k);
+    for (uint32_t q = 0; q < k; ++q) a.plan[1u + pos + q] = (t << 6) | (q << 2) | code;
+  }
+  // summary for the host (host-mapped memory: read at a later dispatch, no copy call)
+  nsplit = (uint32_t)block_sum64(nsplit, s_red);
+  if (tid == 0u && a.stats) {
+    PlanStats* st = a.stats;
+    st->nitems = a.plan[0];
+    st->nsplit = nsplit;
+    st->want_extra = want;
+    st->max_cost = (uint32_t)(mx < 0xffffffffull ? mx : 0xffffffffull);
+    st->mean_cost = n ? (uint32_t)(sum / n) : 0u;
+    st->threshold = (uint32_t)(T < 0xffffffffull ? T : 0xffffffffull);
+    st->plans += 1u;
+  }
+}
+
+hipError_t launch_tile_plan(const PlanArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_tile_plan, dim3(1), dim3(kPlanThreads), 0, s, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_trace_rays(const SceneView& sc, const float* rays, uint32_t n, bool any_hit, bool cull,

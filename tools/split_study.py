@@ -135,6 +135,32 @@ def main():
             ms = makespan(us(d))
             print(f"  adaptive alpha {alpha}: L {L:.1f} us, {nsplit} tiles split, waves {len(d)}, longest-first "
                   f"makespan {ms:.1f} us ({ms / base:.3f}), longest {us(d.max()):.1f} us")
+        # the kernel's rule (the plan kernel only knows whole-tile costs): T = beta x L; a tile costing more than T
+        # becomes 4 sub-packets when 0.55 x its cost (the median costliest quadrant) fits T, else 16; waves ordered
+        # by estimated cost (tile cost x 0.55 / 0.35 for parts), longest first
+        for beta in (0.3, 0.35, 0.4, 0.5):
+            wt = us(flat[:, 0])
+            L = wt.sum() / SLOTS
+            T = max(L, beta * wt.max())
+            est, act = [], []
+            nsplit = 0
+            for row, cw in zip(flat, wt):
+                if cw <= T:
+                    est.append(cw)
+                    act.append(row[0])
+                    continue
+                nsplit += 1
+                if 0.55 * cw <= T:
+                    est.extend([0.55 * cw] * 4)
+                    act.extend(row[3:7])
+                else:
+                    est.extend([0.35 * cw] * 16)
+                    act.extend(row[7:23])
+            order = np.argsort(-np.array(est), kind="stable")
+            d = np.array(act)[order]
+            ms = makespan(us(d))
+            print(f"  rule T = max(L, {beta} x costliest): T {T:.1f} us, {nsplit} tiles split, waves {len(d)}, makespan {ms:.1f} us "
+                  f"({ms / base:.3f}), longest {us(d.max()):.1f} us")
 
 
 if __name__ == "__main__":
