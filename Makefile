@@ -30,7 +30,31 @@ RCPCHECK  := tools/bin/recip_check
 
 HDRS      := include/rt_api.h $(SRC)/rt_device.hpp $(SRC)/rt_internal.hpp
 
-all: $(LIB) $(APP) $(ORACLE) $(BASELINE) $(RCPCHECK)
+# Library variants with the non-default code-shape knobs still in the tree (rt_device.hpp / rt_trace.hip), each
+# checked against the oracle on the GPU by tests/test_gpu_variants.py:
+#   n1        RT_SHADOW_COMPACT=1 RT_HYBRID_T=8: workgroup shadow-ray compaction + per-lane subtree hand-off (the
+#             north star's ballot / prefix-sum compaction designs)
+#   n1root    RT_HYBRID_T=16 RT_HYBRID_ROOT=1: the hand-off considered at BLAS roots only
+#   rays2     RT_PACKET_RAYS=2 RT_SAMPLE_LANES=0 RT_RCP_EXACT=0: two rays per lane (8 x 16 tiles), multi-sample
+#             frames through the sample loop, IEEE divisions everywhere
+#   alt       RT_PACKET_OCT=0 RT_REF_NOREFL=0 RT_RCP_EXACT=7 RT_MS_WIDE=1: min/max slab planes, the reflective REF
+#             kernel for reflectivity 0, rcp + Newton everywhere, wide multi-sample tiles
+#   wavetimes RT_WAVE_TIMES=1: the per-wave clock records of tools/wave_times.py
+VDIR      := $(LIBDIR)/variants
+VSRCS     := $(SRC)/rt_api.cpp $(SRC)/rt_comm.cpp $(SRC)/rt_lbvh.hip $(SRC)/rt_trace.hip $(SRC)/rt_raster.hip \
+             $(SRC)/rt_host.cpp $(HDRS) tools/build_variant.sh
+VARIANTS  := n1 n1root rays2 alt wavetimes
+VLIBS     := $(foreach v,$(VARIANTS),$(VDIR)/$(v)/librtamd.so)
+DEFS_n1        := -DRT_SHADOW_COMPACT=1 -DRT_HYBRID_T=8
+DEFS_n1root    := -DRT_HYBRID_T=16 -DRT_HYBRID_ROOT=1
+DEFS_rays2     := -DRT_PACKET_RAYS=2 -DRT_SAMPLE_LANES=0 -DRT_RCP_EXACT=0
+DEFS_alt       := -DRT_PACKET_OCT=0 -DRT_REF_NOREFL=0 -DRT_RCP_EXACT=7 -DRT_MS_WIDE=1
+DEFS_wavetimes := -DRT_WAVE_TIMES=1
+
+all: $(LIB) $(APP) $(ORACLE) $(BASELINE) $(RCPCHECK) $(VLIBS)
+
+$(VDIR)/%/librtamd.so: $(VSRCS)
+	bash tools/build_variant.sh $* $(DEFS_$*) > /dev/null
 
 $(BUILD)/%.o: $(SRC)/%.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -76,6 +100,6 @@ $(BUILD) $(LIBDIR):
 	mkdir -p $@
 
 clean:
-	rm -rf $(BUILD) $(LIB) $(APP) $(ORACLE) $(BASELINE) $(RCPCHECK)
+	rm -rf $(BUILD) $(LIB) $(APP) $(ORACLE) $(BASELINE) $(RCPCHECK) $(VDIR)
 
 .PHONY: all clean ref

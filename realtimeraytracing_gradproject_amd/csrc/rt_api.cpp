@@ -1094,7 +1094,8 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
   uint32_t plan_items = 0;
   ScratchSlot* plan_slot = nullptr;
   const bool forced = c->balance >= 2;
-  if (c->balance && g.packet && (forced || !c->stats_on) && (uint64_t)g.waves_per_frame * nframes < (1ull << 26)) {
+  if (c->balance && g.packet && g.plannable && (forced || !c->stats_on) &&
+      (uint64_t)g.waves_per_frame * nframes < (1ull << 26)) {
     const uint32_t ntiles = g.waves_per_frame * nframes;
     hipError_t be;
     BalanceMap* m = balance_map(c, W, nrows, d_rows, nframes, ntiles, s, &be);

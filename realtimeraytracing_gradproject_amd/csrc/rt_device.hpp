@@ -17,19 +17,12 @@
 
 #define RT_HD __host__ __device__ __forceinline__
 
-// Code-shape knobs, A/B-timed in one process with tools/ab.py (results in DESIGN.md §3.2). They
-// change instruction schedules only: every setting renders the identical image.
-#ifndef RT_MT_EARLY_EXIT
-#define RT_MT_EARLY_EXIT 1  // Moller-Trumbore with early rejects (vs one final predicate)
-#endif
-#ifndef RT_COND_PUSH
-#define RT_COND_PUSH 1      // push only hit children (vs unconditional LDS writes, predicated sp)
-#endif
+// Code-shape knobs, A/B-timed in one process with tools/ab.py (results in DESIGN.md §3.2). Each renders the
+// identical image; the non-default settings kept in the tree are built and checked against the oracle by
+// tests/test_gpu_variants.py (the library variants __graft_entry__.build() compiles). Settings measured slower
+// and removed are listed in DESIGN.md §3.2.
 #ifndef RT_PACKET_RAYS
 #define RT_PACKET_RAYS 1    // rays per lane in a packet (2: 128-ray packets, 8 x 16 pixels per wave)
-#endif
-#ifndef RT_ARGMIN_ORDER
-#define RT_ARGMIN_ORDER 0   // nearest child only (vs the full 4-sort; the sort culls better)
 #endif
 
 namespace rt {
@@ -389,49 +382,21 @@ RT_HD void sort4(float t[4], int32_t r[4]) {
   cswap(t[1], r[1], t[2], r[2]);
 }
 
-#ifndef RT_MT_FMA
-#define RT_MT_FMA 2  // bit 0: the triangle test's dot products as fused multiply-add chains; bit 1: its cross products
-#endif
-// dot / cross for the triangle test. Default: cross products fused (fma(a.y, b.z, -(a.z * b.y)) ...), dot products
+// dot / cross for the triangle test: cross products fused (fma(a.y, b.z, -(a.z * b.y)) ...), dot products
 // unfused, mirrored bit for bit by the oracle's omt_cross / omt_dot (as the slab test's fmas are by oslab4).
 // profiles/r03_ab_mt_fma.txt: fused cross 1-2% faster frames with the seam-probe leak count nearly unchanged
-// (1727 -> 1832 of 66,304 edge rays); fusing the dots as well gains 2-4% but raises it to 2514, so they stay unfused.
-// Any other setting renders frames the oracle no longer matches bit for bit.
-RT_HD float mt_dot(V3 a, V3 b) {
-#if RT_MT_FMA & 1
-  return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x));
-#else
-  return dot(a, b);
-#endif
-}
+// (1727 -> 1832 of 66,304 edge rays, pinned by tests/test_oracle.py); fusing the dots as well gained 2-4% but
+// raised it to 2514, so they stay unfused (a deliberate deviation from DXR's watertight test).
+RT_HD float mt_dot(V3 a, V3 b) { return dot(a, b); }
 RT_HD V3 mt_cross(V3 a, V3 b) {
-#if RT_MT_FMA & 2
   return v3(__builtin_fmaf(a.y, b.z, -(a.z * b.y)), __builtin_fmaf(a.z, b.x, -(a.x * b.z)),
             __builtin_fmaf(a.x, b.y, -(a.y * b.x)));
-#else
-  return cross(a, b);
-#endif
 }
 
-#ifndef RT_FLAT_BITS
-#define RT_FLAT_BITS 1  // the packet walk's triangle acceptance as bitwise & (no exec-mask region; A/B knob)
-#endif
-#ifndef RT_FLAT_UV2
-#define RT_FLAT_UV2 1  // the bitwise acceptance with the implied u <= 1 dropped and min(u, v) >= 0
-#endif
-#ifndef RT_FACE_FOLD
-#define RT_FACE_FOLD 1  // the culling term skipped where face is the constant 0 (same acceptance)
-#endif
 // The culling term of the triangle test: det * face < 0 rejects. With face == 0 (no culling: primary and shadow
 // rays) det * 0 is +-0 or NaN, never < 0, so the term is always false; written so the compiler folds it away when
 // face is the constant 0 after inlining (it does not fold x * 0 < 0 itself) instead of a multiply and a compare.
-RT_HD bool culled(float det, float face) {
-#if RT_FACE_FOLD
-  return face != 0.0f && det * face < 0.0f;
-#else
-  return det * face < 0.0f;
-#endif
-}
+RT_HD bool culled(float det, float face) { return face != 0.0f && det * face < 0.0f; }
 
 // 1 / det of the triangle test (RT_RCP_EXACT bit 1: rcp_exact; off: the division, same bits)
 RT_HD float mt_rcp(float det) {
@@ -447,7 +412,6 @@ RT_HD float mt_rcp(float det) {
 // RAY_FLAG_CULL_BACK_FACING_TRIANGLES (front = clockwise seen from the ray origin = det > 0 with
 // det = e1 . (d x e2), the sense flipped by a negative instance-transform determinant: face = -1).
 RT_HD bool moller_trumbore(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, float& t, float& u, float& v) {
-#if RT_MT_EARLY_EXIT
   V3 p = mt_cross(d, e2);
   float det = mt_dot(e1, p);
   if (det == 0.0f || culled(det, face)) return false;
@@ -460,31 +424,6 @@ RT_HD bool moller_trumbore(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, float& t
   if (!(v >= 0.0f && u + v <= 1.0f)) return false;
   t = mt_dot(e2, q) * inv;
   return true;
-#else
-  const V3 p = mt_cross(d, e2);
-  const float det = mt_dot(e1, p);
-  const float inv = mt_rcp(det);
-  const V3 s = sub(o, v0);
-  u = mt_dot(s, p) * inv;
-  const V3 q = mt_cross(s, e1);
-  v = mt_dot(d, q) * inv;
-  t = mt_dot(e2, q) * inv;
-  return det != 0.0f && !culled(det, face) && u >= 0.0f && u <= 1.0f && v >= 0.0f && u + v <= 1.0f;
-#endif
-}
-
-// Bitwise acceptance (no short-circuit, so no exec-mask branch around the u / v / t products):
-// the same predicate, every term evaluated.
-RT_HD bool moller_trumbore_bits(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, float& t, float& u, float& v) {
-  const V3 p = mt_cross(d, e2);
-  const float det = mt_dot(e1, p);
-  const float inv = mt_rcp(det);
-  const V3 s = sub(o, v0);
-  u = mt_dot(s, p) * inv;
-  const V3 q = mt_cross(s, e1);
-  v = mt_dot(d, q) * inv;
-  t = mt_dot(e2, q) * inv;
-  return (det != 0.0f) & !culled(det, face) & (u >= 0.0f) & (u <= 1.0f) & (v >= 0.0f) & (u + v <= 1.0f);
 }
 
 // Moller-Trumbore without early exits: every lane runs the same instructions (the wave-packet
@@ -499,16 +438,11 @@ RT_HD bool moller_trumbore_flat(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float face, flo
   const V3 q = mt_cross(s, e1);
   v = mt_dot(d, q) * inv;
   t = mt_dot(e2, q) * inv;
-#if RT_FLAT_BITS && RT_FLAT_UV2
-  // The same acceptance with two terms fewer. u <= 1 is implied: v >= 0 (not NaN) makes u + v >= u exactly, and
-  // rounding is monotone, so fl(u + v) <= 1 gives u <= 1 (a NaN u fails u + v <= 1). min(u, v) >= 0 is u >= 0 and
-  // v >= 0 for non-NaN u, v (-0 included); a NaN one (the min returns the other) fails u + v <= 1 anyway.
+  // Bitwise & (no exec-mask region), with two terms fewer than the early-exit form. u <= 1 is implied: v >= 0
+  // (not NaN) makes u + v >= u exactly, and rounding is monotone, so fl(u + v) <= 1 gives u <= 1 (a NaN u fails
+  // u + v <= 1). min(u, v) >= 0 is u >= 0 and v >= 0 for non-NaN u, v (-0 included); a NaN one (the min returns
+  // the other) fails u + v <= 1 anyway (tests/test_acceptance.py).
   return (det != 0.0f) & !culled(det, face) & (__builtin_fminf(u, v) >= 0.0f) & (u + v <= 1.0f);
-#elif RT_FLAT_BITS
-  return (det != 0.0f) & !culled(det, face) & (u >= 0.0f) & (u <= 1.0f) & (v >= 0.0f) & (u + v <= 1.0f);
-#else
-  return det != 0.0f && !culled(det, face) && u >= 0.0f && u <= 1.0f && v >= 0.0f && u + v <= 1.0f;
-#endif
 }
 
 // HLSL reflect(i, n) = i - 2 * n * dot(i, n), evaluated as i - (2 n) * dot(i, n).

@@ -86,6 +86,7 @@ struct PacketGeometry {
   uint32_t wx = 1, wy = 1, wl = 1;     // waves of a workgroup along x, y; total
   uint32_t waves_per_frame = 0;
   uint32_t kmax_code = 0;              // largest tile-balance split code the tile allows (0: none, 1: 4, 2: 16)
+  bool plannable = false;              // a work list may drive the launch
 };
 PacketGeometry packet_geometry(const SceneView& sc, const FrameParams& fp, int schedule);
 

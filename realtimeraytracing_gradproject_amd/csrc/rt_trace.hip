@@ -56,39 +56,12 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 typedef int i4v __attribute__((ext_vector_type(4)));
 typedef int i8v __attribute__((ext_vector_type(8)));
 typedef float f8v __attribute__((ext_vector_type(8)));
-#ifndef RT_SINGLE_SKIP
-#define RT_SINGLE_SKIP 1  // closest-hit BLAS nodes with one entered internal child skip the keys
-#endif
-#ifndef RT_TLAS_SINGLE_SKIP
-#define RT_TLAS_SINGLE_SKIP 1  // the same for TLAS nodes
-#endif
 #ifndef RT_REF0_WAVES
 #define RT_REF0_WAVES 6  // the reflectivity-0 REF kernel (MODE 3, one sample): 73 VGPRs, no spills (7 waves: 2
                          // spilled VGPRs, the same frame time)
 #endif
 #ifndef RT_REF_NOREFL
 #define RT_REF_NOREFL 1  // RT_SHADE_REF with reflectivity 0: the kernel specialised without reflection rays
-#endif
-#ifndef RT_KEY_BFI
-#define RT_KEY_BFI 1  // nearest-child keys masked by v_bfi against the entered set (no s_not)
-#endif
-#ifndef RT_PUSH_P_VALU
-#define RT_PUSH_P_VALU 0  // closest-hit BLAS push: the pending set formed per lane in VALU (A/B knob)
-#endif
-#ifndef RT_TRI_UNROLL
-#define RT_TRI_UNROLL 1  // triangle children tested per slot, unrolled (0: a ctz loop with a ref-select chain)
-#endif
-#ifndef RT_ANY_MT_BITS
-#define RT_ANY_MT_BITS 0  // any-hit triangle tests with the bitwise acceptance (A/B knob)
-#endif
-#ifndef RT_OCT_BASES
-#define RT_OCT_BASES 2  // uniform-octant row loads: 1 one SGPR base per row, 2 node base + row soffset (A/B)
-#endif
-#ifndef RT_TBEST_ASM
-#define RT_TBEST_ASM 1  // slab tests: the min with the ray's t as v_min asm (no per-node canonicalise: C2 -2 % median, C4/C5 -0.3..0.6 %)
-#endif
-#ifndef RT_KEY64
-#define RT_KEY64 1  // closest-hit tie-break (instance, primitive) as one 64-bit compare (C2 -1.4 %)
 #endif
 #ifndef RT_PACKET_OCT
 #define RT_PACKET_OCT 1  // uniform-octant BLAS walks load near/far planes directly (no min/max pairs)
@@ -192,27 +165,11 @@ __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, H
       if (STATS)
         cnt.aabb += (uint32_t)(r[0] != kEmptyChild) + (uint32_t)(r[1] != kEmptyChild) +
                     (uint32_t)(r[2] != kEmptyChild) + (uint32_t)(r[3] != kEmptyChild);
-#if RT_ARGMIN_ORDER
-      // nearest child first; the others keep slot order
-      {
-        int b = 0;
-#pragma unroll
-        for (int k = 1; k < 4; ++k) b = tn[k] < tn[b] ? k : b;
-        const float tb = tn[b];
-        const int32_t rb = r[b];
-        tn[b] = tn[0];
-        r[b] = r[0];
-        tn[0] = tb;
-        r[0] = rb;
-      }
-#else
       sort4(tn, r);
-#endif
       if (tn[0] != __builtin_inff()) {
 #pragma unroll
         for (int k = 3; k >= 1; --k) {
           const bool h = tn[k] != __builtin_inff();
-#if RT_COND_PUSH
           if (h) {
             if (sp < cap) {
               stk.put(sp, r[k]);
@@ -221,12 +178,6 @@ __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, H
               ++cnt.overflow;
             }
           }
-#else
-          // unconditional write (a miss leaves a dead value above the top), predicated sp
-          stk.put(sp, r[k]);
-          if (STATS && h && sp >= cap) ++cnt.overflow;
-          sp += (h && sp < cap) ? 1 : 0;
-#endif
         }
         ref = r[0];
         continue;
@@ -319,14 +270,6 @@ __device__ __forceinline__ uint64_t wave_ballot(bool p) { return __builtin_amdgc
 
 __device__ __forceinline__ f4v cld4(const RT_CONST char* p) { return *(const RT_CONST f4v*)p; }
 
-// -1 in every lane if bit k of the uniform m is set, else 0 (VALU: v_bfe_i32 on an SGPR operand;
-// keeps this per-child select off the scalar unit, the packet walk's tightest pipe)
-__device__ __forceinline__ uint32_t bit_mask_v(uint32_t m, int k) {
-  uint32_t r;
-  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(r) : "s"(m), "i"(k));
-  return r;
-}
-
 // key where bit k of the uniform entered set m is set, else all ones (v_bfe_i32 + v_bfi_b32 on the
 // SGPR m: no scalar instruction to invert m first)
 __device__ __forceinline__ uint32_t key_if_entered(uint32_t key, uint32_t m, int k) {
@@ -351,21 +294,6 @@ __device__ __forceinline__ int push_entry(int stk, int& sp, uint32_t entry_base,
       "s_or_b32 %2, %6, %0"
       : "=&s"(p), "+s"(sp), "=&s"(e), "=&s"(lane)
       : "s"(ent), "s"(nearest), "s"(entry_base)
-      : "scc");
-  return amdgcn_writelane((int)e, (int)lane, stk);
-}
-
-// The same push with P = pk & 15 already formed per lane in VALU (the lead lane's pk, read with the
-// child's ref): SCC comes from that one s_and.
-__device__ __forceinline__ int push_entry_p(int stk, int& sp, uint32_t entry_base, uint32_t pk) {
-  uint32_t p, e, lane;
-  asm volatile(
-      "s_and_b32 %0, %4, 15\n\t"
-      "s_cselect_b32 %3, %1, 63\n\t"
-      "s_addc_u32 %1, %1, 0\n\t"
-      "s_or_b32 %2, %5, %0"
-      : "=&s"(p), "+s"(sp), "=&s"(e), "=&s"(lane)
-      : "s"(pk), "s"(entry_base)
       : "scc");
   return amdgcn_writelane((int)e, (int)lane, stk);
 }
@@ -464,23 +392,15 @@ __device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref
   for (int r = 0; r < R; ++r) {
     if (STATS && ray_live(hit[r])) ++cnt.tri;
     float t, u, v;
-    const bool ok = (ANY_HIT && RT_ANY_MT_BITS)
-                        ? moller_trumbore_bits(ry.o[r], ry.d[r], v3(ta.x, ta.y, ta.z), v3(tb.x, tb.y, tb.z),
-                                               v3(tc.x, tc.y, tc.z), face, t, u, v)
-                        : moller_trumbore_flat(ry.o[r], ry.d[r], v3(ta.x, ta.y, ta.z), v3(tb.x, tb.y, tb.z),
-                                               v3(tc.x, tc.y, tc.z), face, t, u, v);
+    const bool ok = moller_trumbore_flat(ry.o[r], ry.d[r], v3(ta.x, ta.y, ta.z), v3(tb.x, tb.y, tb.z),
+                                         v3(tc.x, tc.y, tc.z), face, t, u, v);
     HitRec& h = hit[r];
     // bitwise & / | (no short-circuit): no exec-mask branches around the compares (-2 %)
     // a ray that is not live has t = -inf and takes nothing; a live any-hit ray still holds
     // {tmax, ~0, ~0}, for which the (t, instance, primitive) order reduces to t <= tmax
-#if RT_KEY64
     // (instance, primitive) order as ONE unsigned 64-bit compare (v_cmp_lt_u64; the uniform side in an SGPR pair)
     const bool id_less = (((uint64_t)cur << 32) | prim) < (((uint64_t)h.inst << 32) | h.prim);
     const bool better = ANY_HIT ? (t <= h.t) : (t < h.t) | ((t == h.t) & id_less);
-#else
-    const bool better = ANY_HIT ? (t <= h.t)
-                                : (t < h.t) | ((t == h.t) & ((cur < h.inst) | ((cur == h.inst) & (prim < h.prim))));
-#endif
     const bool take = ok & (t >= tmin) & better;
     // an any-hit ray that accepts leaves the packet with t = -inf: every later slab test rejects it
     h.t = take ? (ANY_HIT ? -__builtin_inff() : t) : h.t;
@@ -525,13 +445,9 @@ __device__ __forceinline__ uint32_t packet_slabs(const f4v (&pl6)[6], const Pack
       float n, f;
       const float fzz = OCT ? thz : fmaxf(tlz, thz);
       float fz;
-#if RT_TBEST_ASM
       // min with the loop-carried t: fminf would re-canonicalise t (a v_max t, t) at every node
       // visit; t is always a quiet value (arithmetic results and +-inf), so v_min gives its bits
       asm("v_min_f32 %0, %1, %2" : "=v"(fz) : "v"(fzz), "v"(tbest));
-#else
-      fz = fminf(fzz, tbest);
-#endif
       if (OCT) {  // lo* hold the near planes, hi* the far planes
         n = fmaxf(fmaxf(tlx, tly), fmaxf(tlz, tmin));
         f = fminf(fminf(thx, thy), fz);
@@ -579,7 +495,7 @@ __device__ __forceinline__ bool packet_tlas_node(const RT_CONST char* pool, int 
   // nearest entered child by the lead ray's key, lowest slot on ties: per lane in VALU (keys
   // masked to the entered set), one readlane. Any-hit walks take the lowest entered slot.
   uint32_t ib;
-  if (ANY_HIT || (RT_TLAS_SINGLE_SKIP && (ent & (ent - 1u)) == 0u)) {  // no choice with one entered child
+  if (ANY_HIT || (ent & (ent - 1u)) == 0u) {  // no choice with one entered child
     ib = (uint32_t)__builtin_ctz(ent);
   } else {
     uint32_t idx = 0;
@@ -587,7 +503,7 @@ __device__ __forceinline__ bool packet_tlas_node(const RT_CONST char* pool, int 
     for (int r = 0; r < R; ++r) {
       uint32_t kk[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) kk[k] = RT_KEY_BFI ? key_if_entered(vkey[r][k], ent, k) : vkey[r][k] | bit_mask_v(~ent, k);
+      for (int k = 0; k < 4; ++k) kk[k] = key_if_entered(vkey[r][k], ent, k);
       const uint32_t m = min(min(kk[0], kk[1]), min(kk[2], kk[3]));
       const uint32_t ir = kk[0] == m ? 0u : kk[1] == m ? 1u : kk[2] == m ? 2u : 3u;
       idx = (r == 0 || pl.lead_r == (uint32_t)r) ? ir : idx;
@@ -750,12 +666,6 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
 #else
   (void)hybrid;
 #endif
-#if RT_OCT_BASES == 1
-  // one base per plane row, the octant's row offset folded in once per BLAS entry: each row load is
-  // then base + the node's 32-bit offset (SGPR soffset), no per-node s_or for the row offsets
-  const RT_CONST char *bnx = pool + oc.nx, *bfx = pool + oc.fx, *bny = pool + oc.ny, *bfy = pool + oc.fy,
-                      *bnz = pool + oc.nz, *bfz = pool + oc.fz;
-#endif
   while (true) {
     const RT_CONST char* nb = pool + ((uint32_t)bref << 7);
     const i8v ch = *(const RT_CONST i8v*)(nb + 96);  // child[4], count, first_inner, inner_mask, entry_base
@@ -766,14 +676,6 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
     if (OCT) {
       // one 32-bit offset per row: the scalar load takes it as its SGPR offset (no 64-bit adds)
       const uint32_t noff = (uint32_t)bref << 7;
-#if RT_OCT_BASES == 1
-      planes[0] = cld4(bnx + noff);
-      planes[1] = cld4(bfx + noff);
-      planes[2] = cld4(bny + noff);
-      planes[3] = cld4(bfy + noff);
-      planes[4] = cld4(bnz + noff);
-      planes[5] = cld4(bfz + noff);
-#elif RT_OCT_BASES == 2
       // each row at the pool base + its octant offset (SGPR soffset) + the node offset as the
       // instruction's... the node offset goes into the base once (two SALU); six s_load_dwordx4 with
       // the row offsets as soffset (the compiler would add 64-bit addresses per row itself)
@@ -790,14 +692,6 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
             "=&s"(planes[5])
           : "s"(nbo), "s"(oc.nx), "s"(oc.fx), "s"(oc.ny), "s"(oc.fy), "s"(oc.nz), "s"(oc.fz)
           : "memory");
-#else
-      planes[0] = cld4(pool + (noff + oc.nx));
-      planes[1] = cld4(pool + (noff + oc.fx));
-      planes[2] = cld4(pool + (noff + oc.ny));
-      planes[3] = cld4(pool + (noff + oc.fy));
-      planes[4] = cld4(pool + (noff + oc.nz));
-      planes[5] = cld4(pool + (noff + oc.fz));
-#endif
     } else {
 #pragma unroll
       for (int q = 0; q < 6; ++q) planes[q] = cld4(nb + 16 * q);
@@ -830,19 +724,10 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
     uint32_t tl = ent & ~imask;
     ent &= imask;
     if (tl) {
-#if RT_TRI_UNROLL
       // one test per slot with the slot's ref in a fixed SGPR (no ref-select chain, no loop)
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         if (tl & (1u << k)) packet_tri<ANY_HIT, STATS, R>(tpool, ch[k], ry, tmin, cur, face, pl, hit, cnt);
-#else
-      do {
-        const uint32_t k = (uint32_t)__builtin_ctz(tl);
-        tl &= tl - 1u;
-        const i4v c4 = {ch[0], ch[1], ch[2], ch[3]};
-        packet_tri<ANY_HIT, STATS, R>(tpool, c4[k], ry, tmin, cur, face, pl, hit, cnt);
-      } while (tl);
-#endif
       if (ANY_HIT) {  // rays can only have left the packet in a triangle test
         if (!pl.update(hit)) return false;
         // children only finished rays wanted are dropped
@@ -858,10 +743,10 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
     }
     if (ent) {
       uint32_t ib, nref;
-      if (ANY_HIT || (RT_SINGLE_SKIP && (ent & (ent - 1u)) == 0u)) {
+      if (ANY_HIT || (ent & (ent - 1u)) == 0u) {
         // occlusion rays skip the nearest-first choice (no keys, no readlane): for an occlusion ray
         // the order only decides how soon it stops; a closest-hit node with ONE entered internal
-        // child has no choice to make (RT_SINGLE_SKIP)
+        // child has no choice to make
         ib = (uint32_t)__builtin_ctz(ent);
         nref = (uint32_t)ch[5] + ib;  // internal children in the lowest slots
       } else {
@@ -874,30 +759,15 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
         for (int r = 0; r < R; ++r) {
           uint32_t kk[4];
 #pragma unroll
-          for (int k = 0; k < 4; ++k)
-            kk[k] = RT_KEY_BFI ? key_if_entered(vkey[r][k], ent, k) : vkey[r][k] | bit_mask_v(~ent, k);
+          for (int k = 0; k < 4; ++k) kk[k] = key_if_entered(vkey[r][k], ent, k);
           const uint32_t m = min(min(kk[0], kk[1]), min(kk[2], kk[3]));
           const uint32_t ir = kk[0] == m ? 0u : kk[1] == m ? 1u : kk[2] == m ? 2u : 3u;
-#if RT_PUSH_P_VALU
-          // ref << 4 | the entered internal children other than ir (VALU: the scalar unit only unpacks)
-          const uint32_t pr = (((uint32_t)ch[5] + ir) << 4) | (ent & ~(1u << ir));
-#else
           const uint32_t pr = (((uint32_t)ch[5] + ir) << 2) | ir;
-#endif
           idx = (r == 0 || pl.lead_r == (uint32_t)r) ? pr : idx;
         }
         const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)idx, (int)pl.lead_l);
-#if RT_PUSH_P_VALU
-        if (STATS && (pk & 15u) && sp + 1 > cap)  // never: cap bounds the entries (one per level)
-#pragma unroll
-          for (int r = 0; r < R; ++r) cnt.overflow += ray_live(hit[r]) ? 1u : 0u;
-        stk.v = push_entry_p(stk.v, sp, (uint32_t)ch[7], pk);
-        bref = (int)(pk >> 4);
-        continue;
-#else
         ib = pk & 3u;
         nref = pk >> 2;
-#endif
       }
       if (STATS && (ent & ~(1u << ib)) && sp + 1 > cap)  // never: cap bounds the entries (one per level)
 #pragma unroll
@@ -1325,35 +1195,13 @@ __device__ bool shadow_compact(const SceneView& sc, V3 P, V3 d, bool need, uint3
 // shade_sample for the wave-packet traversal: identical arithmetic per ray, with every trace
 // hoisted to wave-uniform control flow (rays without a trace of that kind join the packet dead).
 // Each lane shades R camera samples (R pixels) at once.
-#ifndef RT_KO_SHADE
-#define RT_KO_SHADE 0  // knock-out studies (tools/ab.py --no-check): never in a shipped build
-#endif
-#ifndef RT_KO_SHADOW
-#define RT_KO_SHADOW 0
-#endif
 #ifndef RT_WAVE_TIMES
 #define RT_WAVE_TIMES 0  // 1: every wave stores its start / end clock (diagnostics; tools/wave_times.py)
-#endif
-#ifndef RT_PRIO
-#define RT_PRIO 0  // 1: s_setprio(1) for every shadow phase; 2: by the primary walk's duration (A/B)
-#endif
-#ifndef RT_PRIO_T
-#define RT_PRIO_T 20000  // RT_PRIO 2: shader clocks of primary walk for priority 1 (2x: priority 2)
-#endif
-#ifndef RT_PHASE_TIMING
-#define RT_PHASE_TIMING 0  // 1: sampled waves printf s_memtime per phase (diagnostics only)
 #endif
 template <int MODE, bool STATS, int R>
 __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, const FrameCam& cam, const uint32_t* px,
                                     const uint32_t* py, float ox, float oy, const bool* inimg, V3* color,
                                     Counters& cnt) {
-#if RT_PHASE_TIMING
-  uint64_t ph[6];
-  ph[0] = __builtin_amdgcn_s_memtime();
-#endif
-#if RT_PRIO
-  const uint64_t t_start = __builtin_amdgcn_s_memtime();
-#endif
   V3 O[R], D[R], P[R], sd[R];
   HitRec hit[R], sh[R];
   bool found[R], occl[R], need[R];
@@ -1450,9 +1298,6 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
     }
   }
   // RT_SHADE_LAMBERT_SHADOW (MODE 1) and RT_SHADE_PRIMARY (MODE 2)
-#if RT_PHASE_TIMING
-  ph[1] = __builtin_amdgcn_s_memtime();
-#endif
   V3 n[R];
   float c[R];
 #pragma unroll
@@ -1460,35 +1305,11 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
     n[r] = v3(0.0f, 0.0f, 0.0f);
     c[r] = 0.0f;
     if (found[r]) {
-#if RT_KO_SHADE  // knock-out study only (wrong image): no hit-instance / vertex fetches
-      n[r] = neg(D[r]);
-#else
       const HitInstance ir = load_hit_instance(sc, hit[r].inst);
       n[r] = ir.hit_group == 2u ? face_world_normal(ir, hit[r].prim)
                                 : neg(interpolated_world_normal(ir, hit[r].prim, hit[r].u, hit[r].v));
-#endif
     }
   }
-#if RT_PHASE_TIMING
-  {
-    float z = 0.0f;
-#pragma unroll
-    for (int r = 0; r < R; ++r) z += n[r].x;
-    asm volatile("" ::"v"(z));  // the normals are complete here
-    ph[2] = __builtin_amdgcn_s_memtime();
-  }
-#endif
-#if RT_PRIO
-  // wave priority for the shadow walks (A/B study): waves whose primary walk was long are the
-  // launch's long waves; give them the SIMD's issue slots first
-  if (RT_PRIO == 1) {
-    __builtin_amdgcn_s_setprio(1);
-  } else {
-    const uint64_t el = __builtin_amdgcn_s_memtime() - t_start;
-    if (el > 2u * (uint64_t)RT_PRIO_T) __builtin_amdgcn_s_setprio(2);
-    else if (el > (uint64_t)RT_PRIO_T) __builtin_amdgcn_s_setprio(1);
-  }
-#endif
   for (uint32_t l = 0; l < fp.nlights; ++l) {
     const LightRec& Lr = fp.lights[l];
     float nl[R];
@@ -1501,7 +1322,7 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
       occl[r] = false;
       if (MODE == 1 && STATS && need[r]) ++cnt.shadow;
     }
-    if (MODE == 1 && !RT_KO_SHADOW) {
+    if (MODE == 1) {
       if (RT_SHADOW_COMPACT && R == 1)
         occl[0] = shadow_compact<STATS>(sc, P[0], sd[0], need[0], l & 1u, cnt);
       else
@@ -1517,11 +1338,6 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
     const float v = c[r] / (float)fp.nlights;
     color[r] = found[r] ? v3(v, v, v) : miss_color(fp, py[r]);
   }
-#if RT_PHASE_TIMING
-  ph[3] = __builtin_amdgcn_s_memtime();
-  if ((threadIdx.x & 63u) == 0 && (blockIdx.x * 7u + blockIdx.y * 13u) % 61u == 0u)
-    printf("PH %lu %lu %lu\n", ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2]);
-#endif
 }
 
 // The pixel store (RayGen.hlsl:42, gOutput = float4(color, 1) into the R8G8B8A8_UNORM UAV): frame `frame` of
@@ -1922,10 +1738,12 @@ PacketGeometry packet_geometry(const SceneView& sc, const FrameParams& fp, int s
   g.grid_x = (fp.width + tw - 1) / tw;
   g.grid_y = (fp.nrows + th - 1) / th;
   g.waves_per_frame = g.grid_x * g.grid_y * g.wl;
-  // a tile splits into 2 x 2 parts when both sides are >= 2 pixels, 4 x 4 when >= 4 (one ray per lane only; the
-  // shadow-ray compaction variant keeps whole tiles: it merges rays across a workgroup's waves)
+  // a tile splits into 2 x 2 parts when both sides are >= 2 pixels, 4 x 4 when >= 4 (one ray per lane only)
   const uint32_t side = tp < tr ? tp : tr;
   g.kmax_code = (R != 1 || RT_SHADOW_COMPACT) ? 0u : side >= 4u ? 2u : side >= 2u ? 1u : 0u;
+  // the shadow-ray compaction variant synchronises a workgroup's waves (barriers): no work list there, whose waves
+  // past its end exit early
+  g.plannable = !RT_SHADOW_COMPACT;
   return g;
 }
 
