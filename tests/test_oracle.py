@@ -431,3 +431,7 @@ def test_seam_watertightness_probe_fixture():
     for k in ("seam_edges", "rays", "hit64", "hit32", "leaks", "extra32", "same_triangle"):
         assert now[k] == fx[k], k
     assert fx["seam_edges"] == 1036 and 0 < fx["leaks"] < fx["rays"] // 10
+    # ceiling: the shipped triangle test (fused cross products, unfused dots, rt_device.hpp mt_cross /
+    # mt_dot) leaks 1,832 of the 66,304 edge rays; a change of that arithmetic may not leak more (regenerating the
+    # fixture does not lift this bound; unfused products gave 1,727, fused dots 2,514: profiles/r03_ab_mt_fma.txt)
+    assert now["leaks"] <= 1832 and fx["leaks"] <= 1832

@@ -18,10 +18,12 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--lib", required=True)
 ap.add_argument("--config", default="C2")
 ap.add_argument("--frames", type=int, default=30)
+ap.add_argument("--balance", type=int, default=1, help="rt_set_tile_balance mode (0: the plain grid)")
 a = ap.parse_args()
 spec = scenes.config(a.config)
 c = rt.Context(0, library=rt._load(a.lib))
 scenes.upload(c, spec)
+c.set_tile_balance(a.balance)
 W, H = spec.width, spec.height
 out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
 tb = torch.zeros((H * W * 4,), dtype=torch.float32, device="cuda")
@@ -41,7 +43,8 @@ base = t0.min()
 t0 -= base
 t1 -= base
 T = t1.max()
-print(f"{a.config}: {len(u)} waves, frame {T * 10 / 1000:.1f} us (100 MHz clock)")
+print(f"{a.config}: {len(u)} waves, frame {T * 10 / 1000:.1f} us (100 MHz clock), tile balance {a.balance}: "
+      f"{c.tile_balance_info()}")
 dur = (t1 - t0) * 10 / 1000
 print(f"wave duration us: mean {dur.mean():.2f} p50 {np.median(dur):.2f} p90 {np.percentile(dur, 90):.2f} "
       f"max {dur.max():.2f}")
@@ -59,5 +62,5 @@ for x in range(8):
     m = xcc == x
     if m.any():
         print(f"XCC {x}: waves {m.sum()} last end {t1[m].max() * 10 / 1000:.1f} us mean dur {dur[m].mean():.2f} us")
-np.savez(os.path.join(ROOT, "gpurun_out", f"wt_{a.config}.npz"), t0=t0, t1=t1, ids=np.nonzero(live)[0], xcc=xcc)
+np.savez(os.path.join(ROOT, "gpurun_out", f"wt_{a.config}_b{a.balance}.npz"), t0=t0, t1=t1, ids=np.nonzero(live)[0], xcc=xcc)
 c.close()
