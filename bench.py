@@ -834,8 +834,10 @@ def main(argv=None) -> int:
     names = a.extra if a.extra is not None else ("C4,C5" if distributed else "C1,C2F,C3,C4,C5,REF")
     for name in [n for n in names.split(",") if n]:
         es = spec_of(name)
-        # few frames: C5 is ~8 ms per frame on one GPU
-        n_steps = max(3, a.steps // (20 if es.spp > 1 else 4))
+        # at least 50 frames (10 at 4 spp: C5 is ~4.4 ms per frame on one GPU): with the driver's 20 steps a quarter
+        # of them was 5 frames, 70 us of C1, where the host's issue and synchronise dominated (C1 / C2F read 24-46 %
+        # below their 200-step rates in BENCH_r03.json)
+        n_steps = max(10, a.steps // 20) if es.spp > 1 else max(50, a.steps // 4)
         x = run_config(be, es, world, rank, n_steps, 2, 0.0, strips, not a.no_pipeline, a.schedule,
                        in_flight=a.in_flight, resettle_ms=a.resettle_ms, frames_per_gather=a.frames_per_gather,
                        frames_per_launch=a.frames_per_launch, loopback=a.loopback,

@@ -377,14 +377,13 @@ rt_status issue_tail_job(rt_comm* c, const Job& j) {
       if (hipEventRecord(o.asm_order, o.asm_stream) != hipSuccess || hipStreamWaitEvent(j.rs, o.asm_order, 0) != hipSuccess)
         return cfail(c, RT_E_HIP, "rt_render_strips: order after an assembly into the same frame");
     }
-    // rank r's block of the gathered slot holds its strips of every frame in turn: frame b starts b frames into it
+    // rank r's block of the gathered slot holds its strips of every frame in turn: frame b starts b frames into it;
+    // the slot's frames are assembled by one launch
     const size_t frame_bytes = (size_t)j.rows_per_rank * j.W * kStripBpp;
-    for (uint32_t b = 0; b < j.nframes; ++b) {
-      const hipError_t e = rt::launch_assemble_strips(j.W, j.H, c->nranks, j.strip, (const char*)s.gathered + b * frame_bytes,
-                                                      j.frame_out[b], j.rs, j.nframes * j.rows_per_rank, kStripBpp);
-      if (e != hipSuccess) return cfail(c, RT_E_HIP, std::string("rt_render_strips: assembly: ") + hipGetErrorString(e));
-      s.asm_frames[b] = j.frame_out[b];
-    }
+    const hipError_t e = rt::launch_assemble_frames(j.W, j.H, c->nranks, j.strip, s.gathered, j.frame_out, j.nframes,
+                                                    frame_bytes, j.rs, j.nframes * j.rows_per_rank, kStripBpp);
+    if (e != hipSuccess) return cfail(c, RT_E_HIP, std::string("rt_render_strips: assembly: ") + hipGetErrorString(e));
+    for (uint32_t b = 0; b < j.nframes; ++b) s.asm_frames[b] = j.frame_out[b];
     s.asm_stream = j.rs;
     s.asm_n = j.nframes;
   }

@@ -117,6 +117,11 @@ hipError_t launch_trace_rays(const SceneView& scene, const float* rays, uint32_t
 hipError_t launch_assemble_strips(uint32_t W, uint32_t H, uint32_t nranks, uint32_t strip_rows,
                                   const void* gathered, void* out, hipStream_t stream, uint32_t rank_stride_rows = 0,
                                   uint32_t in_bpp = 4);
+// The frames of a batched gather: frame b's strips start b x frame_bytes into every rank's block of `gathered`
+// (rank stride rank_stride_rows rows); RGB8 strips of a 4-aligned width go in ONE launch (grid z = frame).
+hipError_t launch_assemble_frames(uint32_t W, uint32_t H, uint32_t nranks, uint32_t strip_rows, const void* gathered,
+                                  void* const* outs, uint32_t nframes, size_t frame_bytes, hipStream_t stream,
+                                  uint32_t rank_stride_rows, uint32_t in_bpp);
 
 // --- Raster fallback (rt_raster.hip) -------------------------------------------------------
 

@@ -1672,12 +1672,18 @@ __global__ __launch_bounds__(256) void k_assemble16(uint32_t W4, uint32_t H, uin
 }
 
 // The same from RGB8 strips: 4 pixels = 12 B (three dwords, 4-B aligned: a strip row is 3 W bytes with W % 4 == 0)
-// in, 16 B out with the alpha bytes set. Dwords a, b, c hold r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3.
+// in, 16 B out with the alpha bytes set. Dwords a, b, c hold r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3. The frames of
+// a batched gather in one launch (grid z = frame b: its strips frame_words x b words into every rank's block).
+struct AsmFrames {
+  uint4* out[kMaxLaunchFrames];
+};
 __global__ __launch_bounds__(256) void k_assemble16_rgb(uint32_t W4, uint32_t H, uint32_t nranks, uint32_t strip_rows,
-                                                        const uint32_t* __restrict__ in, uint4* __restrict__ out,
-                                                        uint32_t rows_per_rank) {
+                                                        const uint32_t* __restrict__ in_all, AsmFrames outs,
+                                                        uint32_t rows_per_rank, uint32_t frame_words) {
   const uint32_t x = blockIdx.x * 256u + threadIdx.x;
   if (x >= W4) return;
+  const uint32_t* in = in_all + (size_t)blockIdx.z * frame_words;
+  uint4* out = outs.out[blockIdx.z];
   const uint32_t y0 = blockIdx.y * kAsmRows;
 #pragma unroll
   for (uint32_t i = 0; i < kAsmRows; ++i) {
@@ -1929,26 +1935,43 @@ hipError_t launch_trace_rays(const SceneView& sc, const float* rays, uint32_t n,
 hipError_t launch_assemble_strips(uint32_t W, uint32_t H, uint32_t nranks, uint32_t strip_rows,
                                   const void* gathered, void* out, hipStream_t s, uint32_t rank_stride_rows,
                                   uint32_t in_bpp) {
+  return launch_assemble_frames(W, H, nranks, strip_rows, gathered, &out, 1, 0, s, rank_stride_rows, in_bpp);
+}
+
+hipError_t launch_assemble_frames(uint32_t W, uint32_t H, uint32_t nranks, uint32_t strip_rows, const void* gathered,
+                                  void* const* outs, uint32_t nframes, size_t frame_bytes, hipStream_t s,
+                                  uint32_t rank_stride_rows, uint32_t in_bpp) {
   const uint32_t nstrips = (H + strip_rows - 1) / strip_rows;
   const uint32_t strips_per_rank = (nstrips + nranks - 1) / nranks;
   const uint32_t rows_per_rank = rank_stride_rows ? rank_stride_rows : strips_per_rank * strip_rows;  // rank stride
-  if (in_bpp != 3u && in_bpp != 4u) return hipErrorInvalidValue;
-  const uintptr_t align = (uintptr_t)gathered % (in_bpp == 4u ? 16u : 4u) | (uintptr_t)out % 16u;
-  if (W % 4 == 0 && align == 0) {
+  if ((in_bpp != 3u && in_bpp != 4u) || nframes == 0 || nframes > (uint32_t)kMaxLaunchFrames) return hipErrorInvalidValue;
+  uintptr_t align = ((uintptr_t)gathered | (uintptr_t)frame_bytes) % (in_bpp == 4u ? 16u : 4u);
+  for (uint32_t b = 0; b < nframes; ++b) align |= (uintptr_t)outs[b] % 16u;
+  if (W % 4 == 0 && align == 0 && in_bpp == 3u) {  // the strips of rt_comm: every frame of the batch in one launch
     const uint32_t W4 = W / 4;
-    dim3 grid((W4 + 255) / 256, (H + kAsmRows - 1) / kAsmRows);
-    if (in_bpp == 4u)
-      hipLaunchKernelGGL(k_assemble16, grid, dim3(256), 0, s, W4, H, nranks, strip_rows, (const uint4*)gathered,
-                         (uint4*)out, rows_per_rank);
-    else
-      hipLaunchKernelGGL(k_assemble16_rgb, grid, dim3(256), 0, s, W4, H, nranks, strip_rows, (const uint32_t*)gathered,
-                         (uint4*)out, rows_per_rank);
+    AsmFrames f{};
+    for (uint32_t b = 0; b < nframes; ++b) f.out[b] = (uint4*)outs[b];
+    dim3 grid((W4 + 255) / 256, (H + kAsmRows - 1) / kAsmRows, nframes);
+    hipLaunchKernelGGL(k_assemble16_rgb, grid, dim3(256), 0, s, W4, H, nranks, strip_rows, (const uint32_t*)gathered,
+                       f, rows_per_rank, (uint32_t)(frame_bytes / 4));
     return hipGetLastError();
   }
-  dim3 grid((W + 255) / 256, H);
-  hipLaunchKernelGGL(k_assemble, grid, dim3(256), 0, s, W, H, nranks, strip_rows, (const uint8_t*)gathered,
-                     (uint32_t*)out, rows_per_rank, in_bpp);
-  return hipGetLastError();
+  for (uint32_t b = 0; b < nframes; ++b) {
+    const char* in = (const char*)gathered + b * frame_bytes;
+    if (W % 4 == 0 && align == 0) {
+      const uint32_t W4 = W / 4;
+      dim3 grid((W4 + 255) / 256, (H + kAsmRows - 1) / kAsmRows);
+      hipLaunchKernelGGL(k_assemble16, grid, dim3(256), 0, s, W4, H, nranks, strip_rows, (const uint4*)in,
+                         (uint4*)outs[b], rows_per_rank);
+    } else {
+      dim3 grid((W + 255) / 256, H);
+      hipLaunchKernelGGL(k_assemble, grid, dim3(256), 0, s, W, H, nranks, strip_rows, (const uint8_t*)in,
+                         (uint32_t*)outs[b], rows_per_rank, in_bpp);
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace rt
