@@ -1108,7 +1108,7 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
       bool hit;
       plan_slot = ring_acquire(c->plans, s, nullptr, &hit, &be);
       if (be != hipSuccess) return hip_fail(c, be, "tile balance: order after in-flight launches");
-      HIPCHK(c, slot_reserve(*plan_slot, ((size_t)plan_items + 1) * 4), "hipMalloc(tile plan)");
+      HIPCHK(c, slot_reserve(*plan_slot, ((size_t)plan_items + ntiles + 1) * 4), "hipMalloc(tile plan)");
       rt::PlanArgs a;
       a.cost = m->cost;
       a.plan = (uint32_t*)plan_slot->buf;

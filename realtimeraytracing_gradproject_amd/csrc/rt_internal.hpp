@@ -96,7 +96,8 @@ struct PlanStats {
 };
 struct PlanArgs {
   const uint32_t* cost;   // per wave slot of the plain grid: the last launch's wave time (ticks)
-  uint32_t* plan;         // out: [0] item count, [1 ..] items (1 + ntiles + extra_cap words)
+  uint32_t* plan;         // out: [0] item count, [1 ..] items (ntiles + extra_cap words), then this launch's
+                          // snapshot of the costs (ntiles words): 1 + 2 ntiles + extra_cap words in all
   PlanStats* stats;       // host-mapped, or null
   uint32_t ntiles;        // wave slots of the plain grid, every frame of the launch
   uint32_t extra_cap;     // items beyond ntiles the launch's grid has waves for

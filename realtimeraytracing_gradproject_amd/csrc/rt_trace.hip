@@ -1828,12 +1828,17 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
   __shared__ uint32_t s_hist[kPlanBuckets], s_off[kPlanBuckets];
   const uint32_t tid = threadIdx.x, n = a.ntiles;
   if (tid < kPlanBuckets) s_hist[tid] = 0u;
+  // the costs are read ONCE into this launch's own snapshot (after the items): launches of the same shape on other
+  // streams write them meanwhile (frames in flight), and every pass below must see the same values, or the
+  // histogram and the scatter would disagree about the items
+  uint32_t* snap = a.plan + 1u + n + a.extra_cap;
   uint64_t T = ~0ull, mx = 0, sum = 0;
   uint32_t want = 0;
   if (!a.force) {
     uint64_t lsum = 0, lmax = 0;
     for (uint32_t t = tid; t < n; t += kPlanThreads) {
-      const uint64_t c = a.cost[t];
+      const uint32_t c = a.cost[t];
+      snap[t] = c;
       lsum += c;
       lmax = c > lmax ? c : lmax;
     }
@@ -1854,18 +1859,18 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
     // the parts must fit the grid's budget: raise T until they do (the first count is the demand, reported)
     for (int iter = 0; iter < 24; ++iter) {
       uint64_t ex = 0;
-      for (uint32_t t = tid; t < n; t += kPlanThreads) ex += split_parts(plan_code(a.cost[t], T, a.kmax_code)) - 1u;
+      for (uint32_t t = tid; t < n; t += kPlanThreads) ex += split_parts(plan_code(snap[t], T, a.kmax_code)) - 1u;
       ex = block_sum64(ex, s_red);
       if (iter == 0) want = (uint32_t)(ex < 0xffffffffull ? ex : 0xffffffffull);
       if (ex <= a.extra_cap) break;
-      T += T / 4u + 1u;
+      T = iter < 23 ? T + T / 4u + 1u : ~0ull;  // the last resort: no tile split
     }
   }
   __syncthreads();
   // histogram of the items by estimated time: bucket 0 the longest
   uint32_t nsplit = 0;
   for (uint32_t t = tid; t < n; t += kPlanThreads) {
-    const uint64_t c = a.force ? 0u : a.cost[t];
+    const uint64_t c = a.force ? 0u : snap[t];
     const uint32_t code = a.force ? plan_forced(a, t) : plan_code(c, T, a.kmax_code);
     const uint64_t e = plan_est(c, code);
     const uint32_t b = mx ? (uint32_t)(((mx - (e < mx ? e : mx)) * kPlanBuckets) / (mx + 1u)) : kPlanBuckets - 1u;
@@ -1879,18 +1884,20 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
       s_off[b] = run;
       run += s_hist[b];
     }
-    a.plan[0] = run;  // the item count (the trace waves past it exit)
+    a.plan[0] = run < n + a.extra_cap ? run : n + a.extra_cap;  // the item count (the trace waves past it exit)
   }
   __syncthreads();
   // scatter (the order inside a bucket is whatever the atomics give: only the schedule depends on it)
+  const uint32_t cap = n + a.extra_cap;  // the items the buffer (and the launch's grid) has room for
   for (uint32_t t = tid; t < n; t += kPlanThreads) {
-    const uint64_t c = a.force ? 0u : a.cost[t];
+    const uint64_t c = a.force ? 0u : snap[t];
     const uint32_t code = a.force ? plan_forced(a, t) : plan_code(c, T, a.kmax_code);
     const uint64_t e = plan_est(c, code);
     const uint32_t b = mx ? (uint32_t)(((mx - (e < mx ? e : mx)) * kPlanBuckets) / (mx + 1u)) : kPlanBuckets - 1u;
     const uint32_t k = split_parts(code);
     const uint32_t pos = atomicAdd(&s_off[b], k);
-    for (uint32_t q = 0; q < k; ++q) a.plan[1u + pos + q] = (t << 6) | (q << 2) | code;
+    for (uint32_t q = 0; q < k; ++q)
+      if (pos + q < cap) a.plan[1u + pos + q] = (t << 6) | (q << 2) | code;  // always true: the budget holds
   }
   // summary for the host (host-mapped memory: read at a later dispatch, no copy call)
   nsplit = (uint32_t)block_sum64(nsplit, s_red);
