@@ -151,6 +151,29 @@ def test_bvh_image_equals_bruteforce(name):
     assert np.array_equal(a32, b32) and np.array_equal(a8, b8)
 
 
+@pytest.mark.parametrize("name,size", [("C2", (480, 270)), ("C2F", (480, 270)), ("C3", (320, 180)),
+                                       ("C4", (320, 180)), ("REF", (320, 180)), ("DEGEN", (256, 144))])
+def test_packet_schedule_image_equals_per_ray(name, size):
+    """The packet emulation (the device's default schedule) renders the per-ray schedule's image (which equals brute
+    force above) on larger frames and a seeded camera sweep around each scene: the slab test's conservative widening
+    holds on every ray. (This test refuted the far-plane prescale of VERDICT r3 #5: with the widening folded into
+    pre-scaled far-plane terms, three DEGEN shadow rays at 256 x 144 lost their occluder)"""
+    base = scenes.config(name) if name != "DEGEN" else scenes.degenerate_scene()
+    spec = base.with_size(*size)
+    o = oracle.Scene(spec)
+    a8, a32, _ = o.render_spec(spec, nthreads=8, want_float=True, schedule=0)
+    b8, b32, _ = o.render_spec(spec, nthreads=8, want_float=True, schedule=1)
+    assert np.array_equal(a32, b32) and np.array_equal(a8, b8), name
+    rng = np.random.default_rng(0x5EED + len(name))
+    for _ in range(3):
+        eye = tuple(float(x) for x in rng.uniform(-1, 1, 3) * [12, 6, 12] + [0, 7, 0])
+        sp = base.with_size(160, 90)
+        sp.camera = (eye, tuple(float(x) for x in rng.uniform(-1, 1, 3) * [2, 1, 2]), (0.0, 1.0, 0.0))
+        a8, _, _ = o.render_spec(sp, nthreads=8, want_float=False, schedule=0)
+        b8, _, _ = o.render_spec(sp, nthreads=8, want_float=False, schedule=1)
+        assert np.array_equal(a8, b8), (name, eye)
+
+
 def random_rays(n, seed):
     rng = np.random.default_rng(seed)
     o = rng.normal(size=(n, 3))
