@@ -225,6 +225,9 @@ class HipBackend:
     def set_tile_rows(self, rows: int):
         self.ctx.set_tile_rows(rows)
 
+    def tile_balance(self) -> dict:
+        return self.ctx.tile_balance_info()
+
     def sync_event(self):
         """Render/gather hand-off of the strips loop: rt_event_* (no timestamp, no system-scope
         fence: ~3 us less per record than a torch.cuda.Event on the frame's critical path)."""
@@ -597,8 +600,11 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
     fpg = rcomm.batch if rcomm is not None else None
     if rcomm is not None:
         rcomm.close()
+    # the tile balance of this rank's last launch shape (rt_tile_balance_info: plans run, tiles split, ...)
+    tb = be.tile_balance() if hasattr(be, "tile_balance") else None
     return {"rays_step": rays_step, "primary": int(counts[1].item()), "shadow": int(counts[2].item()), "fpg": fpg,
             "fpl": fpl if native else None, "latency_ms": latency_ms, "loopback": loopback if native else 0,
+            "tile_balance": tb,
             "tmax": tmax, "kernel_ms": kernel_ms, "stats": st, "build": build, "rows_local": len(rows) if strips else H,
             "tile_rows": tile_rows, "tile_ms": tile_ms, "in_flight": nstream, "in_flight_ms": flight_ms,
             "strips_loop": ("rt_render_strips_frames (C-ABI: render RGB8 strips -> "
@@ -851,6 +857,7 @@ def main(argv=None) -> int:
                           "n_gpus": world, "parallelism": f"strips{world}+gather" if strips else f"frames{world}",
                           "tile_rows": x["tile_rows"], "frames_in_flight": x["in_flight"],
                           "frame_latency_ms": None if x["latency_ms"] is None else round(x["latency_ms"], 4),
+                          "tile_balance": x["tile_balance"],
                           "aabb_tests_per_ray_rank0": round(st["aabb_tests"] / rays, 2) if not distributed else None,
                           "node_fetches": int(st["node_fetches"]), "tri_fetches": int(st["tri_fetches"])})
     if not distributed and (a.extra is None) and isinstance(be, HipBackend):
@@ -896,6 +903,7 @@ def main(argv=None) -> int:
                        # this is SURVEY 8(d)'s frame latency: enqueue -> complete)
                        "frame_ms_one_stream": round(r["kernel_ms"], 4),
                        "frame_ms_one_stream_is_latency": not strips,
+                       "tile_balance": r["tile_balance"],
                        "settle_ms": a.settle_ms, "resettle_ms": a.resettle_ms},
             "roofline": rf,
             "cpu_baseline": cpu,
