@@ -573,6 +573,7 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
     # included; the reference's frame time spans submit -> fence, D3D12HelloTriangle.cpp:436-470): strips mode, one
     # frame per gather, one frame at a time, host clock from the call to the synchronised drain; rank 0's median
     latency_ms = None
+    fpg = rcomm.batch if rcomm is not None else None  # the timed loop's (the latency pass below gathers 1 frame)
     if strips and latency_frames > 0:
         if rcomm is not None:
             rcomm.set_batch(1)
@@ -597,7 +598,6 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
             rcomm.synchronize()
         img = frame[last] if strips else local[last][:H]
         np.save(save_image, img.cpu().numpy())
-    fpg = rcomm.batch if rcomm is not None else None
     if rcomm is not None:
         rcomm.close()
     # the tile balance of this rank's last launch shape (rt_tile_balance_info: plans run, tiles split, ...)
