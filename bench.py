@@ -605,7 +605,7 @@ def run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_
     return {"rays_step": rays_step, "primary": int(counts[1].item()), "shadow": int(counts[2].item()), "fpg": fpg,
             "fpl": fpl if native else None, "latency_ms": latency_ms, "loopback": loopback if native else 0,
             "tile_balance": tb,
-            "tmax": tmax, "kernel_ms": kernel_ms, "stats": st, "build": build, "rows_local": len(rows) if strips else H,
+            "tmax": tmax, "kernel_ms": kernel_ms, "stats": st, "build": build, "rows_local": len(rows) if rows is not None else H,
             "tile_rows": tile_rows, "tile_ms": tile_ms, "in_flight": nstream, "in_flight_ms": flight_ms,
             "strips_loop": ("rt_render_strips_frames (C-ABI: render RGB8 strips -> "
                             + (f"loopback gather of {loopback} emulated ranks" if loopback else "ncclGather")
