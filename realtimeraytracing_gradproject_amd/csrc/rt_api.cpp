@@ -197,7 +197,7 @@ hipError_t note_reader(TlasVersion& v, hipStream_t s) {
 struct BalanceMap {
   uint32_t W = 0, nrows = 0, nframes = 0, tile_rows = 0, spp = 0, ntiles = 0;
   const uint32_t* rows = nullptr;
-  uint32_t* cost = nullptr;          // device: ntiles wave times (s_memrealtime ticks)
+  uint32_t* cost = nullptr;          // device: 2 words per tile (whole wave time, costliest part; PlanArgs)
   rt::PlanStats* stats = nullptr;    // host-mapped, written by k_tile_plan
   rt::PlanStats* stats_dev = nullptr;
   uint32_t extra_cap = 0;
@@ -246,6 +246,9 @@ struct rt_ctx {
   // tile balance (rt_set_tile_balance): 0 off, 1 adaptive, 2 / 3 / 4 forced layouts (tests); one cost map per launch
   // shape (least recently used of kMaxBalanceMaps replaced); the work lists, one per launch in flight, from a ring
   int balance = 1;
+  // the adaptive plan's split of costly tiles and its front class (PlanArgs::split, front; A/B diagnostics:
+  // RT_BALANCE_SPLIT, RT_BALANCE_FRONT at context creation) and the list's cover check (RT_BALANCE_CHECK, tests)
+  uint32_t bal_split = 1, bal_front = 8, bal_check = 0;
   static constexpr size_t kMaxBalanceMaps = 16;
   std::vector<BalanceMap> bal;
   uint64_t bal_clock = 0;
@@ -459,6 +462,9 @@ rt_status rt_create(int hip_device, rt_ctx_t* out) {
   rt_ctx* c = new (std::nothrow) rt_ctx();
   if (!c) return RT_E_OOM;
   c->device = hip_device;
+  if (const char* ev = std::getenv("RT_BALANCE_SPLIT")) c->bal_split = std::strtoul(ev, nullptr, 10) ? 1u : 0u;
+  if (const char* ev = std::getenv("RT_BALANCE_FRONT")) c->bal_front = (uint32_t)std::strtoul(ev, nullptr, 10);
+  if (const char* ev = std::getenv("RT_BALANCE_CHECK")) c->bal_check = std::strtoul(ev, nullptr, 10) ? 1u : 0u;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&c->d_stats, RT_STAT_COUNT * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(c->d_stats, 0, RT_STAT_COUNT * sizeof(unsigned long long)) != hipSuccess) {
@@ -795,9 +801,9 @@ rt_status rt_set_tile_balance(rt_ctx_t c, int mode) {
   return RT_OK;
 }
 
-rt_status rt_tile_balance_info(rt_ctx_t c, uint32_t out[8]) {
+rt_status rt_tile_balance_info(rt_ctx_t c, uint32_t out[12]) {
   if (!c || !out) return RT_E_INVALID;
-  std::memset(out, 0, 8 * sizeof(uint32_t));
+  std::memset(out, 0, 12 * sizeof(uint32_t));
   const BalanceMap* m = c->bal_last;
   if (!m || !m->stats) return RT_OK;
   const volatile rt::PlanStats* st = m->stats;
@@ -809,6 +815,10 @@ rt_status rt_tile_balance_info(rt_ctx_t c, uint32_t out[8]) {
   out[5] = st->mean_cost;
   out[6] = st->threshold;
   out[7] = (uint32_t)std::min<uint64_t>(m->launches, 0xffffffffu);
+  out[8] = st->pays;
+  out[9] = st->bad;
+  out[10] = st->first_bad_tile;
+  out[11] = st->first_bad_word;
   return RT_OK;
 }
 
@@ -1015,8 +1025,8 @@ static BalanceMap* balance_map(rt_ctx* c, uint32_t W, uint32_t nrows, const uint
   m->ntiles = ntiles;
   m->extra_cap = ntiles / 4u + 64u;
   m->tick = ++c->bal_clock;
-  if ((*err = hipMalloc(&m->cost, (size_t)ntiles * 4)) != hipSuccess ||
-      (*err = hipMemsetAsync(m->cost, 0, (size_t)ntiles * 4, s)) != hipSuccess ||
+  if ((*err = hipMalloc(&m->cost, (size_t)ntiles * 8)) != hipSuccess ||
+      (*err = hipMemsetAsync(m->cost, 0, (size_t)ntiles * 8, s)) != hipSuccess ||
       (*err = hipHostMalloc((void**)&m->stats, sizeof(rt::PlanStats), hipHostMallocMapped)) != hipSuccess) {
     m->release();
     return nullptr;
@@ -1030,15 +1040,15 @@ static BalanceMap* balance_map(rt_ctx* c, uint32_t W, uint32_t nrows, const uint
 }
 
 // Whether this launch runs the plan kernel (adaptive mode): not before the shape has wave times; every launch while
-// the last plan saw a costliest tile above 2.5 x the mean (the slowest tiles set the frame time); else one launch
-// in 16 re-checks. The summary is read from host-mapped memory without a copy call (it may lag by a few launches).
+// the last plan found the costliest tile above the load bound (the slowest tiles form the launch's tail); else one
+// launch in 16 re-checks. The summary is read from host-mapped memory without a copy call (it may lag by a few
+// launches).
 static bool balance_wants_plan(BalanceMap& m) {
   const volatile rt::PlanStats* st = m.stats;
-  const uint32_t plans = st->plans, mx = st->max_cost, mean = st->mean_cost, want = st->want_extra;
+  const uint32_t plans = st->plans, want = st->want_extra;
   if (plans) m.extra_cap = std::min<uint64_t>((uint64_t)want + want / 4u + 64u, 15ull * m.ntiles);
   if (m.launches == 0) return false;
-  if (plans == 0) return true;
-  if ((uint64_t)mx * 2u > (uint64_t)mean * 5u) return true;
+  if (plans == 0 || st->pays) return true;
   return m.launches % 16u == 0u;
 }
 
@@ -1094,8 +1104,12 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
   uint32_t plan_items = 0;
   ScratchSlot* plan_slot = nullptr;
   const bool forced = c->balance >= 2;
+  if (forced && (uint64_t)g.waves_per_frame * nframes > rt::kPlanMaxTiles)
+    return fail(c, RT_E_UNSUPPORTED, "tile balance: forced layouts take at most 32768 waves per launch");
+  // launches of more waves than the plan kernel holds run the plain grid (they are many rounds of the GPU's wave
+  // slots deep: the slowest tile is a small part of them, C5's 518,400 waves)
   if (c->balance && g.packet && g.plannable && (forced || !c->stats_on) &&
-      (uint64_t)g.waves_per_frame * nframes < (1ull << 26)) {
+      (uint64_t)g.waves_per_frame * nframes <= rt::kPlanMaxTiles) {
     const uint32_t ntiles = g.waves_per_frame * nframes;
     hipError_t be;
     BalanceMap* m = balance_map(c, W, nrows, d_rows, nframes, ntiles, s, &be);
@@ -1108,7 +1122,7 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
       bool hit;
       plan_slot = ring_acquire(c->plans, s, nullptr, &hit, &be);
       if (be != hipSuccess) return hip_fail(c, be, "tile balance: order after in-flight launches");
-      HIPCHK(c, slot_reserve(*plan_slot, ((size_t)plan_items + ntiles + 1) * 4), "hipMalloc(tile plan)");
+      HIPCHK(c, slot_reserve(*plan_slot, ((size_t)plan_items + 2u * ntiles + 1) * 4), "hipMalloc(tile plan)");
       rt::PlanArgs a;
       a.cost = m->cost;
       a.plan = (uint32_t*)plan_slot->buf;
@@ -1118,6 +1132,10 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
       a.slots = 7u * 1024u;  // the LAMBERT_SHADOW kernel's 7 waves per SIMD x 1024 SIMDs
       a.kmax_code = g.kmax_code;
       a.force = forced ? (uint32_t)(c->balance - 1) : 0u;
+      a.split = c->bal_split;
+      a.front = c->bal_front;
+      a.check = c->bal_check;
+      a.min_gain = 1000u;  // 10 us: above the plan kernel's own time
       a.waves_per_frame = g.waves_per_frame;
       a.grid_x = g.grid_x;
       a.wx = g.wx;

@@ -92,20 +92,30 @@ PacketGeometry packet_geometry(const SceneView& sc, const FrameParams& fp, int s
 
 // Tile balance (k_tile_plan): the summary the plan kernel leaves in host-mapped memory for the next dispatches.
 struct PlanStats {
-  uint32_t nitems, nsplit, want_extra, max_cost, mean_cost, threshold, plans, pad;
+  uint32_t nitems, nsplit, want_extra, max_cost, mean_cost, threshold, plans;
+  uint32_t pays;  // the last plan found the costliest tile above the load bound (its list is not the plain order)
+  // PlanArgs::check: tiles whose items were not exactly one layout's parts, summed over the plans; the first one
+  uint32_t bad, first_bad_tile, first_bad_word;
 };
 struct PlanArgs {
-  const uint32_t* cost;   // per wave slot of the plain grid: the last launch's wave time (ticks)
-  uint32_t* plan;         // out: [0] item count, [1 ..] items (ntiles + extra_cap words), then this launch's
-                          // snapshot of the costs (ntiles words): 1 + 2 ntiles + extra_cap words in all
+  uint32_t* cost;         // per wave slot of the plain grid, 2 words: the last whole wave's time (ticks), the
+                          // costliest part of the last split (time << 2 | layout; cleared here when splitting)
+  uint32_t* plan;         // out: [0] item count, [1 ..] items (ntiles + extra_cap words), then the cover check's
+                          // scratch (2 ntiles words): 1 + 3 ntiles + extra_cap words in all
   PlanStats* stats;       // host-mapped, or null
   uint32_t ntiles;        // wave slots of the plain grid, every frame of the launch
   uint32_t extra_cap;     // items beyond ntiles the launch's grid has waves for
   uint32_t slots;         // wave slots of the GPU for the trace kernel (waves per SIMD x SIMDs)
   uint32_t kmax_code;
   uint32_t force;         // 0 adaptive; 1 / 2 / 3 forced layouts (tests)
+  uint32_t split;         // adaptive: split tiles (0: order only)
+  uint32_t front;         // adaptive: items estimated above front / 16 x the load bound go first (0: tile order)
+  uint32_t check;         // diagnostics: verify the list covers every tile once (PlanStats::bad)
+  uint32_t min_gain;      // adaptive: ticks the costliest tile must outlast the load bound by (the plan's own time)
   uint32_t waves_per_frame, grid_x, wx, wy, wl;
 };
+// one workgroup holding the costs in registers: launches of at most kPlanMaxTiles wave slots
+constexpr uint32_t kPlanMaxTiles = 32u * 1024u;
 hipError_t launch_tile_plan(const PlanArgs& a, hipStream_t stream);
 
 hipError_t launch_trace_rays(const SceneView& scene, const float* rays, uint32_t n, bool any_hit, bool cull,

@@ -1507,11 +1507,7 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
   } else {
     slot = ((bz * gridDim.y + by) * gridDim.x + bx) * WL + w;
   }
-  if (fp.cost) {
-    t_wave = __builtin_amdgcn_s_memrealtime();
-    // the first part of a split tile restarts the tile's estimate (the parts raise it with atomicMax at their end)
-    if (split && part == 0u && lane == 0u) fp.cost[slot] = 0u;
-  }
+  if (fp.cost) t_wave = __builtin_amdgcn_s_memrealtime();
   const uint32_t sample = lane % NS, pix = lane / NS;
   // split tiles: only the lanes of this part's sub-rectangle of the pixel tile trace (2 x 2 or 4 x 4 parts;
   // the others join the packets dead and store nothing)
@@ -1585,11 +1581,12 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
   }
   if (STATS) flush_stats<true>(cnt, stats);
   if (fp.cost && lane == 0u) {
-    // this wave's time (100 MHz ticks); a part's time scaled to an estimate of its whole tile (the
-    // costliest part of a split tile takes about 0.55 (4 parts) / 0.35 (16) of the whole: split_parts)
-    const uint32_t dt = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_wave);
-    if (split == 0u) fp.cost[slot] = dt;
-    else atomicMax(fp.cost + slot, split == 1u ? (dt * 29u) >> 4 : (dt * 46u) >> 4);
+    // this wave's time (100 MHz ticks): a whole tile's into its first word, a part's into the second as the
+    // costliest part of the tile's last split (time << 2 | layout; the plan kernel clears it when it splits)
+    uint32_t dt = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_wave);
+    dt = dt < (1u << 30) ? dt : (1u << 30) - 1u;
+    if (split == 0u) fp.cost[2u * slot] = dt;
+    else atomicMax(fp.cost + 2u * slot + 1u, (dt << 2) | split);
   }
 #if RT_WAVE_TIMES
   // diagnostics only: (start, end) of this wave on the 100 MHz clock + its XCC / CU ids, into the
@@ -1779,18 +1776,23 @@ hipError_t launch_trace_frame(const SceneView& sc, const FrameParams& fp, const 
 // ------------------------------------------------------------------------------------------
 // Tile balance: the wave work list of one launch (k_tile_plan, one workgroup). A frame lasts as long as its
 // slowest tiles (a wave walks the union of its 64 rays' paths; on C4 one 8 x 8 tile takes as long as the rest of
-// the frame, profiles/r03_wave_times_C4.txt). From the per-tile wave times of the last launch of this shape
-// (FrameParams::cost), the load bound L = summed time / the GPU's wave slots and the threshold T = max(L, 0.35 x
-// the costliest tile): a tile above T is traced as 4 parts (2 x 2 sub-rectangles) when 0.55 x its time fits T,
-// else as 16; then every item is dealt longest first (a counting sort into kPlanBuckets classes of estimated
-// time), so the long waves start at the front of the launch instead of forming its tail. The list is always a
-// valid cover (each tile once, or each of its parts once) whatever the costs hold: the image never depends on it,
-// only the schedule. Items beyond the grid's budget are refused by raising T. (tools/split_study.py models the
-// rule on the oracle's packet fetches: C4 whole frame 0.71, rank 0's share at N = 4 / 8 0.45 / 0.48 of the plain
-// grid's time.) The north star's "wavefront ballot/prefix-sum" appears here as the block scan of the buckets.
+// the frame, profiles/r03_wave_times_C4.txt). The packet kernel leaves two words per tile (FrameParams::cost): the
+// time of its last whole wave (w), and the costliest part of its last split (p, time << 2 | layout). From them:
+// the load bound L = sum(w) / the GPU's wave slots. The plan pays only while the costliest tile outlasts L (it
+// then forms the launch's tail); otherwise the list is the plain grid's order. When it pays, T = max(L, 0.35 x the
+// costliest tile): a tile above T is traced as 4 parts (2 x 2 sub-rectangles) when 0.55 x its time fits T, else
+// as 16 — unless its last split measured a part above 0.8 x the whole (coherent rays: the parts walk nearly the
+// whole tile's nodes each, so splitting only adds waves), which keeps it whole. The items are then laid out in two
+// classes, those estimated above a fraction of L first, each class in tile order: the long waves start at the
+// front, and neighbouring waves still trace neighbouring tiles (they share the BVH nodes in the scalar cache and
+// L2; a strict longest-first order scattered them and lost more than the tail it saved, profiles/
+// r04_balance_ab_v1.txt). The list is always a valid cover (each tile once, or each of its parts once) whatever
+// the costs hold: the image never depends on it, only the schedule. Items beyond the grid's budget are refused by
+// raising T. (tools/split_study.py models the split on the oracle's packet fetches.) The north star's "wavefront
+// ballot/prefix-sum" appears here as the block scan that places each item.
 // ------------------------------------------------------------------------------------------
-constexpr uint32_t kPlanBuckets = 64;
 constexpr uint32_t kPlanThreads = 1024;
+static_assert(kPlanMaxTiles == 32u * kPlanThreads, "k_tile_plan<32> covers the largest launch");
 
 __device__ __forceinline__ uint32_t plan_code(uint64_t c, uint64_t T, uint32_t kmax) {
   if (c <= T || kmax == 0u) return 0u;
@@ -1799,6 +1801,36 @@ __device__ __forceinline__ uint32_t plan_code(uint64_t c, uint64_t T, uint32_t k
 
 __device__ __forceinline__ uint64_t plan_est(uint64_t c, uint32_t code) {
   return code == 0u ? c : code == 1u ? (c * 11u) / 20u : (c * 7u) / 20u;
+}
+
+// the layout of tile t (adaptive) from its snapshot words (w, p) and its estimated time
+__device__ __forceinline__ uint32_t plan_pick(const PlanArgs& a, uint32_t w, uint32_t p, uint64_t T, uint64_t* est) {
+  uint32_t code = a.split ? plan_code(w, T, a.kmax_code) : 0u;
+  // the last split of this tile measured a part above 0.8 x the whole: splitting does not pay there
+  if (code && p && (uint64_t)(p >> 2) * 5u > (uint64_t)w * 4u) code = 0u;
+  *est = code == 0u ? w : (p && (p & 3u) == code) ? (p >> 2) : plan_est(w, code);
+  return code;
+}
+
+// exclusive prefix sum over the workgroup (wave scan by shuffles, the waves' totals through LDS)
+__device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t* s_w, uint64_t* total) {
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  uint64_t x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  __syncthreads();  // s_w may still be read by the previous reduction
+  if (lane == 63u) s_w[wv] = x;
+  __syncthreads();
+  uint64_t before = 0, tot = 0;
+  for (uint32_t k = 0; k < kPlanThreads / 64u; ++k) {
+    const uint64_t s = s_w[k];
+    before += k < wv ? s : 0u;
+    tot += s;
+  }
+  *total = tot;
+  return before + x - v;
 }
 
 // forced layouts (tests: the oracle emulates the same parts): 1 every tile in 4, 2 every tile in 16, 3 by tile
@@ -1823,97 +1855,181 @@ __device__ uint64_t block_sum64(uint64_t v, uint64_t* sh) {
   return t;
 }
 
+__device__ uint64_t block_max64(uint64_t v, uint64_t* sh) {
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint64_t q = __shfl_xor(v, o, 64);
+    v = q > v ? q : v;
+  }
+  __syncthreads();
+  if ((threadIdx.x & 63u) == 0u) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint64_t m = 0;
+  for (uint32_t k = 0; k < kPlanThreads / 64u; ++k) m = sh[k] > m ? sh[k] : m;
+  return m;
+}
+
+// One workgroup. The launch's snapshot of the costs lives in LDS (launches of the same shape on other streams write
+// the costs meanwhile, and every step must see the same values): one word per tile, the whole wave's time and the
+// last split's costliest part, 16 bits each (10-ns ticks up to 655 us; the part in 40-ns units with its layout), at
+// a padded index (a word per 32 tiles) so a thread's run of consecutive tiles is bank-conflict free. No pass goes
+// back to memory: thread i owns tiles [m i, m i + m) (m = ceil(ntiles / 1024)); one block scan places every
+// thread's items (front class, then the rest, each in tile order).
+__device__ __forceinline__ uint32_t plan_lds_ix(uint32_t t) { return t + (t >> 5); }
+
+__device__ __forceinline__ uint32_t plan_pack(uint32_t w, uint32_t p) {
+  const uint32_t w16 = w < 0xffffu ? w : 0xffffu;
+  const uint32_t pt = (p >> 2) >> 2;  // the part's time in 40-ns units
+  const uint32_t p16 = p ? ((pt < 0x3fffu ? pt : 0x3fffu) << 2) | (p & 3u) : 0u;
+  return w16 | (p16 << 16);
+}
+
+__device__ __forceinline__ uint32_t plan_pick_packed(const PlanArgs& a, uint32_t c, uint64_t T, uint64_t* est) {
+  const uint32_t p16 = c >> 16;
+  return plan_pick(a, c & 0xffffu, p16 ? ((p16 >> 2) << 4) | (p16 & 3u) : 0u, T, est);
+}
+
 __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
+  __shared__ uint32_t s_c[kPlanMaxTiles + kPlanMaxTiles / 32];
   __shared__ uint64_t s_red[kPlanThreads / 64];
-  __shared__ uint32_t s_hist[kPlanBuckets], s_off[kPlanBuckets];
-  const uint32_t tid = threadIdx.x, n = a.ntiles;
-  if (tid < kPlanBuckets) s_hist[tid] = 0u;
-  // the costs are read ONCE into this launch's own snapshot (after the items): launches of the same shape on other
-  // streams write them meanwhile (frames in flight), and every pass below must see the same values, or the
-  // histogram and the scatter would disagree about the items
-  uint32_t* snap = a.plan + 1u + n + a.extra_cap;
-  uint64_t T = ~0ull, mx = 0, sum = 0;
-  uint32_t want = 0;
-  if (!a.force) {
-    uint64_t lsum = 0, lmax = 0;
+  const uint32_t tid = threadIdx.x, n = a.ntiles, cap = n + a.extra_cap;
+  const uint32_t m = (n + kPlanThreads - 1) / kPlanThreads, t0 = tid * m, t1 = t0 + m < n ? t0 + m : n;
+  uint64_t lsum = 0, lmax = 0;
+  if (!a.force)
     for (uint32_t t = tid; t < n; t += kPlanThreads) {
-      const uint32_t c = a.cost[t];
-      snap[t] = c;
-      lsum += c;
-      lmax = c > lmax ? c : lmax;
+      const uint2 v = reinterpret_cast<const uint2*>(a.cost)[t];
+      const uint32_t c = plan_pack(v.x, v.y);
+      s_c[plan_lds_ix(t)] = c;
+      lsum += c & 0xffffu;
+      lmax = (c & 0xffffu) > lmax ? (c & 0xffffu) : lmax;
     }
-    sum = block_sum64(lsum, s_red);
-    // max through the same reduction (as a sum of one-hot maxima is not available): a second pass over LDS
-    for (int o = 32; o >= 1; o >>= 1) {
-      const uint64_t q = __shfl_xor(lmax, o, 64);
-      lmax = q > lmax ? q : lmax;
-    }
-    __syncthreads();
-    if ((tid & 63u) == 0u) s_red[tid >> 6] = lmax;
-    __syncthreads();
-    for (uint32_t k = 0; k < kPlanThreads / 64u; ++k) mx = s_red[k] > mx ? s_red[k] : mx;
-    if (mx > 0u) {
-      const uint64_t L = sum / (a.slots ? a.slots : 1u), F = (mx * 7u) / 20u;
+  uint64_t T = ~0ull, mx = 0, sum = 0, L = 0;
+  uint32_t want = 0;
+  bool tail = false;
+  if (!a.force) {
+    sum = block_sum64(lsum, s_red);  // its barriers also publish s_c
+    mx = block_max64(lmax, s_red);
+    L = sum / (a.slots ? a.slots : 1u);
+    // the costliest tile outlasts the load bound by a quarter and by more than this kernel takes
+    tail = mx * 4u > L * 5u && mx > L + a.min_gain;
+    if (tail) {
+      const uint64_t F = (mx * 7u) / 20u;
       T = L > F ? L : F;
-    }
-    // the parts must fit the grid's budget: raise T until they do (the first count is the demand, reported)
-    for (int iter = 0; iter < 24; ++iter) {
-      uint64_t ex = 0;
-      for (uint32_t t = tid; t < n; t += kPlanThreads) ex += split_parts(plan_code(snap[t], T, a.kmax_code)) - 1u;
-      ex = block_sum64(ex, s_red);
-      if (iter == 0) want = (uint32_t)(ex < 0xffffffffull ? ex : 0xffffffffull);
-      if (ex <= a.extra_cap) break;
-      T = iter < 23 ? T + T / 4u + 1u : ~0ull;  // the last resort: no tile split
+      // the parts must fit the grid's budget: raise T until they do (the first count is the demand, reported)
+      for (int iter = 0; a.split && iter < 24; ++iter) {
+        uint64_t ex = 0, e;
+        for (uint32_t t = t0; t < t1; ++t) ex += split_parts(plan_pick_packed(a, s_c[plan_lds_ix(t)], T, &e)) - 1u;
+        ex = block_sum64(ex, s_red);
+        if (iter == 0) want = (uint32_t)(ex < 0xffffffffull ? ex : 0xffffffffull);
+        if (ex <= a.extra_cap) break;
+        T = iter < 23 ? T + T / 4u + 1u : ~0ull;  // the last resort: no tile split
+      }
     }
   }
-  __syncthreads();
-  // histogram of the items by estimated time: bucket 0 the longest
-  uint32_t nsplit = 0;
-  for (uint32_t t = tid; t < n; t += kPlanThreads) {
-    const uint64_t c = a.force ? 0u : snap[t];
-    const uint32_t code = a.force ? plan_forced(a, t) : plan_code(c, T, a.kmax_code);
-    const uint64_t e = plan_est(c, code);
-    const uint32_t b = mx ? (uint32_t)(((mx - (e < mx ? e : mx)) * kPlanBuckets) / (mx + 1u)) : kPlanBuckets - 1u;
-    atomicAdd(&s_hist[b], split_parts(code));
-    nsplit += code ? 1u : 0u;
+  uint32_t nsplit = 0, nitems = n;
+  bool pays = false;
+  if (!a.force && !tail) {
+    // no tail: the plain grid's order, every tile whole
+    for (uint32_t t = tid; t < n; t += kPlanThreads) a.plan[1u + t] = t << 6;
+  } else {
+    // two classes (estimated above front / 16 x L first), each in tile order
+    const uint64_t TF = (!a.force && a.front) ? (L * a.front) >> 4 : ~0ull;
+    uint32_t cf = 0, cb = 0, tf = 0;
+    uint64_t e = 0;
+    for (uint32_t t = t0; t < t1; ++t) {
+      const uint32_t code = a.force ? plan_forced(a, t) : plan_pick_packed(a, s_c[plan_lds_ix(t)], T, &e);
+      const uint32_t k = split_parts(code);
+      const bool fr = !a.force && e > TF;
+      cf += fr ? k : 0u;
+      cb += fr ? 0u : k;
+      tf += fr ? 1u : 0u;
+      nsplit += code ? 1u : 0u;
+    }
+    uint64_t tot;
+    const uint64_t ex = block_excl_scan64(((uint64_t)cf << 32) | cb, s_red, &tot);
+    uint32_t pf = (uint32_t)(ex >> 32), pb = (uint32_t)(tot >> 32) + (uint32_t)ex;
+    for (uint32_t t = t0; t < t1; ++t) {
+      const uint32_t code = a.force ? plan_forced(a, t) : plan_pick_packed(a, s_c[plan_lds_ix(t)], T, &e);
+      const uint32_t k = split_parts(code);
+      const bool fr = !a.force && e > TF;
+      uint32_t pos = fr ? pf : pb;
+      for (uint32_t q = 0; q < k; ++q, ++pos)
+        if (pos < cap) a.plan[1u + pos] = (t << 6) | (q << 2) | code;  // always true: the budget holds
+      if (fr) pf += k;
+      else pb += k;
+      // a split tile's part word restarts (its parts raise it with atomicMax at their end)
+      if (!a.force && code) a.cost[2u * t + 1u] = 0u;
+    }
+    const uint32_t all = (uint32_t)(tot >> 32) + (uint32_t)tot;
+    nitems = all < cap ? all : cap;
+    // whether the list differs from the plain grid's in what the launch's time depends on: a tile split, or (more
+    // waves than the GPU's slots) a front class that is neither empty nor everything
+    const uint64_t r = block_sum64(((uint64_t)nsplit << 32) | tf, s_red);
+    nsplit = (uint32_t)(r >> 32);
+    const uint32_t nfront_tiles = (uint32_t)r;
+    pays = nsplit > 0u || (n > a.slots && nfront_tiles > 0u && nfront_tiles < n);
   }
-  __syncthreads();
+  // diagnostics (PlanArgs::check): the list must cover every tile exactly once — each tile's items one layout, its
+  // parts 0 .. k - 1 once each (the words after the items count them)
+  uint32_t bad = 0, first_bad = 0xffffffffu, first_word = 0;
+  if (a.check) {
+    uint32_t* sw = a.plan + 1u + cap;
+    uint32_t* sp = sw + n;
+    __syncthreads();  // every item is written
+    for (uint32_t t = tid; t < n; t += kPlanThreads) sw[t] = sp[t] = 0u;
+    __syncthreads();
+    for (uint32_t i = tid; i < nitems; i += kPlanThreads) {
+      const uint32_t it = a.plan[1u + i], slot = it >> 6, q = (it >> 2) & 15u, code = it & 3u;
+      if (slot >= n || code > 2u || q >= split_parts(code)) {
+        bad += 1u;
+        continue;
+      }
+      atomicAdd(&sp[slot], 1u << q);
+      atomicOr(&sw[slot], 1u << code);
+    }
+    __syncthreads();
+    for (uint32_t t = tid; t < n; t += kPlanThreads) {
+      const uint32_t m = sw[t], c = sp[t];
+      const bool ok = (m == 1u && c == 1u) || (m == 2u && c == 0xfu) || (m == 4u && c == 0xffffu);
+      if (!ok) {
+        bad += 1u;
+        if (t < first_bad) {
+          first_bad = t;
+          first_word = (m << 24) | (c & 0xffffffu);
+        }
+      }
+    }
+    bad = (uint32_t)block_sum64(bad, s_red);
+    const uint64_t fb = block_max64(~(((uint64_t)first_bad << 32) | first_word), s_red);  // the lowest tile
+    first_bad = (uint32_t)(~fb >> 32);
+    first_word = (uint32_t)~fb;
+  }
+  // the item count (the trace waves past it exit), and the summary for the host (host-mapped memory: read at a
+  // later dispatch, no copy call)
   if (tid == 0u) {
-    uint32_t run = 0;
-    for (uint32_t b = 0; b < kPlanBuckets; ++b) {
-      s_off[b] = run;
-      run += s_hist[b];
+    a.plan[0] = nitems;
+    if (a.stats) {
+      PlanStats* st = a.stats;
+      st->nitems = nitems;
+      st->nsplit = nsplit;
+      st->want_extra = want;
+      st->max_cost = (uint32_t)(mx < 0xffffffffull ? mx : 0xffffffffull);
+      st->mean_cost = n ? (uint32_t)(sum / n) : 0u;
+      st->threshold = (uint32_t)(T < 0xffffffffull ? T : 0xffffffffull);
+      st->pays = pays ? 1u : 0u;
+      st->plans += 1u;
+      if (a.check) {
+        st->bad += bad;
+        if (bad && !st->first_bad_word) {
+          st->first_bad_tile = first_bad;
+          st->first_bad_word = first_word | 0x80000000u;
+        }
+      }
     }
-    a.plan[0] = run < n + a.extra_cap ? run : n + a.extra_cap;  // the item count (the trace waves past it exit)
-  }
-  __syncthreads();
-  // scatter (the order inside a bucket is whatever the atomics give: only the schedule depends on it)
-  const uint32_t cap = n + a.extra_cap;  // the items the buffer (and the launch's grid) has room for
-  for (uint32_t t = tid; t < n; t += kPlanThreads) {
-    const uint64_t c = a.force ? 0u : snap[t];
-    const uint32_t code = a.force ? plan_forced(a, t) : plan_code(c, T, a.kmax_code);
-    const uint64_t e = plan_est(c, code);
-    const uint32_t b = mx ? (uint32_t)(((mx - (e < mx ? e : mx)) * kPlanBuckets) / (mx + 1u)) : kPlanBuckets - 1u;
-    const uint32_t k = split_parts(code);
-    const uint32_t pos = atomicAdd(&s_off[b], k);
-    for (uint32_t q = 0; q < k; ++q)
-      if (pos + q < cap) a.plan[1u + pos + q] = (t << 6) | (q << 2) | code;  // always true: the budget holds
-  }
-  // summary for the host (host-mapped memory: read at a later dispatch, no copy call)
-  nsplit = (uint32_t)block_sum64(nsplit, s_red);
-  if (tid == 0u && a.stats) {
-    PlanStats* st = a.stats;
-    st->nitems = a.plan[0];
-    st->nsplit = nsplit;
-    st->want_extra = want;
-    st->max_cost = (uint32_t)(mx < 0xffffffffull ? mx : 0xffffffffull);
-    st->mean_cost = n ? (uint32_t)(sum / n) : 0u;
-    st->threshold = (uint32_t)(T < 0xffffffffull ? T : 0xffffffffull);
-    st->plans += 1u;
   }
 }
 
 hipError_t launch_tile_plan(const PlanArgs& a, hipStream_t s) {
+  if (a.ntiles > kPlanMaxTiles) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_tile_plan, dim3(1), dim3(kPlanThreads), 0, s, a);
   return hipGetLastError();
 }

@@ -4,6 +4,8 @@ time). Each wave records its tile's time; a one-workgroup plan kernel splits the
 oracle's bit for bit in every layout. The forced layouts (modes 2 / 3 / 4) are deterministic, so the traversal
 counters are also compared with the oracle's emulation of the same parts (oracle_render_split): every part is its
 own packet with the lanes outside its sub-rectangle dead."""
+import os
+
 import numpy as np
 import pytest
 
@@ -17,6 +19,23 @@ import oracle  # noqa: E402
 
 KEYS = ["primary_rays", "shadow_rays", "aabb_tests", "tri_tests", "instance_entries", "stack_overflows"]
 FETCH = ["node_fetches", "tri_fetches", "instance_fetches"]
+
+
+def checked_context():
+    """A context whose plan kernel verifies each work list covers every tile exactly once (RT_BALANCE_CHECK, read at
+    creation; tile_balance_info()["check_bad"])."""
+    os.environ["RT_BALANCE_CHECK"] = "1"
+    try:
+        return rt.Context(0)
+    finally:
+        del os.environ["RT_BALANCE_CHECK"]
+
+
+def bad_tiles(a, b):
+    """(tx, ty) of the 8 x 8 tiles where two frames differ (the first few), for the failure message."""
+    d = (a != b).any(axis=-1)
+    ys, xs = np.nonzero(d)
+    return sorted({(int(x) // 8, int(y) // 8) for x, y in zip(xs, ys)})[:8], int(d.sum())
 
 
 def render(c, spec, stream=None, rows=None):
@@ -83,19 +102,23 @@ def test_adaptive_balance_frames_equal_oracle(name):
     run the plan (the costliest tiles split, longest first). Eight frames on two streams (frames in flight: plans
     from the ring, cost maps read while written) all equal the oracle's frame; the plan ran and split tiles."""
     spec = scenes.config(name)
-    c = rt.Context(0)
+    c = checked_context()
     scenes.upload(c, spec)
     streams = [torch.cuda.Stream() for _ in range(2)]
     outs = []
     for k in range(8):
-        outs.append(render(c, spec, stream=streams[k % 2])[0])
+        # both outputs stay referenced until the end: a buffer dropped while its stream's kernel still writes it
+        # would go to the next frame (the allocator's stream is the current one, not the kernel's)
+        outs.append(render(c, spec, stream=streams[k % 2]))
         if k == 0:
             torch.cuda.synchronize()
     torch.cuda.synchronize()
     info = c.tile_balance_info()
+    assert info["check_bad"] == 0, info
     o8, _, _ = oracle.Scene(spec).render_spec(spec, nthreads=16, want_float=False, schedule=1)
-    for k, f in enumerate(outs):
-        assert np.array_equal(f.cpu().numpy(), o8), f"{name} frame {k}"
+    for k, (f, _) in enumerate(outs):
+        g = f.cpu().numpy()
+        assert np.array_equal(g, o8), f"{name} frame {k}: tiles {bad_tiles(g, o8)} {info}"
     assert info["launches"] == 8 and info["plans"] >= 1 and info["split"] > 0, info
     assert info["max_ticks"] > 2 * info["mean_ticks"] > 0, info
     c.close()
@@ -105,7 +128,7 @@ def test_adaptive_balance_multi_frame_launch_and_off():
     """Several frames in one launch (the grid's frames share one work list) with the adaptive plan, then the plain
     grid (mode 0): every frame equals the oracle's."""
     spec = scenes.config("C4").with_size(480, 270)
-    c = rt.Context(0)
+    c = checked_context()
     scenes.upload(c, spec)
     comm = rt.Comm.loopback(c, 2)
     comm.set_batch(4)
@@ -126,6 +149,7 @@ def test_adaptive_balance_multi_frame_launch_and_off():
     off = [torch.zeros((spec.height, spec.width, 4), dtype=torch.uint8, device="cuda") for _ in range(4)]
     comm.render_strips_frames(spec.width, spec.height, off, cameras=cams)
     comm.close()
+    assert c.tile_balance_info()["check_bad"] == 0
     for q, sp in enumerate(specs):
         o8, _, _ = oracle.Scene(sp).render_spec(sp, nthreads=16, want_float=False, schedule=1)
         for rep in range(4):

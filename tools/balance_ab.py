@@ -2,8 +2,10 @@
 """Tile balance A/B on the GPU (rt_set_tile_balance 0 = plain grid vs 1 = adaptive): ms per frame of whole frames and
 of rank 0's strip share at N ranks (interleaved 8-row strips, the row list a rank of the tiled-frame loop renders),
 one stream back to back (the frame latency) and with 3 frames in flight, interleaved rounds, medians; every variant's
-frame is checked equal to the first's.
-  python3 tools/balance_ab.py --configs C4,C2F,C2 --shares 1,4,8 --rounds 5"""
+frame is checked equal to the first's. --variants names the arms: b0 (off), b1 (adaptive, the defaults), and b1 with
+the plan's diagnostics (RT_BALANCE_SPLIT / RT_BALANCE_FRONT, read at context creation): b1s0 (no split, order
+only), b1f0 (tile order, split only), b1f<k> (front class above k / 16 x the load bound).
+  python3 tools/balance_ab.py --configs C4,C2F,C2 --shares 1,4,8 --rounds 5 --variants b0,b1,b1s0"""
 import argparse
 import json
 import os
@@ -41,13 +43,21 @@ def main():
     ap.add_argument("--shares", default="1,4,8")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=40)
+    ap.add_argument("--variants", default="b0,b1")
     a = ap.parse_args()
+    variants = a.variants.split(",")
     res = {}
     for name in a.configs.split(","):
         spec = scenes.config(name)
         frames = max(4, a.frames // (8 if spec.spp > 1 else 1))
-        c = rt.Context(0)
-        scenes.upload(c, spec)
+        ctxs = {}
+        for v in variants:
+            env = {"RT_BALANCE_SPLIT": "0" if "s0" in v else "1",
+                   "RT_BALANCE_FRONT": v.split("f")[1] if "f" in v else "8"}
+            os.environ.update(env)
+            ctxs[v] = rt.Context(0)
+            scenes.upload(ctxs[v], spec)
+            ctxs[v].set_tile_balance(0 if v == "b0" else 1)
         for share in [int(x) for x in a.shares.split(",")]:
             rows = None if share == 1 else rt.strip_rows(spec.height, share, 0)
             nr = spec.height if rows is None else len(rows)
@@ -56,22 +66,24 @@ def main():
             t = {}
             ref = None
             for rnd in range(a.rounds):
-                for mode in (0, 1):
-                    c.set_tile_balance(mode)
+                for v in variants:
+                    c = ctxs[v]
                     for key, ss in (("one", streams[:1]), ("inflight3", streams)):
                         timed(c, spec, rows, bufs, ss, 3)  # the shape's costs / plan warm
                         ms = timed(c, spec, rows, bufs, ss, frames)
-                        t.setdefault(f"b{mode}_{key}", []).append(ms)
+                        t.setdefault(f"{v}_{key}", []).append(ms)
                     img = bufs[0].cpu().numpy()
                     if ref is None:
                         ref = img
-                    assert np.array_equal(img, ref), f"{name} share {share} mode {mode}: frame differs"
-            info = c.tile_balance_info()
-            line = {k: round(float(np.median(v)), 4) for k, v in t.items()}
-            line["balance_info"] = info
+                    assert np.array_equal(img, ref), f"{name} share {share} {v}: frame differs"
+            line = {k: round(float(np.median(x)), 4) for k, x in t.items()}
+            for v in variants:
+                if v != "b0":
+                    line[f"{v}_info"] = ctxs[v].tile_balance_info()
             res[f"{name}_N{share}"] = line
             print(name, f"share N={share}", json.dumps(line), flush=True)
-        c.close()
+        for c in ctxs.values():
+            c.close()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "balance_ab.json"), "w") as f:
         json.dump(res, f, indent=1)
