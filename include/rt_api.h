@@ -204,8 +204,9 @@ rt_status rt_set_tile_balance(rt_ctx_t ctx, int mode);
  * [7] launches of the shape, [8] the last plan found the costliest tile above the load bound (its list is not the
  * plain order), [9] tiles the lists failed to cover exactly once, [10] the first such tile, [11] its check word
  * ([9..11] only when the context was created with RT_BALANCE_CHECK=1 in the environment: a cover check after each
- * plan, diagnostics). Host-side read of host-mapped memory (may lag the device by a few launches). */
-rt_status rt_tile_balance_info(rt_ctx_t ctx, uint32_t out[12]);
+ * plan, diagnostics), [12..14] the last plan kernel's phases in 10-ns ticks (snapshot + load bound, budget,
+ * placement), [15] 0. Host-side read of host-mapped memory (may lag the device by a few launches). */
+rt_status rt_tile_balance_info(rt_ctx_t ctx, uint32_t out[16]);
 /* Enables device counters (rt_stats). Costs time: off for timed runs. */
 rt_status rt_set_stats(rt_ctx_t ctx, int enable);
 

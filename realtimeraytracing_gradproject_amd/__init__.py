@@ -632,10 +632,11 @@ class Context:
         self._check(self._lib.rt_set_tile_balance(self._h, mode), "rt_set_tile_balance")
 
     def tile_balance_info(self) -> dict:
-        out = (ctypes.c_uint32 * 12)()
+        out = (ctypes.c_uint32 * 16)()
         self._check(self._lib.rt_tile_balance_info(self._h, out), "rt_tile_balance_info")
         return dict(zip(("plans", "split", "items", "extra_cap", "max_ticks", "mean_ticks", "threshold", "launches",
-                         "pays", "check_bad", "check_first_tile", "check_first_word"), list(out)))
+                         "pays", "check_bad", "check_first_tile", "check_first_word", "plan_load_ticks",
+                         "plan_budget_ticks", "plan_place_ticks"), list(out)))
 
     def set_stats(self, on: bool):
         self._check(self._lib.rt_set_stats(self._h, 1 if on else 0), "rt_set_stats")

@@ -193,7 +193,10 @@ hipError_t note_reader(TlasVersion& v, hipStream_t s) {
 
 // Tile balance (rt_set_tile_balance) of one launch shape (frame size, row list, frames per launch, tile layout):
 // the per-tile wave times the packet kernel leaves (FrameParams::cost), the plan kernel's summary in host-mapped
-// memory, and the work list's budget of extra waves for split tiles.
+// memory, the work list's budget of extra waves for split tiles, and the shape's work lists. A list is a valid
+// cover of the shape's tiles whatever costs it was planned from, so launches reuse the current one and the plan
+// kernel runs again only every few launches (balance_wants_plan). Two lists: the current one, and the one before it,
+// which launches on other streams may still be reading; the next plan overwrites that older one, ordered after them.
 struct BalanceMap {
   uint32_t W = 0, nrows = 0, nframes = 0, tile_rows = 0, spp = 0, ntiles = 0;
   const uint32_t* rows = nullptr;
@@ -201,10 +204,24 @@ struct BalanceMap {
   rt::PlanStats* stats = nullptr;    // host-mapped, written by k_tile_plan
   rt::PlanStats* stats_dev = nullptr;
   uint32_t extra_cap = 0;
-  uint64_t launches = 0, tick = 0;
+  uint64_t launches = 0, tick = 0;   // launches: those with the balance active
+  hipStream_t last_stream = nullptr; // the stream of the shape's previous launch
+  hipEvent_t done = nullptr;         // recorded after each launch of the shape
+  bool done_recorded = false;
+  ScratchSlot list[2];               // work lists; uses recorded when a list stops being current
+  int cur = -1;                      // the current list (its plan kernel enqueued), or none
+  uint32_t cur_items = 0;            // its launch's grid budget (tiles + extra waves)
+  uint64_t planned_at = 0;           // launches of the shape when it was planned
+  hipEvent_t ready = nullptr;        // recorded after the current list's plan kernel
+  std::vector<hipStream_t> waited;   // streams ordered after `ready`
+  std::vector<hipStream_t> readers;  // streams that launched with the current list since it became current
   void release() {
     if (cost) (void)hipFree(cost);
     if (stats) (void)hipHostFree(stats);
+    slot_release(list[0]);
+    slot_release(list[1]);
+    if (ready) (void)hipEventDestroy(ready);
+    if (done) (void)hipEventDestroy(done);
     *this = BalanceMap();
   }
 };
@@ -801,9 +818,9 @@ rt_status rt_set_tile_balance(rt_ctx_t c, int mode) {
   return RT_OK;
 }
 
-rt_status rt_tile_balance_info(rt_ctx_t c, uint32_t out[12]) {
+rt_status rt_tile_balance_info(rt_ctx_t c, uint32_t out[16]) {
   if (!c || !out) return RT_E_INVALID;
-  std::memset(out, 0, 12 * sizeof(uint32_t));
+  std::memset(out, 0, 16 * sizeof(uint32_t));
   const BalanceMap* m = c->bal_last;
   if (!m || !m->stats) return RT_OK;
   const volatile rt::PlanStats* st = m->stats;
@@ -819,6 +836,7 @@ rt_status rt_tile_balance_info(rt_ctx_t c, uint32_t out[12]) {
   out[9] = st->bad;
   out[10] = st->first_bad_tile;
   out[11] = st->first_bad_word;
+  for (int k = 0; k < 3; ++k) out[12 + k] = st->phase_ticks[k];
   return RT_OK;
 }
 
@@ -979,6 +997,16 @@ hipError_t ctx_forget_stream(rt_ctx* c, hipStream_t s) {
     const hipError_t e = slot_mark_use(v.use, s);  // covers every launch of s so far
     if (e != hipSuccess && first == hipSuccess) first = e;
   }
+  // the tile balance's lists: the same for their readers; a later stream with the same handle must wait for
+  // `ready` itself
+  for (BalanceMap& m : c->bal) {
+    m.waited.erase(std::remove(m.waited.begin(), m.waited.end(), s), m.waited.end());
+    auto it = std::find(m.readers.begin(), m.readers.end(), s);
+    if (it == m.readers.end() || m.cur < 0) continue;
+    m.readers.erase(it);
+    const hipError_t e = slot_mark_use(m.list[m.cur], s);
+    if (e != hipSuccess && first == hipSuccess) first = e;
+  }
   return first;
 }
 void* ctx_stream(rt_ctx* c) { return c ? (void*)c->stream : nullptr; }
@@ -1006,6 +1034,7 @@ static BalanceMap* balance_map(rt_ctx* c, uint32_t W, uint32_t nrows, const uint
     if (!lru || m.tick < lru->tick) lru = &m;
   }
   BalanceMap* m = nullptr;
+  c->bal.reserve(rt_ctx::kMaxBalanceMaps);  // the maps never move (bal_last points at one)
   if (c->bal.size() < rt_ctx::kMaxBalanceMaps) {
     c->bal.emplace_back();
     m = &c->bal.back();
@@ -1039,17 +1068,42 @@ static BalanceMap* balance_map(rt_ctx* c, uint32_t W, uint32_t nrows, const uint
   return m;
 }
 
-// Whether this launch runs the plan kernel (adaptive mode): not before the shape has wave times; every launch while
-// the last plan found the costliest tile above the load bound (the slowest tiles form the launch's tail); else one
-// launch in 16 re-checks. The summary is read from host-mapped memory without a copy call (it may lag by a few
-// launches).
-static bool balance_wants_plan(BalanceMap& m) {
+// Adaptive mode: whether this launch runs the plan kernel (a new list), and whether it runs with the shape's current
+// list at all. Not before the shape has wave times. A list that differs from the plain order (the last plan's
+// `pays`) is used by every launch and re-planned every kReplan launches (the costs drift with the camera);
+// otherwise the launches take the plain grid and one in kRecheck plans again. The summary is read from host-mapped
+// memory without a copy call (it may lag by a few launches: any list is a valid cover).
+constexpr uint64_t kReplan = 8, kRecheck = 32;
+
+static void balance_wants_plan(BalanceMap& m, bool* plan, bool* use) {
   const volatile rt::PlanStats* st = m.stats;
   const uint32_t plans = st->plans, want = st->want_extra;
   if (plans) m.extra_cap = std::min<uint64_t>((uint64_t)want + want / 4u + 64u, 15ull * m.ntiles);
-  if (m.launches == 0) return false;
-  if (plans == 0 || st->pays) return true;
-  return m.launches % 16u == 0u;
+  *plan = *use = false;
+  if (m.launches == 0) return;
+  if (m.cur < 0) {
+    *plan = *use = true;
+    return;
+  }
+  const uint64_t age = m.launches - m.planned_at;
+  *use = st->pays != 0;
+  *plan = age >= (*use ? kReplan : kRecheck);
+  if (*plan) *use = true;
+}
+
+// The current list stops being current: one event per stream that launched with it (covering all of that stream's
+// launches so far), so the plan that overwrites it later orders after them on the device. On a failed record
+// (a stream destroyed without rt_forget_stream) the device is drained instead.
+static hipError_t balance_swap_out(BalanceMap& m) {
+  hipError_t first = hipSuccess;
+  if (m.cur >= 0)
+    for (hipStream_t r : m.readers) {
+      const hipError_t e = slot_mark_use(m.list[m.cur], r);
+      if (e != hipSuccess && first == hipSuccess) first = e;
+    }
+  m.readers.clear();
+  if (first != hipSuccess) (void)hipDeviceSynchronize();
+  return first;
 }
 
 // RayGen's per-frame constants from a camera buffer (UpdateCameraBuffer's 256 B, D3D12HelloTriangle.cpp:1144-1170):
@@ -1103,6 +1157,7 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
   c->fp.waves_per_frame = g.waves_per_frame;
   uint32_t plan_items = 0;
   ScratchSlot* plan_slot = nullptr;
+  BalanceMap* bm = nullptr;
   const bool forced = c->balance >= 2;
   if (forced && (uint64_t)g.waves_per_frame * nframes > rt::kPlanMaxTiles)
     return fail(c, RT_E_UNSUPPORTED, "tile balance: forced layouts take at most 32768 waves per launch");
@@ -1115,36 +1170,74 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
     BalanceMap* m = balance_map(c, W, nrows, d_rows, nframes, ntiles, s, &be);
     if (!m) return hip_fail(c, be, "tile balance: cost map");
     c->bal_last = m;
-    c->fp.cost = forced ? nullptr : m->cost;
-    if (forced || balance_wants_plan(*m)) {
-      const uint32_t extra = forced ? 15u * ntiles : m->extra_cap;
-      plan_items = ntiles + extra;
+    // frames in flight (the shape's previous launch still runs on another stream): the next frame's waves already
+    // fill the slots the slowest tiles leave idle, so the balance only adds work there (split parts, the plan). It
+    // runs when this launch follows the previous one on its stream or the previous one has finished (frame
+    // latency: one frame at a time, a rank's share of a frame).
+    const bool prev_done = !m->done_recorded || hipEventQuery(m->done) == hipSuccess;
+    const bool active = forced || s == m->last_stream || prev_done;
+    m->last_stream = s;
+    bm = m;
+    c->fp.cost = (active && !forced) ? m->cost : nullptr;
+    bool plan = forced, use = forced;
+    if (active && !forced) balance_wants_plan(*m, &plan, &use);
+    rt::PlanArgs a;
+    a.cost = m->cost;
+    a.stats = forced ? nullptr : m->stats_dev;
+    a.ntiles = ntiles;
+    a.slots = 7u * 1024u;  // the LAMBERT_SHADOW kernel's 7 waves per SIMD x 1024 SIMDs
+    a.kmax_code = g.kmax_code;
+    a.force = forced ? (uint32_t)(c->balance - 1) : 0u;
+    a.split = c->bal_split;
+    a.front = c->bal_front;
+    a.check = c->bal_check;
+    a.min_gain = 1000u;  // 10 us: above the plan kernel's own time
+    a.waves_per_frame = g.waves_per_frame;
+    a.grid_x = g.grid_x;
+    a.wx = g.wx;
+    a.wy = g.wy;
+    a.wl = g.wl;
+    if (forced) {
+      // tests: a fresh list per launch from the ring
+      a.extra_cap = 15u * ntiles;
+      plan_items = ntiles + a.extra_cap;
       bool hit;
       plan_slot = ring_acquire(c->plans, s, nullptr, &hit, &be);
       if (be != hipSuccess) return hip_fail(c, be, "tile balance: order after in-flight launches");
       HIPCHK(c, slot_reserve(*plan_slot, ((size_t)plan_items + 2u * ntiles + 1) * 4), "hipMalloc(tile plan)");
-      rt::PlanArgs a;
-      a.cost = m->cost;
       a.plan = (uint32_t*)plan_slot->buf;
-      a.stats = forced ? nullptr : m->stats_dev;
-      a.ntiles = ntiles;
-      a.extra_cap = extra;
-      a.slots = 7u * 1024u;  // the LAMBERT_SHADOW kernel's 7 waves per SIMD x 1024 SIMDs
-      a.kmax_code = g.kmax_code;
-      a.force = forced ? (uint32_t)(c->balance - 1) : 0u;
-      a.split = c->bal_split;
-      a.front = c->bal_front;
-      a.check = c->bal_check;
-      a.min_gain = 1000u;  // 10 us: above the plan kernel's own time
-      a.waves_per_frame = g.waves_per_frame;
-      a.grid_x = g.grid_x;
-      a.wx = g.wx;
-      a.wy = g.wy;
-      a.wl = g.wl;
       HIPCHK(c, rt::launch_tile_plan(a, s), "tile plan launch");
       c->fp.plan = a.plan;
+    } else {
+      if (plan) {
+        // the next list goes into the older buffer, after every launch that read it
+        const int b = m->cur < 0 ? 0 : 1 - m->cur;
+        ScratchSlot& sl = m->list[b];
+        HIPCHK(c, slot_order_after_others(sl, s), "tile balance: order after the list's readers");
+        HIPCHK(c, balance_swap_out(*m), "tile balance: record the list's readers");
+        a.extra_cap = m->extra_cap;
+        const uint32_t items = ntiles + a.extra_cap;
+        HIPCHK(c, slot_reserve(sl, ((size_t)items + 2u * ntiles + 1) * 4), "hipMalloc(tile plan)");
+        a.plan = (uint32_t*)sl.buf;
+        HIPCHK(c, rt::launch_tile_plan(a, s), "tile plan launch");
+        if (!m->ready && !(m->ready = new_sync_event())) return fail(c, RT_E_HIP, "tile balance: event");
+        HIPCHK(c, hipEventRecord(m->ready, s), "tile balance: record the plan");
+        m->waited.assign(1, s);
+        m->cur = b;
+        m->cur_items = items;
+        m->planned_at = m->launches;
+      }
+      if (use && m->cur >= 0) {
+        if (std::find(m->waited.begin(), m->waited.end(), s) == m->waited.end()) {
+          HIPCHK(c, hipStreamWaitEvent(s, m->ready, 0), "tile balance: wait for the plan");
+          m->waited.push_back(s);
+        }
+        if (std::find(m->readers.begin(), m->readers.end(), s) == m->readers.end()) m->readers.push_back(s);
+        c->fp.plan = (const uint32_t*)m->list[m->cur].buf;
+        plan_items = m->cur_items;
+      }
     }
-    m->launches += 1;
+    if (active) m->launches += 1;
   }
   hipError_t e = rt::launch_trace_frame(sv, c->fp, d_rows, rgba8, rgba32f, c->d_stats, c->stats_on,
                                         c->schedule, plan_items, s);
@@ -1152,6 +1245,11 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
   HIPCHK(c, note_reader(c->ver[c->cur], s), "rt_dispatch_rays: record use");
   if (ovf_slot) HIPCHK(c, slot_mark_use(*ovf_slot, s), "overflow stack: record use");
   if (plan_slot) HIPCHK(c, slot_mark_use(*plan_slot, s), "tile plan: record use");
+  if (bm) {
+    if (!bm->done && !(bm->done = new_sync_event())) return fail(c, RT_E_HIP, "tile balance: event");
+    HIPCHK(c, hipEventRecord(bm->done, s), "tile balance: record the launch");
+    bm->done_recorded = true;
+  }
   if (c->stats_on) {
     c->dispatches += nframes;
     c->pixels += (uint64_t)W * nrows * nframes;

@@ -1792,25 +1792,7 @@ hipError_t launch_trace_frame(const SceneView& sc, const FrameParams& fp, const 
 // ballot/prefix-sum" appears here as the block scan that places each item.
 // ------------------------------------------------------------------------------------------
 constexpr uint32_t kPlanThreads = 1024;
-static_assert(kPlanMaxTiles == 32u * kPlanThreads, "k_tile_plan<32> covers the largest launch");
-
-__device__ __forceinline__ uint32_t plan_code(uint64_t c, uint64_t T, uint32_t kmax) {
-  if (c <= T || kmax == 0u) return 0u;
-  return (kmax == 1u || c * 11u <= T * 20u) ? 1u : 2u;  // 0.55 c fits T: 4 parts, else 16
-}
-
-__device__ __forceinline__ uint64_t plan_est(uint64_t c, uint32_t code) {
-  return code == 0u ? c : code == 1u ? (c * 11u) / 20u : (c * 7u) / 20u;
-}
-
-// the layout of tile t (adaptive) from its snapshot words (w, p) and its estimated time
-__device__ __forceinline__ uint32_t plan_pick(const PlanArgs& a, uint32_t w, uint32_t p, uint64_t T, uint64_t* est) {
-  uint32_t code = a.split ? plan_code(w, T, a.kmax_code) : 0u;
-  // the last split of this tile measured a part above 0.8 x the whole: splitting does not pay there
-  if (code && p && (uint64_t)(p >> 2) * 5u > (uint64_t)w * 4u) code = 0u;
-  *est = code == 0u ? w : (p && (p & 3u) == code) ? (p >> 2) : plan_est(w, code);
-  return code;
-}
+static_assert(kPlanMaxTiles == 32u * kPlanThreads, "a run of at most 32 tiles per thread");
 
 // exclusive prefix sum over the workgroup (wave scan by shuffles, the waves' totals through LDS)
 __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t* s_w, uint64_t* total) {
@@ -1883,18 +1865,28 @@ __device__ __forceinline__ uint32_t plan_pack(uint32_t w, uint32_t p) {
   return w16 | (p16 << 16);
 }
 
-__device__ __forceinline__ uint32_t plan_pick_packed(const PlanArgs& a, uint32_t c, uint64_t T, uint64_t* est) {
-  const uint32_t p16 = c >> 16;
-  return plan_pick(a, c & 0xffffu, p16 ? ((p16 >> 2) << 4) | (p16 & 3u) : 0u, T, est);
+// the layout of a tile from its snapshot word (w16 | p16 << 16) and its estimated time; 32-bit: a time is at most
+// 65535 ticks, and T (0xffffffff: split nothing) is below 65535 wherever a tile exceeds it
+__device__ __forceinline__ uint32_t plan_pick32(const PlanArgs& a, uint32_t c, uint32_t T, uint32_t* est) {
+  const uint32_t w = c & 0xffffu, p16 = c >> 16, pt = (p16 >> 2) << 2;  // the part's time in ticks
+  uint32_t code = 0;
+  if (a.split && a.kmax_code && w > T) code = (a.kmax_code == 1u || w * 11u <= T * 20u) ? 1u : 2u;
+  // the last split of this tile measured a part above 0.8 x the whole: splitting does not pay there
+  if (code && p16 && pt * 5u > w * 4u) code = 0u;
+  *est = code == 0u ? w : (p16 && (p16 & 3u) == code) ? pt : (code == 1u ? (w * 11u) / 20u : (w * 7u) / 20u);
+  return code;
 }
 
 __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
   __shared__ uint32_t s_c[kPlanMaxTiles + kPlanMaxTiles / 32];
   __shared__ uint64_t s_red[kPlanThreads / 64];
+  const uint64_t t_begin = __builtin_amdgcn_s_memrealtime();
   const uint32_t tid = threadIdx.x, n = a.ntiles, cap = n + a.extra_cap;
   const uint32_t m = (n + kPlanThreads - 1) / kPlanThreads, t0 = tid * m, t1 = t0 + m < n ? t0 + m : n;
-  uint64_t lsum = 0, lmax = 0;
-  if (!a.force)
+  // 1. the snapshot (coalesced loads, tile t by thread t % 1024, unrolled so the loads overlap) and the load bound
+  uint32_t lsum = 0, lmax = 0;  // < 32 tiles x 65535 per thread
+  if (!a.force) {
+#pragma unroll 8
     for (uint32_t t = tid; t < n; t += kPlanThreads) {
       const uint2 v = reinterpret_cast<const uint2*>(a.cost)[t];
       const uint32_t c = plan_pack(v.x, v.y);
@@ -1902,41 +1894,49 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
       lsum += c & 0xffffu;
       lmax = (c & 0xffffu) > lmax ? (c & 0xffffu) : lmax;
     }
-  uint64_t T = ~0ull, mx = 0, sum = 0, L = 0;
-  uint32_t want = 0;
+  }
+  uint32_t T = 0xffffffffu, mx = 0, L = 0, want = 0;
+  uint64_t sum = 0;
   bool tail = false;
   if (!a.force) {
     sum = block_sum64(lsum, s_red);  // its barriers also publish s_c
-    mx = block_max64(lmax, s_red);
-    L = sum / (a.slots ? a.slots : 1u);
+    mx = (uint32_t)block_max64(lmax, s_red);
+    L = (uint32_t)(sum / (a.slots ? a.slots : 1u));
     // the costliest tile outlasts the load bound by a quarter and by more than this kernel takes
-    tail = mx * 4u > L * 5u && mx > L + a.min_gain;
-    if (tail) {
-      const uint64_t F = (mx * 7u) / 20u;
-      T = L > F ? L : F;
-      // the parts must fit the grid's budget: raise T until they do (the first count is the demand, reported)
-      for (int iter = 0; a.split && iter < 24; ++iter) {
-        uint64_t ex = 0, e;
-        for (uint32_t t = t0; t < t1; ++t) ex += split_parts(plan_pick_packed(a, s_c[plan_lds_ix(t)], T, &e)) - 1u;
-        ex = block_sum64(ex, s_red);
-        if (iter == 0) want = (uint32_t)(ex < 0xffffffffull ? ex : 0xffffffffull);
-        if (ex <= a.extra_cap) break;
-        T = iter < 23 ? T + T / 4u + 1u : ~0ull;  // the last resort: no tile split
-      }
+    tail = (uint64_t)mx * 4u > (uint64_t)L * 5u && mx > L + a.min_gain;
+  }
+  const uint64_t t_loaded = __builtin_amdgcn_s_memrealtime();
+  if (tail) {
+    const uint32_t F = (mx * 7u) / 20u;
+    T = L > F ? L : F;
+    // 2. the parts must fit the grid's budget: raise T until they do (the first count is the demand, reported)
+    for (int iter = 0; a.split && iter < 24; ++iter) {
+      uint32_t ex = 0, e;
+#pragma unroll 4
+      for (uint32_t t = tid; t < n; t += kPlanThreads)
+        ex += split_parts(plan_pick32(a, s_c[plan_lds_ix(t)], T, &e)) - 1u;
+      const uint64_t tot = block_sum64(ex, s_red);
+      if (iter == 0) want = (uint32_t)(tot < 0xffffffffull ? tot : 0xffffffffull);
+      if (tot <= a.extra_cap) break;
+      T = (iter < 23 && T < 65535u) ? T + T / 4u + 1u : 0xffffffffu;  // the last resort: no tile split
     }
   }
+  const uint64_t t_budget = __builtin_amdgcn_s_memrealtime();
   uint32_t nsplit = 0, nitems = n;
   bool pays = false;
   if (!a.force && !tail) {
     // no tail: the plain grid's order, every tile whole
+#pragma unroll 4
     for (uint32_t t = tid; t < n; t += kPlanThreads) a.plan[1u + t] = t << 6;
   } else {
-    // two classes (estimated above front / 16 x L first), each in tile order
-    const uint64_t TF = (!a.force && a.front) ? (L * a.front) >> 4 : ~0ull;
-    uint32_t cf = 0, cb = 0, tf = 0;
-    uint64_t e = 0;
+    // 3. each tile's layout and class (estimated above front / 16 x L: first); thread i's run of tiles
+    // [m i, m i + m) counts its items, one block scan of the runs' (front, rest) counts places them, and each
+    // tile's first item position (with its layout) replaces its snapshot word
+    const uint32_t TF = (!a.force && a.front) ? (L * a.front) >> 4 : 0xffffffffu;
+    uint32_t cf = 0, cb = 0, tf = 0, e = 0;
+#pragma unroll 4
     for (uint32_t t = t0; t < t1; ++t) {
-      const uint32_t code = a.force ? plan_forced(a, t) : plan_pick_packed(a, s_c[plan_lds_ix(t)], T, &e);
+      const uint32_t code = a.force ? plan_forced(a, t) : plan_pick32(a, s_c[plan_lds_ix(t)], T, &e);
       const uint32_t k = split_parts(code);
       const bool fr = !a.force && e > TF;
       cf += fr ? k : 0u;
@@ -1947,15 +1947,22 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
     uint64_t tot;
     const uint64_t ex = block_excl_scan64(((uint64_t)cf << 32) | cb, s_red, &tot);
     uint32_t pf = (uint32_t)(ex >> 32), pb = (uint32_t)(tot >> 32) + (uint32_t)ex;
+#pragma unroll 4
     for (uint32_t t = t0; t < t1; ++t) {
-      const uint32_t code = a.force ? plan_forced(a, t) : plan_pick_packed(a, s_c[plan_lds_ix(t)], T, &e);
+      const uint32_t code = a.force ? plan_forced(a, t) : plan_pick32(a, s_c[plan_lds_ix(t)], T, &e);
       const uint32_t k = split_parts(code);
       const bool fr = !a.force && e > TF;
-      uint32_t pos = fr ? pf : pb;
-      for (uint32_t q = 0; q < k; ++q, ++pos)
-        if (pos < cap) a.plan[1u + pos] = (t << 6) | (q << 2) | code;  // always true: the budget holds
+      s_c[plan_lds_ix(t)] = ((fr ? pf : pb) << 2) | code;
       if (fr) pf += k;
       else pb += k;
+    }
+    __syncthreads();
+    // 4. the items, tile t by thread t % 1024 again: neighbouring lanes write neighbouring words
+#pragma unroll 4
+    for (uint32_t t = tid; t < n; t += kPlanThreads) {
+      const uint32_t d = s_c[plan_lds_ix(t)], code = d & 3u, k = split_parts(code), pos = d >> 2;
+      for (uint32_t q = 0; q < k; ++q)
+        if (pos + q < cap) a.plan[1u + pos + q] = (t << 6) | (q << 2) | code;  // always true: the budget holds
       // a split tile's part word restarts (its parts raise it with atomicMax at their end)
       if (!a.force && code) a.cost[2u * t + 1u] = 0u;
     }
@@ -1968,6 +1975,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
     const uint32_t nfront_tiles = (uint32_t)r;
     pays = nsplit > 0u || (n > a.slots && nfront_tiles > 0u && nfront_tiles < n);
   }
+  const uint64_t t_placed = __builtin_amdgcn_s_memrealtime();
   // diagnostics (PlanArgs::check): the list must cover every tile exactly once — each tile's items one layout, its
   // parts 0 .. k - 1 once each (the words after the items count them)
   uint32_t bad = 0, first_bad = 0xffffffffu, first_word = 0;
@@ -2012,11 +2020,15 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
       st->nitems = nitems;
       st->nsplit = nsplit;
       st->want_extra = want;
-      st->max_cost = (uint32_t)(mx < 0xffffffffull ? mx : 0xffffffffull);
+      st->max_cost = mx;
       st->mean_cost = n ? (uint32_t)(sum / n) : 0u;
-      st->threshold = (uint32_t)(T < 0xffffffffull ? T : 0xffffffffull);
+      st->threshold = T;
       st->pays = pays ? 1u : 0u;
       st->plans += 1u;
+      // thread 0's view of the phases (10-ns ticks): load + bound, budget, layout + positions + items
+      st->phase_ticks[0] = (uint32_t)(t_loaded - t_begin);
+      st->phase_ticks[1] = (uint32_t)(t_budget - t_loaded);
+      st->phase_ticks[2] = (uint32_t)(t_placed - t_budget);
       if (a.check) {
         st->bad += bad;
         if (bad && !st->first_bad_word) {
