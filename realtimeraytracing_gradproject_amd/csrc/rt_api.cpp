@@ -1075,11 +1075,14 @@ static BalanceMap* balance_map(rt_ctx* c, uint32_t W, uint32_t nrows, const uint
 // memory without a copy call (it may lag by a few launches: any list is a valid cover).
 constexpr uint64_t kReplan = 8, kRecheck = 32;
 
-static void balance_wants_plan(BalanceMap& m, bool* plan, bool* use) {
+// record: whether the launch's waves record their times. A shape whose list does not pay runs the plain kernel
+// and records only on the launch before a re-check (the plan reads those times).
+static void balance_wants_plan(BalanceMap& m, bool* plan, bool* use, bool* record) {
   const volatile rt::PlanStats* st = m.stats;
   const uint32_t plans = st->plans, want = st->want_extra;
   if (plans) m.extra_cap = std::min<uint64_t>((uint64_t)want + want / 4u + 64u, 15ull * m.ntiles);
   *plan = *use = false;
+  *record = true;
   if (m.launches == 0) return;
   if (m.cur < 0) {
     *plan = *use = true;
@@ -1089,6 +1092,7 @@ static void balance_wants_plan(BalanceMap& m, bool* plan, bool* use) {
   *use = st->pays != 0;
   *plan = age >= (*use ? kReplan : kRecheck);
   if (*plan) *use = true;
+  *record = *use || age + 1u >= kRecheck;
 }
 
 // The current list stops being current: one event per stream that launched with it (covering all of that stream's
@@ -1178,9 +1182,9 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
     const bool active = forced || s == m->last_stream || prev_done;
     m->last_stream = s;
     bm = m;
-    c->fp.cost = (active && !forced) ? m->cost : nullptr;
-    bool plan = forced, use = forced;
-    if (active && !forced) balance_wants_plan(*m, &plan, &use);
+    bool plan = forced, use = forced, record = false;
+    if (active && !forced) balance_wants_plan(*m, &plan, &use, &record);
+    c->fp.cost = record ? m->cost : nullptr;
     rt::PlanArgs a;
     a.cost = m->cost;
     a.stats = forced ? nullptr : m->stats_dev;

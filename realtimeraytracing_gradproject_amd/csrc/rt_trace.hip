@@ -1467,7 +1467,9 @@ __host__ __device__ constexpr int packet_block(int ks) { return 64 * packet_wx(k
 static_assert(packet_block(1) <= 64 * kMaxPacketWaves && packet_block(2) <= 64 * kMaxPacketWaves,
               "lane_subtree's LDS stacks: one per wave of a packet workgroup");
 
-template <int MODE, bool STATS, int R, int KS>
+// BAL: the launch runs a tile-balance work list or records the waves' times (FrameParams::plan / cost); the plain
+// grid's kernel carries none of it (a 64-bit start time and the slot live across the whole walk cost registers)
+template <int MODE, bool STATS, int R, int KS, bool BAL>
 __global__ __launch_bounds__(packet_block(KS)) __attribute__((amdgpu_waves_per_eu(
     (MODE == 1 && !STATS) ? (KS == 0 ? RT_SPP_WAVES : (KS == 1 ? RT_LS_WAVES : RT_KS_WAVES))
     : (MODE == 3 && !STATS) ? (KS == 0 ? RT_SPP_WAVES : (KS == 1 ? RT_REF0_WAVES : RT_KS_WAVES))
@@ -1491,7 +1493,7 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
   // balance): a whole tile or one part of a split one, costliest first. All uniform (SALU).
   uint32_t bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z, slot = 0, split = 0, part = 0;
   uint64_t t_wave = 0;
-  if (fp.plan) {
+  if (BAL && fp.plan) {
     const RT_CONST uint32_t* plan = (const RT_CONST uint32_t*)fp.plan;
     const uint32_t i = blockIdx.x * WL + w;
     if (i >= plan[0]) return;  // the grid is sized for the list's budget: the waves past its end have nothing
@@ -1504,10 +1506,10 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
     w = f - wg * WL;
     by = wg / fp.grid_x;
     bx = wg - by * fp.grid_x;
-  } else {
+  } else if (BAL) {
     slot = ((bz * gridDim.y + by) * gridDim.x + bx) * WL + w;
   }
-  if (fp.cost) t_wave = __builtin_amdgcn_s_memrealtime();
+  if (BAL && fp.cost) t_wave = __builtin_amdgcn_s_memrealtime();
   const uint32_t sample = lane % NS, pix = lane / NS;
   // split tiles: only the lanes of this part's sub-rectangle of the pixel tile trace (2 x 2 or 4 x 4 parts;
   // the others join the packets dead and store nothing)
@@ -1580,7 +1582,7 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
     }
   }
   if (STATS) flush_stats<true>(cnt, stats);
-  if (fp.cost && lane == 0u) {
+  if (BAL && fp.cost && lane == 0u) {
     // this wave's time (100 MHz ticks): a whole tile's into its first word, a part's into the second as the
     // costliest part of the tile's last split (time << 2 | layout; the plan kernel clears it when it splits)
     uint32_t dt = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_wave);
@@ -1707,8 +1709,16 @@ hipError_t launch_mode(const SceneView& sc, const FrameParams& fp, const uint32_
     // the plain grid, or (tile balance) one wave per work-list item, as many as the list's budget
     dim3 gp = fp.plan ? dim3((plan_items + g.wl - 1) / g.wl) : dim3(g.grid_x, g.grid_y, fp.nframes);
 #define RT_LAUNCH_PACKET(KS)                                                                                   \
-  hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R, (R == 1 ? KS : 0)>), gp, dim3(packet_block(R == 1 ? KS : 0)), 0, s, sc, fp, \
-                     rows, (uint32_t*)rgba8, (float4*)rgba32f, stats)
+  do {                                                                                                         \
+    if (fp.plan || fp.cost)                                                                                    \
+      hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R, (R == 1 ? KS : 0), true>), gp,                 \
+                         dim3(packet_block(R == 1 ? KS : 0)), 0, s, sc, fp, rows, (uint32_t*)rgba8,           \
+                         (float4*)rgba32f, stats);                                                             \
+    else                                                                                                       \
+      hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R, (R == 1 ? KS : 0), false>), gp,                \
+                         dim3(packet_block(R == 1 ? KS : 0)), 0, s, sc, fp, rows, (uint32_t*)rgba8,           \
+                         (float4*)rgba32f, stats);                                                             \
+  } while (0)
     if (ks == 1) RT_LAUNCH_PACKET(1);
     else if (ks == 2) RT_LAUNCH_PACKET(2);
     else if (ks == 4) RT_LAUNCH_PACKET(4);

@@ -1,6 +1,6 @@
 set -u
 cd $GRAFT_REPO_ROOT
-STEPS="tests" TAG=r04j PYTEST_K="balance or variants" bash tools/gpu_r04.sh || exit 1
-timeout -k 10 600 python3 tools/lib_ab.py --roots ab/r03,. --configs C2,C2F,C4 --rounds 3 > gpurun_out/lib_ab_r04j.txt 2>&1 || { echo lib_ab failed; tail -20 gpurun_out/lib_ab_r04j.txt; exit 1; }
-tail -40 gpurun_out/lib_ab_r04j.txt
-STEPS="balance" TAG=r04j BAL_ARGS="--configs C4,C2F,C2 --shares 1,4,8 --rounds 3 --variants b0,b1" bash tools/gpu_r04.sh
+STEPS="tests" TAG=r04l PYTEST_K="balance or variants" bash tools/gpu_r04.sh || exit 1
+timeout -k 10 900 python3 tools/lib_ab.py --roots ab/r03,.,.:bal0 --configs C2,C2F,C4 --rounds 3 > gpurun_out/lib_ab_r04l.txt 2>&1 || { echo lib_ab failed; tail -20 gpurun_out/lib_ab_r04l.txt; exit 1; }
+python3 -c "
+import json;t=open('gpurun_out/lib_ab_r04l.txt').read();d=json.loads(t[t.index('{\n'):]);print(json.dumps(d['median_ms']))"

@@ -17,12 +17,14 @@ sys.path.insert(0, sys.argv[1])
 import torch
 import realtimeraytracing_gradproject_amd as rt
 from realtimeraytracing_gradproject_amd import scenes
-assert rt.__file__.startswith(sys.argv[1]), rt.__file__
+assert rt.__file__.startswith(sys.argv[1].split(":")[0]), rt.__file__
 res = {}
 for name in sys.argv[2].split(","):
     spec = scenes.config(name)
     c = rt.Context(0)
     scenes.upload(c, spec)
+    if sys.argv[3] == "0":
+        c.set_tile_balance(0)
     W, H = spec.width, spec.height
     bufs = [torch.empty((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(3)]
     ss = [torch.cuda.Stream() for _ in range(3)]
@@ -43,23 +45,26 @@ print(json.dumps(res))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--roots", default="ab/r03,.")
+    ap.add_argument("--roots", default="ab/r03,.", help="builds; <root>:bal0 runs that build with the balance off")
     ap.add_argument("--configs", default="C2,C2F,C4")
     ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
-    roots = [os.path.abspath(os.path.join(ROOT, r)) for r in a.roots.split(",")]
+    roots = a.roots.split(",")
     out = {}
     for rnd in range(a.rounds):
         for r in roots:
-            p = subprocess.run([sys.executable, "-c", CHILD, r, a.configs], capture_output=True, text=True, timeout=300)
+            path = os.path.abspath(os.path.join(ROOT, r.split(":")[0]))
+            bal = "0" if r.endswith(":bal0") else "1"
+            p = subprocess.run([sys.executable, "-c", CHILD, path, a.configs, bal], capture_output=True, text=True,
+                               timeout=300)
             if p.returncode != 0:
                 print(p.stderr[-2000:], flush=True)
                 sys.exit(1)
             res = json.loads(p.stdout.strip().splitlines()[-1])
             for cfg, v in res.items():
                 for k, ms in v.items():
-                    out.setdefault(cfg, {}).setdefault(f"{os.path.relpath(r, ROOT)}:{k}", []).append(round(ms, 4))
-            print(rnd, os.path.relpath(r, ROOT), json.dumps(res), flush=True)
+                    out.setdefault(cfg, {}).setdefault(f"{r}:{k}", []).append(round(ms, 4))
+            print(rnd, r, json.dumps(res), flush=True)
     med = {cfg: {k: sorted(v)[len(v) // 2] for k, v in d.items()} for cfg, d in out.items()}
     print(json.dumps({"median_ms": med, "runs": out}, indent=1))
 
