@@ -31,6 +31,15 @@ autotune (pick_in_flight, per rank) and reported as config.frames_in_flight besi
 value = rays traced in one step (all ranks, counted by the device counters in an untimed pass)
 x steps / max-over-ranks wall time of the timed region.
 
+The other configs under "extra" are timed over max(50, steps / 4) frames (multi-sample C5: max(10,
+steps / 20)): with the driver's 20 steps a quarter of them was 5 frames, 0.07 ms of C1, where the host's issue and
+the synchronise return dominated (the driver's BENCH_r03.json read C1 17.0 and C2F 67.2 Grays/s against 31.4 /
+88.3 over 50 frames).
+
+Tile balance (rt_set_tile_balance, the library's default): off while frames are in flight (the next frame fills
+the slots the slowest tiles leave idle), on for the one-stream frame time and a rank's share when frames run one
+at a time; config.tile_balance reports the last shape's plans.
+
 Untimed before the W warmup frames: a clock settle (--settle-ms of frames: the GPU needs ~20 ms of
 load to reach its steady clock; with 5 warmup frames alone the same build read 0.20 ms instead of
 0.15 ms per frame; the ranks agree on its length), the tile-rows and frames-in-flight autotunes,

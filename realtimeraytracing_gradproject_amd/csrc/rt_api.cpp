@@ -205,9 +205,7 @@ struct BalanceMap {
   rt::PlanStats* stats_dev = nullptr;
   uint32_t extra_cap = 0;
   uint64_t launches = 0, tick = 0;   // launches: those with the balance active
-  hipStream_t last_stream = nullptr; // the stream of the shape's previous launch
-  hipEvent_t done = nullptr;         // recorded after each launch of the shape
-  bool done_recorded = false;
+  hipStream_t last_stream = nullptr; // the stream of the shape's previous launch (cleared by rt_forget_stream)
   ScratchSlot list[2];               // work lists; uses recorded when a list stops being current
   int cur = -1;                      // the current list (its plan kernel enqueued), or none
   uint32_t cur_items = 0;            // its launch's grid budget (tiles + extra waves)
@@ -221,7 +219,6 @@ struct BalanceMap {
     slot_release(list[0]);
     slot_release(list[1]);
     if (ready) (void)hipEventDestroy(ready);
-    if (done) (void)hipEventDestroy(done);
     *this = BalanceMap();
   }
 };
@@ -1000,6 +997,7 @@ hipError_t ctx_forget_stream(rt_ctx* c, hipStream_t s) {
   // the tile balance's lists: the same for their readers; a later stream with the same handle must wait for
   // `ready` itself
   for (BalanceMap& m : c->bal) {
+    if (m.last_stream == s) m.last_stream = nullptr;
     m.waited.erase(std::remove(m.waited.begin(), m.waited.end(), s), m.waited.end());
     auto it = std::find(m.readers.begin(), m.readers.end(), s);
     if (it == m.readers.end() || m.cur < 0) continue;
@@ -1161,7 +1159,6 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
   c->fp.waves_per_frame = g.waves_per_frame;
   uint32_t plan_items = 0;
   ScratchSlot* plan_slot = nullptr;
-  BalanceMap* bm = nullptr;
   const bool forced = c->balance >= 2;
   if (forced && (uint64_t)g.waves_per_frame * nframes > rt::kPlanMaxTiles)
     return fail(c, RT_E_UNSUPPORTED, "tile balance: forced layouts take at most 32768 waves per launch");
@@ -1176,12 +1173,10 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
     c->bal_last = m;
     // frames in flight (the shape's previous launch still runs on another stream): the next frame's waves already
     // fill the slots the slowest tiles leave idle, so the balance only adds work there (split parts, the plan). It
-    // runs when this launch follows the previous one on its stream or the previous one has finished (frame
-    // latency: one frame at a time, a rank's share of a frame).
-    const bool prev_done = !m->done_recorded || hipEventQuery(m->done) == hipSuccess;
-    const bool active = forced || s == m->last_stream || prev_done;
+    // runs when this launch follows the previous one on its stream or that stream has drained (frame latency: one
+    // frame at a time, a rank's share of a frame). A host query of the stream: no event in the launch's stream.
+    const bool active = forced || s == m->last_stream || !m->last_stream || hipStreamQuery(m->last_stream) == hipSuccess;
     m->last_stream = s;
-    bm = m;
     bool plan = forced, use = forced, record = false;
     if (active && !forced) balance_wants_plan(*m, &plan, &use, &record);
     c->fp.cost = record ? m->cost : nullptr;
@@ -1249,11 +1244,6 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
   HIPCHK(c, note_reader(c->ver[c->cur], s), "rt_dispatch_rays: record use");
   if (ovf_slot) HIPCHK(c, slot_mark_use(*ovf_slot, s), "overflow stack: record use");
   if (plan_slot) HIPCHK(c, slot_mark_use(*plan_slot, s), "tile plan: record use");
-  if (bm) {
-    if (!bm->done && !(bm->done = new_sync_event())) return fail(c, RT_E_HIP, "tile balance: event");
-    HIPCHK(c, hipEventRecord(bm->done, s), "tile balance: record the launch");
-    bm->done_recorded = true;
-  }
   if (c->stats_on) {
     c->dispatches += nframes;
     c->pixels += (uint64_t)W * nrows * nframes;

@@ -25,7 +25,7 @@ for step in ${STEPS:-tests}; do
     waves)
       for b in 0 1; do
         timeout -k 10 120 python3 tools/wave_times.py --lib realtimeraytracing_gradproject_amd/lib/variants/wavetimes/librtamd.so \
-          --config ${WT_CONFIG:-C4} --balance $b > "$O/wave_times_${TAG}_b$b.txt" 2>&1 \
+          --config ${WT_CONFIG:-C4} --balance $b ${WT_ARGS:-} > "$O/wave_times_${TAG}_b$b.txt" 2>&1 \
           || { echo "wave_times failed rc=$?"; tail -20 "$O/wave_times_${TAG}_b$b.txt"; exit 1; }
         cat "$O/wave_times_${TAG}_b$b.txt"
       done ;;

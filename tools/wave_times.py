@@ -19,20 +19,23 @@ ap.add_argument("--lib", required=True)
 ap.add_argument("--config", default="C2")
 ap.add_argument("--frames", type=int, default=30)
 ap.add_argument("--balance", type=int, default=1, help="rt_set_tile_balance mode (0: the plain grid)")
+ap.add_argument("--share", type=int, default=1, help="rank 0's interleaved 8-row strips of a frame over N ranks")
 a = ap.parse_args()
 spec = scenes.config(a.config)
 c = rt.Context(0, library=rt._load(a.lib))
 scenes.upload(c, spec)
 c.set_tile_balance(a.balance)
 W, H = spec.width, spec.height
-out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
-tb = torch.zeros((H * W * 4,), dtype=torch.float32, device="cuda")
+rows = None if a.share == 1 else rt.strip_rows(H, a.share, 0)
+NR = H if rows is None else len(rows)
+out = torch.zeros((NR, W, 4), dtype=torch.uint8, device="cuda")
+tb = torch.zeros((NR * W * 4,), dtype=torch.float32, device="cuda")  # 16 B per pixel: room for every wave record
 s = torch.cuda.current_stream().cuda_stream
 for _ in range(a.frames):
-    c.dispatch(W, H, out, tb.view(H, W, 4), stream=s)
+    c.dispatch(W, H, out, tb.view(NR, W, 4), rows=rows, stream=s)
 torch.cuda.synchronize()
 tb.zero_()
-c.dispatch(W, H, out, tb.view(H, W, 4), stream=s)
+c.dispatch(W, H, out, tb.view(NR, W, 4), rows=rows, stream=s)
 torch.cuda.synchronize()
 u = tb.view(torch.int32).cpu().numpy().astype(np.uint32).reshape(-1, 4)
 live = u[:, 1] != 0
@@ -43,7 +46,7 @@ base = t0.min()
 t0 -= base
 t1 -= base
 T = t1.max()
-print(f"{a.config}: {len(u)} waves, frame {T * 10 / 1000:.1f} us (100 MHz clock), tile balance {a.balance}: "
+print(f"{a.config} share 1/{a.share}: {len(u)} waves, frame {T * 10 / 1000:.1f} us (100 MHz clock), tile balance {a.balance}: "
       f"{c.tile_balance_info()}")
 dur = (t1 - t0) * 10 / 1000
 print(f"wave duration us: mean {dur.mean():.2f} p50 {np.median(dur):.2f} p90 {np.percentile(dur, 90):.2f} "
@@ -62,5 +65,5 @@ for x in range(8):
     m = xcc == x
     if m.any():
         print(f"XCC {x}: waves {m.sum()} last end {t1[m].max() * 10 / 1000:.1f} us mean dur {dur[m].mean():.2f} us")
-np.savez(os.path.join(ROOT, "gpurun_out", f"wt_{a.config}_b{a.balance}.npz"), t0=t0, t1=t1, ids=np.nonzero(live)[0], xcc=xcc)
+np.savez(os.path.join(ROOT, "gpurun_out", f"wt_{a.config}_n{a.share}_b{a.balance}.npz"), t0=t0, t1=t1, ids=np.nonzero(live)[0], xcc=xcc)
 c.close()
