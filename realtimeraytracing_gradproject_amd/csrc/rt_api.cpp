@@ -194,9 +194,11 @@ hipError_t note_reader(TlasVersion& v, hipStream_t s) {
 // Tile balance (rt_set_tile_balance) of one launch shape (frame size, row list, frames per launch, tile layout):
 // the per-tile wave times the packet kernel leaves (FrameParams::cost), the plan kernel's summary in host-mapped
 // memory, the work list's budget of extra waves for split tiles, and the shape's work lists. A list is a valid
-// cover of the shape's tiles whatever costs it was planned from, so launches reuse the current one and the plan
-// kernel runs again only every few launches (balance_wants_plan). Two lists: the current one, and the one before it,
-// which launches on other streams may still be reading; the next plan overwrites that older one, ordered after them.
+// cover of the shape's tiles whatever costs it was planned from, so launches reuse the current one, the plan kernel
+// runs again only every few launches (balance_wants_plan), and it runs OFF the launches' streams: on the context's
+// low-priority plan stream, and a launch switches to the new list once a host query finds its plan complete (no
+// launch ever waits for a plan). Two lists: the current one, and the other — the one before it, which launches on
+// other streams may still be reading; the next plan overwrites it, ordered after them.
 struct BalanceMap {
   uint32_t W = 0, nrows = 0, nframes = 0, tile_rows = 0, spp = 0, ntiles = 0;
   const uint32_t* rows = nullptr;
@@ -207,18 +209,21 @@ struct BalanceMap {
   uint64_t launches = 0, tick = 0;   // launches: those with the balance active
   hipStream_t last_stream = nullptr; // the stream of the shape's previous launch (cleared by rt_forget_stream)
   ScratchSlot list[2];               // work lists; uses recorded when a list stops being current
-  int cur = -1;                      // the current list (its plan kernel enqueued), or none
+  int cur = -1;                      // the current list (its plan complete), or none
   uint32_t cur_items = 0;            // its launch's grid budget (tiles + extra waves)
-  uint64_t planned_at = 0;           // launches of the shape when it was planned
-  hipEvent_t ready = nullptr;        // recorded after the current list's plan kernel
-  std::vector<hipStream_t> waited;   // streams ordered after `ready`
+  int pending = -1;                  // the list a plan kernel is writing, or none
+  uint32_t pending_items = 0;
+  uint64_t planned_at = 0;           // launches of the shape when the last plan started
+  hipEvent_t pend_ev = nullptr;      // recorded on the plan stream after the pending plan
+  hipEvent_t src_ev = nullptr;       // recorded on the launch's stream: the plan starts after its earlier work
   std::vector<hipStream_t> readers;  // streams that launched with the current list since it became current
   void release() {
     if (cost) (void)hipFree(cost);
     if (stats) (void)hipHostFree(stats);
     slot_release(list[0]);
     slot_release(list[1]);
-    if (ready) (void)hipEventDestroy(ready);
+    if (pend_ev) (void)hipEventDestroy(pend_ev);
+    if (src_ev) (void)hipEventDestroy(src_ev);
     *this = BalanceMap();
   }
 };
@@ -260,6 +265,7 @@ struct rt_ctx {
   // tile balance (rt_set_tile_balance): 0 off, 1 adaptive, 2 / 3 / 4 forced layouts (tests); one cost map per launch
   // shape (least recently used of kMaxBalanceMaps replaced); the work lists, one per launch in flight, from a ring
   int balance = 1;
+  hipStream_t plan_stream = nullptr;  // the adaptive plans' stream (lowest priority; created on first use)
   // the adaptive plan's split of costly tiles and its front class (PlanArgs::split, front; A/B diagnostics:
   // RT_BALANCE_SPLIT, RT_BALANCE_FRONT at context creation) and the list's cover check (RT_BALANCE_CHECK, tests)
   uint32_t bal_split = 1, bal_front = 8, bal_check = 0;
@@ -510,6 +516,7 @@ rt_status rt_destroy(rt_ctx_t c) {
     if (p) (void)hipFree(p);
   if (c->raster_total_host) (void)hipHostFree(c->raster_total_host);
   (void)hipStreamDestroy(c->stream);
+  if (c->plan_stream) (void)hipStreamDestroy(c->plan_stream);
   delete c;
   return RT_OK;
 }
@@ -994,11 +1001,9 @@ hipError_t ctx_forget_stream(rt_ctx* c, hipStream_t s) {
     const hipError_t e = slot_mark_use(v.use, s);  // covers every launch of s so far
     if (e != hipSuccess && first == hipSuccess) first = e;
   }
-  // the tile balance's lists: the same for their readers; a later stream with the same handle must wait for
-  // `ready` itself
+  // the tile balance's lists: the same for their readers
   for (BalanceMap& m : c->bal) {
     if (m.last_stream == s) m.last_stream = nullptr;
-    m.waited.erase(std::remove(m.waited.begin(), m.waited.end(), s), m.waited.end());
     auto it = std::find(m.readers.begin(), m.readers.end(), s);
     if (it == m.readers.end() || m.cur < 0) continue;
     m.readers.erase(it);
@@ -1066,11 +1071,11 @@ static BalanceMap* balance_map(rt_ctx* c, uint32_t W, uint32_t nrows, const uint
   return m;
 }
 
-// Adaptive mode: whether this launch runs the plan kernel (a new list), and whether it runs with the shape's current
-// list at all. Not before the shape has wave times. A list that differs from the plain order (the last plan's
-// `pays`) is used by every launch and re-planned every kReplan launches (the costs drift with the camera);
-// otherwise the launches take the plain grid and one in kRecheck plans again. The summary is read from host-mapped
-// memory without a copy call (it may lag by a few launches: any list is a valid cover).
+// Adaptive mode: whether this launch starts a plan (the next list, on the plan stream), and whether it runs with the
+// shape's current list at all. Not before the shape has wave times. A list that differs from the plain order (the
+// last plan's `pays`) is used by every launch and re-planned every kReplan launches (the costs drift with the
+// camera); otherwise the launches take the plain grid and one in kRecheck plans again. One plan at a time per
+// shape. The summary is read from host-mapped memory without a copy call (it may lag: any list is a valid cover).
 constexpr uint64_t kReplan = 8, kRecheck = 32;
 
 // record: whether the launch's waves record their times. A shape whose list does not pay runs the plain kernel
@@ -1082,15 +1087,14 @@ static void balance_wants_plan(BalanceMap& m, bool* plan, bool* use, bool* recor
   *plan = *use = false;
   *record = true;
   if (m.launches == 0) return;
-  if (m.cur < 0) {
-    *plan = *use = true;
+  if (m.cur < 0) {  // the first list: the plain grid (recording) until it is ready
+    *plan = m.pending < 0;
     return;
   }
   const uint64_t age = m.launches - m.planned_at;
   *use = st->pays != 0;
-  *plan = age >= (*use ? kReplan : kRecheck);
-  if (*plan) *use = true;
-  *record = *use || age + 1u >= kRecheck;
+  *plan = m.pending < 0 && age >= (*use ? kReplan : kRecheck);
+  *record = *use || age + 1u >= kRecheck || m.pending >= 0;
 }
 
 // The current list stops being current: one event per stream that launched with it (covering all of that stream's
@@ -1207,30 +1211,41 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
       a.plan = (uint32_t*)plan_slot->buf;
       HIPCHK(c, rt::launch_tile_plan(a, s), "tile plan launch");
       c->fp.plan = a.plan;
-    } else {
+    } else if (active) {
+      // the pending list is ready: it becomes the current one (the old one's readers recorded for the next plan)
+      if (m->pending >= 0 && hipEventQuery(m->pend_ev) == hipSuccess) {
+        HIPCHK(c, balance_swap_out(*m), "tile balance: record the list's readers");
+        m->cur = m->pending;
+        m->cur_items = m->pending_items;
+        m->pending = -1;
+      }
       if (plan) {
-        // the next list goes into the older buffer, after every launch that read it
+        // the next list goes into the other buffer, on the plan stream, after every launch that read that buffer
+        // and after this stream's earlier work (the costs it recorded); this launch keeps the current list
+        if (!c->plan_stream) {
+          int least = 0, greatest = 0;
+          (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+          HIPCHK(c, hipStreamCreateWithPriority(&c->plan_stream, hipStreamNonBlocking, least), "plan stream");
+        }
+        hipStream_t ps = c->plan_stream;
         const int b = m->cur < 0 ? 0 : 1 - m->cur;
         ScratchSlot& sl = m->list[b];
-        HIPCHK(c, slot_order_after_others(sl, s), "tile balance: order after the list's readers");
-        HIPCHK(c, balance_swap_out(*m), "tile balance: record the list's readers");
+        if ((!m->pend_ev && !(m->pend_ev = new_sync_event())) || (!m->src_ev && !(m->src_ev = new_sync_event())))
+          return fail(c, RT_E_HIP, "tile balance: event");
+        HIPCHK(c, hipEventRecord(m->src_ev, s), "tile balance: record the launch stream");
+        HIPCHK(c, hipStreamWaitEvent(ps, m->src_ev, 0), "tile balance: order the plan");
+        HIPCHK(c, slot_order_after_others(sl, ps), "tile balance: order after the list's readers");
         a.extra_cap = m->extra_cap;
         const uint32_t items = ntiles + a.extra_cap;
         HIPCHK(c, slot_reserve(sl, ((size_t)items + 2u * ntiles + 1) * 4), "hipMalloc(tile plan)");
         a.plan = (uint32_t*)sl.buf;
-        HIPCHK(c, rt::launch_tile_plan(a, s), "tile plan launch");
-        if (!m->ready && !(m->ready = new_sync_event())) return fail(c, RT_E_HIP, "tile balance: event");
-        HIPCHK(c, hipEventRecord(m->ready, s), "tile balance: record the plan");
-        m->waited.assign(1, s);
-        m->cur = b;
-        m->cur_items = items;
+        HIPCHK(c, rt::launch_tile_plan(a, ps), "tile plan launch");
+        HIPCHK(c, hipEventRecord(m->pend_ev, ps), "tile balance: record the plan");
+        m->pending = b;
+        m->pending_items = items;
         m->planned_at = m->launches;
       }
       if (use && m->cur >= 0) {
-        if (std::find(m->waited.begin(), m->waited.end(), s) == m->waited.end()) {
-          HIPCHK(c, hipStreamWaitEvent(s, m->ready, 0), "tile balance: wait for the plan");
-          m->waited.push_back(s);
-        }
         if (std::find(m->readers.begin(), m->readers.end(), s) == m->readers.end()) m->readers.push_back(s);
         c->fp.plan = (const uint32_t*)m->list[m->cur].buf;
         plan_items = m->cur_items;
