@@ -196,8 +196,8 @@ hipError_t note_reader(TlasVersion& v, hipStream_t s) {
 // memory, the work list's budget of extra waves for split tiles, and the shape's work lists. A list is a valid
 // cover of the shape's tiles whatever costs it was planned from, so launches reuse the current one, the plan kernel
 // runs again only every few launches (balance_wants_plan), and it runs OFF the launches' streams: on the context's
-// low-priority plan stream, and a launch switches to the new list once a host query finds its plan complete (no
-// launch ever waits for a plan). Two lists: the current one, and the other — the one before it, which launches on
+// own stream (a further stream would change which of the caller's streams share a hardware queue), and a launch
+// switches to the new list once a host query finds its plan complete (no launch ever waits for a plan). Two lists: the current one, and the other — the one before it, which launches on
 // other streams may still be reading; the next plan overwrites it, ordered after them.
 struct BalanceMap {
   uint32_t W = 0, nrows = 0, nframes = 0, tile_rows = 0, spp = 0, ntiles = 0;
@@ -208,6 +208,7 @@ struct BalanceMap {
   uint32_t extra_cap = 0;
   uint64_t launches = 0, tick = 0;   // launches: those with the balance active
   hipStream_t last_stream = nullptr; // the stream of the shape's previous launch (cleared by rt_forget_stream)
+  uint32_t active_run = 0;           // launches in a row with the balance active
   ScratchSlot list[2];               // work lists; uses recorded when a list stops being current
   int cur = -1;                      // the current list (its plan complete), or none
   uint32_t cur_items = 0;            // its launch's grid budget (tiles + extra waves)
@@ -265,7 +266,6 @@ struct rt_ctx {
   // tile balance (rt_set_tile_balance): 0 off, 1 adaptive, 2 / 3 / 4 forced layouts (tests); one cost map per launch
   // shape (least recently used of kMaxBalanceMaps replaced); the work lists, one per launch in flight, from a ring
   int balance = 1;
-  hipStream_t plan_stream = nullptr;  // the adaptive plans' stream (lowest priority; created on first use)
   // the adaptive plan's split of costly tiles and its front class (PlanArgs::split, front; A/B diagnostics:
   // RT_BALANCE_SPLIT, RT_BALANCE_FRONT at context creation) and the list's cover check (RT_BALANCE_CHECK, tests)
   uint32_t bal_split = 1, bal_front = 8, bal_check = 0;
@@ -516,7 +516,6 @@ rt_status rt_destroy(rt_ctx_t c) {
     if (p) (void)hipFree(p);
   if (c->raster_total_host) (void)hipHostFree(c->raster_total_host);
   (void)hipStreamDestroy(c->stream);
-  if (c->plan_stream) (void)hipStreamDestroy(c->plan_stream);
   delete c;
   return RT_OK;
 }
@@ -1076,10 +1075,14 @@ static BalanceMap* balance_map(rt_ctx* c, uint32_t W, uint32_t nrows, const uint
 // last plan's `pays`) is used by every launch and re-planned every kReplan launches (the costs drift with the
 // camera); otherwise the launches take the plain grid and one in kRecheck plans again. One plan at a time per
 // shape. The summary is read from host-mapped memory without a copy call (it may lag: any list is a valid cover).
-constexpr uint64_t kReplan = 8, kRecheck = 32;
+constexpr uint64_t kReplan = 8, kRecheck = 32, kRecheckNoTail = 128;
 
 // record: whether the launch's waves record their times. A shape whose list does not pay runs the plain kernel
 // and records only on the launch before a re-check (the plan reads those times).
+// A plan starts only on the second active launch in a row (the first launch after the caller drained its streams
+// is active too, and a plan started there would run beside the frames in flight that follow). A shape whose last
+// plan found no tail at all re-checks every kRecheckNoTail launches, one whose tail splitting could not shorten
+// every kRecheck.
 static void balance_wants_plan(BalanceMap& m, bool* plan, bool* use, bool* record) {
   const volatile rt::PlanStats* st = m.stats;
   const uint32_t plans = st->plans, want = st->want_extra;
@@ -1087,14 +1090,16 @@ static void balance_wants_plan(BalanceMap& m, bool* plan, bool* use, bool* recor
   *plan = *use = false;
   *record = true;
   if (m.launches == 0) return;
+  const bool may_plan = m.pending < 0 && m.active_run >= 2u;
   if (m.cur < 0) {  // the first list: the plain grid (recording) until it is ready
-    *plan = m.pending < 0;
+    *plan = may_plan;
     return;
   }
   const uint64_t age = m.launches - m.planned_at;
   *use = st->pays != 0;
-  *plan = m.pending < 0 && age >= (*use ? kReplan : kRecheck);
-  *record = *use || age + 1u >= kRecheck || m.pending >= 0;
+  const uint64_t every = *use ? kReplan : (st->threshold == 0xffffffffu ? kRecheckNoTail : kRecheck);
+  *plan = may_plan && age >= every;
+  *record = *use || age + 1u >= every || m.pending >= 0;
 }
 
 // The current list stops being current: one event per stream that launched with it (covering all of that stream's
@@ -1181,6 +1186,7 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
     // frame at a time, a rank's share of a frame). A host query of the stream: no event in the launch's stream.
     const bool active = forced || s == m->last_stream || !m->last_stream || hipStreamQuery(m->last_stream) == hipSuccess;
     m->last_stream = s;
+    m->active_run = active ? m->active_run + 1u : 0u;
     bool plan = forced, use = forced, record = false;
     if (active && !forced) balance_wants_plan(*m, &plan, &use, &record);
     c->fp.cost = record ? m->cost : nullptr;
@@ -1222,12 +1228,7 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
       if (plan) {
         // the next list goes into the other buffer, on the plan stream, after every launch that read that buffer
         // and after this stream's earlier work (the costs it recorded); this launch keeps the current list
-        if (!c->plan_stream) {
-          int least = 0, greatest = 0;
-          (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
-          HIPCHK(c, hipStreamCreateWithPriority(&c->plan_stream, hipStreamNonBlocking, least), "plan stream");
-        }
-        hipStream_t ps = c->plan_stream;
+        hipStream_t ps = c->stream;
         const int b = m->cur < 0 ? 0 : 1 - m->cur;
         ScratchSlot& sl = m->list[b];
         if ((!m->pend_ev && !(m->pend_ev = new_sync_event())) || (!m->src_ev && !(m->src_ev = new_sync_event())))

@@ -1877,10 +1877,10 @@ __device__ __forceinline__ uint32_t plan_pack(uint32_t w, uint32_t p) {
 
 // the layout of a tile from its snapshot word (w16 | p16 << 16) and its estimated time; 32-bit: a time is at most
 // 65535 ticks, and T (0xffffffff: split nothing) is below 65535 wherever a tile exceeds it
-__device__ __forceinline__ uint32_t plan_pick32(const PlanArgs& a, uint32_t c, uint32_t T, uint32_t* est) {
+__device__ __forceinline__ uint32_t plan_pick32(const PlanArgs& a, bool split, uint32_t c, uint32_t T, uint32_t* est) {
   const uint32_t w = c & 0xffffu, p16 = c >> 16, pt = (p16 >> 2) << 2;  // the part's time in ticks
   uint32_t code = 0;
-  if (a.split && a.kmax_code && w > T) code = (a.kmax_code == 1u || w * 11u <= T * 20u) ? 1u : 2u;
+  if (split && a.kmax_code && w > T) code = (a.kmax_code == 1u || w * 11u <= T * 20u) ? 1u : 2u;
   // the last split of this tile measured a part above 0.8 x the whole: splitting does not pay there
   if (code && p16 && pt * 5u > w * 4u) code = 0u;
   *est = code == 0u ? w : (p16 && (p16 & 3u) == code) ? pt : (code == 1u ? (w * 11u) / 20u : (w * 7u) / 20u);
@@ -1895,6 +1895,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
   const uint32_t m = (n + kPlanThreads - 1) / kPlanThreads, t0 = tid * m, t1 = t0 + m < n ? t0 + m : n;
   // 1. the snapshot (coalesced loads, tile t by thread t % 1024, unrolled so the loads overlap) and the load bound
   uint32_t lsum = 0, lmax = 0;  // < 32 tiles x 65535 per thread
+  uint32_t lsplits = 0;          // the tiles' measured splits: useless << 16 | useful
   if (!a.force) {
 #pragma unroll 8
     for (uint32_t t = tid; t < n; t += kPlanThreads) {
@@ -1903,14 +1904,20 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
       s_c[plan_lds_ix(t)] = c;
       lsum += c & 0xffffu;
       lmax = (c & 0xffffu) > lmax ? (c & 0xffffu) : lmax;
+      if (v.y && v.x) lsplits += ((uint64_t)(v.y >> 2) * 5u > (uint64_t)v.x * 4u) ? 0x10000u : 1u;
     }
   }
   uint32_t T = 0xffffffffu, mx = 0, L = 0, want = 0;
   uint64_t sum = 0;
-  bool tail = false;
+  bool tail = false, split = a.split != 0u;
   if (!a.force) {
     sum = block_sum64(lsum, s_red);  // its barriers also publish s_c
     mx = (uint32_t)block_max64(lmax, s_red);
+    // the shape's tiles are coherent (most measured splits had a part above 0.8 x the whole): no splitting at all,
+    // instead of learning it a few hundred tiles per plan
+    const uint64_t sp = block_sum64(((uint64_t)(lsplits >> 16) << 32) | (lsplits & 0xffffu), s_red);
+    const uint32_t useless = (uint32_t)(sp >> 32), useful = (uint32_t)sp;
+    if (useless >= 16u && useless > 3u * useful) split = false;
     L = (uint32_t)(sum / (a.slots ? a.slots : 1u));
     // the costliest tile outlasts the load bound by a quarter and by more than this kernel takes
     tail = (uint64_t)mx * 4u > (uint64_t)L * 5u && mx > L + a.min_gain;
@@ -1920,11 +1927,11 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
     const uint32_t F = (mx * 7u) / 20u;
     T = L > F ? L : F;
     // 2. the parts must fit the grid's budget: raise T until they do (the first count is the demand, reported)
-    for (int iter = 0; a.split && iter < 24; ++iter) {
+    for (int iter = 0; split && iter < 24; ++iter) {
       uint32_t ex = 0, e;
 #pragma unroll 4
       for (uint32_t t = tid; t < n; t += kPlanThreads)
-        ex += split_parts(plan_pick32(a, s_c[plan_lds_ix(t)], T, &e)) - 1u;
+        ex += split_parts(plan_pick32(a, split, s_c[plan_lds_ix(t)], T, &e)) - 1u;
       const uint64_t tot = block_sum64(ex, s_red);
       if (iter == 0) want = (uint32_t)(tot < 0xffffffffull ? tot : 0xffffffffull);
       if (tot <= a.extra_cap) break;
@@ -1946,7 +1953,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
     uint32_t cf = 0, cb = 0, tf = 0, e = 0;
 #pragma unroll 4
     for (uint32_t t = t0; t < t1; ++t) {
-      const uint32_t code = a.force ? plan_forced(a, t) : plan_pick32(a, s_c[plan_lds_ix(t)], T, &e);
+      const uint32_t code = a.force ? plan_forced(a, t) : plan_pick32(a, split, s_c[plan_lds_ix(t)], T, &e);
       const uint32_t k = split_parts(code);
       const bool fr = !a.force && e > TF;
       cf += fr ? k : 0u;
@@ -1959,7 +1966,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
     uint32_t pf = (uint32_t)(ex >> 32), pb = (uint32_t)(tot >> 32) + (uint32_t)ex;
 #pragma unroll 4
     for (uint32_t t = t0; t < t1; ++t) {
-      const uint32_t code = a.force ? plan_forced(a, t) : plan_pick32(a, s_c[plan_lds_ix(t)], T, &e);
+      const uint32_t code = a.force ? plan_forced(a, t) : plan_pick32(a, split, s_c[plan_lds_ix(t)], T, &e);
       const uint32_t k = split_parts(code);
       const bool fr = !a.force && e > TF;
       s_c[plan_lds_ix(t)] = ((fr ? pf : pb) << 2) | code;

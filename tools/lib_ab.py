@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Same-box A/B of two builds of the library (e.g. a past round's, built from its commit into ab/<name>/ — package and
 lib only, git-ignored — against the tree's): ms per frame with 3 frames in flight and one stream back to back,
-each build in its own process, alternating, medians over rounds.
+each build in its own process, alternating (the order reversed every other round), medians over rounds.
   python3 tools/lib_ab.py --roots ab/r03,. --configs C2,C2F,C4 --rounds 3"""
 import argparse
 import json
@@ -52,7 +52,7 @@ def main():
     roots = a.roots.split(",")
     out = {}
     for rnd in range(a.rounds):
-        for r in roots:
+        for r in (roots if rnd % 2 == 0 else roots[::-1]):  # alternate the order: no build always runs first
             path = os.path.abspath(os.path.join(ROOT, r.split(":")[0]))
             bal = "0" if r.endswith(":bal0") else "1"
             p = subprocess.run([sys.executable, "-c", CHILD, path, a.configs, bal], capture_output=True, text=True,
