@@ -1081,8 +1081,8 @@ constexpr uint64_t kReplan = 8, kRecheck = 32, kRecheckNoTail = 128;
 // and records only on the launch before a re-check (the plan reads those times).
 // A plan starts only on the second active launch in a row (the first launch after the caller drained its streams
 // is active too, and a plan started there would run beside the frames in flight that follow). A shape whose last
-// plan found no tail at all re-checks every kRecheckNoTail launches, one whose tail splitting could not shorten
-// every kRecheck.
+// plan found no tail at all, or whose tiles are coherent (no split helped), re-checks every kRecheckNoTail launches,
+// one whose tail splitting could not shorten every kRecheck.
 static void balance_wants_plan(BalanceMap& m, bool* plan, bool* use, bool* record) {
   const volatile rt::PlanStats* st = m.stats;
   const uint32_t plans = st->plans, want = st->want_extra;
@@ -1097,7 +1097,7 @@ static void balance_wants_plan(BalanceMap& m, bool* plan, bool* use, bool* recor
   }
   const uint64_t age = m.launches - m.planned_at;
   *use = st->pays != 0;
-  const uint64_t every = *use ? kReplan : (st->threshold == 0xffffffffu ? kRecheckNoTail : kRecheck);
+  const uint64_t every = *use ? kReplan : ((st->threshold == 0xffffffffu || st->coherent) ? kRecheckNoTail : kRecheck);
   *plan = may_plan && age >= every;
   *record = *use || age + 1u >= every || m.pending >= 0;
 }

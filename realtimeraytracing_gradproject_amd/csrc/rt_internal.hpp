@@ -97,6 +97,7 @@ struct PlanStats {
   // PlanArgs::check: tiles whose items were not exactly one layout's parts, summed over the plans; the first one
   uint32_t bad, first_bad_tile, first_bad_word;
   uint32_t phase_ticks[3];  // the last plan's phases: snapshot + load bound, budget, placement (10-ns ticks)
+  uint32_t coherent;        // the last plan found every measured split useless (it split nothing)
 };
 struct PlanArgs {
   uint32_t* cost;         // per wave slot of the plain grid, 2 words: the last whole wave's time (ticks), the
