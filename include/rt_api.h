@@ -226,10 +226,12 @@ rt_status rt_set_stats(rt_ctx_t ctx, int enable);
 rt_status rt_dispatch_rays(rt_ctx_t ctx, uint32_t W, uint32_t H, const uint32_t* rows,
                            uint32_t nrows, void* rgba8_dev, float* rgba32f_dev, void* hip_stream);
 /* Stream lifetime: the context notes (host-side, no event per launch) which streams launched with the current
- * TLAS version, and records one event on each of them when the next rt_tlas_build swaps that version out. A caller
- * that destroys a stream it launched on (rt_dispatch_rays, rt_trace_rays) before that build calls
- * rt_forget_stream(ctx, stream) first: the event is recorded now, while the stream is valid. (The reference's
- * command lists and fences have no equivalent: D3D12HelloTriangle.cpp:627-647 waits for the GPU every frame.) */
+ * TLAS version, and records one event on each of them when the next rt_tlas_build swaps that version out; the tile
+ * balance likewise notes the streams that read a work list, and queries the stream of a shape's previous launch
+ * (whether frames are in flight). A caller that destroys a stream it launched on (rt_dispatch_rays,
+ * rt_trace_rays) calls rt_forget_stream(ctx, stream) first: the events are recorded now, while the stream is valid,
+ * and the context holds no handle to it afterwards. (The reference's command lists and fences have no equivalent:
+ * D3D12HelloTriangle.cpp:627-647 waits for the GPU every frame.) */
 rt_status rt_forget_stream(rt_ctx_t ctx, void* hip_stream);
 
 /* TraceRay ray flags (the D3D12_RAY_FLAG values the reference passes, Common.hlsl:44-82). */
