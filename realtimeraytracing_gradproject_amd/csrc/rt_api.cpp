@@ -1091,15 +1091,18 @@ static void balance_wants_plan(BalanceMap& m, bool* plan, bool* use, bool* recor
   *record = true;
   if (m.launches == 0) return;
   const bool may_plan = m.pending < 0 && m.active_run >= 2u;
-  if (m.cur < 0) {  // the first list: the plain grid (recording) until it is ready
+  if (m.cur < 0) {  // the first list: the plain grid until it is ready, recording until its plan starts
     *plan = may_plan;
+    *record = m.pending < 0;
     return;
   }
   const uint64_t age = m.launches - m.planned_at;
   *use = st->pays != 0;
   const uint64_t every = *use ? kReplan : ((st->threshold == 0xffffffffu || st->coherent) ? kRecheckNoTail : kRecheck);
   *plan = may_plan && age >= every;
-  *record = *use || age + 1u >= every || m.pending >= 0;
+  // a launch with a list runs the recording kernel anyway; otherwise only the launch before a re-check records
+  // (not every launch issued while a plan is pending: a host running far ahead issues many of those)
+  *record = *use || age + 1u >= every;
 }
 
 // The current list stops being current: one event per stream that launched with it (covering all of that stream's
