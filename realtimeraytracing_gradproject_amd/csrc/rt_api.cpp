@@ -267,8 +267,9 @@ struct rt_ctx {
   // shape (least recently used of kMaxBalanceMaps replaced); the work lists, one per launch in flight, from a ring
   int balance = 1;
   // the adaptive plan's split of costly tiles and its front class (PlanArgs::split, front; A/B diagnostics:
-  // RT_BALANCE_SPLIT, RT_BALANCE_FRONT at context creation) and the list's cover check (RT_BALANCE_CHECK, tests)
-  uint32_t bal_split = 1, bal_front = 8, bal_check = 0;
+  // RT_BALANCE_SPLIT, RT_BALANCE_FRONT, RT_BALANCE_BUDGET — the extra waves as a divisor of the tiles — at context
+  // creation) and the list's cover check (RT_BALANCE_CHECK, tests)
+  uint32_t bal_split = 1, bal_front = 8, bal_check = 0, bal_budget = 4;
   static constexpr size_t kMaxBalanceMaps = 16;
   std::vector<BalanceMap> bal;
   uint64_t bal_clock = 0;
@@ -485,6 +486,8 @@ rt_status rt_create(int hip_device, rt_ctx_t* out) {
   if (const char* ev = std::getenv("RT_BALANCE_SPLIT")) c->bal_split = std::strtoul(ev, nullptr, 10) ? 1u : 0u;
   if (const char* ev = std::getenv("RT_BALANCE_FRONT")) c->bal_front = (uint32_t)std::strtoul(ev, nullptr, 10);
   if (const char* ev = std::getenv("RT_BALANCE_CHECK")) c->bal_check = std::strtoul(ev, nullptr, 10) ? 1u : 0u;
+  if (const char* ev = std::getenv("RT_BALANCE_BUDGET"))
+    c->bal_budget = std::max<uint32_t>(1u, (uint32_t)std::strtoul(ev, nullptr, 10));
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&c->d_stats, RT_STAT_COUNT * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(c->d_stats, 0, RT_STAT_COUNT * sizeof(unsigned long long)) != hipSuccess) {
@@ -1054,7 +1057,11 @@ static BalanceMap* balance_map(rt_ctx* c, uint32_t W, uint32_t nrows, const uint
   m->tile_rows = c->tile_rows;
   m->spp = c->fp.spp_side;
   m->ntiles = ntiles;
-  m->extra_cap = ntiles / 4u + 64u;
+  // the extra waves a list may add for split tiles: a quarter of the tiles. The plan raises its threshold until the
+  // parts fit, so only the heaviest tiles split. (A budget that followed the plan's demand let later plans split
+  // every tile above max(L, 0.35 x the costliest): rank 0's C4 share of 4 went from 120 to 167 us per launch,
+  // profiles/r04_share_trace_C4_n4.txt.)
+  m->extra_cap = ntiles / c->bal_budget + 64u;
   m->tick = ++c->bal_clock;
   if ((*err = hipMalloc(&m->cost, (size_t)ntiles * 8)) != hipSuccess ||
       (*err = hipMemsetAsync(m->cost, 0, (size_t)ntiles * 8, s)) != hipSuccess ||
@@ -1085,8 +1092,6 @@ constexpr uint64_t kReplan = 8, kRecheck = 32, kRecheckNoTail = 128;
 // one whose tail splitting could not shorten every kRecheck.
 static void balance_wants_plan(BalanceMap& m, bool* plan, bool* use, bool* record) {
   const volatile rt::PlanStats* st = m.stats;
-  const uint32_t plans = st->plans, want = st->want_extra;
-  if (plans) m.extra_cap = std::min<uint64_t>((uint64_t)want + want / 4u + 64u, 15ull * m.ntiles);
   *plan = *use = false;
   *record = true;
   if (m.launches == 0) return;
@@ -1191,6 +1196,13 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
     m->last_stream = s;
     m->active_run = active ? m->active_run + 1u : 0u;
     bool plan = forced, use = forced, record = false;
+    // a pending list that is ready becomes the current one (the old one's readers recorded for the next plan)
+    if (active && !forced && m->pending >= 0 && hipEventQuery(m->pend_ev) == hipSuccess) {
+      HIPCHK(c, balance_swap_out(*m), "tile balance: record the list's readers");
+      m->cur = m->pending;
+      m->cur_items = m->pending_items;
+      m->pending = -1;
+    }
     if (active && !forced) balance_wants_plan(*m, &plan, &use, &record);
     c->fp.cost = record ? m->cost : nullptr;
     rt::PlanArgs a;
@@ -1221,13 +1233,6 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
       HIPCHK(c, rt::launch_tile_plan(a, s), "tile plan launch");
       c->fp.plan = a.plan;
     } else if (active) {
-      // the pending list is ready: it becomes the current one (the old one's readers recorded for the next plan)
-      if (m->pending >= 0 && hipEventQuery(m->pend_ev) == hipSuccess) {
-        HIPCHK(c, balance_swap_out(*m), "tile balance: record the list's readers");
-        m->cur = m->pending;
-        m->cur_items = m->pending_items;
-        m->pending = -1;
-      }
       if (plan) {
         // the next list goes into the other buffer, on the plan stream, after every launch that read that buffer
         // and after this stream's earlier work (the costs it recorded); this launch keeps the current list

@@ -4,7 +4,8 @@ of rank 0's strip share at N ranks (interleaved 8-row strips, the row list a ran
 one stream back to back (the frame latency) and with 3 frames in flight, interleaved rounds, medians; every variant's
 frame is checked equal to the first's. --variants names the arms: b0 (off), b1 (adaptive, the defaults), and b1 with
 the plan's diagnostics (RT_BALANCE_SPLIT / RT_BALANCE_FRONT, read at context creation): b1s0 (no split, order
-only), b1f0 (tile order, split only), b1f<k> (front class above k / 16 x the load bound).
+only), b1f0 (tile order, split only), b1f<k> (front class above k / 16 x the load bound), b1q<d> (extra waves for
+split tiles: ntiles / d).
   python3 tools/balance_ab.py --configs C4,C2F,C2 --shares 1,4,8 --rounds 5 --variants b0,b1,b1s0"""
 import argparse
 import json
@@ -53,7 +54,8 @@ def main():
         ctxs = {}
         for v in variants:
             env = {"RT_BALANCE_SPLIT": "0" if "s0" in v else "1",
-                   "RT_BALANCE_FRONT": v.split("f")[1] if "f" in v else "8"}
+                   "RT_BALANCE_FRONT": v.split("f")[1].split("q")[0] if "f" in v else "8",
+                   "RT_BALANCE_BUDGET": v.split("q")[1] if "q" in v else "4"}
             os.environ.update(env)
             ctxs[v] = rt.Context(0)
             scenes.upload(ctxs[v], spec)
