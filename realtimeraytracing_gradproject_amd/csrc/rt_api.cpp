@@ -209,6 +209,7 @@ struct BalanceMap {
   uint64_t launches = 0, tick = 0;   // launches: those with the balance active
   hipStream_t last_stream = nullptr; // the stream of the shape's previous launch (cleared by rt_forget_stream)
   uint32_t active_run = 0;           // launches in a row with the balance active
+  uint32_t idle_queries = 0;         // launches in flight since the last stream query
   ScratchSlot list[2];               // work lists; uses recorded when a list stops being current
   int cur = -1;                      // the current list (its plan complete), or none
   uint32_t cur_items = 0;            // its launch's grid budget (tiles + extra waves)
@@ -1192,7 +1193,11 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
     // fill the slots the slowest tiles leave idle, so the balance only adds work there (split parts, the plan). It
     // runs when this launch follows the previous one on its stream or that stream has drained (frame latency: one
     // frame at a time, a rank's share of a frame). A host query of the stream: no event in the launch's stream.
-    const bool active = forced || s == m->last_stream || !m->last_stream || hipStreamQuery(m->last_stream) == hipSuccess;
+    // While the shape is in flight the stream is queried on one launch in 16 only: frames in flight are issued as
+    // fast as the host can (C1's 9-us frames are bound by the host's issue), and the query is a runtime call.
+    bool active = forced || s == m->last_stream || !m->last_stream;
+    if (!active && (m->active_run > 0u || (++m->idle_queries & 15u) == 0u))
+      active = hipStreamQuery(m->last_stream) == hipSuccess;
     m->last_stream = s;
     m->active_run = active ? m->active_run + 1u : 0u;
     bool plan = forced, use = forced, record = false;
