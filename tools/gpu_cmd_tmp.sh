@@ -1,3 +1,6 @@
 set -u
 cd $GRAFT_REPO_ROOT
-STEPS="balance" TAG=r04y BAL_ARGS="--configs C4,C2F --shares 1,4,8 --rounds 3 --variants b0,b1,b1q8,b1q16" bash tools/gpu_r04.sh
+timeout -k 10 900 python3 tools/lib_ab.py --roots ab/r03,.,.:bal0 --configs C2,C2F,C4 --rounds 3 > gpurun_out/lib_ab_final.txt 2>&1 || { echo lib_ab failed; tail -20 gpurun_out/lib_ab_final.txt; exit 1; }
+python3 -c "
+import json;t=open('gpurun_out/lib_ab_final.txt').read();d=json.loads(t[t.index('{\n'):]);print(json.dumps(d['median_ms']))"
+STEPS="strips" TAG=r04final bash tools/gpu_r04.sh
