@@ -270,7 +270,7 @@ struct rt_ctx {
   // the adaptive plan's split of costly tiles and its front class (PlanArgs::split, front; A/B diagnostics:
   // RT_BALANCE_SPLIT, RT_BALANCE_FRONT, RT_BALANCE_BUDGET — the extra waves as a divisor of the tiles — at context
   // creation) and the list's cover check (RT_BALANCE_CHECK, tests)
-  uint32_t bal_split = 1, bal_front = 8, bal_check = 0, bal_budget = 4;
+  uint32_t bal_split = 1, bal_front = 8, bal_check = 0, bal_budget = 8;
   static constexpr size_t kMaxBalanceMaps = 16;
   std::vector<BalanceMap> bal;
   uint64_t bal_clock = 0;
@@ -1058,8 +1058,9 @@ static BalanceMap* balance_map(rt_ctx* c, uint32_t W, uint32_t nrows, const uint
   m->tile_rows = c->tile_rows;
   m->spp = c->fp.spp_side;
   m->ntiles = ntiles;
-  // the extra waves a list may add for split tiles: a quarter of the tiles. The plan raises its threshold until the
-  // parts fit, so only the heaviest tiles split. (A budget that followed the plan's demand let later plans split
+  // the extra waves a list may add for split tiles: an eighth of the tiles. The plan raises its threshold until the
+  // parts fit, so only the heaviest tiles split (a quarter or a sixteenth measured 3-9 % slower on C4 / C2F frames
+  // and shares, profiles/r04_balance_budget_sweep2.txt). (A budget that followed the plan's demand let later plans split
   // every tile above max(L, 0.35 x the costliest): rank 0's C4 share of 4 went from 120 to 167 us per launch,
   // profiles/r04_share_trace_C4_n4.txt.)
   m->extra_cap = ntiles / c->bal_budget + 64u;
