@@ -99,7 +99,33 @@ $(RCPCHECK): tools/recip_check.hip $(SRC)/rt_device.hpp include/rt_api.h
 $(BUILD) $(LIBDIR):
 	mkdir -p $@
 
+# Host sanitizer builds (ASan/UBSan for the oracle and the ingest; CPU only — GPU sanitizers are not
+# available on this pool). build/asan/librtamd.so is the product library with its host C++ (rt_host.cpp: OBJ ingest,
+# normals, camera, manipulator) compiled with -fsanitize=address,undefined, linked by g++ against the same HIP objects;
+# build/asan/liboracle.so is the checker likewise. tools/asan_check.sh runs the CPU tests of those parts over them
+# (RT_LIBRARY / ORACLE_LIBRARY, the gcc sanitizer runtimes preloaded into python).
+ASAN      := $(BUILD)/asan
+SANFLAGS  := -fsanitize=address,undefined -fno-omit-frame-pointer -fno-sanitize-recover=undefined
+asan: $(ASAN)/librtamd.so $(ASAN)/liboracle.so $(ASAN)/obj_ingest_fuzz
+
+$(ASAN)/rt_host.o: $(SRC)/rt_host.cpp include/rt_api.h | $(ASAN)
+	g++ -O1 -g -std=c++17 -fPIC -ffp-contract=off -Wall $(SANFLAGS) -c $< -o $@
+
+$(ASAN)/librtamd.so: $(BUILD)/rt_api.o $(BUILD)/rt_comm.o $(ASAN)/rt_host.o $(BUILD)/rt_lbvh.o $(BUILD)/rt_trace.o $(BUILD)/rt_raster.o
+	g++ -shared $(SANFLAGS) -o $@ $^ -L$(ROCM)/lib -lamdhip64 -ldl -Wl,-rpath,$(ROCM)/lib
+
+$(ASAN)/liboracle.so: oracle/rt_oracle.c oracle/rt_raster_oracle.c oracle/rt_oracle.h | $(ASAN)
+	gcc -O1 -g -std=c11 -fPIC -ffp-contract=off -mfma -Wall -Wno-unused-function $(SANFLAGS) \
+	    -DORACLE_FLAGS='"asan"' -shared -o $@ oracle/rt_oracle.c oracle/rt_raster_oracle.c -lm -lpthread
+
+# a standalone driver of the sanitized ingest over random and adversarial OBJ text (no Python in the process)
+$(ASAN)/obj_ingest_fuzz: tools/obj_ingest_fuzz.cpp $(ASAN)/rt_host.o | $(ASAN)
+	g++ -O1 -g -std=c++17 $(SANFLAGS) -o $@ $^
+
+$(ASAN):
+	mkdir -p $@
+
 clean:
 	rm -rf $(BUILD) $(LIB) $(APP) $(ORACLE) $(BASELINE) $(RCPCHECK) $(VDIR)
 
-.PHONY: all clean ref
+.PHONY: all clean ref asan

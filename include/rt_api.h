@@ -205,8 +205,18 @@ rt_status rt_set_tile_balance(rt_ctx_t ctx, int mode);
  * plain order), [9] tiles the lists failed to cover exactly once, [10] the first such tile, [11] its check word
  * ([9..11] only when the context was created with RT_BALANCE_CHECK=1 in the environment: a cover check after each
  * plan, diagnostics), [12..14] the last plan kernel's phases in 10-ns ticks (snapshot + load bound, budget,
- * placement), [15] 0. Host-side read of host-mapped memory (may lag the device by a few launches). */
-rt_status rt_tile_balance_info(rt_ctx_t ctx, uint32_t out[16]);
+ * placement), [15] the wave slots of the last plan's load bound (the list kernel's occupancy per CU, from the
+ * runtime, x CUs), [16] work items the plans refused for want of budget (summed; a plan that refuses any item falls
+ * back to the plain grid's list, so no part is ever dropped), [17] the plans that fell back, [18..19] 0. Host-side
+ * read of host-mapped memory (may lag the device by a few launches). */
+#define RT_BALANCE_INFO_COUNT 20
+rt_status rt_tile_balance_info(rt_ctx_t ctx, uint32_t out[RT_BALANCE_INFO_COUNT]);
+/* Context diagnostics: out[0] device-wide synchronisations so far (builds, rebuilds, buffer growth: never a frame
+ * launch on a steady pipeline), [1] tile-balance maps recycled for a new launch shape (only once every stream that
+ * used them is idle: host queries, no synchronisation), [2] launches that ran the plain grid because every map was
+ * in use by work in flight, [3] maps held. */
+#define RT_CTX_COUNTERS 4
+rt_status rt_ctx_counters(rt_ctx_t ctx, uint64_t out[RT_CTX_COUNTERS]);
 /* Enables device counters (rt_stats). Costs time: off for timed runs. */
 rt_status rt_set_stats(rt_ctx_t ctx, int enable);
 
@@ -314,9 +324,23 @@ rt_status rt_comm_init(rt_ctx_t ctx, uint32_t nranks, uint32_t rank, const void*
  * the RCCL communicator calls ncclGather. Strip plan, frame batching, events, tails and the rank-strided assembly
  * are the RCCL path's, so the N > 1 frame layout runs on a one-GPU box. The communicator is rank 0. */
 rt_status rt_comm_init_loopback(rt_ctx_t ctx, uint32_t nranks, rt_comm_t* out);
+/* Loopback rehearsal of one rank's share of the cost (tools/share_ceiling.py): from the next frame on, only the
+ * emulated ranks [first, first + count) render; the others' blocks of the slot keep whatever they hold, while the
+ * gather copy and rank 0's assembly still move and assemble every rank's block. A step then costs this process what
+ * it costs rank `first` of an N-rank run (its strips' render, the gather, the assembly), minus the xGMI transfer;
+ * the frames hold stale strips for the ranks not rendered. count 0: every rank (the default). Loopback
+ * communicators only (RT_E_INVALID otherwise). No reference counterpart. */
+rt_status rt_comm_loopback_render_ranks(rt_comm_t comm, uint32_t first, uint32_t count);
 /* Drains the pipeline first (a partly filled slot is gathered and assembled as it is, every rank alike: destroy
  * is collective like the frames), then stops the issue thread. Destroy communicators before their context. */
 rt_status rt_comm_destroy(rt_comm_t comm);
+/* The failure path (SURVEY.md §5 "Failure detection"; the reference's only failure handling is ThrowIfFailed,
+ * DXSampleHelper.h:16-22): frees the communicator WITHOUT issuing another collective, so one rank can leave on an
+ * error while the others may never call again. The partly filled slot is discarded (never gathered or assembled),
+ * steps not yet handed to the issue thread are dropped, the issue thread stops, and ncclCommAbort cancels the
+ * collectives in flight (their peers may never match them). Local, unlike rt_comm_destroy. The frames of discarded or
+ * cancelled steps have undefined content; the context stays usable. Destroy communicators before their context. */
+rt_status rt_comm_abort(rt_comm_t comm);
 const char* rt_comm_last_error(rt_comm_t comm);
 /* The communicator's gather stream, made to wait (on the device) for every step issued so far, the
  * assemblies on the render streams included: work the caller enqueues on it after this call sees rank 0's

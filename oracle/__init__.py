@@ -13,7 +13,8 @@ from typing import Optional
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liboracle.so")
+# ORACLE_LIBRARY (tools/asan_check.sh: the checker built with the address / undefined-behaviour sanitizers)
+LIB_PATH = os.environ.get("ORACLE_LIBRARY") or os.path.join(_HERE, "liboracle.so")
 
 _P = ctypes.c_void_p
 _U32 = ctypes.c_uint32

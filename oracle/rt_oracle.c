@@ -11,6 +11,7 @@
  */
 #include "rt_oracle.h"
 
+#include <float.h>
 #include <math.h>
 #include <pthread.h>
 #include <stdlib.h>
@@ -41,21 +42,39 @@ static inline vec3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
 /* ---------------------------------------------------------------------------------------- */
 static int is_ws(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\v' || c == '\f'; }
 
+/* `ss >> float` (OBJ_FileManager.cpp:30) as libstdc++ extracts it in the "C" locale (num_get::_M_extract_float, then
+ * __convert_to_v): the longest prefix [sign] digits [. digits] [e|E [sign] digits] is accepted (a second '.', an 'e'
+ * before any digit or a second 'e' ends it), strtof must consume all of it (else 0, failbit), an overflow to +-inf
+ * gives +-FLT_MAX and failbit; the stream stops right after the accepted characters. */
 static int o_parse_float(const char** pp, const char* end, float* out) {
   const char* p = *pp;
   while (p < end && is_ws(*p)) ++p;
-  const char* b = p;
-  while (p < end && ((*p >= '0' && *p <= '9') || *p == '+' || *p == '-' || *p == '.' || *p == 'e' || *p == 'E')) ++p;
-  *pp = p;
-  if (p == b) { *out = 0.0f; return 0; }
-  char buf[128];
-  size_t n = (size_t)(p - b);
-  if (n > 127) n = 127;
-  memcpy(buf, b, n);
+  char* buf = (char*)malloc((size_t)(end - p) + 2);
+  size_t n = 0;
+  if (!buf) { *pp = p; *out = 0.0f; return 0; }
+  if (p < end && (*p == '+' || *p == '-')) buf[n++] = *p++;
+  int mant = 0, dec = 0, sci = 0;
+  while (p < end) {
+    const char ch = *p;
+    if (ch >= '0' && ch <= '9') { buf[n++] = ch; mant = 1; }
+    else if (ch == '.' && !dec && !sci) { buf[n++] = '.'; dec = 1; }
+    else if ((ch == 'e' || ch == 'E') && !sci && mant) {
+      buf[n++] = 'e';
+      sci = 1;
+      if (++p == end) break;
+      if (*p != '+' && *p != '-') continue; /* the character after the 'e' is examined again */
+      buf[n++] = *p;
+    } else break;
+    ++p;
+  }
   buf[n] = 0;
+  *pp = p;
   char* ep = NULL;
   float v = strtof(buf, &ep);
-  if (ep == buf) { *out = 0.0f; return 0; }
+  int ok = !(ep == buf || *ep != 0);
+  free(buf);
+  if (!ok) { *out = 0.0f; return 0; }
+  if (v == HUGE_VALF || v == -HUGE_VALF) { *out = v > 0.0f ? FLT_MAX : -FLT_MAX; return 0; }
   *out = v;
   return 1;
 }

@@ -22,13 +22,15 @@ except Exception:  # pragma: no cover - torch is part of the image
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "librtamd.so")
+# RT_LIBRARY (diagnostics: tools/asan_check.sh's sanitizer build of the same library) overrides the path
+LIB_PATH = os.environ.get("RT_LIBRARY") or os.path.join(_HERE, "lib", "librtamd.so")
 ASSETS = os.path.join(_HERE, "assets")
 
 RT_OK, RT_E_INVALID, RT_E_OOM, RT_E_HIP, RT_E_RCCL, RT_E_UNSUPPORTED, RT_E_IO = 0, -1, -2, -3, -4, -5, -6
 RT_HITGROUP_MODEL, RT_HITGROUP_SHADOW, RT_HITGROUP_PLANE = 0, 1, 2
 RT_SHADE_REF, RT_SHADE_LAMBERT_SHADOW, RT_SHADE_PRIMARY = 0, 1, 2
 RT_SCHED_PACKET, RT_SCHED_LANE = 0, 1
+RT_BALANCE_INFO_COUNT = 20
 RT_RAY_FLAG_ACCEPT_FIRST_HIT_AND_END_SEARCH, RT_RAY_FLAG_CULL_BACK_FACING_TRIANGLES = 0x04, 0x10
 RT_RAY_FLAG_CULL_FRONT_FACING_TRIANGLES = 0x20
 STAT_NAMES = ("primary_rays", "shadow_rays", "aabb_tests", "tri_tests", "instance_entries",
@@ -101,6 +103,7 @@ SIGNATURES = [
     ("rt_set_tile_rows", _I, [_P, _I]),
     ("rt_set_tile_balance", _I, [_P, _I]),
     ("rt_tile_balance_info", _I, [_P, _UP]),
+    ("rt_ctx_counters", _I, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     ("rt_set_stats", _I, [_P, _I]),
     ("rt_dispatch_rays", _I, [_P, _U32, _U32, _P, _U32, _P, _P, _P]),
     ("rt_trace_rays", _I, [_P, _P, _U32, _U32, _P, _P, _P]),
@@ -117,6 +120,8 @@ SIGNATURES = [
     ("rt_comm_init", _I, [_P, _U32, _U32, _P, ctypes.POINTER(_P)]),
     ("rt_comm_init_loopback", _I, [_P, _U32, ctypes.POINTER(_P)]),
     ("rt_comm_destroy", _I, [_P]),
+    ("rt_comm_abort", _I, [_P]),
+    ("rt_comm_loopback_render_ranks", _I, [_P, _U32, _U32]),
     ("rt_comm_last_error", ctypes.c_char_p, [_P]),
     ("rt_comm_stream", _P, [_P]),
     ("rt_comm_synchronize", _I, [_P]),
@@ -483,9 +488,36 @@ class Comm:
             if st != RT_OK:
                 raise RtError(st, "rt_comm_destroy")
 
-    def __del__(self):
-        try:
+    def loopback_render_ranks(self, first: int = 0, count: int = 0):
+        """rt_comm_loopback_render_ranks: a loopback communicator renders only emulated ranks [first, first + count)
+        (0: all) — the rehearsal of one rank's share of a step; the other ranks' strips are stale."""
+        self._check(self._lib.rt_comm_loopback_render_ranks(self._h, first, count), "rt_comm_loopback_render_ranks")
+
+    def abort(self):
+        """rt_comm_abort: the failure path. Frees the communicator without another collective (the partly filled
+        batch is discarded, ncclCommAbort cancels gathers in flight): safe when other ranks may never call again."""
+        if getattr(self, "_h", None):
+            h, self._h = self._h, None
+            st = self._lib.rt_comm_abort(h)
+            if st != RT_OK:
+                raise RtError(st, "rt_comm_abort")
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, exc_type, exc, tb):
+        # a normal exit drains (collective); an exception may have left the ranks out of step: abort
+        if exc_type is None:
             self.close()
+        else:
+            self.abort()
+        return False
+
+    def __del__(self):
+        # an unclosed communicator is garbage (an exception path, or interpreter shutdown): the other ranks may not
+        # issue the collective a draining destroy would need, so it aborts
+        try:
+            self.abort()
         except Exception:  # noqa: BLE001  (interpreter shutdown)
             pass
 
@@ -632,11 +664,17 @@ class Context:
         self._check(self._lib.rt_set_tile_balance(self._h, mode), "rt_set_tile_balance")
 
     def tile_balance_info(self) -> dict:
-        out = (ctypes.c_uint32 * 16)()
+        out = (ctypes.c_uint32 * RT_BALANCE_INFO_COUNT)()
         self._check(self._lib.rt_tile_balance_info(self._h, out), "rt_tile_balance_info")
         return dict(zip(("plans", "split", "items", "extra_cap", "max_ticks", "mean_ticks", "threshold", "launches",
                          "pays", "check_bad", "check_first_tile", "check_first_word", "plan_load_ticks",
-                         "plan_budget_ticks", "plan_place_ticks"), list(out)))
+                         "plan_budget_ticks", "plan_place_ticks", "slots", "refused", "refused_plans"), list(out)))
+
+    def counters(self) -> dict:
+        """rt_ctx_counters: device-wide synchronisations, tile-balance maps recycled / full, maps held."""
+        out = (ctypes.c_uint64 * 4)()
+        self._check(self._lib.rt_ctx_counters(self._h, out), "rt_ctx_counters")
+        return dict(zip(("device_syncs", "balance_recycled", "balance_full", "balance_maps"), list(out)))
 
     def set_stats(self, on: bool):
         self._check(self._lib.rt_set_stats(self._h, 1 if on else 0), "rt_set_stats")

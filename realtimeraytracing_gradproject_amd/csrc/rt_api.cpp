@@ -63,6 +63,7 @@ struct ScratchSlot {
   hipEvent_t upload_ev = nullptr;
   hipStream_t upload_stream = nullptr;
   bool uploaded = false;  // an upload may still be pending (upload_ev not yet seen complete)
+  uint64_t gen = 0;       // row-list slots: the context's generation of the list held (new at every upload)
 };
 
 struct ScratchRing {
@@ -202,7 +203,10 @@ hipError_t note_reader(TlasVersion& v, hipStream_t s) {
 struct BalanceMap {
   uint32_t W = 0, nrows = 0, nframes = 0, tile_rows = 0, spp = 0, ntiles = 0;
   const uint32_t* rows = nullptr;
+  uint64_t rows_gen = 0;             // the row list's generation (a ring slot re-used for another list is a new shape)
   uint32_t* cost = nullptr;          // device: 2 words per tile (whole wave time, costliest part; PlanArgs)
+  uint32_t cost_cap = 0;             // tiles the cost buffer holds (a recycled map keeps it)
+  std::vector<hipStream_t> streams;  // every stream that launched reading or writing the map's buffers
   rt::PlanStats* stats = nullptr;    // host-mapped, written by k_tile_plan
   rt::PlanStats* stats_dev = nullptr;
   uint32_t extra_cap = 0;
@@ -271,7 +275,8 @@ struct rt_ctx {
   // RT_BALANCE_SPLIT, RT_BALANCE_FRONT, RT_BALANCE_BUDGET — the extra waves as a divisor of the tiles — at context
   // creation) and the list's cover check (RT_BALANCE_CHECK, tests)
   uint32_t bal_split = 1, bal_front = 8, bal_check = 0, bal_budget = 8;
-  static constexpr size_t kMaxBalanceMaps = 16;
+  uint32_t bal_forced_cap = 0;  // RT_BALANCE_FORCED_CAP (tests): the forced layouts' extra waves (0: 15 x the tiles)
+  static constexpr size_t kMaxBalanceMaps = 32;
   std::vector<BalanceMap> bal;
   uint64_t bal_clock = 0;
   BalanceMap* bal_last = nullptr;
@@ -291,6 +296,10 @@ struct rt_ctx {
   hipEvent_t raster_ev = nullptr;
   hipStream_t raster_stream = nullptr;
   bool raster_pending = false;
+  uint64_t rows_gen = 0;  // row-list generations (ensure_rows uploads, rt_comm plans)
+  // rt_ctx_counters: device-wide synchronisations (quiesce), balance maps recycled for a new shape, launches that ran
+  // the plain grid because every map was in use
+  uint64_t n_quiesce = 0, bal_recycled = 0, bal_full = 0;
 };
 
 
@@ -319,6 +328,7 @@ rt_status hip_fail(rt_ctx* c, hipError_t e, const char* what) {
 // Only the rare mutating calls pay this (builds, rebuilds, a changed row list, buffer growth).
 hipError_t quiesce(rt_ctx* c) {
   (void)hipSetDevice(c->device);
+  ++c->n_quiesce;
   return hipDeviceSynchronize();
 }
 
@@ -489,6 +499,7 @@ rt_status rt_create(int hip_device, rt_ctx_t* out) {
   if (const char* ev = std::getenv("RT_BALANCE_CHECK")) c->bal_check = std::strtoul(ev, nullptr, 10) ? 1u : 0u;
   if (const char* ev = std::getenv("RT_BALANCE_BUDGET"))
     c->bal_budget = std::max<uint32_t>(1u, (uint32_t)std::strtoul(ev, nullptr, 10));
+  if (const char* ev = std::getenv("RT_BALANCE_FORCED_CAP")) c->bal_forced_cap = (uint32_t)std::strtoul(ev, nullptr, 10);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&c->d_stats, RT_STAT_COUNT * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(c->d_stats, 0, RT_STAT_COUNT * sizeof(unsigned long long)) != hipSuccess) {
@@ -825,9 +836,18 @@ rt_status rt_set_tile_balance(rt_ctx_t c, int mode) {
   return RT_OK;
 }
 
-rt_status rt_tile_balance_info(rt_ctx_t c, uint32_t out[16]) {
+rt_status rt_ctx_counters(rt_ctx_t c, uint64_t out[RT_CTX_COUNTERS]) {
   if (!c || !out) return RT_E_INVALID;
-  std::memset(out, 0, 16 * sizeof(uint32_t));
+  out[0] = c->n_quiesce;
+  out[1] = c->bal_recycled;
+  out[2] = c->bal_full;
+  out[3] = c->bal.size();
+  return RT_OK;
+}
+
+rt_status rt_tile_balance_info(rt_ctx_t c, uint32_t out[RT_BALANCE_INFO_COUNT]) {
+  if (!c || !out) return RT_E_INVALID;
+  std::memset(out, 0, RT_BALANCE_INFO_COUNT * sizeof(uint32_t));
   const BalanceMap* m = c->bal_last;
   if (!m || !m->stats) return RT_OK;
   const volatile rt::PlanStats* st = m->stats;
@@ -844,6 +864,9 @@ rt_status rt_tile_balance_info(rt_ctx_t c, uint32_t out[16]) {
   out[10] = st->first_bad_tile;
   out[11] = st->first_bad_word;
   for (int k = 0; k < 3; ++k) out[12 + k] = st->phase_ticks[k];
+  out[15] = st->slots;
+  out[16] = st->refused;
+  out[17] = st->refused_plans;
   return RT_OK;
 }
 
@@ -952,7 +975,7 @@ static rt_status ensure_overflow(rt_ctx* c, rt::SceneView& sv, size_t lanes, hip
 
 // Device copy of a strip dispatch's row list, shared by every launch that renders the same rows.
 static rt_status ensure_rows(rt_ctx* c, const uint32_t* rows, uint32_t nrows, hipStream_t s, ScratchSlot** used,
-                             const uint32_t** d_rows) {
+                             const uint32_t** d_rows, uint64_t* gen) {
   std::vector<uint32_t> key(rows, rows + nrows);
   bool hit;
   hipError_t e;
@@ -974,6 +997,7 @@ static rt_status ensure_rows(rt_ctx* c, const uint32_t* rows, uint32_t nrows, hi
     if (!sl->upload_ev && !(sl->upload_ev = new_sync_event())) return fail(c, RT_E_HIP, "rows: event");
     std::memcpy(sl->staging, rows, bytes);
     sl->key.swap(key);
+    sl->gen = ++c->rows_gen;
     HIPCHK(c, hipMemcpyAsync(sl->buf, sl->staging, bytes, hipMemcpyHostToDevice, s), "upload rows");
     HIPCHK(c, hipEventRecord(sl->upload_ev, s), "upload rows");
     sl->uploaded = true;
@@ -985,6 +1009,7 @@ static rt_status ensure_rows(rt_ctx* c, const uint32_t* rows, uint32_t nrows, hi
   }
   *used = sl;
   *d_rows = (const uint32_t*)sl->buf;
+  *gen = sl->gen;
   return RT_OK;
 }
 
@@ -993,6 +1018,7 @@ static rt_status ensure_rows(rt_ctx* c, const uint32_t* rows, uint32_t nrows, hi
 namespace rt {
 
 int ctx_device(rt_ctx* c) { return c ? c->device : 0; }
+uint64_t ctx_next_rows_gen(rt_ctx* c) { return c ? ++c->rows_gen : 0; }
 
 hipError_t ctx_forget_stream(rt_ctx* c, hipStream_t s) {
   if (!c || !s) return hipSuccess;
@@ -1007,6 +1033,7 @@ hipError_t ctx_forget_stream(rt_ctx* c, hipStream_t s) {
   // the tile balance's lists: the same for their readers
   for (BalanceMap& m : c->bal) {
     if (m.last_stream == s) m.last_stream = nullptr;
+    m.streams.erase(std::remove(m.streams.begin(), m.streams.end(), s), m.streams.end());
     auto it = std::find(m.readers.begin(), m.readers.end(), s);
     if (it == m.readers.end() || m.cur < 0) continue;
     m.readers.erase(it);
@@ -1026,34 +1053,77 @@ rt_status check_dispatch(rt_ctx* c, uint32_t W, uint32_t H, const void* rgba8) {
   return RT_OK;
 }
 
-// The cost map of a launch shape (created with zero costs on stream s: the first launch runs the plain grid).
-static BalanceMap* balance_map(rt_ctx* c, uint32_t W, uint32_t nrows, const uint32_t* d_rows, uint32_t nframes,
-                               uint32_t ntiles, hipStream_t s, hipError_t* err) {
+// Whether nothing in flight can touch a map's buffers any more: every stream that launched with it is idle and its
+// pending plan (context stream) has completed. Host queries only (no device-wide synchronisation).
+static bool balance_idle(const BalanceMap& m) {
+  if (m.pending >= 0 && m.pend_ev && hipEventQuery(m.pend_ev) != hipSuccess) return false;
+  for (hipStream_t s : m.streams)
+    if (hipStreamQuery(s) != hipSuccess) return false;
+  return true;
+}
+
+// The load bound's wave slots for a plan: the occupancy of the kernel the list will drive (from the runtime, for
+// the instantiation launched) x the device's CUs; the documented 8 waves per SIMD x 1024 SIMDs if the runtime
+// cannot tell.
+static uint32_t plan_slots(rt_ctx* c, const rt::SceneView& sv) {
+  const uint32_t n = rt::trace_wave_slots(sv, c->fp, c->schedule, c->device);
+  return n ? n : 8u * 1024u;
+}
+
+// The cost map of a launch shape (created with zero costs on stream s: the first launch runs the plain grid). With
+// every map in use (kMaxBalanceMaps shapes: a loopback communicator emulating many ranks has one per rank), a map
+// whose buffers nothing in flight can touch and whose cost buffer is large enough is recycled (never a
+// device-wide synchronisation on the frame path); if there is none, null with *err = hipSuccess: the launch runs
+// the plain grid. Forced layouts (tests) instead wait for the device and replace the least recently used map.
+static BalanceMap* balance_map(rt_ctx* c, uint32_t W, uint32_t nrows, const uint32_t* d_rows, uint64_t rows_gen,
+                               uint32_t nframes, uint32_t ntiles, hipStream_t s, bool forced, hipError_t* err) {
   *err = hipSuccess;
   BalanceMap* lru = nullptr;
   for (BalanceMap& m : c->bal) {
-    if (m.W == W && m.nrows == nrows && m.rows == d_rows && m.nframes == nframes && m.tile_rows == c->tile_rows &&
-        m.spp == c->fp.spp_side && m.ntiles == ntiles) {
+    if (m.W == W && m.nrows == nrows && m.rows == d_rows && m.rows_gen == rows_gen && m.nframes == nframes &&
+        m.tile_rows == c->tile_rows && m.spp == c->fp.spp_side && m.ntiles == ntiles) {
       m.tick = ++c->bal_clock;
       return &m;
     }
     if (!lru || m.tick < lru->tick) lru = &m;
   }
   BalanceMap* m = nullptr;
+  bool recycled = false;
   c->bal.reserve(rt_ctx::kMaxBalanceMaps);  // the maps never move (bal_last points at one)
   if (c->bal.size() < rt_ctx::kMaxBalanceMaps) {
     c->bal.emplace_back();
     m = &c->bal.back();
+  } else if (!forced) {
+    for (BalanceMap& o : c->bal)  // the least recently used idle map that fits
+      if (o.cost_cap >= ntiles && (!m || o.tick < m->tick) && balance_idle(o)) m = &o;
+    if (!m) {
+      ++c->bal_full;
+      return nullptr;
+    }
+    ++c->bal_recycled;
+    recycled = true;
   } else {
-    // the least recently used shape's buffers may still be read by launches in flight
+    // tests: the least recently used shape's buffers may still be read by launches in flight
     if ((*err = quiesce(c)) != hipSuccess) return nullptr;
     m = lru;
     if (c->bal_last == m) c->bal_last = nullptr;
     m->release();
   }
+  if (recycled) {
+    // keep the buffers (cost, lists, stats, events); restart the shape's state
+    m->launches = 0;
+    m->last_stream = nullptr;
+    m->active_run = m->idle_queries = 0;
+    m->cur = m->pending = -1;
+    m->cur_items = m->pending_items = 0;
+    m->planned_at = 0;
+    m->readers.clear();
+    m->streams.clear();
+  }
   m->W = W;
   m->nrows = nrows;
   m->rows = d_rows;
+  m->rows_gen = rows_gen;
   m->nframes = nframes;
   m->tile_rows = c->tile_rows;
   m->spp = c->fp.spp_side;
@@ -1065,6 +1135,12 @@ static BalanceMap* balance_map(rt_ctx* c, uint32_t W, uint32_t nrows, const uint
   // profiles/r04_share_trace_C4_n4.txt.)
   m->extra_cap = ntiles / c->bal_budget + 64u;
   m->tick = ++c->bal_clock;
+  if (recycled) {
+    if ((*err = hipMemsetAsync(m->cost, 0, (size_t)ntiles * 8, s)) != hipSuccess) return nullptr;
+    std::memset(m->stats, 0, sizeof(rt::PlanStats));
+    return m;
+  }
+  m->cost_cap = ntiles;
   if ((*err = hipMalloc(&m->cost, (size_t)ntiles * 8)) != hipSuccess ||
       (*err = hipMemsetAsync(m->cost, 0, (size_t)ntiles * 8, s)) != hipSuccess ||
       (*err = hipHostMalloc((void**)&m->stats, sizeof(rt::PlanStats), hipHostMallocMapped)) != hipSuccess) {
@@ -1144,7 +1220,7 @@ void frame_cam(const float cb[64], FrameCam& cam) {
 // 3 = RGB8 (strips).
 rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_rows, uint32_t nrows, void* rgba8,
                          float* rgba32f, hipStream_t s, uint32_t out_bpp, uint32_t nframes, const float* cams,
-                         uint64_t frame_stride) {
+                         uint64_t frame_stride, uint64_t rows_gen) {
   if (nframes < 1 || nframes > (uint32_t)rt::kMaxLaunchFrames || (out_bpp != 3 && out_bpp != 4) ||
       (nframes > 1 && rgba32f))
     return fail(c, RT_E_INVALID, "dispatch: 1..4 frames per launch, RGBA8 or RGB8, float output for one frame only");
@@ -1187,86 +1263,95 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
       (uint64_t)g.waves_per_frame * nframes <= rt::kPlanMaxTiles) {
     const uint32_t ntiles = g.waves_per_frame * nframes;
     hipError_t be;
-    BalanceMap* m = balance_map(c, W, nrows, d_rows, nframes, ntiles, s, &be);
-    if (!m) return hip_fail(c, be, "tile balance: cost map");
-    c->bal_last = m;
-    // frames in flight (the shape's previous launch still runs on another stream): the next frame's waves already
-    // fill the slots the slowest tiles leave idle, so the balance only adds work there (split parts, the plan). It
-    // runs when this launch follows the previous one on its stream or that stream has drained (frame latency: one
-    // frame at a time, a rank's share of a frame). A host query of the stream: no event in the launch's stream.
-    // While the shape is in flight the stream is queried on one launch in 16 only: frames in flight are issued as
-    // fast as the host can (C1's 9-us frames are bound by the host's issue), and the query is a runtime call.
-    bool active = forced || s == m->last_stream || !m->last_stream;
-    if (!active && (m->active_run > 0u || (++m->idle_queries & 15u) == 0u))
-      active = hipStreamQuery(m->last_stream) == hipSuccess;
-    m->last_stream = s;
-    m->active_run = active ? m->active_run + 1u : 0u;
-    bool plan = forced, use = forced, record = false;
-    // a pending list that is ready becomes the current one (the old one's readers recorded for the next plan)
-    if (active && !forced && m->pending >= 0 && hipEventQuery(m->pend_ev) == hipSuccess) {
-      HIPCHK(c, balance_swap_out(*m), "tile balance: record the list's readers");
-      m->cur = m->pending;
-      m->cur_items = m->pending_items;
-      m->pending = -1;
-    }
-    if (active && !forced) balance_wants_plan(*m, &plan, &use, &record);
-    c->fp.cost = record ? m->cost : nullptr;
-    rt::PlanArgs a;
-    a.cost = m->cost;
-    a.stats = forced ? nullptr : m->stats_dev;
-    a.ntiles = ntiles;
-    a.slots = 7u * 1024u;  // the LAMBERT_SHADOW kernel's 7 waves per SIMD x 1024 SIMDs
-    a.kmax_code = g.kmax_code;
-    a.force = forced ? (uint32_t)(c->balance - 1) : 0u;
-    a.split = c->bal_split;
-    a.front = c->bal_front;
-    a.check = c->bal_check;
-    a.min_gain = 1000u;  // 10 us: above the plan kernel's own time
-    a.waves_per_frame = g.waves_per_frame;
-    a.grid_x = g.grid_x;
-    a.wx = g.wx;
-    a.wy = g.wy;
-    a.wl = g.wl;
-    if (forced) {
-      // tests: a fresh list per launch from the ring
-      a.extra_cap = 15u * ntiles;
-      plan_items = ntiles + a.extra_cap;
-      bool hit;
-      plan_slot = ring_acquire(c->plans, s, nullptr, &hit, &be);
-      if (be != hipSuccess) return hip_fail(c, be, "tile balance: order after in-flight launches");
-      HIPCHK(c, slot_reserve(*plan_slot, ((size_t)plan_items + 2u * ntiles + 1) * 4), "hipMalloc(tile plan)");
-      a.plan = (uint32_t*)plan_slot->buf;
-      HIPCHK(c, rt::launch_tile_plan(a, s), "tile plan launch");
-      c->fp.plan = a.plan;
-    } else if (active) {
-      if (plan) {
-        // the next list goes into the other buffer, on the plan stream, after every launch that read that buffer
-        // and after this stream's earlier work (the costs it recorded); this launch keeps the current list
-        hipStream_t ps = c->stream;
-        const int b = m->cur < 0 ? 0 : 1 - m->cur;
-        ScratchSlot& sl = m->list[b];
-        if ((!m->pend_ev && !(m->pend_ev = new_sync_event())) || (!m->src_ev && !(m->src_ev = new_sync_event())))
-          return fail(c, RT_E_HIP, "tile balance: event");
-        HIPCHK(c, hipEventRecord(m->src_ev, s), "tile balance: record the launch stream");
-        HIPCHK(c, hipStreamWaitEvent(ps, m->src_ev, 0), "tile balance: order the plan");
-        HIPCHK(c, slot_order_after_others(sl, ps), "tile balance: order after the list's readers");
-        a.extra_cap = m->extra_cap;
-        const uint32_t items = ntiles + a.extra_cap;
-        HIPCHK(c, slot_reserve(sl, ((size_t)items + 2u * ntiles + 1) * 4), "hipMalloc(tile plan)");
-        a.plan = (uint32_t*)sl.buf;
-        HIPCHK(c, rt::launch_tile_plan(a, ps), "tile plan launch");
-        HIPCHK(c, hipEventRecord(m->pend_ev, ps), "tile balance: record the plan");
-        m->pending = b;
-        m->pending_items = items;
-        m->planned_at = m->launches;
+    BalanceMap* m = balance_map(c, W, nrows, d_rows, rows_gen, nframes, ntiles, s, forced, &be);
+    if (!m && be != hipSuccess) return hip_fail(c, be, "tile balance: cost map");
+    if (m) {
+      c->bal_last = m;
+      // frames in flight (the shape's previous launch still runs on another stream): the next frame's waves already
+      // fill the slots the slowest tiles leave idle, so the balance only adds work there (split parts, the plan). It
+      // runs when this launch follows the previous one on its stream or that stream has drained (frame latency: one
+      // frame at a time, a rank's share of a frame). A host query of the stream: no event in the launch's stream.
+      // While the shape is in flight the stream is queried on one launch in 16 only: frames in flight are issued as
+      // fast as the host can (C1's 9-us frames are bound by the host's issue), and the query is a runtime call.
+      bool active = forced || s == m->last_stream || !m->last_stream;
+      if (!active && (m->active_run > 0u || (++m->idle_queries & 15u) == 0u))
+        active = hipStreamQuery(m->last_stream) == hipSuccess;
+      m->last_stream = s;
+      m->active_run = active ? m->active_run + 1u : 0u;
+      bool plan = forced, use = forced, record = false;
+      // a pending list that is ready becomes the current one (the old one's readers recorded for the next plan)
+      if (active && !forced && m->pending >= 0 && hipEventQuery(m->pend_ev) == hipSuccess) {
+        HIPCHK(c, balance_swap_out(*m), "tile balance: record the list's readers");
+        m->cur = m->pending;
+        m->cur_items = m->pending_items;
+        m->pending = -1;
       }
-      if (use && m->cur >= 0) {
-        if (std::find(m->readers.begin(), m->readers.end(), s) == m->readers.end()) m->readers.push_back(s);
-        c->fp.plan = (const uint32_t*)m->list[m->cur].buf;
-        plan_items = m->cur_items;
+      if (active && !forced) balance_wants_plan(*m, &plan, &use, &record);
+      c->fp.cost = record ? m->cost : nullptr;
+      rt::PlanArgs a;
+      a.cost = m->cost;
+      a.stats = forced ? nullptr : m->stats_dev;
+      a.ntiles = ntiles;
+      a.slots = 0;  // set below for a plan: the list's kernel's occupancy x CUs, from the runtime
+      a.kmax_code = g.kmax_code;
+      a.force = forced ? (uint32_t)(c->balance - 1) : 0u;
+      a.split = c->bal_split;
+      a.front = c->bal_front;
+      a.check = c->bal_check;
+      a.min_gain = 1000u;  // 10 us: above the plan kernel's own time
+      a.waves_per_frame = g.waves_per_frame;
+      a.grid_x = g.grid_x;
+      a.wx = g.wx;
+      a.wy = g.wy;
+      a.wl = g.wl;
+      if (forced) {
+        // tests: a fresh list per launch from the ring (RT_BALANCE_FORCED_CAP, tests: a smaller budget of extra waves,
+        // so the plan must refuse parts and fall back to the plain grid's list)
+        a.extra_cap = c->bal_forced_cap ? c->bal_forced_cap : 15u * ntiles;
+        a.stats = m->stats_dev;
+        a.slots = plan_slots(c, sv);
+        plan_items = ntiles + a.extra_cap;
+        bool hit;
+        plan_slot = ring_acquire(c->plans, s, nullptr, &hit, &be);
+        if (be != hipSuccess) return hip_fail(c, be, "tile balance: order after in-flight launches");
+        HIPCHK(c, slot_reserve(*plan_slot, ((size_t)plan_items + 2u * ntiles + 1) * 4), "hipMalloc(tile plan)");
+        a.plan = (uint32_t*)plan_slot->buf;
+        HIPCHK(c, rt::launch_tile_plan(a, s), "tile plan launch");
+        c->fp.plan = a.plan;
+      } else if (active) {
+        if (plan) {
+          // the next list goes into the other buffer, on the plan stream, after every launch that read that buffer
+          // and after this stream's earlier work (the costs it recorded); this launch keeps the current list
+          hipStream_t ps = c->stream;
+          const int b = m->cur < 0 ? 0 : 1 - m->cur;
+          ScratchSlot& sl = m->list[b];
+          if ((!m->pend_ev && !(m->pend_ev = new_sync_event())) || (!m->src_ev && !(m->src_ev = new_sync_event())))
+            return fail(c, RT_E_HIP, "tile balance: event");
+          HIPCHK(c, hipEventRecord(m->src_ev, s), "tile balance: record the launch stream");
+          HIPCHK(c, hipStreamWaitEvent(ps, m->src_ev, 0), "tile balance: order the plan");
+          HIPCHK(c, slot_order_after_others(sl, ps), "tile balance: order after the list's readers");
+          a.extra_cap = m->extra_cap;
+          a.slots = plan_slots(c, sv);
+          const uint32_t items = ntiles + a.extra_cap;
+          HIPCHK(c, slot_reserve(sl, ((size_t)items + 2u * ntiles + 1) * 4), "hipMalloc(tile plan)");
+          a.plan = (uint32_t*)sl.buf;
+          HIPCHK(c, rt::launch_tile_plan(a, ps), "tile plan launch");
+          HIPCHK(c, hipEventRecord(m->pend_ev, ps), "tile balance: record the plan");
+          m->pending = b;
+          m->pending_items = items;
+          m->planned_at = m->launches;
+        }
+        if (use && m->cur >= 0) {
+          if (std::find(m->readers.begin(), m->readers.end(), s) == m->readers.end()) m->readers.push_back(s);
+          c->fp.plan = (const uint32_t*)m->list[m->cur].buf;
+          plan_items = m->cur_items;
+        }
       }
+      if (active) m->launches += 1;
+      // the streams whose launches read or write the map's buffers (its recycling waits until all are idle)
+      if ((c->fp.cost || c->fp.plan) && std::find(m->streams.begin(), m->streams.end(), s) == m->streams.end())
+        m->streams.push_back(s);
     }
-    if (active) m->launches += 1;
   }
   hipError_t e = rt::launch_trace_frame(sv, c->fp, d_rows, rgba8, rgba32f, c->d_stats, c->stats_on,
                                         c->schedule, plan_items, s);
@@ -1419,8 +1504,10 @@ rt_status rt_dispatch_rays(rt_ctx_t c, uint32_t W, uint32_t H, const uint32_t* r
   if (st != RT_OK) return st;
   const uint32_t* d_rows = nullptr;
   ScratchSlot* rows_slot = nullptr;
-  if (rows && (st = ensure_rows(c, rows, nrows, s, &rows_slot, &d_rows)) != RT_OK) return st;
-  if ((st = rt::dispatch_frame(c, W, H, d_rows, nrows, rgba8, rgba32f, s, 4, 1, nullptr, 0)) != RT_OK) return st;
+  uint64_t rows_gen = 0;
+  if (rows && (st = ensure_rows(c, rows, nrows, s, &rows_slot, &d_rows, &rows_gen)) != RT_OK) return st;
+  if ((st = rt::dispatch_frame(c, W, H, d_rows, nrows, rgba8, rgba32f, s, 4, 1, nullptr, 0, rows_gen)) != RT_OK)
+    return st;
   if (rows_slot) HIPCHK(c, slot_mark_use(*rows_slot, s), "rows: record use");
   return RT_OK;
 }

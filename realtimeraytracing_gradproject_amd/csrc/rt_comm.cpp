@@ -58,6 +58,7 @@ struct RcclApi {
   ncclResult_t (*getUniqueId)(ncclUniqueId*) = nullptr;
   ncclResult_t (*commInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*commDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*commAbort)(ncclComm_t) = nullptr;  // rt_comm_abort (optional: older RCCL builds may lack it)
   ncclResult_t (*gather)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
   const char* (*getErrorString)(ncclResult_t) = nullptr;
 };
@@ -77,6 +78,7 @@ RcclApi& rccl() {
     api.getUniqueId = (decltype(api.getUniqueId))sym("ncclGetUniqueId");
     api.commInitRank = (decltype(api.commInitRank))sym("ncclCommInitRank");
     api.commDestroy = (decltype(api.commDestroy))sym("ncclCommDestroy");
+    api.commAbort = (decltype(api.commAbort))sym("ncclCommAbort");
     api.gather = (decltype(api.gather))sym("ncclGather");
     api.getErrorString = (decltype(api.getErrorString))sym("ncclGetErrorString");
     api.ok = api.getUniqueId && api.commInitRank && api.commDestroy && api.gather && api.getErrorString;
@@ -150,7 +152,9 @@ struct rt_comm {
   uint32_t W = 0, H = 0, strip = 0, rows_per_rank = 0;
   std::vector<uint32_t> rows;  // this rank's global rows, output order (loopback: every rank's in turn)
   uint32_t* d_rows = nullptr;  // ... on the device (uploaded once per plan)
+  uint64_t rows_gen = 0;       // ... its generation (rt::ctx_next_rows_gen, per plan)
   std::vector<uint32_t> lb_first, lb_count;  // loopback: rank r's rows are rows[lb_first[r] ..][0 .. lb_count[r])
+  uint32_t lb_render_first = 0, lb_render_count = 0;  // rt_comm_loopback_render_ranks (0: every emulated rank)
   size_t local_bytes = 0;      // one rank's block of a slot: batch x rows_per_rank x W x kStripBpp
   hipEvent_t xev = nullptr;    // a frame issued on another stream than its slot's: the slot's stream waits for it
   // RT_COMM_TIMING=1 (diagnostics): host time per part of rt_render_strips, printed by rt_comm_destroy
@@ -178,6 +182,7 @@ struct rt_comm {
   // gather (no waiting), and at the latest before its slot renders again (waiting if the issue thread is behind)
   std::deque<Job> tails;
   bool stop = false;
+  bool aborting = false;        // rt_comm_abort: the issue thread drops its queue and returns
   rt_status werr = RT_OK;       // the issue thread's first failure, returned by the next call
   std::string wmsg;
   double w_parts[3] = {0, 0, 0};  // RT_COMM_TIMING: issue-thread hand-off, ncclGather, gather event
@@ -252,6 +257,7 @@ rt_status plan(rt_comm* c, uint32_t W, uint32_t H, uint32_t strip) {
     if (hipMemcpy(c->d_rows, c->rows.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess)
       return cfail(c, RT_E_HIP, "rt_render_strips: upload rows");
   }
+  c->rows_gen = rt::ctx_next_rows_gen(c->ctx);
   const uint32_t nstrips = (H + strip - 1) / strip;
   c->rows_per_rank = ((nstrips + c->nranks - 1) / c->nranks) * strip;
   c->local_bytes = (size_t)c->rows_per_rank * W * kStripBpp * c->batch;
@@ -291,6 +297,7 @@ void issue_loop(rt_comm* c) {
       c->sleeping.store(true, std::memory_order_seq_cst);
       c->cv_job.wait(lk, [c] { return c->stop || !c->jobs.empty(); });
       c->sleeping.store(false, std::memory_order_relaxed);
+      if (c->aborting) c->jobs.clear();  // rt_comm_abort: no further collective
       if (c->jobs.empty()) return;  // stop requested and nothing left
       j = c->jobs.front();
       c->jobs.pop_front();
@@ -584,6 +591,35 @@ rt_status rt_comm_destroy(rt_comm_t c) {
   return st;
 }
 
+// The failure path: no drain, no further collective. The caller thread's pending state (the slot being filled, the
+// tails not yet issued) is dropped, the issue thread empties its queue and returns (a gather it is enqueuing right
+// now completes its enqueue: RCCL calls return once enqueued), then ncclCommAbort cancels whatever the gather stream
+// still waits on, so the stream synchronisations in comm_free return even when a peer never calls again.
+rt_status rt_comm_abort(rt_comm_t c) {
+  if (!c) return RT_E_INVALID;
+  (void)hipSetDevice(c->device);
+  c->fill = 0;
+  c->tails.clear();
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->aborting = true;
+    c->stop = true;
+    c->jobs.clear();
+  }
+  c->cv_job.notify_all();
+  if (c->worker.joinable()) c->worker.join();
+  (void)hipSetDevice(c->device);
+  rt_status st = RT_OK;
+  if (c->comm) {
+    RcclApi& api = rccl();
+    const ncclResult_t r = api.commAbort ? api.commAbort(c->comm) : api.commDestroy(c->comm);
+    if (r != ncclSuccess) st = RT_E_RCCL;
+    c->comm = nullptr;
+  }
+  comm_free(c);
+  return st;
+}
+
 const char* rt_comm_last_error(rt_comm_t c) { return c ? c->err.c_str() : "null communicator"; }
 
 void* rt_comm_stream(rt_comm_t c) {
@@ -694,9 +730,10 @@ rt_status rt_render_strips_frames(rt_comm_t c, uint32_t W, uint32_t H, uint32_t 
   const uint64_t frame_bytes = (uint64_t)c->rows_per_rank * W * kStripBpp;
   for (size_t r = 0; r < c->lb_count.size(); ++r) {
     if (!c->lb_count[r]) continue;  // a rank with no rows (H < nranks x strip_rows) renders nothing
+    if (c->lb_render_count && (r < c->lb_render_first || r >= c->lb_render_first + c->lb_render_count)) continue;
     char* dst = (char*)s.local + r * c->local_bytes + (size_t)c->fill * frame_bytes;
     st = rt::dispatch_frame(c->ctx, W, H, c->d_rows + c->lb_first[r], c->lb_count[r], dst, nullptr, c->cur.rs,
-                            kStripBpp, nframes, cameras, frame_bytes);
+                            kStripBpp, nframes, cameras, frame_bytes, c->rows_gen);
     if (st != RT_OK) return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));
   }
   lap(1);
@@ -733,5 +770,15 @@ rt_status rt_comm_set_batch(rt_comm_t c, uint32_t frames_per_gather) {
 }
 
 uint32_t rt_comm_batch(rt_comm_t c) { return c ? c->batch : 0; }
+
+rt_status rt_comm_loopback_render_ranks(rt_comm_t c, uint32_t first, uint32_t count) {
+  if (!c) return RT_E_INVALID;
+  if (!c->loopback) return cfail(c, RT_E_INVALID, "rt_comm_loopback_render_ranks: loopback communicators only");
+  if (count && (first >= c->nranks || count > c->nranks - first))
+    return cfail(c, RT_E_INVALID, "rt_comm_loopback_render_ranks: ranks out of range");
+  c->lb_render_first = count ? first : 0;
+  c->lb_render_count = count;
+  return RT_OK;
+}
 
 }  // extern "C"

@@ -155,8 +155,11 @@ struct FrameParams {
   // Tile balance (packet schedule, rt_set_tile_balance). plan: the launch's wave work list written by k_tile_plan
   // (plan[0] = item count, plan[1 + i] = item i = wave slot << 6 | part << 2 | split code; split code 0: the whole
   // tile, 1: quadrant `part` of 4, 2: cell `part` of 16), dealt to the waves of a 1-D grid in list order (costliest
-  // first), or null: wave slot = the plain grid's wave index. cost: per wave slot, the s_memrealtime ticks its tile
-  // took in the last launch of this shape (split tiles: the estimate from their parts), written at wave end, or null.
+  // first), or null: wave slot = the plain grid's wave index. cost: per wave slot, two words written at wave end (or
+  // null): [0] the ticks (s_memrealtime) of the tile's last whole wave, bit 31 set by every part of a split since
+  // (the whole time is then older than the parts), [1] the costliest part of the tile's last split (ticks << 2 |
+  // layout, atomicMax; cleared by the plan that splits the tile). A split tile's current cost is estimated from its
+  // parts (k_tile_plan), so a tile that became cheap while split is traced whole again.
   const uint32_t* plan;
   uint32_t* cost;
   uint32_t grid_x;           // workgroups along x of the plain grid

@@ -9,6 +9,7 @@
 //   D3D12HelloTriangle::UpdateCameraBuffer    src/D3D12HelloTriangle.cpp:1144-1170
 //   Manipulator motion/mouseMove/wheel/orbit/pan/dolly/trackball
 //                                             src/manipulator.cpp:135-445
+#include <cfloat>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -28,21 +29,44 @@ namespace {
 
 // Parses one float the way `std::stringstream >> float` does on the reference (libstdc++ num_get
 // accumulates [+-0-9.eE] characters, then converts with strtof). Returns false on failure.
+// `std::stringstream >> float` as the C++ library extracts it (libstdc++ num_get::_M_extract_float in the "C" locale,
+// then __convert_to_v): the longest prefix of [sign] digits [. digits] [e|E [sign] digits] — a second '.', an 'e'
+// before any digit or a second 'e' ends it — goes to strtof, which must consume all of it, else the value is 0 and the
+// stream fails ("1e", "1e+", "+", "."); an overflow to +-inf gives +-FLT_MAX and fails the stream too. The stream
+// stops right after the accepted characters ("1.5.5" reads 1.5, and the next value starts at ".5"). Pinned against
+// the reference's code path compiled here (tests/golden/obj_malformed.json).
 bool parse_float(const char*& p, const char* end, float& out) {
   while (p < end && (*p == ' ' || *p == '\t' || *p == '\r' || *p == '\v' || *p == '\f')) ++p;
-  const char* b = p;
-  while (p < end && ((*p >= '0' && *p <= '9') || *p == '+' || *p == '-' || *p == '.' || *p == 'e' ||
-                     *p == 'E'))
+  std::string tok;
+  if (p < end && (*p == '+' || *p == '-')) tok += *p++;
+  bool mant = false, dec = false, sci = false;
+  while (p < end) {
+    const char ch = *p;
+    if (ch >= '0' && ch <= '9') {
+      tok += ch;
+      mant = true;
+    } else if (ch == '.' && !dec && !sci) {
+      tok += '.';
+      dec = true;
+    } else if ((ch == 'e' || ch == 'E') && !sci && mant) {
+      tok += 'e';
+      sci = true;
+      if (++p == end) break;
+      if (*p != '+' && *p != '-') continue;  // the character after the 'e' is examined again
+      tok += *p;
+    } else {
+      break;
+    }
     ++p;
-  if (p == b) {
+  }
+  char* ep = nullptr;
+  const float v = std::strtof(tok.c_str(), &ep);
+  if (ep == tok.c_str() || *ep != '\0') {
     out = 0.0f;
     return false;
   }
-  std::string tok(b, p);
-  char* ep = nullptr;
-  float v = std::strtof(tok.c_str(), &ep);
-  if (ep == tok.c_str()) {
-    out = 0.0f;
+  if (v == HUGE_VALF || v == -HUGE_VALF) {
+    out = v > 0.0f ? FLT_MAX : -FLT_MAX;
     return false;
   }
   out = v;

@@ -10,6 +10,9 @@ namespace rt {
 
 // --- context accessors for the other host translation units (rt_comm.cpp) ---------------------
 int ctx_device(rt_ctx* c);
+// a fresh row-list generation (the tile balance keys a launch shape on the row list's pointer AND generation: a
+// buffer re-used for another list is another shape)
+uint64_t ctx_next_rows_gen(rt_ctx* c);
 void* ctx_stream(rt_ctx* c);
 // rt_dispatch_rays' argument / scene checks and its launch with a device row list (rt_render_strips keeps its
 // rank's rows on the device and skips the host list's upload ring)
@@ -19,7 +22,7 @@ rt_status check_dispatch(rt_ctx* c, uint32_t W, uint32_t H, const void* rgba8);
 // (the strips of rt_comm)
 rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_rows, uint32_t nrows, void* rgba8,
                          float* rgba32f, hipStream_t s, uint32_t out_bpp, uint32_t nframes, const float* cams,
-                         uint64_t frame_stride);
+                         uint64_t frame_stride, uint64_t rows_gen);
 // A stream that launched work on the context is going away (rt_forget_stream): the TLAS version it read gets
 // that stream's completion event now, so a later rt_tlas_build never records on the destroyed handle.
 hipError_t ctx_forget_stream(rt_ctx* c, hipStream_t s);
@@ -89,6 +92,10 @@ struct PacketGeometry {
   bool plannable = false;              // a work list may drive the launch
 };
 PacketGeometry packet_geometry(const SceneView& sc, const FrameParams& fp, int schedule);
+// The GPU's wave slots for the packet kernel a tile-balance launch of this shape runs (the recording / list
+// instantiation): hipOccupancyMaxActiveBlocksPerMultiprocessor of that kernel x waves per workgroup x the device's
+// CUs, cached per (kernel, device); 0 if the runtime cannot tell.
+uint32_t trace_wave_slots(const SceneView& sc, const FrameParams& fp, int schedule, int device);
 
 // Tile balance (k_tile_plan): the summary the plan kernel leaves in host-mapped memory for the next dispatches.
 struct PlanStats {
@@ -98,6 +105,11 @@ struct PlanStats {
   uint32_t bad, first_bad_tile, first_bad_word;
   uint32_t phase_ticks[3];  // the last plan's phases: snapshot + load bound, budget, placement (10-ns ticks)
   uint32_t coherent;        // the last plan found every measured split useless (it split nothing)
+  // items the plans could not place inside the list's budget (summed), and the plans that therefore fell back to the
+  // plain grid's list (every tile whole, in order): the budget loop should make both 0 (loud, not a
+  // silently dropped part)
+  uint32_t refused, refused_plans;
+  uint32_t slots;           // the wave slots the last plan's load bound divided by (PlanArgs::slots)
 };
 struct PlanArgs {
   uint32_t* cost;         // per wave slot of the plain grid, 2 words: the last whole wave's time (ticks), the
@@ -107,7 +119,8 @@ struct PlanArgs {
   PlanStats* stats;       // host-mapped, or null
   uint32_t ntiles;        // wave slots of the plain grid, every frame of the launch
   uint32_t extra_cap;     // items beyond ntiles the launch's grid has waves for
-  uint32_t slots;         // wave slots of the GPU for the trace kernel (waves per SIMD x SIMDs)
+  uint32_t slots;         // wave slots of the GPU for the list's trace kernel: its occupancy (waves per CU, from the
+                          // runtime for the instantiation launched) x CUs (trace_wave_slots)
   uint32_t kmax_code;
   uint32_t force;         // 0 adaptive; 1 / 2 / 3 forced layouts (tests)
   uint32_t split;         // adaptive: split tiles (0: order only)

@@ -119,4 +119,38 @@ class CpuBackendCommFails(CpuBackend):
 
             def close(self):
                 pass
+
+            def abort(self):  # bench.py must abort (no draining collective) the communicator the other rank lacks
+                print(f"comm aborted on rank {rank}", file=sys.stderr, flush=True)
         return _Comm()
+
+
+class CpuBackendStepFails(CpuBackend):
+    """The native strips loop at world 1 whose render call raises on its STEP_FAIL_AT-th call (an error mid-loop,
+    with a partly filled batch pending): bench.py must abort the communicator (rt_comm_abort, no draining gather) and
+    let the error propagate."""
+    native_strips = True
+    rt = _CommAvailable()
+
+    def comm_open(self, world, rank):
+        class _Comm:
+            depth, batch = 3, 1
+
+            def set_batch(self, b):
+                self.batch = b
+
+            def synchronize(self):
+                pass
+
+            def close(self):
+                print("comm closed", file=sys.stderr, flush=True)
+
+            def abort(self):
+                print("comm aborted", file=sys.stderr, flush=True)
+        self._calls = 0
+        return _Comm()
+
+    def render_strips(self, comm, frames, stream):
+        self._calls += 1
+        if self._calls == int(os.environ.get("STEP_FAIL_AT", "3")):
+            raise RuntimeError("simulated render failure")

@@ -5,6 +5,10 @@ camera_glm.json   glm::lookAt / glm::rotate from the reference's vendored glm, v
 obj_ingest.json   OBJFileManager::LoadObjFile output for teapot.obj / rabbit.obj (counts, sha256 of
                   positions and indices) from oracle/ref_obj_ingest.cpp: the reference's own
                   OBJ_Loader.h / OBJ_Loader.cpp compiled from /root/reference (`make ref`).
+obj_malformed.json  LoadObjFile's output for malformed / adversarial OBJ texts (bad numbers, partial lines, signs,
+                  overflow, exponents, hex, stray bytes, CR/NUL) from the same harness: the C++ library's own
+                  stringstream extraction rules, which the product's parser must reproduce (its three
+                  uninitialised locals pinned to 0).
 manipulator.json  camera-manipulator trajectories (mouseMove / motion / wheel / roll in every mode)
                   from oracle/ref_glm_manip.cpp over the reference's vendored glm (oracle/_ref/).
 frames_small.npz  oracle frames (RGBA8 + float32) of every config at small sizes; each is first
@@ -84,6 +88,61 @@ def obj_ingest():
                   "first_face": idx[:3].tolist(), "last_face": idx[-3:].tolist()}
     with open(os.path.join(HERE, "obj_ingest.json"), "w") as f:
         json.dump(out, f, indent=1)
+
+
+# Inputs of obj_malformed.json: each line kind the reference's `ss >> x >> y >> z` /
+# `ss >> i0 >> i1 >> i2` may meet in an untrusted file, plus a seeded byte soup.
+MALFORMED = [
+    b"v 1 2 3\nv 4 5 6\nv 7 8 9\nf 1 2 3\n",
+    b"v 1.5.5 2 3\n", b"v 1e 2 3\n", b"v 1e+ 2 3\n", b"v 1e5x 2 3\n", b"v .5 -.5 +.5\n", b"v 5. -5. +5.e1\n",
+    b"v 0x10 1 2\n", b"v 1e40 -1e40 1e-50\n", b"v inf -inf nan\n", b"v 1,5 2 3\n", b"v - 2 3\n", b"v -- 1 2\n",
+    b"v +-1 2 3\n", b"v 1 2\n", b"v 1\n", b"v\t1 2 3\n", b"vt 1 2 3\n", b"v 1 2 3 4 5\n", b"v 1e-2e3 4 5\n",
+    b"v 3.4028236e38 1.17e-38 1e-45\n", b"v 00001.2500 -0 +0\n",
+    b"f 1/1/1 2/2/2 3/3/3\n", b"f 1//1 2//2 3//3\n", b"f -1 2 3\n", b"f +1 +2 +3\n", b"f -0 0 1\n",
+    b"f 4294967295 4294967296 1\n", b"f 99999999999999999999 1 2\n", b"f 1.5 2 3\n", b"f 1e2 2 3\n",
+    b"f 1 2\n", b"f 1\n", b"f\t1 2 3\n", b"f  1  2  3\n", b"f 1 x 3\n", b"f 0x1 2 3\n", b"f 1 2 3 4\n",
+    b"f -4294967295 1 2\n", b"f - 1 2\n",
+    b"v 1 2 3\r\nf 1 1 1\r\n", b"v 1 2 3\rv 4 5 6\r", b"v 1 2\x003\n", b"\x00\x00\nv 1 2 3\n",
+    b"v 1 2 3", b"f 1 2 3", b"v", b"f", b"\n\n\n", b"v\n", b" v 1 2 3\n", b"V 1 2 3\n", b"F 1 2 3\n",
+    b"v 1 2 3\xff\xfe\n", b"v \xc3\xa9 1 2\n", b"v 1 2 3 # comment\n", b"v 1 2 3#4\n",
+    b"v " + b"9" * 400 + b" 1 2\n", b"f " + b"1" * 400 + b" 2 3\n", b"v " + b"0." + b"0" * 300 + b"1 2 3\n",
+]
+
+
+def _malformed_soup(n=24, seed=5):
+    rng = np.random.default_rng(seed)
+    alphabet = b"vf 0123456789+-.eExX/\t\r\n\x00#abc"
+    out = []
+    for _ in range(n):
+        k = int(rng.integers(1, 120))
+        out.append(bytes(alphabet[i] for i in rng.integers(0, len(alphabet), k)))
+    return out
+
+
+def obj_malformed():
+    """obj_malformed.json: the reference LoadObjFile code path (oracle/_ref/obj_ingest: the reference's OBJ_Loader
+    + its statement sequence over the C++ library's stringstream) on each malformed text: vertex positions as float
+    bit patterns, indices."""
+    import base64
+    import tempfile
+    subprocess.run(["make", "-C", ROOT, "ref"], check=True)
+    exe = os.path.join(ROOT, "oracle", "_ref", "obj_ingest")
+    cases = []
+    with tempfile.TemporaryDirectory() as td:
+        for text in MALFORMED + _malformed_soup():
+            src, b = os.path.join(td, "m.obj"), os.path.join(td, "o.bin")
+            with open(src, "wb") as f:
+                f.write(text)
+            subprocess.run([exe, src, b], check=True)
+            raw = open(b, "rb").read()
+            nv, ni = (int(x) for x in np.frombuffer(raw[:8], np.uint32))
+            pos = np.frombuffer(raw[8:8 + 12 * nv], np.uint32)
+            idx = np.frombuffer(raw[8 + 12 * nv:8 + 12 * nv + 4 * ni], np.uint32)
+            cases.append({"text_b64": base64.b64encode(text).decode(), "position_bits": pos.tolist(),
+                          "indices": idx.tolist()})
+    with open(os.path.join(HERE, "obj_malformed.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py --malformed (oracle/_ref/obj_ingest)", "cases": cases},
+                  f, indent=0)
 
 
 def frames():
@@ -246,6 +305,9 @@ def seam_leaks():
 
 
 if __name__ == "__main__":
+    if "--malformed" in sys.argv:
+        obj_malformed()
+        sys.exit(0)
     if "--seams" in sys.argv:
         seam_leaks()
         sys.exit(0)
@@ -255,4 +317,5 @@ if __name__ == "__main__":
     if "--frames-only" not in sys.argv:
         camera()
         obj_ingest()
+        obj_malformed()
     frames()

@@ -182,8 +182,26 @@ def test_bench_native_comm_failure_falls_back_together(tmp_path):
     p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     assert "simulated RCCL failure" in p.stderr
+    assert "comm aborted on rank 0" in p.stderr  # rank 0's communicator came up: aborted, no collective on it
     out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
     assert out["config"]["strips_loop"] == "torch.distributed gather"
     spec = scenes.config("C2F").with_size(64, 44)
     o8, _, _ = oracle.Scene(spec).render_spec(spec, nthreads=2, want_float=False)
     assert np.array_equal(np.load(img), o8)
+
+
+def test_bench_native_loop_error_aborts_communicator(tmp_path):
+    """An error inside bench.py's native strips loop (the render call raises on its 3rd call, a partly filled batch
+    of 4 pending): the communicator is aborted (rt_comm_abort: no draining gather the other ranks might never match,
+    VERDICT r4 #7), not closed, and the error propagates (non-zero exit)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, RT_BENCH_TEST_BACKEND="tests.bench_cpu_backend:CpuBackendStepFails", STEP_FAIL_AT="3",
+               PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""), OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--mode", "strips", "--config", "C2F", "--size", "64x44",
+           "--steps", "3", "--warmup", "4", "--settle-ms", "0", "--resettle-ms", "0", "--extra=", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert p.returncode != 0
+    assert "simulated render failure" in p.stderr
+    assert "comm aborted" in p.stderr and "comm closed" not in p.stderr, p.stderr[-3000:]

@@ -100,6 +100,63 @@ def test_loopback_frames_in_one_launch_equal_oracle(nranks):
     c.close()
 
 
+# The multi-GPU configs through the same loop: the workloads the 8-GPU run tiles first. C5 is 4 spp
+# (the KS = 2 sample-lane kernel: a wave covers 4 x 4 pixels, RayGen.hlsl:33's pixel mapping per sample) over 257
+# instances, C4 64 instances and 2 lights. Eyes: the config's own first, then moves around the grid.
+GRID_EYES = {"C4": [(18.0, 14.0, 18.0), (15.0, 12.0, 21.0), (21.0, 16.0, 14.0), (-17.0, 13.0, 19.0)],
+             "C5": [(30.0, 22.0, 30.0), (26.0, 18.0, 34.0), (34.0, 26.0, 25.0), (-28.0, 20.0, 31.0)]}
+_GRID_ORACLE = {}
+
+
+def _grid_spec(name, size, k):
+    sp = scenes.config(name).with_size(*size)
+    _, at, up = sp.camera
+    sp.camera = (GRID_EYES[name][k], at, up)
+    return sp
+
+
+def _grid_oracle(name, size, k):
+    key = (name, size, k)
+    if key not in _GRID_ORACLE:
+        sp = _grid_spec(name, size, k)
+        _GRID_ORACLE[key] = oracle.Scene(sp).render_spec(sp, nthreads=16, want_float=False, schedule=1)[0]
+    return _GRID_ORACLE[key]
+
+
+@pytest.mark.parametrize("name,size,nranks,calls", [
+    ("C5", (960, 540), 8, (4, 4, 3)),      # 540 rows: 67.5 strips over 8 ranks (ragged), the last batch 3 of 4
+    ("C5", (3840, 2160), 8, (1,)),         # one full BASELINE frame (configs[4]), a batch of 1 of 4
+    ("C4", (1920, 1080), 4, (4, 4, 2)),    # BASELINE configs[3] at its N = 4
+], ids=["C5-960x540-N8", "C5-3840x2160-N8", "C4-1920x1080-N4"])
+def test_loopback_multisample_and_grid_frames_equal_oracle(name, size, nranks, calls):
+    """rt_render_strips_frames at 4 frames per gather and up to 4 frames per launch (one camera each, grid z =
+    frame) on the communicator's own render streams, the tile balance at its default: every assembled frame of
+    C5 (4 spp, N = 8) and C4 (N = 4) equals the oracle's, the last batch partly filled and gathered at
+    rt_comm_synchronize."""
+    W, H = size
+    c = rt.Context(0)
+    scenes.upload(c, _grid_spec(name, size, 0))
+    comm = rt.Comm.loopback(c, nranks)
+    comm.set_batch(4)
+    neyes = len(GRID_EYES[name])
+    frames, cams, k = [], [], 0
+    for nf in calls:
+        fs = [torch.full((H, W, 4), 7, dtype=torch.uint8, device="cuda") for _ in range(nf)]
+        cs = [(k + j) % neyes for j in range(nf)]
+        cb = np.concatenate([_grid_spec(name, size, q).camera_buffer().ravel() for q in cs])
+        comm.render_strips_frames(W, H, fs, cameras=cb, stream=None)
+        frames += fs
+        cams += cs
+        k += nf
+    comm.synchronize()
+    for f, q in zip(frames, cams):
+        got = f.cpu().numpy()
+        bad = int((got != _grid_oracle(name, size, q)).any(axis=2).sum())
+        assert bad == 0, f"{name} {W}x{H} N={nranks}: camera {q}: {bad} pixels differ"
+    comm.close()
+    c.close()
+
+
 @pytest.mark.parametrize("loop", ["loopback8", "rccl1"])
 def test_close_with_partly_filled_batch_returns(loop):
     """rt_comm_destroy with a partly filled slot and no rt_comm_synchronize: 2 frames at 3
@@ -172,4 +229,66 @@ def test_forget_stream_then_tlas_update():
     torch.cuda.synchronize()
     o8, _, _ = oracle.Scene(spec).render_spec(spec, nthreads=16, want_float=False, schedule=1)
     assert np.array_equal(out.cpu().numpy(), o8)
+    c.close()
+
+
+@pytest.mark.parametrize("loop", ["loopback8", "rccl1"])
+def test_abort_with_partly_filled_batch_returns(loop):
+    """rt_comm_abort, the failure path: 2 frames at 3 frames per gather, then abort() — no drain,
+    no further collective (a real peer may never call again), ncclCommAbort for RCCL. It returns under the test
+    timeout, and the context keeps rendering correct frames, also through a new communicator."""
+    size = (960, 544)
+    W, H = size
+    c = rt.Context(0)
+    scenes.upload(c, _spec(size, 0))
+    comm = rt.Comm.loopback(c, 8) if loop == "loopback8" else rt.Comm(c, 1, 0, rt.comm_unique_id())
+    comm.set_batch(3)
+    frames = [torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    for k in range(2):
+        c.set_camera(_spec(size, k + 1).camera_buffer())
+        comm.render_strips(W, H, frames[k], None)
+    comm.abort()
+    comm.abort()  # a second abort (or close) of the same Python object is a no-op
+    comm.close()
+    torch.cuda.synchronize()
+    c.set_camera(_spec(size, 3).camera_buffer())
+    out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+    c.dispatch(W, H, out, stream=torch.cuda.current_stream().cuda_stream)
+    comm2 = rt.Comm.loopback(c, 2)
+    again = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+    comm2.render_strips(W, H, again, None)
+    comm2.close()
+    torch.cuda.synchronize()
+    _check([out, again], size, [3, 3], f"{loop} after abort")
+    c.close()
+
+
+def test_many_emulated_ranks_never_synchronise_the_device():
+    """every emulated rank's row list is its own tile-balance shape, so 40 ranks exceed the context's table
+    of cost maps. A full table must not cost a device-wide synchronisation per launch (it used to evict with
+    hipDeviceSynchronize on every rank's dispatch): the launches that find no idle map run the plain grid. Over
+    steady-state frames the context's device-sync counter does not move, and every frame equals the oracle's."""
+    size = (1920, 1080)
+    W, H = size
+    c = rt.Context(0)
+    scenes.upload(c, _spec(size, 0))
+    comm = rt.Comm.loopback(c, 40)
+    comm.set_batch(2)
+    frames = [torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(comm.depth)]
+    for k in range(comm.depth):  # warm: plans, slots, the cost maps
+        comm.render_strips(W, H, frames[k], None)
+    comm.synchronize()
+    before = c.counters()
+    cams = []
+    for k in range(2 * comm.depth):
+        q = k % len(EYES)
+        c.set_camera(_spec(size, q).camera_buffer())
+        comm.render_strips(W, H, frames[k % comm.depth], None)
+        cams.append(q)
+    comm.synchronize()
+    after = c.counters()
+    assert after["device_syncs"] == before["device_syncs"], (before, after)
+    assert after["balance_maps"] <= 32 and after["balance_full"] + after["balance_recycled"] > 0, after
+    _check(frames, size, cams[-comm.depth:], "40 emulated ranks")
+    comm.close()
     c.close()

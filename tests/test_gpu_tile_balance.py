@@ -188,3 +188,64 @@ def test_adaptive_balance_multi_frame_launch_and_off():
     with pytest.raises(rt.RtError):
         c.set_tile_balance(5)
     c.close()
+
+
+def test_refused_items_fall_back_to_the_plain_grid():
+    """a work list whose parts exceed the launch's budget must not silently drop any. With a budget of
+    64 extra waves (RT_BALANCE_FORCED_CAP, read at context creation) every-tile-in-16 (mode 3) cannot fit: the plan
+    refuses the excess, reports it (tile_balance_info refused / refused_plans) and hands the launch the plain grid's
+    list, so the frame and every traversal counter equal the oracle's plain (unsplit) packet walk. The cover check
+    (RT_BALANCE_CHECK) passes on the fallback list."""
+    spec = scenes.config("C4").with_size(256, 136)
+    os.environ["RT_BALANCE_FORCED_CAP"] = "64"
+    os.environ["RT_BALANCE_CHECK"] = "1"
+    try:
+        c = rt.Context(0)
+    finally:
+        del os.environ["RT_BALANCE_FORCED_CAP"], os.environ["RT_BALANCE_CHECK"]
+    scenes.upload(c, spec)
+    c.set_tile_balance(3)
+    c.set_stats(True)
+    c.stats_reset()
+    g8, g32 = render(c, spec)
+    torch.cuda.synchronize()
+    s = c.stats()
+    info = c.tile_balance_info()
+    o8, o32, ost = oracle.Scene(spec).render_spec(spec, nthreads=8, split=0)
+    assert info["refused"] > 0 and info["refused_plans"] == 1 and info["split"] == 0, info
+    assert info["check_bad"] == 0, info
+    assert np.array_equal(g8.cpu().numpy(), o8) and np.array_equal(g32.cpu().numpy(), o32)
+    assert [s[k] for k in KEYS] == [int(x) for x in ost[:6]]
+    assert [s[k] for k in FETCH] == [int(x) for x in ost[9:12]]
+    c.close()
+
+
+def test_split_tiles_rejoin_when_the_view_becomes_cheap():
+    """a split tile's whole-wave time is not refreshed while it stays split, so the plan must judge it from
+    its parts. C4 at 1080p from its own camera (a tail: the plan splits the costliest tiles, the list pays), then the
+    camera turned to the sky (every ray misses: uniform, cheap tiles): within a few re-plans nothing is split and the
+    list no longer pays. Every frame equals the oracle's."""
+    spec = scenes.config("C4")
+    sky = spec.with_size(spec.width, spec.height)
+    sky.camera = ((18.0, 14.0, 18.0), (60.0, 40.0, 60.0), (0.0, 1.0, 0.0))
+    c = checked_context()
+    scenes.upload(c, spec)
+    s = torch.cuda.Stream()
+    outs = [render(c, spec, stream=s)[0] for _ in range(40)]
+    torch.cuda.synchronize()
+    costly = c.tile_balance_info()
+    c.set_camera(sky.camera_buffer())
+    outs_sky = [render(c, sky, stream=s)[0] for _ in range(80)]
+    torch.cuda.synchronize()
+    cheap = c.tile_balance_info()
+    assert costly["pays"] == 1 and costly["split"] > 0, costly
+    assert cheap["pays"] == 0 and cheap["split"] == 0 and cheap["plans"] > costly["plans"], cheap
+    assert cheap["check_bad"] == 0 and cheap["refused"] == 0, cheap
+    assert 0 < cheap["slots"] <= 10 * 1024, cheap  # the load bound's slots come from the runtime's occupancy
+    o8, _, _ = oracle.Scene(spec).render_spec(spec, nthreads=16, want_float=False, schedule=1)
+    s8, _, _ = oracle.Scene(sky).render_spec(sky, nthreads=16, want_float=False, schedule=1)
+    for k in (0, 1, len(outs) - 1):
+        assert np.array_equal(outs[k].cpu().numpy(), o8), f"costly frame {k}"
+    for k in (0, 1, len(outs_sky) - 1):
+        assert np.array_equal(outs_sky[k].cpu().numpy(), s8), f"sky frame {k}"
+    c.close()

@@ -1,0 +1,48 @@
+#!/bin/bash
+# One GPU call of a round-5 session (run on the GPU box from the repo root). STEPS selects: tests, bench, strips5,
+# shares, balance, waves. Each step under its own time limit; the script stops at the first failure.
+#   STEPS="tests bench" TAG=r05a bash tools/gpu_r05.sh
+set -u
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+TAG="${TAG:-r05}"
+O="$R/gpurun_out"
+mkdir -p "$O"
+cd "$R"
+for step in ${STEPS:-tests}; do
+  case $step in
+    tests)
+      timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} \
+        > "$O/gputest_${TAG}.log" 2>&1 || { echo "gpu tests failed rc=$?"; grep -E "FAIL|Error|error" "$O/gputest_${TAG}.log" | head -20; tail -40 "$O/gputest_${TAG}.log"; exit 1; }
+      tail -3 "$O/gputest_${TAG}.log" ;;
+    bench)
+      timeout -k 10 600 python3 bench.py ${BENCH_ARGS:-} > "$O/bench_${TAG}.json" 2> "$O/bench_${TAG}.err" \
+        || { echo "bench failed rc=$?"; tail -20 "$O/bench_${TAG}.err"; exit 1; }
+      head -c 1500 "$O/bench_${TAG}.json"; echo ;;
+    strips5)
+      # the C5 (4 spp, 4K) and C4 tiled loops through the loopback transport
+      for cfg in "C5 8" "C4 4"; do
+        set -- $cfg
+        timeout -k 10 300 python3 bench.py --mode strips --loopback $2 --config $1 --extra= --no-cpu-baseline \
+          --steps ${STRIPS_STEPS:-40} --warmup 8 \
+          > "$O/strips_${1}_lb${2}_${TAG}.json" 2> "$O/strips_${1}_lb${2}_${TAG}.err" \
+          || { echo "strips loopback $1 $2 failed rc=$?"; tail -20 "$O/strips_${1}_lb${2}_${TAG}.err"; exit 1; }
+        head -c 900 "$O/strips_${1}_lb${2}_${TAG}.json"; echo
+      done ;;
+    shares)
+      timeout -k 10 900 python3 -u tools/share_ceiling.py ${SHARE_ARGS:-} > "$O/shares_${TAG}.jsonl" 2> "$O/shares_${TAG}.err" \
+        || { echo "share_ceiling failed rc=$?"; tail -20 "$O/shares_${TAG}.err"; exit 1; }
+      cat "$O/shares_${TAG}.jsonl" ;;
+    balance)
+      timeout -k 10 600 python3 tools/balance_ab.py ${BAL_ARGS:-} > "$O/balance_${TAG}.txt" 2>&1 \
+        || { echo "balance_ab failed rc=$?"; tail -20 "$O/balance_${TAG}.txt"; exit 1; }
+      cat "$O/balance_${TAG}.txt" ;;
+    waves)
+      for b in 0 1; do
+        timeout -k 10 120 python3 tools/wave_times.py --lib realtimeraytracing_gradproject_amd/lib/variants/wavetimes/librtamd.so \
+          --config ${WT_CONFIG:-C4} --balance $b ${WT_ARGS:-} > "$O/wave_times_${TAG}_b$b.txt" 2>&1 \
+          || { echo "wave_times failed rc=$?"; tail -20 "$O/wave_times_${TAG}_b$b.txt"; exit 1; }
+        cat "$O/wave_times_${TAG}_b$b.txt"
+      done ;;
+  esac
+done
+exit 0

@@ -65,5 +65,28 @@ for x in range(8):
     m = xcc == x
     if m.any():
         print(f"XCC {x}: waves {m.sum()} last end {t1[m].max() * 10 / 1000:.1f} us mean dur {dur[m].mean():.2f} us")
-np.savez(os.path.join(ROOT, "gpurun_out", f"wt_{a.config}_n{a.share}_b{a.balance}.npz"), t0=t0, t1=t1, ids=np.nonzero(live)[0], xcc=xcc)
+# residency: the instantaneous peak of resident waves (a sweep over the start / end events, not a bin
+# mean), and where the waves sat: HW_ID (gfx9 layout) = wave slot [3:0], SIMD [5:4], CU [11:8], SH [12], SE [15:13]
+hw = u[:, 3]
+simd_key = (xcc.astype(np.int64) << 16) | ((hw >> 8) & 0xff).astype(np.int64) << 4 | ((hw >> 4) & 3)
+cu_key = simd_key >> 2
+ev_t = np.concatenate([t0, t1])
+ev_d = np.concatenate([np.ones_like(t0), -np.ones_like(t1)])
+order = np.lexsort((ev_d, ev_t))  # ends before starts at equal clocks
+peak = int(np.cumsum(ev_d[order]).max())
+per_simd = []
+for key in np.unique(simd_key):
+    m = simd_key == key
+    et = np.concatenate([t0[m], t1[m]])
+    ed = np.concatenate([np.ones(m.sum(), np.int64), -np.ones(m.sum(), np.int64)])
+    o = np.lexsort((ed, et))
+    per_simd.append(int(np.cumsum(ed[o]).max()))
+per_simd = np.array(per_simd)
+slot_ids = np.unique(hw & 0xf)
+print(f"residency: peak {peak} waves at once; {len(np.unique(cu_key))} CUs, {len(per_simd)} SIMDs seen; most waves at "
+      f"once on one SIMD {per_simd.max()} (SIMDs reaching it: {(per_simd == per_simd.max()).sum()}); HW wave slot ids "
+      f"used {slot_ids.min()}..{slot_ids.max()}; the plan's load-bound slots (rt_tile_balance_info[15]): "
+      f"{c.tile_balance_info().get('slots')}")
+np.savez(os.path.join(ROOT, "gpurun_out", f"wt_{a.config}_n{a.share}_b{a.balance}.npz"), t0=t0, t1=t1, ids=np.nonzero(live)[0], xcc=xcc,
+         hw=hw)
 c.close()
