@@ -27,6 +27,7 @@ APP       := $(LIBDIR)/rt_app
 ORACLE    := oracle/liboracle.so
 BASELINE  := oracle/libbaseline.so
 RCPCHECK  := tools/bin/recip_check
+OCCPROBE  := tools/bin/occupancy_probe
 
 HDRS      := include/rt_api.h $(SRC)/rt_device.hpp $(SRC)/rt_internal.hpp
 
@@ -51,7 +52,7 @@ DEFS_rays2     := -DRT_PACKET_RAYS=2 -DRT_SAMPLE_LANES=0 -DRT_RCP_EXACT=0
 DEFS_alt       := -DRT_PACKET_OCT=0 -DRT_REF_NOREFL=0 -DRT_RCP_EXACT=7 -DRT_MS_WIDE=1
 DEFS_wavetimes := -DRT_WAVE_TIMES=1
 
-all: $(LIB) $(APP) $(ORACLE) $(BASELINE) $(RCPCHECK) $(VLIBS)
+all: $(LIB) $(APP) $(ORACLE) $(BASELINE) $(RCPCHECK) $(OCCPROBE) $(VLIBS)
 
 $(VDIR)/%/librtamd.so: $(VSRCS)
 	bash tools/build_variant.sh $* $(DEFS_$*) > /dev/null
@@ -96,6 +97,11 @@ $(RCPCHECK): tools/recip_check.hip $(SRC)/rt_device.hpp include/rt_api.h
 	mkdir -p tools/bin
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off -o $@ $<
 
+# resident waves per SIMD by register footprint (the wave-time traces' 7-wave ceiling)
+$(OCCPROBE): tools/occupancy_probe.hip
+	mkdir -p tools/bin
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
+
 $(BUILD) $(LIBDIR):
 	mkdir -p $@
 
@@ -126,6 +132,6 @@ $(ASAN):
 	mkdir -p $@
 
 clean:
-	rm -rf $(BUILD) $(LIB) $(APP) $(ORACLE) $(BASELINE) $(RCPCHECK) $(VDIR)
+	rm -rf $(BUILD) $(LIB) $(APP) $(ORACLE) $(BASELINE) $(RCPCHECK) $(OCCPROBE) $(VDIR)
 
 .PHONY: all clean ref asan

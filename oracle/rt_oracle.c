@@ -992,6 +992,9 @@ static int opk_node(const o4node* nd, const opkray* ry, float tmin, ohit* h, int
   uint64_t hm[4] = {0, 0, 0, 0};
   uint32_t vkey[OPK][4];
   OST(9, 1); /* one node fetch per wave */
+#ifdef OSTUDY_NODE_HOOK /* design studies only (tools/path_study.c): node fetches by tree level and ray kind */
+  OSTUDY_NODE_HOOK(leaves != NULL, any);
+#endif
   for (int l = 0; l < OPK; ++l) {
     for (int k = 0; k < 4; ++k) {
       float tlx = fmaf(nd->lox[k], ry->invd[l].x, ry->no[l].x), thx = fmaf(nd->hix[k], ry->invd[l].x, ry->no[l].x);
@@ -1309,8 +1312,9 @@ typedef struct {
   const float* mat;
   int mode, k, brute;
   uint32_t W, H;
-  int split; /* the device's forced tile-balance layouts (rt_set_tile_balance 2..4): 1 every tile in 2 x 2 parts,
-                2 in 4 x 4, 3 by tile position (tx + 2 ty) % 3 -> whole / 2 x 2 / 4 x 4; capped by the tile shape */
+  int split; /* the device's forced tile-balance layouts (rt_set_tile_balance 2..5): 1 every tile in 2 x 2 parts,
+                2 in 4 x 4, 3 by tile position (tx + 2 ty) % 3 -> whole / 2 x 2 / 4 x 4, 4 in 8 x 8 (one pixel each);
+                capped by the tile shape */
 } octx;
 
 static int trace_any(const octx* c, vec3 P, vec3 dir, ostats* st) {
@@ -1595,7 +1599,7 @@ static void* render_tiles(void* arg) {
   const uint32_t tw = (c->W + tp - 1) / tp, th = (j->nrows + tp - 1) / tp;
   /* tile balance (rt_trace.hip packet_geometry / k_tile_plan): the parts a tile is traced as, each its own
    * packet with the lanes outside its sub-rectangle dead; 4 x 4 parts need 4-pixel tile sides */
-  const uint32_t kmax = tp >= 4u ? 2u : tp >= 2u ? 1u : 0u;
+  const uint32_t kmax = tp >= 8u ? 3u : tp >= 4u ? 2u : tp >= 2u ? 1u : 0u;
   for (uint32_t t = j->tid; t < tw * th; t += j->nthreads) {
     const uint32_t tx = t % tw, ty = t / tw;
     uint32_t px[OPK], py[OPK], orow[OPK];
@@ -1612,9 +1616,9 @@ static void* render_tiles(void* arg) {
       oy[l] = ((float)(s / (uint32_t)lanes_k) + 0.5f) / (float)lanes_k;
       acc[l] = mk(0, 0, 0);
     }
-    uint32_t code = c->split == 1 ? 1u : c->split == 2 ? 2u : c->split == 3 ? (tx + 2u * ty) % 3u : 0u;
+    uint32_t code = c->split == 1 ? 1u : c->split == 2 ? 2u : c->split == 3 ? (tx + 2u * ty) % 3u : c->split == 4 ? 3u : 0u;
     if (code > kmax) code = kmax;
-    const uint32_t nparts = code == 0u ? 1u : code == 1u ? 4u : 16u, pq = 1u << code;
+    const uint32_t nparts = code == 0u ? 1u : code == 1u ? 4u : code == 2u ? 16u : 64u, pq = 1u << code;
     for (uint32_t part = 0; part < nparts; ++part) {
       for (int l = 0; l < OPK; ++l) {
         const uint32_t p = (uint32_t)l / ns;

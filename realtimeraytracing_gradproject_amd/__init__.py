@@ -660,7 +660,7 @@ class Context:
         self._check(self._lib.rt_set_tile_rows(self._h, rows), "rt_set_tile_rows")
 
     def set_tile_balance(self, mode: int):
-        """rt_set_tile_balance: 0 off, 1 adaptive (default), 2 / 3 / 4 forced split layouts (tests)."""
+        """rt_set_tile_balance: 0 off, 1 adaptive (default), 2 / 3 / 4 / 5 forced split layouts (tests)."""
         self._check(self._lib.rt_set_tile_balance(self._h, mode), "rt_set_tile_balance")
 
     def tile_balance_info(self) -> dict:

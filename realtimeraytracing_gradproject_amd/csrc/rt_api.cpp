@@ -257,6 +257,7 @@ struct rt_ctx {
   double tlas_wall_ms = 0.0;     // host wall time of the last rt_tlas_build
   // frame state
   rt::FrameParams fp{};
+  float cam_cb[64] = {};  // rt_set_camera's buffer: view, proj, viewInv, projInv in XMMATRIX memory order
   bool have_camera = false, have_shading = false;
   int schedule = RT_SCHED_PACKET;
   uint32_t tile_rows = 8;  // rt_set_tile_rows
@@ -275,7 +276,9 @@ struct rt_ctx {
   // RT_BALANCE_SPLIT, RT_BALANCE_FRONT, RT_BALANCE_BUDGET — the extra waves as a divisor of the tiles — at context
   // creation) and the list's cover check (RT_BALANCE_CHECK, tests)
   uint32_t bal_split = 1, bal_front = 8, bal_check = 0, bal_budget = 8;
-  uint32_t bal_forced_cap = 0;  // RT_BALANCE_FORCED_CAP (tests): the forced layouts' extra waves (0: 15 x the tiles)
+  uint32_t bal_forced_cap = 0;  // RT_BALANCE_FORCED_CAP (tests): the forced layouts' extra waves (0: 63 x the tiles)
+  uint32_t bal_prio = 1;        // RT_BALANCE_PRIO (A/B): the front class's waves raise their issue priority
+  uint32_t bal_fine = 1;        // RT_BALANCE_FINE (A/B): adaptive plans may split a tile into 64 one-pixel parts
   static constexpr size_t kMaxBalanceMaps = 32;
   std::vector<BalanceMap> bal;
   uint64_t bal_clock = 0;
@@ -499,6 +502,8 @@ rt_status rt_create(int hip_device, rt_ctx_t* out) {
   if (const char* ev = std::getenv("RT_BALANCE_CHECK")) c->bal_check = std::strtoul(ev, nullptr, 10) ? 1u : 0u;
   if (const char* ev = std::getenv("RT_BALANCE_BUDGET"))
     c->bal_budget = std::max<uint32_t>(1u, (uint32_t)std::strtoul(ev, nullptr, 10));
+  if (const char* ev = std::getenv("RT_BALANCE_PRIO")) c->bal_prio = std::strtoul(ev, nullptr, 10) ? 1u : 0u;
+  if (const char* ev = std::getenv("RT_BALANCE_FINE")) c->bal_fine = std::strtoul(ev, nullptr, 10) ? 1u : 0u;
   if (const char* ev = std::getenv("RT_BALANCE_FORCED_CAP")) c->bal_forced_cap = (uint32_t)std::strtoul(ev, nullptr, 10);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&c->d_stats, RT_STAT_COUNT * sizeof(unsigned long long)) != hipSuccess ||
@@ -792,7 +797,7 @@ rt_status rt_tlas_export(rt_ctx_t c, void* nodes, size_t nodes_bytes) {
 
 rt_status rt_set_camera(rt_ctx_t c, const float cb[64]) {
   if (!c || !cb) return fail(c, RT_E_INVALID, "rt_set_camera: null argument");
-  std::memcpy(c->fp.cb, cb, 64 * sizeof(float));  // RayGen's constants are derived per launch (frame_cam)
+  std::memcpy(c->cam_cb, cb, 64 * sizeof(float));  // RayGen's constants are derived per launch (frame_cam)
   c->have_camera = true;
   return RT_OK;
 }
@@ -831,7 +836,7 @@ rt_status rt_set_tile_rows(rt_ctx_t c, int rows) {
 
 rt_status rt_set_tile_balance(rt_ctx_t c, int mode) {
   if (!c) return RT_E_INVALID;
-  if (mode < 0 || mode > 4) return fail(c, RT_E_INVALID, "rt_set_tile_balance: mode 0 .. 4");
+  if (mode < 0 || mode > 5) return fail(c, RT_E_INVALID, "rt_set_tile_balance: mode 0 .. 5");
   c->balance = mode;
   return RT_OK;
 }
@@ -1235,7 +1240,7 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
   c->fp.out_bpp = out_bpp;
   c->fp.nframes = nframes;
   c->fp.frame_bytes = (uint32_t)frame_bytes;
-  for (uint32_t z = 0; z < nframes; ++z) frame_cam(cams ? cams + 64 * z : c->fp.cb, c->fp.cam[z]);
+  for (uint32_t z = 0; z < nframes; ++z) frame_cam(cams ? cams + 64 * z : c->cam_cb, c->fp.cam[z]);
   rt::SceneView sv = scene_view(c);
   if (sv.stack_cap > rt::kMaxTraversalStack)
     return fail(c, RT_E_UNSUPPORTED, "rt_dispatch_rays: BVH too deep for the traversal stack");
@@ -1293,10 +1298,12 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
       a.stats = forced ? nullptr : m->stats_dev;
       a.ntiles = ntiles;
       a.slots = 0;  // set below for a plan: the list's kernel's occupancy x CUs, from the runtime
-      a.kmax_code = g.kmax_code;
+      // adaptive plans split into at most 16 parts unless RT_BALANCE_FINE allows the 64 single-pixel parts
+      a.kmax_code = forced ? g.kmax_code : std::min<uint32_t>(g.kmax_code, c->bal_fine ? 3u : 2u);
       a.force = forced ? (uint32_t)(c->balance - 1) : 0u;
       a.split = c->bal_split;
       a.front = c->bal_front;
+      a.prio = c->bal_prio;
       a.check = c->bal_check;
       a.min_gain = 1000u;  // 10 us: above the plan kernel's own time
       a.waves_per_frame = g.waves_per_frame;
@@ -1307,14 +1314,14 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
       if (forced) {
         // tests: a fresh list per launch from the ring (RT_BALANCE_FORCED_CAP, tests: a smaller budget of extra waves,
         // so the plan must refuse parts and fall back to the plain grid's list)
-        a.extra_cap = c->bal_forced_cap ? c->bal_forced_cap : 15u * ntiles;
+        a.extra_cap = c->bal_forced_cap ? c->bal_forced_cap : 63u * ntiles;
         a.stats = m->stats_dev;
         a.slots = plan_slots(c, sv);
         plan_items = ntiles + a.extra_cap;
         bool hit;
         plan_slot = ring_acquire(c->plans, s, nullptr, &hit, &be);
         if (be != hipSuccess) return hip_fail(c, be, "tile balance: order after in-flight launches");
-        HIPCHK(c, slot_reserve(*plan_slot, ((size_t)plan_items + 2u * ntiles + 1) * 4), "hipMalloc(tile plan)");
+        HIPCHK(c, slot_reserve(*plan_slot, ((size_t)plan_items + 3u * ntiles + 1) * 4), "hipMalloc(tile plan)");
         a.plan = (uint32_t*)plan_slot->buf;
         HIPCHK(c, rt::launch_tile_plan(a, s), "tile plan launch");
         c->fp.plan = a.plan;
@@ -1333,7 +1340,7 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
           a.extra_cap = m->extra_cap;
           a.slots = plan_slots(c, sv);
           const uint32_t items = ntiles + a.extra_cap;
-          HIPCHK(c, slot_reserve(sl, ((size_t)items + 2u * ntiles + 1) * 4), "hipMalloc(tile plan)");
+          HIPCHK(c, slot_reserve(sl, ((size_t)items + 3u * ntiles + 1) * 4), "hipMalloc(tile plan)");
           a.plan = (uint32_t*)sl.buf;
           HIPCHK(c, rt::launch_tile_plan(a, ps), "tile plan launch");
           HIPCHK(c, hipEventRecord(m->pend_ev, ps), "tile balance: record the plan");
@@ -1401,8 +1408,8 @@ rt_status rt_raster_draw(rt_ctx_t c, const rt_blas_t* draws, uint32_t ndraws, co
     for (int i = 0; i < 3; ++i) rv.o2w[j * 4 + i] = T[i * 4 + j];
     rv.o2w[j * 4 + 3] = j == 3 ? 1.0f : 0.0f;
   }
-  std::memcpy(rv.view, c->fp.cb, 16 * sizeof(float));
-  std::memcpy(rv.proj, c->fp.cb + 16, 16 * sizeof(float));
+  std::memcpy(rv.view, c->cam_cb, 16 * sizeof(float));
+  std::memcpy(rv.proj, c->cam_cb + 16, 16 * sizeof(float));
   rv.width = W;
   rv.height = H;
   (void)hipSetDevice(c->device);

@@ -132,8 +132,9 @@ struct FrameCam {
 };
 
 // Everything a frame needs besides the scene buffers; passed by value as a kernel argument.
+// (The camera buffer itself stays on the host, rt_ctx::cam_cb: RayGen reads the per-frame FrameCam derived from it,
+// and every byte here is kernel-argument data copied per launch.)
 struct FrameParams {
-  float cb[64];  // view, proj, viewInv, projInv in XMMATRIX memory order (the context's camera)
   LightRec lights[kMaxLights];
   MaterialRec material;
   uint32_t nlights;
@@ -153,8 +154,8 @@ struct FrameParams {
   uint32_t frame_bytes;
   FrameCam cam[kMaxLaunchFrames];
   // Tile balance (packet schedule, rt_set_tile_balance). plan: the launch's wave work list written by k_tile_plan
-  // (plan[0] = item count, plan[1 + i] = item i = wave slot << 6 | part << 2 | split code; split code 0: the whole
-  // tile, 1: quadrant `part` of 4, 2: cell `part` of 16), dealt to the waves of a 1-D grid in list order (costliest
+  // (plan[0] = item count, plan[1 + i] = item i = wave slot << 8 | part << 2 | split code, bit 31 the front class;
+  // split code 0: the whole tile, 1: quadrant `part` of 4, 2: cell `part` of 16, 3: pixel `part` of 64), dealt to the waves of a 1-D grid in list order (costliest
   // first), or null: wave slot = the plain grid's wave index. cost: per wave slot, two words written at wave end (or
   // null): [0] the ticks (s_memrealtime) of the tile's last whole wave, bit 31 set by every part of a split since
   // (the whole time is then older than the parts), [1] the costliest part of the tile's last split (ticks << 2 |
@@ -169,7 +170,7 @@ struct FrameParams {
 // Tile-balance split codes (FrameParams::plan): parts per tile. The costliest quadrant of the costliest C4 tiles
 // takes 0.55 of the whole packet's fetches, the costliest 2 x 2 cell 0.35 (tools/split_study.py): the kernel's
 // estimate of a whole tile from one part's time, and the plan's estimate of a part from the whole.
-RT_HD uint32_t split_parts(uint32_t code) { return code == 0u ? 1u : code == 1u ? 4u : 16u; }
+RT_HD uint32_t split_parts(uint32_t code) { return code == 0u ? 1u : code == 1u ? 4u : code == 2u ? 16u : 64u; }
 
 // The trace kernels read one node pool and one triangle pool per scene: [TLAS | BLAS 0 | BLAS 1 ..]
 // with child refs rebased to pool indices (BLAS leaves -> ~(global triangle slot)). A uniform base

@@ -88,7 +88,7 @@ struct PacketGeometry {
   uint32_t grid_x = 0, grid_y = 0;     // workgroups of one frame
   uint32_t wx = 1, wy = 1, wl = 1;     // waves of a workgroup along x, y; total
   uint32_t waves_per_frame = 0;
-  uint32_t kmax_code = 0;              // largest tile-balance split code the tile allows (0: none, 1: 4, 2: 16)
+  uint32_t kmax_code = 0;              // largest tile-balance split code the tile allows (0: none, 1: 4, 2: 16, 3: 64)
   bool plannable = false;              // a work list may drive the launch
 };
 PacketGeometry packet_geometry(const SceneView& sc, const FrameParams& fp, int schedule);
@@ -115,7 +115,7 @@ struct PlanArgs {
   uint32_t* cost;         // per wave slot of the plain grid, 2 words: the last whole wave's time (ticks), the
                           // costliest part of the last split (time << 2 | layout; cleared here when splitting)
   uint32_t* plan;         // out: [0] item count, [1 ..] items (ntiles + extra_cap words), then the cover check's
-                          // scratch (2 ntiles words): 1 + 3 ntiles + extra_cap words in all
+                          // scratch (3 ntiles words): 1 + 4 ntiles + extra_cap words in all
   PlanStats* stats;       // host-mapped, or null
   uint32_t ntiles;        // wave slots of the plain grid, every frame of the launch
   uint32_t extra_cap;     // items beyond ntiles the launch's grid has waves for
@@ -127,10 +127,13 @@ struct PlanArgs {
   uint32_t front;         // adaptive: items estimated above front / 16 x the load bound go first (0: tile order)
   uint32_t check;         // diagnostics: verify the list covers every tile once (PlanStats::bad)
   uint32_t min_gain;      // adaptive: ticks the costliest tile must outlast the load bound by (the plan's own time)
+  uint32_t prio;          // adaptive: mark the front class's items (bit 31): their waves raise their issue priority
   uint32_t waves_per_frame, grid_x, wx, wy, wl;
 };
 // one workgroup holding the costs in registers: launches of at most kPlanMaxTiles wave slots
 constexpr uint32_t kPlanMaxTiles = 32u * 1024u;
+// work-list items: wave slot << 8 | part << 2 | split code, bit 31 the front class (PlanArgs::prio)
+constexpr uint32_t kPlanSlotMask = 0x7fffffu;
 hipError_t launch_tile_plan(const PlanArgs& a, hipStream_t stream);
 
 hipError_t launch_trace_rays(const SceneView& scene, const float* rays, uint32_t n, bool any_hit, bool cull,

@@ -1346,9 +1346,15 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
 
 // The pixel store (RayGen.hlsl:42, gOutput = float4(color, 1) into the R8G8B8A8_UNORM UAV): frame `frame` of
 // the launch, RGBA8 or, for the tiled-frame loop's strips, RGB8 (the alpha byte is the constant 255: the assembly
-// restores it, so it never crosses xGMI). out_bpp is uniform: one branch per wave.
+// restores it, so it never crosses xGMI). out_bpp is uniform: one branch per wave. MF false (a launch of one
+// RGBA8 frame, rt_dispatch_rays): the plain RGBA8 store, no frame offset and no out_bpp read.
+template <bool MF = true>
 __device__ __forceinline__ void store_pixel(const FrameParams& fp, uint32_t* out, uint32_t o, V3 a, uint32_t frame) {
   const uint32_t r = unorm8(a.x), g = unorm8(a.y), b = unorm8(a.z);
+  if (!MF) {
+    out[o] = r | (g << 8) | (b << 16) | (255u << 24);
+    return;
+  }
   char* base = (char*)out + (size_t)frame * fp.frame_bytes;
   if (fp.out_bpp == 3u) {
     uint8_t* p = (uint8_t*)base + (size_t)o * 3u;
@@ -1452,6 +1458,9 @@ __global__ __launch_bounds__(kBlock) RT_TRACE_ATTR void k_trace_frame(SceneView 
 #ifndef RT_PACKET_WX_MS
 #define RT_PACKET_WX_MS 1  // multi-sample kernels (KS = 2, 4): one-wave workgroups (C5 -2.8 % vs 2 x 1)
 #endif
+#ifndef RT_BALANCE_FRONT_PRIO
+#define RT_BALANCE_FRONT_PRIO 3  // s_setprio of a work list's front-class waves (0 .. 3)
+#endif
 #ifndef RT_MS_WIDE
 #define RT_MS_WIDE 0  // multi-sample waves: 1 = pixel tiles 8 (or 64 / samples) wide (32-B row stores), 0 = square
 #endif
@@ -1472,8 +1481,11 @@ static_assert(packet_block(1) <= 64 * kMaxPacketWaves && packet_block(2) <= 64 *
               "lane_subtree's LDS stacks: one per wave of a packet workgroup");
 
 // BAL: the launch runs a tile-balance work list or records the waves' times (FrameParams::plan / cost); the plain
-// grid's kernel carries none of it (a 64-bit start time and the slot live across the whole walk cost registers)
-template <int MODE, bool STATS, int R, int KS, bool BAL>
+// grid's kernel carries none of it (a 64-bit start time and the slot live across the whole walk cost registers).
+// MF: several frames per launch (grid z / the item's frame: a camera per frame) or RGB8 strips (rt_render_strips);
+// false for one RGBA8 frame (rt_dispatch_rays, the bench's frames loop): camera 0 at its fixed kernel-argument
+// offset and the plain store, without the per-frame address arithmetic and its dependent argument loads
+template <int MODE, bool STATS, int R, int KS, bool BAL, bool MF>
 __global__ __launch_bounds__(packet_block(KS)) __attribute__((amdgpu_waves_per_eu(
     (MODE == 1 && !STATS) ? (KS == 0 ? RT_SPP_WAVES : (KS == 1 ? RT_LS_WAVES : RT_KS_WAVES))
     : (MODE == 3 && !STATS) ? (KS == 0 ? RT_SPP_WAVES : (KS == 1 ? RT_REF0_WAVES : RT_KS_WAVES))
@@ -1502,8 +1514,11 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
     const uint32_t i = blockIdx.x * WL + w;
     if (i >= plan[0]) return;  // the grid is sized for the list's budget: the waves past its end have nothing
     const uint32_t it = plan[1 + i];
-    slot = it >> 6;
-    part = (it >> 2) & 15u;
+    // the plan's front class (the waves estimated to outlast half the load bound: the launch's critical path) issues
+    // ahead of the other waves on its SIMD
+    if (it >> 31) __builtin_amdgcn_s_setprio(RT_BALANCE_FRONT_PRIO);
+    slot = (it >> 8) & kPlanSlotMask;
+    part = (it >> 2) & 63u;
     split = it & 3u;
     bz = slot / fp.waves_per_frame;
     const uint32_t f = slot - bz * fp.waves_per_frame, wg = f / WL;
@@ -1536,7 +1551,7 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
   }
   Counters cnt;
   const uint32_t k = KS == 1 ? 1u : (KS > 1 ? (uint32_t)KS : fp.spp_side);
-  const FrameCam& cam = fp.cam[bz];
+  const FrameCam& cam = fp.cam[MF ? bz : 0u];
   if (KS == 1) {
     shade_sample_packet<MODE, STATS, R>(sc, fp, cam, px, py, 0.5f, 0.5f, inimg, acc, cnt);  // (0 + 0.5) / 1
   } else if (KS > 1) {
@@ -1581,7 +1596,7 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
     }
     if (out[r] != 0xffffffffu) {
       const uint32_t o = out[r];
-      store_pixel(fp, rgba8, o, a, bz);
+      store_pixel<MF>(fp, rgba8, o, a, MF ? bz : 0u);
       if (rgba32f && !RT_WAVE_TIMES) rgba32f[o] = make_float4(a.x, a.y, a.z, 1.0f);
     }
   }
@@ -1707,6 +1722,9 @@ __global__ __launch_bounds__(256) void k_assemble16_rgb(uint32_t W4, uint32_t H,
   }
 }
 
+// whether a launch needs the general frame kernel (MF): several frames, or RGB8 strips
+__host__ inline bool launch_multi_frame(const FrameParams& fp) { return fp.nframes > 1u || fp.out_bpp != 4u; }
+
 template <int MODE, bool STATS>
 hipError_t launch_mode(const SceneView& sc, const FrameParams& fp, const uint32_t* rows, void* rgba8,
                        float* rgba32f, unsigned long long* stats, int schedule, uint32_t plan_items, hipStream_t s) {
@@ -1717,22 +1735,31 @@ hipError_t launch_mode(const SceneView& sc, const FrameParams& fp, const uint32_
     const int ks = g.ks;
     // the plain grid, or (tile balance) one wave per work-list item, as many as the list's budget
     dim3 gp = fp.plan ? dim3((plan_items + g.wl - 1) / g.wl) : dim3(g.grid_x, g.grid_y, fp.nframes);
+    // counter passes always take the general (MF) kernel: fewer instantiations
+    const bool mf = STATS || launch_multi_frame(fp);
+#define RT_LAUNCH_PACKET_K(KS, BALV, MFV)                                                                      \
+  hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R, (R == 1 ? KS : 0), BALV, MFV>), gp,                \
+                     dim3(packet_block(R == 1 ? KS : 0)), 0, s, sc, fp, rows, (uint32_t*)rgba8, (float4*)rgba32f, \
+                     stats)
 #define RT_LAUNCH_PACKET(KS)                                                                                   \
   do {                                                                                                         \
-    if (fp.plan || fp.cost)                                                                                    \
-      hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R, (R == 1 ? KS : 0), true>), gp,                 \
-                         dim3(packet_block(R == 1 ? KS : 0)), 0, s, sc, fp, rows, (uint32_t*)rgba8,           \
-                         (float4*)rgba32f, stats);                                                             \
-    else                                                                                                       \
-      hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R, (R == 1 ? KS : 0), false>), gp,                \
-                         dim3(packet_block(R == 1 ? KS : 0)), 0, s, sc, fp, rows, (uint32_t*)rgba8,           \
-                         (float4*)rgba32f, stats);                                                             \
+    if constexpr (STATS) {                                                                                     \
+      if (fp.plan || fp.cost) RT_LAUNCH_PACKET_K(KS, true, true);                                              \
+      else RT_LAUNCH_PACKET_K(KS, false, true);                                                                \
+    } else if (fp.plan || fp.cost) {                                                                           \
+      if (mf) RT_LAUNCH_PACKET_K(KS, true, true);                                                              \
+      else RT_LAUNCH_PACKET_K(KS, true, false);                                                                \
+    } else {                                                                                                   \
+      if (mf) RT_LAUNCH_PACKET_K(KS, false, true);                                                             \
+      else RT_LAUNCH_PACKET_K(KS, false, false);                                                               \
+    }                                                                                                          \
   } while (0)
     if (ks == 1) RT_LAUNCH_PACKET(1);
     else if (ks == 2) RT_LAUNCH_PACKET(2);
     else if (ks == 4) RT_LAUNCH_PACKET(4);
     else RT_LAUNCH_PACKET(0);
 #undef RT_LAUNCH_PACKET
+#undef RT_LAUNCH_PACKET_K
   } else {
     size_t lds = (size_t)sc.lds_cap * kBlock * sizeof(int);
     hipLaunchKernelGGL((k_trace_frame<MODE, STATS>), grid, dim3(kBlock), lds, s, sc, fp, rows,
@@ -1762,7 +1789,7 @@ PacketGeometry packet_geometry(const SceneView& sc, const FrameParams& fp, int s
   g.waves_per_frame = g.grid_x * g.grid_y * g.wl;
   // a tile splits into 2 x 2 parts when both sides are >= 2 pixels, 4 x 4 when >= 4 (one ray per lane only)
   const uint32_t side = tp < tr ? tp : tr;
-  g.kmax_code = (R != 1 || RT_SHADOW_COMPACT) ? 0u : side >= 4u ? 2u : side >= 2u ? 1u : 0u;
+  g.kmax_code = (R != 1 || RT_SHADOW_COMPACT) ? 0u : side >= 8u ? 3u : side >= 4u ? 2u : side >= 2u ? 1u : 0u;
   // the shadow-ray compaction variant synchronises a workgroup's waves (barriers): no work list there, whose waves
   // past its end exit early
   g.plannable = !RT_SHADOW_COMPACT;
@@ -1835,9 +1862,9 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t* s_w,
 }
 
 // forced layouts (tests: the oracle emulates the same parts): 1 every tile in 4, 2 every tile in 16, 3 by tile
-// position ((tx + 2 ty) % 3: whole, 4, 16), capped by the tile shape
+// position ((tx + 2 ty) % 3: whole, 4, 16), 4 every tile in 64 (one pixel each), capped by the tile shape
 __device__ __forceinline__ uint32_t plan_forced(const PlanArgs& a, uint32_t t) {
-  uint32_t code = a.force == 1u ? 1u : a.force == 2u ? 2u : 0u;
+  uint32_t code = a.force == 1u ? 1u : a.force == 2u ? 2u : a.force == 4u ? 3u : 0u;
   if (a.force == 3u) {
     const uint32_t f = t % a.waves_per_frame, wg = f / a.wl, w = f % a.wl;
     const uint32_t tx = (wg % a.grid_x) * a.wx + w % a.wx, ty = (wg / a.grid_x) * a.wy + w / a.wx;
@@ -1888,13 +1915,14 @@ __device__ __forceinline__ uint32_t plan_pack(uint32_t w, uint32_t p) {
 
 // A tile's current cost: its last whole wave's time, or — when parts of a split ran since (the whole time is then
 // older than them) — the whole estimated from its costliest part (the inverse of the part estimates in
-// plan_pick32: 0.55 / 0.35 of the whole). So a split tile whose view became cheap is seen cheap, is traced whole
-// again and measures a fresh whole time; a stale whole time never keeps it split.
+// plan_pick32: 0.55 / 0.35 / 0.21 of the whole). So a split tile whose view became cheap is seen cheap, is traced
+// whole again and measures a fresh whole time; a stale whole time never keeps it split.
+// x 20 / 11, 20 / 7 and 1 / 0.21 in 10-bit fixed point
+__device__ __forceinline__ uint32_t plan_inv_part(uint32_t code) { return code == 1u ? 1862u : code == 2u ? 2926u : 4876u; }
 __device__ __forceinline__ uint32_t plan_cur(uint32_t c) {
   const uint32_t w = c & 0xffffu, p15 = (c >> 16) & 0x7fffu;
   if (!(c >> 31) || !p15) return w;
-  // x 20 / 11 and x 20 / 7 in 10-bit fixed point
-  const uint32_t pt = (p15 >> 2) << 3, e = (pt * ((p15 & 3u) == 1u ? 1862u : 2926u)) >> 10;
+  const uint32_t pt = (p15 >> 2) << 3, e = (pt * plan_inv_part(p15 & 3u)) >> 10;
   return e < 0xffffu ? e : 0xffffu;
 }
 
@@ -1902,7 +1930,8 @@ __device__ __forceinline__ uint32_t plan_cur(uint32_t c) {
 // selected constant, crashes this compiler's instruction selection: ROCm 7.2 clang 22, AMDGPU DAG->DAG)
 __device__ __forceinline__ uint32_t plan_cur_raw(uint32_t w16, uint32_t p, bool since) {
   const uint32_t q = (p >> 5) < 0x1fffu ? (p >> 5) : 0x1fffu;  // the part in 80-ns units, as plan_pack keeps it
-  const uint32_t e = (p & 3u) == 1u ? ((q << 3) * 1862u) >> 10 : ((q << 3) * 2926u) >> 10;
+  const uint32_t e = (p & 3u) == 1u ? ((q << 3) * 1862u) >> 10
+                                    : (p & 3u) == 2u ? ((q << 3) * 2926u) >> 10 : ((q << 3) * 4876u) >> 10;
   return since && p ? (e < 0xffffu ? e : 0xffffu) : w16;
 }
 
@@ -1912,11 +1941,16 @@ __device__ __forceinline__ uint32_t plan_pick32(const PlanArgs& a, bool split, u
   const uint32_t w = c & 0xffffu, p15 = (c >> 16) & 0x7fffu, pt = (p15 >> 2) << 3;  // the part's time in ticks
   const uint32_t cur = plan_cur(c);
   uint32_t code = 0;
-  if (split && a.kmax_code && cur > T) code = (a.kmax_code == 1u || cur * 11u <= T * 20u) ? 1u : 2u;
+  // 4 parts when 0.55 x the tile fits T, else 16 when 0.35 x fits (or 4 x 4 is the finest the tile allows), else 64
+  // single-pixel parts (the worst C4 tiles' costliest pixel walks 0.2 of the whole packet's fetches,
+  // tools/path_study.py)
+  if (split && a.kmax_code && cur > T)
+    code = (a.kmax_code == 1u || cur * 11u <= T * 20u) ? 1u : (a.kmax_code == 2u || cur * 7u <= T * 20u) ? 2u : 3u;
   // the last split of this tile measured a part above 0.8 x its whole wave: splitting does not pay there
   if (code && p15 && pt * 5u > w * 4u) code = 0u;
   *est = code == 0u ? cur
-                    : (p15 && (p15 & 3u) == code) ? pt : (code == 1u ? (cur * 11u) / 20u : (cur * 7u) / 20u);
+                    : (p15 && (p15 & 3u) == code) ? pt
+                    : (code == 1u ? (cur * 11u) / 20u : code == 2u ? (cur * 7u) / 20u : (cur * 215u) >> 10);
   return code;
 }
 
@@ -1959,7 +1993,9 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
   }
   const uint64_t t_loaded = __builtin_amdgcn_s_memrealtime();
   if (tail) {
-    const uint32_t F = (mx * 7u) / 20u;
+    // the floor a split can reach: the costliest part of the finest split allowed (0.35 of the tile at 16 parts,
+    // 0.21 at 64)
+    const uint32_t F = a.kmax_code >= 3u ? (mx * 215u) >> 10 : (mx * 7u) / 20u;
     T = L > F ? L : F;
     // 2. the parts must fit the grid's budget: raise T until they do (the first count is the demand, reported)
     for (int iter = 0; split && iter < 24; ++iter) {
@@ -1979,7 +2015,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
   if (!a.force && !tail) {
     // no tail: the plain grid's order, every tile whole
 #pragma unroll 4
-    for (uint32_t t = tid; t < n; t += kPlanThreads) a.plan[1u + t] = t << 6;
+    for (uint32_t t = tid; t < n; t += kPlanThreads) a.plan[1u + t] = t << 8;
   } else {
     // 3. each tile's layout and class (estimated above front / 16 x L: first); thread i's run of tiles
     // [m i, m i + m) counts its items, one block scan of the runs' (front, rest) counts places them, and each
@@ -1998,6 +2034,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
     }
     uint64_t tot;
     const uint64_t ex = block_excl_scan64(((uint64_t)cf << 32) | cb, s_red, &tot);
+    const uint32_t nfront_items = (uint32_t)(tot >> 32);  // the front class occupies the list's first positions
     uint32_t pf = (uint32_t)(ex >> 32), pb = (uint32_t)(tot >> 32) + (uint32_t)ex;
 #pragma unroll 4
     for (uint32_t t = t0; t < t1; ++t) {
@@ -2016,7 +2053,8 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
     for (uint32_t t = tid; t < n; t += kPlanThreads) {
       const uint32_t d = s_c[plan_lds_ix(t)], code = d & 3u, k = split_parts(code), pos = d >> 2;
       for (uint32_t q = 0; q < k; ++q) {
-        if (pos + q < cap) a.plan[1u + pos + q] = (t << 6) | (q << 2) | code;
+        if (pos + q < cap)
+          a.plan[1u + pos + q] = (t << 8) | (q << 2) | code | ((a.prio && pos + q < nfront_items) ? 0x80000000u : 0u);
         else ++lref;
       }
       // a split tile's part word restarts (its parts raise it with atomicMax at their end)
@@ -2035,34 +2073,36 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
   refused = (uint32_t)block_sum64(lref, s_red);
   if (refused) {
     // a list missing any part would leave pixels unwritten: the plain grid's list instead (every tile whole)
-    for (uint32_t t = tid; t < n; t += kPlanThreads) a.plan[1u + t] = t << 6;
+    for (uint32_t t = tid; t < n; t += kPlanThreads) a.plan[1u + t] = t << 8;
     nitems = n;
     nsplit = 0;
     pays = false;
   }
   const uint64_t t_placed = __builtin_amdgcn_s_memrealtime();
   // diagnostics (PlanArgs::check): the list must cover every tile exactly once — each tile's items one layout, its
-  // parts 0 .. k - 1 once each (the words after the items count them)
+  // parts 0 .. k - 1 once each (the words after the items count them: the layouts seen, parts 0 .. 31, parts 32 .. 63)
   uint32_t bad = 0, first_bad = 0xffffffffu, first_word = 0;
   if (a.check) {
     uint32_t* sw = a.plan + 1u + cap;
     uint32_t* sp = sw + n;
+    uint32_t* sq = sp + n;
     __syncthreads();  // every item is written
-    for (uint32_t t = tid; t < n; t += kPlanThreads) sw[t] = sp[t] = 0u;
+    for (uint32_t t = tid; t < n; t += kPlanThreads) sw[t] = sp[t] = sq[t] = 0u;
     __syncthreads();
     for (uint32_t i = tid; i < nitems; i += kPlanThreads) {
-      const uint32_t it = a.plan[1u + i], slot = it >> 6, q = (it >> 2) & 15u, code = it & 3u;
-      if (slot >= n || code > 2u || q >= split_parts(code)) {
+      const uint32_t it = a.plan[1u + i], slot = (it >> 8) & kPlanSlotMask, q = (it >> 2) & 63u, code = it & 3u;
+      if (slot >= n || q >= split_parts(code)) {
         bad += 1u;
         continue;
       }
-      atomicAdd(&sp[slot], 1u << q);
+      atomicAdd(q < 32u ? &sp[slot] : &sq[slot], 1u << (q & 31u));
       atomicOr(&sw[slot], 1u << code);
     }
     __syncthreads();
     for (uint32_t t = tid; t < n; t += kPlanThreads) {
-      const uint32_t m = sw[t], c = sp[t];
-      const bool ok = (m == 1u && c == 1u) || (m == 2u && c == 0xfu) || (m == 4u && c == 0xffffu);
+      const uint32_t m = sw[t], c = sp[t], c2 = sq[t];
+      const bool ok = (m == 1u && c == 1u && c2 == 0u) || (m == 2u && c == 0xfu && c2 == 0u) ||
+                      (m == 4u && c == 0xffffu && c2 == 0u) || (m == 8u && c == 0xffffffffu && c2 == 0xffffffffu);
       if (!ok) {
         bad += 1u;
         if (t < first_bad) {
@@ -2111,26 +2151,29 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
 
 namespace {
 template <int MODE, int KS>
-const void* bal_kernel() {
+const void* bal_kernel(bool mf) {
   constexpr int R = RT_PACKET_RAYS;
-  return reinterpret_cast<const void*>(&k_trace_frame_packet<MODE, false, R, (R == 1 ? KS : 0), true>);
+  return mf ? reinterpret_cast<const void*>(&k_trace_frame_packet<MODE, false, R, (R == 1 ? KS : 0), true, true>)
+            : reinterpret_cast<const void*>(&k_trace_frame_packet<MODE, false, R, (R == 1 ? KS : 0), true, false>);
 }
 template <int MODE>
-const void* bal_kernel_ks(int ks) {
-  return ks == 1 ? bal_kernel<MODE, 1>() : ks == 2 ? bal_kernel<MODE, 2>() : ks == 4 ? bal_kernel<MODE, 4>()
-                                                                               : bal_kernel<MODE, 0>();
+const void* bal_kernel_ks(int ks, bool mf) {
+  return ks == 1 ? bal_kernel<MODE, 1>(mf) : ks == 2 ? bal_kernel<MODE, 2>(mf) : ks == 4 ? bal_kernel<MODE, 4>(mf)
+                                                                                       : bal_kernel<MODE, 0>(mf);
 }
 }  // namespace
 
 uint32_t trace_wave_slots(const SceneView& sc, const FrameParams& fp, int schedule, int device) {
   const PacketGeometry g = packet_geometry(sc, fp, schedule);
   if (!g.packet) return 0;
+  const bool mf = launch_multi_frame(fp);
   const void* k = nullptr;
   switch (fp.shade_mode) {  // the instantiation launch_trace_frame picks (non-STATS, BAL)
-    case 0: k = (fp.material.reflectivity == 0.0f && RT_REF_NOREFL) ? bal_kernel_ks<3>(g.ks) : bal_kernel_ks<0>(g.ks);
+    case 0: k = (fp.material.reflectivity == 0.0f && RT_REF_NOREFL) ? bal_kernel_ks<3>(g.ks, mf)
+                                                                    : bal_kernel_ks<0>(g.ks, mf);
             break;
-    case 1: k = bal_kernel_ks<1>(g.ks); break;
-    case 2: k = bal_kernel_ks<2>(g.ks); break;
+    case 1: k = bal_kernel_ks<1>(g.ks, mf); break;
+    case 2: k = bal_kernel_ks<2>(g.ks, mf); break;
     default: return 0;
   }
   static std::mutex mu;

@@ -52,7 +52,7 @@ def render(c, spec, stream=None, rows=None):
 CASES = [("C4", (256, 136)), ("C2F", (200, 101)), ("REF", (96, 54)), ("C1", (64, 64)), ("C5", (48, 27))]
 
 
-@pytest.mark.parametrize("mode", [2, 3, 4])
+@pytest.mark.parametrize("mode", [2, 3, 4, 5])
 @pytest.mark.parametrize("name,size", CASES)
 def test_forced_layouts_equal_oracle_with_counters(name, size, mode):
     spec = scenes.config(name).with_size(*size)

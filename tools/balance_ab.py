@@ -5,7 +5,8 @@ one stream back to back (the frame latency) and with 3 frames in flight, interle
 frame is checked equal to the first's. --variants names the arms: b0 (off), b1 (adaptive, the defaults), and b1 with
 the plan's diagnostics (RT_BALANCE_SPLIT / RT_BALANCE_FRONT, read at context creation): b1s0 (no split, order
 only), b1f0 (tile order, split only), b1f<k> (front class above k / 16 x the load bound), b1q<d> (extra waves for
-split tiles: ntiles / d).
+split tiles: ntiles / d, default 8 as shipped), ...p0 (the front class's waves keep the default issue priority:
+RT_BALANCE_PRIO=0), ...n0 (adaptive plans split into at most 16 parts, not 64: RT_BALANCE_FINE=0).
   python3 tools/balance_ab.py --configs C4,C2F,C2 --shares 1,4,8 --rounds 5 --variants b0,b1,b1s0"""
 import argparse
 import json
@@ -54,8 +55,10 @@ def main():
         ctxs = {}
         for v in variants:
             env = {"RT_BALANCE_SPLIT": "0" if "s0" in v else "1",
-                   "RT_BALANCE_FRONT": v.split("f")[1].split("q")[0] if "f" in v else "8",
-                   "RT_BALANCE_BUDGET": v.split("q")[1] if "q" in v else "4"}
+                   "RT_BALANCE_FRONT": v.split("f")[1].split("q")[0].split("p")[0].split("n")[0] if "f" in v else "8",
+                   "RT_BALANCE_BUDGET": v.split("q")[1].split("p")[0].split("n")[0] if "q" in v else "8",
+                   "RT_BALANCE_PRIO": "0" if "p0" in v else "1",
+                   "RT_BALANCE_FINE": "0" if "n0" in v else "1"}
             os.environ.update(env)
             ctxs[v] = rt.Context(0)
             scenes.upload(ctxs[v], spec)

@@ -32,6 +32,14 @@ for step in ${STEPS:-tests}; do
       timeout -k 10 900 python3 -u tools/share_ceiling.py ${SHARE_ARGS:-} > "$O/shares_${TAG}.jsonl" 2> "$O/shares_${TAG}.err" \
         || { echo "share_ceiling failed rc=$?"; tail -20 "$O/shares_${TAG}.err"; exit 1; }
       cat "$O/shares_${TAG}.jsonl" ;;
+    libab)
+      timeout -k 10 900 python3 tools/lib_ab.py --roots ${AB_ROOTS:-ab/r03,.,.:bal0} --configs ${AB_CONFIGS:-C2,C2F,C4} \
+        --rounds ${AB_ROUNDS:-5} > "$O/libab_${TAG}.txt" 2>&1 || { echo "lib_ab failed rc=$?"; tail -20 "$O/libab_${TAG}.txt"; exit 1; }
+      tail -40 "$O/libab_${TAG}.txt" ;;
+    occ)
+      timeout -k 10 120 ./tools/bin/occupancy_probe > "$O/occupancy_${TAG}.jsonl" 2>&1 \
+        || { echo "occupancy_probe failed rc=$?"; tail -20 "$O/occupancy_${TAG}.jsonl"; exit 1; }
+      cat "$O/occupancy_${TAG}.jsonl" ;;
     balance)
       timeout -k 10 600 python3 tools/balance_ab.py ${BAL_ARGS:-} > "$O/balance_${TAG}.txt" 2>&1 \
         || { echo "balance_ab failed rc=$?"; tail -20 "$O/balance_${TAG}.txt"; exit 1; }
