@@ -1314,7 +1314,9 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
       if (forced) {
         // tests: a fresh list per launch from the ring (RT_BALANCE_FORCED_CAP, tests: a smaller budget of extra waves,
         // so the plan must refuse parts and fall back to the plain grid's list)
-        a.extra_cap = c->bal_forced_cap ? c->bal_forced_cap : 63u * ntiles;
+        // the layout's own parts (modes 2 / 3 / 4 / 5: at most 4 / 16 / 16 / 64 per tile)
+      const uint32_t most = c->balance == 2 ? 4u : c->balance == 5 ? 64u : 16u;
+      a.extra_cap = c->bal_forced_cap ? c->bal_forced_cap : (most - 1u) * ntiles;
         a.stats = m->stats_dev;
         a.slots = plan_slots(c, sv);
         plan_items = ntiles + a.extra_cap;

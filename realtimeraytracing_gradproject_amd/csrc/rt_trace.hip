@@ -17,6 +17,7 @@
 // [entry][lane] (bank = lane: conflict free) with an HBM overflow for deep paths.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <mutex>
 #include <utility>
 #include <vector>
@@ -1485,11 +1486,22 @@ static_assert(packet_block(1) <= 64 * kMaxPacketWaves && packet_block(2) <= 64 *
 // MF: several frames per launch (grid z / the item's frame: a camera per frame) or RGB8 strips (rt_render_strips);
 // false for one RGBA8 frame (rt_dispatch_rays, the bench's frames loop): camera 0 at its fixed kernel-argument
 // offset and the plain store, without the per-frame address arithmetic and its dependent argument loads
+#ifndef RT_PACKET_HW_WAVES
+#define RT_PACKET_HW_WAVES (RT_PACKET_SGPRS && RT_PACKET_SGPRS <= 80 ? 8 : 7)  // resident waves per SIMD (SGPRs)
+#endif
+#ifndef RT_PACKET_SGPRS
+#define RT_PACKET_SGPRS 0  // > 0: cap the packet kernels' SGPRs (amdgpu_num_sgpr), A/B of the hardware residency
+#endif
+#if RT_PACKET_SGPRS
+#define RT_PACKET_SGPR_ATTR __attribute__((amdgpu_num_sgpr(RT_PACKET_SGPRS)))
+#else
+#define RT_PACKET_SGPR_ATTR
+#endif
 template <int MODE, bool STATS, int R, int KS, bool BAL, bool MF>
 __global__ __launch_bounds__(packet_block(KS)) __attribute__((amdgpu_waves_per_eu(
     (MODE == 1 && !STATS) ? (KS == 0 ? RT_SPP_WAVES : (KS == 1 ? RT_LS_WAVES : RT_KS_WAVES))
     : (MODE == 3 && !STATS) ? (KS == 0 ? RT_SPP_WAVES : (KS == 1 ? RT_REF0_WAVES : RT_KS_WAVES))
-                            : ((MODE == 0 && !STATS && KS == 1) ? RT_REF_WAVES : 1))))
+                            : ((MODE == 0 && !STATS && KS == 1) ? RT_REF_WAVES : 1)))) RT_PACKET_SGPR_ATTR
 void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restrict__ rows,
                           uint32_t* __restrict__ rgba8, float4* __restrict__ rgba32f,
                           unsigned long long* __restrict__ stats) {
@@ -2186,7 +2198,14 @@ uint32_t trace_wave_slots(const SceneView& sc, const FrameParams& fp, int schedu
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, block, 0) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || nb <= 0 || cus <= 0)
     return 0;
-  const uint32_t slots = (uint32_t)nb * (uint32_t)(block / 64) * (uint32_t)cus;
+  // waves per SIMD: the runtime's figure counts VGPRs and workgroup slots but not the hardware's SGPR budget, which
+  // holds these kernels (88 SGPRs) to 7 waves per SIMD where the runtime and the compiler report 8: the wave-time
+  // trace finds every one of the 1,024 SIMDs at 7 resident waves, HW wave slots 0..6 (profiles/r05_wave_times_C4.txt),
+  // and the register probe puts the limit at 72 SGPRs for 8 waves (tools/occupancy_probe.hip,
+  // profiles/r05_occupancy_probe.jsonl). A build capped at 80 SGPRs (72 used) does reach 8 waves but spills 20 SGPRs
+  // and is not faster
+  const uint32_t per_simd = std::min<uint32_t>((uint32_t)nb * (uint32_t)(block / 64) / 4u, RT_PACKET_HW_WAVES);
+  const uint32_t slots = per_simd * 4u * (uint32_t)cus;
   cache.push_back({{k, device}, slots});
   return slots;
 }

@@ -186,7 +186,7 @@ def test_adaptive_balance_multi_frame_launch_and_off():
             assert np.array_equal(frames[rep][q].cpu().numpy(), o8), f"launch {rep} frame {q}"
         assert np.array_equal(off[q].cpu().numpy(), o8), f"plain grid frame {q}"
     with pytest.raises(rt.RtError):
-        c.set_tile_balance(5)
+        c.set_tile_balance(6)
     c.close()
 
 
@@ -248,4 +248,38 @@ def test_split_tiles_rejoin_when_the_view_becomes_cheap():
         assert np.array_equal(outs[k].cpu().numpy(), o8), f"costly frame {k}"
     for k in (0, 1, len(outs_sky) - 1):
         assert np.array_equal(outs_sky[k].cpu().numpy(), s8), f"sky frame {k}"
+    c.close()
+
+
+def test_load_bound_slots_match_the_hardware_residency():
+    """the plan's load bound divides by the GPU's wave slots for the list's kernel. The `wavetimes`
+    variant stamps every wave's start / end clock and HW_ID: a sweep over those events gives the waves resident at
+    once, and it must equal rt_tile_balance_info's slots (7 waves per SIMD for these 88-SGPR kernels, not the 8 that
+    hipOccupancyMaxActiveBlocksPerMultiprocessor reports). A forced layout (every tile in 4 parts,
+    129,600 waves at 1080p) fills the machine many times over."""
+    import os as _os
+    path = _os.path.join(_os.path.dirname(rt.LIB_PATH), "variants", "wavetimes", "librtamd.so")
+    c = rt.Context(0, library=rt._load(path))
+    spec = scenes.config("C2")
+    scenes.upload(c, spec)
+    c.set_tile_balance(2)
+    W, H = spec.width, spec.height
+    out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+    rec = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(3):
+        c.dispatch(W, H, out, rec, stream=s)
+    rec.zero_()
+    c.dispatch(W, H, out, rec, stream=s)
+    torch.cuda.synchronize()
+    slots = c.tile_balance_info()["slots"]
+    u = rec.view(torch.int32).cpu().numpy().astype(np.uint32).reshape(-1, 4)
+    u = u[u[:, 1] != 0]
+    assert len(u) == 4 * (W // 8) * (H // 8), len(u)  # every part's wave left its record
+    t0, t1 = u[:, 0].astype(np.int64), u[:, 1].astype(np.int64)
+    ev_t = np.concatenate([t0, t1])
+    ev_d = np.concatenate([np.ones_like(t0), -np.ones_like(t1)])
+    order = np.lexsort((ev_d, ev_t))
+    peak = int(np.cumsum(ev_d[order]).max())
+    assert peak == slots, (peak, slots)
     c.close()

@@ -36,6 +36,8 @@ for step in ${STEPS:-tests}; do
       timeout -k 10 900 python3 tools/lib_ab.py --roots ${AB_ROOTS:-ab/r03,.,.:bal0} --configs ${AB_CONFIGS:-C2,C2F,C4} \
         --rounds ${AB_ROUNDS:-5} > "$O/libab_${TAG}.txt" 2>&1 || { echo "lib_ab failed rc=$?"; tail -20 "$O/libab_${TAG}.txt"; exit 1; }
       tail -40 "$O/libab_${TAG}.txt" ;;
+    prof)
+      CFGS="${PROF_CFGS:-C2 C4 C5}" TAG="$TAG" bash tools/profile_round.sh || { echo "profile_round failed"; exit 1; } ;;
     occ)
       timeout -k 10 120 ./tools/bin/occupancy_probe > "$O/occupancy_${TAG}.jsonl" 2>&1 \
         || { echo "occupancy_probe failed rc=$?"; tail -20 "$O/occupancy_${TAG}.jsonl"; exit 1; }
@@ -45,8 +47,8 @@ for step in ${STEPS:-tests}; do
         || { echo "balance_ab failed rc=$?"; tail -20 "$O/balance_${TAG}.txt"; exit 1; }
       cat "$O/balance_${TAG}.txt" ;;
     waves)
-      for b in 0 1; do
-        timeout -k 10 120 python3 tools/wave_times.py --lib realtimeraytracing_gradproject_amd/lib/variants/wavetimes/librtamd.so \
+      for b in ${WT_BAL:-0 1}; do
+        timeout -k 10 120 python3 tools/wave_times.py --lib ${WT_LIB:-realtimeraytracing_gradproject_amd/lib/variants/wavetimes/librtamd.so} \
           --config ${WT_CONFIG:-C4} --balance $b ${WT_ARGS:-} > "$O/wave_times_${TAG}_b$b.txt" 2>&1 \
           || { echo "wave_times failed rc=$?"; tail -20 "$O/wave_times_${TAG}_b$b.txt"; exit 1; }
         cat "$O/wave_times_${TAG}_b$b.txt"
