@@ -38,6 +38,14 @@ for step in ${STEPS:-tests}; do
       tail -40 "$O/libab_${TAG}.txt" ;;
     prof)
       CFGS="${PROF_CFGS:-C2 C4 C5}" TAG="$TAG" bash tools/profile_round.sh || { echo "profile_round failed"; exit 1; } ;;
+    sqc)
+      # scalar data cache hit rate of the trace kernel (one pass; counters of the SQC block only)
+      cd /tmp && export TMPDIR=/tmp
+      timeout -s KILL 90 rocprofv3 --pmc ${SQC_SET:-SQC_DCACHE_REQ SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_DCACHE_MISSES_DUPLICATE} \
+        --kernel-include-regex k_trace_frame -d "$O/sqc_${TAG}" -o run --output-format csv \
+        -- python3 "$R/tools/one_config.py" --config ${SQC_CONFIG:-C2} --frames 12 > "$O/sqc_${TAG}.log" 2>&1 \
+        || { echo "sqc pass failed rc=$?"; tail -20 "$O/sqc_${TAG}.log"; exit 1; }
+      cd "$R"; find "$O/sqc_${TAG}" -name "*counter_collection.csv" | head -1 | xargs -r tail -5 ;;
     occ)
       timeout -k 10 120 ./tools/bin/occupancy_probe > "$O/occupancy_${TAG}.jsonl" 2>&1 \
         || { echo "occupancy_probe failed rc=$?"; tail -20 "$O/occupancy_${TAG}.jsonl"; exit 1; }
