@@ -114,3 +114,42 @@ def test_random_scene_tiled_loop_equals_oracle(seed, nranks):
         comm.close()
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("seed", list(range(3000, 3006)))
+def test_random_scene_trace_rays_equal_oracle(seed):
+    """rt_trace_rays (the TraceRay entry point with D3D12 ray flags) on random scenes: 20,000 rays aimed at the
+    scene from random origins, random tmin / tmax, closest hit, any hit, back- and front-face culling: hit records
+    and barycentrics == the oracle's BVH walk, the closest hits == brute force on a subset."""
+    spec = random_scene(seed)
+    rng = np.random.default_rng(seed)
+    n = 20000
+    o_ = rng.normal(size=(n, 3))
+    o_ = o_ / np.linalg.norm(o_, axis=1, keepdims=True) * rng.uniform(2, 25, size=(n, 1))
+    d = rng.uniform(-4, 4, size=(n, 3)) - o_
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.zeros((n, 8), np.float32)
+    rays[:, :3], rays[:, 4:7] = o_, d
+    rays[:, 3] = rng.choice([0.0, 0.01, 1.0], size=n)
+    rays[:, 7] = rng.choice([1e5, 12.0, 3.0], size=n)
+    c = rt.Context(0)
+    try:
+        scenes.upload(c, spec)
+        o = oracle.Scene(spec)
+        d_rays = torch.from_numpy(rays).cuda()
+        for any_hit, cull_back, cull_front in [(False, False, False), (True, False, False), (False, True, False),
+                                               (False, False, True)]:
+            d_hits = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+            d_uv = torch.zeros((n, 2), dtype=torch.float32, device="cuda")
+            c.trace_rays(d_rays, n, any_hit, d_hits, d_uv, cull_back=cull_back, cull_front=cull_front)
+            torch.cuda.synchronize()
+            g = d_hits.cpu().numpy().view(np.uint32)
+            ob, ouv, _ = o.trace_rays(rays, any_hit=any_hit, cull_back=cull_back, cull_front=cull_front)
+            what = f"seed {seed} any_hit={any_hit} cull_back={cull_back} cull_front={cull_front}"
+            assert np.array_equal(g, ob), what
+            if not any_hit:
+                assert np.array_equal(d_uv.cpu().numpy(), ouv), what
+                bb, _, _ = o.trace_rays(rays[:2000], brute_force=True, cull_back=cull_back, cull_front=cull_front)
+                assert np.array_equal(g[:2000], bb), what + ": brute force"
+    finally:
+        c.close()
