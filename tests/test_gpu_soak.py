@@ -1,0 +1,91 @@
+"""Soak: long runs of the adaptive tile balance with the camera moving every frame (the async plan / list swap, the
+cost maps written and read by launches on several streams, split tiles rejoining as the view changes),
+alternating segments of one-at-a-time frames (the balance active: feedback, plans, lists) and frames in flight over
+three streams (the balance off, then taken up again). Every frame gets its own camera; a sample of frames spread over
+the run is compared with the oracle bit for bit, and the plan kernel's own cover check (RT_BALANCE_CHECK) must never
+have failed."""
+import math
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import realtimeraytracing_gradproject_amd as rt  # noqa: E402
+from realtimeraytracing_gradproject_amd import scenes  # noqa: E402
+
+import oracle  # noqa: E402
+
+
+def orbit(spec, k, n):
+    """Frame k of n on a circle around the scene's target, the height swinging (views from grazing to steep)."""
+    (ex, ey, ez), tgt, up = spec.camera
+    r = math.hypot(ex - tgt[0], ez - tgt[2])
+    a = math.atan2(ez - tgt[2], ex - tgt[0]) + 2.0 * math.pi * k / n
+    h = ey * (0.55 + 0.45 * math.cos(5.0 * math.pi * k / n))
+    sp = spec.with_size(spec.width, spec.height)
+    sp.camera = ((tgt[0] + r * math.cos(a), h, tgt[2] + r * math.sin(a)), tgt, up)
+    return sp
+
+
+@pytest.mark.parametrize("name,size", [("C2F", (640, 360)), ("C4", (640, 360))])
+def test_balance_soak_moving_camera(name, size):
+    base = scenes.config(name).with_size(*size)
+    os.environ["RT_BALANCE_CHECK"] = "1"
+    try:
+        c = rt.Context(0)
+    finally:
+        del os.environ["RT_BALANCE_CHECK"]
+    scenes.upload(c, base)
+    W, H = size
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    n = 360
+    outs, specs = [], []
+    for k in range(n):
+        seg = (k // 60) % 2  # 0: one stream (balance active), 1: three streams in flight
+        sp = orbit(base, k, n)
+        c.set_camera(sp.camera_buffer())
+        out = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
+        c.dispatch(W, H, out, stream=streams[0 if seg == 0 else k % 3].cuda_stream)
+        outs.append(out)
+        specs.append(sp)
+    torch.cuda.synchronize()
+    info = c.tile_balance_info()
+    assert info["check_bad"] == 0 and info["refused"] == 0, info
+    assert info["plans"] >= 3, info  # re-planned along the run (the plan runs every few active launches)
+    o = oracle.Scene(base)
+    for k in range(0, n, 15):
+        want, _, _ = o.render_spec(specs[k], nthreads=16, want_float=False)
+        got = outs[k].cpu().numpy()
+        bad = int((got != want).any(axis=2).sum())
+        assert bad == 0, f"{name} frame {k}: {bad} pixels differ ({info})"
+    c.close()
+
+
+def test_loopback_loop_soak_moving_camera():
+    """The tiled multi-GPU loop (loopback, N = 4, 4 frames per gather and per launch) over 160 frames with a camera
+    each: sampled frames equal the oracle's."""
+    base = scenes.config("C4").with_size(480, 270)
+    c = rt.Context(0)
+    scenes.upload(c, base)
+    comm = rt.Comm.loopback(c, 4)
+    comm.set_batch(4)
+    W, H = base.width, base.height
+    n = 160
+    frames, specs = [], []
+    for k0 in range(0, n, 4):
+        sps = [orbit(base, k, n) for k in range(k0, k0 + 4)]
+        fs = [torch.empty((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(4)]
+        comm.render_strips_frames(W, H, fs, cameras=np.concatenate([sp.camera_buffer().ravel() for sp in sps]))
+        frames += fs
+        specs += sps
+    comm.synchronize()
+    comm.close()
+    o = oracle.Scene(base)
+    for k in range(0, n, 13):
+        want, _, _ = o.render_spec(specs[k], nthreads=16, want_float=False)
+        bad = int((frames[k].cpu().numpy() != want).any(axis=2).sum())
+        assert bad == 0, f"frame {k}: {bad} pixels differ"
+    c.close()
