@@ -969,7 +969,9 @@ static int otrace(const oracle_scene* s, vec3 o, vec3 d, float tmin, float tmax,
 /* together; a child is entered when any live lane's slab test accepts it. Emulated lane by   */
 /* lane so the traversal order and the per-lane counters are those of the device.            */
 /* ---------------------------------------------------------------------------------------- */
-#define OPK 64
+#ifndef OPK
+#define OPK 64 /* lanes of an emulated packet (design studies may build 128: two rays per lane) */
+#endif
 #define OSTACK 4096 /* emulated per-child stack: its bound is at most 3 entries per tree level */
 
 typedef struct {
