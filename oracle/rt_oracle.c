@@ -991,7 +991,8 @@ static int olead(const int* live) {
 static int opk_node(const o4node* nd, const opkray* ry, float tmin, ohit* h, int* live, int* lead,
                     const otri* leaves, uint32_t cur, float face, int any, int* found, int* stack, int* sp,
                     int cap, int* next, ostats* st) {
-  uint64_t hm[4] = {0, 0, 0, 0};
+  uint64_t hm[4] = {0, 0, 0, 0}; /* ballots (OPK <= 64; wider study builds use acc below) */
+  uint8_t acc[OPK][4];           /* lane l's own slab test accepts child k (live lanes only) */
   uint32_t vkey[OPK][4];
   OST(9, 1); /* one node fetch per wave */
 #ifdef OSTUDY_NODE_HOOK /* design studies only (tools/path_study.c): node fetches by tree level and ray kind */
@@ -1005,7 +1006,8 @@ static int opk_node(const o4node* nd, const opkray* ry, float tmin, ohit* h, int
       float n = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), tmin));
       float f = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), h[l].t));
       int hit = n <= f * 1.0000004f; /* empty slots hold +inf boxes: never accepted */
-      if (hit && live[l]) hm[k] |= 1ull << l;
+      acc[l][k] = (uint8_t)(hit && live[l]);
+      if (hit && live[l] && l < 64) hm[k] |= 1ull << l;
 #ifdef OCLOSEST_KEY /* design studies only (tools/key_study.c): another nearest-first key */
       vkey[l][k] = hit ? OCLOSEST_KEY(n, f) : 0x7f800000u;
 #else
@@ -1015,7 +1017,8 @@ static int opk_node(const o4node* nd, const opkray* ry, float tmin, ohit* h, int
     if (live[l]) OST(2, nd->count);
   }
   uint32_t ent = 0;
-  for (int k = 0; k < 4; ++k) if (hm[k]) ent |= 1u << k;
+  for (int l = 0; l < OPK; ++l)
+    for (int k = 0; k < 4; ++k) if (acc[l][k]) ent |= 1u << k;
   if (!ent) return 0;
   if (leaves) {
     uint32_t leafbits = 0;
@@ -1030,7 +1033,9 @@ static int opk_node(const o4node* nd, const opkray* ry, float tmin, ohit* h, int
         if (!live[l]) continue;
         float t, u, v;
         OST(3, 1);
-        if (omt(ry->o[l], ry->d[l], tr, face, &t, &u, &v) && t >= tmin && better(t, cur, tr->prim, &h[l])) {
+        /* only a lane whose own slab test accepted the triangle's slot may take the hit (packet_tri's own mask) */
+        if (acc[l][k] && omt(ry->o[l], ry->d[l], tr, face, &t, &u, &v) && t >= tmin &&
+            better(t, cur, tr->prim, &h[l])) {
           h[l].t = t; h[l].u = u; h[l].v = v; h[l].inst = cur; h[l].prim = tr->prim;
           found[l] = 1;
           if (any) live[l] = 0;
@@ -1040,9 +1045,11 @@ static int opk_node(const o4node* nd, const opkray* ry, float tmin, ohit* h, int
     if (any) {
       *lead = olead(live);
       if (*lead < 0) return 2;
-      uint64_t lm = 0;
-      for (int l = 0; l < OPK; ++l) if (live[l]) lm |= 1ull << l;
-      for (int k = 0; k < 4; ++k) if (!(hm[k] & lm)) ent &= ~(1u << k);
+      for (int k = 0; k < 4; ++k) {
+        int keep = 0;
+        for (int l = 0; l < OPK; ++l) keep |= acc[l][k] && live[l];
+        if (!keep) ent &= ~(1u << k);
+      }
     }
     if (!ent) return 0;
   }

@@ -259,7 +259,8 @@ __device__ bool trace(const SceneView& sc, V3 o, V3 d, float tmin, float tmax, H
 // the packet's 64 x R rays: R > 1 spends more VALU per node to amortise the SALU further.
 // Results are those of the per-ray traversal: the closest hit is the lexicographic minimum of
 // (t, instance, primitive) over every triangle a ray reaches, and every triangle whose root
-// path the ray's slab tests accept is visited, whatever the order.
+// path the ray's slab tests accept is visited, whatever the order; a ray dragged into a leaf by
+// other lanes takes no hit there unless its own test accepted the triangle's box (packet_tri).
 // ------------------------------------------------------------------------------------------
 #define RT_CONST __attribute__((address_space(4)))
 
@@ -382,10 +383,16 @@ struct PacketRay {
 
 // Triangle leaf for every live ray (uniform triangle, scalar loads). ANY_HIT: a ray that accepts
 // a hit leaves the packet. Branch-free: selects instead of exec-mask regions.
+// own[r]: the lanes whose ray r accepted this triangle's slot box (the node's ballot for the slot). Only they may
+// take a hit: a ray the packet drags into a leaf its own slab test rejected would otherwise see Moller-Trumbore's
+// float32 false positives — a grazing ray passing just outside a triangle corner (float64 barycentrics ~-1e-4, a
+// point outside the triangle's box) — which the per-ray walk never tests. With the mask a ray's accepted set is the
+// per-ray walk's: a hit needs the triangle's own box, which implies every ancestor box (their planes enclose it and
+// the fma is monotone in the plane), so the image does not depend on the schedule. One s_and_b64 per test.
 template <bool ANY_HIT, bool STATS, int R>
 __device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref, const PacketRay<R>& ry,
                                            float tmin, uint32_t cur, float face, PacketLive<R>& pl, HitRec* hit,
-                                           Counters& cnt) {
+                                           const uint64_t* own, Counters& cnt) {
   // 32-bit byte offsets (pools are < 2 GiB): the scalar load takes them as its SGPR offset
   const RT_CONST char* tq = (const RT_CONST char*)tpool + (uint32_t)(~ref) * 48u;
   const f8v tab = *(const RT_CONST f8v*)tq;  // one s_load_dwordx8 + one x4 for the 48-B record
@@ -406,7 +413,7 @@ __device__ __forceinline__ void packet_tri(const RT_CONST TriRec* tpool, int ref
     // (instance, primitive) order as ONE unsigned 64-bit compare (v_cmp_lt_u64; the uniform side in an SGPR pair)
     const bool id_less = (((uint64_t)cur << 32) | prim) < (((uint64_t)h.inst << 32) | h.prim);
     const bool better = ANY_HIT ? (t <= h.t) : (t < h.t) | ((t == h.t) & id_less);
-    const bool take = ok & (t >= tmin) & better;
+    const bool take = ok & (t >= tmin) & better & __builtin_amdgcn_inverse_ballot_w64(own[r]);
     // an any-hit ray that accepts leaves the packet with t = -inf: every later slab test rejects it
     h.t = take ? (ANY_HIT ? -__builtin_inff() : t) : h.t;
     h.u = take ? u : h.u;
@@ -732,7 +739,12 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
       // one test per slot with the slot's ref in a fixed SGPR (no ref-select chain, no loop)
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        if (tl & (1u << k)) packet_tri<ANY_HIT, STATS, R>(tpool, ch[k], ry, tmin, cur, face, pl, hit, cnt);
+        if (tl & (1u << k)) {
+          uint64_t own[R];
+#pragma unroll
+          for (int r = 0; r < R; ++r) own[r] = hm[r][k];
+          packet_tri<ANY_HIT, STATS, R>(tpool, ch[k], ry, tmin, cur, face, pl, hit, own, cnt);
+        }
       if (ANY_HIT) {  // rays can only have left the packet in a triangle test
         if (!pl.update(hit)) return false;
         // children only finished rays wanted are dropped

@@ -828,3 +828,18 @@ def test_gpu_frames_equal_committed_goldens(name):
         assert [s[k] for k in ["primary_rays", "shadow_rays", "aabb_tests", "tri_tests"]] == \
             [int(x) for x in gold[f"{name}_{key}"][:4]]
     c.close()
+
+
+@pytest.mark.parametrize("case", [0, 1])
+def test_stress_cases_schedules_equal_per_ray(case):
+    """The stress run's two frames (tests/test_oracle.py _stress_cases: a packet lane taking a float32
+    Moller-Trumbore false positive in a box its own slab test rejected): with packet_tri's own-box mask the GPU's
+    packet and per-lane frames both equal the oracle's per-ray frame, float32 and RGBA8."""
+    from test_oracle import _stress_cases
+    name, spec, _ = _stress_cases()[case]
+    c, o = load_both(spec)
+    o8, o32, _ = o.render_spec(spec, nthreads=16, schedule=1)
+    for sched in (rt.RT_SCHED_PACKET, rt.RT_SCHED_LANE):
+        g8, g32 = gpu_render(c, spec, schedule=sched)
+        assert_images_equal(g8, g32, o8, o32, f"{name} schedule {sched}")
+    c.close()

@@ -458,3 +458,36 @@ def test_seam_watertightness_probe_fixture():
     # mt_dot) leaks 1,832 of the 66,304 edge rays; a change of that arithmetic may not leak more (regenerating the
     # fixture does not lift this bound; unfused products gave 1,727, fused dots 2,514: profiles/r03_ab_mt_fma.txt)
     assert now["leaks"] <= 1832 and fx["leaks"] <= 1832
+
+
+def _stress_cases():
+    """The two frames the round-5 stress run (tools/stress.py) found where the packet walk took a float32
+    Moller-Trumbore false positive the per-ray walk never tests: a grazing ray just outside a triangle corner
+    (float64 barycentrics about -1e-4), its own slab test rejecting the triangle's box while other lanes of its packet
+    entered it. DEGEN (a sliver across the soup's box) and C4 with its instances moved as a per-frame update."""
+    import math
+    deg = scenes.degenerate_scene().with_size(80, 44)
+    deg.camera = ((-4.14559724980539, 7.847480531308231, 21.095124369916352), (0.0, 1.0, 1.0), (0.0, 1.0, 0.0))
+    c4 = scenes.config("C4").with_size(960, 540)
+    c4.camera = ((-11.381945623573028, 13.932030315755242, 22.76952599027979), (0.0, 1.0, 0.0), (0.0, 1.0, 0.0))
+    inst = []
+    for (m, x, iid, hg) in c4.instances:
+        x = np.array(x, np.float32).copy()
+        if hg == 0:
+            x[7] += 0.25 * math.sin(0.3 * 4 + 0.7 * iid)
+        inst.append((m, x, iid, hg))
+    c4.instances = inst
+    return [("DEGEN", deg, (26, 30)), ("C4moved", c4, (374, 411))]
+
+
+@pytest.mark.parametrize("case", [0, 1])
+def test_packet_takes_only_its_own_boxes_hits(case):
+    """Each lane of a packet may only take hits of triangles whose slot box its own slab test accepted
+    (packet_tri's own mask): the packet image then equals the per-ray image on the stress cases too. The
+    pixel in question is lit in both (the per-ray walk's answer; the unmasked packet walk had it black)."""
+    name, spec, (y, x) = _stress_cases()[case]
+    o = oracle.Scene(spec)
+    a8, a32, _ = o.render_spec(spec, nthreads=8, schedule=1)
+    b8, b32, _ = o.render_spec(spec, nthreads=8, schedule=0)
+    assert np.array_equal(a8, b8) and np.array_equal(a32, b32), name
+    assert b32[y, x, 0] > 0.5, (name, b32[y, x])
