@@ -1,6 +1,8 @@
 """Seeded random scenes on the CPU oracle (tests/random_scenes.py): the packet emulation (the device's default
-schedule) renders the per-ray schedule's image bit for bit, and both equal brute force (every triangle of every
-instance tested per ray) where the scene is small enough for it. Random meshes, instance transforms (rotated,
+schedule) renders the per-ray schedule's image bit for bit (its lanes take hits only in boxes their own slab tests
+accept), and on these seeds both equal brute force (every triangle of every instance tested per ray) where
+the scene is small enough for it — brute force alone can take float32 Moller-Trumbore false positives of rays grazing
+a triangle corner outside its box, which none of these seeds has. Random meshes, instance transforms (rotated,
 non-uniformly scaled, mirrored, translate-only), hit groups, lights, materials, cameras, shading modes and 1 / 4 spp:
 the cases the fixed configs do not reach."""
 import numpy as np
