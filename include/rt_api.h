@@ -197,7 +197,9 @@ rt_status rt_set_tile_rows(rt_ctx_t ctx, int rows);
  * kernel before the launch splits the tiles above max(load bound, the finest split's floor) into 4, 16 or 64 sub-packets and
  * deals every wave longest first. The image never depends on it. 0: off (the plain grid). 2 / 3 / 4 / 5 (tests):
  * every tile in 4 parts / in 16 parts / by position (tx + 2 ty) % 3 whole, 4, 16 / in 64 one-pixel parts — also
- * under rt_set_stats, so the counters can be compared with the oracle's emulation of the same parts. */
+ * under rt_set_stats, so the counters can be compared with the oracle's emulation of the same parts. A launch
+ * whose forced layout would exceed 32768 waves (all its frames) fails with RT_E_UNSUPPORTED and renders nothing;
+ * the adaptive mode has no such limit. */
 rt_status rt_set_tile_balance(rt_ctx_t ctx, int mode);
 /* The last launch shape's tile balance: out[0] plans run, [1] tiles split by the last plan, [2] its work items,
  * [3] the extra-wave budget, [4] the costliest / [5] the mean tile time (10-ns ticks), [6] the split threshold,
