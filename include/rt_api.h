@@ -237,6 +237,14 @@ rt_status rt_set_stats(rt_ctx_t ctx, int enable);
  * small ring of slots, each ordered on the device after the other streams' last uses of it (no host wait). */
 rt_status rt_dispatch_rays(rt_ctx_t ctx, uint32_t W, uint32_t H, const uint32_t* rows,
                            uint32_t nrows, void* rgba8_dev, float* rgba32f_dev, void* hip_stream);
+/* nframes (1 .. 4) full W x H frames in ONE launch (the grid's z): frame z with the 64-float camera buffer
+ * cameras[64 z ..] (NULL: the context's camera for every frame), written as R8G8B8A8_UNORM at
+ * rgba8_dev + z * frame_stride bytes (0: W * H * 4, the frames back to back). Each frame equals the one
+ * rt_dispatch_rays renders with that camera. No reference counterpart (one DispatchRays per frame,
+ * D3D12HelloTriangle.cpp:584-592): a batch of views or of consecutive frames pays one launch and one host issue,
+ * and the frames' waves share one grid (no tail between them). Same stream rules as rt_dispatch_rays. */
+rt_status rt_dispatch_frames(rt_ctx_t ctx, uint32_t W, uint32_t H, uint32_t nframes, const float* cameras,
+                             void* rgba8_dev, uint64_t frame_stride, void* hip_stream);
 /* Stream lifetime: the context notes (host-side, no event per launch) which streams launched with the current
  * TLAS version, and records one event on each of them when the next rt_tlas_build swaps that version out; the tile
  * balance likewise notes the streams that read a work list, and queries the stream of a shape's previous launch

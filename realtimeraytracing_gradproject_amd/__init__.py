@@ -106,6 +106,7 @@ SIGNATURES = [
     ("rt_ctx_counters", _I, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     ("rt_set_stats", _I, [_P, _I]),
     ("rt_dispatch_rays", _I, [_P, _U32, _U32, _P, _U32, _P, _P, _P]),
+    ("rt_dispatch_frames", _I, [_P, _U32, _U32, _U32, _P, _P, ctypes.c_uint64, _P]),
     ("rt_trace_rays", _I, [_P, _P, _U32, _U32, _P, _P, _P]),
     ("rt_raster_draw", _I, [_P, _UP, _U32, _FP, _U32, _U32, _P, _P, _P]),
     ("rt_assemble_strips", _I, [_P, _U32, _U32, _U32, _U32, _P, _P, _P]),
@@ -697,6 +698,16 @@ class Context:
             rp, nr = None, height
         self._check(self._lib.rt_dispatch_rays(self._h, width, height, rp, nr, _ptr(rgba8), _ptr(rgba32f), stream),
                     "rt_dispatch_rays")
+
+    def dispatch_frames(self, width: int, height: int, rgba8, cameras=None, stream: Optional[int] = None,
+                        frame_stride: int = 0):
+        """rt_dispatch_frames: len(rgba8) (1..4) full frames in one launch. rgba8: an (n, H, W, 4) uint8 device
+        tensor (frames back to back, or frame_stride bytes apart); cameras: n x 64 floats (None: the context's
+        camera for every frame)."""
+        n = int(rgba8.shape[0])
+        cams = None if cameras is None else _f32(cameras, 64 * n)
+        self._check(self._lib.rt_dispatch_frames(self._h, width, height, n, None if cams is None else _fptr(cams),
+                                                 _ptr(rgba8), frame_stride, stream), "rt_dispatch_frames")
 
     def trace_rays(self, rays, n: int, any_hit: bool, hits, uv=None, stream: Optional[int] = None,
                    cull_back: bool = False, cull_front: bool = False):

@@ -1521,6 +1521,20 @@ rt_status rt_dispatch_rays(rt_ctx_t c, uint32_t W, uint32_t H, const uint32_t* r
   return RT_OK;
 }
 
+rt_status rt_dispatch_frames(rt_ctx_t c, uint32_t W, uint32_t H, uint32_t nframes, const float* cameras,
+                             void* rgba8, uint64_t frame_stride, void* stream) {
+  if (!c) return RT_E_INVALID;
+  if (nframes < 1 || nframes > (uint32_t)rt::kMaxLaunchFrames)
+    return fail(c, RT_E_INVALID, "rt_dispatch_frames: 1..4 frames per launch");
+  if (frame_stride && frame_stride < (uint64_t)W * H * 4)
+    return fail(c, RT_E_INVALID, "rt_dispatch_frames: frame stride below one frame");
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  rt_status st = rt::check_dispatch(c, W, H, rgba8);
+  if (st != RT_OK) return st;
+  return rt::dispatch_frame(c, W, H, nullptr, H, rgba8, nullptr, s, 4, nframes, cameras, frame_stride, 0);
+}
+
 rt_status rt_trace_rays(rt_ctx_t c, const float* rays, uint32_t n, uint32_t ray_flags, uint32_t* hits, float* uv,
                         void* stream) {
   if (!c || (!rays && n) || (!hits && n)) return fail(c, RT_E_INVALID, "rt_trace_rays: null argument");

@@ -843,3 +843,39 @@ def test_stress_cases_schedules_equal_per_ray(case):
         g8, g32 = gpu_render(c, spec, schedule=sched)
         assert_images_equal(g8, g32, o8, o32, f"{name} schedule {sched}")
     c.close()
+
+
+@pytest.mark.parametrize("name,size,nframes", [("C2", (192, 108), 4), ("C4", (200, 101), 3), ("C5", (96, 54), 2),
+                                                ("REF", (160, 90), 4), ("C1", (64, 64), 1)])
+def test_dispatch_frames_equal_oracle(name, size, nframes):
+    """rt_dispatch_frames: n frames in one launch, a camera each, back to back or at a padded stride: every frame
+    equals the oracle's frame for its camera (one-sample, 4-spp sample-lane and REF kernels)."""
+    base = scenes.config(name).with_size(*size)
+    c, o = load_both(base)
+    eyes = [(1.5, 1.5, 1.5), (2.2, 1.4, 1.1), (1.1, 1.9, 2.4), (3.0, 2.0, 0.5)]
+    specs = []
+    for k in range(nframes):
+        sp = base.with_size(*size)
+        if name in ("C4", "C5"):
+            sp.camera = ((18.0 + 2 * k, 14.0 - k, 18.0 - 3 * k), (0.0, 1.0, 0.0), (0.0, 1.0, 0.0))
+        else:
+            sp.camera = (eyes[k], (0.0, 0.0, 0.0), (0.0, 1.0, 0.0))
+        specs.append(sp)
+    W, H = size
+    cams = np.stack([sp.camera_buffer().ravel() for sp in specs])
+    for pad in (0, 4096):
+        stride = W * H * 4 + pad
+        buf = torch.full((nframes * stride,), 7, dtype=torch.uint8, device="cuda")
+        c.dispatch_frames(W, H, buf.view(nframes, -1), cams, stream=torch.cuda.current_stream().cuda_stream,
+                          frame_stride=stride if pad else 0)
+        torch.cuda.synchronize()
+        host = buf.cpu().numpy()
+        for k, sp in enumerate(specs):
+            o8, _, _ = o.render_spec(sp, nthreads=8, want_float=False)
+            got = host[k * stride:k * stride + W * H * 4].reshape(H, W, 4)
+            assert np.array_equal(got, o8), f"{name} frame {k} pad {pad}"
+            if pad:
+                assert (host[k * stride + W * H * 4:(k + 1) * stride] == 7).all(), "wrote past the frame"
+    with pytest.raises(rt.RtError):
+        c.dispatch_frames(W, H, torch.empty((5, H, W, 4), dtype=torch.uint8, device="cuda"))
+    c.close()
