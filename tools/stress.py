@@ -87,7 +87,7 @@ def main():
     t_end = time.time() + a.minutes * 60.0
     t_print = time.time()
     tally = {"episodes": 0, "frames": 0, "schedule_checks": 0, "oracle_checks": 0, "loopback_episodes": 0,
-             "tlas_updates": 0, "hot_reloads": 0, "limit_refusals": 0, "plans": 0,
+             "tlas_updates": 0, "hot_reloads": 0, "limit_refusals": 0, "batch_episodes": 0, "plans": 0,
              "by_scene": {}}
     while time.time() < t_end:
         name, spec = pick_scene(rng)
@@ -103,7 +103,61 @@ def main():
         n = int(rng.integers(8, 80))
         wobble = float(rng.uniform(0.05, 1.0))
         grid = len(spec.instances) > 8 and name != "RANDOM"
-        if rng.random() < 0.2 and spec.width >= 8 and spec.height >= 8:
+        if rng.random() < 0.12:
+            # batches (rt_dispatch_frames: 1..4 frames, a camera each) on 1..3 streams, rt_trace_rays launched on
+            # another stream between them; sampled frames == a single rt_dispatch_rays of the same camera, the rays'
+            # hits == the same rays traced again alone
+            tally["batch_episodes"] += 1
+            nstreams = int(rng.integers(1, 4))
+            streams = [torch.cuda.Stream() for _ in range(nstreams)]
+            sr = torch.cuda.Stream()
+            nray = 4096
+            o_ = rng.normal(size=(nray, 3))
+            o_ = o_ / np.linalg.norm(o_, axis=1, keepdims=True) * 20.0
+            d_ = rng.uniform(-3, 3, size=(nray, 3)) - o_
+            d_ /= np.linalg.norm(d_, axis=1, keepdims=True)
+            rays = np.zeros((nray, 8), np.float32)
+            rays[:, :3], rays[:, 4:7], rays[:, 7] = o_, d_, 1e5
+            d_rays = torch.from_numpy(rays).cuda()
+            hits_a = torch.zeros((nray, 4), dtype=torch.int32, device="cuda")
+            batches, specs = [], []
+            for k0 in range(0, n, 4):
+                F = int(rng.integers(1, 5))
+                sps = [moved(spec, k, n, wobble) for k in range(k0, k0 + F)]
+                buf = torch.empty((F, spec.height, spec.width, 4), dtype=torch.uint8, device="cuda")
+                cams = np.stack([sp.camera_buffer().ravel() for sp in sps])
+                try:
+                    c.dispatch_frames(spec.width, spec.height, buf, cams, stream=streams[(k0 // 4) % nstreams].cuda_stream)
+                except rt.RtError as e:
+                    if "forced layouts take at most" not in str(e):
+                        raise
+                    tally["limit_refusals"] += 1  # the documented cap of the test-only forced layouts
+                    c.set_tile_balance(1)
+                    c.dispatch_frames(spec.width, spec.height, buf, cams, stream=streams[(k0 // 4) % nstreams].cuda_stream)
+                batches.append(buf)
+                specs.append(sps)
+                if k0 == 0:
+                    any_hit = bool(rng.random() < 0.5)
+                    c.trace_rays(d_rays, nray, any_hit, hits_a, stream=sr.cuda_stream)
+            torch.cuda.synchronize()
+            tally["frames"] += sum(len(x) for x in specs)
+            hits_b = torch.zeros((nray, 4), dtype=torch.int32, device="cuda")
+            c.trace_rays(d_rays, nray, any_hit, hits_b, stream=sr.cuda_stream)
+            torch.cuda.synchronize()
+            if not torch.equal(hits_a, hits_b):
+                print(json.dumps({"error": "rays traced beside frames != traced alone", "scene": name}), flush=True)
+                return 1
+            for q in sorted(set(int(x) for x in rng.integers(0, len(batches), size=2))):
+                j = int(rng.integers(0, len(specs[q])))
+                c.set_camera(specs[q][j].camera_buffer())
+                ref = render(c, specs[q][j], streams[0], rt.RT_SCHED_PACKET)
+                torch.cuda.synchronize()
+                if not torch.equal(ref, batches[q][j]):
+                    print(json.dumps({"error": "batched frame != dispatch", "scene": name, "batch": q, "frame": j,
+                                      "mode": mode}), flush=True)
+                    return 1
+                tally["schedule_checks"] += 1
+        elif rng.random() < 0.2 and spec.width >= 8 and spec.height >= 8:
             # the tiled loop on the loopback transport, a camera per frame
             tally["loopback_episodes"] += 1
             nranks = int(rng.integers(2, 9))
