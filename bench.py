@@ -668,35 +668,74 @@ def fetched_bytes(st: dict, pixels: int) -> int:
             + BYTES_PER_PIXEL * pixels)
 
 
+# SURVEY.md §8(d)'s per-lane algorithmic bytes: 24 B per AABB test + 36 B per triangle test + 4 B per pixel. The
+# packet walk loads a node / triangle once per WAVE into SGPRs and every lane tests it from there, so this model
+# counts a wave-uniform scalar fetch 64 times: a logical figure (it exceeds the HBM peak), not memory traffic.
+LOGICAL_BYTES_PER_AABB_TEST = 24
+LOGICAL_BYTES_PER_TRI_TEST = 36
+N_CU, N_SIMD = 256, 1024
+
+
+def logical_bytes(st: dict, pixels: int) -> int:
+    return (LOGICAL_BYTES_PER_AABB_TEST * st["aabb_tests"] + LOGICAL_BYTES_PER_TRI_TEST * st["tri_tests"]
+            + BYTES_PER_PIXEL * pixels)
+
+
 def roofline(config: str, st: dict, pixels: int, kernel_ms: float, schedule: str) -> dict:
-    """Fetched bytes per launch (per-wave record fetches, counted by the STATS pass) against the L2
-    roof, the measured HBM traffic against the HBM roof, and the SALU / VALU issue fractions from the
-    committed SQ counters; `bound` names the pipe closest to its roof."""
+    """The trace kernel against every roof it could meet, and the binding one on top (the line's
+    achieved / peak / frac are the BOUND pipe's, so frac = achieved / peak = fracs[bound]):
+      l2    bytes fetched per launch (per-wave record fetches from the STATS pass) / kernel time vs the L2 roof;
+      hbm   measured HBM bytes per launch (rocprofv3 PMC, profiles/) / kernel time vs 8 TB/s;
+      valu  wave64 VALU instructions per launch / (1024 SIMDs x cycles / 2), from the committed SQ counters, stated
+            as G instructions / s at the counters' shader clock (cycles per XCD / the profiled kernel time);
+      salu  scalar instructions / (256 CUs x cycles), likewise.
+    `logical_bytes` is SURVEY §8(d)'s per-lane model, labelled: it counts wave-uniform fetches once per lane."""
     b = fetched_bytes(st, pixels)
-    achieved = b / (kernel_ms * 1e-3) / 1e9
+    l2_ach = b / (kernel_ms * 1e-3) / 1e9
     prof = load_profile(config) or {}
     traffic = prof.get("hbm_bytes_per_launch")
     issue = prof.get("issue")
-    fracs = {"l2": achieved / L2_PEAK_GBS}
+    pipes = {"l2": {"achieved": round(l2_ach, 1), "peak": L2_PEAK_GBS, "unit": "GB/s", "frac": l2_ach / L2_PEAK_GBS,
+                    "bytes_per_launch": int(b)}}
     if traffic:
-        fracs["hbm"] = traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
-    if issue:
-        fracs["salu"] = issue["salu_frac"]
-        fracs["valu"] = issue["valu_frac"]
+        hb = traffic / (kernel_ms * 1e-3) / 1e9
+        pipes["hbm"] = {"achieved": round(hb, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hb / HBM_PEAK_GBS,
+                        "source": prof.get("source")}
+    rk = prof.get("rocprof_kernel_avg_ms")
+    if issue and rk:
+        cyc = issue["cycles_per_xcd"]
+        clk = cyc / (rk * 1e6)  # GHz: the counters' cycles over the profiled kernel time
+        for pipe, per_launch, width in (("valu", issue["valu_per_launch"], N_SIMD / 2),
+                                        ("salu", issue["salu_per_launch"], N_CU)):
+            frac = issue[pipe + "_frac"]
+            pipes[pipe] = {"achieved": round(per_launch / (rk * 1e6), 2), "peak": round(width * clk, 2),
+                           "unit": "G instructions/s", "frac": frac, "per_launch": per_launch,
+                           "clock_ghz": round(clk, 3)}
+    fracs = {k: v["frac"] for k, v in pipes.items()}
     bound = max(fracs, key=fracs.get)
-    out = {"bound": bound, "achieved": round(achieved, 1), "peak": L2_PEAK_GBS, "unit": "GB/s",
-           "frac": round(achieved / L2_PEAK_GBS, 4), "traffic": traffic,
+    top = pipes[bound]
+    lb = logical_bytes(st, pixels)
+    out = {"bound": bound, "achieved": top["achieved"], "peak": top["peak"], "unit": top["unit"],
+           "frac": round(top["frac"], 4), "traffic": traffic,
+           "l2_frac": round(fracs["l2"], 4),
            "kernel": "k_trace_frame" if schedule == "lane" else "k_trace_frame_packet",
            "kernel_ms": round(kernel_ms, 4), "bytes_per_launch": int(b),
            "model": (f"{BYTES_PER_NODE_FETCH} B/node fetch + {BYTES_PER_TRI_FETCH} B/triangle fetch + "
                      f"{BYTES_PER_INST_FETCH} B/instance fetch (per wave in packets) + {BYTES_PER_SHADE} B/primary "
                      f"ray shading + {BYTES_PER_PIXEL} B/pixel"),
+           "logical_bytes": {"bytes_per_launch": int(lb), "GB_per_s": round(lb / (kernel_ms * 1e-3) / 1e9, 1),
+                             "model": (f"SURVEY 8(d): {LOGICAL_BYTES_PER_AABB_TEST} B/AABB test + "
+                                       f"{LOGICAL_BYTES_PER_TRI_TEST} B/triangle test (per lane) + "
+                                       f"{BYTES_PER_PIXEL} B/pixel"),
+                             "note": "per-lane logical bytes: a wave-uniform scalar fetch counted once per lane; "
+                                     "not memory traffic (l2 / hbm are)"},
            "node_fetches": int(st["node_fetches"]), "tri_fetches": int(st["tri_fetches"]),
            "instance_fetches": int(st["instance_fetches"]),
            "aabb_tests": int(st["aabb_tests"]), "tri_tests": int(st["tri_tests"]),
-           "fracs": {k: round(v, 4) for k, v in fracs.items()}}
+           "fracs": {k: round(v, 4) for k, v in fracs.items()},
+           "pipes": {k: {**v, "frac": round(v["frac"], 4)} for k, v in pipes.items()}}
     if traffic:
-        out["hbm"] = {"achieved": round(traffic / (kernel_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+        out["hbm"] = {"achieved": pipes["hbm"]["achieved"], "peak": HBM_PEAK_GBS,
                       "frac": round(fracs["hbm"], 4), "source": prof.get("source")}
     if issue:
         out["issue"] = dict(issue)

@@ -212,12 +212,20 @@ rt_status rt_set_tile_balance(rt_ctx_t ctx, int mode);
  * back to the plain grid's list, so no part is ever dropped), [17] the plans that fell back, [18..19] 0. Host-side
  * read of host-mapped memory (may lag the device by a few launches). */
 #define RT_BALANCE_INFO_COUNT 20
-rt_status rt_tile_balance_info(rt_ctx_t ctx, uint32_t out[RT_BALANCE_INFO_COUNT]);
+/* rt_tile_balance_info_n fills min(n, RT_BALANCE_INFO_COUNT) words of out (the array may grow in later versions:
+ * pass its capacity). rt_tile_balance_info is the round-4 entry point and fills exactly its 16 words ([0..15]). */
+rt_status rt_tile_balance_info_n(rt_ctx_t ctx, uint32_t* out, uint32_t n);
+#define RT_BALANCE_INFO_COUNT_V1 16
+rt_status rt_tile_balance_info(rt_ctx_t ctx, uint32_t out[RT_BALANCE_INFO_COUNT_V1]);
 /* Context diagnostics: out[0] device-wide synchronisations so far (builds, rebuilds, buffer growth: never a frame
  * launch on a steady pipeline), [1] tile-balance maps recycled for a new launch shape (only once every stream that
- * used them is idle: host queries, no synchronisation), [2] launches that ran the plain grid because every map was
- * in use by work in flight, [3] maps held. */
+ * used them is idle and none of them was used in the last 64 shape lookups: host queries, no synchronisation), [2]
+ * launches that ran the plain grid because no map was free (after a miss the table is rescanned only every 16 such
+ * launches), [3] maps held, [4] recycled maps that went on to start a plan (recycling that paid off).
+ * rt_ctx_counters_n fills min(n, RT_CTX_COUNTERS_V2) words; rt_ctx_counters exactly its 4 ([0..3]). */
 #define RT_CTX_COUNTERS 4
+#define RT_CTX_COUNTERS_V2 5
+rt_status rt_ctx_counters_n(rt_ctx_t ctx, uint64_t* out, uint32_t n);
 rt_status rt_ctx_counters(rt_ctx_t ctx, uint64_t out[RT_CTX_COUNTERS]);
 /* Enables device counters (rt_stats). Costs time: off for timed runs. */
 rt_status rt_set_stats(rt_ctx_t ctx, int enable);
@@ -238,8 +246,9 @@ rt_status rt_set_stats(rt_ctx_t ctx, int enable);
 rt_status rt_dispatch_rays(rt_ctx_t ctx, uint32_t W, uint32_t H, const uint32_t* rows,
                            uint32_t nrows, void* rgba8_dev, float* rgba32f_dev, void* hip_stream);
 /* nframes (1 .. 4) full W x H frames in ONE launch (the grid's z): frame z with the 64-float camera buffer
- * cameras[64 z ..] (NULL: the context's camera for every frame), written as R8G8B8A8_UNORM at
- * rgba8_dev + z * frame_stride bytes (0: W * H * 4, the frames back to back). Each frame equals the one
+ * cameras[64 z ..] (NULL: the context's camera for every frame, which rt_set_camera must then have set), written as
+ * R8G8B8A8_UNORM at rgba8_dev + z * frame_stride bytes (0: W * H * 4, the frames back to back; else at least one
+ * frame and a multiple of 4: RT_E_INVALID otherwise). Each frame equals the one
  * rt_dispatch_rays renders with that camera. No reference counterpart (one DispatchRays per frame,
  * D3D12HelloTriangle.cpp:584-592): a batch of views or of consecutive frames pays one launch and one host issue,
  * and the frames' waves share one grid (no tail between them). Same stream rules as rt_dispatch_rays. */
@@ -371,6 +380,19 @@ uint32_t rt_comm_pipeline_depth(rt_comm_t comm);
  * multi-GPU loop is this library's). */
 rt_status rt_comm_set_batch(rt_comm_t comm, uint32_t frames_per_gather);
 uint32_t rt_comm_batch(rt_comm_t comm);
+/* Phase timing of the loop on this rank (diagnostics for the multi-GPU bench line; no reference counterpart — the
+ * reference has no multi-GPU path, its frame spans submit -> fence, D3D12HelloTriangle.cpp:436-470). When on, each
+ * step records timing-event pairs around its render launch(es) (render stream), its gather (gather stream: from the
+ * moment this rank's render is done to the gather's end, any wait for the other ranks inside the collective
+ * included) and rank 0's assembly, and the host time of each rt_render_strips* call and of the issue thread's work.
+ * Drains the pipeline (like rt_comm_set_batch: every rank between the same calls) and resets the sums. */
+rt_status rt_comm_set_phase_timing(rt_comm_t comm, int on);
+/* The sums since rt_comm_set_phase_timing(on) (drains the pipeline first). out[0] frames, [1] render launches, [2]
+ * their summed ms, [3] gathers, [4] summed ms, [5] assemblies (rank 0), [6] summed ms, [7] caller host us summed over
+ * [8] calls, [9] the issue thread's host us, [10] bytes into rank 0 from the other ranks, [11] bytes of every rank's
+ * block. Fills min(n, RT_COMM_PHASE_COUNT) doubles. */
+#define RT_COMM_PHASE_COUNT 12
+rt_status rt_comm_phase_stats(rt_comm_t comm, double* out, uint32_t n);
 /* One tiled frame, collective over the ranks (every rank calls it, in the same frame order): this rank's
  * strips are rendered on render_stream into one of the communicator's pipeline slots (NULL: slot k's own
  * stream of the communicator; its render streams and its gather stream sit on separate hardware queues). The

@@ -1175,7 +1175,7 @@ static float olog2(float x) {
   float m; memcpy(&m, &mb, 4);
   if (m > 1.41421356f) { m = m * 0.5f; e = e + 1; }
   float f = m - 1.0f;
-  float s = f / (2.0f + f);
+  float s = f * (1.0f / (2.0f + f)); /* the device's rcp_exact(2 + f) */
   float s2 = s * s;
   float p = 1.0f / 11.0f;
   p = p * s2 + 1.0f / 9.0f;
@@ -1211,67 +1211,82 @@ float oracle_pow(float x, float y) { if (!(x > 1e-30f)) return 0.0f; return oexp
 
 static const float OPI = 3.14159265359f; /* Common.hlsl:1 */
 
-/* CalculateDirectLighting (Hit.hlsl:83-95) */
-static vec3 odirect(vec3 P, vec3 n, vec3 albedo, const oracle_light* L, uint32_t nl) {
-  vec3 c = mk(0, 0, 0);
-  for (uint32_t l = 0; l < nl; ++l) {
-    vec3 lp = ld3(L[l].position), lc = ld3(L[l].color);
-    vec3 tl = vneg(vnorm(vsub(lp, P)));
-    float f = vdot(n, tl);
-    float ti = fmax2(0.0f, f * L[l].intensity);
-    c = vadd(c, vscale(vmul(albedo, lc), ti));
-  }
-  return c;
-}
-
-/* CalculatePBRShading (Hit.hlsl:97-174) with FresnelSchlick :97-100, GGX :102-113,
- * SchlickGGX :115-122, Smith :124-130 */
-static vec3 opbr(vec3 n, vec3 cam, vec3 P, const oracle_light* Ls, uint32_t nl, const float* mat) {
+/* ClosestHit's finalSurfaceColor = CalculateDirectLighting (Hit.hlsl:83-95) + CalculatePBRShading
+ * (:97-174, FresnelSchlick :97-100, GGX :102-113, SchlickGGX :115-122, Smith :124-130), in the pinned
+ * float32 form of the device's surface_ref (csrc/rt_trace.hip, round 6): one loop over the lights
+ * (the direct term's -normalize(lp - P) and the PBR term's L and distance share one sqrt and one
+ * reciprocal), pixel and material invariants out of the loop, each quotient a product with the
+ * IEEE reciprocal 1.0f / x (the device's rcp_exact gives the same bits), the diffuse term
+ * (1 - F) * ((1 - metallic) albedo / PI). The two sums keep their own accumulators and light order. */
+static void osurface(vec3 P, vec3 n, vec3 cam, const oracle_light* Ls, uint32_t nl, const float* mat,
+                     vec3* direct, vec3* pbr) {
   vec3 albedo = ld3(mat);
   float rough = mat[3], metal = mat[4];
-  vec3 N = vneg(vnorm(n));
-  vec3 V = vnorm(vsub(cam, P));
-  vec3 L0 = mk(0, 0, 0);
+  float a = rough * rough, a2 = a * a;
+  float rp1 = rough + 1.0f;
+  float k = (rp1 * rp1) / 8.0f;
+  float omk = 1.0f - k;
+  vec3 F0 = mk(0.04f + metal * (albedo.x - 0.04f), 0.04f + metal * (albedo.y - 0.04f), 0.04f + metal * (albedo.z - 0.04f));
+  float km = 1.0f - metal;
+  vec3 kdA = mk((km * albedo.x) / OPI, (km * albedo.y) / OPI, (km * albedo.z) / OPI);
+  vec3 N = vneg(vscale(n, 1.0f / sqrtf(vdot(n, n))));
+  vec3 Vd = vsub(cam, P);
+  vec3 V = vscale(Vd, 1.0f / sqrtf(vdot(Vd, Vd)));
+  float NdotV = fmax2(vdot(N, V), 0.0f);
+  float ggx2 = NdotV * (1.0f / (NdotV * omk + k));
+  float v4 = 4.0f * NdotV;
+  vec3 cd = mk(0, 0, 0), L0 = mk(0, 0, 0);
   for (uint32_t l = 0; l < nl; ++l) {
     vec3 lp = ld3(Ls[l].position), lc = ld3(Ls[l].color);
-    vec3 L = vnorm(vsub(lp, P));
-    vec3 H = vnorm(vadd(V, L));
     vec3 dv = vsub(lp, P);
     float dist = sqrtf(vdot(dv, dv));
+    vec3 L = vscale(dv, 1.0f / dist);
+    float ti = fmax2(0.0f, vdot(n, vneg(L)) * Ls[l].intensity);
+    cd = vadd(cd, vscale(vmul(albedo, lc), ti));
+    vec3 Hd = vadd(V, L);
+    vec3 H = vscale(Hd, 1.0f / sqrtf(vdot(Hd, Hd)));
     float att = 1.0f / fmax2(dist * dist, 1.0f);
     vec3 radiance = vscale(lc, att);
-    vec3 F0 = mk(0.04f + metal * (albedo.x - 0.04f), 0.04f + metal * (albedo.y - 0.04f), 0.04f + metal * (albedo.z - 0.04f));
     float x = 1.0f - fmax2(vdot(H, V), 0.0f);
     x = fmin2(fmax2(x, 0.0f), 1.0f);
     float x5 = ((x * x) * (x * x)) * x;
     vec3 F = mk(F0.x + (1.0f - F0.x) * x5, F0.y + (1.0f - F0.y) * x5, F0.z + (1.0f - F0.z) * x5);
-    float a = rough * rough, a2 = a * a;
     float NdotH = fmax2(vdot(N, H), 0.0f);
     float NdotH2 = NdotH * NdotH;
     float denom = NdotH2 * (a2 - 1.0f) + 1.0f;
     denom = (OPI * denom) * denom;
-    float NDF = a2 / denom;
-    float r = rough + 1.0f;
-    float k = (r * r) / 8.0f;
-    float NdotV = fmax2(vdot(N, V), 0.0f);
+    float NDF = a2 * (1.0f / denom);
     float NdotL = fmax2(vdot(N, L), 0.0f);
-    float ggx2 = NdotV / (NdotV * (1.0f - k) + k);
-    float ggx1 = NdotL / (NdotL * (1.0f - k) + k);
+    float ggx1 = NdotL * (1.0f / (NdotL * omk + k));
     float G = ggx1 * ggx2;
-    vec3 num = vscale(F, NDF * G);
-    float den = (4.0f * fmax2(vdot(N, V), 0.0f)) * fmax2(vdot(N, L), 0.0f) + 0.0001f;
-    vec3 spec = mk(num.x / den, num.y / den, num.z / den);
-    vec3 kD = mk(1.0f - F.x, 1.0f - F.y, 1.0f - F.z);
-    float km = 1.0f - metal;
-    kD = mk(kD.x * km, kD.y * km, kD.z * km);
-    vec3 diff = mk((kD.x * albedo.x) / OPI, (kD.y * albedo.y) / OPI, (kD.z * albedo.z) / OPI);
-    float NdL = fmax2(vdot(N, L), 0.0f);
-    L0 = vadd(L0, vscale(vmul(vadd(diff, spec), radiance), NdL));
+    float sp = (NDF * G) * (1.0f / (v4 * NdotL + 0.0001f));
+    vec3 spec = vscale(F, sp);
+    vec3 diff = mk((1.0f - F.x) * kdA.x, (1.0f - F.y) * kdA.y, (1.0f - F.z) * kdA.z);
+    L0 = vadd(L0, vscale(vmul(vadd(diff, spec), radiance), NdotL));
   }
   vec3 c = vscale(L0, 0.2f);
-  c = mk(c.x / (c.x + 1.0f), c.y / (c.y + 1.0f), c.z / (c.z + 1.0f));
+  c = mk(c.x * (1.0f / (c.x + 1.0f)), c.y * (1.0f / (c.y + 1.0f)), c.z * (1.0f / (c.z + 1.0f)));
   float g = 1.0f / 2.2f;
-  return mk(oracle_pow(c.x, g), oracle_pow(c.y, g), oracle_pow(c.z, g));
+  *direct = cd;
+  *pbr = mk(oracle_pow(c.x, g), oracle_pow(c.y, g), oracle_pow(c.z, g));
+}
+static vec3 osurface_sum(vec3 P, vec3 n, vec3 cam, const oracle_light* Ls, uint32_t nl, const float* mat) {
+  vec3 d, p;
+  osurface(P, n, cam, Ls, nl, mat, &d, &p);
+  return vadd(d, p);
+}
+
+/* the two terms of osurface alone (tests/test_oracle.py checks each against the float64 restatement) */
+static vec3 opbr(vec3 n, vec3 cam, vec3 P, const oracle_light* Ls, uint32_t nl, const float* mat) {
+  vec3 d, p;
+  osurface(P, n, cam, Ls, nl, mat, &d, &p);
+  return p;
+}
+static vec3 odirect(vec3 P, vec3 n, vec3 albedo, const oracle_light* L, uint32_t nl) {
+  float mat[6] = {albedo.x, albedo.y, albedo.z, 0.5f, 0.0f, 0.0f};
+  vec3 d, p;
+  osurface(P, n, P, L, nl, mat, &d, &p);
+  return d;
 }
 
 void oracle_pbr(const float n[3], const float cam[3], const float P[3], const oracle_light* lights, uint32_t nl,
@@ -1390,7 +1405,7 @@ static vec3 oshade_ref(const octx* c, uint32_t py, vec3 O, vec3 D, int f, ohit h
         term = oplane(c, P, &h, st);
       } else {
         vec3 n = o_interp_normal(c->s, h.inst, h.prim, h.u, h.v);
-        vec3 s = vadd(odirect(P, n, ld3(c->mat), c->L, c->nl), opbr(n, ro, P, c->L, c->nl, c->mat));
+        vec3 s = osurface_sum(P, n, ro, c->L, c->nl, c->mat);
         if (refl != 0.0f && (ir->instance_id == 0u || ir->instance_id == 1u) && depth < O_MAX_REFLECT) {
           sk[depth] = s;
           vec3 dir = vnorm(vnorm(vreflect(vnorm(rd), n)));
@@ -1509,7 +1524,7 @@ static void osample_packet(const octx* c, const uint32_t* px, const uint32_t* py
             continue;
           }
           vec3 n = o_interp_normal(c->s, h[l].inst, h[l].prim, h[l].u, h[l].v);
-          vec3 s = vadd(odirect(P[l], n, ld3(c->mat), c->L, c->nl), opbr(n, ro[l], P[l], c->L, c->nl, c->mat));
+          vec3 s = osurface_sum(P[l], n, ro[l], c->L, c->nl, c->mat);
           if (refl != 0.0f && (ir->instance_id == 0u || ir->instance_id == 1u) && depth < O_MAX_REFLECT) {
             sk[l][depth] = s;
             vec3 dir = vnorm(vnorm(vreflect(vnorm(rd[l]), n)));

@@ -103,7 +103,9 @@ SIGNATURES = [
     ("rt_set_tile_rows", _I, [_P, _I]),
     ("rt_set_tile_balance", _I, [_P, _I]),
     ("rt_tile_balance_info", _I, [_P, _UP]),
+    ("rt_tile_balance_info_n", _I, [_P, _UP, _U32]),
     ("rt_ctx_counters", _I, [_P, ctypes.POINTER(ctypes.c_uint64)]),
+    ("rt_ctx_counters_n", _I, [_P, ctypes.POINTER(ctypes.c_uint64), _U32]),
     ("rt_set_stats", _I, [_P, _I]),
     ("rt_dispatch_rays", _I, [_P, _U32, _U32, _P, _U32, _P, _P, _P]),
     ("rt_dispatch_frames", _I, [_P, _U32, _U32, _U32, _P, _P, ctypes.c_uint64, _P]),
@@ -123,6 +125,8 @@ SIGNATURES = [
     ("rt_comm_destroy", _I, [_P]),
     ("rt_comm_abort", _I, [_P]),
     ("rt_comm_loopback_render_ranks", _I, [_P, _U32, _U32]),
+    ("rt_comm_set_phase_timing", _I, [_P, ctypes.c_int]),
+    ("rt_comm_phase_stats", _I, [_P, ctypes.POINTER(ctypes.c_double), _U32]),
     ("rt_comm_last_error", ctypes.c_char_p, [_P]),
     ("rt_comm_stream", _P, [_P]),
     ("rt_comm_synchronize", _I, [_P]),
@@ -416,6 +420,8 @@ class Comm:
         the nranks ranks on its one GPU and the gather is a device copy (rank must be 0)."""
         self._lib = ctx._lib
         self.ctx, self.nranks, self.rank = ctx, nranks, rank
+        self.is_loopback = uid is None
+        self._pending = False  # frames handed to render_strips* since the last synchronize (a partly filled batch)
         h = _P()
         if uid is None:
             if rank != 0:
@@ -445,6 +451,7 @@ class Comm:
     def render_strips(self, width: int, height: int, frame_out=None, stream: Optional[int] = None,
                       strip_rows_: int = 8):
         """One tiled frame (rt_render_strips): frame_out is rank 0's H x W x 4 device buffer."""
+        self._pending = True
         self._check(self._lib.rt_render_strips(self._h, width, height, strip_rows_, _ptr(frame_out), stream),
                     "rt_render_strips")
 
@@ -455,6 +462,7 @@ class Comm:
         n = len(frames_out)
         ptrs = (_P * n)(*[_ptr(f) for f in frames_out])
         cams = None if cameras is None else _f32(cameras, 64 * n)
+        self._pending = True
         self._check(self._lib.rt_render_strips_frames(self._h, width, height, strip_rows_, n,
                                                       None if cams is None else _fptr(cams), ptrs, stream),
                     "rt_render_strips_frames")
@@ -480,14 +488,31 @@ class Comm:
 
     def synchronize(self):
         self._check(self._lib.rt_comm_synchronize(self._h), "rt_comm_synchronize")
+        self._pending = False
 
     def close(self):
-        """rt_comm_destroy: drains the pipeline (a partly filled batch included), then frees the communicator."""
+        """rt_comm_destroy: drains the pipeline (a partly filled batch included), then frees the communicator.
+        Collective for an RCCL communicator: EVERY rank must call close() (or every rank abort()); a rank that drops
+        its communicator unclosed aborts it (__del__), and a peer draining a partly filled batch would then wait for
+        a gather that rank never issues."""
         if getattr(self, "_h", None):
             h, self._h = self._h, None
             st = self._lib.rt_comm_destroy(h)
             if st != RT_OK:
                 raise RtError(st, "rt_comm_destroy")
+
+    def set_phase_timing(self, on: bool):
+        """rt_comm_set_phase_timing: timing-event pairs around each step's render, gather and assembly (drains)."""
+        self._check(self._lib.rt_comm_set_phase_timing(self._h, 1 if on else 0), "rt_comm_set_phase_timing")
+        self._pending = False
+
+    def phase_stats(self) -> dict:
+        """rt_comm_phase_stats: the phase sums since set_phase_timing(True) (drains the pipeline)."""
+        out = (ctypes.c_double * 12)()
+        self._check(self._lib.rt_comm_phase_stats(self._h, out, 12), "rt_comm_phase_stats")
+        self._pending = False
+        return dict(zip(("frames", "renders", "render_ms", "gathers", "gather_ms", "assemblies", "assembly_ms",
+                         "host_us", "calls", "issue_us", "bytes_in", "bytes"), list(out)))
 
     def loopback_render_ranks(self, first: int = 0, count: int = 0):
         """rt_comm_loopback_render_ranks: a loopback communicator renders only emulated ranks [first, first + count)
@@ -515,9 +540,20 @@ class Comm:
         return False
 
     def __del__(self):
-        # an unclosed communicator is garbage (an exception path, or interpreter shutdown): the other ranks may not
-        # issue the collective a draining destroy would need, so it aborts
+        # An unclosed communicator is garbage. Loopback: no peers, so it drains like close() (frames already handed
+        # to render_strips are rendered and assembled). RCCL: the other ranks may not issue the collective a
+        # draining destroy would need (an exception path, interpreter shutdown), so it aborts -- and says so when
+        # that discards frames (close() is required on every rank).
+        if not getattr(self, "_h", None):
+            return
         try:
+            if self.is_loopback:
+                self.close()
+                return
+            if self._pending:
+                import warnings
+                warnings.warn("rt.Comm garbage-collected unclosed with frames pending: aborted (their partly filled "
+                              "batch is discarded); call close() on every rank", ResourceWarning, stacklevel=2)
             self.abort()
         except Exception:  # noqa: BLE001  (interpreter shutdown)
             pass
@@ -666,16 +702,18 @@ class Context:
 
     def tile_balance_info(self) -> dict:
         out = (ctypes.c_uint32 * RT_BALANCE_INFO_COUNT)()
-        self._check(self._lib.rt_tile_balance_info(self._h, out), "rt_tile_balance_info")
+        self._check(self._lib.rt_tile_balance_info_n(self._h, out, RT_BALANCE_INFO_COUNT), "rt_tile_balance_info_n")
         return dict(zip(("plans", "split", "items", "extra_cap", "max_ticks", "mean_ticks", "threshold", "launches",
                          "pays", "check_bad", "check_first_tile", "check_first_word", "plan_load_ticks",
                          "plan_budget_ticks", "plan_place_ticks", "slots", "refused", "refused_plans"), list(out)))
 
     def counters(self) -> dict:
-        """rt_ctx_counters: device-wide synchronisations, tile-balance maps recycled / full, maps held."""
-        out = (ctypes.c_uint64 * 4)()
-        self._check(self._lib.rt_ctx_counters(self._h, out), "rt_ctx_counters")
-        return dict(zip(("device_syncs", "balance_recycled", "balance_full", "balance_maps"), list(out)))
+        """rt_ctx_counters_n: device-wide synchronisations, tile-balance maps recycled / full, maps held, recycled maps
+        that reached a plan."""
+        out = (ctypes.c_uint64 * 5)()
+        self._check(self._lib.rt_ctx_counters_n(self._h, out, 5), "rt_ctx_counters_n")
+        return dict(zip(("device_syncs", "balance_recycled", "balance_full", "balance_maps", "balance_recycled_planned"),
+                        list(out)))
 
     def set_stats(self, on: bool):
         self._check(self._lib.rt_set_stats(self._h, 1 if on else 0), "rt_set_stats")
@@ -706,6 +744,7 @@ class Context:
         camera for every frame)."""
         n = int(rgba8.shape[0])
         cams = None if cameras is None else _f32(cameras, 64 * n)
+        self._pending = True
         self._check(self._lib.rt_dispatch_frames(self._h, width, height, n, None if cams is None else _fptr(cams),
                                                  _ptr(rgba8), frame_stride, stream), "rt_dispatch_frames")
 

@@ -223,11 +223,14 @@ struct BalanceMap {
   hipEvent_t pend_ev = nullptr;      // recorded on the plan stream after the pending plan
   hipEvent_t src_ev = nullptr;       // recorded on the launch's stream: the plan starts after its earlier work
   std::vector<hipStream_t> readers;  // streams that launched with the current list since it became current
+  ScratchSlot forgotten;             // events on streams dropped by rt_forget_stream (their launches may still run)
+  bool recycled = false, recycled_planned = false;  // reused for this shape; a plan has started on it since
   void release() {
     if (cost) (void)hipFree(cost);
     if (stats) (void)hipHostFree(stats);
     slot_release(list[0]);
     slot_release(list[1]);
+    slot_release(forgotten);
     if (pend_ev) (void)hipEventDestroy(pend_ev);
     if (src_ev) (void)hipEventDestroy(src_ev);
     *this = BalanceMap();
@@ -280,8 +283,10 @@ struct rt_ctx {
   uint32_t bal_prio = 1;        // RT_BALANCE_PRIO (A/B): the front class's waves raise their issue priority
   uint32_t bal_fine = 1;        // RT_BALANCE_FINE (A/B): adaptive plans may split a tile into 64 one-pixel parts
   static constexpr size_t kMaxBalanceMaps = 32;
+  static constexpr uint32_t kRecycleBackoff = 16;
   std::vector<BalanceMap> bal;
   uint64_t bal_clock = 0;
+  uint32_t bal_backoff = 0;  // launches of unknown shapes left before the next recycling scan
   BalanceMap* bal_last = nullptr;
   ScratchRing plans;
   // scene pools read by the trace kernels (rebuilt by every rt_tlas_build)
@@ -303,6 +308,7 @@ struct rt_ctx {
   // rt_ctx_counters: device-wide synchronisations (quiesce), balance maps recycled for a new shape, launches that ran
   // the plain grid because every map was in use
   uint64_t n_quiesce = 0, bal_recycled = 0, bal_full = 0;
+  uint64_t bal_recycled_planned = 0;  // recycled maps that went on to start a plan (recycling that paid off)
 };
 
 
@@ -841,18 +847,21 @@ rt_status rt_set_tile_balance(rt_ctx_t c, int mode) {
   return RT_OK;
 }
 
-rt_status rt_ctx_counters(rt_ctx_t c, uint64_t out[RT_CTX_COUNTERS]) {
-  if (!c || !out) return RT_E_INVALID;
-  out[0] = c->n_quiesce;
-  out[1] = c->bal_recycled;
-  out[2] = c->bal_full;
-  out[3] = c->bal.size();
+rt_status rt_ctx_counters_n(rt_ctx_t c, uint64_t* out, uint32_t n) {
+  if (!c || (!out && n)) return RT_E_INVALID;
+  const uint64_t v[RT_CTX_COUNTERS_V2] = {c->n_quiesce, c->bal_recycled, c->bal_full, c->bal.size(),
+                                          c->bal_recycled_planned};
+  std::memcpy(out, v, std::min<uint32_t>(n, RT_CTX_COUNTERS_V2) * sizeof(uint64_t));
   return RT_OK;
 }
 
-rt_status rt_tile_balance_info(rt_ctx_t c, uint32_t out[RT_BALANCE_INFO_COUNT]) {
-  if (!c || !out) return RT_E_INVALID;
-  std::memset(out, 0, RT_BALANCE_INFO_COUNT * sizeof(uint32_t));
+rt_status rt_ctx_counters(rt_ctx_t c, uint64_t out[RT_CTX_COUNTERS]) { return rt_ctx_counters_n(c, out, RT_CTX_COUNTERS); }
+
+rt_status rt_tile_balance_info_n(rt_ctx_t c, uint32_t* out_words, uint32_t n) {
+  if (!c || (!out_words && n)) return RT_E_INVALID;
+  uint32_t out[RT_BALANCE_INFO_COUNT];
+  std::memset(out, 0, sizeof(out));
+  std::memset(out_words, 0, std::min<uint32_t>(n, RT_BALANCE_INFO_COUNT) * sizeof(uint32_t));
   const BalanceMap* m = c->bal_last;
   if (!m || !m->stats) return RT_OK;
   const volatile rt::PlanStats* st = m->stats;
@@ -872,7 +881,13 @@ rt_status rt_tile_balance_info(rt_ctx_t c, uint32_t out[RT_BALANCE_INFO_COUNT]) 
   out[15] = st->slots;
   out[16] = st->refused;
   out[17] = st->refused_plans;
+  std::memcpy(out_words, out, std::min<uint32_t>(n, RT_BALANCE_INFO_COUNT) * sizeof(uint32_t));
   return RT_OK;
+}
+
+// the round-4 entry point: exactly its 16 words (a caller built against uint32_t[16] must not be overrun)
+rt_status rt_tile_balance_info(rt_ctx_t c, uint32_t out[RT_BALANCE_INFO_COUNT_V1]) {
+  return rt_tile_balance_info_n(c, out, RT_BALANCE_INFO_COUNT_V1);
 }
 
 rt_status rt_set_stats(rt_ctx_t c, int enable) {
@@ -1038,7 +1053,14 @@ hipError_t ctx_forget_stream(rt_ctx* c, hipStream_t s) {
   // the tile balance's lists: the same for their readers
   for (BalanceMap& m : c->bal) {
     if (m.last_stream == s) m.last_stream = nullptr;
-    m.streams.erase(std::remove(m.streams.begin(), m.streams.end(), s), m.streams.end());
+    auto used = std::find(m.streams.begin(), m.streams.end(), s);
+    if (used != m.streams.end()) {
+      // its last launch may still write the cost map: balance_idle queries this event before the map is recycled
+      // (a recycled map's memset and new shape must not race a forgotten stream's cost stores)
+      m.streams.erase(used);
+      const hipError_t e = slot_mark_use(m.forgotten, s);
+      if (e != hipSuccess && first == hipSuccess) first = e;
+    }
     auto it = std::find(m.readers.begin(), m.readers.end(), s);
     if (it == m.readers.end() || m.cur < 0) continue;
     m.readers.erase(it);
@@ -1049,11 +1071,12 @@ hipError_t ctx_forget_stream(rt_ctx* c, hipStream_t s) {
 }
 void* ctx_stream(rt_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
-rt_status check_dispatch(rt_ctx* c, uint32_t W, uint32_t H, const void* rgba8) {
+rt_status check_dispatch(rt_ctx* c, uint32_t W, uint32_t H, const void* rgba8, bool cameras_given) {
   if (c->cur < 0 && !c->tlas_stale) return fail(c, RT_E_INVALID, "rt_dispatch_rays: no TLAS built");
   if (c->tlas_stale)
     return fail(c, RT_E_INVALID, "rt_dispatch_rays: scene stale (BLAS rebuilt, or the last rt_tlas_build failed)");
-  if (!c->have_camera || !c->have_shading) return fail(c, RT_E_INVALID, "rt_dispatch_rays: camera/shading not set");
+  if (!c->have_shading) return fail(c, RT_E_INVALID, "rt_dispatch_rays: shading not set");
+  if (!c->have_camera && !cameras_given) return fail(c, RT_E_INVALID, "rt_dispatch_rays: camera not set");
   if (W == 0 || H == 0 || !rgba8) return fail(c, RT_E_INVALID, "rt_dispatch_rays: bad size or output");
   return RT_OK;
 }
@@ -1064,7 +1087,7 @@ static bool balance_idle(const BalanceMap& m) {
   if (m.pending >= 0 && m.pend_ev && hipEventQuery(m.pend_ev) != hipSuccess) return false;
   for (hipStream_t s : m.streams)
     if (hipStreamQuery(s) != hipSuccess) return false;
-  return true;
+  return slot_free_for(m.forgotten, nullptr);  // the forgotten streams' last launches too
 }
 
 // The load bound's wave slots for a plan: the occupancy of the kernel the list will drive (from the runtime, for
@@ -1099,10 +1122,22 @@ static BalanceMap* balance_map(rt_ctx* c, uint32_t W, uint32_t nrows, const uint
     c->bal.emplace_back();
     m = &c->bal.back();
   } else if (!forced) {
+    // more live shapes than maps (e.g. 40 emulated loopback ranks, each its own row list) would recycle
+    // maps in a cycle where none survives to its first plan, paying a memset and host queries per launch for a
+    // balance that never runs. A map used within the last 2 x kMaxBalanceMaps lookups is not taken, and after a
+    // miss the table is scanned again only every kRecycleBackoff launches of unknown shapes.
+    if (c->bal_backoff) {
+      --c->bal_backoff;
+      ++c->bal_full;
+      return nullptr;
+    }
     for (BalanceMap& o : c->bal)  // the least recently used idle map that fits
-      if (o.cost_cap >= ntiles && (!m || o.tick < m->tick) && balance_idle(o)) m = &o;
+      if (o.cost_cap >= ntiles && c->bal_clock - o.tick > 2 * rt_ctx::kMaxBalanceMaps && (!m || o.tick < m->tick) &&
+          balance_idle(o))
+        m = &o;
     if (!m) {
       ++c->bal_full;
+      c->bal_backoff = rt_ctx::kRecycleBackoff;
       return nullptr;
     }
     ++c->bal_recycled;
@@ -1124,6 +1159,8 @@ static BalanceMap* balance_map(rt_ctx* c, uint32_t W, uint32_t nrows, const uint
     m->planned_at = 0;
     m->readers.clear();
     m->streams.clear();
+    m->recycled = true;
+    m->recycled_planned = false;
   }
   m->W = W;
   m->nrows = nrows;
@@ -1349,6 +1386,10 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
           m->pending = b;
           m->pending_items = items;
           m->planned_at = m->launches;
+          if (m->recycled && !m->recycled_planned) {
+            m->recycled_planned = true;
+            ++c->bal_recycled_planned;
+          }
         }
         if (use && m->cur >= 0) {
           if (std::find(m->readers.begin(), m->readers.end(), s) == m->readers.end()) m->readers.push_back(s);
@@ -1528,9 +1569,11 @@ rt_status rt_dispatch_frames(rt_ctx_t c, uint32_t W, uint32_t H, uint32_t nframe
     return fail(c, RT_E_INVALID, "rt_dispatch_frames: 1..4 frames per launch");
   if (frame_stride && frame_stride < (uint64_t)W * H * 4)
     return fail(c, RT_E_INVALID, "rt_dispatch_frames: frame stride below one frame");
+  if (frame_stride % 4)  // the RGBA8 stores are 32-bit words
+    return fail(c, RT_E_INVALID, "rt_dispatch_frames: frame stride not a multiple of 4 bytes");
   (void)hipSetDevice(c->device);
   hipStream_t s = pick_stream(c, stream);
-  rt_status st = rt::check_dispatch(c, W, H, rgba8);
+  rt_status st = rt::check_dispatch(c, W, H, rgba8, cameras != nullptr);
   if (st != RT_OK) return st;
   return rt::dispatch_frame(c, W, H, nullptr, H, rgba8, nullptr, s, 4, nframes, cameras, frame_stride, 0);
 }

@@ -123,6 +123,13 @@ hipEvent_t pipeline_event() {
 
 }  // namespace
 
+// rt_comm_set_phase_timing: one timed interval of a step on the device (a pair of timing events on one stream)
+enum PhaseKind { kPhaseRender = 0, kPhaseGather = 1, kPhaseAssembly = 2, kPhases = 3 };
+struct PhaseSpan {
+  hipEvent_t a = nullptr, b = nullptr;
+  int kind = 0;
+};
+
 struct Job {
   uint32_t slot = 0;
   uint32_t nframes = 0;              // frames in the slot (their strips are gathered by one ncclGather)
@@ -186,6 +193,18 @@ struct rt_comm {
   rt_status werr = RT_OK;       // the issue thread's first failure, returned by the next call
   std::string wmsg;
   double w_parts[3] = {0, 0, 0};  // RT_COMM_TIMING: issue-thread hand-off, ncclGather, gather event
+  // rt_comm_set_phase_timing (what a step costs, per phase, on this rank): timing-event pairs around
+  // the render launches (render stream), the gather (gather stream, from the moment the render is done) and rank
+  // 0's assembly, resolved into sums once complete; the host time of the caller's calls and of the issue thread
+  bool phase = false;
+  std::mutex pmu;                 // the two threads record spans
+  std::vector<hipEvent_t> pfree;  // resolved events, reused
+  std::deque<PhaseSpan> ppend;    // recorded spans not yet resolved
+  double p_ms[kPhases] = {0, 0, 0};
+  uint64_t p_n[kPhases] = {0, 0, 0};
+  uint64_t p_frames = 0, p_calls = 0;
+  double p_host_us = 0, p_issue_us = 0;
+  double p_bytes_in = 0, p_bytes = 0;  // bytes into rank 0 from the other ranks; every rank's block
 };
 
 namespace {
@@ -193,6 +212,79 @@ namespace {
 rt_status cfail(rt_comm* c, rt_status st, const std::string& m) {
   if (c) c->err = m;
   return st;
+}
+
+// phase timing: an event with a timestamp (no system-scope fence: the host only reads the time)
+hipEvent_t phase_event(rt_comm* c) {
+  {
+    std::lock_guard<std::mutex> lk(c->pmu);
+    if (!c->pfree.empty()) {
+      hipEvent_t e = c->pfree.back();
+      c->pfree.pop_back();
+      return e;
+    }
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
+  return e;
+}
+
+// records the start of a span on s (null when phase timing is off or an event could not be had)
+hipEvent_t phase_begin(rt_comm* c, hipStream_t s) {
+  if (!c->phase) return nullptr;
+  hipEvent_t a = phase_event(c);
+  if (a && hipEventRecord(a, s) != hipSuccess) {
+    std::lock_guard<std::mutex> lk(c->pmu);
+    c->pfree.push_back(a);
+    return nullptr;
+  }
+  return a;
+}
+
+void phase_end(rt_comm* c, hipStream_t s, hipEvent_t a, int kind) {
+  if (!a) return;
+  hipEvent_t b = phase_event(c);
+  std::lock_guard<std::mutex> lk(c->pmu);
+  if (!b || hipEventRecord(b, s) != hipSuccess) {
+    c->pfree.push_back(a);
+    if (b) c->pfree.push_back(b);
+    return;
+  }
+  PhaseSpan sp;
+  sp.a = a;
+  sp.b = b;
+  sp.kind = kind;
+  c->ppend.push_back(sp);
+}
+
+// resolves the recorded spans into the sums: those complete (wait = false), or all of them (wait = true)
+void phase_collect(rt_comm* c, bool wait) {
+  std::lock_guard<std::mutex> lk(c->pmu);
+  std::deque<PhaseSpan> keep;
+  for (const PhaseSpan& sp : c->ppend) {
+    if (wait) (void)hipEventSynchronize(sp.b);
+    else if (hipEventQuery(sp.b) != hipSuccess) {
+      keep.push_back(sp);
+      continue;
+    }
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, sp.a, sp.b) == hipSuccess) {
+      c->p_ms[sp.kind] += ms;
+      c->p_n[sp.kind] += 1;
+    }
+    c->pfree.push_back(sp.a);
+    c->pfree.push_back(sp.b);
+  }
+  c->ppend.swap(keep);
+}
+
+void phase_reset(rt_comm* c) {
+  phase_collect(c, true);
+  std::lock_guard<std::mutex> lk(c->pmu);
+  for (int k = 0; k < kPhases; ++k) c->p_ms[k] = 0.0, c->p_n[k] = 0;
+  c->p_frames = c->p_calls = 0;
+  c->p_host_us = c->p_issue_us = 0.0;
+  c->p_bytes_in = c->p_bytes = 0.0;
 }
 
 rt_status nccl_fail(rt_comm* c, ncclResult_t r, const char* what) {
@@ -303,6 +395,7 @@ void issue_loop(rt_comm* c) {
       c->jobs.pop_front();
     }
     clk::time_point t0, t1, t2, t3;
+    const clk::time_point tp0 = c->phase ? clk::now() : clk::time_point();
     if (c->timing) t0 = clk::now();
     Slot& s = c->slots[j.slot];
     rt_status st = RT_OK;
@@ -312,8 +405,16 @@ void issue_loop(rt_comm* c) {
       msg = "rt_render_strips: render -> gather hand-off";
     }
     if (c->timing) t1 = clk::now();
+    // the span starts once the gather stream is past the render (the wait above): the gather's own time, with any
+    // wait for the other ranks' strips inside the collective
+    hipEvent_t pa = st == RT_OK ? phase_begin(c, c->stream) : nullptr;
     if (st == RT_OK) {
       const size_t count = (size_t)j.nframes * j.rows_per_rank * j.W * kStripBpp;  // every frame of the slot, one call
+      if (pa) {
+        std::lock_guard<std::mutex> lk(c->pmu);
+        c->p_bytes_in += (double)count * (c->nranks - 1);
+        c->p_bytes += (double)count * c->nranks;
+      }
       if (c->loopback) {
         // rank r's block (its first `count` bytes) to r x count in rank 0's buffer: ncclGather's layout
         const hipError_t e = hipMemcpy2DAsync(s.gathered, count, s.local, c->local_bytes, count, c->nranks,
@@ -331,6 +432,7 @@ void issue_loop(rt_comm* c) {
         }
       }
     }
+    phase_end(c, c->stream, pa, kPhaseGather);
     if (c->timing) t2 = clk::now();
     // the gather's completion, for the step's tail on the slot's render stream (issue_tail_job, caller thread)
     if (st == RT_OK && j.rs != c->stream && hipEventRecord(s.gathered_ev, c->stream) != hipSuccess) {
@@ -342,6 +444,10 @@ void issue_loop(rt_comm* c) {
       c->w_parts[0] += std::chrono::duration<double, std::micro>(t1 - t0).count();
       c->w_parts[1] += std::chrono::duration<double, std::micro>(t2 - t1).count();
       c->w_parts[2] += std::chrono::duration<double, std::micro>(t3 - t2).count();
+    }
+    if (c->phase) {
+      std::lock_guard<std::mutex> lk(c->pmu);
+      c->p_issue_us += std::chrono::duration<double, std::micro>(clk::now() - tp0).count();
     }
     {
       std::lock_guard<std::mutex> lk(c->mu);
@@ -387,8 +493,10 @@ rt_status issue_tail_job(rt_comm* c, const Job& j) {
     // rank r's block of the gathered slot holds its strips of every frame in turn: frame b starts b frames into it;
     // the slot's frames are assembled by one launch
     const size_t frame_bytes = (size_t)j.rows_per_rank * j.W * kStripBpp;
+    hipEvent_t pa = phase_begin(c, j.rs);
     const hipError_t e = rt::launch_assemble_frames(j.W, j.H, c->nranks, j.strip, s.gathered, j.frame_out, j.nframes,
                                                     frame_bytes, j.rs, j.nframes * j.rows_per_rank, kStripBpp);
+    phase_end(c, j.rs, pa, kPhaseAssembly);
     if (e != hipSuccess) return cfail(c, RT_E_HIP, std::string("rt_render_strips: assembly: ") + hipGetErrorString(e));
     for (uint32_t b = 0; b < j.nframes; ++b) s.asm_frames[b] = j.frame_out[b];
     s.asm_stream = j.rs;
@@ -528,6 +636,11 @@ void comm_free(rt_comm* c) {
   for (hipEvent_t j : c->join)
     if (j) (void)hipEventDestroy(j);
   if (c->xev) (void)hipEventDestroy(c->xev);
+  for (const PhaseSpan& sp : c->ppend) {
+    (void)hipEventDestroy(sp.a);
+    (void)hipEventDestroy(sp.b);
+  }
+  for (hipEvent_t e : c->pfree) (void)hipEventDestroy(e);
   delete c;
 }
 
@@ -671,6 +784,7 @@ rt_status rt_render_strips_frames(rt_comm_t c, uint32_t W, uint32_t H, uint32_t 
   if (st != RT_OK) return st;
   using clk = std::chrono::steady_clock;
   clk::time_point t0;
+  const clk::time_point tp0 = c->phase ? clk::now() : clk::time_point();
   if (c->timing) t0 = clk::now();
   auto lap = [&](int part) {
     if (!c->timing) return;
@@ -686,7 +800,7 @@ rt_status rt_render_strips_frames(rt_comm_t c, uint32_t W, uint32_t H, uint32_t 
   }
   if ((st = plan(c, W, H, strip_rows)) != RT_OK) return st;
   // every frame is validated (the scene may have changed since the slot's first frame)
-  if (!c->rows.empty() && (st = rt::check_dispatch(c->ctx, W, H, c->slots[0].local)) != RT_OK)
+  if (!c->rows.empty() && (st = rt::check_dispatch(c->ctx, W, H, c->slots[0].local, cameras != nullptr)) != RT_OK)
     return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));
   hipStream_t fs = nullptr;  // the caller's stream when it is not the slot's
   if (c->fill == 0) {  // a new slot: its first frame picks the render stream every frame of the slot uses
@@ -728,6 +842,7 @@ rt_status rt_render_strips_frames(rt_comm_t c, uint32_t W, uint32_t H, uint32_t 
   // frames fill..fill+nframes-1 of the slot, one launch per rendered rank: frame b's strips b frames into the
   // rank's block, on the slot's render stream
   const uint64_t frame_bytes = (uint64_t)c->rows_per_rank * W * kStripBpp;
+  hipEvent_t pa = phase_begin(c, c->cur.rs);
   for (size_t r = 0; r < c->lb_count.size(); ++r) {
     if (!c->lb_count[r]) continue;  // a rank with no rows (H < nranks x strip_rows) renders nothing
     if (c->lb_render_count && (r < c->lb_render_first || r >= c->lb_render_first + c->lb_render_count)) continue;
@@ -736,6 +851,7 @@ rt_status rt_render_strips_frames(rt_comm_t c, uint32_t W, uint32_t H, uint32_t 
                             kStripBpp, nframes, cameras, frame_bytes, c->rows_gen);
     if (st != RT_OK) return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));
   }
+  phase_end(c, c->cur.rs, pa, kPhaseRender);
   lap(1);
   for (uint32_t b = 0; b < nframes; ++b) {
     c->cur.frame_out[c->fill] = frames_out ? frames_out[b] : nullptr;
@@ -749,6 +865,13 @@ rt_status rt_render_strips_frames(rt_comm_t c, uint32_t W, uint32_t H, uint32_t 
   lap(5);
   if (st != RT_OK) return st;
   ++c->t_calls;
+  if (c->phase) {
+    phase_collect(c, false);  // keeps the pending list short (host queries only)
+    std::lock_guard<std::mutex> lk(c->pmu);
+    c->p_frames += nframes;
+    c->p_calls += 1;
+    c->p_host_us += std::chrono::duration<double, std::micro>(clk::now() - tp0).count();
+  }
   return RT_OK;
 }
 
@@ -770,6 +893,31 @@ rt_status rt_comm_set_batch(rt_comm_t c, uint32_t frames_per_gather) {
 }
 
 uint32_t rt_comm_batch(rt_comm_t c) { return c ? c->batch : 0; }
+
+rt_status rt_comm_set_phase_timing(rt_comm_t c, int on) {
+  if (!c) return RT_E_INVALID;
+  (void)hipSetDevice(c->device);
+  const rt_status st = drain(c);  // the issue thread reads the flag: no step in flight when it changes
+  if (st != RT_OK) return st;
+  phase_reset(c);
+  c->phase = on != 0;
+  return RT_OK;
+}
+
+rt_status rt_comm_phase_stats(rt_comm_t c, double* out, uint32_t n) {
+  if (!c || (!out && n)) return RT_E_INVALID;
+  (void)hipSetDevice(c->device);
+  const rt_status st = drain(c);  // every span recorded so far is on a stream that has drained
+  if (st != RT_OK) return st;
+  phase_collect(c, true);
+  std::lock_guard<std::mutex> lk(c->pmu);
+  const double v[RT_COMM_PHASE_COUNT] = {(double)c->p_frames, (double)c->p_n[kPhaseRender], c->p_ms[kPhaseRender],
+                                         (double)c->p_n[kPhaseGather], c->p_ms[kPhaseGather],
+                                         (double)c->p_n[kPhaseAssembly], c->p_ms[kPhaseAssembly], c->p_host_us,
+                                         (double)c->p_calls, c->p_issue_us, c->p_bytes_in, c->p_bytes};
+  std::memcpy(out, v, std::min<uint32_t>(n, RT_COMM_PHASE_COUNT) * sizeof(double));
+  return RT_OK;
+}
 
 rt_status rt_comm_loopback_render_ranks(rt_comm_t c, uint32_t first, uint32_t count) {
   if (!c) return RT_E_INVALID;

@@ -303,7 +303,7 @@ RT_HD float det_log2(float x) {
     e = e + 1;
   }
   float f = m - 1.0f;
-  float s = f / (2.0f + f);
+  float s = f * rcp_exact(2.0f + f);  // 2 + f in [1.7, 2.5]: rcp_exact's fast path, the IEEE 1 / (2 + f)
   float s2 = s * s;
   float p = 1.0f / 11.0f;
   p = p * s2 + 1.0f / 9.0f;

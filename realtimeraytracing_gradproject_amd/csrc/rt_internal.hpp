@@ -16,7 +16,7 @@ uint64_t ctx_next_rows_gen(rt_ctx* c);
 void* ctx_stream(rt_ctx* c);
 // rt_dispatch_rays' argument / scene checks and its launch with a device row list (rt_render_strips keeps its
 // rank's rows on the device and skips the host list's upload ring)
-rt_status check_dispatch(rt_ctx* c, uint32_t W, uint32_t H, const void* rgba8);
+rt_status check_dispatch(rt_ctx* c, uint32_t W, uint32_t H, const void* rgba8, bool cameras_given = false);
 // nframes (1 .. kMaxLaunchFrames) frames in one launch, frame z with camera buffer cams[64 z ..] (null: the
 // context's camera) into rgba8 + z * frame_stride bytes (0: nrows * W * out_bpp); out_bpp 4 = RGBA8, 3 = RGB8
 // (the strips of rt_comm)

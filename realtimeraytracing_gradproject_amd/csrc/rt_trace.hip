@@ -955,43 +955,60 @@ __device__ V3 face_world_normal(const HitInstance& hi, uint32_t prim) {
   return mat3_mul(hi.nrm, n);
 }
 
-// CalculateDirectLighting (Hit.hlsl:83-95).
-__device__ V3 direct_lighting(const FrameParams& fp, V3 P, V3 n, V3 albedo) {
-  V3 color = v3(0.0f, 0.0f, 0.0f);
-  for (uint32_t l = 0; l < fp.nlights; ++l) {
-    const LightRec& L = fp.lights[l];
-    const V3 lp = v3(L.position[0], L.position[1], L.position[2]);
-    const V3 lc = v3(L.color[0], L.color[1], L.color[2]);
-    const V3 to_light = neg(normalize(sub(lp, P)));
-    const float f = dot(n, to_light);
-    const float ti = maxf(0.0f, f * L.intensity);
-    color = add(color, muls(mul(albedo, lc), ti));
-  }
-  return color;
-}
+#ifndef RT_SURFACE_V
+#define RT_SURFACE_V 2  // ClosestHit's surface colour: 2 = one light loop, quotients as reciprocals (round 6)
+#endif
 
-// CalculatePBRShading (Hit.hlsl:97-174).
-__device__ V3 pbr_shading(const FrameParams& fp, V3 n, V3 cam, V3 P) {
+// ClosestHit's finalSurfaceColor = CalculateDirectLighting (Hit.hlsl:83-95) + CalculatePBRShading
+// (:97-174), pinned for float32 and mirrored bit for bit by oracle/rt_oracle.c osurface (round 6):
+//  * ONE loop over the lights: the direct term's -normalize(lp - P) and the PBR term's L and distance
+//    share one sqrt and one reciprocal (normalize is v * (1 / sqrt(dot v v)), length that same sqrt);
+//    the two sums keep their own accumulators and light order, and are added at the end as before;
+//  * the pixel's invariants (N, V, N.V, Smith's view term) out of the loop, the material's (a^2, k,
+//    F0, (1 - metallic) albedo / PI) evaluated once;
+//  * every quotient as a product with a reciprocal (rcp_exact: the IEEE 1.0f / x, bits and all):
+//    NDF = a2 * (1 / denom), Smith's light term NdotL * (1 / (NdotL (1 - k) + k)), the specular
+//    term F * ((NDF G) * (1 / (4 N.V N.L + 1e-4))), the tone map c * (1 / (c + 1)); the diffuse
+//    term (1 - F) * ((1 - metallic) albedo / PI).
+// Against the float64 restatement (oracle/np_reference.py) this changes nothing measurable (the
+// goldens' L-inf stays <= 1e-4); against the HLSL it is as faithful as the IEEE quotients were,
+// since DXC compiles HLSL divisions to reciprocal products itself.
+__device__ __forceinline__ float srcp(float x) { return rcp_exact(x); }
+
+__device__ V3 surface_ref(const FrameParams& fp, V3 P, V3 n, V3 cam) {
   const MaterialRec& m = fp.material;
   const V3 albedo = v3(m.albedo[0], m.albedo[1], m.albedo[2]);
-  const V3 N = neg(normalize(n));
-  const V3 V = normalize(sub(cam, P));
-  V3 L0 = v3(0.0f, 0.0f, 0.0f);
   const float r = m.roughness;
   const float a = r * r;
   const float a2 = a * a;
   const float rp1 = r + 1.0f;
   const float k = (rp1 * rp1) / 8.0f;
+  const float omk = 1.0f - k;
   const V3 F0 = v3(0.04f + m.metallic * (albedo.x - 0.04f), 0.04f + m.metallic * (albedo.y - 0.04f),
                    0.04f + m.metallic * (albedo.z - 0.04f));
+  const float km = 1.0f - m.metallic;
+  const V3 kdA = v3((km * albedo.x) / kPi, (km * albedo.y) / kPi, (km * albedo.z) / kPi);
+  const V3 N = neg(muls(n, srcp(sqrtf(dot(n, n)))));
+  const V3 Vd = sub(cam, P);
+  const V3 V = muls(Vd, srcp(sqrtf(dot(Vd, Vd))));
+  const float NdotV = maxf(dot(N, V), 0.0f);
+  const float ggx2 = NdotV * srcp(NdotV * omk + k);
+  const float v4 = 4.0f * NdotV;
+  V3 cd = v3(0.0f, 0.0f, 0.0f), L0 = v3(0.0f, 0.0f, 0.0f);
   for (uint32_t l = 0; l < fp.nlights; ++l) {
     const LightRec& Lr = fp.lights[l];
     const V3 lp = v3(Lr.position[0], Lr.position[1], Lr.position[2]);
     const V3 lc = v3(Lr.color[0], Lr.color[1], Lr.color[2]);
-    const V3 L = normalize(sub(lp, P));
-    const V3 H = normalize(add(V, L));
-    const float dist = length(sub(lp, P));
-    const float att = sh_rcp(maxf(dist * dist, 1.0f));
+    const V3 dv = sub(lp, P);
+    const float dist = sqrtf(dot(dv, dv));
+    const V3 L = muls(dv, srcp(dist));
+    // CalculateDirectLighting
+    const float ti = maxf(0.0f, dot(n, neg(L)) * Lr.intensity);
+    cd = add(cd, muls(mul(albedo, lc), ti));
+    // CalculatePBRShading
+    const V3 Hd = add(V, L);
+    const V3 H = muls(Hd, srcp(sqrtf(dot(Hd, Hd))));
+    const float att = srcp(maxf(dist * dist, 1.0f));
     const V3 radiance = muls(lc, att);
     const float x = clamp01(1.0f - maxf(dot(H, V), 0.0f));
     const float x2 = x * x;
@@ -1001,24 +1018,19 @@ __device__ V3 pbr_shading(const FrameParams& fp, V3 n, V3 cam, V3 P) {
     const float NdotH2 = NdotH * NdotH;
     float denom = NdotH2 * (a2 - 1.0f) + 1.0f;
     denom = (kPi * denom) * denom;
-    const float NDF = a2 / denom;
-    const float NdotV = maxf(dot(N, V), 0.0f);
+    const float NDF = a2 * srcp(denom);
     const float NdotL = maxf(dot(N, L), 0.0f);
-    const float ggx2 = NdotV / (NdotV * (1.0f - k) + k);
-    const float ggx1 = NdotL / (NdotL * (1.0f - k) + k);
+    const float ggx1 = NdotL * srcp(NdotL * omk + k);
     const float G = ggx1 * ggx2;
-    const V3 numerator = muls(F, NDF * G);
-    const float denominator = (4.0f * NdotV) * NdotL + 0.0001f;
-    const V3 spec = v3(numerator.x / denominator, numerator.y / denominator, numerator.z / denominator);
-    const float km = 1.0f - m.metallic;
-    const V3 kD = v3((1.0f - F.x) * km, (1.0f - F.y) * km, (1.0f - F.z) * km);
-    const V3 diff = v3((kD.x * albedo.x) / kPi, (kD.y * albedo.y) / kPi, (kD.z * albedo.z) / kPi);
+    const float sp = (NDF * G) * srcp(v4 * NdotL + 0.0001f);
+    const V3 spec = muls(F, sp);
+    const V3 diff = v3((1.0f - F.x) * kdA.x, (1.0f - F.y) * kdA.y, (1.0f - F.z) * kdA.z);
     L0 = add(L0, muls(mul(add(diff, spec), radiance), NdotL));
   }
   V3 c = muls(L0, 0.2f);
-  c = v3(c.x / (c.x + 1.0f), c.y / (c.y + 1.0f), c.z / (c.z + 1.0f));
+  c = v3(c.x * srcp(c.x + 1.0f), c.y * srcp(c.y + 1.0f), c.z * srcp(c.z + 1.0f));
   const float g = 1.0f / 2.2f;
-  return v3(det_pow(c.x, g), det_pow(c.y, g), det_pow(c.z, g));
+  return add(cd, v3(det_pow(c.x, g), det_pow(c.y, g), det_pow(c.z, g)));
 }
 
 template <bool STATS>
@@ -1070,7 +1082,6 @@ template <bool STATS>
 __device__ V3 shade_ref(const SceneView& sc, const FrameParams& fp, uint32_t py, V3 O, V3 D, bool f, HitRec hit,
                         const LaneStack& stk, Counters& cnt) {
   const float refl = fp.material.reflectivity;
-  const V3 albedo = v3(fp.material.albedo[0], fp.material.albedo[1], fp.material.albedo[2]);
   V3 sk[kMaxReflectDepth];
   V3 ro = O, rd = D;
   for (int depth = 0;; ++depth) {
@@ -1093,7 +1104,7 @@ __device__ V3 shade_ref(const SceneView& sc, const FrameParams& fp, uint32_t py,
         term = v3(c, c, c);
       } else {
         const V3 n = interpolated_world_normal(ir, hit.prim, hit.u, hit.v);
-        const V3 s = add(direct_lighting(fp, P, n, albedo), pbr_shading(fp, n, ro, P));
+        const V3 s = surface_ref(fp, P, n, ro);
         if (reflective(fp, ir, depth)) {
           sk[depth] = s;
           reflection_ray(P, n, rd, ro, rd);
@@ -1244,7 +1255,6 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
     // shade_ref level by level for the whole packet: each level's shadow rays and next
     // reflection rays are one packet each (mirrored by oracle osample_packet)
     const float refl = fp.material.reflectivity;
-    const V3 albedo = v3(fp.material.albedo[0], fp.material.albedo[1], fp.material.albedo[2]);
     V3 ro[R], rd[R], ldir[R], nf[R];
     V3 sk[R][kMaxReflectDepth];  // surface colours of the reflective levels (unwound innermost first)
     bool act[R], nxt[R];
@@ -1277,7 +1287,7 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
             continue;
           }
           const V3 n = interpolated_world_normal(ir, hit[r].prim, hit[r].u, hit[r].v);
-          const V3 s = add(direct_lighting(fp, P[r], n, albedo), pbr_shading(fp, n, ro[r], P[r]));
+          const V3 s = surface_ref(fp, P[r], n, ro[r]);
           if (MODE == 0 && reflective(fp, ir, depth)) {
             sk[r][depth] = s;
             reflection_ray(P[r], n, rd[r], ro[r], rd[r]);

@@ -263,6 +263,41 @@ def test_abort_with_partly_filled_batch_returns(loop):
     c.close()
 
 
+def test_unclosed_communicator_garbage_collected(recwarn):
+    """a loopback communicator dropped unclosed drains like close() — the frames already handed to
+    render_strips (2 of a 3-frame batch) are rendered and assembled; an RCCL one aborts (peers may never match a
+    draining gather) and warns that it discarded pending frames."""
+    import gc
+    size = (960, 544)
+    W, H = size
+    c = rt.Context(0)
+    scenes.upload(c, _spec(size, 0))
+    comm = rt.Comm.loopback(c, 8)
+    comm.set_batch(3)
+    frames = [torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    torch.cuda.synchronize()  # the zero fill (torch's stream) before the communicator's own streams write
+    for k in range(2):
+        c.set_camera(_spec(size, k + 1).camera_buffer())
+        comm.render_strips(W, H, frames[k], None)
+    del comm
+    gc.collect()
+    torch.cuda.synchronize()
+    _check(frames, size, [1, 2], "loopback dropped unclosed")
+    assert not [w for w in recwarn if issubclass(w.category, ResourceWarning)]
+    comm = rt.Comm(c, 1, 0, rt.comm_unique_id())
+    comm.set_batch(3)
+    comm.render_strips(W, H, frames[0], None)
+    with pytest.warns(ResourceWarning, match="close"):
+        comm.__del__()
+    del comm
+    out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+    c.set_camera(_spec(size, 3).camera_buffer())
+    c.dispatch(W, H, out, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    _check([out], size, [3], "after the RCCL abort")
+    c.close()
+
+
 def test_many_emulated_ranks_never_synchronise_the_device():
     """every emulated rank's row list is its own tile-balance shape, so 40 ranks exceed the context's table
     of cost maps. A full table must not cost a device-wide synchronisation per launch (it used to evict with

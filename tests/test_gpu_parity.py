@@ -417,7 +417,7 @@ def test_trace_rays_equals_bruteforce(any_hit, cull):
     d_rays = torch.from_numpy(rays).cuda()
     d_hits = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
     d_uv = torch.zeros((n, 2), dtype=torch.float32, device="cuda")
-    c.trace_rays(d_rays, n, any_hit, d_hits, d_uv, cull_back=cull)
+    c.trace_rays(d_rays, n, any_hit, d_hits, d_uv, cull_back=cull, stream=torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     g = d_hits.cpu().numpy().view(np.uint32)
     guv = d_uv.cpu().numpy()
@@ -463,7 +463,7 @@ def test_large_soup_multi_kernel_build_and_trace(any_hit):
     d_rays = torch.from_numpy(rays).cuda()
     d_hits = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
     d_uv = torch.zeros((n, 2), dtype=torch.float32, device="cuda")
-    c.trace_rays(d_rays, n, any_hit, d_hits, d_uv)
+    c.trace_rays(d_rays, n, any_hit, d_hits, d_uv, stream=torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     g = d_hits.cpu().numpy().view(np.uint32)
     oh, ouv, _ = o.trace_rays(rays, any_hit=any_hit)
@@ -489,7 +489,7 @@ def test_trace_rays_degenerate_and_transformed(any_hit, cull):
     d_rays = torch.from_numpy(rays).cuda()
     d_hits = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
     d_uv = torch.zeros((n, 2), dtype=torch.float32, device="cuda")
-    c.trace_rays(d_rays, n, any_hit, d_hits, d_uv, cull_back=cull == "back", cull_front=cull == "front")
+    c.trace_rays(d_rays, n, any_hit, d_hits, d_uv, cull_back=cull == "back", cull_front=cull == "front", stream=torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     g = d_hits.cpu().numpy().view(np.uint32)
     guv = d_uv.cpu().numpy()

@@ -141,7 +141,7 @@ def test_random_scene_trace_rays_equal_oracle(seed):
                                                (False, False, True)]:
             d_hits = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
             d_uv = torch.zeros((n, 2), dtype=torch.float32, device="cuda")
-            c.trace_rays(d_rays, n, any_hit, d_hits, d_uv, cull_back=cull_back, cull_front=cull_front)
+            c.trace_rays(d_rays, n, any_hit, d_hits, d_uv, cull_back=cull_back, cull_front=cull_front, stream=torch.cuda.current_stream().cuda_stream)
             torch.cuda.synchronize()
             g = d_hits.cpu().numpy().view(np.uint32)
             ob, ouv, _ = o.trace_rays(rays, any_hit=any_hit, cull_back=cull_back, cull_front=cull_front)

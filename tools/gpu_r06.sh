@@ -1,0 +1,71 @@
+#!/bin/bash
+# One GPU call of a round-6 session (run on the GPU box from the repo root). STEPS selects: tests, bench, strips5,
+# shares, balance, waves. Each step under its own time limit; the script stops at the first failure.
+#   STEPS="tests bench" TAG=r06a bash tools/gpu_r06.sh
+set -u
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+TAG="${TAG:-r06}"
+O="$R/gpurun_out"
+mkdir -p "$O"
+cd "$R"
+for step in ${STEPS:-tests}; do
+  case $step in
+    tests)
+      timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} \
+        > "$O/gputest_${TAG}.log" 2>&1 || { echo "gpu tests failed rc=$?"; grep -E "FAIL|Error|error" "$O/gputest_${TAG}.log" | head -20; tail -40 "$O/gputest_${TAG}.log"; exit 1; }
+      tail -3 "$O/gputest_${TAG}.log" ;;
+    bench)
+      timeout -k 10 600 python3 bench.py ${BENCH_ARGS:-} > "$O/bench_${TAG}.json" 2> "$O/bench_${TAG}.err" \
+        || { echo "bench failed rc=$?"; tail -20 "$O/bench_${TAG}.err"; exit 1; }
+      head -c 1500 "$O/bench_${TAG}.json"; echo ;;
+    strips5)
+      # the C5 (4 spp, 4K) and C4 tiled loops through the loopback transport
+      for cfg in "C5 8" "C4 4"; do
+        set -- $cfg
+        timeout -k 10 300 python3 bench.py --mode strips --loopback $2 --config $1 --extra= --no-cpu-baseline \
+          --steps ${STRIPS_STEPS:-40} --warmup 8 \
+          > "$O/strips_${1}_lb${2}_${TAG}.json" 2> "$O/strips_${1}_lb${2}_${TAG}.err" \
+          || { echo "strips loopback $1 $2 failed rc=$?"; tail -20 "$O/strips_${1}_lb${2}_${TAG}.err"; exit 1; }
+        head -c 900 "$O/strips_${1}_lb${2}_${TAG}.json"; echo
+      done ;;
+    shares)
+      timeout -k 10 900 python3 -u tools/share_ceiling.py ${SHARE_ARGS:-} > "$O/shares_${TAG}.jsonl" 2> "$O/shares_${TAG}.err" \
+        || { echo "share_ceiling failed rc=$?"; tail -20 "$O/shares_${TAG}.err"; exit 1; }
+      cat "$O/shares_${TAG}.jsonl" ;;
+    libab)
+      timeout -k 10 900 python3 tools/lib_ab.py --roots ${AB_ROOTS:-ab/r03,.,.:bal0} --configs ${AB_CONFIGS:-C2,C2F,C4} \
+        --rounds ${AB_ROUNDS:-5} > "$O/libab_${TAG}.txt" 2>&1 || { echo "lib_ab failed rc=$?"; tail -20 "$O/libab_${TAG}.txt"; exit 1; }
+      tail -40 "$O/libab_${TAG}.txt" ;;
+    prof)
+      CFGS="${PROF_CFGS:-C2 C4 C5}" TAG="$TAG" bash tools/profile_round.sh || { echo "profile_round failed"; exit 1; } ;;
+    sqc)
+      # scalar data cache hit rate of the trace kernel (one pass; counters of the SQC block only)
+      cd /tmp && export TMPDIR=/tmp
+      timeout -s KILL 90 rocprofv3 --pmc ${SQC_SET:-SQC_DCACHE_REQ SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_DCACHE_MISSES_DUPLICATE} \
+        --kernel-include-regex k_trace_frame -d "$O/sqc_${TAG}" -o run --output-format csv \
+        -- python3 "$R/tools/one_config.py" --config ${SQC_CONFIG:-C2} --frames 12 > "$O/sqc_${TAG}.log" 2>&1 \
+        || { echo "sqc pass failed rc=$?"; tail -20 "$O/sqc_${TAG}.log"; exit 1; }
+      cd "$R"; find "$O/sqc_${TAG}" -name "*counter_collection.csv" | head -1 | xargs -r tail -5 ;;
+    occ)
+      timeout -k 10 120 ./tools/bin/occupancy_probe > "$O/occupancy_${TAG}.jsonl" 2>&1 \
+        || { echo "occupancy_probe failed rc=$?"; tail -20 "$O/occupancy_${TAG}.jsonl"; exit 1; }
+      cat "$O/occupancy_${TAG}.jsonl" ;;
+    ab)
+      # one-process interleaved A/B of library variants (tools/ab.py; AB_VARIANTS name=lib ...)
+      timeout -k 10 900 python3 tools/ab.py ${AB_ARGS:-} ${AB_VARIANTS} > "$O/ab_${TAG}.txt" 2>&1 \
+        || { echo "ab failed rc=$?"; tail -20 "$O/ab_${TAG}.txt"; exit 1; }
+      tail -40 "$O/ab_${TAG}.txt" ;;
+    balance)
+      timeout -k 10 600 python3 tools/balance_ab.py ${BAL_ARGS:-} > "$O/balance_${TAG}.txt" 2>&1 \
+        || { echo "balance_ab failed rc=$?"; tail -20 "$O/balance_${TAG}.txt"; exit 1; }
+      cat "$O/balance_${TAG}.txt" ;;
+    waves)
+      for b in ${WT_BAL:-0 1}; do
+        timeout -k 10 120 python3 tools/wave_times.py --lib ${WT_LIB:-realtimeraytracing_gradproject_amd/lib/variants/wavetimes/librtamd.so} \
+          --config ${WT_CONFIG:-C4} --balance $b ${WT_ARGS:-} > "$O/wave_times_${TAG}_b$b.txt" 2>&1 \
+          || { echo "wave_times failed rc=$?"; tail -20 "$O/wave_times_${TAG}_b$b.txt"; exit 1; }
+        cat "$O/wave_times_${TAG}_b$b.txt"
+      done ;;
+  esac
+done
+exit 0

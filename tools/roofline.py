@@ -130,6 +130,9 @@ def load_line(path):
 
 
 def check(path):
+    """Recomputes every roofline field of a bench line and enforces the pairing: `frac` is the
+    `bound` pipe's fraction, `bound` the largest fraction, achieved / peak == frac for the top-level pipe and every
+    pipe under `pipes`, `l2_frac` the fetched bytes over the L2 roof, `logical_bytes` SURVEY §8(d)'s per-lane model."""
     import bench
     from realtimeraytracing_gradproject_amd import scenes
     d = load_line(path)
@@ -138,16 +141,30 @@ def check(path):
     spec = scenes.config(name)
     pixels = spec.width * spec.height
     st = {"node_fetches": rf["node_fetches"], "tri_fetches": rf["tri_fetches"],
-          "instance_fetches": rf["instance_fetches"], "primary_rays": d["config"]["primary_rays"]}
+          "instance_fetches": rf["instance_fetches"], "primary_rays": d["config"]["primary_rays"],
+          "aabb_tests": rf["aabb_tests"], "tri_tests": rf["tri_tests"]}
     b = bench.fetched_bytes(st, pixels)
     ach = b / (rf["kernel_ms"] * 1e-3) / 1e9
     problems = []
     if b != rf["bytes_per_launch"]:
         problems.append(f"bytes_per_launch {rf['bytes_per_launch']} != {b}")
-    if abs(ach - rf["achieved"]) > 0.05 + 1e-3 * ach:  # kernel_ms is rounded to 4 decimals in the line
-        problems.append(f"achieved {rf['achieved']} != {ach:.1f}")
-    if abs(rf["frac"] - ach / L2_PEAK_GBS) > 1e-3:
-        problems.append(f"frac {rf['frac']} != {ach / L2_PEAK_GBS:.4f}")
+    pipes = rf.get("pipes", {})
+    l2 = pipes.get("l2", {})
+    if abs(l2.get("achieved", -1) - ach) > 0.05 + 1e-3 * ach:  # kernel_ms is rounded to 4 decimals in the line
+        problems.append(f"l2 achieved {l2.get('achieved')} != {ach:.1f}")
+    if abs(rf.get("l2_frac", -1) - ach / L2_PEAK_GBS) > 1e-3:
+        problems.append(f"l2_frac {rf.get('l2_frac')} != {ach / L2_PEAK_GBS:.4f}")
+    fr = dict(rf.get("fracs", {}))
+    if not fr or rf["bound"] != max(fr, key=fr.get):
+        problems.append(f"bound {rf['bound']} is not the largest fraction {fr}")
+    elif abs(rf["frac"] - fr[rf["bound"]]) > 1e-4:
+        problems.append(f"frac {rf['frac']} is not the bound pipe's {fr[rf['bound']]}")
+    top = pipes.get(rf["bound"], {})
+    if (rf["achieved"], rf["peak"], rf["unit"]) != (top.get("achieved"), top.get("peak"), top.get("unit")):
+        problems.append(f"achieved / peak / unit are not the bound pipe's ({top})")
+    for k, v in pipes.items():
+        if v["peak"] and abs(v["achieved"] / v["peak"] - v["frac"]) > 2e-3 * max(1.0, v["frac"]):
+            problems.append(f"pipe {k}: achieved / peak {v['achieved'] / v['peak']:.4f} != frac {v['frac']}")
     if rf["frac"] > 1:
         problems.append("frac > 1")
     prof = bench.load_profile(name) or {}
@@ -157,14 +174,16 @@ def check(path):
         for k in ("salu_frac", "valu_frac"):
             if rf["issue"][k] != prof["issue"][k]:
                 problems.append(f"issue.{k} {rf['issue'][k]} != profiles {prof['issue'][k]}")
-    fr = dict(rf.get("fracs", {}))
-    if fr and rf["bound"] != max(fr, key=fr.get):
-        problems.append(f"bound {rf['bound']} is not the largest fraction {fr}")
+            if pipes.get(k[:4], {}).get("frac") != round(prof["issue"][k], 4):
+                problems.append(f"pipes.{k[:4]}.frac != profiles issue.{k}")
+    lb = bench.logical_bytes(st, pixels)
+    if rf.get("logical_bytes", {}).get("bytes_per_launch") != lb:
+        problems.append(f"logical_bytes {rf.get('logical_bytes')} != {lb}")
     rk = prof.get("rocprof_kernel_avg_ms")
     agree = None if not rk else round(rf["kernel_ms"] / rk, 3)
     print(json.dumps({"bench": path, "config": name, "bytes_per_launch": b, "achieved_GBs": round(ach, 1),
-                      "frac_l2": round(ach / L2_PEAK_GBS, 4), "bound": rf["bound"], "fracs": fr,
-                      "bench_kernel_ms_over_rocprof": agree, "problems": problems}, indent=1))
+                      "l2_frac": round(ach / L2_PEAK_GBS, 4), "bound": rf["bound"], "frac": rf["frac"], "fracs": fr,
+                      "logical_bytes": lb, "bench_kernel_ms_over_rocprof": agree, "problems": problems}, indent=1))
     return 1 if problems else 0
 
 
