@@ -96,6 +96,9 @@ def parse(argv=None):
                    help="N>1: strips = one frame tiled over ranks + RCCL gather (default); frames = N "
                         "independent replicas (no collective)")
     p.add_argument("--no-pipeline", action="store_true", help="strips: gather after each frame, no overlap")
+    p.add_argument("--phase-frames", type=int, default=64,
+                   help="strips through the native loop: frames of the per-phase pass after the timed region "
+                        "(config.phases; 0: none)")
     p.add_argument("--frames-per-gather", type=int, default=4,
                    help="strips through the native loop: consecutive frames whose strips one ncclGather moves "
                         "(rt_comm_set_batch; the gather half of a step is paid once per this many frames)")
@@ -396,7 +399,7 @@ def run_config(*args, **kw):
 def _run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle_ms: float, strips: bool,
                 pipeline: bool, schedule: str, save_image: str = "", in_flight: int = 0, resettle_ms: float = 0.0,
                 frames_per_gather: int = 1, frames_per_launch: int = 0, loopback: int = 0, latency_frames: int = 20,
-                held: dict = None):
+                phase_frames: int = 0, held: dict = None):
     from realtimeraytracing_gradproject_amd import distributed as D
     distributed = world > 1
     W, H = spec.width, spec.height
@@ -615,6 +618,24 @@ def _run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle
                 lat.append(time.perf_counter() - t1)
         latency_ms = float(np.median(lat)) * 1e3
 
+    # per-phase cost of a step (the N > 1 line names its own binding cost), untimed for `value`: the
+    # timed loop's batching and streams again, with the communicator's timing-event pairs around each render, gather
+    # and assembly (rt_comm_set_phase_timing), over the wall clock of the pass
+    phases = None
+    if native and phase_frames > 0:
+        rcomm.set_batch(fpg)
+        rcomm.set_phase_timing(True)
+        if distributed:
+            dist.barrier()
+        be.synchronize()
+        t1 = time.perf_counter()
+        issue_native(phase_frames, fpl)
+        ps = rcomm.phase_stats()  # drains the pipeline
+        be.synchronize()
+        wall = time.perf_counter() - t1
+        rcomm.set_phase_timing(False)
+        phases = phase_summary(ps, wall, world, rank, loopback, distributed, be.device)
+
     if save_image and rank == 0:
         last = (ncall[0] - 1) % rcomm.depth if native else (k - 1) % nslot
         if native:
@@ -628,6 +649,7 @@ def _run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle
     tb = be.tile_balance() if hasattr(be, "tile_balance") else None
     return {"rays_step": rays_step, "primary": int(counts[1].item()), "shadow": int(counts[2].item()), "fpg": fpg,
             "fpl": fpl if native else None, "latency_ms": latency_ms, "loopback": loopback if native else 0,
+            "phases": phases,
             "tile_balance": tb,
             "tmax": tmax, "kernel_ms": kernel_ms, "stats": st, "build": build, "rows_local": len(rows) if rows is not None else H,
             "tile_rows": tile_rows, "tile_ms": tile_ms, "in_flight": nstream, "in_flight_ms": flight_ms,
@@ -642,6 +664,38 @@ def _run_config(be, spec, world: int, rank: int, steps: int, warmup: int, settle
 # ---------------------------------------------------------------------------------------------
 # roofline
 # ---------------------------------------------------------------------------------------------
+
+def phase_summary(ps: dict, wall_s: float, world: int, rank: int, loopback: int, distributed: bool, device) -> dict:
+    """Per-frame phases of the native strips loop on this rank (rank 0's line): the render of its share (loopback:
+    every emulated rank's share, one GPU renders them all), the gather (gather stream, from this rank's render done to
+    the gather's end: the transfer plus any wait for the other ranks), rank 0's assembly, the host's issue (caller
+    thread per frame, the library's issue thread per frame), the bytes into rank 0 and their rate over the gather
+    time, the pass's period; the render share's max / min over the ranks (all-reduce)."""
+    f = max(ps["frames"], 1.0)
+    render = ps["render_ms"] / f
+    rr = torch.tensor([render, -render], dtype=torch.float64, device=device)
+    if distributed:
+        dist.all_reduce(rr, op=dist.ReduceOp.MAX)
+    period = wall_s * 1e3 / f
+    gather = ps["gather_ms"] / f
+    asm = ps["assembly_ms"] / f
+    out = {"frames": int(ps["frames"]), "period_ms": round(period, 4),
+           "render_share_ms": round(render, 4),
+           "render_share_ms_max": round(float(rr[0].item()), 4), "render_share_ms_min": round(float(-rr[1].item()), 4),
+           "render_launches_per_frame": round(ps["renders"] / f, 3),
+           "gather_ms": round(gather, 4), "assembly_ms": round(asm, 4),
+           "host_issue_us": round(ps["host_us"] / f, 2), "issue_thread_us": round(ps["issue_us"] / f, 2),
+           "bytes_into_rank0_per_frame": int(ps["bytes_in"] / f),
+           "ingress_GBps_over_gather": (round(ps["bytes_in"] / (ps["gather_ms"] * 1e-3) / 1e9, 3)
+                                        if ps["gather_ms"] > 0 else None),
+           "ingress_GBps_at_period": round(ps["bytes_in"] / f / (period * 1e-3) / 1e9, 3) if period > 0 else None,
+           "phase_sum_over_period": round((render + gather + asm) / period, 3) if period > 0 else None,
+           "rank": rank, "world": world, "loopback_ranks": loopback or None,
+           "note": ("loopback: one GPU renders every emulated rank's share (render_share_ms is their sum) and the "
+                    "gather is a device copy" if loopback else
+                    "this rank's share; gather = ncclGather from this rank's render done to its end")}
+    return out
+
 
 def lib_sha() -> str:
     p = os.path.join(ROOT, "realtimeraytracing_gradproject_amd", "lib", "librtamd.so")
@@ -897,7 +951,7 @@ def main(argv=None) -> int:
     spec = spec_of(a.config)
     r = run_config(be, spec, world, rank, a.steps, a.warmup, a.settle_ms, strips, not a.no_pipeline, a.schedule,
                    a.save_image, a.in_flight, a.resettle_ms, a.frames_per_gather, a.frames_per_launch, a.loopback,
-                   a.latency_frames)
+                   a.latency_frames, a.phase_frames)
 
     extra = []
     names = a.extra if a.extra is not None else ("C4,C5" if distributed else "C1,C2F,C3,C4,C5,REF")
@@ -959,6 +1013,8 @@ def main(argv=None) -> int:
                        # SURVEY 8(d)'s frame latency in strips mode: enqueue -> assembled on rank 0, gather included,
                        # one frame per gather, one at a time (the batched throughput is `value`)
                        "frame_latency_ms": None if r["latency_ms"] is None else round(r["latency_ms"], 4),
+                       # what a step costs per phase on rank 0 (native strips loop; null otherwise)
+                       "phases": r["phases"],
                        "schedule": a.schedule,
                        "tile_rows": r["tile_rows"], "tile_ms_rank0": r["tile_ms"],
                        "frames_in_flight": r["in_flight"], "in_flight_ms_rank0": r["in_flight_ms"],

@@ -382,7 +382,7 @@ rt_status rt_comm_set_batch(rt_comm_t comm, uint32_t frames_per_gather);
 uint32_t rt_comm_batch(rt_comm_t comm);
 /* Phase timing of the loop on this rank (diagnostics for the multi-GPU bench line; no reference counterpart — the
  * reference has no multi-GPU path, its frame spans submit -> fence, D3D12HelloTriangle.cpp:436-470). When on, each
- * step records timing-event pairs around its render launch(es) (render stream), its gather (gather stream: from the
+ * step records timing-event pairs around its render launches (render stream; every emulated rank's on a loopback), its gather (gather stream: from the
  * moment this rank's render is done to the gather's end, any wait for the other ranks inside the collective
  * included) and rank 0's assembly, and the host time of each rt_render_strips* call and of the issue thread's work.
  * Drains the pipeline (like rt_comm_set_batch: every rank between the same calls) and resets the sums. */

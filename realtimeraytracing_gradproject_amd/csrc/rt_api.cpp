@@ -225,6 +225,7 @@ struct BalanceMap {
   std::vector<hipStream_t> readers;  // streams that launched with the current list since it became current
   ScratchSlot forgotten;             // events on streams dropped by rt_forget_stream (their launches may still run)
   bool recycled = false, recycled_planned = false;  // reused for this shape; a plan has started on it since
+  uint32_t nopay_run = 0;            // consecutive completed plans whose list did not pay (re-check back-off)
   void release() {
     if (cost) (void)hipFree(cost);
     if (stats) (void)hipHostFree(stats);
@@ -1161,6 +1162,7 @@ static BalanceMap* balance_map(rt_ctx* c, uint32_t W, uint32_t nrows, const uint
     m->streams.clear();
     m->recycled = true;
     m->recycled_planned = false;
+    m->nopay_run = 0;
   }
   m->W = W;
   m->nrows = nrows;
@@ -1203,6 +1205,10 @@ static BalanceMap* balance_map(rt_ctx* c, uint32_t W, uint32_t nrows, const uint
 // camera); otherwise the launches take the plain grid and one in kRecheck plans again. One plan at a time per
 // shape. The summary is read from host-mapped memory without a copy call (it may lag: any list is a valid cover).
 constexpr uint64_t kReplan = 8, kRecheck = 32, kRecheckNoTail = 128;
+// a shape whose plans keep finding nothing to gain (C2: 17 plans, none paid, in one bench run) doubles
+// its re-check interval after each such plan, up to 2^kNoPayBackoff times the base (128 -> 4096 launches for C2);
+// one plan that pays resets it
+constexpr uint32_t kNoPayBackoff = 5;
 
 // record: whether the launch's waves record their times. A shape whose list does not pay runs the plain kernel
 // and records only on the launch before a re-check (the plan reads those times).
@@ -1223,7 +1229,9 @@ static void balance_wants_plan(BalanceMap& m, bool* plan, bool* use, bool* recor
   }
   const uint64_t age = m.launches - m.planned_at;
   *use = st->pays != 0;
-  const uint64_t every = *use ? kReplan : ((st->threshold == 0xffffffffu || st->coherent) ? kRecheckNoTail : kRecheck);
+  const uint64_t base = (st->threshold == 0xffffffffu || st->coherent) ? kRecheckNoTail : kRecheck;
+  const uint32_t back = m.nopay_run > 1u ? std::min(m.nopay_run - 1u, kNoPayBackoff) : 0u;
+  const uint64_t every = *use ? kReplan : base << back;
   *plan = may_plan && age >= every;
   // a launch with a list runs the recording kernel anyway; otherwise only the launch before a re-check records
   // (not every launch issued while a plan is pending: a host running far ahead issues many of those)
@@ -1327,6 +1335,9 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
         m->cur = m->pending;
         m->cur_items = m->pending_items;
         m->pending = -1;
+        // the plan just landed (its event completed: its host-mapped summary is visible)
+        const volatile rt::PlanStats* ps = m->stats;
+        m->nopay_run = ps->pays ? 0u : m->nopay_run + 1u;
       }
       if (active && !forced) balance_wants_plan(*m, &plan, &use, &record);
       c->fp.cost = record ? m->cost : nullptr;

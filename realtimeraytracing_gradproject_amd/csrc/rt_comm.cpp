@@ -202,7 +202,7 @@ struct rt_comm {
   std::deque<PhaseSpan> ppend;    // recorded spans not yet resolved
   double p_ms[kPhases] = {0, 0, 0};
   uint64_t p_n[kPhases] = {0, 0, 0};
-  uint64_t p_frames = 0, p_calls = 0;
+  uint64_t p_frames = 0, p_calls = 0, p_launches = 0;
   double p_host_us = 0, p_issue_us = 0;
   double p_bytes_in = 0, p_bytes = 0;  // bytes into rank 0 from the other ranks; every rank's block
 };
@@ -282,7 +282,7 @@ void phase_reset(rt_comm* c) {
   phase_collect(c, true);
   std::lock_guard<std::mutex> lk(c->pmu);
   for (int k = 0; k < kPhases; ++k) c->p_ms[k] = 0.0, c->p_n[k] = 0;
-  c->p_frames = c->p_calls = 0;
+  c->p_frames = c->p_calls = c->p_launches = 0;
   c->p_host_us = c->p_issue_us = 0.0;
   c->p_bytes_in = c->p_bytes = 0.0;
 }
@@ -843,6 +843,7 @@ rt_status rt_render_strips_frames(rt_comm_t c, uint32_t W, uint32_t H, uint32_t 
   // rank's block, on the slot's render stream
   const uint64_t frame_bytes = (uint64_t)c->rows_per_rank * W * kStripBpp;
   hipEvent_t pa = phase_begin(c, c->cur.rs);
+  uint32_t launches = 0;
   for (size_t r = 0; r < c->lb_count.size(); ++r) {
     if (!c->lb_count[r]) continue;  // a rank with no rows (H < nranks x strip_rows) renders nothing
     if (c->lb_render_count && (r < c->lb_render_first || r >= c->lb_render_first + c->lb_render_count)) continue;
@@ -850,6 +851,7 @@ rt_status rt_render_strips_frames(rt_comm_t c, uint32_t W, uint32_t H, uint32_t 
     st = rt::dispatch_frame(c->ctx, W, H, c->d_rows + c->lb_first[r], c->lb_count[r], dst, nullptr, c->cur.rs,
                             kStripBpp, nframes, cameras, frame_bytes, c->rows_gen);
     if (st != RT_OK) return cfail(c, st, std::string("rt_render_strips: ") + rt_last_error(c->ctx));
+    ++launches;
   }
   phase_end(c, c->cur.rs, pa, kPhaseRender);
   lap(1);
@@ -870,6 +872,7 @@ rt_status rt_render_strips_frames(rt_comm_t c, uint32_t W, uint32_t H, uint32_t 
     std::lock_guard<std::mutex> lk(c->pmu);
     c->p_frames += nframes;
     c->p_calls += 1;
+    c->p_launches += launches;
     c->p_host_us += std::chrono::duration<double, std::micro>(clk::now() - tp0).count();
   }
   return RT_OK;
@@ -911,7 +914,7 @@ rt_status rt_comm_phase_stats(rt_comm_t c, double* out, uint32_t n) {
   if (st != RT_OK) return st;
   phase_collect(c, true);
   std::lock_guard<std::mutex> lk(c->pmu);
-  const double v[RT_COMM_PHASE_COUNT] = {(double)c->p_frames, (double)c->p_n[kPhaseRender], c->p_ms[kPhaseRender],
+  const double v[RT_COMM_PHASE_COUNT] = {(double)c->p_frames, (double)c->p_launches, c->p_ms[kPhaseRender],
                                          (double)c->p_n[kPhaseGather], c->p_ms[kPhaseGather],
                                          (double)c->p_n[kPhaseAssembly], c->p_ms[kPhaseAssembly], c->p_host_us,
                                          (double)c->p_calls, c->p_issue_us, c->p_bytes_in, c->p_bytes};

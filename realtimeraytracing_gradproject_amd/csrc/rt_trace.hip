@@ -1871,8 +1871,14 @@ hipError_t launch_trace_frame(const SceneView& sc, const FrameParams& fp, const 
 // raising T. (tools/split_study.py models the split on the oracle's packet fetches.) The north star's "wavefront
 // ballot/prefix-sum" appears here as the block scan that places each item.
 // ------------------------------------------------------------------------------------------
-constexpr uint32_t kPlanThreads = 1024;
-static_assert(kPlanMaxTiles == 32u * kPlanThreads, "a run of at most 32 tiles per thread");
+#ifndef RT_PLAN_THREADS
+#define RT_PLAN_THREADS 1024  // the plan workgroup (A/B: 512 needs 2 free wave slots per SIMD to dispatch, not 4)
+#endif
+#ifndef RT_PLAN_PRIO
+#define RT_PLAN_PRIO 0  // s_setprio of the plan's waves (A/B: issue ahead of the trace waves sharing their SIMDs)
+#endif
+constexpr uint32_t kPlanThreads = RT_PLAN_THREADS;
+static_assert(kPlanMaxTiles <= 64u * kPlanThreads, "a run of at most 64 tiles per thread (sums of 16-bit times)");
 
 // exclusive prefix sum over the workgroup (wave scan by shuffles, the waves' totals through LDS)
 __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t* s_w, uint64_t* total) {
@@ -1991,11 +1997,12 @@ __device__ __forceinline__ uint32_t plan_pick32(const PlanArgs& a, bool split, u
 __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
   __shared__ uint32_t s_c[kPlanMaxTiles + kPlanMaxTiles / 32];
   __shared__ uint64_t s_red[kPlanThreads / 64];
+  if (RT_PLAN_PRIO) __builtin_amdgcn_s_setprio(RT_PLAN_PRIO);
   const uint64_t t_begin = __builtin_amdgcn_s_memrealtime();
   const uint32_t tid = threadIdx.x, n = a.ntiles, cap = n + a.extra_cap;
   const uint32_t m = (n + kPlanThreads - 1) / kPlanThreads, t0 = tid * m, t1 = t0 + m < n ? t0 + m : n;
   // 1. the snapshot (coalesced loads, tile t by thread t % 1024, unrolled so the loads overlap) and the load bound
-  uint32_t lsum = 0, lmax = 0;  // < 32 tiles x 65535 per thread
+  uint32_t lsum = 0, lmax = 0;  // < 64 tiles x 65535 per thread
   uint32_t lsplits = 0;          // the tiles' measured splits: useless << 16 | useful
   if (!a.force) {
 #pragma unroll 8

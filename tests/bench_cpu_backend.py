@@ -154,3 +154,69 @@ class CpuBackendStepFails(CpuBackend):
         self._calls += 1
         if self._calls == int(os.environ.get("STEP_FAIL_AT", "3")):
             raise RuntimeError("simulated render failure")
+
+
+class CpuBackendNative(CpuBackend):
+    """bench.py's native strips loop (rt_render_strips_frames) at world N over gloo: a stand-in communicator renders
+    this rank's strips with the oracle, gathers them to rank 0 (torch.distributed gather) and assembles the frames
+    there, timing each phase on the wall clock the way the library's phase timing reports them (rt_comm_phase_stats'
+    fields). Exercises bench.py's phase pass and its max / min render share over the ranks."""
+    native_strips = True
+    rt = _CommAvailable()
+
+    def comm_open(self, world, rank):
+        be = self
+        H = self.spec.height
+        rows, padded = D.rank_rows(H, world, rank), D.padded_rows(H, world)
+
+        class _Comm:
+            depth, batch = 3, 1
+
+            def __init__(self):
+                self.on = False
+                self.ps = {}
+
+            def set_batch(self, b):
+                self.batch = b
+
+            def synchronize(self):
+                pass
+
+            def close(self):
+                pass
+
+            def abort(self):
+                pass
+
+            def set_phase_timing(self, on):
+                self.on = bool(on)
+                self.ps = dict.fromkeys(("frames", "renders", "render_ms", "gathers", "gather_ms", "assemblies",
+                                         "assembly_ms", "host_us", "calls", "issue_us", "bytes_in", "bytes"), 0.0)
+
+            def phase_stats(self):
+                return dict(self.ps)
+
+            def step(self, frames, n):
+                t0 = time.perf_counter()
+                local = torch.zeros((padded, be.spec.width, 4), dtype=torch.uint8)
+                be._render(local, rows)
+                t1 = time.perf_counter()
+                bufs = [torch.zeros_like(local) for _ in range(world)] if rank == 0 else None
+                dist.gather(local, bufs, dst=0)
+                t2 = time.perf_counter()
+                if rank == 0:
+                    g = torch.stack(bufs)
+                    for f in frames:
+                        f[:] = torch.from_numpy(D.assemble_host(g.numpy(), H, world))
+                t3 = time.perf_counter()
+                if self.on:
+                    for k, v in (("frames", n), ("renders", 1), ("render_ms", (t1 - t0) * 1e3), ("gathers", 1),
+                                 ("gather_ms", (t2 - t1) * 1e3), ("assemblies", 1 if rank == 0 else 0),
+                                 ("assembly_ms", (t3 - t2) * 1e3), ("host_us", (t3 - t0) * 1e6), ("calls", 1),
+                                 ("bytes_in", local.numel() * (world - 1) if rank == 0 else 0),
+                                 ("bytes", local.numel() * world)):
+                        self.ps[k] += v
+        return _Comm()
+
+    def render_strips(self, comm, frames, stream):
+        comm.step([f for f in frames if f is not None], len(frames))

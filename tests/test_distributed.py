@@ -205,3 +205,37 @@ def test_bench_native_loop_error_aborts_communicator(tmp_path):
     assert p.returncode != 0
     assert "simulated render failure" in p.stderr
     assert "comm aborted" in p.stderr and "comm closed" not in p.stderr, p.stderr[-3000:]
+
+
+def test_bench_native_loop_phases_gloo(tmp_path):
+    """the N > 1 line names its own binding cost. bench.py's native strips loop at world 2 (a stand-in
+    communicator over gloo that renders, gathers and assembles, timing each phase as rt_comm_phase_stats reports
+    them): config.phases carries the render share (with its max / min over the ranks), the gather, the assembly, the
+    host issue per frame, the bytes into rank 0 and their rate, and the period; the assembled frame is the oracle's."""
+    import json
+    import subprocess
+    import sys
+    sys.path.insert(0, ROOT)
+    import oracle
+    from realtimeraytracing_gradproject_amd import scenes
+    img = tmp_path / "frame.npy"
+    env = dict(os.environ, RT_BENCH_TEST_BACKEND="tests.bench_cpu_backend:CpuBackendNative",
+               PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""), OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "C2F", "--size", "64x44",
+           "--steps", "3", "--warmup", "1", "--settle-ms", "0", "--resettle-ms", "0", "--extra=", "--no-cpu-baseline",
+           "--phase-frames", "4", "--latency-frames", "2", "--save-image", str(img)]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    ph = out["config"]["phases"]
+    assert ph["frames"] == 4 and ph["world"] == 2 and ph["rank"] == 0
+    assert ph["render_share_ms_max"] >= ph["render_share_ms"] >= ph["render_share_ms_min"] > 0
+    assert ph["gather_ms"] > 0 and ph["assembly_ms"] > 0 and ph["host_issue_us"] > 0
+    # rank 1's padded strip block (3 strips of 8 rows), one block per call of 4 frames (the stand-in gathers once)
+    assert ph["bytes_into_rank0_per_frame"] == 24 * 64 * 4 // 4
+    assert ph["ingress_GBps_over_gather"] > 0 and ph["period_ms"] > 0
+    assert 0.5 <= ph["phase_sum_over_period"] <= 1.5  # one thread runs the phases back to back: they are the period
+    spec = scenes.config("C2F").with_size(64, 44)
+    o8, _, _ = oracle.Scene(spec).render_spec(spec, nthreads=2, want_float=False)
+    assert np.array_equal(np.load(img), o8)

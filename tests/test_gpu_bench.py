@@ -92,8 +92,42 @@ def test_bench_native_strips_world1(tmp_path, config, size, in_flight, extra):
     assert out["config"]["frame_ms_one_stream_is_latency"] is False
     if extra:
         assert out["config"]["loopback_ranks"] == int(extra[1])
+    ph = out["config"]["phases"]  # the per-phase pass of the native loop
+    assert ph["frames"] > 0 and ph["render_share_ms"] > 0 and ph["gather_ms"] > 0 and ph["assembly_ms"] > 0
+    assert ph["host_issue_us"] > 0 and ph["period_ms"] > 0
     w, h = (int(v) for v in size.split("x"))
     spec = scenes.config(config).with_size(w, h)
     o8, _, st = oracle.Scene(spec).render_spec(spec, nthreads=8, want_float=False)
     assert out["config"]["rays_per_step"] == int(st[0] + st[1])
     assert np.array_equal(np.load(img), o8)
+
+
+@pytest.mark.parametrize("loopback", [8, 0], ids=["loopback8", "rccl-world1"])
+def test_bench_strips_phases_name_the_period(loopback):
+    """the strips line carries what a step costs per phase (config.phases: rank 0's render share with
+    the max / min over ranks, the gather — ncclGather, or the loopback's device copy —, the assembly, the host's issue
+    per frame, the bytes into rank 0 and their rate, the period). On the loopback one GPU renders every emulated rank's
+    share, copies and assembles: the phases account for at least 0.9 of the period (C2, 1080p, N = 8, the shipped
+    4 frames per gather and per launch, the communicator's 3 render streams)."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--mode", "strips", "--config", "C2", "--steps", "40",
+           "--warmup", "8", "--settle-ms", "100", "--extra=", "--no-cpu-baseline", "--latency-frames", "3",
+           "--phase-frames", "96"] + (["--loopback", str(loopback)] if loopback else [])
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    ph = out["config"]["phases"]
+    print(json.dumps(ph))
+    assert ph["frames"] == 96 and ph["world"] == 1
+    assert ph["render_share_ms_max"] == ph["render_share_ms"] == ph["render_share_ms_min"] > 0
+    assert ph["render_launches_per_frame"] == pytest.approx((loopback or 1) / 4, rel=0.01)
+    assert ph["gather_ms"] > 0 and ph["assembly_ms"] > 0 and 0 < ph["host_issue_us"] < 1000
+    if loopback:
+        # 7 of 8 ranks' RGB8 blocks (17 strips of 8 rows x 1920 x 3 B) come into rank 0's buffer per frame
+        assert ph["bytes_into_rank0_per_frame"] == 7 * 136 * 1920 * 3
+        assert ph["ingress_GBps_over_gather"] > 50
+        assert ph["phase_sum_over_period"] >= 0.9, ph
+    else:
+        assert ph["bytes_into_rank0_per_frame"] == 0

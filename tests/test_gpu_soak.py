@@ -54,13 +54,51 @@ def test_balance_soak_moving_camera(name, size):
     torch.cuda.synchronize()
     info = c.tile_balance_info()
     assert info["check_bad"] == 0 and info["refused"] == 0, info
-    assert info["plans"] >= 1, info  # the balance ran (how often it re-plans depends on the view and the timing)
+    assert info["plans"] >= 1, info
+    # the re-plan cadence of balance_wants_plan, over the shape's active (one-stream) launches: a list
+    # that pays is re-planned every 8 of them (at most twice that with the plan's own latency); one that does not
+    # re-checks every 32 (a tail splitting could not shorten) or 128 launches (no tail, or coherent tiles), doubling
+    # after each further plan that did not pay — never more often than every 32
+    act = info["launches"]
+    if info["pays"]:
+        assert info["plans"] >= act // 16, info
+    else:
+        assert info["plans"] <= 2 + act // 32, info
     o = oracle.Scene(base)
     for k in range(0, n, 15):
         want, _, _ = o.render_spec(specs[k], nthreads=16, want_float=False)
         got = outs[k].cpu().numpy()
         bad = int((got != want).any(axis=2).sum())
         assert bad == 0, f"{name} frame {k}: {bad} pixels differ ({info})"
+    c.close()
+
+
+def test_balance_replans_every_8_launches_while_it_pays():
+    """the cadence pinned where the list pays. C4 at 1920 x 1080, one frame at a time with the camera
+    orbiting (each view changes which tiles are costly): the slowest tiles outlast the load bound, so every plan splits
+    some and pays, and balance_wants_plan re-plans every kReplan = 8 active launches (a plan landing a launch or two
+    after it starts): over 160 launches at least 160 / 16 plans, each list a valid cover (RT_BALANCE_CHECK)."""
+    base = scenes.config("C4")
+    os.environ["RT_BALANCE_CHECK"] = "1"
+    try:
+        c = rt.Context(0)
+    finally:
+        del os.environ["RT_BALANCE_CHECK"]
+    scenes.upload(c, base)
+    W, H = base.width, base.height
+    s = torch.cuda.Stream()
+    out = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
+    n = 160
+    for k in range(n):
+        c.set_camera(orbit(base, k, 4 * n).camera_buffer())
+        c.dispatch(W, H, out, stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    info = c.tile_balance_info()
+    assert info["check_bad"] == 0 and info["refused"] == 0, info
+    assert info["launches"] == n and info["pays"] == 1, info
+    assert info["plans"] >= n // 16, info
+    want, _, _ = oracle.Scene(base).render_spec(orbit(base, n - 1, 4 * n), nthreads=16, want_float=False)
+    assert int((out.cpu().numpy() != want).any(axis=2).sum()) == 0
     c.close()
 
 

@@ -46,6 +46,46 @@ for step in ${STEPS:-tests}; do
         -- python3 "$R/tools/one_config.py" --config ${SQC_CONFIG:-C2} --frames 12 > "$O/sqc_${TAG}.log" 2>&1 \
         || { echo "sqc pass failed rc=$?"; tail -20 "$O/sqc_${TAG}.log"; exit 1; }
       cd "$R"; find "$O/sqc_${TAG}" -name "*counter_collection.csv" | head -1 | xargs -r tail -5 ;;
+    clock)
+      # do the recording kernel's clock reads fetch from the fabric? (tools/clock_probe.hip)
+      cd /tmp && export TMPDIR=/tmp
+      for ctr in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 60 rocprofv3 --pmc $ctr --kernel-include-regex k_clock -d "$O/clock_${TAG}_$ctr" -o run \
+          --output-format csv -- "$R/tools/bin/clock_probe" > "$O/clock_${TAG}_$ctr.log" 2>&1 \
+          || { echo "clock probe $ctr failed rc=$?"; tail -20 "$O/clock_${TAG}_$ctr.log"; exit 1; }
+      done
+      cd "$R"; find "$O/clock_${TAG}_FETCH_SIZE" -name "*counter_collection.csv" | head -1 | xargs -r cat | head -12 ;;
+    planload)
+      # k_tile_plan under load, per library build (PLAN_LIBS), rocprofv3 kernel stats of each
+      cd /tmp && export TMPDIR=/tmp
+      for lib in ${PLAN_LIBS:-realtimeraytracing_gradproject_amd/lib/librtamd.so}; do
+        nm=$(basename $(dirname $lib))
+        timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$O/planload_${TAG}_$nm" -o run --output-format csv \
+          -- python3 "$R/tools/plan_load.py" --lib "$R/$lib" > "$O/planload_${TAG}_$nm.log" 2>&1 \
+          || { echo "plan_load $nm failed rc=$?"; tail -20 "$O/planload_${TAG}_$nm.log"; exit 1; }
+        grep '^{' "$O/planload_${TAG}_$nm.log"
+        find "$O/planload_${TAG}_$nm" -name "*kernel_stats.csv" | head -1 | xargs -r grep -E "k_tile_plan|Name" | cut -c1-200
+      done
+      cd "$R" ;;
+    fetchab)
+      # where the recording kernel's extra HBM reads come from — FETCH_SIZE per dispatch of C2F / C4
+      # with the balance off, adaptive, adaptive without splits or front class (the list never pays: the plain
+      # kernel, recording on some launches), and the forced 4-part layout (a plan before every launch)
+      cd /tmp && export TMPDIR=/tmp
+      for cfg in ${FAB_CFGS:-C2F C4}; do
+        for v in "off:--balance 0" "adaptive:" "nosplit:" "forced4:--balance 2"; do
+          nm=${v%%:*}; args=${v#*:}
+          if [ "$nm" = nosplit ]; then export RT_BALANCE_SPLIT=0 RT_BALANCE_FRONT=0; else unset RT_BALANCE_SPLIT RT_BALANCE_FRONT; fi
+          timeout -s KILL 90 rocprofv3 --pmc ${FAB_CTR:-FETCH_SIZE} -d "$O/fab_${TAG}_${cfg}_$nm" -o run \
+            --output-format csv -- python3 "$R/tools/one_config.py" --config $cfg --frames 24 $args \
+            > "$O/fab_${TAG}_${cfg}_$nm.log" 2>&1 || { echo "fetchab $cfg $nm failed rc=$?"; tail -5 "$O/fab_${TAG}_${cfg}_$nm.log"; exit 1; }
+          unset RT_BALANCE_SPLIT RT_BALANCE_FRONT
+          echo "== $cfg $nm"
+          find "$O/fab_${TAG}_${cfg}_$nm" -name "*counter_collection.csv" | head -1 | xargs -r \
+            python3 -c "import csv,sys; [print(r['Dispatch_Id'], r['Kernel_Name'][:70], r['Counter_Value']) for r in csv.DictReader(open(sys.argv[1]))]" | tail -14
+        done
+      done
+      cd "$R" ;;
     occ)
       timeout -k 10 120 ./tools/bin/occupancy_probe > "$O/occupancy_${TAG}.jsonl" 2>&1 \
         || { echo "occupancy_probe failed rc=$?"; tail -20 "$O/occupancy_${TAG}.jsonl"; exit 1; }

@@ -98,8 +98,21 @@ def share_loop(ctx, spec, nranks, rank, frames, fpl=4, rounds=3):
         torch.cuda.synchronize()
         best = min(best, (time.perf_counter() - t0) * 1e3 / frames)
         host = min(host, th * 1e6 / (frames / fpl))
+    # where the share's period goes (rt_comm_set_phase_timing: event pairs around the render launch, the gather
+    # copy, rank 0's assembly), one more pass
+    comm.set_phase_timing(True)
+    t0 = time.perf_counter()
+    issue(frames)
+    ps = comm.phase_stats()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) * 1e3 / frames
+    comm.set_phase_timing(False)
+    f = max(ps["frames"], 1)
+    phases = {"period_ms": round(wall, 4), "render_ms": round(ps["render_ms"] / f, 4),
+              "gather_copy_ms": round(ps["gather_ms"] / f, 4), "assembly_ms": round(ps["assembly_ms"] / f, 4),
+              "host_us_per_frame": round(ps["host_us"] / f, 2), "issue_thread_us_per_frame": round(ps["issue_us"] / f, 2)}
     comm.close()
-    return best, host
+    return best, host, phases
 
 
 def main():
@@ -124,11 +137,11 @@ def main():
             ranks = range(n) if a.all_ranks else sorted({0, n - 1})
             per = {}
             for r in ranks:
-                ms, host = share_loop(ctx, spec, n, r, nf)
+                ms, host, phases = share_loop(ctx, spec, n, r, nf)
                 per[r] = ms
                 print(json.dumps({"config": name, "n": n, "rank": r, "ms_per_frame": round(ms, 4),
                                   "host_us_per_call": round(host, 2), "frames": nf, "frames_per_launch": 4,
-                                  "frames_per_gather": 4}), flush=True)
+                                  "frames_per_gather": 4, "phases": phases}), flush=True)
             worst = max(per.values())
             ingress = rgb_frame * (n - 1) / n  # bytes into rank 0 per frame
             print(json.dumps({
