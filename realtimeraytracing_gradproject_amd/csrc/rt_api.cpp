@@ -283,6 +283,9 @@ struct rt_ctx {
   uint32_t bal_forced_cap = 0;  // RT_BALANCE_FORCED_CAP (tests): the forced layouts' extra waves (0: 63 x the tiles)
   uint32_t bal_prio = 1;        // RT_BALANCE_PRIO (A/B): the front class's waves raise their issue priority
   uint32_t bal_fine = 1;        // RT_BALANCE_FINE (A/B): adaptive plans may split a tile into 64 one-pixel parts
+  uint32_t bal_diag = 0;        // RT_BALANCE_DIAG (diagnostics: the recording kernel's traffic): 1 record
+                                // on every launch and never use a list, 2 use the lists but stop recording once the
+                                // first plan has started, 3 use the current list even where it does not pay
   static constexpr size_t kMaxBalanceMaps = 32;
   static constexpr uint32_t kRecycleBackoff = 16;
   std::vector<BalanceMap> bal;
@@ -505,6 +508,7 @@ rt_status rt_create(int hip_device, rt_ctx_t* out) {
   if (!c) return RT_E_OOM;
   c->device = hip_device;
   if (const char* ev = std::getenv("RT_BALANCE_SPLIT")) c->bal_split = std::strtoul(ev, nullptr, 10) ? 1u : 0u;
+  if (const char* ev = std::getenv("RT_BALANCE_DIAG")) c->bal_diag = (uint32_t)std::strtoul(ev, nullptr, 10);
   if (const char* ev = std::getenv("RT_BALANCE_FRONT")) c->bal_front = (uint32_t)std::strtoul(ev, nullptr, 10);
   if (const char* ev = std::getenv("RT_BALANCE_CHECK")) c->bal_check = std::strtoul(ev, nullptr, 10) ? 1u : 0u;
   if (const char* ev = std::getenv("RT_BALANCE_BUDGET"))
@@ -1340,6 +1344,14 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
         m->nopay_run = ps->pays ? 0u : m->nopay_run + 1u;
       }
       if (active && !forced) balance_wants_plan(*m, &plan, &use, &record);
+      if (c->bal_diag == 1) {
+        plan = use = false;
+        record = true;
+      } else if (c->bal_diag == 2 && (m->cur >= 0 || m->pending >= 0)) {
+        record = false;
+      } else if (c->bal_diag == 3 && m->cur >= 0) {
+        use = true;  // the current list even where it does not pay (with RT_BALANCE_SPLIT=0 RT_BALANCE_FRONT=0: the plain order)
+      }
       c->fp.cost = record ? m->cost : nullptr;
       rt::PlanArgs a;
       a.cost = m->cost;
@@ -1371,7 +1383,8 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
         bool hit;
         plan_slot = ring_acquire(c->plans, s, nullptr, &hit, &be);
         if (be != hipSuccess) return hip_fail(c, be, "tile balance: order after in-flight launches");
-        HIPCHK(c, slot_reserve(*plan_slot, ((size_t)plan_items + 3u * ntiles + 1) * 4), "hipMalloc(tile plan)");
+        HIPCHK(c, slot_reserve(*plan_slot, ((size_t)rt::plan_xwords(plan_items, a.wl) + 3u * ntiles + 1) * 4),
+               "hipMalloc(tile plan)");
         a.plan = (uint32_t*)plan_slot->buf;
         HIPCHK(c, rt::launch_tile_plan(a, s), "tile plan launch");
         c->fp.plan = a.plan;
@@ -1390,7 +1403,7 @@ rt_status dispatch_frame(rt_ctx* c, uint32_t W, uint32_t H, const uint32_t* d_ro
           a.extra_cap = m->extra_cap;
           a.slots = plan_slots(c, sv);
           const uint32_t items = ntiles + a.extra_cap;
-          HIPCHK(c, slot_reserve(sl, ((size_t)items + 3u * ntiles + 1) * 4), "hipMalloc(tile plan)");
+          HIPCHK(c, slot_reserve(sl, ((size_t)rt::plan_xwords(items, a.wl) + 3u * ntiles + 1) * 4), "hipMalloc(tile plan)");
           a.plan = (uint32_t*)sl.buf;
           HIPCHK(c, rt::launch_tile_plan(a, ps), "tile plan launch");
           HIPCHK(c, hipEventRecord(m->pend_ev, ps), "tile balance: record the plan");

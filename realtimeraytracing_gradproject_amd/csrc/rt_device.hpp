@@ -154,7 +154,7 @@ struct FrameParams {
   uint32_t frame_bytes;
   FrameCam cam[kMaxLaunchFrames];
   // Tile balance (packet schedule, rt_set_tile_balance). plan: the launch's wave work list written by k_tile_plan
-  // (plan[0] = item count, plan[1 + i] = item i = wave slot << 8 | part << 2 | split code, bit 31 the front class;
+  // (plan[0] = item count, plan[1 + plan_xaddr(i)] = item i = wave slot << 8 | part << 2 | split code, bit 31 the front class;
   // split code 0: the whole tile, 1: quadrant `part` of 4, 2: cell `part` of 16, 3: pixel `part` of 64), dealt to the waves of a 1-D grid in list order (costliest
   // first), or null: wave slot = the plain grid's wave index. cost: per wave slot, two words written at wave end (or
   // null): [0] the ticks (s_memrealtime) of the tile's last whole wave, bit 31 set by every part of a split since
@@ -171,6 +171,20 @@ struct FrameParams {
 // takes 0.55 of the whole packet's fetches, the costliest 2 x 2 cell 0.35 (tools/split_study.py): the kernel's
 // estimate of a whole tile from one part's time, and the plan's estimate of a part from the whole.
 RT_HD uint32_t split_parts(uint32_t code) { return code == 0u ? 1u : code == 1u ? 4u : code == 2u ? 16u : 64u; }
+
+// Work-list storage (round 6). The launch deals the list's items to its waves in list order (item p to
+// wave p % wl of workgroup p / wl) and the dispatcher deals workgroups round robin over the 8 XCDs, so in list order
+// every 64-B line of the list was read by all 8 XCDs' L2s (measured: 1.0 MB of FETCH_SIZE per 1080p launch, C2F and
+// C4 alike, with the list equal to the plain order). The items are therefore stored XCD-major: position p lives at
+// word plan_xaddr(p), the workgroups of one XCD (linear id = x mod 8) reading a contiguous slice. Only the storage is
+// permuted (the plan writes and the launch reads through the same map): the list, its order and the image are not.
+RT_HD uint32_t plan_xaddr(uint32_t p, uint32_t wl, uint32_t groups) {
+  const uint32_t k = p / wl, j = p - k * wl, per = (groups + 7u) / 8u;
+  return ((k & 7u) * per + (k >> 3)) * wl + j;
+}
+// the workgroups of a launch over a list of `cap` items, and the words its permuted storage spans
+RT_HD uint32_t plan_groups(uint32_t cap, uint32_t wl) { return (cap + wl - 1u) / wl; }
+RT_HD uint32_t plan_xwords(uint32_t cap, uint32_t wl) { return (plan_groups(cap, wl) + 7u) / 8u * 8u * wl; }
 
 // The trace kernels read one node pool and one triangle pool per scene: [TLAS | BLAS 0 | BLAS 1 ..]
 // with child refs rebased to pool indices (BLAS leaves -> ~(global triangle slot)). A uniform base

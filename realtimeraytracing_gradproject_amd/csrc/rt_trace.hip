@@ -955,8 +955,8 @@ __device__ V3 face_world_normal(const HitInstance& hi, uint32_t prim) {
   return mat3_mul(hi.nrm, n);
 }
 
-#ifndef RT_SURFACE_V
-#define RT_SURFACE_V 2  // ClosestHit's surface colour: 2 = one light loop, quotients as reciprocals (round 6)
+#ifndef RT_SURFACE_UNROLL
+#define RT_SURFACE_UNROLL 1  // A/B: the light loop of surface_ref unrolled (independent lights interleaved; same sums)
 #endif
 
 // ClosestHit's finalSurfaceColor = CalculateDirectLighting (Hit.hlsl:83-95) + CalculatePBRShading
@@ -995,6 +995,9 @@ __device__ V3 surface_ref(const FrameParams& fp, V3 P, V3 n, V3 cam) {
   const float ggx2 = NdotV * srcp(NdotV * omk + k);
   const float v4 = 4.0f * NdotV;
   V3 cd = v3(0.0f, 0.0f, 0.0f), L0 = v3(0.0f, 0.0f, 0.0f);
+#if RT_SURFACE_UNROLL > 1
+#pragma unroll RT_SURFACE_UNROLL
+#endif
   for (uint32_t l = 0; l < fp.nlights; ++l) {
     const LightRec& Lr = fp.lights[l];
     const V3 lp = v3(Lr.position[0], Lr.position[1], Lr.position[2]);
@@ -1547,7 +1550,7 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
     const RT_CONST uint32_t* plan = (const RT_CONST uint32_t*)fp.plan;
     const uint32_t i = blockIdx.x * WL + w;
     if (i >= plan[0]) return;  // the grid is sized for the list's budget: the waves past its end have nothing
-    const uint32_t it = plan[1 + i];
+    const uint32_t it = plan[1 + plan_xaddr(i, WL, gridDim.x)];  // XCD-major storage (plan_xaddr)
     // the plan's front class (the waves estimated to outlast half the load bound: the launch's critical path) issues
     // ahead of the other waves on its SIMD
     if (it >> 31) __builtin_amdgcn_s_setprio(RT_BALANCE_FRONT_PRIO);
@@ -2000,6 +2003,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
   if (RT_PLAN_PRIO) __builtin_amdgcn_s_setprio(RT_PLAN_PRIO);
   const uint64_t t_begin = __builtin_amdgcn_s_memrealtime();
   const uint32_t tid = threadIdx.x, n = a.ntiles, cap = n + a.extra_cap;
+  const uint32_t G = plan_groups(cap, a.wl);  // the launch's workgroups: the items' storage map (plan_xaddr)
   const uint32_t m = (n + kPlanThreads - 1) / kPlanThreads, t0 = tid * m, t1 = t0 + m < n ? t0 + m : n;
   // 1. the snapshot (coalesced loads, tile t by thread t % 1024, unrolled so the loads overlap) and the load bound
   uint32_t lsum = 0, lmax = 0;  // < 64 tiles x 65535 per thread
@@ -2056,7 +2060,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
   if (!a.force && !tail) {
     // no tail: the plain grid's order, every tile whole
 #pragma unroll 4
-    for (uint32_t t = tid; t < n; t += kPlanThreads) a.plan[1u + t] = t << 8;
+    for (uint32_t t = tid; t < n; t += kPlanThreads) a.plan[1u + plan_xaddr(t, a.wl, G)] = t << 8;
   } else {
     // 3. each tile's layout and class (estimated above front / 16 x L: first); thread i's run of tiles
     // [m i, m i + m) counts its items, one block scan of the runs' (front, rest) counts places them, and each
@@ -2095,7 +2099,8 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
       const uint32_t d = s_c[plan_lds_ix(t)], code = d & 3u, k = split_parts(code), pos = d >> 2;
       for (uint32_t q = 0; q < k; ++q) {
         if (pos + q < cap)
-          a.plan[1u + pos + q] = (t << 8) | (q << 2) | code | ((a.prio && pos + q < nfront_items) ? 0x80000000u : 0u);
+          a.plan[1u + plan_xaddr(pos + q, a.wl, G)] =
+              (t << 8) | (q << 2) | code | ((a.prio && pos + q < nfront_items) ? 0x80000000u : 0u);
         else ++lref;
       }
       // a split tile's part word restarts (its parts raise it with atomicMax at their end)
@@ -2114,7 +2119,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
   refused = (uint32_t)block_sum64(lref, s_red);
   if (refused) {
     // a list missing any part would leave pixels unwritten: the plain grid's list instead (every tile whole)
-    for (uint32_t t = tid; t < n; t += kPlanThreads) a.plan[1u + t] = t << 8;
+    for (uint32_t t = tid; t < n; t += kPlanThreads) a.plan[1u + plan_xaddr(t, a.wl, G)] = t << 8;
     nitems = n;
     nsplit = 0;
     pays = false;
@@ -2124,14 +2129,15 @@ __global__ __launch_bounds__(kPlanThreads) void k_tile_plan(PlanArgs a) {
   // parts 0 .. k - 1 once each (the words after the items count them: the layouts seen, parts 0 .. 31, parts 32 .. 63)
   uint32_t bad = 0, first_bad = 0xffffffffu, first_word = 0;
   if (a.check) {
-    uint32_t* sw = a.plan + 1u + cap;
+    uint32_t* sw = a.plan + 1u + plan_xwords(cap, a.wl);
     uint32_t* sp = sw + n;
     uint32_t* sq = sp + n;
     __syncthreads();  // every item is written
     for (uint32_t t = tid; t < n; t += kPlanThreads) sw[t] = sp[t] = sq[t] = 0u;
     __syncthreads();
     for (uint32_t i = tid; i < nitems; i += kPlanThreads) {
-      const uint32_t it = a.plan[1u + i], slot = (it >> 8) & kPlanSlotMask, q = (it >> 2) & 63u, code = it & 3u;
+      const uint32_t it = a.plan[1u + plan_xaddr(i, a.wl, G)], slot = (it >> 8) & kPlanSlotMask, q = (it >> 2) & 63u,
+                     code = it & 3u;
       if (slot >= n || q >= split_parts(code)) {
         bad += 1u;
         continue;

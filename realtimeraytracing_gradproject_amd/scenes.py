@@ -263,10 +263,12 @@ def deep_scene() -> SceneSpec:
                      ((20.0, 22.0, 70.0), (20.0, 18.0, 0.0), (0.0, 1.0, 0.0)), 96, 64, RT_SHADE_LAMBERT_SHADOW)
 
 
-def upload(ctx, spec: SceneSpec) -> List[int]:
-    """Builds BLAS/TLAS and frame state of `spec` on a Context; returns the BLAS ids."""
+def upload(ctx, spec: SceneSpec, camera: bool = True) -> List[int]:
+    """Builds BLAS/TLAS and frame state of `spec` on a Context; returns the BLAS ids. camera False leaves the
+    context's camera unset (launches must then bring their own: rt_dispatch_frames' camera array)."""
     ids = [ctx.blas_build(v, i) for (v, i) in spec.meshes]
     ctx.tlas_build([(ids[m], x, iid, hg) for (m, x, iid, hg) in spec.instances])
-    ctx.set_camera(spec.camera_buffer())
+    if camera:
+        ctx.set_camera(spec.camera_buffer())
     ctx.set_shading(spec.lights, spec.material, spec.mode, spec.spp)
     return ids

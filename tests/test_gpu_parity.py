@@ -879,3 +879,30 @@ def test_dispatch_frames_equal_oracle(name, size, nframes):
     with pytest.raises(rt.RtError):
         c.dispatch_frames(W, H, torch.empty((5, H, W, 4), dtype=torch.uint8, device="cuda"))
     c.close()
+
+
+def test_dispatch_frames_argument_rules():
+    """rt_dispatch_frames refuses a frame stride that is not a multiple of 4 bytes (the RGBA8 stores are
+    32-bit words), and renders from the cameras it is given on a context whose rt_set_camera was never called (it
+    refuses a NULL camera array there)."""
+    spec = scenes.config("C2F").with_size(96, 54)
+    c = rt.Context(0)
+    scenes.upload(c, spec)
+    W, H = spec.width, spec.height
+    cams = spec.camera_buffer().reshape(1, 64)
+    buf = torch.zeros((2 * W * H * 4 + 8,), dtype=torch.uint8, device="cuda")
+    with pytest.raises(rt.RtError):
+        c.dispatch_frames(W, H, buf.view(1, -1), cams, stream=torch.cuda.current_stream().cuda_stream,
+                          frame_stride=W * H * 4 + 2)
+    c.close()
+    # a context set up without rt_set_camera: the launch's own camera array is enough
+    c2 = rt.Context(0)
+    scenes.upload(c2, spec, camera=False)
+    out = torch.zeros((1, H, W, 4), dtype=torch.uint8, device="cuda")
+    with pytest.raises(rt.RtError):
+        c2.dispatch_frames(W, H, out, None, stream=torch.cuda.current_stream().cuda_stream)
+    c2.dispatch_frames(W, H, out, cams, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    o8, _, _ = oracle.Scene(spec).render_spec(spec, nthreads=8, want_float=False)
+    assert np.array_equal(out[0].cpu().numpy(), o8)
+    c2.close()

@@ -11,7 +11,7 @@ cd "$R"
 for step in ${STEPS:-tests}; do
   case $step in
     tests)
-      timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} \
+      timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v ${PYTEST_EXTRA:-} --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} \
         > "$O/gputest_${TAG}.log" 2>&1 || { echo "gpu tests failed rc=$?"; grep -E "FAIL|Error|error" "$O/gputest_${TAG}.log" | head -20; tail -40 "$O/gputest_${TAG}.log"; exit 1; }
       tail -3 "$O/gputest_${TAG}.log" ;;
     bench)
@@ -73,13 +73,19 @@ for step in ${STEPS:-tests}; do
       # kernel, recording on some launches), and the forced 4-part layout (a plan before every launch)
       cd /tmp && export TMPDIR=/tmp
       for cfg in ${FAB_CFGS:-C2F C4}; do
-        for v in "off:--balance 0" "adaptive:" "nosplit:" "forced4:--balance 2"; do
+        for v in ${FAB_SET:-off:--balance=0 adaptive: recordonly: listonly: forced4:--balance=2}; do
           nm=${v%%:*}; args=${v#*:}
-          if [ "$nm" = nosplit ]; then export RT_BALANCE_SPLIT=0 RT_BALANCE_FRONT=0; else unset RT_BALANCE_SPLIT RT_BALANCE_FRONT; fi
+          unset RT_BALANCE_SPLIT RT_BALANCE_FRONT RT_BALANCE_DIAG
+          if [ "$nm" = nosplit ]; then export RT_BALANCE_SPLIT=0 RT_BALANCE_FRONT=0; fi
+          if [ "$nm" = recordonly ]; then export RT_BALANCE_DIAG=1; fi
+          if [ "$nm" = listonly ]; then export RT_BALANCE_DIAG=2; fi
+          if [ "$nm" = plainlist ]; then export RT_BALANCE_DIAG=3 RT_BALANCE_SPLIT=0 RT_BALANCE_FRONT=0; fi
+          if [ "$nm" = frontlist ]; then export RT_BALANCE_DIAG=3 RT_BALANCE_SPLIT=0; fi
+          if [ "$nm" = splitlist ]; then export RT_BALANCE_DIAG=3 RT_BALANCE_FRONT=0; fi
           timeout -s KILL 90 rocprofv3 --pmc ${FAB_CTR:-FETCH_SIZE} -d "$O/fab_${TAG}_${cfg}_$nm" -o run \
             --output-format csv -- python3 "$R/tools/one_config.py" --config $cfg --frames 24 $args \
             > "$O/fab_${TAG}_${cfg}_$nm.log" 2>&1 || { echo "fetchab $cfg $nm failed rc=$?"; tail -5 "$O/fab_${TAG}_${cfg}_$nm.log"; exit 1; }
-          unset RT_BALANCE_SPLIT RT_BALANCE_FRONT
+          unset RT_BALANCE_SPLIT RT_BALANCE_FRONT RT_BALANCE_DIAG
           echo "== $cfg $nm"
           find "$O/fab_${TAG}_${cfg}_$nm" -name "*counter_collection.csv" | head -1 | xargs -r \
             python3 -c "import csv,sys; [print(r['Dispatch_Id'], r['Kernel_Name'][:70], r['Counter_Value']) for r in csv.DictReader(open(sys.argv[1]))]" | tail -14
