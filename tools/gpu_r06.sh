@@ -20,8 +20,8 @@ for step in ${STEPS:-tests}; do
       head -c 1500 "$O/bench_${TAG}.json"; echo ;;
     strips5)
       # the C5 (4 spp, 4K) and C4 tiled loops through the loopback transport
-      for cfg in "C5 8" "C4 4"; do
-        set -- $cfg
+      for cfg in ${STRIPS_CFGS:-C5:8 C4:4}; do
+        set -- ${cfg%%:*} ${cfg#*:}
         timeout -k 10 300 python3 bench.py --mode strips --loopback $2 --config $1 --extra= --no-cpu-baseline \
           --steps ${STRIPS_STEPS:-40} --warmup 8 \
           > "$O/strips_${1}_lb${2}_${TAG}.json" 2> "$O/strips_${1}_lb${2}_${TAG}.err" \
