@@ -28,6 +28,7 @@ ORACLE    := oracle/liboracle.so
 BASELINE  := oracle/libbaseline.so
 RCPCHECK  := tools/bin/recip_check
 OCCPROBE  := tools/bin/occupancy_probe
+CLKPROBE  := tools/bin/clock_probe
 
 HDRS      := include/rt_api.h $(SRC)/rt_device.hpp $(SRC)/rt_internal.hpp
 
@@ -52,7 +53,7 @@ DEFS_rays2     := -DRT_PACKET_RAYS=2 -DRT_SAMPLE_LANES=0 -DRT_RCP_EXACT=0
 DEFS_alt       := -DRT_PACKET_OCT=0 -DRT_REF_NOREFL=0 -DRT_RCP_EXACT=7 -DRT_MS_WIDE=1
 DEFS_wavetimes := -DRT_WAVE_TIMES=1
 
-all: $(LIB) $(APP) $(ORACLE) $(BASELINE) $(RCPCHECK) $(OCCPROBE) $(VLIBS)
+all: $(LIB) $(APP) $(ORACLE) $(BASELINE) $(RCPCHECK) $(OCCPROBE) $(CLKPROBE) $(VLIBS)
 
 $(VDIR)/%/librtamd.so: $(VSRCS)
 	bash tools/build_variant.sh $* $(DEFS_$*) > /dev/null
@@ -102,6 +103,11 @@ $(OCCPROBE): tools/occupancy_probe.hip
 	mkdir -p tools/bin
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
 
+# fabric traffic of the clock reads the tile balance's recording waves make
+$(CLKPROBE): tools/clock_probe.hip
+	mkdir -p tools/bin
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
+
 $(BUILD) $(LIBDIR):
 	mkdir -p $@
 
@@ -132,6 +138,6 @@ $(ASAN):
 	mkdir -p $@
 
 clean:
-	rm -rf $(BUILD) $(LIB) $(APP) $(ORACLE) $(BASELINE) $(RCPCHECK) $(OCCPROBE) $(VDIR)
+	rm -rf $(BUILD) $(LIB) $(APP) $(ORACLE) $(BASELINE) $(RCPCHECK) $(OCCPROBE) $(CLKPROBE) $(VDIR)
 
 .PHONY: all clean ref asan

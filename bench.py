@@ -964,7 +964,8 @@ def main(argv=None) -> int:
         x = run_config(be, es, world, rank, n_steps, 2, 0.0, strips, not a.no_pipeline, a.schedule,
                        in_flight=a.in_flight, resettle_ms=a.resettle_ms, frames_per_gather=a.frames_per_gather,
                        frames_per_launch=a.frames_per_launch, loopback=a.loopback,
-                       latency_frames=min(a.latency_frames, 5))
+                       latency_frames=min(a.latency_frames, 5),
+                       phase_frames=min(a.phase_frames, 16 if es.spp > 1 else 64))
         if rank == 0:
             st = x["stats"]
             rays = max(x["rays_step"], 1)
@@ -974,7 +975,7 @@ def main(argv=None) -> int:
                           "n_gpus": world, "parallelism": f"strips{world}+gather" if strips else f"frames{world}",
                           "tile_rows": x["tile_rows"], "frames_in_flight": x["in_flight"],
                           "frame_latency_ms": None if x["latency_ms"] is None else round(x["latency_ms"], 4),
-                          "tile_balance": x["tile_balance"],
+                          "tile_balance": x["tile_balance"], "phases": x["phases"],
                           "aabb_tests_per_ray_rank0": round(st["aabb_tests"] / rays, 2) if not distributed else None,
                           "node_fetches": int(st["node_fetches"]), "tri_fetches": int(st["tri_fetches"])})
     if not distributed and (a.extra is None) and isinstance(be, HipBackend):

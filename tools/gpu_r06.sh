@@ -92,6 +92,11 @@ for step in ${STEPS:-tests}; do
         done
       done
       cd "$R" ;;
+    stress)
+      # one long seed per kernel change
+      timeout -k 10 900 python3 -u tools/stress.py --minutes ${STRESS_MIN:-8} --seed ${STRESS_SEED:-12} \
+        > "$O/stress_${TAG}.log" 2>&1 || { echo "stress failed rc=$?"; tail -30 "$O/stress_${TAG}.log"; exit 1; }
+      tail -3 "$O/stress_${TAG}.log" ;;
     occ)
       timeout -k 10 120 ./tools/bin/occupancy_probe > "$O/occupancy_${TAG}.jsonl" 2>&1 \
         || { echo "occupancy_probe failed rc=$?"; tail -20 "$O/occupancy_${TAG}.jsonl"; exit 1; }
