@@ -97,6 +97,12 @@ for step in ${STEPS:-tests}; do
       timeout -k 10 900 python3 -u tools/stress.py --minutes ${STRESS_MIN:-8} --seed ${STRESS_SEED:-12} \
         > "$O/stress_${TAG}.log" 2>&1 || { echo "stress failed rc=$?"; tail -30 "$O/stress_${TAG}.log"; exit 1; }
       tail -3 "$O/stress_${TAG}.log" ;;
+    queue)
+      cd /tmp && export TMPDIR=/tmp
+      timeout -k 10 180 rocprofv3 --kernel-trace --stats -d "$O/queue_${TAG}" -o run --output-format csv \
+        -- python3 "$R/tools/queue_probe.py" > "$O/queue_${TAG}.log" 2>&1 \
+        || { echo "queue probe failed rc=$?"; tail -20 "$O/queue_${TAG}.log"; exit 1; }
+      cd "$R"; find "$O/queue_${TAG}" -name "*kernel_trace.csv" | head -1 | xargs -r python3 tools/queue_summary.py ;;
     occ)
       timeout -k 10 120 ./tools/bin/occupancy_probe > "$O/occupancy_${TAG}.jsonl" 2>&1 \
         || { echo "occupancy_probe failed rc=$?"; tail -20 "$O/occupancy_${TAG}.jsonl"; exit 1; }
