@@ -29,6 +29,7 @@ BASELINE  := oracle/libbaseline.so
 RCPCHECK  := tools/bin/recip_check
 OCCPROBE  := tools/bin/occupancy_probe
 CLKPROBE  := tools/bin/clock_probe
+DSPPROBE  := tools/bin/libdispatch_probe.so
 
 HDRS      := include/rt_api.h $(SRC)/rt_device.hpp $(SRC)/rt_internal.hpp
 
@@ -53,7 +54,7 @@ DEFS_rays2     := -DRT_PACKET_RAYS=2 -DRT_SAMPLE_LANES=0 -DRT_RCP_EXACT=0
 DEFS_alt       := -DRT_PACKET_OCT=0 -DRT_REF_NOREFL=0 -DRT_RCP_EXACT=7 -DRT_MS_WIDE=1
 DEFS_wavetimes := -DRT_WAVE_TIMES=1
 
-all: $(LIB) $(APP) $(ORACLE) $(BASELINE) $(RCPCHECK) $(OCCPROBE) $(CLKPROBE) $(VLIBS)
+all: $(LIB) $(APP) $(ORACLE) $(BASELINE) $(RCPCHECK) $(OCCPROBE) $(CLKPROBE) $(DSPPROBE) $(VLIBS)
 
 $(VDIR)/%/librtamd.so: $(VSRCS)
 	bash tools/build_variant.sh $* $(DEFS_$*) > /dev/null
@@ -108,6 +109,11 @@ $(CLKPROBE): tools/clock_probe.hip
 	mkdir -p tools/bin
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
 
+# one-workgroup kernels of k_tile_plan's shape and without its LDS / its 16 waves (tools/queue_probe.py)
+$(DSPPROBE): tools/dispatch_probe.hip
+	mkdir -p tools/bin
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -shared -fPIC -o $@ $<
+
 $(BUILD) $(LIBDIR):
 	mkdir -p $@
 
@@ -138,6 +144,6 @@ $(ASAN):
 	mkdir -p $@
 
 clean:
-	rm -rf $(BUILD) $(LIB) $(APP) $(ORACLE) $(BASELINE) $(RCPCHECK) $(OCCPROBE) $(CLKPROBE) $(VDIR)
+	rm -rf $(BUILD) $(LIB) $(APP) $(ORACLE) $(BASELINE) $(RCPCHECK) $(OCCPROBE) $(CLKPROBE) $(DSPPROBE) $(VDIR)
 
 .PHONY: all clean ref asan

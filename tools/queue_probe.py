@@ -28,22 +28,29 @@ def main():
     small = torch.zeros(64, device="cuda")
     big = torch.ones(1 << 18, device="cuda")
     res = torch.zeros(1, device="cuda")
-    torch.cuda.synchronize()
-    # idle reference: the probe kernels alone
-    for _ in range(20):
+    import ctypes
+    probe = ctypes.CDLL(os.path.join(ROOT, "tools", "bin", "libdispatch_probe.so"))
+    probe.dispatch_probe.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    pout = torch.zeros(4, dtype=torch.int32, device="cuda")
+    s_probe = [torch.cuda.Stream() for _ in range(4)]
+
+    def probes():
         with torch.cuda.stream(s_small):
             small.add_(1.0)
         with torch.cuda.stream(s_big):
             torch.sum(big, dim=0, out=res)
+        for kind in range(4):  # the plan's shape (1024 threads, 135 KB LDS), and without each of the two
+            assert probe.dispatch_probe(kind, pout.data_ptr(), s_probe[kind].cuda_stream) == 0
+    torch.cuda.synchronize()
+    # idle reference: the probe kernels alone
+    for _ in range(20):
+        probes()
         torch.cuda.synchronize()
     # loaded: beside back-to-back frames
     for k in range(400):
         c.dispatch(W, H, out, stream=s_main.cuda_stream)
         if k % 8 == 4:
-            with torch.cuda.stream(s_small):
-                small.add_(1.0)
-            with torch.cuda.stream(s_big):
-                torch.sum(big, dim=0, out=res)
+            probes()
     torch.cuda.synchronize()
     c.close()
     print("ok")
