@@ -55,6 +55,21 @@ for step in ${STEPS:-tests}; do
           || { echo "clock probe $ctr failed rc=$?"; tail -20 "$O/clock_${TAG}_$ctr.log"; exit 1; }
       done
       cd "$R"; find "$O/clock_${TAG}_FETCH_SIZE" -name "*counter_collection.csv" | head -1 | xargs -r cat | head -12 ;;
+    planstream)
+      # A/B: the plans on the context stream vs a high-priority stream of their own (RT_PLAN_STREAM_PRIO), twice each
+      cd /tmp && export TMPDIR=/tmp
+      for rep in 1 2; do
+        for ps in 0 1; do
+          export RT_PLAN_STREAM_PRIO=$ps
+          timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$O/planstream_${TAG}_${ps}_$rep" -o run --output-format csv \
+            -- python3 "$R/tools/plan_load.py" --configs C2F,C4,C4/4,C2@3,C4@3 --frames 400 > "$O/planstream_${TAG}_${ps}_$rep.log" 2>&1 \
+            || { echo "planstream $ps failed rc=$?"; tail -20 "$O/planstream_${TAG}_${ps}_$rep.log"; exit 1; }
+          unset RT_PLAN_STREAM_PRIO
+          echo "== plan stream prio $ps rep $rep"; grep '^{' "$O/planstream_${TAG}_${ps}_$rep.log"
+          find "$O/planstream_${TAG}_${ps}_$rep" -name "*kernel_stats.csv" | head -1 | xargs -r grep -E "k_tile_plan" | cut -c1-160
+        done
+      done
+      cd "$R" ;;
     planload)
       # k_tile_plan under load, per library build (PLAN_LIBS), rocprofv3 kernel stats of each
       cd /tmp && export TMPDIR=/tmp

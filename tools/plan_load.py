@@ -29,22 +29,24 @@ def main():
     lib = rt._load(a.lib) if a.lib else None
     out = {"lib": a.lib or "tree"}
     for item in a.configs.split(","):
-        name, _, share = item.partition("/")
+        item_, _, nst = item.partition("@")  # C2@3: frames in flight over 3 streams (the balance stays off there)
+        name, _, share = item_.partition("/")
         n = int(share) if share else 1
+        nstreams = int(nst) if nst else 1
         spec = scenes.config(name)
         W, H = spec.width, spec.height
         c = rt.Context(0, library=lib) if lib else rt.Context(0)
         scenes.upload(c, spec)
         rows = rt.strip_rows(H, n, 0) if n > 1 else None
         NR = len(rows) if rows is not None else H
-        buf = torch.zeros((NR, W, 4), dtype=torch.uint8, device="cuda")
-        s = torch.cuda.Stream()
-        for _ in range(60):  # clock ramp + the shape's first plans
-            c.dispatch(W, H, buf, rows=rows, stream=s.cuda_stream)
+        bufs = [torch.zeros((NR, W, 4), dtype=torch.uint8, device="cuda") for _ in range(nstreams)]
+        ss = [torch.cuda.Stream() for _ in range(nstreams)]
+        for k in range(60):  # clock ramp + the shape's first plans
+            c.dispatch(W, H, bufs[k % nstreams], rows=rows, stream=ss[k % nstreams].cuda_stream)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(a.frames):
-            c.dispatch(W, H, buf, rows=rows, stream=s.cuda_stream)
+        for k in range(a.frames):
+            c.dispatch(W, H, bufs[k % nstreams], rows=rows, stream=ss[k % nstreams].cuda_stream)
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) * 1e3 / a.frames
         tb = c.tile_balance_info()
