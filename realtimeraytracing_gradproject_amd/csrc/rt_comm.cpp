@@ -196,7 +196,8 @@ struct rt_comm {
   // rt_comm_set_phase_timing (what a step costs, per phase, on this rank): timing-event pairs around
   // the render launches (render stream), the gather (gather stream, from the moment the render is done) and rank
   // 0's assembly, resolved into sums once complete; the host time of the caller's calls and of the issue thread
-  bool phase = false;
+  bool phase = false;  // written only with the pipeline drained; the issue thread reads it per job, after the job's
+                       // hand-off under `mu` (so the write happens-before every read that can see a new job)
   std::mutex pmu;                 // the two threads record spans
   std::vector<hipEvent_t> pfree;  // resolved events, reused
   std::deque<PhaseSpan> ppend;    // recorded spans not yet resolved
