@@ -824,6 +824,7 @@ rt_status rt_set_shading(rt_ctx_t c, const rt_light* lights, uint32_t nlights, c
   if (!k) return fail(c, RT_E_INVALID, "rt_set_shading: spp must be 1, 4, 9 or 16");
   for (uint32_t l = 0; l < nlights; ++l) std::memcpy(&c->fp.lights[l], &lights[l], sizeof(rt::LightRec));
   std::memcpy(&c->fp.material, m, sizeof(rt::MaterialRec));
+  rt::surface_consts(c->fp.material, c->fp.surf);
   c->fp.nlights = nlights;
   c->fp.shade_mode = (uint32_t)shade_mode;
   c->fp.spp_side = (uint32_t)k;

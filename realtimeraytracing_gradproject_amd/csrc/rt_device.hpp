@@ -118,6 +118,30 @@ struct MaterialRec {
   float roughness, metallic, reflectivity;
 };
 
+// The material's constants of ClosestHit's surface colour (surface_ref, rt_trace.hip), evaluated once per
+// rt_set_shading on the host with the same IEEE float operations the kernel would run per pixel (so the same bits):
+// GGX's a^2, Smith's k and 1 - k (Hit.hlsl:104-117), F0 = lerp(0.04, albedo, metallic) (:148-149) and the diffuse
+// factor (1 - metallic) albedo / PI (:158-162 as pinned in round 6).
+struct SurfaceConsts {
+  float a2, k, omk;
+  float F0[3];
+  float kdA[3];
+};
+constexpr float kPiF = 3.14159265359f;  // Common.hlsl:1
+inline void surface_consts(const MaterialRec& m, SurfaceConsts& c) {
+  const float r = m.roughness;
+  const float a = r * r;
+  c.a2 = a * a;
+  const float rp1 = r + 1.0f;
+  c.k = (rp1 * rp1) / 8.0f;
+  c.omk = 1.0f - c.k;
+  const float km = 1.0f - m.metallic;
+  for (int i = 0; i < 3; ++i) {
+    c.F0[i] = 0.04f + m.metallic * (m.albedo[i] - 0.04f);
+    c.kdA[i] = (km * m.albedo[i]) / kPiF;
+  }
+}
+
 // Frames one launch renders (rt_render_strips_frames: a batch of a tiled-frame loop's frames, one camera each,
 // the frame index = blockIdx.z)
 constexpr int kMaxLaunchFrames = 4;
@@ -137,6 +161,7 @@ struct FrameCam {
 struct FrameParams {
   LightRec lights[kMaxLights];
   MaterialRec material;
+  SurfaceConsts surf;  // derived from material by rt_set_shading (surface_consts)
   uint32_t nlights;
   uint32_t shade_mode;
   uint32_t spp_side;  // k for k x k stratified samples

@@ -955,9 +955,6 @@ __device__ V3 face_world_normal(const HitInstance& hi, uint32_t prim) {
   return mat3_mul(hi.nrm, n);
 }
 
-#ifndef RT_SURFACE_UNROLL
-#define RT_SURFACE_UNROLL 1  // A/B: the light loop of surface_ref unrolled (independent lights interleaved; same sums)
-#endif
 
 // ClosestHit's finalSurfaceColor = CalculateDirectLighting (Hit.hlsl:83-95) + CalculatePBRShading
 // (:97-174), pinned for float32 and mirrored bit for bit by oracle/rt_oracle.c osurface (round 6):
@@ -965,7 +962,7 @@ __device__ V3 face_world_normal(const HitInstance& hi, uint32_t prim) {
 //    share one sqrt and one reciprocal (normalize is v * (1 / sqrt(dot v v)), length that same sqrt);
 //    the two sums keep their own accumulators and light order, and are added at the end as before;
 //  * the pixel's invariants (N, V, N.V, Smith's view term) out of the loop, the material's (a^2, k,
-//    F0, (1 - metallic) albedo / PI) evaluated once;
+//    F0, (1 - metallic) albedo / PI) evaluated once per rt_set_shading on the host (FrameParams::surf);
 //  * every quotient as a product with a reciprocal (rcp_exact: the IEEE 1.0f / x, bits and all):
 //    NDF = a2 * (1 / denom), Smith's light term NdotL * (1 / (NdotL (1 - k) + k)), the specular
 //    term F * ((NDF G) * (1 / (4 N.V N.L + 1e-4))), the tone map c * (1 / (c + 1)); the diffuse
@@ -978,16 +975,11 @@ __device__ __forceinline__ float srcp(float x) { return rcp_exact(x); }
 __device__ V3 surface_ref(const FrameParams& fp, V3 P, V3 n, V3 cam) {
   const MaterialRec& m = fp.material;
   const V3 albedo = v3(m.albedo[0], m.albedo[1], m.albedo[2]);
-  const float r = m.roughness;
-  const float a = r * r;
-  const float a2 = a * a;
-  const float rp1 = r + 1.0f;
-  const float k = (rp1 * rp1) / 8.0f;
-  const float omk = 1.0f - k;
-  const V3 F0 = v3(0.04f + m.metallic * (albedo.x - 0.04f), 0.04f + m.metallic * (albedo.y - 0.04f),
-                   0.04f + m.metallic * (albedo.z - 0.04f));
-  const float km = 1.0f - m.metallic;
-  const V3 kdA = v3((km * albedo.x) / kPi, (km * albedo.y) / kPi, (km * albedo.z) / kPi);
+  // the material's constants, from rt_set_shading (surface_consts: the same IEEE operations on the host, the same
+  // bits; per pixel they were three divisions and a dozen products: REF -1.5 %, REFL -6 %, frames bit-equal)
+  const float a2 = fp.surf.a2, k = fp.surf.k, omk = fp.surf.omk;
+  const V3 F0 = v3(fp.surf.F0[0], fp.surf.F0[1], fp.surf.F0[2]);
+  const V3 kdA = v3(fp.surf.kdA[0], fp.surf.kdA[1], fp.surf.kdA[2]);
   const V3 N = neg(muls(n, srcp(sqrtf(dot(n, n)))));
   const V3 Vd = sub(cam, P);
   const V3 V = muls(Vd, srcp(sqrtf(dot(Vd, Vd))));
@@ -995,9 +987,6 @@ __device__ V3 surface_ref(const FrameParams& fp, V3 P, V3 n, V3 cam) {
   const float ggx2 = NdotV * srcp(NdotV * omk + k);
   const float v4 = 4.0f * NdotV;
   V3 cd = v3(0.0f, 0.0f, 0.0f), L0 = v3(0.0f, 0.0f, 0.0f);
-#if RT_SURFACE_UNROLL > 1
-#pragma unroll RT_SURFACE_UNROLL
-#endif
   for (uint32_t l = 0; l < fp.nlights; ++l) {
     const LightRec& Lr = fp.lights[l];
     const V3 lp = v3(Lr.position[0], Lr.position[1], Lr.position[2]);
