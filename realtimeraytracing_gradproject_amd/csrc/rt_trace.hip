@@ -930,7 +930,17 @@ __device__ __forceinline__ void tri_vertex_ids(const HitInstance& hi, uint32_t p
   }
 }
 
+// normalize with its 1 / sqrt by rcp_exact when EX (the IEEE 1.0f / x, bit for bit: the same vector). Used on the REF
+// shading's paths only: in the Lambert kernels the extra uniform branch of rcp_exact's slow path costs more than the
+// division it replaces (RT_RCP_EXACT), in the REF kernels it pays.
+template <bool EX>
+__device__ __forceinline__ V3 normalize_x(V3 a) {
+  if (EX) return muls(a, rcp_exact(sqrtf(dot(a, a))));
+  return normalize(a);
+}
+
 // CalculateInterpolatedWorldNormal (Hit.hlsl:67-81): vertex order 1,2,0 against (u, v, 1-u-v).
+template <bool EX = false>
 __device__ V3 interpolated_world_normal(const HitInstance& hi, uint32_t prim, float u, float v) {
   uint32_t i0, i1, i2;
   tri_vertex_ids(hi, prim, i0, i1, i2);
@@ -938,20 +948,21 @@ __device__ V3 interpolated_world_normal(const HitInstance& hi, uint32_t prim, fl
   const V3 n1 = ldg3(hi.vtx + (size_t)i2 * 6 + 3);
   const V3 n2 = ldg3(hi.vtx + (size_t)i0 * 6 + 3);
   const float bz = (1.0f - u) - v;
-  V3 n = normalize(add(add(muls(n0, u), muls(n1, v)), muls(n2, bz)));
+  V3 n = normalize_x<EX>(add(add(muls(n0, u), muls(n1, v)), muls(n2, bz)));
   n = mat3_mul(hi.nrm, n);
-  return normalize(n);
+  return normalize_x<EX>(n);
 }
 
 // PlaneClosestHit face normal (Hit.hlsl:218-222): normalize(cross(e1, e2)), then the instance
 // normal matrix without renormalisation.
+template <bool EX = false>
 __device__ V3 face_world_normal(const HitInstance& hi, uint32_t prim) {
   uint32_t i0, i1, i2;
   tri_vertex_ids(hi, prim, i0, i1, i2);
   const V3 p0 = ldg3(hi.vtx + (size_t)i0 * 6);
   const V3 p1 = ldg3(hi.vtx + (size_t)i1 * 6);
   const V3 p2 = ldg3(hi.vtx + (size_t)i2 * 6);
-  V3 n = normalize(cross(sub(p1, p0), sub(p2, p0)));
+  V3 n = normalize_x<EX>(cross(sub(p1, p0), sub(p2, p0)));
   return mat3_mul(hi.nrm, n);
 }
 
@@ -1040,7 +1051,7 @@ __device__ __forceinline__ V3 miss_color(const FrameParams& fp, uint32_t py) {
 // ReflectRay + CastReflectionRay (Hit.hlsl:176-181, Common.hlsl:58-69): the reflected direction
 // (normalised three times, as the HLSL does) and the offset origin.
 __device__ __forceinline__ void reflection_ray(V3 P, V3 n, V3 rd, V3& ro_next, V3& rd_next) {
-  const V3 dir = normalize(normalize(reflect_dir(normalize(rd), n)));
+  const V3 dir = normalize_x<true>(normalize_x<true>(reflect_dir(normalize_x<true>(rd), n)));
   ro_next = add(P, muls(dir, 0.001f));
   rd_next = dir;
 }
@@ -1271,14 +1282,14 @@ __device__ void shade_sample_packet(const SceneView& sc, const FrameParams& fp, 
           P[r] = add(ro[r], muls(rd[r], hit[r].t));
           if (ir.hit_group == 2u) {
             const LightRec& L0 = fp.lights[0];
-            ldir[r] = normalize(sub(v3(L0.position[0], L0.position[1], L0.position[2]), P[r]));
-            nf[r] = face_world_normal(ir, hit[r].prim);
+            ldir[r] = normalize_x<true>(sub(v3(L0.position[0], L0.position[1], L0.position[2]), P[r]));
+            nf[r] = face_world_normal<true>(ir, hit[r].prim);
             need[r] = true;
-            sd[r] = normalize(ldir[r]);
+            sd[r] = normalize_x<true>(ldir[r]);
             if (STATS) ++cnt.shadow;
             continue;
           }
-          const V3 n = interpolated_world_normal(ir, hit[r].prim, hit[r].u, hit[r].v);
+          const V3 n = interpolated_world_normal<true>(ir, hit[r].prim, hit[r].u, hit[r].v);
           const V3 s = surface_ref(fp, P[r], n, ro[r]);
           if (MODE == 0 && reflective(fp, ir, depth)) {
             sk[r][depth] = s;
