@@ -43,16 +43,19 @@ HDRS      := include/rt_api.h $(SRC)/rt_device.hpp $(SRC)/rt_internal.hpp
 #   alt       RT_PACKET_OCT=0 RT_REF_NOREFL=0 RT_RCP_EXACT=7 RT_MS_WIDE=1: min/max slab planes, the reflective REF
 #             kernel for reflectivity 0, rcp + Newton everywhere, wide multi-sample tiles
 #   wavetimes RT_WAVE_TIMES=1: the per-wave clock records of tools/wave_times.py
+#   ldstop    RT_LDS_TOP=21: the largest BLAS's top two BFS levels staged in LDS per packet workgroup (the north
+#             star's "LDS node packets", measured slower than the scalar-cache node loads: DESIGN §9)
 VDIR      := $(LIBDIR)/variants
 VSRCS     := $(SRC)/rt_api.cpp $(SRC)/rt_comm.cpp $(SRC)/rt_lbvh.hip $(SRC)/rt_trace.hip $(SRC)/rt_raster.hip \
              $(SRC)/rt_host.cpp $(HDRS) tools/build_variant.sh
-VARIANTS  := n1 n1root rays2 alt wavetimes
+VARIANTS  := n1 n1root rays2 alt wavetimes ldstop
 VLIBS     := $(foreach v,$(VARIANTS),$(VDIR)/$(v)/librtamd.so)
 DEFS_n1        := -DRT_SHADOW_COMPACT=1 -DRT_HYBRID_T=8
 DEFS_n1root    := -DRT_HYBRID_T=16 -DRT_HYBRID_ROOT=1
 DEFS_rays2     := -DRT_PACKET_RAYS=2 -DRT_SAMPLE_LANES=0 -DRT_RCP_EXACT=0
 DEFS_alt       := -DRT_PACKET_OCT=0 -DRT_REF_NOREFL=0 -DRT_RCP_EXACT=7 -DRT_MS_WIDE=1
 DEFS_wavetimes := -DRT_WAVE_TIMES=1
+DEFS_ldstop    := -DRT_LDS_TOP=21
 
 all: $(LIB) $(APP) $(ORACLE) $(BASELINE) $(RCPCHECK) $(OCCPROBE) $(CLKPROBE) $(DSPPROBE) $(VLIBS)
 

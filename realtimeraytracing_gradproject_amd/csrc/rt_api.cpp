@@ -924,6 +924,16 @@ static rt::SceneView scene_view(rt_ctx* c) {
   sv.ovf_lanes = 0;
   sv.cull_sense = 1.0f;
   sv.hybrid = maxb <= (uint32_t)rt::kHybridStack ? 1 : 0;
+#if RT_LDS_TOP
+  sv.lds_root = 0;
+  sv.lds_n = 0;
+  for (size_t k = 0; k < c->blas.size() && k < c->node_base.size(); ++k)
+    if ((int)c->blas[k].nnodes > sv.lds_n) {
+      sv.lds_n = (int)c->blas[k].nnodes;
+      sv.lds_root = (int)c->node_base[k];
+    }
+  sv.lds_n = sv.lds_n < RT_LDS_TOP ? sv.lds_n : RT_LDS_TOP;
+#endif
   return sv;
 }
 

@@ -24,6 +24,10 @@
 #ifndef RT_PACKET_RAYS
 #define RT_PACKET_RAYS 1    // rays per lane in a packet (2: 128-ray packets, 8 x 16 pixels per wave)
 #endif
+// VERDICT r5 #5's LDS candidate, measured slower than the scalar-cache node loads; a variant (ldstop):
+#ifndef RT_LDS_TOP
+#define RT_LDS_TOP 0        // > 0: the top RT_LDS_TOP BFS nodes of the largest BLAS staged in LDS per packet workgroup
+#endif
 
 namespace rt {
 
@@ -230,6 +234,10 @@ struct SceneView {
   int hybrid;          // every BLAS's worst-case stack fits kHybridStack: packet walks may hand subtrees to
                        // per-lane walks (lane_subtree)
   int tlas_root;       // the TLAS root's index in the node pool (the TLAS version launches read)
+#if RT_LDS_TOP
+  int lds_root;  // RT_LDS_TOP experiment: the largest BLAS's root in the pool and how many of its first (BFS)
+  int lds_n;     // nodes each packet workgroup copies into LDS (0: none)
+#endif
 };
 
 // ------------------------------------------------------------------------------------------

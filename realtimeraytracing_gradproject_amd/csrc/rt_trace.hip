@@ -530,11 +530,11 @@ __device__ __forceinline__ bool packet_tlas_node(const RT_CONST char* pool, int 
   if (STATS && sp + __builtin_popcount(P) > cap)  // never: cap is the exact worst case
 #pragma unroll
     for (int r = 0; r < R; ++r) cnt.overflow += ray_live(hit[r]) ? 1u : 0u;
+  // a uniform branch per slot around its write (round 6: −1 … −3 % on every config against writing the slots not
+  // pushed to the spare lane)
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int pos = sp + __builtin_popcount(P >> (k + 1));
-    stk.put(((P >> k) & 1u) ? pos : kPacketStack - 1, cref[k]);
-  }
+  for (int k = 0; k < 4; ++k)
+    if ((P >> k) & 1u) stk.put(sp + __builtin_popcount(P >> (k + 1)), cref[k]);
   sp = __builtin_amdgcn_readfirstlane(sp + __builtin_popcount(P));  // uniform by construction: an SGPR
   next = rb;
   return true;
@@ -552,6 +552,12 @@ constexpr int kMaxPacketWaves = 2;                                // waves of a 
 // the per-lane subtree stacks of a packet workgroup: one LDS array for every instantiation of the walk
 // (a __shared__ inside the template would be allocated once per instantiation)
 __shared__ int g_hyb[kMaxPacketWaves][kHybridStack * kHybridLanes];
+#endif
+#if RT_LDS_TOP
+// RT_LDS_TOP experiment ("LDS node packets"): the first RT_LDS_TOP nodes (BFS order: the top levels)
+// of the scene's largest BLAS, copied in by every packet workgroup at its start; the BLAS walk reads those nodes'
+// planes from here (ds_read_b128, a broadcast of one address) instead of the scalar cache
+__shared__ f4v g_top[RT_LDS_TOP * 8];
 #endif
 
 // Per-lane subtree walk inside the packet schedule (north star: wavefront ballot / prefix-sum ray
@@ -669,7 +675,10 @@ template <bool ANY_HIT, bool STATS, int R, bool OCT>
 __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, const RT_CONST TriRec* tpool, int bref,
                                                  const PacketRay<R>& ry, float tmin, uint32_t cur, float face,
                                                  PacketLive<R>& pl, HitRec* hit, WaveStack& stk, int& sp, int cap,
-                                                 const NodeOct& oc, int hybrid, Counters& cnt) {
+                                                 const NodeOct& oc, int hybrid, int lds_root, int lds_n,
+                                                 Counters& cnt) {
+  (void)lds_root;
+  (void)lds_n;
   const int base = sp;
 #if RT_HYBRID_T
   // the same pools for per-lane (vector) loads in lane_subtree
@@ -685,6 +694,29 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
     uint64_t hm[R][4];
     uint32_t vkey[R][4];
     f4v planes[6];
+    uint32_t ent;
+#if RT_LDS_TOP
+    const uint32_t rel = (uint32_t)(bref - lds_root);
+    if (rel < (uint32_t)lds_n) {
+      // rows at the octant offsets (or in order), from LDS into VGPRs; a separate slab call so the scalar path's
+      // SGPR planes are not merged into VGPRs
+      const char* sn = (const char*)g_top + (rel << 7);
+      f4v lp[6];
+      if (OCT) {
+        lp[0] = *(const f4v*)(sn + oc.nx);
+        lp[1] = *(const f4v*)(sn + oc.fx);
+        lp[2] = *(const f4v*)(sn + oc.ny);
+        lp[3] = *(const f4v*)(sn + oc.fy);
+        lp[4] = *(const f4v*)(sn + oc.nz);
+        lp[5] = *(const f4v*)(sn + oc.fz);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) lp[q] = *(const f4v*)(sn + 16 * q);
+      }
+      ent = packet_slabs<STATS, R, OCT>(lp, ry, tmin, pl, hit, (uint32_t)ch[4], hm, vkey, cnt);
+    } else
+#endif
+    {
     if (OCT) {
       // one 32-bit offset per row: the scalar load takes it as its SGPR offset (no 64-bit adds)
       const uint32_t noff = (uint32_t)bref << 7;
@@ -708,7 +740,8 @@ __device__ __forceinline__ bool packet_blas_walk(const RT_CONST char* pool, cons
 #pragma unroll
       for (int q = 0; q < 6; ++q) planes[q] = cld4(nb + 16 * q);
     }
-    uint32_t ent = packet_slabs<STATS, R, OCT>(planes, ry, tmin, pl, hit, (uint32_t)ch[4], hm, vkey, cnt);
+    ent = packet_slabs<STATS, R, OCT>(planes, ry, tmin, pl, hit, (uint32_t)ch[4], hm, vkey, cnt);
+    }
     asm volatile("" ::"s"(ch[0]), "s"(ch[1]), "s"(ch[2]), "s"(ch[3]), "s"(ch[5]), "s"(ch[6]), "s"(ch[7]));
 #if RT_HYBRID_T
     // few lanes want this node: they walk its subtree on their own (lane_subtree), then the packet pops
@@ -870,11 +903,17 @@ __device__ __forceinline__ void packet_walk(const SceneView& sc, const V3* o, co
         oc = NodeOct{ox, 16u - ox, 32u + oy, 48u - oy, 64u + oz, 80u - oz};
       }
 #endif
+#if RT_LDS_TOP
+      const int lroot = sc.lds_root, ln = sc.lds_n;
+#else
+      const int lroot = 0, ln = 0;
+#endif
       const bool more = uni ? packet_blas_walk<ANY_HIT, STATS, R, true>(pool, tpool, (int)ir.pool_root, b, tmin, cur,
-                                                                          face, pl, hit, stk, sp, cap, oc, sc.hybrid, cnt)
+                                                                          face, pl, hit, stk, sp, cap, oc, sc.hybrid,
+                                                                          lroot, ln, cnt)
                             : packet_blas_walk<ANY_HIT, STATS, R, false>(pool, tpool, (int)ir.pool_root, b, tmin,
                                                                            cur, face, pl, hit, stk, sp, cap, oc, sc.hybrid,
-                                                                           cnt);
+                                                                           lroot, ln, cnt);
       if (ANY_HIT && !more) return;
     }
     if (!descend) {
@@ -1531,6 +1570,14 @@ void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restri
                           uint32_t* __restrict__ rgba8, float4* __restrict__ rgba32f,
                           unsigned long long* __restrict__ stats) {
   static_assert(KS <= 1 || R == 1, "sample lanes need one ray per lane");
+#if RT_LDS_TOP
+  {  // every thread, before any wave may leave (the work list's end): the barrier needs the whole workgroup
+    const RT_GLOBAL f4v* src = (const RT_GLOBAL f4v*)((const RT_GLOBAL char*)sc.pool_nodes + ((uint32_t)sc.lds_root << 7));
+    const uint32_t nrow = (uint32_t)sc.lds_n * 8u;
+    for (uint32_t i = threadIdx.x; i < nrow; i += packet_block(KS)) g_top[i] = src[i];
+    __syncthreads();
+  }
+#endif
 #if RT_WAVE_TIMES
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif

@@ -20,10 +20,10 @@ from realtimeraytracing_gradproject_amd import scenes  # noqa: E402
 import oracle  # noqa: E402
 
 VDIR = os.path.join(os.path.dirname(rt.LIB_PATH), "variants")
-VARIANTS = ["n1", "n1root", "rays2", "alt", "wavetimes"]
+VARIANTS = ["n1", "n1root", "rays2", "alt", "wavetimes", "ldstop"]
 # the shipped walk's packets (counters equal the oracle's packet emulation): the code-shape variant, except its
-# multi-sample frames (RT_MS_WIDE: 8 x 2-pixel tiles of 4 sample lanes instead of 4 x 4)
-SAME_PACKETS = {"alt"}
+# multi-sample frames (RT_MS_WIDE: 8 x 2-pixel tiles of 4 sample lanes instead of 4 x 4); the LDS-staged node loads
+SAME_PACKETS = {"alt", "ldstop"}
 # (config, size): Lambert + shadow (C2 from inside the teapot, C2F framed, C4 64 instances), multi-sample (C5),
 # the reference scene (PBR, plane shadow ray) with and without reflection chains, the degenerate scene
 CASES = [("C2", (192, 108)), ("C2F", (200, 101)), ("C4", (256, 136)), ("C5", (64, 36)), ("REF", (96, 54)),
