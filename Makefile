@@ -68,7 +68,10 @@ $(BUILD)/%.o: $(SRC)/%.hip $(HDRS) | $(BUILD)
 # The trace kernel without SLP vectorisation: packed v_pk_mul_f32 Moller-Trumbore products need their
 # scalar triangle operands paired by s_mov (SALU, the kernel's tighter pipe) and VGPR pairs; scalar
 # VALU reads the SGPRs directly (72 -> 58 VGPRs, C2 -4.6 %, C4 -4.2 %, C5 -4.6 %).
-TRACEFLAGS := -fno-slp-vectorize
+# Uniform regions left unstructurized: the walk's branches are wave-uniform (SCC / SGPR conditions), and the
+# structurizer's flag registers and exec-mask glue around them cost SALU issue and SGPRs (C2's kernel 88 -> 84
+# SGPRs, 59 -> 55 VGPRs; C2 / C3 / C4 -4 %, REF -1 %, C2F -2 %, frames bit-equal).
+TRACEFLAGS := -fno-slp-vectorize -mllvm -structurizecfg-skip-uniform-regions=1
 $(BUILD)/rt_trace.o: $(SRC)/rt_trace.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) $(TRACEFLAGS) -c $< -o $@
 

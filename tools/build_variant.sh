@@ -13,7 +13,7 @@ SRC=realtimeraytracing_gradproject_amd/csrc
 /opt/rocm/bin/hipcc $FLAGS -c $SRC/rt_api.cpp -o $OBJ/rt_api.o &
 /opt/rocm/bin/hipcc $FLAGS -c $SRC/rt_comm.cpp -o $OBJ/rt_comm.o &
 /opt/rocm/bin/hipcc $FLAGS -c $SRC/rt_lbvh.hip -o $OBJ/rt_lbvh.o &
-/opt/rocm/bin/hipcc $FLAGS -fno-slp-vectorize -c $SRC/rt_trace.hip -o $OBJ/rt_trace.o &  # as the Makefile
+/opt/rocm/bin/hipcc $FLAGS -fno-slp-vectorize -mllvm -structurizecfg-skip-uniform-regions=1 -c $SRC/rt_trace.hip -o $OBJ/rt_trace.o &  # as the Makefile
 /opt/rocm/bin/hipcc $FLAGS -c $SRC/rt_raster.hip -o $OBJ/rt_raster.o &
 g++ -O2 -std=c++17 -fPIC -ffp-contract=off -c $SRC/rt_host.cpp -o $OBJ/rt_host.o &
 wait
