@@ -1786,6 +1786,31 @@ __global__ __launch_bounds__(256) void k_assemble16(uint32_t W4, uint32_t H, uin
 struct AsmFrames {
   uint4* out[kMaxLaunchFrames];
 };
+// 3 words of RGB8 (4 pixels) -> 4 RGBA8 words, alpha 255
+__device__ __forceinline__ uint4 rgb4_to_rgba(uint32_t a, uint32_t b, uint32_t c) {
+  return make_uint4((a & 0xffffffu) | 0xff000000u, (a >> 24) | ((b & 0xffffu) << 8) | 0xff000000u,
+                    (b >> 16) | ((c & 0xffu) << 16) | 0xff000000u, (c >> 8) | 0xff000000u);
+}
+// The strips of rt_comm into RGBA8 frames, 16 pixels per thread (W % 16 == 0, 16-B aligned buffers): three 16-B
+// loads and four 16-B stores per thread, consecutive lanes on consecutive 48-B / 64-B chunks of one row (a wave
+// reads 3 KB and writes 4 KB contiguously); one thread per (row, 16-pixel group) of every frame of the batch (z).
+__global__ __launch_bounds__(256) void k_assemble48_rgb(uint32_t W16, uint32_t H, uint32_t nranks, uint32_t strip_rows,
+                                                        const uint4* __restrict__ in_all, AsmFrames outs,
+                                                        uint32_t rows_per_rank, uint32_t frame_vec4) {
+  const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+  if (t >= W16 * H) return;
+  const uint32_t y = t / W16, xg = t - y * W16;
+  const uint32_t s = y / strip_rows, within = y % strip_rows;
+  const uint32_t rank = s % nranks, local_strip = s / nranks;
+  const uint32_t lrow = local_strip * strip_rows + within;
+  const uint4* p = in_all + (size_t)blockIdx.z * frame_vec4 + ((size_t)rank * rows_per_rank + lrow) * (W16 * 3u) + xg * 3u;
+  const uint4 q0 = p[0], q1 = p[1], q2 = p[2];
+  uint4* o = outs.out[blockIdx.z] + (size_t)y * (W16 * 4u) + xg * 4u;
+  o[0] = rgb4_to_rgba(q0.x, q0.y, q0.z);
+  o[1] = rgb4_to_rgba(q0.w, q1.x, q1.y);
+  o[2] = rgb4_to_rgba(q1.z, q1.w, q2.x);
+  o[3] = rgb4_to_rgba(q2.y, q2.z, q2.w);
+}
 __global__ __launch_bounds__(256) void k_assemble16_rgb(uint32_t W4, uint32_t H, uint32_t nranks, uint32_t strip_rows,
                                                         const uint32_t* __restrict__ in_all, AsmFrames outs,
                                                         uint32_t rows_per_rank, uint32_t frame_words) {
@@ -2336,6 +2361,16 @@ hipError_t launch_assemble_frames(uint32_t W, uint32_t H, uint32_t nranks, uint3
   if ((in_bpp != 3u && in_bpp != 4u) || nframes == 0 || nframes > (uint32_t)kMaxLaunchFrames) return hipErrorInvalidValue;
   uintptr_t align = ((uintptr_t)gathered | (uintptr_t)frame_bytes) % (in_bpp == 4u ? 16u : 4u);
   for (uint32_t b = 0; b < nframes; ++b) align |= (uintptr_t)outs[b] % 16u;
+  if (W % 16 == 0 && H > 0 && W / 16 <= 0xffffffffu / H && ((uintptr_t)gathered | (uintptr_t)frame_bytes) % 16u == 0 &&
+      align == 0 && in_bpp == 3u) {  // the strips of rt_comm, 16 pixels per thread: every frame of the batch
+    const uint32_t W16 = W / 16;
+    AsmFrames f{};
+    for (uint32_t b = 0; b < nframes; ++b) f.out[b] = (uint4*)outs[b];
+    dim3 grid((W16 * H + 255u) / 256u, 1, nframes);
+    hipLaunchKernelGGL(k_assemble48_rgb, grid, dim3(256), 0, s, W16, H, nranks, strip_rows, (const uint4*)gathered, f,
+                       rows_per_rank, (uint32_t)(frame_bytes / 16));
+    return hipGetLastError();
+  }
   if (W % 4 == 0 && align == 0 && in_bpp == 3u) {  // the strips of rt_comm: every frame of the batch in one launch
     const uint32_t W4 = W / 4;
     AsmFrames f{};

@@ -17,8 +17,10 @@ from realtimeraytracing_gradproject_amd import scenes  # noqa: E402
 import oracle  # noqa: E402
 
 # C2 (the BASELINE frame) and a ragged frame: 1083 rows = 135 full 8-row strips + a 3-row one, which leaves the
-# ranks with different row counts (some a strip short) at N = 2, 3 and 8
-SIZES = [(1920, 1080), (1920, 1083)]
+# ranks with different row counts (some a strip short) at N = 2, 3 and 8; then one small frame per assembly kernel
+# (launch_assemble_frames): width a multiple of 16 (16 pixels per thread), of 4 only (4 per thread), neither (generic)
+SIZES = [(1920, 1080), (1920, 1083), (208, 97), (200, 101), (202, 99)]
+SIZE_IDS = ["1920x1080", "1920x1083", "208x97", "200x101", "202x99"]
 EYES = [(1.5, 1.5, 1.5), (2.2, 1.4, 1.1), (1.1, 1.9, 2.4), (3.0, 2.0, 0.5)]  # the first is the reference camera
 _ORACLE = {}
 
@@ -46,7 +48,7 @@ def _check(frames, size, cams, what):
         assert bad == 0, f"{what}: frame {k} (camera {cams[k]}): {bad} pixels differ"
 
 
-@pytest.mark.parametrize("size", SIZES, ids=["1920x1080", "1920x1083"])
+@pytest.mark.parametrize("size", SIZES, ids=SIZE_IDS)
 @pytest.mark.parametrize("nranks", [2, 3, 8])
 def test_loopback_strips_every_batch_equals_oracle(size, nranks):
     """N ranks x frames per gather 1, 2, 4: 2 x depth + 1 frames (every slot reused, the last batch partly filled
