@@ -31,7 +31,7 @@ OCCPROBE  := tools/bin/occupancy_probe
 CLKPROBE  := tools/bin/clock_probe
 DSPPROBE  := tools/bin/libdispatch_probe.so
 
-HDRS      := include/rt_api.h $(SRC)/rt_device.hpp $(SRC)/rt_internal.hpp
+HDRS      := include/rt_api.h $(SRC)/rt_device.hpp $(SRC)/rt_internal.hpp $(SRC)/rt_trace_packet.inc
 
 # Library variants with the non-default code-shape knobs still in the tree (rt_device.hpp / rt_trace.hip), each
 # checked against the oracle on the GPU by tests/test_gpu_variants.py:

@@ -772,7 +772,7 @@ def roofline(config: str, st: dict, pixels: int, kernel_ms: float, schedule: str
     out = {"bound": bound, "achieved": top["achieved"], "peak": top["peak"], "unit": top["unit"],
            "frac": round(top["frac"], 4), "traffic": traffic,
            "l2_frac": round(fracs["l2"], 4),
-           "kernel": "k_trace_frame" if schedule == "lane" else "k_trace_frame_packet",
+           "kernel": "k_trace_frame" if schedule == "lane" else "k_trace_frame_packet8",
            "kernel_ms": round(kernel_ms, 4), "bytes_per_launch": int(b),
            "model": (f"{BYTES_PER_NODE_FETCH} B/node fetch + {BYTES_PER_TRI_FETCH} B/triangle fetch + "
                      f"{BYTES_PER_INST_FETCH} B/instance fetch (per wave in packets) + {BYTES_PER_SHADE} B/primary "

@@ -1558,162 +1558,40 @@ static_assert(packet_block(1) <= 64 * kMaxPacketWaves && packet_block(2) <= 64 *
 #ifndef RT_PACKET_SGPRS
 #define RT_PACKET_SGPRS 0  // > 0: cap the packet kernels' SGPRs (amdgpu_num_sgpr), A/B of the hardware residency
 #endif
+#ifndef RT_PLAIN_SGPRS
+// the kernels without the tile balance (the frames loop, the strips, REF): 80 SGPRs (72 used) fit 8 waves per SIMD
+// where 84 hold them to 7; the few SGPRs spilled to VGPR lanes cost less than the eighth wave gains since their
+// uniform regions stopped being structurized (C2 -1.3 %, C5 -3.7 %, REF -1 %; the balance's kernels lose with the
+// cap: C2F +3.5 % one at a time, so they keep theirs)
+#define RT_PLAIN_SGPRS 80
+#endif
 #if RT_PACKET_SGPRS
 #define RT_PACKET_SGPR_ATTR __attribute__((amdgpu_num_sgpr(RT_PACKET_SGPRS)))
 #else
 #define RT_PACKET_SGPR_ATTR
 #endif
-template <int MODE, bool STATS, int R, int KS, bool BAL, bool MF>
-__global__ __launch_bounds__(packet_block(KS)) __attribute__((amdgpu_waves_per_eu(
-    (MODE == 1 && !STATS) ? (KS == 0 ? RT_SPP_WAVES : (KS == 1 ? RT_LS_WAVES : RT_KS_WAVES))
-    : (MODE == 3 && !STATS) ? (KS == 0 ? RT_SPP_WAVES : (KS == 1 ? RT_REF0_WAVES : RT_KS_WAVES))
-                            : ((MODE == 0 && !STATS && KS == 1) ? RT_REF_WAVES : 1)))) RT_PACKET_SGPR_ATTR
-void k_trace_frame_packet(SceneView sc, FrameParams fp, const uint32_t* __restrict__ rows,
-                          uint32_t* __restrict__ rgba8, float4* __restrict__ rgba32f,
-                          unsigned long long* __restrict__ stats) {
-  static_assert(KS <= 1 || R == 1, "sample lanes need one ray per lane");
-#if RT_LDS_TOP
-  {  // every thread, before any wave may leave (the work list's end): the barrier needs the whole workgroup
-    const RT_GLOBAL f4v* src = (const RT_GLOBAL f4v*)((const RT_GLOBAL char*)sc.pool_nodes + ((uint32_t)sc.lds_root << 7));
-    const uint32_t nrow = (uint32_t)sc.lds_n * 8u;
-    for (uint32_t i = threadIdx.x; i < nrow; i += packet_block(KS)) g_top[i] = src[i];
-    __syncthreads();
-  }
+// The frame kernel, defined twice from rt_trace_packet.inc (amdgpu_num_sgpr takes no template-dependent value):
+// k_trace_frame_packet8, held to RT_PLAIN_SGPRS so that it fits 8 waves per SIMD, for the launches that can use the
+// eighth wave — no tile balance, no counters, a one-sample tile layout (KS >= 1: <= 64 VGPRs) and not the reflective
+// REF kernel (MODE 0: 84 VGPRs); k_trace_frame_packet, with the compiler's own budget, for every other launch.
+#if RT_PACKET_SGPRS
+#define RT_PLAIN_SGPR_ATTR RT_PACKET_SGPR_ATTR
+#elif RT_PLAIN_SGPRS
+#define RT_PLAIN_SGPR_ATTR __attribute__((amdgpu_num_sgpr(RT_PLAIN_SGPRS)))
+#else
+#define RT_PLAIN_SGPR_ATTR
 #endif
-#if RT_WAVE_TIMES
-  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-#endif
-  constexpr uint32_t NS = KS > 1 ? KS * KS : 1;  // samples of a pixel held by consecutive lanes
-  constexpr uint32_t TP = ms_tile_w(KS);          // tile width in pixels (KS > 1: ms_tile_h(KS) rows)
-  constexpr uint32_t WX = packet_wx(KS), WY = packet_wy(KS), WL = WX * WY;
-  // tile rows of a wave: TP, or 4 for 8 x 8 tiles at rt_set_tile_rows(4) (lanes past them idle)
-  const uint32_t TR = (KS <= 1 && fp.tile_rows == 4u) ? 4u : ms_tile_h(KS);
-  // the wave index is uniform: an SGPR, so the pixel of a lane can be re-derived from its lane id
-  const uint32_t lane = threadIdx.x & 63u;
-  uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  // this wave's tile: the plain grid's (workgroup bx, by of frame bz, wave w), or the work list's item (tile
-  // balance): a whole tile or one part of a split one, costliest first. All uniform (SALU).
-  uint32_t bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z, slot = 0, split = 0, part = 0;
-  uint64_t t_wave = 0;
-  if (BAL && fp.plan) {
-    const RT_CONST uint32_t* plan = (const RT_CONST uint32_t*)fp.plan;
-    const uint32_t i = blockIdx.x * WL + w;
-    if (i >= plan[0]) return;  // the grid is sized for the list's budget: the waves past its end have nothing
-    const uint32_t it = plan[1 + plan_xaddr(i, WL, gridDim.x)];  // XCD-major storage (plan_xaddr)
-    // the plan's front class (the waves estimated to outlast half the load bound: the launch's critical path) issues
-    // ahead of the other waves on its SIMD
-    if (it >> 31) __builtin_amdgcn_s_setprio(RT_BALANCE_FRONT_PRIO);
-    slot = (it >> 8) & kPlanSlotMask;
-    part = (it >> 2) & 63u;
-    split = it & 3u;
-    bz = slot / fp.waves_per_frame;
-    const uint32_t f = slot - bz * fp.waves_per_frame, wg = f / WL;
-    w = f - wg * WL;
-    by = wg / fp.grid_x;
-    bx = wg - by * fp.grid_x;
-  } else if (BAL) {
-    slot = ((bz * gridDim.y + by) * gridDim.x + bx) * WL + w;
-  }
-  if (BAL && fp.cost) t_wave = __builtin_amdgcn_s_memrealtime();
-  const uint32_t sample = lane % NS, pix = lane / NS;
-  // split tiles: only the lanes of this part's sub-rectangle of the pixel tile trace (2 x 2 or 4 x 4 parts;
-  // the others join the packets dead and store nothing)
-  const uint32_t psh = split, pq = 1u << psh;  // parts per side: 1, 2, 4
-  const bool inpart = ((pix % TP) >> (31u - __builtin_clz(TP) - psh)) == (part & (pq - 1u)) &&
-                      ((pix / TP) >> (31u - __builtin_clz(TR) - psh)) == (part >> psh);
-  const uint32_t x = bx * (TP * WX) + (w % WX) * TP + (pix % TP);
-  uint32_t px[R], py[R], out[R];  // out: the pixel's output index, ~0 when this lane stores nothing
-  bool inimg[R];
-  V3 acc[R], col[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    px[r] = x;
-    const uint32_t orow = by * (TR * R * WY) + (w / WX) * (TR * R) + TR * r + pix / TP;
-    inimg[r] = x < fp.width && orow < fp.nrows && pix / TP < TR && (R > 1 || inpart);
-    py[r] = 0;
-    if (inimg[r]) py[r] = rows ? rows[orow] : orow;
-    out[r] = (inimg[r] && sample == 0) ? orow * fp.width + x : 0xffffffffu;  // < 2^32 pixels (rt_api.cpp)
-    acc[r] = v3(0.0f, 0.0f, 0.0f);
-  }
-  Counters cnt;
-  const uint32_t k = KS == 1 ? 1u : (KS > 1 ? (uint32_t)KS : fp.spp_side);
-  const FrameCam& cam = fp.cam[MF ? bz : 0u];
-  if (KS == 1) {
-    shade_sample_packet<MODE, STATS, R>(sc, fp, cam, px, py, 0.5f, 0.5f, inimg, acc, cnt);  // (0 + 0.5) / 1
-  } else if (KS > 1) {
-    // this lane's sample (sx, sy) of the k x k grid, the sample loop's offsets
-    const float ox = ((float)(sample % KS) + 0.5f) / (float)KS;
-    const float oy = ((float)(sample / KS) + 0.5f) / (float)KS;
-    shade_sample_packet<MODE, STATS, R>(sc, fp, cam, px, py, ox, oy, inimg, col, cnt);
-    // sum in sample order: ((0 + c0) + c1) + ... exactly as the loop adds them (0 + c0 == c0).
-    // The lane id is re-read here (v_mbcnt) rather than kept live across the traces.
-    uint32_t lid;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lid));
-    const int base = (int)(lid & ~(NS - 1u));
-    V3 sum = v3(__shfl(col[0].x, base, 64), __shfl(col[0].y, base, 64), __shfl(col[0].z, base, 64));
-#pragma unroll
-    for (int q = 1; q < (int)NS; ++q)
-      sum = add(sum, v3(__shfl(col[0].x, base + q, 64), __shfl(col[0].y, base + q, 64),
-                        __shfl(col[0].z, base + q, 64)));
-    acc[0] = sum;
-    // the store index too (not kept live across the traces: the 7-wave budget has no VGPR to spare)
-    const uint32_t xp = lid / NS, xx = bx * (TP * WX) + (w % WX) * TP + (xp % TP);
-    constexpr uint32_t TH = ms_tile_h(KS);
-    const uint32_t orow = by * (TH * WY) + (w / WX) * TH + xp / TP;
-    const bool lpart = ((xp % TP) >> (31u - __builtin_clz(TP) - psh)) == (part & (pq - 1u)) &&
-                       ((xp / TP) >> (31u - __builtin_clz(TH) - psh)) == (part >> psh);
-    out[0] = (xx < fp.width && orow < fp.nrows && (lid % NS) == 0u && lpart) ? orow * fp.width + xx : 0xffffffffu;
-  } else {
-    for (uint32_t sy = 0; sy < k; ++sy)
-      for (uint32_t sx = 0; sx < k; ++sx) {
-        const float ox = ((float)sx + 0.5f) / (float)k;
-        const float oy = ((float)sy + 0.5f) / (float)k;
-        shade_sample_packet<MODE, STATS, R>(sc, fp, cam, px, py, ox, oy, inimg, col, cnt);
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = add(acc[r], col[r]);
-      }
-  }
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    V3 a = acc[r];
-    if (k > 1) {
-      const float ns = (float)(k * k);
-      a = v3(a.x / ns, a.y / ns, a.z / ns);
-    }
-    if (out[r] != 0xffffffffu) {
-      const uint32_t o = out[r];
-      store_pixel<MF>(fp, rgba8, o, a, MF ? bz : 0u);
-      if (rgba32f && !RT_WAVE_TIMES) rgba32f[o] = make_float4(a.x, a.y, a.z, 1.0f);
-    }
-  }
-  if (STATS) flush_stats<true>(cnt, stats);
-  if (BAL && fp.cost && lane == 0u) {
-    // this wave's time (100 MHz ticks): a whole tile's into its first word (bit 31 clear), a part's into the second
-    // as the costliest part of the tile's last split (time << 2 | layout; the plan kernel clears it when it splits),
-    // and bit 31 of the first word: parts ran since the whole time was measured (k_tile_plan's plan_cur)
-    uint32_t dt = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_wave);
-    dt = dt < (1u << 30) ? dt : (1u << 30) - 1u;
-    if (split == 0u) {
-      fp.cost[2u * slot] = dt;
-    } else {
-      atomicMax(fp.cost + 2u * slot + 1u, (dt << 2) | split);
-      atomicOr(fp.cost + 2u * slot, 0x80000000u);
-    }
-  }
-#if RT_WAVE_TIMES
-  // diagnostics only: (start, end) of this wave on the 100 MHz clock + its XCC / CU ids, into the
-  // caller's float4 buffer (slot = wave index; the float image is not written in this variant)
-  if (rgba32f && (threadIdx.x & 63u) == 0) {
-    const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-    uint32_t xcc, hw;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    const uint32_t wid = (blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    uint4* o = reinterpret_cast<uint4*>(rgba32f) + wid;
-    *o = make_uint4((uint32_t)t_start, (uint32_t)t_end, xcc, hw);
-  }
-#endif
-}
+#define RT_PK_NAME k_trace_frame_packet8
+#define RT_PK_SGPR_ATTR RT_PLAIN_SGPR_ATTR
+#include "rt_trace_packet.inc"
+#undef RT_PK_NAME
+#undef RT_PK_SGPR_ATTR
+#define RT_PK_NAME k_trace_frame_packet
+#define RT_PK_SGPR_ATTR RT_PACKET_SGPR_ATTR
+#include "rt_trace_packet.inc"
+#undef RT_PK_NAME
+#undef RT_PK_SGPR_ATTR
+
 
 template <bool ANY_HIT, bool STATS, bool CULL>
 __global__ __launch_bounds__(kBlock) void k_trace_rays(SceneView sc, const float4* __restrict__ rays,
@@ -1849,9 +1727,16 @@ hipError_t launch_mode(const SceneView& sc, const FrameParams& fp, const uint32_
     // counter passes always take the general (MF) kernel: fewer instantiations
     const bool mf = STATS || launch_multi_frame(fp);
 #define RT_LAUNCH_PACKET_K(KS, BALV, MFV)                                                                      \
-  hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R, (R == 1 ? KS : 0), BALV, MFV>), gp,                \
-                     dim3(packet_block(R == 1 ? KS : 0)), 0, s, sc, fp, rows, (uint32_t*)rgba8, (float4*)rgba32f, \
-                     stats)
+  do {                                                                                                         \
+    if constexpr (!BALV && !STATS && MODE != 0 && (R == 1 ? KS : 0) >= 1)                                        \
+      hipLaunchKernelGGL((k_trace_frame_packet8<MODE, STATS, R, (R == 1 ? KS : 0), BALV, MFV>), gp,           \
+                         dim3(packet_block(R == 1 ? KS : 0)), 0, s, sc, fp, rows, (uint32_t*)rgba8,             \
+                         (float4*)rgba32f, stats);                                                             \
+    else                                                                                                       \
+      hipLaunchKernelGGL((k_trace_frame_packet<MODE, STATS, R, (R == 1 ? KS : 0), BALV, MFV>), gp,            \
+                         dim3(packet_block(R == 1 ? KS : 0)), 0, s, sc, fp, rows, (uint32_t*)rgba8,             \
+                         (float4*)rgba32f, stats);                                                             \
+  } while (0)
 #define RT_LAUNCH_PACKET(KS)                                                                                   \
   do {                                                                                                         \
     if constexpr (STATS) {                                                                                     \

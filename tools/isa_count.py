@@ -31,7 +31,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "realtimeraytracing_gradproject_amd", "csrc", "rt_trace.hip")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-munsafe-fp-atomics",
          "-fno-slp-vectorize", "-mllvm", "-structurizecfg-skip-uniform-regions=1"]  # Makefile HIPFLAGS + TRACEFLAGS
-C2_KERNEL = ("_ZN2rt12_GLOBAL__N_120k_trace_frame_packetILi1ELb0ELi1ELi1ELb0ELb0EEEvNS_9SceneViewENS_11FrameParams"
+C2_KERNEL = ("_ZN2rt12_GLOBAL__N_121k_trace_frame_packet8ILi1ELb0ELi1ELi1ELb0ELb0EEEvNS_9SceneViewENS_11FrameParams"
              "EPKjPjP15HIP_vector_typeIfLj4EEPy")
 ROW_LOAD = re.compile(r"^s_load_dwordx4 s\[\d+:\d+\], s\[\d+:\d+\], s\d+$")
 KINDS = ["valu", "salu", "smem", "nop", "wait", "br", "vmem", "lds"]
